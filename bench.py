@@ -1,0 +1,165 @@
+#!/usr/bin/env python3
+"""Headline benchmark: vGPU isolation overhead + aggregate throughput.
+
+BASELINE.json metric "vGPU isolation overhead % + aggregate throughput, N pods
+sharing 1 MI355X".  On every GPU (one torchrun rank per GPU) the bench runs
+``--slices`` vGPU slices = separate processes, each a pod-equivalent with the
+device plugin's environment (libmivgpu.so preloaded, HBM hard limit
+``--gpumem-mib``, disjoint HSA_CU_MASK CU ranges = ``gpucores`` 100/slices %),
+each decoding a Qwen3-8B-shaped model (random init, synthetic KV context) at
+``--batch`` sequences.  The same slices are first run natively (no shim, no
+limits, no masks): overhead = 1 - shim / native aggregate tokens/s.
+
+``value`` = whole-job aggregate decode tokens/s of the shim round over all
+GPUs and slices, timed over exactly ``--steps`` hipGraph-replayed decode steps
+per slice between a barrier + torch.cuda.synchronize() on both sides (max
+over ranks).  The reference publishes no number -> vs_baseline
+is null; the native round is the comparison point.
+
+    python bench.py --gpus 1 --steps 20 --warmup 5
+    torchrun --nproc-per-node 8 bench.py --gpus 8 ...
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "vGPU isolation overhead % + aggregate throughput, N pods sharing 1 MI355X"
+
+
+def physical_gpu_for(local_rank: int) -> str:
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v:
+            ids = [x for x in v.split(",") if x != ""]
+            if local_rank < len(ids):
+                return ids[local_rank]
+    return str(local_rank)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--slices", type=int, default=4, help="vGPU slices (pods) per GPU")
+    ap.add_argument("--batch", type=int, default=32, help="decode sequences per slice")
+    ap.add_argument("--ctx", type=int, default=1024, help="KV context length at decode start")
+    ap.add_argument("--gpumem-mib", type=int, default=36864, help="HBM hard limit per slice")
+    ap.add_argument("--model", default="qwen3-8b", choices=["qwen3-8b", "qwen3-tiny"])
+    ap.add_argument("--mode", default="both", choices=["both", "shim", "native"])
+    ap.add_argument("--no-spatial", action="store_true", help="no HSA_CU_MASK (temporal governor)")
+    ap.add_argument("--policy", default="default", choices=["default", "force", "disable"])
+    ap.add_argument("--out", default=None, help="also write the JSON line here")
+    args = ap.parse_args()
+
+    from k8s_vgpu_scheduler_amd.bench.slices import plan_slices, run_round, spawn_round
+    from k8s_vgpu_scheduler_amd.utils import build
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if rank == 0 and not build.SHIM_SO.exists():
+        build.build_all()
+    phys = physical_gpu_for(local_rank)
+    work = Path(tempfile.mkdtemp(prefix=f"mivgpu-bench-r{rank}-"))
+    log_dir = Path(os.environ.get("MIVGPU_BENCH_LOGS", work))
+    log_dir.mkdir(parents=True, exist_ok=True)
+    child_args = ["--model", args.model, "--batch", str(args.batch), "--ctx", str(args.ctx),
+                  "--steps", str(args.steps), "--warmup", str(args.warmup)]
+
+    # Spawn every slice process of both rounds BEFORE this process touches HIP.
+    rounds = []
+    if args.mode in ("both", "native"):
+        rounds.append(("native", spawn_round(plan_slices(args.slices, shim=False, gpumem_mib=None),
+                                             phys, work, log_dir, child_args, "native")))
+    if args.mode in ("both", "shim"):
+        rounds.append(("shim", spawn_round(
+            plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib,
+                        spatial=not args.no_spatial, policy=args.policy),
+            phys, work, log_dir, child_args, "shim")))
+
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        barrier = dist.barrier
+    else:
+        torch.cuda.set_device(0)
+        barrier = None
+
+    def sync():
+        torch.cuda.synchronize()
+
+    results = {}
+    for name, procs in rounds:
+        r = run_round(procs, barrier=barrier, sync=sync)
+        wall = torch.tensor([r["wall_s"]], dtype=torch.float64, device="cuda")
+        toks = torch.tensor([float(r["tokens"])], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+            dist.all_reduce(toks, op=dist.ReduceOp.SUM)
+        r["max_wall_s"] = wall.item()
+        r["total_tokens"] = toks.item()
+        r["tok_s"] = toks.item() / wall.item()
+        results[name] = r
+
+    if rank == 0:
+        head = results.get("shim") or results["native"]
+        per_slice = [round(d["tok_s"], 1) for d in head["done"]]
+        out = {
+            "metric": METRIC,
+            "value": round(head["tok_s"], 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(head["max_wall_s"] / args.steps * 1000.0, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random-init weights, random KV context)",
+            "config": {
+                "model": "Qwen3-8B" if args.model == "qwen3-8b" else "Qwen3-tiny",
+                "global_batch": world * args.slices * args.batch,
+                "seq_len": args.ctx,
+                "parallelism": f"dp{world} x {args.slices} vGPU slices/GPU",
+                "slices_per_gpu": args.slices,
+                "batch_per_slice": args.batch,
+                "gpumem_mib_per_slice": args.gpumem_mib,
+                "gpucores_per_slice": 100 // args.slices if args.slices > 1 else 100,
+                "isolation": "HSA_CU_MASK + libmivgpu" if not args.no_spatial else f"governor ({args.policy})",
+            },
+            "round": "shim" if "shim" in results else "native",
+            "per_slice_tok_s_rank0": per_slice,
+            "slice_fairness_min_over_max": round(min(per_slice) / max(per_slice), 3) if per_slice else None,
+            "slice_mem_total_mib": [rd["mem_total_mib"] for rd in head["ready"]],
+        }
+        if "native" in results and "shim" in results:
+            nat = results["native"]["tok_s"]
+            out["native_value"] = round(nat, 2)
+            out["isolation_overhead_pct"] = round((1.0 - head["tok_s"] / nat) * 100.0, 2)
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.out:
+            Path(args.out).parent.mkdir(parents=True, exist_ok=True)
+            Path(args.out).write_text(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

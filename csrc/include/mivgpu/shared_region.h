@@ -1,0 +1,128 @@
+// mivgpu shared-region ABI (version 1.0).
+//
+// One file-backed region per container, mmap'd MAP_SHARED by every process of
+// the container that loads libmivgpu.so and, from the host side, by the node's
+// vgpu-monitor.  It is the AMD-native counterpart of HAMi-core's
+// `shared_region_t` whose Go mirror lives in the reference at
+// pkg/monitor/nvidia/v1/spec.go:24-87 (offsets pinned by v1/spec_test.go:40-70).
+//
+// Design choices that differ from the reference on purpose:
+//   * an aggregate per-device usage counter (`dev_used`) so an allocation check
+//     is O(1) instead of a sweep over 1024 process slots;
+//   * the header is small and cache-line aligned, the process table sits at the
+//     end, so the monitor's hot fields (limits, switches) share few lines;
+//   * a robust, process-shared pthread mutex guards slot ownership (a crashed
+//     holder is recovered with EOWNERDEAD instead of a semaphore leak);
+//   * cu_limit is a percentage of the device's CUs; cu_mask_count records how
+//     many CUs the device plugin gave the container through HSA_CU_MASK (0 = no
+//     spatial mask), which decides whether the temporal governor has to run.
+//
+// Layout is pinned by tests/test_shared_region_abi.py against
+// k8s_vgpu_scheduler_amd/monitor/region.py (ctypes mirror) via the exported
+// mivgpu_abi_offsetof() of libmivgpu.so.
+#ifndef MIVGPU_SHARED_REGION_H
+#define MIVGPU_SHARED_REGION_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MIVGPU_MAGIC 0x4D495647u /* 'MIVG' */
+#define MIVGPU_MAJOR 1
+#define MIVGPU_MINOR 0
+#define MIVGPU_MAX_DEVICES 16
+#define MIVGPU_MAX_PROCS 1024
+#define MIVGPU_UUID_LEN 96
+#define MIVGPU_LOCK_BYTES 64
+
+/* Process slot status. */
+#define MIVGPU_SLOT_FREE 0
+#define MIVGPU_SLOT_ACTIVE 1
+
+typedef struct {
+  uint64_t context;  /* HIP context / runtime-internal bytes (estimated)   */
+  uint64_t module;   /* code objects                                       */
+  uint64_t buffer;   /* hipMalloc & friends                                */
+  uint64_t vmm;      /* hipMemCreate physical handles (expandable segments) */
+  uint64_t total;    /* context+module+buffer+vmm                          */
+  uint64_t peak;     /* high-water mark of total                           */
+  uint64_t unused[2];
+} mivgpu_mem_t; /* 64 B */
+
+typedef struct {
+  uint64_t launches;      /* kernel + graph launches seen by the shim       */
+  uint64_t busy_ns;       /* GPU busy time measured by the governor gate    */
+  uint64_t throttled_ns;  /* time gate kernels held the stream              */
+  uint64_t gates;         /* gate kernels enqueued                          */
+  uint64_t util_pct;      /* last computed utilisation, percent             */
+  uint64_t unused[3];
+} mivgpu_util_t; /* 64 B */
+
+typedef struct {
+  int32_t pid;       /* pid inside the container's pid namespace           */
+  int32_t hostpid;   /* pid on the host (filled by the monitor if known)    */
+  int32_t status;    /* MIVGPU_SLOT_*                                      */
+  int32_t priority;  /* HIP_TASK_PRIORITY of the process                    */
+  uint64_t start_ns;
+  uint64_t heartbeat_ns;
+  uint64_t unused[5];
+  mivgpu_mem_t used[MIVGPU_MAX_DEVICES];
+  mivgpu_util_t util[MIVGPU_MAX_DEVICES];
+} mivgpu_proc_slot_t; /* 2112 B */
+
+typedef struct {
+  uint32_t magic;
+  int32_t major_version;
+  int32_t minor_version;
+  int32_t initialized;            /* 1 once the creator finished init          */
+  uint64_t owner_pid;             /* pid that created the region               */
+  uint8_t lock[MIVGPU_LOCK_BYTES];/* robust pshared pthread_mutex_t             */
+  uint64_t num_devices;
+  int32_t procnum;                /* slots in use (high-water index+1)         */
+  int32_t utilization_switch;     /* monitor -> lib: 1 = enforce core limit    */
+  int32_t recent_kernel;          /* lib sets >0 on launch; monitor -1 = block */
+  int32_t priority;               /* container task priority                   */
+  int64_t last_kernel_time;       /* unix seconds of the most recent launch     */
+  int32_t core_policy;            /* 0 default, 1 force, 2 disable             */
+  int32_t oversubscribe;          /* 1 = allow > limit (host-spill semantics)  */
+  uint64_t unused0[2];
+  char uuids[MIVGPU_MAX_DEVICES][MIVGPU_UUID_LEN];
+  uint64_t mem_limit[MIVGPU_MAX_DEVICES];     /* bytes, 0 = unlimited          */
+  uint64_t cu_limit[MIVGPU_MAX_DEVICES];      /* percent 1..100, 0 = unlimited */
+  uint64_t cu_mask_count[MIVGPU_MAX_DEVICES]; /* CUs granted by HSA_CU_MASK    */
+  uint64_t dev_used[MIVGPU_MAX_DEVICES];      /* aggregate bytes in use        */
+  uint64_t unused1[16];
+  mivgpu_proc_slot_t procs[MIVGPU_MAX_PROCS];
+} mivgpu_shared_region_t;
+
+/* Field ids understood by mivgpu_abi_offsetof() (exported by libmivgpu.so). */
+enum {
+  MIVGPU_F_MAGIC = 0,
+  MIVGPU_F_LOCK,
+  MIVGPU_F_NUM_DEVICES,
+  MIVGPU_F_PROCNUM,
+  MIVGPU_F_UTIL_SWITCH,
+  MIVGPU_F_RECENT_KERNEL,
+  MIVGPU_F_PRIORITY,
+  MIVGPU_F_LAST_KERNEL_TIME,
+  MIVGPU_F_CORE_POLICY,
+  MIVGPU_F_UUIDS,
+  MIVGPU_F_MEM_LIMIT,
+  MIVGPU_F_CU_LIMIT,
+  MIVGPU_F_CU_MASK_COUNT,
+  MIVGPU_F_DEV_USED,
+  MIVGPU_F_PROCS,
+  MIVGPU_F_SIZEOF_REGION,
+  MIVGPU_F_SIZEOF_SLOT,
+  MIVGPU_F_SLOT_USED,
+  MIVGPU_F_SLOT_UTIL,
+  MIVGPU_F_COUNT
+};
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MIVGPU_SHARED_REGION_H */

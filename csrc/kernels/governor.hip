@@ -1,0 +1,151 @@
+// mivgpu governor: device-side token-bucket gate for CU-time throttling (gfx950).
+//
+// Reference behaviour being replaced: HAMi-core throttles the SM share of a
+// container by blocking the HOST thread inside cuLaunchKernel on a token bucket
+// refilled from NVML utilisation samples (contract inferred in SURVEY.md §2.6
+// from pkg/device-plugin/nvidiadevice/nvinternal/plugin/server.go:837 and
+// cmd/vGPUmonitor/feedback.go:74-134).
+//
+// MI355X-first design: the shim enqueues this one-wave kernel on the SAME
+// stream, in front of a user launch, at most once per `min interval` of host
+// submission.  The gate
+//   1. reads the 100 MHz constant clock (s_memrealtime -> 10 ns ticks),
+//   2. debits the stream's GPU-busy time since its previous gate from a bucket
+//      shared by every stream of the process on this device,
+//   3. refills the bucket at `rate_ppm` of wall time (the container's CU share),
+//   4. if the bucket is in debt, holds the stream on-device (s_sleep loop)
+//      until the debt is repaid -- other tenants' queues run meanwhile.
+// No host thread ever blocks, launches stay asynchronous, and graph replays are
+// gated by the same mechanism.  Every spin is bounded (max_hold_ns), so a gate
+// can never wedge a queue.
+//
+// Memory model (MI355X_MICROARCH.md "Workgroup dispatch ... visibility"): gates
+// of different streams can run on different XCDs, so every access to the
+// shared state is an agent-scope atomic, the critical section is bracketed by
+// acquire/release on the lock word, and only lane 0 of one wave touches it.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MIVGPU_GATE_SLOTS 64
+
+struct mivgpu_gate_state {
+  unsigned long long lock;
+  long long last_ns;       // device ns at which the bucket was last settled
+  long long tokens_ns;     // balance in ns of GPU time (may go negative)
+  unsigned long long busy_total_ns;
+  unsigned long long held_total_ns;
+  unsigned long long gates;
+  unsigned long long pad[2];
+  long long slot_exit_ns[MIVGPU_GATE_SLOTS];  // per-stream last gate exit
+};
+
+// Written with plain system-visible stores into fine-grained host memory so
+// the shim's bookkeeping thread can read stats without synchronising a stream.
+struct mivgpu_gate_host_stats {
+  unsigned long long busy_total_ns;
+  unsigned long long held_total_ns;
+  unsigned long long gates;
+  long long last_now_ns;
+  long long last_tokens_ns;
+  long long last_hold_ns;
+  unsigned long long pad[2];
+};
+
+__device__ __forceinline__ long long rt_ns() {
+  return (long long)__builtin_amdgcn_s_memrealtime() * 10ll;
+}
+
+__device__ __forceinline__ long long aload(long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void astore(long long* p, long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long aloadu(unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void astoreu(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+extern "C" __global__ void __launch_bounds__(64)
+mivgpu_gate(mivgpu_gate_state* st, mivgpu_gate_host_stats* hs, long long submit_ns,
+            int slot, unsigned int rate_ppm, long long cap_ns, long long max_hold_ns) {
+  if (threadIdx.x != 0) return;
+  if (slot < 0 || slot >= MIVGPU_GATE_SLOTS) slot = 0;
+  if (rate_ppm == 0) rate_ppm = 1;
+
+  // Bounded spin lock (acquire).  If it cannot be taken in ~0.5 s something is
+  // badly wrong (a gate died holding it); proceed unlocked rather than hang.
+  bool locked = false;
+  for (unsigned int spins = 0; spins < (1u << 17); ++spins) {
+    unsigned long long expected = 0ull;
+    if (__hip_atomic_compare_exchange_strong(&st->lock, &expected, 1ull, __ATOMIC_ACQUIRE,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      locked = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+
+  const long long now = rt_ns();
+  long long last = aload(&st->last_ns);
+  long long tokens = aload(&st->tokens_ns);
+  if (last == 0) {  // first gate of the process on this device: full bucket
+    last = now;
+    tokens = cap_ns;
+  }
+  long long elapsed = now - last;
+  if (elapsed < 0) elapsed = 0;  // bucket already settled into the future by a hold
+  tokens += (long long)(((__int128)elapsed * rate_ppm) / 1000000);
+  if (tokens > cap_ns) tokens = cap_ns;
+
+  // GPU time this stream consumed since its previous gate.  The stream is
+  // in-order, so everything between max(previous gate exit, first submission
+  // after it) and `now` was the stream's own work.
+  const long long prev_exit = aload(&st->slot_exit_ns[slot]);
+  long long begin = prev_exit > submit_ns ? prev_exit : submit_ns;
+  if (begin <= 0 || begin > now) begin = now;
+  const long long busy = now - begin;
+  tokens -= busy;
+
+  long long hold = 0;
+  if (tokens < 0) {
+    hold = (long long)(((__int128)(-tokens) * 1000000) / rate_ppm);
+    if (hold > max_hold_ns) hold = max_hold_ns;
+    tokens += (long long)(((__int128)hold * rate_ppm) / 1000000);
+  }
+  const long long t_end = now + hold;
+  astore(&st->last_ns, t_end);
+  astore(&st->tokens_ns, tokens);
+  astore(&st->slot_exit_ns[slot], t_end);
+  const unsigned long long busy_tot = aloadu(&st->busy_total_ns) + (unsigned long long)busy;
+  const unsigned long long held_tot = aloadu(&st->held_total_ns) + (unsigned long long)hold;
+  const unsigned long long gates = aloadu(&st->gates) + 1ull;
+  astoreu(&st->busy_total_ns, busy_tot);
+  astoreu(&st->held_total_ns, held_tot);
+  astoreu(&st->gates, gates);
+  if (locked) __hip_atomic_store(&st->lock, 0ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+
+  // Publish stats to host memory (system scope, plain stores are enough: the
+  // host only ever reads them as monotone counters).
+  if (hs) {
+    __hip_atomic_store(&hs->busy_total_ns, busy_tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&hs->held_total_ns, held_tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&hs->gates, gates, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&hs->last_now_ns, now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&hs->last_tokens_ns, tokens, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&hs->last_hold_ns, hold, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+
+  // Hold the stream on-device.  ~3.4 us per s_sleep(127) at 2.4 GHz; bounded
+  // by max_hold_ns through t_end.
+  while (rt_ns() < t_end) __builtin_amdgcn_s_sleep(127);
+}
+
+// Clock calibration: device realtime (ns) for the host<->device offset.
+extern "C" __global__ void __launch_bounds__(64) mivgpu_clock(long long* out) {
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(out, rt_ns(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}

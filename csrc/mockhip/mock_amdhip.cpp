@@ -1,0 +1,139 @@
+// CPU stand-in for libamdhip64.so used ONLY by the CPU test-suite to exercise
+// libmivgpu.so's interposition, accounting and virtualisation logic without a
+// GPU.  It exports the subset of the HIP runtime the shim resolves, under the
+// same ELF version nodes as the real library (mock_amdhip.map), so a driver
+// linked against it carries exactly the versioned references a PyTorch binary
+// carries.  "Device memory" is host malloc bounded by MOCKHIP_TOTAL_MIB.
+#include <hip/hip_runtime_api.h>
+
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <mutex>
+#include <unordered_map>
+
+#define EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace {
+std::mutex mu;
+std::unordered_map<void*, size_t> allocs;
+size_t used_bytes[16] = {0};
+thread_local int cur_dev = 0;
+std::atomic<unsigned long long> launches{0};
+
+size_t total_bytes() {
+  const char* t = getenv("MOCKHIP_TOTAL_MIB");
+  size_t mib = t ? strtoull(t, nullptr, 10) : 65536;
+  return mib << 20;
+}
+int ndev() {
+  const char* n = getenv("MOCKHIP_DEVICES");
+  return n ? atoi(n) : 1;
+}
+hipError_t do_alloc(void** p, size_t sz) {
+  std::lock_guard<std::mutex> lk(mu);
+  if (used_bytes[cur_dev] + sz > total_bytes()) return hipErrorOutOfMemory;
+  // Never touch the pages: tests allocate "GiB" without committing RAM.
+  void* m = malloc(sz < 64 ? 64 : (sz > (1u << 20) ? 4096 : sz));
+  if (!m) return hipErrorOutOfMemory;
+  allocs[m] = sz;
+  used_bytes[cur_dev] += sz;
+  *p = m;
+  return hipSuccess;
+}
+hipError_t do_free(void* p) {
+  if (!p) return hipSuccess;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = allocs.find(p);
+  if (it == allocs.end()) return hipErrorInvalidValue;
+  used_bytes[cur_dev] -= it->second;
+  allocs.erase(it);
+  free(p);
+  return hipSuccess;
+}
+}  // namespace
+
+EXPORT hipError_t hipGetDeviceCount(int* n) { *n = ndev(); return hipSuccess; }
+EXPORT hipError_t hipGetDevice(int* d) { *d = cur_dev; return hipSuccess; }
+EXPORT hipError_t hipSetDevice(int d) {
+  if (d < 0 || d >= ndev()) return hipErrorInvalidDevice;
+  cur_dev = d;
+  return hipSuccess;
+}
+EXPORT hipError_t hipMalloc(void** p, size_t sz) { return do_alloc(p, sz); }
+EXPORT hipError_t hipExtMallocWithFlags(void** p, size_t sz, unsigned int) { return do_alloc(p, sz); }
+EXPORT hipError_t hipMallocManaged(void** p, size_t sz, unsigned int) { return do_alloc(p, sz); }
+EXPORT hipError_t hipMallocAsync(void** p, size_t sz, hipStream_t) { return do_alloc(p, sz); }
+EXPORT hipError_t hipMallocFromPoolAsync(void** p, size_t sz, hipMemPool_t, hipStream_t) {
+  return do_alloc(p, sz);
+}
+EXPORT hipError_t hipMallocPitch(void** p, size_t* pitch, size_t w, size_t h) {
+  *pitch = (w + 255) & ~size_t(255);
+  return do_alloc(p, *pitch * h);
+}
+EXPORT hipError_t hipMemAllocPitch(hipDeviceptr_t* p, size_t* pitch, size_t w, size_t h, unsigned int) {
+  *pitch = (w + 255) & ~size_t(255);
+  return do_alloc(reinterpret_cast<void**>(p), *pitch * h);
+}
+EXPORT hipError_t hipFree(void* p) { return do_free(p); }
+EXPORT hipError_t hipFreeAsync(void* p, hipStream_t) { return do_free(p); }
+EXPORT hipError_t hipMemCreate(hipMemGenericAllocationHandle_t* h, size_t sz,
+                               const hipMemAllocationProp*, unsigned long long) {
+  void* p = nullptr;
+  hipError_t rc = do_alloc(&p, sz);
+  *h = reinterpret_cast<hipMemGenericAllocationHandle_t>(p);
+  return rc;
+}
+EXPORT hipError_t hipMemRelease(hipMemGenericAllocationHandle_t h) {
+  return do_free(reinterpret_cast<void*>(h));
+}
+EXPORT hipError_t hipHostMalloc(void** p, size_t sz, unsigned int) {
+  *p = malloc(sz < 64 ? 64 : (sz > (1u << 20) ? 4096 : sz));
+  return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+EXPORT hipError_t hipHostFree(void* p) { free(p); return hipSuccess; }
+EXPORT hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned int) { *d = h; return hipSuccess; }
+EXPORT hipError_t hipMemset(void* p, int v, size_t n) { (void)p; (void)v; (void)n; return hipSuccess; }
+EXPORT hipError_t hipMemGetInfo(size_t* f, size_t* t) {
+  std::lock_guard<std::mutex> lk(mu);
+  *t = total_bytes();
+  *f = total_bytes() - used_bytes[cur_dev];
+  return hipSuccess;
+}
+EXPORT hipError_t hipDeviceTotalMem(size_t* b, hipDevice_t) { *b = total_bytes(); return hipSuccess; }
+EXPORT hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_tR0600* p, int) {
+  memset(p, 0, sizeof(*p));
+  strcpy(p->name, "AMD Instinct MI355X (mock)");
+  p->totalGlobalMem = total_bytes();
+  p->multiProcessorCount = 256;
+  return hipSuccess;
+}
+EXPORT hipError_t hipGetDevicePropertiesR0000(void* p, int) {
+  memset(p, 0, 512);
+  strcpy(static_cast<char*>(p), "AMD Instinct MI355X (mock)");
+  *reinterpret_cast<size_t*>(static_cast<char*>(p) + 256) = total_bytes();
+  return hipSuccess;
+}
+EXPORT hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t, int) { *v = 0; return hipSuccess; }
+EXPORT hipError_t hipLaunchKernel(const void*, dim3, dim3, void**, size_t, hipStream_t) {
+  launches++;
+  return hipSuccess;
+}
+EXPORT hipError_t hipModuleLaunchKernel(hipFunction_t, unsigned, unsigned, unsigned, unsigned,
+                                        unsigned, unsigned, unsigned, hipStream_t, void**, void**) {
+  launches++;
+  return hipSuccess;
+}
+EXPORT hipError_t hipGraphLaunch(hipGraphExec_t, hipStream_t) { launches++; return hipSuccess; }
+EXPORT hipError_t hipStreamIsCapturing(hipStream_t, hipStreamCaptureStatus* s) {
+  *s = hipStreamCaptureStatusNone;
+  return hipSuccess;
+}
+EXPORT hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+// No GPU: the governor code object cannot load, so temporal gating stays off.
+EXPORT hipError_t hipModuleLoadData(hipModule_t*, const void*) { return hipErrorNoBinaryForGpu; }
+EXPORT hipError_t hipModuleGetFunction(hipFunction_t*, hipModule_t, const char*) {
+  return hipErrorNotFound;
+}
+EXPORT unsigned long long mockhip_launch_count(void) { return launches.load(); }

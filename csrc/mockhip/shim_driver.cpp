@@ -1,0 +1,89 @@
+// Test driver for libmivgpu.so against the mock HIP runtime (CPU tests).
+// Linked against the mock libamdhip64.so, so its HIP references are versioned
+// exactly like PyTorch's.  Commands (argv):
+//   alloc <MiB>      hipMalloc, prints rc and slot index
+//   allocasync <MiB> hipMallocAsync
+//   vmm <MiB>        hipMemCreate
+//   freeall          hipFree / hipMemRelease everything allocated so far
+//   meminfo          hipMemGetInfo
+//   props            hipGetDevicePropertiesR0600 totalGlobalMem + hipDeviceTotalMem
+//   launch <n>       n x hipLaunchKernel
+//   usage            mivgpu_process_usage(0) via dlsym
+//   sleep <ms>
+//   device <i>       hipSetDevice
+#include <hip/hip_runtime_api.h>
+
+#include <dlfcn.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <vector>
+
+extern "C" hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_tR0600*, int);
+
+int main(int argc, char** argv) {
+  std::vector<void*> bufs;
+  std::vector<hipMemGenericAllocationHandle_t> handles;
+  for (int i = 1; i < argc; ++i) {
+    const char* c = argv[i];
+    if (!strcmp(c, "alloc") || !strcmp(c, "allocasync")) {
+      size_t mib = strtoull(argv[++i], nullptr, 10);
+      void* p = nullptr;
+      hipError_t rc = !strcmp(c, "alloc") ? hipMalloc(&p, mib << 20)
+                                         : hipMallocAsync(&p, mib << 20, nullptr);
+      printf("{\"op\":\"%s\",\"mib\":%zu,\"rc\":%d}\n", c, mib, (int)rc);
+      if (rc == hipSuccess) bufs.push_back(p);
+    } else if (!strcmp(c, "vmm")) {
+      size_t mib = strtoull(argv[++i], nullptr, 10);
+      hipMemGenericAllocationHandle_t h{};
+      hipMemAllocationProp prop{};
+      prop.type = hipMemAllocationTypePinned;
+      prop.location.type = hipMemLocationTypeDevice;
+      int d = 0;
+      hipGetDevice(&d);
+      prop.location.id = d;
+      hipError_t rc = hipMemCreate(&h, mib << 20, &prop, 0);
+      printf("{\"op\":\"vmm\",\"mib\":%zu,\"rc\":%d}\n", mib, (int)rc);
+      if (rc == hipSuccess) handles.push_back(h);
+    } else if (!strcmp(c, "freeall")) {
+      int bad = 0;
+      for (void* p : bufs) bad += hipFree(p) != hipSuccess;
+      for (auto h : handles) bad += hipMemRelease(h) != hipSuccess;
+      bufs.clear();
+      handles.clear();
+      printf("{\"op\":\"freeall\",\"errors\":%d}\n", bad);
+    } else if (!strcmp(c, "meminfo")) {
+      size_t f = 0, t = 0;
+      hipError_t rc = hipMemGetInfo(&f, &t);
+      printf("{\"op\":\"meminfo\",\"rc\":%d,\"free_mib\":%zu,\"total_mib\":%zu}\n", (int)rc, f >> 20,
+             t >> 20);
+    } else if (!strcmp(c, "props")) {
+      hipDeviceProp_tR0600 p;
+      hipGetDevicePropertiesR0600(&p, 0);
+      size_t tm = 0;
+      hipDeviceTotalMem(&tm, 0);
+      printf("{\"op\":\"props\",\"total_mib\":%zu,\"devtotal_mib\":%zu}\n", p.totalGlobalMem >> 20,
+             tm >> 20);
+    } else if (!strcmp(c, "launch")) {
+      long n = strtol(argv[++i], nullptr, 10);
+      static char dummy;
+      for (long k = 0; k < n; ++k) hipLaunchKernel(&dummy, dim3(1), dim3(64), nullptr, 0, nullptr);
+      auto f = (unsigned long long (*)(void))dlsym(RTLD_DEFAULT, "mivgpu_launch_count");
+      auto g = (unsigned long long (*)(void))dlsym(RTLD_DEFAULT, "mockhip_launch_count");
+      printf("{\"op\":\"launch\",\"n\":%ld,\"shim_seen\":%llu,\"real_seen\":%llu}\n", n,
+             f ? f() : 0ull, g ? g() : 0ull);
+    } else if (!strcmp(c, "usage")) {
+      auto f = (long long (*)(int))dlsym(RTLD_DEFAULT, "mivgpu_process_usage");
+      printf("{\"op\":\"usage\",\"bytes\":%lld}\n", f ? f(0) : -2ll);
+    } else if (!strcmp(c, "sleep")) {
+      usleep((useconds_t)strtoul(argv[++i], nullptr, 10) * 1000);
+    } else if (!strcmp(c, "device")) {
+      int d = atoi(argv[++i]);
+      printf("{\"op\":\"device\",\"rc\":%d}\n", (int)hipSetDevice(d));
+    }
+    fflush(stdout);
+  }
+  return 0;
+}

@@ -1,0 +1,409 @@
+// Hand-written gfx950 kernels for the benchmark workload (Qwen3-style decode).
+//
+// The reference has no kernels; its benchmark drives vLLM
+// Qwen3-8B decode (benchmarks/ai-benchmark/benchmark.py:72-75).  These are the
+// non-GEMM hot ops of that decode step, written for CDNA4 (64-wide waves,
+// 16-byte vector memory ops, wave-shuffle reductions, LDS staging), exported
+// with a C ABI so Python calls them through ctypes with raw device pointers and
+// the caller's HIP stream (and so they are captured by hipGraphs).
+//
+//   mivgpu_rmsnorm          out = rmsnorm(x) * w
+//   mivgpu_add_rmsnorm      res += x ; out = rmsnorm(res) * w      (fused)
+//   mivgpu_qk_norm_rope_kv  per-head RMSNorm(q,k) + NeoX RoPE + KV-cache append
+//   mivgpu_decode_attention GQA split-K flash-decoding (partials + combine)
+//   mivgpu_silu_mul         out = silu(gate) * up
+//
+// All tensors bf16 (raw uint16 bits) unless noted; fp32 accumulation.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+
+__device__ __forceinline__ float bf2f(bf16_t x) { return __uint_as_float(((uint32_t)x) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (bf16_t)((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));
+  u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even
+  return (bf16_t)(u >> 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Unpack 8 bf16 held in a uint4 into floats.
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
+  v.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
+  v.z = (uint32_t)f2bf(f[4]) | ((uint32_t)f2bf(f[5]) << 16);
+  v.w = (uint32_t)f2bf(f[6]) | ((uint32_t)f2bf(f[7]) << 16);
+  return v;
+}
+
+// ----------------------------------------------------------------- RMSNorm --
+// One 256-thread workgroup per row; each thread owns dim/256 contiguous
+// elements loaded as 16-byte vectors (dim % 2048 == 0 for the fast path; a
+// scalar tail loop handles any dim % 8 == 0).
+template <bool ADD>
+__global__ void __launch_bounds__(256)
+rmsnorm_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ res, const bf16_t* __restrict__ w,
+               bf16_t* __restrict__ out, int dim, float eps) {
+  const int row = blockIdx.x;
+  const int t = threadIdx.x;
+  const bf16_t* xr = x + (size_t)row * dim;
+  bf16_t* rr = res + (size_t)row * dim;
+  bf16_t* orow = out + (size_t)row * dim;
+  __shared__ float red[4];
+  constexpr int MAXV = 4;  // up to 4 x 8 elements per thread (dim <= 8192)
+  float v[MAXV][8];
+  const int nvec = dim / 8;
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = t + k * 256;
+    if (vi < nvec) {
+      float a[8];
+      if (ADD) {
+        float b[8];
+        unpack8(reinterpret_cast<const uint4*>(xr)[vi], a);
+        unpack8(reinterpret_cast<const uint4*>(rr)[vi], b);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] += b[e];
+        reinterpret_cast<uint4*>(rr)[vi] = pack8(a);
+        // Normalise the bf16-rounded residual, exactly what is stored.
+        unpack8(reinterpret_cast<const uint4*>(rr)[vi], a);
+      } else {
+        unpack8(reinterpret_cast<const uint4*>(xr)[vi], a);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[k][e] = a[e];
+        ss += a[e] * a[e];
+      }
+    }
+  }
+  ss = wave_sum(ss);
+  if ((t & 63) == 0) red[t >> 6] = ss;
+  __syncthreads();
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  const float inv = rsqrtf(tot / (float)dim + eps);
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = t + k * 256;
+    if (vi < nvec) {
+      float wf[8], o[8];
+      unpack8(reinterpret_cast<const uint4*>(w)[vi], wf);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = v[k][e] * inv * wf[e];
+      reinterpret_cast<uint4*>(orow)[vi] = pack8(o);
+    }
+  }
+}
+
+// ------------------------------------------- QK-norm + RoPE + KV append ----
+// grid = (B, Hq + 2*Hkv); one wave per (token, head).  D = 128: lane l owns
+// elements l and l+64, which is exactly a NeoX rotate-half pair.
+__global__ void __launch_bounds__(64)
+qk_norm_rope_kv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ qw,
+                       const bf16_t* __restrict__ kw, const int* __restrict__ pos,
+                       bf16_t* __restrict__ q_out, bf16_t* __restrict__ k_cache,
+                       bf16_t* __restrict__ v_cache, int Hq, int Hkv, int max_ctx, float eps,
+                       float theta) {
+  constexpr int D = 128;
+  const int b = blockIdx.x;
+  const int h = blockIdx.y;
+  const int l = threadIdx.x;
+  const int row_stride = (Hq + 2 * Hkv) * D;
+  const bf16_t* src = qkv + (size_t)b * row_stride + (size_t)h * D;
+  float x0 = bf2f(src[l]);
+  float x1 = bf2f(src[l + 64]);
+  const int p = pos[b];
+  const bool in_range = p >= 0 && p < max_ctx;  // never write past the cache
+  if (h >= Hq + Hkv) {  // V head: plain copy into the cache
+    if (!in_range) return;
+    const int hv = h - Hq - Hkv;
+    bf16_t* dst = v_cache + (((size_t)b * Hkv + hv) * max_ctx + p) * D;
+    dst[l] = f2bf(x0);
+    dst[l + 64] = f2bf(x1);
+    return;
+  }
+  const bool is_q = h < Hq;
+  const bf16_t* nw = is_q ? qw : kw;
+  const float ss = wave_sum(x0 * x0 + x1 * x1);
+  const float inv = rsqrtf(ss / (float)D + eps);
+  x0 = x0 * inv * bf2f(nw[l]);
+  x1 = x1 * inv * bf2f(nw[l + 64]);
+  // inv_freq = theta^(-2l/D)
+  const float inv_freq = exp2f(-(2.0f * (float)l / (float)D) * log2f(theta));
+  float s, c;
+  sincosf((float)p * inv_freq, &s, &c);
+  const float o0 = x0 * c - x1 * s;
+  const float o1 = x1 * c + x0 * s;
+  bf16_t* dst;
+  if (is_q) {
+    dst = q_out + ((size_t)b * Hq + h) * D;
+  } else {
+    if (!in_range) return;
+    const int hk = h - Hq;
+    dst = k_cache + (((size_t)b * Hkv + hk) * max_ctx + p) * D;
+  }
+  dst[l] = f2bf(o0);
+  dst[l + 64] = f2bf(o1);
+}
+
+// ---------------------------------------------- GQA split-K decode attention --
+// grid = (nsplit, Hkv, B), 256 threads.  Each workgroup scores SPLIT keys of
+// one (batch, kv-head) against the G = Hq/Hkv query heads that share it, so
+// every K/V byte is read once per group instead of once per query head.
+//   scores: 8 lanes per key (16 dims each), 8 keys per wave-iteration
+//   P.V   : 16 lanes per key row (8 dims each, one 16-B load), 16 rows at once
+// Partials (unnormalised O, running max m, sum l) go to fp32 workspace; the
+// combine kernel merges splits.  G <= 8 supported (Qwen3-8B: G = 4).
+constexpr int ATT_SPLIT = 256;
+constexpr int ATT_D = 128;
+
+template <int G>
+__global__ void __launch_bounds__(256)
+decode_attn_partial_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k_cache,
+                           const bf16_t* __restrict__ v_cache, const int* __restrict__ seqlens,
+                           float* __restrict__ o_part, float* __restrict__ ml_part, int Hq, int Hkv,
+                           int max_ctx, int nsplit, float scale) {
+  const int split = blockIdx.x;
+  const int hk = blockIdx.y;
+  const int b = blockIdx.z;
+  const int t = threadIdx.x;
+  const int L = min(seqlens[b], max_ctx);
+  const int j0 = split * ATT_SPLIT;
+  const int n = min(ATT_SPLIT, L - j0);
+  __shared__ float s_p[G][ATT_SPLIT];
+  __shared__ float s_red[8][G];
+  __shared__ float s_acc[16][G][ATT_D / 2];  // reduced in two halves of D
+  const size_t part_base = ((size_t)b * Hq + (size_t)hk * G);
+  if (n <= 0) {  // empty split (short sequence): neutral partial
+    if (t < G) {
+      ml_part[((part_base + t) * nsplit + split) * 2 + 0] = -INFINITY;
+      ml_part[((part_base + t) * nsplit + split) * 2 + 1] = 0.f;
+    }
+    return;
+  }
+  const bf16_t* kb = k_cache + ((size_t)b * Hkv + hk) * (size_t)max_ctx * ATT_D;
+  const bf16_t* vb = v_cache + ((size_t)b * Hkv + hk) * (size_t)max_ctx * ATT_D;
+
+  // ---- scores
+  {
+    const int lane = t & 63, wave = t >> 6;
+    const int sub = lane & 7;       // 16-dim chunk
+    const int krow = lane >> 3;     // key within the wave-iteration
+    float qf[G][16];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const uint4* qp = reinterpret_cast<const uint4*>(q + (part_base + g) * ATT_D + sub * 16);
+      unpack8(qp[0], &qf[g][0]);
+      unpack8(qp[1], &qf[g][8]);
+    }
+    for (int jj = wave * 8 + krow; jj < n; jj += 32) {
+      const uint4* kp = reinterpret_cast<const uint4*>(kb + (size_t)(j0 + jj) * ATT_D + sub * 16);
+      float kf[16];
+      unpack8(kp[0], &kf[0]);
+      unpack8(kp[1], &kf[8]);
+      float acc[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        float a = 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) a = fmaf(qf[g][e], kf[e], a);
+        a += __shfl_xor(a, 1, 64);
+        a += __shfl_xor(a, 2, 64);
+        a += __shfl_xor(a, 4, 64);
+        acc[g] = a;
+      }
+      if (sub == 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) s_p[g][jj] = acc[g] * scale;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- softmax statistics per query head (t indexes keys)
+  float m[G], lsum[G];
+  {
+    float mv[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) mv[g] = t < n ? s_p[g][t] : -INFINITY;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float w = wave_max(mv[g]);
+      if ((t & 63) == 0) s_red[t >> 6][g] = w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < G; ++g) m[g] = fmaxf(fmaxf(s_red[0][g], s_red[1][g]), fmaxf(s_red[2][g], s_red[3][g]));
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float e = t < n ? __expf(mv[g] - m[g]) : 0.f;
+      if (t < n) s_p[g][t] = e;
+      float w = wave_sum(e);
+      if ((t & 63) == 0) s_red[4 + (t >> 6)][g] = w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < G; ++g) lsum[g] = s_red[4][g] + s_red[5][g] + s_red[6][g] + s_red[7][g];
+  }
+
+  // ---- P.V: group r = t>>4 walks rows r, r+16, ...; column chunk c = t&15
+  const int r = t >> 4, c = t & 15;
+  float acc[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[g][e] = 0.f;
+  for (int jj = r; jj < n; jj += 16) {
+    float vf[8];
+    unpack8(*reinterpret_cast<const uint4*>(vb + (size_t)(j0 + jj) * ATT_D + c * 8), vf);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float p = s_p[g][jj];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[g][e] = fmaf(p, vf[e], acc[g][e]);
+    }
+  }
+  // Cross-group reduction through LDS, one half of D at a time (16 KB for G=4).
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const bool mine = (c >> 3) == half;
+    if (mine) {
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s_acc[r][g][(c & 7) * 8 + e] = acc[g][e];
+    }
+    __syncthreads();
+    for (int idx = t; idx < G * (ATT_D / 2); idx += 256) {
+      const int g = idx / (ATT_D / 2), d = idx % (ATT_D / 2);
+      float s = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) s += s_acc[rr][g][d];
+      o_part[((part_base + g) * nsplit + split) * ATT_D + half * (ATT_D / 2) + d] = s;
+    }
+    __syncthreads();
+  }
+  if (t < G) {
+    ml_part[((part_base + t) * nsplit + split) * 2 + 0] = m[t];
+    ml_part[((part_base + t) * nsplit + split) * 2 + 1] = lsum[t];
+  }
+}
+
+// grid = (Hq, B), 128 threads (one per output dim).
+__global__ void __launch_bounds__(128)
+decode_attn_combine_kernel(const float* __restrict__ o_part, const float* __restrict__ ml_part,
+                           bf16_t* __restrict__ out, int Hq, int nsplit) {
+  const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
+  const size_t base = (size_t)b * Hq + h;
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ml_part[(base * nsplit + s) * 2]);
+  float num = 0.f, den = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float ms = ml_part[(base * nsplit + s) * 2];
+    if (ms == -INFINITY) continue;
+    const float w = __expf(ms - M);
+    den += w * ml_part[(base * nsplit + s) * 2 + 1];
+    num += w * o_part[(base * nsplit + s) * ATT_D + d];
+  }
+  out[base * ATT_D + d] = f2bf(den > 0.f ? num / den : 0.f);
+}
+
+// ---------------------------------------------------------------- SiLU*mul --
+__global__ void __launch_bounds__(256)
+silu_mul_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ out, int inter, int rows) {
+  const int nvec = inter / 8;
+  const size_t total = (size_t)rows * nvec;
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < total; i += (size_t)gridDim.x * 256ull) {
+    const size_t row = i / nvec, vi = i % nvec;
+    float g[8], u[8], o[8];
+    unpack8(reinterpret_cast<const uint4*>(gu + row * 2 * inter)[vi], g);
+    unpack8(reinterpret_cast<const uint4*>(gu + row * 2 * inter + inter)[vi], u);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = g[e] / (1.f + __expf(-g[e])) * u[e];
+    reinterpret_cast<uint4*>(out + row * inter)[vi] = pack8(o);
+  }
+}
+
+// ================================================================ C ABI ====
+extern "C" {
+
+int mivgpu_rmsnorm(const void* x, const void* w, void* out, int rows, int dim, float eps,
+                   hipStream_t s) {
+  if (dim % 8 || dim > 8192 || rows <= 0) return -1;
+  hipLaunchKernelGGL(rmsnorm_kernel<false>, dim3(rows), dim3(256), 0, s, (const bf16_t*)x,
+                     (bf16_t*)nullptr, (const bf16_t*)w, (bf16_t*)out, dim, eps);
+  return (int)hipGetLastError();
+}
+
+int mivgpu_add_rmsnorm(const void* x, void* res, const void* w, void* out, int rows, int dim,
+                       float eps, hipStream_t s) {
+  if (dim % 8 || dim > 8192 || rows <= 0) return -1;
+  hipLaunchKernelGGL(rmsnorm_kernel<true>, dim3(rows), dim3(256), 0, s, (const bf16_t*)x,
+                     (bf16_t*)res, (const bf16_t*)w, (bf16_t*)out, dim, eps);
+  return (int)hipGetLastError();
+}
+
+int mivgpu_qk_norm_rope_kv(const void* qkv, const void* qw, const void* kw, const int* pos,
+                           void* q_out, void* k_cache, void* v_cache, int B, int Hq, int Hkv,
+                           int head_dim, int max_ctx, float eps, float theta, hipStream_t s) {
+  if (head_dim != 128 || B <= 0) return -1;
+  hipLaunchKernelGGL(qk_norm_rope_kv_kernel, dim3(B, Hq + 2 * Hkv), dim3(64), 0, s,
+                     (const bf16_t*)qkv, (const bf16_t*)qw, (const bf16_t*)kw, pos,
+                     (bf16_t*)q_out, (bf16_t*)k_cache, (bf16_t*)v_cache, Hq, Hkv, max_ctx, eps,
+                     theta);
+  return (int)hipGetLastError();
+}
+
+// Workspace: o_part = B*Hq*nsplit*128 floats, ml_part = B*Hq*nsplit*2 floats.
+int mivgpu_decode_attention(const void* q, const void* k_cache, const void* v_cache,
+                            const int* seqlens, void* out, void* o_part, void* ml_part, int B,
+                            int Hq, int Hkv, int head_dim, int max_ctx, int nsplit, float scale,
+                            hipStream_t s) {
+  if (head_dim != ATT_D || Hq % Hkv || nsplit <= 0 || B <= 0) return -1;
+  const int G = Hq / Hkv;
+  dim3 grid(nsplit, Hkv, B);
+  switch (G) {
+    case 1: hipLaunchKernelGGL(decode_attn_partial_kernel<1>, grid, dim3(256), 0, s, (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, seqlens, (float*)o_part, (float*)ml_part, Hq, Hkv, max_ctx, nsplit, scale); break;
+    case 2: hipLaunchKernelGGL(decode_attn_partial_kernel<2>, grid, dim3(256), 0, s, (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, seqlens, (float*)o_part, (float*)ml_part, Hq, Hkv, max_ctx, nsplit, scale); break;
+    case 4: hipLaunchKernelGGL(decode_attn_partial_kernel<4>, grid, dim3(256), 0, s, (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, seqlens, (float*)o_part, (float*)ml_part, Hq, Hkv, max_ctx, nsplit, scale); break;
+    case 8: hipLaunchKernelGGL(decode_attn_partial_kernel<8>, grid, dim3(256), 0, s, (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, seqlens, (float*)o_part, (float*)ml_part, Hq, Hkv, max_ctx, nsplit, scale); break;
+    default: return -2;
+  }
+  hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(Hq, B), dim3(ATT_D), 0, s,
+                     (const float*)o_part, (const float*)ml_part, (bf16_t*)out, Hq, nsplit);
+  return (int)hipGetLastError();
+}
+
+int mivgpu_silu_mul(const void* gate_up, void* out, int rows, int inter, hipStream_t s) {
+  if (inter % 8 || rows <= 0) return -1;
+  const size_t total = (size_t)rows * (inter / 8);
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(silu_mul_kernel, dim3(blocks), dim3(256), 0, s, (const bf16_t*)gate_up,
+                     (bf16_t*)out, inter, rows);
+  return (int)hipGetLastError();
+}
+
+int mivgpu_ops_attn_split() { return ATT_SPLIT; }
+
+}  // extern "C"

@@ -1,0 +1,214 @@
+"""N vGPU slices sharing one MI355X: the isolation-overhead benchmark engine.
+
+BASELINE.json metric: "vGPU isolation overhead % + aggregate throughput, N
+pods sharing 1 MI355X".  Each slice is a separate process (one pod's
+container), started with exactly the environment the device plugin's
+``Allocate`` would inject (``deviceplugin.allocate.container_env``):
+``LD_PRELOAD=libmivgpu.so``, ``HIP_DEVICE_MEMORY_LIMIT_0``, ``HSA_CU_MASK``,
+``HIP_DEVICE_CORE_LIMIT`` ... and runs the Qwen3-8B-shaped decode workload.
+The native round runs the same processes with no shim, no mask, no limit.
+
+Protocol (stdin/stdout lines, JSON payloads):
+    parent -> child  LOAD            child builds model, captures graph, warms up
+    child  -> parent READY {...}
+    parent -> child  GO              child times `steps` graph replays
+    child  -> parent DONE {...}
+Children are spawned before the parent initialises HIP (fork/exec after GPU
+init is forbidden on the box), and block on LOAD without touching the GPU.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import select
+import subprocess
+import sys
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+
+from k8s_vgpu_scheduler_amd.shim import shim_env
+
+MI355X_CUS = 256
+MI355X_XCDS = 8
+
+
+@dataclass
+class SliceSpec:
+    index: int
+    gpumem_mib: int | None      # None = no limit
+    cu_ranges: list | None      # [(lo, hi), ...] for HSA_CU_MASK, None = all CUs
+    core_pct: int = 100
+    shim: bool = True
+    policy: str = "default"
+    env: dict = field(default_factory=dict)
+
+
+def cu_mask_string(ranges) -> str:
+    return ",".join(f"{a}-{b}" if b > a else f"{a}" for a, b in ranges)
+
+
+def plan_slices(n: int, shim: bool, gpumem_mib: int | None, spatial: bool = True,
+                policy: str = "default") -> list[SliceSpec]:
+    """Equal split of one GPU into n slices (CUs in contiguous, XCD-sized runs)."""
+    specs = []
+    per = MI355X_CUS // n
+    for i in range(n):
+        ranges = [(i * per, (i + 1) * per - 1)] if (shim and spatial and n > 1) else None
+        specs.append(SliceSpec(index=i, gpumem_mib=gpumem_mib if shim else None, cu_ranges=ranges,
+                               core_pct=max(1, 100 // n) if n > 1 else 100, shim=shim,
+                               policy=policy))
+    return specs
+
+
+def slice_env(spec: SliceSpec, physical_gpu: str | None, cache_dir: Path) -> dict:
+    env = {}
+    if physical_gpu is not None:
+        env["ROCR_VISIBLE_DEVICES"] = physical_gpu
+        env.pop("HIP_VISIBLE_DEVICES", None)
+    if spec.shim:
+        env.update(shim_env(""))
+        env["MIVGPU_SHARED_CACHE"] = str(cache_dir / f"slice{spec.index}.cache")
+        if spec.gpumem_mib:
+            env["HIP_DEVICE_MEMORY_LIMIT_0"] = f"{spec.gpumem_mib}m"
+        if spec.core_pct < 100:
+            env["HIP_DEVICE_CORE_LIMIT"] = str(spec.core_pct)
+        env["GPU_CORE_UTILIZATION_POLICY"] = spec.policy
+        if spec.cu_ranges:
+            env["HSA_CU_MASK"] = "0:" + cu_mask_string(spec.cu_ranges)
+    env.update(spec.env)
+    return env
+
+
+class SliceProc:
+    def __init__(self, spec: SliceSpec, env: dict, args: list, log_path: Path):
+        full = dict(os.environ)
+        for k in ("LD_PRELOAD", "HSA_CU_MASK", "HIP_DEVICE_CORE_LIMIT"):
+            full.pop(k, None)
+        full.update(env)
+        if env.get("ROCR_VISIBLE_DEVICES") is not None:
+            full.pop("HIP_VISIBLE_DEVICES", None)
+            full.pop("CUDA_VISIBLE_DEVICES", None)
+        self.spec = spec
+        self.log = open(log_path, "w")
+        self.p = subprocess.Popen(
+            [sys.executable, "-m", "k8s_vgpu_scheduler_amd.bench.slices", "--child", *args],
+            env=full, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=self.log, text=True,
+            bufsize=1)
+
+    def send(self, line: str):
+        self.p.stdin.write(line + "\n")
+        self.p.stdin.flush()
+
+    def expect(self, tag: str, timeout: float) -> dict:
+        deadline = time.time() + timeout
+        while True:
+            left = deadline - time.time()
+            if left <= 0:
+                raise TimeoutError(f"slice {self.spec.index}: no {tag} within {timeout}s")
+            r, _, _ = select.select([self.p.stdout], [], [], left)
+            if not r:
+                continue
+            line = self.p.stdout.readline()
+            if not line:
+                raise RuntimeError(f"slice {self.spec.index} exited (rc={self.p.poll()}) before {tag}; "
+                                   f"see {self.log.name}")
+            if line.startswith(tag + " "):
+                return json.loads(line[len(tag) + 1:])
+
+    def close(self, timeout=60):
+        try:
+            if self.p.stdin:
+                self.p.stdin.close()
+        except OSError:
+            pass
+        try:
+            self.p.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            self.p.kill()
+            self.p.wait()
+        self.log.close()
+
+
+def child_main(argv):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="qwen3-8b")
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--ctx", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    a = ap.parse_args(argv)
+    cmd = sys.stdin.readline().strip()
+    if cmd != "LOAD":
+        return 0
+    import torch
+
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_8B, QWEN3_TINY, Qwen3Decoder
+
+    cfg = {"qwen3-8b": QWEN3_8B, "qwen3-tiny": QWEN3_TINY}[a.model]
+    t_load = time.time()
+    max_ctx = a.ctx + a.warmup + a.steps + 16
+    dec = Qwen3Decoder(cfg, batch=a.batch, max_ctx=max_ctx, device="cuda")
+    dec.fill_context(a.ctx)
+    dec.capture(warmup=1)
+    for _ in range(a.warmup):
+        dec.step()
+    torch.cuda.synchronize()
+    free, total = torch.cuda.mem_get_info()
+    ready = {"load_s": round(time.time() - t_load, 2), "mem_total_mib": total >> 20,
+             "mem_free_mib": free >> 20, "allocated_mib": torch.cuda.memory_allocated() >> 20,
+             "cus": torch.cuda.get_device_properties(0).multi_processor_count,
+             "preload": os.environ.get("LD_PRELOAD", ""), "cu_mask": os.environ.get("HSA_CU_MASK", "")}
+    print("READY " + json.dumps(ready), flush=True)
+    if sys.stdin.readline().strip() != "GO":
+        return 0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        dec.step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    print("DONE " + json.dumps({"seconds": dt, "tokens": a.batch * a.steps,
+                                "tok_s": a.batch * a.steps / dt}), flush=True)
+    return 0
+
+
+def spawn_round(specs, physical_gpu, cache_dir: Path, log_dir: Path, child_args, tag: str):
+    procs = []
+    for s in specs:
+        env = slice_env(s, physical_gpu, cache_dir)
+        procs.append(SliceProc(s, env, child_args, log_dir / f"{tag}_slice{s.index}.log"))
+    return procs
+
+
+def run_round(procs, barrier=None, sync=None, load_timeout=900, run_timeout=900) -> dict:
+    """Drive one spawned round through LOAD/READY/GO/DONE; returns timings."""
+    for p in procs:
+        p.send("LOAD")
+    readies = [p.expect("READY", load_timeout) for p in procs]
+    if barrier:
+        barrier()
+    if sync:
+        sync()
+    t0 = time.perf_counter()
+    for p in procs:
+        p.send("GO")
+    dones = [p.expect("DONE", run_timeout) for p in procs]
+    if sync:
+        sync()
+    t1 = time.perf_counter()
+    if barrier:
+        barrier()
+    for p in procs:
+        p.close()
+    return {"wall_s": t1 - t0, "ready": readies, "done": dones,
+            "tokens": sum(d["tokens"] for d in dones)}
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "--child":
+        sys.exit(child_main(sys.argv[2:]))
+    print("use bench.py", file=sys.stderr)
+    sys.exit(2)

@@ -1,0 +1,206 @@
+"""Qwen3-architecture decoder for the isolation benchmark (random-init weights).
+
+The reference's only benchmark is vLLM serving Qwen3-8B bf16 at TP=1
+(benchmarks/ai-benchmark/Dockerfile:7-9, benchmark.py:72-75) inside a HAMi
+slice vs. natively.  This module is the MI355X-native stand-in for that
+workload: a Qwen3-8B-shaped decoder (GQA 32q/8kv x 128, per-head QK RMSNorm,
+NeoX RoPE theta 1e6, SwiGLU 12288, vocab 151936) whose decode step runs
+  * GEMMs on hipBLASLt (``F.linear``, the "plain library GEMM" path),
+  * every other op on the hand-written gfx950 kernels of libmivgpu_ops.so,
+  * the whole step captured in one hipGraph (launch overhead -> one replay).
+No network: weights are random normal(0, 0.02) of the exact architecture.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from k8s_vgpu_scheduler_amd import ops
+from k8s_vgpu_scheduler_amd.ops import reference as ref
+
+
+@dataclass(frozen=True)
+class Qwen3Config:
+    name: str = "Qwen3-8B"
+    hidden: int = 4096
+    layers: int = 36
+    heads: int = 32
+    kv_heads: int = 8
+    head_dim: int = 128
+    intermediate: int = 12288
+    vocab: int = 151936
+    rope_theta: float = 1_000_000.0
+    eps: float = 1e-6
+    tie_embeddings: bool = False
+
+    @property
+    def qkv_dim(self) -> int:
+        return (self.heads + 2 * self.kv_heads) * self.head_dim
+
+    def param_count(self) -> int:
+        h, l = self.hidden, self.layers
+        per_layer = (self.qkv_dim * h + self.heads * self.head_dim * h + 2 * self.intermediate * h
+                     + self.intermediate * h + 2 * h + 2 * self.head_dim)
+        emb = self.vocab * h * (1 if self.tie_embeddings else 2)
+        return l * per_layer + emb + h
+
+
+QWEN3_8B = Qwen3Config()
+# Same family, tiny: CPU tests and GPU smoke.
+QWEN3_TINY = Qwen3Config(name="Qwen3-tiny", hidden=512, layers=2, heads=8, kv_heads=2,
+                         head_dim=128, intermediate=1024, vocab=4096)
+
+
+class Qwen3Weights:
+    def __init__(self, cfg: Qwen3Config, device, dtype=torch.bfloat16, seed: int = 0):
+        g = torch.Generator(device=device)
+        g.manual_seed(seed)
+        std = 0.02
+
+        def rnd(*shape):
+            return (torch.randn(*shape, generator=g, device=device, dtype=torch.float32) * std).to(dtype)
+
+        def ones(n):
+            # Norm weights around 1 so activations stay O(1) through 36 layers.
+            return (1.0 + 0.05 * torch.randn(n, generator=g, device=device)).to(dtype)
+
+        h = cfg.hidden
+        self.embed = rnd(cfg.vocab, h)
+        self.layers = []
+        for _ in range(cfg.layers):
+            self.layers.append(dict(
+                ln1=ones(h), ln2=ones(h),
+                wqkv=rnd(cfg.qkv_dim, h),
+                q_norm=ones(cfg.head_dim), k_norm=ones(cfg.head_dim),
+                wo=rnd(h, cfg.heads * cfg.head_dim),
+                wgu=rnd(2 * cfg.intermediate, h),
+                wd=rnd(h, cfg.intermediate),
+            ))
+        self.final_norm = ones(h)
+        self.lm_head = self.embed if cfg.tie_embeddings else rnd(cfg.vocab, h)
+
+
+class Qwen3Decoder:
+    """Static-shape batched decoder with a persistent KV cache.
+
+    ``native=True`` runs the HIP kernels (required on GPU); ``native=False``
+    uses the fp32 PyTorch references (CPU tests).
+    """
+
+    def __init__(self, cfg: Qwen3Config, batch: int, max_ctx: int, device="cuda",
+                 native: bool | None = None, seed: int = 0):
+        self.cfg = cfg
+        self.B = batch
+        self.T = max_ctx
+        self.device = torch.device(device)
+        self.native = (self.device.type == "cuda") if native is None else native
+        if self.native:
+            ops.require_native()
+        self.w = Qwen3Weights(cfg, self.device, seed=seed)
+        dt = torch.bfloat16
+        kvshape = (batch, cfg.kv_heads, max_ctx, cfg.head_dim)
+        self.k_cache = [torch.zeros(kvshape, dtype=dt, device=self.device) for _ in range(cfg.layers)]
+        self.v_cache = [torch.zeros(kvshape, dtype=dt, device=self.device) for _ in range(cfg.layers)]
+        self.tokens = torch.zeros(batch, dtype=torch.long, device=self.device)
+        self.pos = torch.zeros(batch, dtype=torch.int32, device=self.device)
+        self.seqlens = torch.ones(batch, dtype=torch.int32, device=self.device)
+        self.nsplit = max(1, math.ceil(max_ctx / (ops.attn_split() if self.native else 256)))
+        h = cfg.hidden
+        # Static activation buffers (graph-capture friendly).
+        self.res = torch.zeros(batch, h, dtype=dt, device=self.device)
+        self.h = torch.zeros(batch, h, dtype=dt, device=self.device)
+        self.q = torch.zeros(batch, cfg.heads, cfg.head_dim, dtype=dt, device=self.device)
+        self.attn = torch.zeros(batch, cfg.heads * cfg.head_dim, dtype=dt, device=self.device)
+        self.act = torch.zeros(batch, cfg.intermediate, dtype=dt, device=self.device)
+        self.o_part = torch.zeros(batch * cfg.heads * self.nsplit * cfg.head_dim, dtype=torch.float32,
+                                  device=self.device)
+        self.ml_part = torch.zeros(batch * cfg.heads * self.nsplit * 2, dtype=torch.float32,
+                                   device=self.device)
+        self.graph = None
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+
+    # ------------------------------------------------------------- setup --
+    def fill_context(self, ctx_len: int, seed: int = 1):
+        """Synthetic prompt state: random KV for the first ctx_len positions."""
+        assert 0 < ctx_len < self.T
+        g = torch.Generator(device=self.device)
+        g.manual_seed(seed)
+        for kc, vc in zip(self.k_cache, self.v_cache):
+            kc[:, :, :ctx_len].normal_(0, 1.0, generator=g)
+            vc[:, :, :ctx_len].normal_(0, 1.0, generator=g)
+        self.pos.fill_(ctx_len)
+        self.seqlens.fill_(ctx_len + 1)
+        self.tokens.copy_(torch.randint(0, self.cfg.vocab, (self.B,), generator=g, device=self.device))
+
+    # -------------------------------------------------------------- step --
+    def _step_impl(self):
+        cfg, w = self.cfg, self.w
+        x = F.embedding(self.tokens, w.embed)
+        self.res.copy_(x)
+        L = cfg.layers
+        if self.native:
+            ops.rmsnorm(self.res, w.layers[0]["ln1"], cfg.eps, out=self.h)
+        else:
+            self.h.copy_(ref.rmsnorm(self.res, w.layers[0]["ln1"], cfg.eps))
+        for li, lw in enumerate(w.layers):
+            qkv = F.linear(self.h, lw["wqkv"])
+            if self.native:
+                ops.qk_norm_rope_kv(qkv, lw["q_norm"], lw["k_norm"], self.pos, self.q,
+                                    self.k_cache[li], self.v_cache[li], cfg.heads, cfg.kv_heads,
+                                    cfg.head_dim, cfg.eps, cfg.rope_theta)
+                ops.decode_attention(self.q, self.k_cache[li], self.v_cache[li], self.seqlens,
+                                     self.attn, self.o_part, self.ml_part, cfg.heads, cfg.kv_heads,
+                                     cfg.head_dim, self.nsplit, self.scale)
+            else:
+                ref.qk_norm_rope_kv(qkv, lw["q_norm"], lw["k_norm"], self.pos, self.q,
+                                    self.k_cache[li], self.v_cache[li], cfg.heads, cfg.kv_heads,
+                                    cfg.head_dim, cfg.eps, cfg.rope_theta)
+                self.attn.copy_(ref.decode_attention(self.q, self.k_cache[li], self.v_cache[li],
+                                                     self.seqlens, cfg.heads, cfg.kv_heads,
+                                                     cfg.head_dim, self.scale).view(self.B, -1))
+            o = F.linear(self.attn, lw["wo"])
+            if self.native:
+                ops.add_rmsnorm(o, self.res, lw["ln2"], cfg.eps, out=self.h)
+            else:
+                self.h.copy_(ref.add_rmsnorm(o, self.res, lw["ln2"], cfg.eps))
+            gu = F.linear(self.h, lw["wgu"])
+            if self.native:
+                ops.silu_mul(gu, out=self.act)
+            else:
+                self.act.copy_(ref.silu_mul(gu))
+            d = F.linear(self.act, lw["wd"])
+            nxt = w.layers[li + 1]["ln1"] if li + 1 < L else w.final_norm
+            if self.native:
+                ops.add_rmsnorm(d, self.res, nxt, cfg.eps, out=self.h)
+            else:
+                self.h.copy_(ref.add_rmsnorm(d, self.res, nxt, cfg.eps))
+        logits = F.linear(self.h, w.lm_head)
+        self.tokens.copy_(torch.argmax(logits, dim=-1))
+        self.pos.add_(1)
+        self.seqlens.add_(1)
+        return logits
+
+    def capture(self, warmup: int = 2):
+        """Capture one decode step into a hipGraph (state advances per replay)."""
+        assert self.device.type == "cuda"
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._step_impl()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._step_impl()
+        torch.cuda.synchronize()
+
+    def step(self):
+        if self.graph is not None:
+            self.graph.replay()
+            return None
+        return self._step_impl()

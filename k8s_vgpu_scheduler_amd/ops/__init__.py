@@ -1,0 +1,123 @@
+"""ctypes bindings for ``libmivgpu_ops.so`` (hand-written gfx950 kernels).
+
+The kernels take raw device pointers and the caller's HIP stream, so they are
+captured by ``torch.cuda.CUDAGraph`` like any other launch.  On a GPU box the
+library MUST load -- ops fail loudly instead of silently falling back to
+PyTorch (``require_native()``); the pure-PyTorch reference implementations in
+:mod:`k8s_vgpu_scheduler_amd.ops.reference` exist for numerics tests and for
+CPU-only development.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+_LIB_PATH = Path(__file__).resolve().parents[1] / "lib" / "libmivgpu_ops.so"
+_lib = None
+
+
+class NativeOpsUnavailable(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not _LIB_PATH.exists():
+            raise NativeOpsUnavailable(
+                f"{_LIB_PATH} missing: run `python -m k8s_vgpu_scheduler_amd.utils.build ops`")
+        # torch must be initialised first so the HIP runtime it bundles
+        # (SONAME libamdhip64.so.7) is the one our library binds to.
+        import torch.cuda  # noqa: F401
+        L = ctypes.CDLL(str(_LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+        vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+        L.mivgpu_rmsnorm.argtypes = [vp, vp, vp, i, i, f, vp]
+        L.mivgpu_add_rmsnorm.argtypes = [vp, vp, vp, vp, i, i, f, vp]
+        L.mivgpu_qk_norm_rope_kv.argtypes = [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, f, f, vp]
+        L.mivgpu_decode_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, f, vp]
+        L.mivgpu_silu_mul.argtypes = [vp, vp, i, i, vp]
+        for fn in ("mivgpu_rmsnorm", "mivgpu_add_rmsnorm", "mivgpu_qk_norm_rope_kv",
+                   "mivgpu_decode_attention", "mivgpu_silu_mul", "mivgpu_ops_attn_split"):
+            getattr(L, fn).restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def available() -> bool:
+    try:
+        lib()
+        return torch.cuda.is_available()
+    except (NativeOpsUnavailable, OSError):
+        return False
+
+
+def require_native():
+    """Raise unless the HIP op library is loadable and a GPU is present."""
+    if not torch.cuda.is_available():
+        raise NativeOpsUnavailable("no GPU visible")
+    lib()
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t: torch.Tensor):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _check(rc: int, name: str):
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with code {rc}")
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | None = None):
+    out = torch.empty_like(x) if out is None else out
+    rows, dim = x.reshape(-1, x.shape[-1]).shape
+    _check(lib().mivgpu_rmsnorm(_p(x), _p(w), _p(out), rows, dim, eps, _stream()), "rmsnorm")
+    return out
+
+
+def add_rmsnorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: float,
+                out: torch.Tensor | None = None):
+    """res += x (in place); returns rmsnorm(res) * w."""
+    out = torch.empty_like(x) if out is None else out
+    rows, dim = x.reshape(-1, x.shape[-1]).shape
+    _check(lib().mivgpu_add_rmsnorm(_p(x), _p(res), _p(w), _p(out), rows, dim, eps, _stream()),
+           "add_rmsnorm")
+    return out
+
+
+def qk_norm_rope_kv(qkv, q_norm_w, k_norm_w, pos, q_out, k_cache, v_cache, n_q_heads, n_kv_heads,
+                    head_dim, eps, theta):
+    B = qkv.shape[0]
+    max_ctx = k_cache.shape[2]
+    _check(lib().mivgpu_qk_norm_rope_kv(_p(qkv), _p(q_norm_w), _p(k_norm_w), _p(pos), _p(q_out),
+                                        _p(k_cache), _p(v_cache), B, n_q_heads, n_kv_heads, head_dim,
+                                        max_ctx, eps, theta, _stream()), "qk_norm_rope_kv")
+
+
+def attn_split() -> int:
+    return int(lib().mivgpu_ops_attn_split())
+
+
+def decode_attention(q, k_cache, v_cache, seqlens, out, o_part, ml_part, n_q_heads, n_kv_heads,
+                     head_dim, nsplit, scale):
+    B = q.shape[0]
+    max_ctx = k_cache.shape[2]
+    _check(lib().mivgpu_decode_attention(_p(q), _p(k_cache), _p(v_cache), _p(seqlens), _p(out),
+                                         _p(o_part), _p(ml_part), B, n_q_heads, n_kv_heads, head_dim,
+                                         max_ctx, nsplit, scale, _stream()), "decode_attention")
+    return out
+
+
+def silu_mul(gate_up: torch.Tensor, out: torch.Tensor | None = None):
+    rows, two_i = gate_up.shape
+    inter = two_i // 2
+    out = torch.empty(rows, inter, dtype=gate_up.dtype, device=gate_up.device) if out is None else out
+    _check(lib().mivgpu_silu_mul(_p(gate_up), _p(out), rows, inter, _stream()), "silu_mul")
+    return out

@@ -1,0 +1,193 @@
+"""GPU isolation probe: runs workload children natively and under libmivgpu.so.
+
+Each scenario is a separate child process (the shim must be LD_PRELOADed
+before the HIP runtime initialises), started BEFORE this process touches the
+GPU.  Children print one JSON line.  Used for the first-light GPU validation
+and by ``bench.py``/tests marked ``gpu``.
+
+    python -m k8s_vgpu_scheduler_amd.shim.probe --out gpurun_out/probe.json
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+from k8s_vgpu_scheduler_amd.shim import shim_env, shim_path
+
+
+def child_matmul(args) -> dict:
+    import torch
+
+    dev = torch.device("cuda:0")
+    free, total = torch.cuda.mem_get_info()
+    props = torch.cuda.get_device_properties(0)
+    n = args.n
+    a = torch.randn(n, n, device=dev, dtype=torch.bfloat16)
+    b = torch.randn(n, n, device=dev, dtype=torch.bfloat16)
+    for _ in range(3):
+        c = a @ b
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.iters):
+        c = a @ b
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    tflops = 2 * n ** 3 * args.iters / dt / 1e12
+    out = {"mode": "matmul", "tflops": tflops, "seconds": dt, "mem_free_mib": free >> 20,
+           "mem_total_mib": total >> 20, "props_total_mib": props.total_memory >> 20,
+           "cus": props.multi_processor_count}
+    if args.oom_probe_mib:
+        try:
+            x = torch.empty(args.oom_probe_mib << 20, dtype=torch.uint8, device=dev)
+            out["oom_probe"] = "allocated"
+            del x
+        except torch.OutOfMemoryError:
+            out["oom_probe"] = "oom"
+        except RuntimeError as e:  # pragma: no cover
+            out["oom_probe"] = f"error: {e}"[:200]
+    del c
+    out.update(gate_stats())
+    return out
+
+
+def gate_stats() -> dict:
+    """Governor counters of the preloaded shim (empty if not preloaded)."""
+    import ctypes
+
+    try:
+        fn = ctypes.CDLL(None).mivgpu_gate_stats
+    except AttributeError:
+        return {}
+    b, h, g = ctypes.c_ulonglong(), ctypes.c_ulonglong(), ctypes.c_ulonglong()
+    if fn(0, ctypes.byref(b), ctypes.byref(h), ctypes.byref(g)) != 0:
+        return {"gate": "inactive"}
+    return {"gate_busy_ms": b.value / 1e6, "gate_held_ms": h.value / 1e6, "gates": g.value}
+
+
+def child_stream(args) -> dict:
+    import torch
+
+    dev = torch.device("cuda:0")
+    n = args.n * 1024 * 1024 * 16  # float elements
+    x = torch.empty(n, device=dev, dtype=torch.float32).fill_(1.0)
+    y = torch.empty_like(x)
+    for _ in range(3):
+        y.copy_(x)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.iters):
+        y.copy_(x)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"mode": "stream", "gbps": 2 * x.numel() * 4 * args.iters / dt / 1e9, "seconds": dt}
+
+
+def run_child(mode: str, env_extra: dict, shim: bool, extra_args=(), timeout=300) -> dict:
+    env = dict(os.environ)
+    if shim:
+        env.update(shim_env())
+    env.update({k: str(v) for k, v in env_extra.items()})
+    cmd = [sys.executable, "-m", "k8s_vgpu_scheduler_amd.shim.probe", "--child", mode, *extra_args]
+    t0 = time.time()
+    r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=timeout)
+    res = {"rc": r.returncode, "wall_s": round(time.time() - t0, 2)}
+    for line in r.stdout.splitlines():
+        if line.startswith("{"):
+            res.update(json.loads(line))
+    if r.returncode != 0:
+        res["stderr"] = r.stderr[-2000:]
+    return res
+
+
+def run_parallel(mode: str, envs: list, shim: bool, extra_args=(), timeout=300) -> list:
+    procs = []
+    for e in envs:
+        env = dict(os.environ)
+        if shim:
+            env.update(shim_env())
+        env.update({k: str(v) for k, v in e.items()})
+        cmd = [sys.executable, "-m", "k8s_vgpu_scheduler_amd.shim.probe", "--child", mode, *extra_args]
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                      text=True))
+    outs = []
+    for p in procs:
+        try:
+            so, se = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            so, se = p.communicate()
+        res = {"rc": p.returncode}
+        for line in so.splitlines():
+            if line.startswith("{"):
+                res.update(json.loads(line))
+        if p.returncode != 0:
+            res["stderr"] = se[-1500:]
+        outs.append(res)
+    return outs
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--child", default=None)
+    ap.add_argument("--n", type=int, default=8192)
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--oom-probe-mib", type=int, default=0)
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--quick", action="store_true")
+    args = ap.parse_args()
+    if args.child:
+        fn = {"matmul": child_matmul, "stream": child_stream}[args.child]
+        print(json.dumps(fn(args)), flush=True)
+        return
+    tmp = Path(os.environ.get("TMPDIR", "/tmp")) / f"mivgpu-probe-{os.getpid()}"
+    tmp.mkdir(parents=True, exist_ok=True)
+    mm = ["--n", "8192", "--iters", "60"]
+    results = {}
+    if args.quick:
+        for pct in (25, 50, 75):
+            results[f"gate_force_{pct}"] = run_child(
+                "matmul", {"MIVGPU_SHARED_CACHE": tmp / f"q{pct}.cache", "HIP_DEVICE_CORE_LIMIT": pct,
+                           "GPU_CORE_UTILIZATION_POLICY": "force"}, True, ["--n", "8192", "--iters", "200"])
+        results["native_200"] = run_child("matmul", {}, False, ["--n", "8192", "--iters", "200"])
+        txt = json.dumps(results, indent=1)
+        print(txt)
+        if args.out:
+            Path(args.out).parent.mkdir(parents=True, exist_ok=True)
+            Path(args.out).write_text(txt)
+        return
+    results["native"] = run_child("matmul", {}, False, mm)
+    results["shim_nolimit"] = run_child("matmul", {"MIVGPU_SHARED_CACHE": tmp / "a.cache"}, True, mm)
+    results["shim_36g"] = run_child(
+        "matmul", {"MIVGPU_SHARED_CACHE": tmp / "b.cache", "HIP_DEVICE_MEMORY_LIMIT_0": "36864m"},
+        True, [*mm, "--oom-probe-mib", "40000"])
+    for cus in (64, 128):
+        results[f"cumask_{cus}"] = run_child("matmul", {"HSA_CU_MASK": f"0:0-{cus - 1}"}, False, mm)
+    results["gate_force_25"] = run_child(
+        "matmul", {"MIVGPU_SHARED_CACHE": tmp / "c.cache", "HIP_DEVICE_CORE_LIMIT": "25",
+                   "GPU_CORE_UTILIZATION_POLICY": "force", "MIVGPU_LOG_LEVEL": "3"}, True, mm)
+    results["stream_native"] = run_child("stream", {}, False, ["--n", "64", "--iters", "50"])
+    results["stream_cumask_64"] = run_child("stream", {"HSA_CU_MASK": "0:0-63"}, False,
+                                            ["--n", "64", "--iters", "50"])
+    if not args.quick:
+        envs = [{"HSA_CU_MASK": f"0:{i * 64}-{i * 64 + 63}"} for i in range(4)]
+        results["4x_cumask_parallel"] = run_parallel("matmul", envs, False, mm)
+        envs = [{"MIVGPU_SHARED_CACHE": tmp / f"g{i}.cache", "HIP_DEVICE_CORE_LIMIT": "25",
+                 "GPU_CORE_UTILIZATION_POLICY": "force"} for i in range(4)]
+        results["4x_gate_parallel"] = run_parallel("matmul", envs, True, mm)
+        results["4x_native_parallel"] = run_parallel("matmul", [{} for _ in range(4)], False, mm)
+    txt = json.dumps(results, indent=1)
+    print(txt)
+    if args.out:
+        Path(args.out).parent.mkdir(parents=True, exist_ok=True)
+        Path(args.out).write_text(txt)
+
+
+if __name__ == "__main__":
+    main()

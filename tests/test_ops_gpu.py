@@ -1,0 +1,132 @@
+"""Numerics of the hand-written gfx950 kernels vs plain PyTorch fp32 references."""
+
+import math
+
+import pytest
+import torch
+
+from k8s_vgpu_scheduler_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from k8s_vgpu_scheduler_amd import ops as o
+    from k8s_vgpu_scheduler_amd.utils import build
+
+    build.build_ops()
+    o.require_native()  # fail loudly: no silent fallback on the GPU box
+    return o
+
+
+def _close(a, b, tol):
+    err = (a.float() - b.float()).abs().max().item()
+    scale = b.float().abs().max().item() + 1e-6
+    assert err / scale < tol, f"rel err {err / scale:.3e} >= {tol}"
+
+
+@pytest.mark.parametrize("rows,dim", [(1, 4096), (33, 4096), (8, 512), (5, 8192)])
+def test_rmsnorm(ops, rows, dim):
+    x = torch.randn(rows, dim, device="cuda", dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(dim, device="cuda")).to(torch.bfloat16)
+    _close(ops.rmsnorm(x, w, 1e-6), ref.rmsnorm(x, w, 1e-6), 2e-2)
+
+
+def test_add_rmsnorm(ops):
+    x = torch.randn(17, 4096, device="cuda", dtype=torch.bfloat16)
+    r = torch.randn(17, 4096, device="cuda", dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(4096, device="cuda")).to(torch.bfloat16)
+    r2 = r.clone()
+    out = ops.add_rmsnorm(x, r, w, 1e-6)
+    exp = ref.add_rmsnorm(x, r2, w, 1e-6)
+    _close(r, r2, 1e-2)
+    _close(out, exp, 2e-2)
+
+
+@pytest.mark.parametrize("B,Hq,Hkv", [(4, 32, 8), (3, 8, 2)])
+def test_qk_norm_rope_kv(ops, B, Hq, Hkv):
+    D, T = 128, 64
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    qw = (1 + 0.1 * torch.randn(D, device="cuda")).to(torch.bfloat16)
+    kw = (1 + 0.1 * torch.randn(D, device="cuda")).to(torch.bfloat16)
+    pos = torch.tensor([0, 5, 63, 17][:B], dtype=torch.int32, device="cuda")
+    q1 = torch.empty(B, Hq, D, device="cuda", dtype=torch.bfloat16)
+    k1 = torch.zeros(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
+    v1 = torch.zeros_like(k1)
+    q2, k2, v2 = q1.clone(), k1.clone(), v1.clone()
+    ops.qk_norm_rope_kv(qkv, qw, kw, pos, q1, k1, v1, Hq, Hkv, D, 1e-6, 1e6)
+    ref.qk_norm_rope_kv(qkv, qw, kw, pos, q2, k2, v2, Hq, Hkv, D, 1e-6, 1e6)
+    torch.cuda.synchronize()
+    _close(q1, q2, 2e-2)
+    _close(k1, k2, 2e-2)
+    _close(v1, v2, 1e-3)
+
+
+def test_qk_norm_rope_kv_out_of_range_pos_is_dropped(ops):
+    B, Hq, Hkv, D, T = 2, 8, 2, 128, 16
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    w = torch.ones(D, device="cuda", dtype=torch.bfloat16)
+    pos = torch.tensor([T, T + 100], dtype=torch.int32, device="cuda")
+    q = torch.empty(B, Hq, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.zeros(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.zeros_like(k)
+    ops.qk_norm_rope_kv(qkv, w, w, pos, q, k, v, Hq, Hkv, D, 1e-6, 1e6)
+    torch.cuda.synchronize()
+    assert k.abs().sum().item() == 0 and v.abs().sum().item() == 0
+
+
+@pytest.mark.parametrize("B,Hq,Hkv,T,lens", [
+    (2, 32, 8, 1024, [1, 1000]),
+    (3, 32, 8, 600, [257, 256, 599]),
+    (2, 8, 8, 300, [300, 7]),
+    (1, 16, 2, 2048, [2048]),
+])
+def test_decode_attention(ops, B, Hq, Hkv, T, lens):
+    D = 128
+    q = torch.randn(B, Hq, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
+    # Spike one key so the softmax max shifts inside a later split.
+    k[0, 0, min(lens[0], T) - 1] *= 8
+    seqlens = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    nsplit = math.ceil(T / ops.attn_split())
+    out = torch.empty(B, Hq * D, device="cuda", dtype=torch.bfloat16)
+    o_part = torch.empty(B * Hq * nsplit * D, device="cuda", dtype=torch.float32)
+    ml = torch.empty(B * Hq * nsplit * 2, device="cuda", dtype=torch.float32)
+    scale = 1 / math.sqrt(D)
+    ops.decode_attention(q, k, v, seqlens, out, o_part, ml, Hq, Hkv, D, nsplit, scale)
+    exp = ref.decode_attention(q, k, v, seqlens, Hq, Hkv, D, scale)
+    _close(out.view(B, Hq, D), exp, 2e-2)
+
+
+@pytest.mark.parametrize("rows,inter", [(1, 12288), (32, 12288), (7, 1024)])
+def test_silu_mul(ops, rows, inter):
+    gu = torch.randn(rows, 2 * inter, device="cuda", dtype=torch.bfloat16)
+    _close(ops.silu_mul(gu), ref.silu_mul(gu), 2e-2)
+
+
+def test_decoder_native_matches_reference():
+    """Whole tiny decoder: HIP path vs fp32 reference path, same weights."""
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
+
+    a = Qwen3Decoder(QWEN3_TINY, batch=3, max_ctx=64, device="cuda", native=True, seed=3)
+    b = Qwen3Decoder(QWEN3_TINY, batch=3, max_ctx=64, device="cuda", native=False, seed=3)
+    a.fill_context(20)
+    b.fill_context(20)
+    la = a.step()
+    lb = b.step()
+    _close(la, lb, 5e-2)
+
+
+def test_decoder_graph_replay_advances_state():
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
+
+    d = Qwen3Decoder(QWEN3_TINY, batch=2, max_ctx=64, device="cuda")
+    d.fill_context(10)
+    d.capture(warmup=1)
+    p0 = d.pos.clone()
+    for _ in range(3):
+        d.step()
+    torch.cuda.synchronize()
+    assert torch.equal(d.pos, p0 + 3)
