@@ -41,6 +41,11 @@ struct mivgpu_gate_state {
 
 // Written with plain system-visible stores into fine-grained host memory so
 // the shim's bookkeeping thread can read stats without synchronising a stream.
+struct mivgpu_gate_trace_entry {
+  long long now_ns, submit_ns, prev_exit_ns, busy_ns, hold_ns, tokens_ns;
+  long long slot, pad;
+};
+#define MIVGPU_GATE_TRACE 128
 struct mivgpu_gate_host_stats {
   unsigned long long busy_total_ns;
   unsigned long long held_total_ns;
@@ -49,6 +54,7 @@ struct mivgpu_gate_host_stats {
   long long last_tokens_ns;
   long long last_hold_ns;
   unsigned long long pad[2];
+  mivgpu_gate_trace_entry trace[MIVGPU_GATE_TRACE];  // ring, index = gates % N
 };
 
 __device__ __forceinline__ long long rt_ns() {
@@ -103,11 +109,16 @@ mivgpu_gate(mivgpu_gate_state* st, mivgpu_gate_host_stats* hs, long long submit_
   // GPU time this stream consumed since its previous gate.  The stream is
   // in-order, so everything between max(previous gate exit, first submission
   // after it) and `now` was the stream's own work.
+  // submit_ns < 0: nothing was submitted on this stream since its previous
+  // gate, so the time since then was idle, not busy.
   const long long prev_exit = aload(&st->slot_exit_ns[slot]);
   long long begin = prev_exit > submit_ns ? prev_exit : submit_ns;
-  if (begin <= 0 || begin > now) begin = now;
+  if (submit_ns < 0 || begin <= 0 || begin > now) begin = now;
   const long long busy = now - begin;
   tokens -= busy;
+  // Bound the debt to one burst: a single mis-measured interval can never
+  // stall a tenant for longer than cap / rate.
+  if (tokens < -cap_ns) tokens = -cap_ns;
 
   long long hold = 0;
   if (tokens < 0) {
@@ -136,6 +147,14 @@ mivgpu_gate(mivgpu_gate_state* st, mivgpu_gate_host_stats* hs, long long submit_
     __hip_atomic_store(&hs->last_now_ns, now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&hs->last_tokens_ns, tokens, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&hs->last_hold_ns, hold, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    mivgpu_gate_trace_entry* e = &hs->trace[(gates - 1) % MIVGPU_GATE_TRACE];
+    e->now_ns = now;
+    e->submit_ns = submit_ns;
+    e->prev_exit_ns = prev_exit;
+    e->busy_ns = busy;
+    e->hold_ns = hold;
+    e->tokens_ns = tokens;
+    e->slot = slot;
   }
 
   // Hold the stream on-device.  ~3.4 us per s_sleep(127) at 2.4 GHz; bounded

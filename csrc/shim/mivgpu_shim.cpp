@@ -167,6 +167,10 @@ REAL_DECL(hipError_t, hipHostMalloc, "hip_4.2", (void**, size_t, unsigned int))
 REAL_DECL(hipError_t, hipHostFree, "hip_4.2", (void*))
 REAL_DECL(hipError_t, hipHostGetDevicePointer, "hip_4.2", (void**, void*, unsigned int))
 REAL_DECL(hipError_t, hipStreamSynchronize, "hip_4.2", (hipStream_t))
+REAL_DECL(hipError_t, hipStreamSynchronize_spt, "hip_5.2", (hipStream_t))
+REAL_DECL(hipError_t, hipDeviceSynchronize, "hip_4.2", (void))
+REAL_DECL(hipError_t, hipStreamBeginCapture, "hip_4.3", (hipStream_t, hipStreamCaptureMode))
+REAL_DECL(hipError_t, hipStreamBeginCapture_spt, "hip_5.3", (hipStream_t, hipStreamCaptureMode))
 REAL_DECL(hipError_t, hipSetDevice, "hip_4.2", (int))
 REAL_DECL(hipError_t, hipMemset, "hip_4.2", (void*, int, size_t))
 
@@ -646,12 +650,15 @@ bool release_tracked(void* p) {
 std::atomic<uint64_t> g_last_kernel_write_ns{0};
 std::atomic<uint64_t> g_launches_local{0};
 
-// Governor (gate) per device.
+// Governor (gate) per device.  Host stats = 8 counters + a 128-entry trace
+// ring of 8 x int64 per gate (layout: governor.hip mivgpu_gate_host_stats).
+constexpr size_t kHostStatsBytes = 64 + 128 * 64;
 struct GateSlot {
   hipStream_t stream;
   uint64_t last_gate_host_ns;
-  uint64_t first_submit_host_ns;
+  uint64_t first_submit_host_ns;   // first launch since the last gate (0 = none pending)
   bool used;
+  uint64_t last_launch_host_ns;    // most recent launch on this stream
 };
 struct DeviceGate {
   std::mutex mu;
@@ -664,6 +671,7 @@ struct DeviceGate {
   void* host_stats = nullptr;   // fine-grained host memory
   long long* clock_host = nullptr;
   int64_t offset_ns = 0;        // device_ns - host_mono_ns
+  bool stamper_started = false;
   GateSlot slots[64];
 };
 DeviceGate g_gates[MIVGPU_MAX_DEVICES];
@@ -689,10 +697,10 @@ bool gate_init_locked(int dev, DeviceGate& G) {
   // State lives in device memory; it is not charged to the tenant's quota.
   if (real_hipMalloc()(&G.state, 4096) != hipSuccess) return false;
   if (real_hipMemset()) real_hipMemset()(G.state, 0, 4096);
-  if (real_hipHostMalloc()(&G.host_stats, 4096, hipHostMallocCoherent | hipHostMallocMapped) !=
+  if (real_hipHostMalloc()(&G.host_stats, kHostStatsBytes, hipHostMallocCoherent | hipHostMallocMapped) !=
       hipSuccess)
     G.host_stats = nullptr;
-  if (G.host_stats) memset(G.host_stats, 0, 4096);
+  if (G.host_stats) memset(G.host_stats, 0, kHostStatsBytes);
   if (real_hipHostMalloc()((void**)&G.clock_host, 64, hipHostMallocCoherent | hipHostMallocMapped) !=
       hipSuccess)
     return false;
@@ -732,37 +740,12 @@ inline bool gate_wanted(int dev) {
   return __atomic_load_n(&g_region->cu_mask_count[dev], __ATOMIC_RELAXED) == 0 || sw == 1;
 }
 
-void maybe_gate(hipStream_t stream) {
-  int dev = current_device();
-  if (!gate_wanted(dev)) return;
-  // Never inject into a stream that is being captured: the gate would be baked
-  // into the graph with stale arguments.  Graph replays are gated at launch.
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (real_hipStreamIsCapturing() && real_hipStreamIsCapturing()(stream, &cs) == hipSuccess &&
-      cs != hipStreamCaptureStatusNone)
-    return;
-  DeviceGate& G = g_gates[dev];
-  std::lock_guard<std::mutex> lk(G.mu);
-  if (!G.tried) G.ok = gate_init_locked(dev, G);
-  if (!G.ok) return;
-  uint64_t now = mono_ns();
-  int slot = -1, free_slot = -1;
-  for (int i = 0; i < 64; ++i) {
-    if (G.slots[i].used && G.slots[i].stream == stream) {
-      slot = i;
-      break;
-    }
-    if (!G.slots[i].used && free_slot < 0) free_slot = i;
-  }
-  if (slot < 0) {
-    slot = free_slot >= 0 ? free_slot : (int)(reinterpret_cast<uintptr_t>(stream) % 64);
-    G.slots[slot] = GateSlot{stream, 0, now, true};
-  }
+// Enqueue one gate on `stream` for slot S (caller holds G.mu, G.ok).
+void enqueue_gate_locked(int dev, DeviceGate& G, int slot, hipStream_t stream, uint64_t now) {
   GateSlot& S = G.slots[slot];
-  if (S.first_submit_host_ns == 0) S.first_submit_host_ns = now;
-  if (S.last_gate_host_ns != 0 && now - S.last_gate_host_ns < g_cfg.gate_min_interval_ns) return;
-  long long submit_dev = (long long)S.first_submit_host_ns + G.offset_ns;
-  unsigned int rate_ppm = (unsigned int)(__atomic_load_n(&g_region->cu_limit[dev], __ATOMIC_RELAXED) * 10000ull);
+  long long submit_dev = S.first_submit_host_ns ? (long long)S.first_submit_host_ns + G.offset_ns : -1;
+  unsigned int rate_ppm =
+      (unsigned int)(__atomic_load_n(&g_region->cu_limit[dev], __ATOMIC_RELAXED) * 10000ull);
   long long cap = g_cfg.gate_cap_ns, hold = g_cfg.gate_max_hold_ns;
   int slot_arg = slot;
   void* state = G.state;
@@ -770,13 +753,119 @@ void maybe_gate(hipStream_t stream) {
   void* args[] = {&state, &hs, &submit_dev, &slot_arg, &rate_ppm, &cap, &hold};
   real_hipModuleLaunchKernel()(G.gate_fn, 1, 1, 1, 64, 1, 1, 0, stream, args, nullptr);
   S.last_gate_host_ns = now;
-  S.first_submit_host_ns = now;  // the user launch that follows starts the next batch
   if (g_slot >= 0 && hs) {
     const uint64_t* h = static_cast<const uint64_t*>(hs);
     mivgpu_util_t* u = &g_region->procs[g_slot].util[dev];
     __atomic_store_n(&u->busy_ns, h[0], __ATOMIC_RELAXED);
     __atomic_store_n(&u->throttled_ns, h[1], __ATOMIC_RELAXED);
     __atomic_store_n(&u->gates, h[2], __ATOMIC_RELAXED);
+  }
+}
+
+bool stream_capturing(hipStream_t stream) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return real_hipStreamIsCapturing() && real_hipStreamIsCapturing()(stream, &cs) == hipSuccess &&
+         cs != hipStreamCaptureStatusNone;
+}
+
+int find_slot_locked(DeviceGate& G, hipStream_t stream, bool create, uint64_t now) {
+  int free_slot = -1;
+  for (int i = 0; i < 64; ++i) {
+    if (G.slots[i].used && G.slots[i].stream == stream) return i;
+    if (!G.slots[i].used && free_slot < 0) free_slot = i;
+  }
+  if (!create) return -1;
+  int slot = free_slot >= 0 ? free_slot : (int)(reinterpret_cast<uintptr_t>(stream) % 64);
+  G.slots[slot] = GateSlot{stream, 0, 0, true, 0};
+  (void)now;
+  return slot;
+}
+
+// Background stamper: once the host has not launched on a stream for
+// kStampIdleNs, close that stream's pending batch with a gate, so a host-side
+// pause (CPU work, library initialisation, data loading) is never charged to
+// the tenant as GPU-busy time.  Runs under G.mu, which hipStreamBeginCapture
+// also takes, so a stamp can never be captured into a user graph.
+constexpr uint64_t kStampIdleNs = 1000000;  // 1 ms
+void enqueue_gate_locked(int dev, DeviceGate& G, int slot, hipStream_t stream, uint64_t now);
+bool stream_capturing(hipStream_t stream);
+
+void* stamper_main(void* arg) {
+  const int dev = (int)(intptr_t)arg;
+  DeviceGate& G = g_gates[dev];
+  {
+    Guard g;  // our own HIP calls must never re-enter the hooks' accounting
+    if (real_hipSetDevice()) real_hipSetDevice()(dev);
+  }
+  for (;;) {
+    usleep(500);
+    Guard g;
+    std::lock_guard<std::mutex> lk(G.mu);
+    const uint64_t now = mono_ns();
+    for (int i = 0; i < 64; ++i) {
+      GateSlot& S = G.slots[i];
+      if (!S.used || S.first_submit_host_ns == 0) continue;
+      if (now - S.last_launch_host_ns < kStampIdleNs) continue;
+      if (stream_capturing(S.stream)) continue;
+      enqueue_gate_locked(dev, G, i, S.stream, now);
+      S.first_submit_host_ns = 0;
+    }
+  }
+  return nullptr;
+}
+
+void start_stamper_locked(int dev, DeviceGate& G) {
+  G.stamper_started = true;
+  pthread_t th;
+  pthread_attr_t a;
+  pthread_attr_init(&a);
+  pthread_attr_setdetachstate(&a, PTHREAD_CREATE_DETACHED);
+  if (pthread_create(&th, &a, stamper_main, (void*)(intptr_t)dev) != 0)
+    mlog(1, "device %d: governor stamper thread failed to start", dev);
+  pthread_attr_destroy(&a);
+}
+
+void maybe_gate(hipStream_t stream) {
+  int dev = current_device();
+  if (!gate_wanted(dev)) return;
+  // Never inject into a stream that is being captured: the gate would be baked
+  // into the graph with stale arguments.  Graph replays are gated at launch.
+  if (stream_capturing(stream)) return;
+  DeviceGate& G = g_gates[dev];
+  std::lock_guard<std::mutex> lk(G.mu);
+  if (!G.tried) G.ok = gate_init_locked(dev, G);
+  if (!G.ok) return;
+  uint64_t now = mono_ns();
+  int slot = find_slot_locked(G, stream, true, now);
+  GateSlot& S = G.slots[slot];
+  S.last_launch_host_ns = now;
+  if (!G.stamper_started) start_stamper_locked(dev, G);
+  const bool pending = S.first_submit_host_ns != 0;
+  if (!pending || S.last_gate_host_ns == 0 || now - S.last_gate_host_ns >= g_cfg.gate_min_interval_ns) {
+    // Gate in front of this launch: settles the batch submitted since the
+    // previous gate (if any); this launch starts the next batch.
+    enqueue_gate_locked(dev, G, slot, stream, now);
+    S.first_submit_host_ns = now;
+    return;
+  }
+}
+
+// The host is about to wait for the GPU, after which the stream idles: stamp
+// the pending batch so that the idle gap is never charged as busy time.
+void stamp_before_sync(hipStream_t stream, bool all_streams) {
+  if (g_cfg.disabled || !g_region) return;
+  int dev = current_device();
+  DeviceGate& G = g_gates[dev];
+  if (!G.ok) return;
+  std::lock_guard<std::mutex> lk(G.mu);
+  uint64_t now = mono_ns();
+  for (int i = 0; i < 64; ++i) {
+    GateSlot& S = G.slots[i];
+    if (!S.used || S.first_submit_host_ns == 0) continue;
+    if (!all_streams && S.stream != stream) continue;
+    if (stream_capturing(S.stream)) continue;
+    enqueue_gate_locked(dev, G, i, S.stream, now);
+    S.first_submit_host_ns = 0;  // nothing pending until the next launch
   }
 }
 
@@ -1050,6 +1139,41 @@ MIVGPU_EXPORT hipError_t hipGraphLaunch_spt(hipGraphExec_t exec, hipStream_t str
   return real_hipGraphLaunch_spt()(exec, stream);
 }
 
+// Serialise capture begin with the background stamper (see stamper_main).
+MIVGPU_EXPORT hipError_t hipStreamBeginCapture(hipStream_t stream, hipStreamCaptureMode mode) {
+  ensure_init();
+  Guard g;
+  DeviceGate& G = g_gates[current_device()];
+  std::lock_guard<std::mutex> lk(G.mu);
+  return real_hipStreamBeginCapture()(stream, mode);
+}
+
+MIVGPU_EXPORT hipError_t hipStreamBeginCapture_spt(hipStream_t stream, hipStreamCaptureMode mode) {
+  ensure_init();
+  Guard g;
+  DeviceGate& G = g_gates[current_device()];
+  std::lock_guard<std::mutex> lk(G.mu);
+  return real_hipStreamBeginCapture_spt()(stream, mode);
+}
+
+MIVGPU_EXPORT hipError_t hipStreamSynchronize(hipStream_t stream) {
+  Guard g;
+  if (g.outer && g_ready.load(std::memory_order_acquire)) stamp_before_sync(stream, false);
+  return real_hipStreamSynchronize()(stream);
+}
+
+MIVGPU_EXPORT hipError_t hipStreamSynchronize_spt(hipStream_t stream) {
+  Guard g;
+  if (g.outer && g_ready.load(std::memory_order_acquire)) stamp_before_sync(stream, false);
+  return real_hipStreamSynchronize_spt()(stream);
+}
+
+MIVGPU_EXPORT hipError_t hipDeviceSynchronize(void) {
+  Guard g;
+  if (g.outer && g_ready.load(std::memory_order_acquire)) stamp_before_sync(nullptr, true);
+  return real_hipDeviceSynchronize()();
+}
+
 // ======================================================================
 // Introspection ABI (MIVGPU_1.0) used by tests and the Python layer.
 // ======================================================================
@@ -1107,6 +1231,24 @@ MIVGPU_EXPORT int mivgpu_gate_stats(int dev, unsigned long long* busy, unsigned 
   if (held) *held = h[1];
   if (gates) *gates = h[2];
   return 0;
+}
+
+// Copy up to `n` most recent gate trace entries (8 x int64 each) into `out`;
+// returns the number copied.
+MIVGPU_EXPORT int mivgpu_gate_trace(int dev, long long* out, int n) {
+  if (dev < 0 || dev >= MIVGPU_MAX_DEVICES || !out || n <= 0) return 0;
+  DeviceGate& G = g_gates[dev];
+  if (!G.ok || !G.host_stats) return 0;
+  const volatile long long* h = static_cast<const volatile long long*>(G.host_stats);
+  const unsigned long long gates = static_cast<const volatile unsigned long long*>(G.host_stats)[2];
+  int cnt = (int)(gates < 128 ? gates : 128);
+  if (cnt > n) cnt = n;
+  for (int i = 0; i < cnt; ++i) {
+    unsigned long long g = gates - cnt + i;
+    const volatile long long* e = h + 8 + (g % 128) * 8;
+    for (int k = 0; k < 8; ++k) out[i * 8 + k] = e[k];
+  }
+  return cnt;
 }
 
 MIVGPU_EXPORT int mivgpu_active(void) {

@@ -1,0 +1,478 @@
+"""MI355X (AMD Instinct) device backend.
+
+Capability target = the union of the reference's AMD backend
+(pkg/device/amd/device.go:42-372: amd.com/gpu|gpumem|gpucores, % -> CU count,
+product type kept in the allocation) and the richer NVIDIA template
+(pkg/device/nvidia/device.go:40-978: handshake health, memory percentage,
+defaults, exclusive-core defaulting, priority / core-policy env, runtime class,
+cordon, NUMA binding, mutex, quota, full-core guard, topology-aware
+combination search), re-designed for MI355X:
+
+  * ``gpucores`` % -> CU count (``floor(pct * devcore / 100)``, clamped to
+    [1, devcore]) AND a concrete, non-overlapping, XCD-aligned CU set chosen
+    from a per-GPU CU bitmap (:mod:`.cu_alloc`), written to
+    ``hami.io/amd-cu-ranges`` and turned into ``HSA_CU_MASK`` by the device
+    plugin -- spatial isolation in hardware;
+  * ``gpucores`` omitted -> no CU reservation (time-shared, governor-gated)
+    unless the container asks for a whole card, which defaults to 100 %;
+  * multi-GPU pods are placed by xGMI pair scores (``hami.io/node-amd-score``)
+    and the node score favours better-connected GPU sets (policy-neutral).
+"""
+
+from __future__ import annotations
+
+import logging
+import math
+import threading
+from dataclasses import dataclass, field
+
+from k8s_vgpu_scheduler_amd.device import codec
+from k8s_vgpu_scheduler_amd.device import common as R
+from k8s_vgpu_scheduler_amd.device import devices as D
+from k8s_vgpu_scheduler_amd.device.init_container import collapse_init_container_usage
+from k8s_vgpu_scheduler_amd.device.quota import get_local_cache
+from k8s_vgpu_scheduler_amd.device.types import (ContainerDevice, ContainerDeviceRequest, DeviceInfo,
+                                                 DeviceUsage, NodeInfo, ResourceNames)
+from k8s_vgpu_scheduler_amd.k8s import quantity
+from k8s_vgpu_scheduler_amd.k8s.client import containers
+from k8s_vgpu_scheduler_amd.utils import nodelock, util
+from k8s_vgpu_scheduler_amd.utils import types as T
+
+from . import cu_alloc, topology
+
+log = logging.getLogger(__name__)
+
+AMD_DEVICE = "AMD"
+AMD_COMMON_WORD = "AMD"
+REGISTER_ANNOS = "hami.io/node-amd-register"
+PAIR_SCORE_ANNOS = "hami.io/node-amd-score"
+HANDSHAKE_ANNOS = "hami.io/node-handshake-amd"
+IN_REQUEST_ANNOS = "hami.io/amd-devices-to-allocate"
+SUPPORT_ANNOS = "hami.io/amd-devices-allocated"
+CU_RANGES_ANNOS = "hami.io/amd-cu-ranges"
+AMD_IN_USE = "amd.com/use-gputype"
+AMD_NO_USE = "amd.com/nouse-gputype"
+AMD_USE_UUID = "amd.com/use-gpu-uuid"
+AMD_NO_USE_UUID = "amd.com/nouse-gpu-uuid"
+AMD_NUMA_BIND = "amd.com/numa-bind"
+NODE_LOCK_AMD = T.NODE_LOCK_KEY
+
+CORE_POLICIES = ("default", "force", "disable")
+
+
+@dataclass
+class AMDConfig:
+    resource_count_name: str = "amd.com/gpu"
+    resource_memory_name: str = "amd.com/gpumem"
+    resource_core_name: str = "amd.com/gpucores"
+    resource_memory_percentage_name: str = "amd.com/gpumem-percentage"
+    resource_priority_name: str = "amd.com/priority"
+    default_memory: int = 0          # MiB; 0 -> whole card when nothing is asked
+    default_cores: int = 0           # %;   0 -> no CU reservation (time-shared)
+    default_gpu_num: int = 1
+    memory_factor: int = 1
+    gpu_core_policy: str = "default"
+    runtime_class_name: str = ""
+    overwrite_env: bool = False
+    # MI355X CU topology used by the CU-range allocator
+    xcds_per_device: int = 8
+    cu_layout: str = "interleaved"
+    # Node-side (device plugin) knobs, shared through the same config
+    device_split_count: int = 8
+    device_memory_scaling: float = 1.0
+    device_core_scaling: float = 1.0
+    extra: dict = field(default_factory=dict)
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "AMDConfig":
+        m = {"resourceCountName": "resource_count_name", "resourceMemoryName": "resource_memory_name",
+             "resourceCoreName": "resource_core_name",
+             "resourceMemoryPercentageName": "resource_memory_percentage_name",
+             "resourcePriorityName": "resource_priority_name", "defaultMemory": "default_memory",
+             "defaultCores": "default_cores", "defaultGPUNum": "default_gpu_num",
+             "memoryFactor": "memory_factor", "gpuCorePolicy": "gpu_core_policy",
+             "runtimeClassName": "runtime_class_name", "overwriteEnv": "overwrite_env",
+             "xcdsPerDevice": "xcds_per_device", "cuLayout": "cu_layout",
+             "deviceSplitCount": "device_split_count", "deviceMemoryScaling": "device_memory_scaling",
+             "deviceCoreScaling": "device_core_scaling"}
+        kw = {}
+        for k, v in (d or {}).items():
+            if k in m:
+                kw[m[k]] = v
+        cfg = cls(**kw)
+        if cfg.gpu_core_policy not in CORE_POLICIES:
+            raise ValueError(f"invalid gpuCorePolicy {cfg.gpu_core_policy!r}")
+        return cfg
+
+
+def _rv(ctr: dict, name: str):
+    return D.resource_value(ctr, name)
+
+
+def _present(ctr: dict, name: str) -> bool:
+    return bool(name) and _rv(ctr, name) is not None
+
+
+def _set_limit(ctr: dict, name: str, value: int):
+    res = ctr.setdefault("resources", {})
+    res.setdefault("limits", {})[name] = str(value)
+
+
+def _env_set(ctr: dict, name: str, value: str):
+    env = ctr.setdefault("env", [])
+    for e in env:
+        if e.get("name") == name:
+            e["value"] = value
+            return
+    env.append({"name": name, "value": value})
+
+
+def cordoned_devices(node_info: NodeInfo | None) -> set[str]:
+    if node_info is None or not node_info.node:
+        return set()
+    raw = ((node_info.node.get("metadata") or {}).get("annotations") or {}).get(T.DEVICE_CORDON_ANNOTATION, "")
+    return {u.strip() for u in raw.split(",") if u.strip()}
+
+
+def cu_count_for(pct: int, total: int) -> int:
+    """gpucores % -> CU count (docs/develop/amd-vgpu.md:136-142)."""
+    if pct <= 0 or total <= 0:
+        return 0
+    return min(total, max(1, (total * pct) // 100))
+
+
+class AMDDevices(D.Devices):
+    policy_neutral_score = True
+
+    def __init__(self, cfg: AMDConfig | None = None):
+        self.cfg = cfg or AMDConfig()
+        self.topo_cache: dict[str, int] = {}    # uuid -> devcore (quota % conversion)
+        self.reported: dict[str, int] = {}      # node -> last allocatable count
+        self.reported_annos: dict[str, str] = {}
+        self._mu = threading.Lock()
+        D.IN_REQUEST_DEVICES.setdefault(AMD_DEVICE, IN_REQUEST_ANNOS)
+        D.SUPPORT_DEVICES.setdefault(AMD_DEVICE, SUPPORT_ANNOS)
+        util.HANDSHAKE_ANNOS.setdefault(AMD_DEVICE, HANDSHAKE_ANNOS)
+
+    def cu_topology(self, total: int) -> cu_alloc.CUTopology:
+        xcds = self.cfg.xcds_per_device if total % max(1, self.cfg.xcds_per_device) == 0 else 1
+        return cu_alloc.CUTopology(total=total, xcds=xcds, layout=self.cfg.cu_layout)
+
+    # ------------------------------------------------------------ identity
+    def common_word(self) -> str:
+        return AMD_COMMON_WORD
+
+    def get_resource_names(self) -> ResourceNames:
+        return ResourceNames(self.cfg.resource_count_name, self.cfg.resource_memory_name,
+                             self.cfg.resource_core_name, self.cfg.memory_factor)
+
+    # ----------------------------------------------------------- admission
+    def mutate_admission(self, ctr: dict, pod: dict) -> bool:
+        c = self.cfg
+        if _present(ctr, c.resource_core_name):
+            v, ok = quantity.as_int64(_rv(ctr, c.resource_core_name))
+            if not ok or v < 0 or v > 100:
+                raise D.AdmissionError(f"{c.resource_core_name} must be an integer percentage between 0 and 100")
+        if _present(ctr, c.resource_memory_percentage_name):
+            v, ok = quantity.as_int64(_rv(ctr, c.resource_memory_percentage_name))
+            if not ok or v < 0 or v > 100:
+                raise D.AdmissionError(
+                    f"invalid {c.resource_memory_percentage_name} value in container {ctr.get('name')}: "
+                    "must be an integer between 0 and 100")
+        if _present(ctr, c.resource_memory_name):
+            v, ok = quantity.as_int64(_rv(ctr, c.resource_memory_name))
+            if not ok or v < 0:
+                raise D.AdmissionError(f"{c.resource_memory_name} must be a non-negative integer (MiB)")
+        if _present(ctr, c.resource_priority_name):
+            _env_set(ctr, T.TASK_PRIORITY_ENV, str(quantity.value(_rv(ctr, c.resource_priority_name))))
+        if c.gpu_core_policy and c.gpu_core_policy != "default":
+            _env_set(ctr, T.CORE_LIMIT_SWITCH_ENV, c.gpu_core_policy)
+
+        has = _present(ctr, c.resource_count_name)
+        if not has and (_present(ctr, c.resource_core_name) or _present(ctr, c.resource_memory_name)
+                        or _present(ctr, c.resource_memory_percentage_name)):
+            if c.default_gpu_num > 0:
+                _set_limit(ctr, c.resource_count_name, c.default_gpu_num)
+                has = True
+        if has and not _present(ctr, c.resource_core_name):
+            # whole-card requests own all CUs (nvidia/device.go:414-450 defaultExclusiveCoreIfNeeded)
+            pct = _rv(ctr, c.resource_memory_percentage_name)
+            if pct is not None:
+                exclusive = quantity.as_int64(pct)[0] == 100
+            else:
+                exclusive = not _present(ctr, c.resource_memory_name)
+            if exclusive:
+                _set_limit(ctr, c.resource_core_name, 100)
+        if has and c.runtime_class_name and not (pod.get("spec") or {}).get("runtimeClassName"):
+            pod.setdefault("spec", {})["runtimeClassName"] = c.runtime_class_name
+        if not has and c.overwrite_env:
+            _env_set(ctr, "ROCR_VISIBLE_DEVICES", "")
+        return has
+
+    # ------------------------------------------------------------ requests
+    def generate_resource_requests(self, ctr: dict) -> ContainerDeviceRequest:
+        c = self.cfg
+        v = _rv(ctr, c.resource_count_name)
+        if v is None:
+            return ContainerDeviceRequest()
+        n, ok = quantity.as_int64(v)
+        if not ok or n <= 0 or n >= 2 ** 31:
+            return ContainerDeviceRequest()
+        mem = 0
+        mv = _rv(ctr, c.resource_memory_name)
+        if mv is not None:
+            m, ok = quantity.as_int64(mv)
+            factor = max(c.memory_factor, 1)
+            if not ok or m < 0 or m > (2 ** 31 - 1) // factor:
+                log.error("amd memory request %r rejected (container %s)", mv, ctr.get("name"))
+                return ContainerDeviceRequest()
+            mem = m * factor
+        mem_pct = 101
+        pv = _rv(ctr, c.resource_memory_percentage_name)
+        if pv is not None:
+            p, ok = quantity.as_int64(pv)
+            if ok:
+                p = min(p, 100)
+                mem_pct = p if p > 0 else 101
+        if mem_pct == 101 and mem == 0:
+            if c.default_memory:
+                mem = c.default_memory
+            else:
+                mem_pct = 100
+        cores = c.default_cores
+        cv = _rv(ctr, c.resource_core_name)
+        if cv is not None:
+            cc, ok = quantity.as_int64(cv)
+            if not ok or cc < 0 or cc > 100:
+                log.error("amd core request %r rejected (container %s)", cv, ctr.get("name"))
+                return ContainerDeviceRequest()
+            cores = cc
+        return ContainerDeviceRequest(nums=n, type=AMD_DEVICE, memreq=mem, mem_percentage_req=mem_pct,
+                                      coresreq=cores)
+
+    # ------------------------------------------------------- node devices
+    def get_node_devices(self, node: dict) -> list[DeviceInfo]:
+        annos = (node.get("metadata") or {}).get("annotations") or {}
+        enc = annos.get(REGISTER_ANNOS)
+        if enc is None:
+            raise LookupError(f"annos not found {REGISTER_ANNOS}")
+        devs = codec.unmarshal_node_devices(enc)
+        if not devs:
+            raise LookupError("no gpu found on node")
+        scores = {}
+        if PAIR_SCORE_ANNOS in annos:
+            scores = codec.decode_pair_scores(annos[PAIR_SCORE_ANNOS])
+        for d in devs:
+            d.devicevendor = AMD_COMMON_WORD
+            d.pair_scores = dict(scores.get(d.id, {}))
+            with self._mu:
+                self.topo_cache[d.id] = d.devcore
+        return devs
+
+    def check_health(self, dev_type: str, node: dict) -> tuple[bool, bool]:
+        """Handshake health + allocatable/registration change tracking (nvidia/device.go:234-272)."""
+        name = node["metadata"]["name"]
+        alloc = ((node.get("status") or {}).get("allocatable") or {}).get(self.cfg.resource_count_name)
+        current = quantity.value(alloc) if alloc is not None else 0
+        reg = ((node.get("metadata") or {}).get("annotations") or {}).get(REGISTER_ANNOS, "")
+        with self._mu:
+            reported = self.reported.get(name, 0)
+            h_ok, h_changed = D.check_health_handshake(dev_type, self.cfg.resource_count_name, node)
+            prev_reg = self.reported_annos.get(name)
+            if current == 0:
+                if reported == 0:
+                    if prev_reg != reg:
+                        self.reported_annos[name] = reg
+                        return h_ok, True
+                    return h_ok, h_changed
+                self.reported[name] = 0
+                self.reported_annos[name] = reg
+                return False, h_changed
+            if reported != current:
+                self.reported[name] = current
+                self.reported_annos[name] = reg
+                return True, True
+            if prev_reg != reg:
+                self.reported_annos[name] = reg
+                return h_ok, True
+            return h_ok, h_changed
+
+    def node_deleted(self, node_name: str) -> None:
+        with self._mu:
+            self.reported.pop(node_name, None)
+            self.reported_annos.pop(node_name, None)
+
+    def node_cleanup(self, node_name: str) -> None:
+        self.node_deleted(node_name)
+        util.remove_node_annotation(node_name, REGISTER_ANNOS, HANDSHAKE_ANNOS, PAIR_SCORE_ANNOS)
+
+    # ---------------------------------------------------------------- locks
+    def _requests_amd(self, pod: dict) -> bool:
+        return any(self.generate_resource_requests(c).nums > 0 for c in containers(pod))
+
+    def lock_node(self, node: dict, pod: dict) -> None:
+        if self._requests_amd(pod):
+            nodelock.lock_node(node["metadata"]["name"], NODE_LOCK_AMD, pod)
+
+    def release_node_lock(self, node: dict, pod: dict) -> None:
+        if self._requests_amd(pod):
+            nodelock.release_node_lock(node["metadata"]["name"], NODE_LOCK_AMD, pod)
+
+    # ---------------------------------------------------------- annotations
+    def patch_annotations(self, pod: dict, annos: dict, pd: dict) -> dict:
+        devlist = pd.get(AMD_DEVICE)
+        if devlist:
+            s = codec.encode_pod_single_device(devlist)
+            annos[IN_REQUEST_ANNOS] = s
+            annos[SUPPORT_ANNOS] = s
+            if any((d.custominfo or {}).get("cu_ranges") for ctr in devlist for d in ctr):
+                annos[CU_RANGES_ANNOS] = codec.encode_cu_ranges(devlist)
+        return annos
+
+    def decode_pod_devices(self, pod: dict, key: str = SUPPORT_ANNOS) -> list:
+        annos = (pod.get("metadata") or {}).get("annotations") or {}
+        pd = codec.decode_pod_devices({AMD_DEVICE: key}, annos).get(AMD_DEVICE)
+        if pd is None:
+            return []
+        return codec.attach_cu_ranges(pd, annos.get(CU_RANGES_ANNOS))
+
+    # -------------------------------------------------------------- scoring
+    def score_node(self, node: dict, pod_single: list, previous: list, policy: str) -> float:
+        """Policy-neutral xGMI connectivity of the chosen GPU sets, 0..1 (higher better)."""
+        if not pod_single:
+            return 0.0
+        prev_by_id = {d.id: d for d in previous or []}
+        scores = {}
+        for d in prev_by_id.values():
+            ps = (d.custominfo or {}).get("pair_scores")
+            if ps:
+                scores[d.id] = ps
+        vals = []
+        for ctr in pod_single:
+            ids = [c.uuid for c in ctr]
+            if len(ids) >= 2 and scores:
+                vals.append(min(1.0, topology.mean_pair_score(ids, scores) / 100.0))
+        return sum(vals) / len(vals) if vals else 0.0
+
+    def add_resource_usage(self, pod: dict, dev: DeviceUsage, ctr: ContainerDevice) -> None:
+        dev.used += 1
+        dev.usedcores += ctr.usedcores
+        dev.usedmem += ctr.usedmem
+        ranges = (ctr.custominfo or {}).get("cu_ranges")
+        if ranges:
+            dev.custominfo["cu_used"] = dev.custominfo.get("cu_used", 0) | cu_alloc.bitmap_from_ranges(ranges)
+
+    def quota_cores(self, d: ContainerDevice) -> int:
+        """CU count -> % for ResourceQuota accounting (limits are written in %)."""
+        total = self.topo_cache.get(d.uuid, 256) or 256
+        return int(math.ceil(d.usedcores * 100 / total))
+
+    def _fit_quota(self, pod, tmp: list, allocated: dict, uuid: str, memreq: int, cu: int, total: int) -> bool:
+        hypo = {t: [list(c) for c in single] for t, single in (allocated or {}).items()}
+        cur = list(tmp) + [ContainerDevice(uuid=uuid, type=AMD_DEVICE, usedmem=memreq, usedcores=cu)]
+        hypo.setdefault(AMD_DEVICE, []).append(cur)
+        mem = core = 0
+        for ctr in (collapse_init_container_usage(pod, hypo) or {}).get(AMD_DEVICE, []):
+            for v in ctr:
+                mem += v.usedmem
+                core += int(math.ceil(v.usedcores * 100 / (self.topo_cache.get(v.uuid, total) or total)))
+        return get_local_cache().fit_quota(pod["metadata"].get("namespace", "default"), mem,
+                                           self.cfg.memory_factor, core, AMD_DEVICE)
+
+    # ------------------------------------------------------------------ fit
+    def fit(self, devices: list[DeviceUsage], request: ContainerDeviceRequest, pod: dict,
+            node_info: NodeInfo | None, allocated: dict) -> tuple[bool, dict, str]:
+        k = ContainerDeviceRequest(request.nums, request.type, request.memreq, request.mem_percentage_req,
+                                   min(request.coresreq, 100))
+        orig = k.nums
+        reasons: dict[str, int] = {}
+        annos = (pod.get("metadata") or {}).get("annotations") or {}
+        policy = util.get_gpu_scheduler_policy_by_pod(D.gpu_scheduler_policy(), pod)
+        need_topo = util.policy_contains(policy, T.GPU_POLICY_TOPOLOGY)
+        is_mutex = util.policy_contains(policy, T.GPU_POLICY_MUTEX)
+        numa_bind = str(annos.get(AMD_NUMA_BIND, "")).lower() in ("1", "t", "true")
+        cordoned = cordoned_devices(node_info)
+        tmp: list[ContainerDevice] = []
+        prevnuma = -1
+
+        def bump(r, n=1):
+            reasons[r] = reasons.get(r, 0) + n
+
+        for dev in reversed(devices):
+            if not dev.health:
+                bump(R.CARD_NOT_HEALTH)
+                continue
+            if dev.id in cordoned:
+                bump(R.CARD_CORDONED)
+                continue
+            if k.type.upper() != AMD_DEVICE or not D.check_type(annos, dev.type, AMD_IN_USE, AMD_NO_USE):
+                bump(R.CARD_TYPE_MISMATCH)
+                continue
+            if numa_bind and prevnuma != dev.numa:
+                if k.nums != orig:
+                    bump(R.NUMA_NOT_FIT, len(tmp))
+                k.nums = orig
+                prevnuma = dev.numa
+                tmp = []
+            if not D.check_uuid(annos, dev.id, AMD_USE_UUID, AMD_NO_USE_UUID):
+                bump(R.CARD_UUID_MISMATCH)
+                continue
+            if dev.count <= dev.used:
+                bump(R.CARD_TIME_SLICING_EXHAUSTED)
+                continue
+            if is_mutex and dev.used > 0:
+                bump(R.EXCLUSIVE_DEVICE_ALLOCATE_CONFLICT)
+                continue
+            memreq = k.memreq if k.memreq > 0 else 0
+            if k.mem_percentage_req != 101 and k.memreq == 0:
+                memreq = dev.totalmem * k.mem_percentage_req // 100
+            cu = cu_count_for(k.coresreq, dev.totalcore)
+            if not self._fit_quota(pod, tmp, allocated, dev.id, memreq, cu, dev.totalcore or 256):
+                bump(R.RESOURCE_QUOTA_NOT_FIT)
+                continue
+            if dev.totalmem - dev.usedmem < memreq:
+                bump(R.CARD_INSUFFICIENT_MEMORY)
+                continue
+            if dev.totalcore - dev.usedcores < cu:
+                bump(R.CARD_INSUFFICIENT_CORE)
+                continue
+            if k.coresreq == 100 and dev.used > 0:
+                bump(R.EXCLUSIVE_DEVICE_ALLOCATE_CONFLICT)
+                continue
+            if dev.totalcore and dev.usedcores >= dev.totalcore and cu == 0:
+                bump(R.CARD_COMPUTE_UNITS_EXHAUSTED)
+                continue
+            info = {}
+            if 0 < cu < dev.totalcore:
+                ranges = cu_alloc.pick(dev.custominfo.get("cu_used", 0), cu, self.cu_topology(dev.totalcore))
+                if ranges is None:
+                    bump(R.CARD_CU_FRAGMENTED)
+                    continue
+                info["cu_ranges"] = ranges
+            if k.nums > 0:
+                if not need_topo:
+                    k.nums -= 1
+                tmp.append(ContainerDevice(idx=dev.index, uuid=dev.id, type=dev.type, usedmem=memreq,
+                                           usedcores=cu, custominfo=info))
+            if k.nums == 0 and not need_topo:
+                return True, {k.type: tmp}, ""
+        if need_topo:
+            scores = {}
+            if node_info is not None:
+                for di in node_info.devices.get(AMD_COMMON_WORD, []):
+                    scores[di.id] = di.pair_scores
+            if len(tmp) == orig:
+                return True, {k.type: tmp}, ""
+            if len(tmp) > orig:
+                chosen = topology.worst_single(tmp, scores) if orig == 1 else \
+                    topology.best_combination(tmp, orig, scores)
+                return True, {k.type: chosen}, ""
+        if tmp:
+            reasons[R.ALLOCATED_CARDS_INSUFFICIENT_REQUEST] = len(tmp)
+        return False, {k.type: tmp}, R.gen_reason(reasons, len(devices))
+
+
+def init_amd_device(cfg: AMDConfig | dict | None = None) -> AMDDevices:
+    if isinstance(cfg, dict):
+        cfg = AMDConfig.from_dict(cfg)
+    return AMDDevices(cfg)

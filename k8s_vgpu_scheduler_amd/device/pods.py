@@ -1,0 +1,112 @@
+"""PodManager: UID -> scheduled pod + effective device usage (pkg/device/pods.go:29-290).
+
+Every read returns deep copies (the stored entries are rewritten in place by
+informer callbacks).  ``init_released`` marks pods whose usage already shrank
+to app-containers-only so an informer resync cannot re-inflate it.
+"""
+
+from __future__ import annotations
+
+import copy
+import logging
+import threading
+from dataclasses import dataclass, field
+
+from .types import copy_pod_devices
+
+log = logging.getLogger(__name__)
+
+
+@dataclass
+class PodInfo:
+    pod: dict
+    node_id: str
+    devices: dict = field(default_factory=dict)
+    init_released: bool = False
+
+    @property
+    def name(self):
+        return self.pod["metadata"]["name"]
+
+    @property
+    def namespace(self):
+        return self.pod["metadata"].get("namespace", "default")
+
+    @property
+    def uid(self):
+        return self.pod["metadata"].get("uid", "")
+
+    @property
+    def annotations(self):
+        return self.pod["metadata"].get("annotations") or {}
+
+    def deepcopy(self) -> "PodInfo":
+        return PodInfo(copy.deepcopy(self.pod), self.node_id, copy_pod_devices(self.devices),
+                       self.init_released)
+
+
+def _uid(pod: dict) -> str:
+    md = pod.get("metadata") or {}
+    return md.get("uid") or f"{md.get('namespace', 'default')}/{md.get('name')}"
+
+
+class PodManager:
+    def __init__(self):
+        self._pods: dict[str, PodInfo] = {}
+        self._mu = threading.RLock()
+
+    def add_pod(self, pod: dict, node_id: str, devices: dict) -> bool:
+        """Store collapsed usage; returns True if newly added."""
+        with self._mu:
+            k = _uid(pod)
+            pi = self._pods.get(k)
+            if pi is None:
+                self._pods[k] = PodInfo(copy.deepcopy(pod), node_id, copy_pod_devices(devices))
+                log.info("pod added %s/%s node=%s", pod["metadata"].get("namespace"), pod["metadata"]["name"], node_id)
+                return True
+            pi.pod = copy.deepcopy(pod)
+            pi.node_id = node_id
+            if not pi.init_released:
+                pi.devices = copy_pod_devices(devices)
+            return False
+
+    def update_pod(self, pod: dict):
+        with self._mu:
+            pi = self._pods.get(_uid(pod))
+            if pi:
+                pi.pod = copy.deepcopy(pod)
+
+    def del_pod(self, pod: dict):
+        with self._mu:
+            self._pods.pop(_uid(pod), None)
+
+    def get_pod(self, pod: dict) -> PodInfo | None:
+        with self._mu:
+            pi = self._pods.get(_uid(pod))
+            return pi.deepcopy() if pi else None
+
+    def take_and_delete_pod(self, pod: dict) -> PodInfo | None:
+        with self._mu:
+            return self._pods.pop(_uid(pod), None)
+
+    def update_pod_device(self, pod: dict, new_devices: dict):
+        with self._mu:
+            pi = self._pods.get(_uid(pod))
+            if pi is None:
+                return None, False
+            old = pi.devices
+            pi.devices = copy_pod_devices(new_devices)
+            pi.init_released = True
+            return old, True
+
+    def list_pods_info(self) -> list[PodInfo]:
+        with self._mu:
+            return [p.deepcopy() for p in self._pods.values()]
+
+    def get_scheduled_pods(self) -> dict[str, PodInfo]:
+        with self._mu:
+            return {k: p.deepcopy() for k, p in self._pods.items()}
+
+    def __len__(self):
+        with self._mu:
+            return len(self._pods)

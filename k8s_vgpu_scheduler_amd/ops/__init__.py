@@ -40,8 +40,10 @@ def lib():
         L.mivgpu_qk_norm_rope_kv.argtypes = [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, f, f, vp]
         L.mivgpu_decode_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, f, vp]
         L.mivgpu_silu_mul.argtypes = [vp, vp, i, i, vp]
+        L.mivgpu_hwid_probe.argtypes = [vp, i, vp]
         for fn in ("mivgpu_rmsnorm", "mivgpu_add_rmsnorm", "mivgpu_qk_norm_rope_kv",
-                   "mivgpu_decode_attention", "mivgpu_silu_mul", "mivgpu_ops_attn_split"):
+                   "mivgpu_decode_attention", "mivgpu_silu_mul", "mivgpu_ops_attn_split",
+                   "mivgpu_hwid_probe"):
             getattr(L, fn).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -121,3 +123,11 @@ def silu_mul(gate_up: torch.Tensor, out: torch.Tensor | None = None):
     out = torch.empty(rows, inter, dtype=gate_up.dtype, device=gate_up.device) if out is None else out
     _check(lib().mivgpu_silu_mul(_p(gate_up), _p(out), rows, inter, _stream()), "silu_mul")
     return out
+
+
+def hwid_probe(blocks: int = 4096) -> torch.Tensor:
+    """[blocks, 2] uint32 (HW_REG_HW_ID, HW_REG_XCC_ID) per workgroup."""
+    out = torch.zeros(blocks * 2, dtype=torch.int32, device="cuda")
+    _check(lib().mivgpu_hwid_probe(_p(out), blocks, _stream()), "hwid_probe")
+    torch.cuda.synchronize()
+    return out.view(blocks, 2).cpu()

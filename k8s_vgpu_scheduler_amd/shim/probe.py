@@ -67,7 +67,15 @@ def gate_stats() -> dict:
     b, h, g = ctypes.c_ulonglong(), ctypes.c_ulonglong(), ctypes.c_ulonglong()
     if fn(0, ctypes.byref(b), ctypes.byref(h), ctypes.byref(g)) != 0:
         return {"gate": "inactive"}
-    return {"gate_busy_ms": b.value / 1e6, "gate_held_ms": h.value / 1e6, "gates": g.value}
+    out = {"gate_busy_ms": b.value / 1e6, "gate_held_ms": h.value / 1e6, "gates": g.value}
+    try:
+        tr = ctypes.CDLL(None).mivgpu_gate_trace
+        buf = (ctypes.c_longlong * (128 * 8))()
+        n = tr(0, buf, 128)
+        out["trace"] = [[buf[i * 8 + k] for k in range(7)] for i in range(n)]
+    except AttributeError:
+        pass
+    return out
 
 
 def child_stream(args) -> dict:
@@ -86,6 +94,18 @@ def child_stream(args) -> dict:
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     return {"mode": "stream", "gbps": 2 * x.numel() * 4 * args.iters / dt / 1e9, "seconds": dt}
+
+
+def child_hwid(args) -> dict:
+    """Which XCD / SE / CU ids does a grid touch under the current HSA_CU_MASK?"""
+    from k8s_vgpu_scheduler_amd import ops
+
+    t = ops.hwid_probe(4096)
+    hw = [v & 0xFFFFFFFF for v in t[:, 0].tolist()]
+    xcc = [v & 0xFFFFFFFF for v in t[:, 1].tolist()]
+    places = sorted({((x & 0xF), (h >> 13) & 0x7, (h >> 12) & 0x1, (h >> 8) & 0xF) for h, x in zip(hw, xcc)})
+    return {"mode": "hwid", "cu_mask": os.environ.get("HSA_CU_MASK", ""), "distinct": len(places),
+            "xccs": sorted({p[0] for p in places}), "places": places[:512]}
 
 
 def run_child(mode: str, env_extra: dict, shim: bool, extra_args=(), timeout=300) -> dict:
@@ -141,15 +161,19 @@ def main():
     ap.add_argument("--oom-probe-mib", type=int, default=0)
     ap.add_argument("--out", default=None)
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--hwid", action="store_true")
     args = ap.parse_args()
     if args.child:
-        fn = {"matmul": child_matmul, "stream": child_stream}[args.child]
+        fn = {"matmul": child_matmul, "stream": child_stream, "hwid": child_hwid}[args.child]
         print(json.dumps(fn(args)), flush=True)
         return
     tmp = Path(os.environ.get("TMPDIR", "/tmp")) / f"mivgpu-probe-{os.getpid()}"
     tmp.mkdir(parents=True, exist_ok=True)
     mm = ["--n", "8192", "--iters", "60"]
     results = {}
+    if args.hwid:
+        for m in ("", "0:0-31", "0:32-63", "0:0-7", "0:0,8,16,24", "0:0-3,128-131"):
+            results[f"hwid[{m}]"] = run_child("hwid", {"HSA_CU_MASK": m} if m else {}, False, [])
     if args.quick:
         for pct in (25, 50, 75):
             results[f"gate_force_{pct}"] = run_child(
