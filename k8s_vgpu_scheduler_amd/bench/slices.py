@@ -54,7 +54,7 @@ def plan_slices(n: int, shim: bool, gpumem_mib: int | None, spatial: bool = True
                 policy: str = "default") -> list[SliceSpec]:
     """Equal split of one GPU into n slices (CUs in contiguous, XCD-sized runs)."""
     specs = []
-    per = MI355X_CUS // n
+    per = (MI355X_CUS // n) // MI355X_XCDS * MI355X_XCDS   # whole 8-CU granules: XCD-balanced
     for i in range(n):
         ranges = [(i * per, (i + 1) * per - 1)] if (shim and spatial and n > 1) else None
         specs.append(SliceSpec(index=i, gpumem_mib=gpumem_mib if shim else None, cu_ranges=ranges,

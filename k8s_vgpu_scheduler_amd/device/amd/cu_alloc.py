@@ -1,22 +1,24 @@
-"""XCD-aware CU-range allocator for ``HSA_CU_MASK`` partitions on MI355X.
+"""XCD-balanced CU-range allocator for ``HSA_CU_MASK`` partitions on MI355X.
 
 The reference only converts ``amd.com/gpucores`` % into a CU *count*
 (pkg/device/amd/device.go:333-344) and leaves choosing non-overlapping CU
 ranges to an unimplemented device-plugin step (docs/develop/amd-vgpu.md:74-90).
 Here the scheduler owns a per-GPU CU bitmap (rebuilt from pod annotations, so
-it survives restarts) and picks the concrete CUs at Fit time, XCD-first:
+it survives restarts) and picks the concrete CUs at Fit time.
 
-  * MI355X = 8 XCDs x 32 CUs; each XCD has its own 4 MiB L2, so a tenant
-    confined to whole XCDs does not share L2 with its neighbours
-    (MI355X_MICROARCH.md, XCD row);
-  * a request of >= 32 CUs takes whole free XCDs first, the remainder by
-    best-fit in the least-free XCD that can hold it (keeps other XCDs whole);
-  * a request < 32 CUs is best-fit into one XCD (never split across L2s unless
-    no single XCD has room).
-
-``layout`` says how ``HSA_CU_MASK`` logical CU indices map to XCDs:
-"blocked" (index // cus_per_xcd) or "interleaved" (index % n_xcd); it is
-measured on hardware by ``shim.probe --hwid`` and set in the device config.
+Measured on MI355X (``python -m k8s_vgpu_scheduler_amd.shim.probe --hwid``,
+profiles/cu_mask_placement.md):
+  * mask index i lives on XCD ``i % 8`` ("interleaved" layout): indices
+    0..7 are CU 0 of XCD 0..7, 8..15 the next CU of each XCD, ...;
+  * an XCD left with NO enabled CU is silently run with ALL its CUs
+    (mask ``0,8,16,24`` -> 228 active CUs), because every dispatch is dealt
+    round-robin to all 8 XCDs.
+So a partition must be XCD-*balanced*: the unit is a granule of one CU on
+each XCD (8 CUs, mask indices ``[8k, 8k+8)``), requests round up to whole
+granules, and a tenant's granules are chosen contiguous (best fit) so its
+CUs stay adjacent within each XCD's shader engines.  Per-XCD L2 isolation
+between tenants is not available through CU masking (it needs CPX partition
+mode, i.e. one HIP device per XCD), which is why the planner never promises it.
 """
 
 from __future__ import annotations
@@ -28,19 +30,24 @@ from dataclasses import dataclass
 class CUTopology:
     total: int = 256
     xcds: int = 8
-    layout: str = "interleaved"   # "interleaved" | "blocked"
+    layout: str = "interleaved"   # "interleaved" (measured on MI355X) | "blocked"
 
     @property
     def per_xcd(self) -> int:
         return max(1, self.total // max(1, self.xcds))
 
-    def xcd_cus(self, x: int) -> list[int]:
-        if self.layout == "blocked":
-            return list(range(x * self.per_xcd, (x + 1) * self.per_xcd))
-        return list(range(x, self.total, self.xcds))
+    @property
+    def granules(self) -> int:
+        return self.per_xcd
 
-    def groups(self) -> list[list[int]]:
-        return [self.xcd_cus(x) for x in range(self.xcds)]
+    def granule_cus(self, k: int) -> list[int]:
+        """CU mask indices of granule k (one CU on every XCD)."""
+        if self.layout == "blocked":
+            return [x * self.per_xcd + k for x in range(self.xcds)]
+        return list(range(k * self.xcds, (k + 1) * self.xcds))
+
+    def xcd_of(self, cu: int) -> int:
+        return cu // self.per_xcd if self.layout == "blocked" else cu % self.xcds
 
 
 def bitmap_from_ranges(ranges) -> int:
@@ -60,60 +67,58 @@ def ranges_from_cus(cus) -> list[tuple[int, int]]:
     return [(a, b) for a, b in out]
 
 
+def round_up_cus(n: int, topo: CUTopology) -> int:
+    """CU count actually granted for a request of n (whole granules)."""
+    if n <= 0:
+        return 0
+    g = -(-n // topo.xcds)
+    return min(topo.total, g * topo.xcds)
+
+
 def free_cus(used_bitmap: int, topo: CUTopology) -> int:
     return topo.total - bin(used_bitmap & ((1 << topo.total) - 1)).count("1")
 
 
+def _granule_free(used_bitmap: int, topo: CUTopology, k: int) -> bool:
+    return all(not (used_bitmap >> c) & 1 for c in topo.granule_cus(k))
+
+
 def pick(used_bitmap: int, n: int, topo: CUTopology) -> list[tuple[int, int]] | None:
-    """Choose n free CUs (XCD-first); None if fewer than n are free."""
+    """Choose ceil(n / xcds) free granules, contiguous if possible (best-fit
+    run), else the lowest free ones.  None if not enough granules are free."""
     if n <= 0:
         return []
-    if n > topo.total:
+    need = -(-n // topo.xcds)
+    if need > topo.granules:
         return None
-    free_by_xcd = []
-    for x, cus in enumerate(topo.groups()):
-        free_by_xcd.append((x, [c for c in cus if not (used_bitmap >> c) & 1]))
-    if sum(len(f) for _, f in free_by_xcd) < n:
+    free = [k for k in range(topo.granules) if _granule_free(used_bitmap, topo, k)]
+    if len(free) < need:
         return None
-    chosen: list[int] = []
-    need = n
-    per = topo.per_xcd
-    # 1) whole free XCDs
-    if need >= per:
-        for x, f in free_by_xcd:
-            if need < per:
-                break
-            if len(f) == per:
-                chosen.extend(f)
-                need -= per
-        taken = {x for x, f in free_by_xcd if f and set(f) <= set(chosen)}
+    # runs of consecutive free granules
+    runs: list[list[int]] = []
+    for k in free:
+        if runs and k == runs[-1][-1] + 1:
+            runs[-1].append(k)
+        else:
+            runs.append([k])
+    fitting = [r for r in runs if len(r) >= need]
+    if fitting:
+        r = min(fitting, key=lambda r: (len(r), r[0]))   # best fit keeps big runs whole
+        chosen = r[:need]
     else:
-        taken = set()
-    # 2) remainder: best fit into a single partially free XCD (least free that fits)
-    if need > 0:
-        cands = [(len(f), x, f) for x, f in free_by_xcd if x not in taken and len(f) >= need]
-        partial = [c for c in cands if c[0] < per]
-        pool = partial or cands
-        if pool:
-            _, x, f = min(pool)
-            chosen.extend(f[:need])
-            need = 0
-    # 3) still short: spill across XCDs, fullest-first to minimise L2 sharing
-    if need > 0:
-        for _, x, f in sorted(((len(f), x, f) for x, f in free_by_xcd if x not in taken), reverse=True):
-            rest = [c for c in f if c not in chosen]
-            take = rest[:need]
-            chosen.extend(take)
-            need -= len(take)
-            if need == 0:
-                break
-    if need > 0:
-        return None
-    return ranges_from_cus(chosen)
+        chosen = free[:need]
+    cus = [c for k in chosen for c in topo.granule_cus(k)]
+    return ranges_from_cus(cus)
 
 
-def xcds_touched(ranges, topo: CUTopology) -> int:
-    cus = set()
+def per_xcd_counts(ranges, topo: CUTopology) -> list[int]:
+    counts = [0] * topo.xcds
     for a, b in ranges:
-        cus.update(range(a, b + 1))
-    return sum(1 for g in topo.groups() if cus & set(g))
+        for c in range(a, b + 1):
+            counts[topo.xcd_of(c)] += 1
+    return counts
+
+
+def is_balanced(ranges, topo: CUTopology) -> bool:
+    c = per_xcd_counts(ranges, topo)
+    return len(set(c)) == 1 and c[0] > 0

@@ -9,8 +9,9 @@ cordon, NUMA binding, mutex, quota, full-core guard, topology-aware
 combination search), re-designed for MI355X:
 
   * ``gpucores`` % -> CU count (``floor(pct * devcore / 100)``, clamped to
-    [1, devcore]) AND a concrete, non-overlapping, XCD-aligned CU set chosen
-    from a per-GPU CU bitmap (:mod:`.cu_alloc`), written to
+    [1, devcore], rounded up to whole XCD-balanced granules of 8 CUs) AND a
+    concrete, non-overlapping CU set chosen from a per-GPU CU bitmap
+    (:mod:`.cu_alloc`: one CU per XCD per granule, as MI355X requires), written to
     ``hami.io/amd-cu-ranges`` and turned into ``HSA_CU_MASK`` by the device
     plugin -- spatial isolation in hardware;
   * ``gpucores`` omitted -> no CU reservation (time-shared, governor-gated)
@@ -74,7 +75,7 @@ class AMDConfig:
     gpu_core_policy: str = "default"
     runtime_class_name: str = ""
     overwrite_env: bool = False
-    # MI355X CU topology used by the CU-range allocator
+    # MI355X CU topology used by the CU-range allocator (measured, cu_alloc.py)
     xcds_per_device: int = 8
     cu_layout: str = "interleaved"
     # Node-side (device plugin) knobs, shared through the same config
@@ -427,6 +428,9 @@ class AMDDevices(D.Devices):
             if k.mem_percentage_req != 101 and k.memreq == 0:
                 memreq = dev.totalmem * k.mem_percentage_req // 100
             cu = cu_count_for(k.coresreq, dev.totalcore)
+            topo = self.cu_topology(dev.totalcore)
+            if 0 < cu < dev.totalcore:
+                cu = cu_alloc.round_up_cus(cu, topo)   # whole XCD-balanced granules
             if not self._fit_quota(pod, tmp, allocated, dev.id, memreq, cu, dev.totalcore or 256):
                 bump(R.RESOURCE_QUOTA_NOT_FIT)
                 continue
@@ -444,7 +448,7 @@ class AMDDevices(D.Devices):
                 continue
             info = {}
             if 0 < cu < dev.totalcore:
-                ranges = cu_alloc.pick(dev.custominfo.get("cu_used", 0), cu, self.cu_topology(dev.totalcore))
+                ranges = cu_alloc.pick(dev.custominfo.get("cu_used", 0), cu, topo)
                 if ranges is None:
                     bump(R.CARD_CU_FRAGMENTED)
                     continue

@@ -1,0 +1,476 @@
+"""Scheduler extender core: caches, registration loop, Filter, simulation Filter, Bind.
+
+Reference: pkg/scheduler/scheduler.go:60-1209.  Behavioural contract kept:
+  * informer-driven pod / node / ResourceQuota (and Lease) caches; pods that
+    carry ``hami.io/vgpu-node`` are decoded from their allocation annotation,
+    collapsed for init containers and added to PodManager + QuotaManager;
+  * ``register`` (leader only, 15 s tick + node/leader notifications) reads
+    every node's registration annotation, checks backend health (handshake),
+    cleans unhealthy/zero-device nodes and marks the cache ``synced``;
+  * ``filter`` is idempotent per pod (take-and-delete previous reservation),
+    rebuilds per-device usage from ALL cached pods, scores every candidate,
+    picks the best node, patches ``hami.io/vgpu-node``/``-time`` plus backend
+    annotations and reserves the usage immediately;
+  * CA simulation (``Nodes`` given) touches no cache;
+  * ``bind`` takes every backend's node lock transactionally (sorted, with
+    rollback; PodGroup members retry until --node-lock-retry-timeout), marks
+    bind-phase=allocating and creates the Binding.
+"""
+
+from __future__ import annotations
+
+import logging
+import os
+import threading
+import time
+
+from k8s_vgpu_scheduler_amd.device import codec
+from k8s_vgpu_scheduler_amd.device import devices as D
+from k8s_vgpu_scheduler_amd.device.init_container import (app_containers_only_device_usage,
+                                                          collapse_init_container_usage)
+from k8s_vgpu_scheduler_amd.device.pods import PodManager
+from k8s_vgpu_scheduler_amd.device.quota import get_local_cache
+from k8s_vgpu_scheduler_amd.device.types import DeviceUsage, NodeInfo
+from k8s_vgpu_scheduler_amd.k8s.client import KubeClient, annotations, name_of, ns_of
+from k8s_vgpu_scheduler_amd.k8s.informer import Informer
+from k8s_vgpu_scheduler_amd.utils import nodelock, util
+from k8s_vgpu_scheduler_amd.utils import types as T
+from k8s_vgpu_scheduler_amd.utils.leaderelection import DummyLeaderManager, LeaderManager
+
+from . import events as E
+from .config import SchedulerConfig
+from .nodes import NodeManager
+from .policy import DeviceListsScore, DeviceUsageList
+from .score import NodeUsage, calc_score
+
+log = logging.getLogger(__name__)
+
+
+def _decode_allocation(pod: dict) -> dict:
+    """Raw per-container PodDevices from the *-allocated annotations (+ CU ranges)."""
+    raw = codec.decode_pod_devices(D.SUPPORT_DEVICES, annotations(pod))
+    for t, single in raw.items():
+        dev = D.get_devices().get(t)
+        key = getattr(dev, "CU_RANGES_ANNOS", None) or "hami.io/amd-cu-ranges"
+        codec.attach_cu_ranges(single, annotations(pod).get(key))
+    return raw
+
+
+class Scheduler:
+    def __init__(self, client: KubeClient, cfg: SchedulerConfig | None = None):
+        self.client = client
+        self.cfg = cfg or SchedulerConfig()
+        self.nodes = NodeManager()
+        self.pod_manager = PodManager()
+        self.quota_manager = get_local_cache()
+        self.events = E.EventRecorder(client)
+        self.overview: dict[str, NodeUsage] = {}
+        self._lock = threading.RLock()
+        self.synced = False
+        self.started = False
+        self._stop = threading.Event()
+        self._notify = threading.Event()
+        if self.cfg.leader_elect:
+            self.leader = LeaderManager(self.cfg.hostname, self.cfg.leader_elect_resource_namespace,
+                                        self.cfg.leader_elect_resource_name,
+                                        on_started=self._notify.set, on_stopped=self._lost_leadership)
+        else:
+            self.leader = DummyLeaderManager(True)
+        self.pods_inf = Informer(client, "pods")
+        self.nodes_inf = Informer(client, "nodes")
+        self.quota_inf = Informer(client, "resourcequotas")
+        self.lease_inf = Informer(client, "leases", self.cfg.leader_elect_resource_namespace) \
+            if self.cfg.leader_elect else None
+
+    # ------------------------------------------------------------ lifecycle
+    def _lost_leadership(self):
+        with self._lock:
+            self.synced = False
+
+    def start(self):
+        self.pods_inf.add_event_handler(self.on_add_pod, self.on_update_pod, self.on_del_pod)
+        self.nodes_inf.add_event_handler(lambda n: self._notify.set(), None, self.on_del_node)
+        self.quota_inf.add_event_handler(self.quota_manager.add_quota,
+                                         lambda o, n: self.quota_manager.update_quota(o, n),
+                                         self.quota_manager.del_quota)
+        self.pods_inf.start()
+        self.nodes_inf.start()
+        self.quota_inf.start()
+        if self.lease_inf is not None:
+            self.lease_inf.add_event_handler(self.leader.on_add, self.leader.on_update, self.leader.on_delete)
+            self.lease_inf.start()
+        self.started = True
+
+    def stop(self):
+        self._stop.set()
+        self._notify.set()
+        for inf in (self.pods_inf, self.nodes_inf, self.quota_inf, self.lease_inf):
+            if inf is not None:
+                inf.stop()
+
+    def run_register_loop(self, period: float = 15.0):
+        """RegisterFromNodeAnnotations (scheduler.go:413-441)."""
+        while not self._stop.is_set():
+            self._notify.wait(timeout=period)
+            self._notify.clear()
+            if self._stop.is_set():
+                return
+            if not self.started:
+                continue
+            try:
+                self.register()
+            except Exception:  # noqa: BLE001
+                log.exception("register failed")
+
+    # ------------------------------------------------------------- pod events
+    def on_add_pod(self, pod: dict):
+        annos = annotations(pod)
+        node_id = annos.get(T.ASSIGNED_NODE_ANNOTATION)
+        if node_id is None:
+            return
+        if util.is_pod_terminated(pod):
+            pi = self.pod_manager.take_and_delete_pod(pod)
+            if pi:
+                self.quota_manager.rm_usage(pod, pi.devices)
+            return
+        if util.is_pod_terminating(pod):
+            self.pod_manager.update_pod(pod)
+            return
+        try:
+            raw = _decode_allocation(pod)
+        except codec.CodecError as e:
+            log.error("failed to decode pod devices %s/%s: %s", ns_of(pod), name_of(pod), e)
+            return
+        eff = collapse_init_container_usage(pod, raw)
+        if self.pod_manager.add_pod(pod, node_id, eff):
+            self.quota_manager.add_usage(pod, eff)
+
+    def on_update_pod(self, old: dict, new: dict):
+        if T.ASSIGNED_NODE_ANNOTATION not in annotations(new):
+            return
+        if util.is_pod_terminated(new):
+            pi = self.pod_manager.take_and_delete_pod(new)
+            if pi:
+                self.quota_manager.rm_usage(new, pi.devices)
+            return
+        if util.is_pod_terminating(new):
+            self.pod_manager.update_pod(new)
+            return
+        pi = self.pod_manager.get_pod(new)
+        if pi is None:
+            self.on_add_pod(new)
+            return
+        self.pod_manager.update_pod(new)
+        if not pi.init_released and util.all_init_containers_succeeded(new):
+            try:
+                raw = _decode_allocation(new)
+            except codec.CodecError:
+                return
+            app_only = app_containers_only_device_usage(new, raw)
+            old_devs, ok = self.pod_manager.update_pod_device(new, app_only)
+            if ok:
+                self.quota_manager.replace_usage(new, old_devs, app_only)
+
+    def on_del_pod(self, pod: dict):
+        if T.ASSIGNED_NODE_ANNOTATION not in annotations(pod):
+            return
+        pi = self.pod_manager.take_and_delete_pod(pod)
+        if pi:
+            self.quota_manager.rm_usage(pod, pi.devices)
+
+    def on_del_node(self, node: dict):
+        name = name_of(node)
+        nodelock.cleanup_node_lock(name)
+        self.nodes.rm_node(name)
+        with self._lock:
+            self.overview.pop(name, None)
+        for dev in D.get_devices().values():
+            dev.node_deleted(name)
+        self._notify.set()
+
+    # ------------------------------------------------------------ register
+    def register(self):
+        with self._lock:
+            if not self.leader.is_leader():
+                return
+            self.update_scheduler_label()
+            names = []
+            for node in self.nodes_inf.list(self.cfg.node_label_selector or None):
+                name = name_of(node)
+                names.append(name)
+                for vendor, dev in D.get_devices().items():
+                    err = None
+                    try:
+                        nodedevs = dev.get_node_devices(node)
+                    except Exception as e:  # noqa: BLE001
+                        nodedevs, err = [], e
+                    healthy, need_update = dev.check_health(vendor, node)
+                    if not healthy:
+                        try:
+                            cur = self.nodes.get_node(name)
+                        except LookupError:
+                            continue
+                        if vendor not in cur.devices:
+                            continue
+                        log.error("device unhealthy, cleaning up node %s vendor %s", name, vendor)
+                        try:
+                            dev.node_cleanup(name)
+                        except Exception as e:  # noqa: BLE001
+                            log.error("node cleanup failed: %s", e)
+                        self.nodes.rm_node_devices(name, vendor)
+                        continue
+                    if err is not None:
+                        continue
+                    if not nodedevs:
+                        try:
+                            if vendor in self.nodes.get_node(name).devices:
+                                self.nodes.rm_node_devices(name, vendor)
+                        except LookupError:
+                            pass
+                        continue
+                    if not need_update:
+                        try:
+                            self.nodes.get_node(name)
+                            continue
+                        except LookupError:
+                            pass  # not cached yet (e.g. restart): register anyway
+                    info = NodeInfo(id=name, node=node, devices={})
+                    for d in nodedevs:
+                        info.devices.setdefault(d.devicevendor or vendor, []).append(d)
+                    self.nodes.add_node(name, info)
+            _, overall, _ = self.get_nodes_usage(names, None)
+            self.overview = overall
+            self.synced = True
+
+    def update_scheduler_label(self):
+        ns, me = os.environ.get("POD_NAMESPACE"), os.environ.get("POD_NAME")
+        if not ns or not me:
+            return
+        for pod in self.pods_inf.list({T.COMPONENT_LABEL: T.COMPONENT_SCHEDULER}, namespace=ns):
+            want = T.ROLE_LEADER if name_of(pod) == me else T.ROLE_FOLLOWER
+            if (pod["metadata"].get("labels") or {}).get(T.ROLE_LABEL) != want:
+                try:
+                    util.patch_pod_labels(ns, name_of(pod), {T.ROLE_LABEL: want})
+                except Exception as e:  # noqa: BLE001
+                    log.error("failed to label scheduler pod %s: %s", name_of(pod), e)
+
+    def wait_for_cache_sync(self, timeout: float = 30.0) -> bool:
+        deadline = time.time() + timeout
+        while time.time() < deadline:
+            with self._lock:
+                if self.synced:
+                    return True
+            time.sleep(0.1)
+        return False
+
+    def inspect_all_nodes_usage(self) -> dict[str, NodeUsage]:
+        with self._lock:
+            return {k: v.deepcopy() for k, v in self.overview.items()}
+
+    # --------------------------------------------------------------- usage
+    def build_node_usage(self, info: NodeInfo, pod: dict | None) -> NodeUsage:
+        policy = util.get_gpu_scheduler_policy_by_pod(D.gpu_scheduler_policy(), pod)
+        numa = str(annotations(pod or {}).get("amd.com/numa-bind", "")).lower() in ("1", "t", "true")
+        lst = DeviceUsageList([], policy, numa)
+        for vendor_devs in info.devices.values():
+            for d in vendor_devs:
+                ci = dict(d.custominfo or {})
+                if d.pair_scores:
+                    ci["pair_scores"] = dict(d.pair_scores)
+                lst.device_lists.append(DeviceListsScore(DeviceUsage(
+                    id=d.id, index=d.index, used=0, count=d.count, usedmem=0, totalmem=d.devmem,
+                    totalcore=d.devcore, usedcores=0, mode=d.mode, numa=d.numa, type=d.type, health=d.health,
+                    pod_infos=[], custominfo=ci)))
+        return NodeUsage(info.node, info, lst)
+
+    def get_nodes_usage(self, node_names: list | None, pod: dict | None):
+        overall: dict[str, NodeUsage] = {}
+        failed: dict[str, str] = {}
+        all_nodes = self.nodes.list_nodes()
+        for nid, info in all_nodes.items():
+            overall[nid] = self.build_node_usage(info, pod)
+        for p in self.pod_manager.list_pods_info():
+            usage = overall.get(p.node_id)
+            if usage is None:
+                continue
+            by_id = {dl.device.id: dl.device for dl in usage.devices.device_lists}
+            for single in p.devices.values():
+                for ctr in single:
+                    for cd in ctr:
+                        d = by_id.get(cd.uuid)
+                        if d is None:
+                            log.error("pod %s/%s holds unknown device %s on %s", p.namespace, p.name,
+                                      cd.uuid, p.node_id)
+                            continue
+                        d.used += max(cd.slots, 1)
+                        d.usedmem += cd.usedmem
+                        d.usedcores += cd.usedcores
+                        d.pod_infos.append((p.namespace, p.name, p.uid))
+                        r = (cd.custominfo or {}).get("cu_ranges")
+                        if r:
+                            from k8s_vgpu_scheduler_amd.device.amd.cu_alloc import bitmap_from_ranges
+                            d.custominfo["cu_used"] = d.custominfo.get("cu_used", 0) | bitmap_from_ranges(r)
+        if node_names is None:
+            return {}, overall, failed
+        cache = {}
+        for n in node_names:
+            if n not in all_nodes:
+                failed[n] = "node unregistered"
+                continue
+            cache[n] = overall[n]
+        return cache, overall, failed
+
+    def get_simulation_nodes_usage(self, nodes: list[dict], pod: dict):
+        cand, failed = {}, {}
+        for node in nodes or []:
+            info = NodeInfo(id=name_of(node), node=node, devices={})
+            for vendor, dev in D.get_devices().items():
+                try:
+                    for d in dev.get_node_devices(node):
+                        info.devices.setdefault(d.devicevendor or vendor, []).append(d)
+                except Exception:  # noqa: BLE001
+                    continue
+            if not info.devices:
+                failed[name_of(node)] = "node unregistered"
+                continue
+            cand[name_of(node)] = self.build_node_usage(info, pod)
+        return cand, failed
+
+    # --------------------------------------------------------------- locks
+    def lock_all_devices(self, node: dict, pod: dict):
+        acquired = []
+        for k in sorted(D.get_devices()):
+            dev = D.get_devices()[k]
+            try:
+                dev.lock_node(node, pod)
+            except Exception:
+                for a in reversed(acquired):
+                    try:
+                        a.release_node_lock(node, pod)
+                    except Exception as e:  # noqa: BLE001
+                        log.error("rollback release failed: %s", e)
+                raise
+            acquired.append(dev)
+
+    def release_all_devices(self, node: dict, pod: dict):
+        for k in sorted(D.get_devices()):
+            try:
+                D.get_devices()[k].release_node_lock(node, pod)
+            except Exception as e:  # noqa: BLE001
+                log.error("release node lock failed: %s", e)
+
+    def acquire_node_locks(self, node: dict, pod: dict):
+        if not util.is_pod_group_member(pod) or self.cfg.node_lock_retry_timeout <= 0:
+            return self.lock_all_devices(node, pod)
+        deadline = time.time() + self.cfg.node_lock_retry_timeout
+        while True:
+            try:
+                return self.lock_all_devices(node, pod)
+            except nodelock.NodeLockContention:
+                if time.time() > deadline:
+                    raise nodelock.NodeLockContention(
+                        f"timed out after {self.cfg.node_lock_retry_timeout}s waiting for node "
+                        f"{name_of(node)} to be unlocked")
+                if self._stop.wait(0.1):
+                    raise
+
+    # ------------------------------------------------------------------ bind
+    def bind(self, args: dict) -> dict:
+        pod_name = args.get("PodName") or args.get("podName")
+        ns = args.get("PodNamespace") or args.get("podNamespace") or "default"
+        uid = args.get("PodUID") or args.get("podUID")
+        node_name = args.get("Node") or args.get("node")
+        current = self.pods_inf.get(pod_name, ns)
+        if current is None:
+            try:
+                current = self.client.get_pod(ns, pod_name)
+            except Exception as e:  # noqa: BLE001
+                self._cleanup_stale({"metadata": {"name": pod_name, "namespace": ns, "uid": uid}})
+                return {"Error": str(e)}
+        node = self.nodes_inf.get(node_name)
+        if node is None:
+            try:
+                node = self.client.get_node(node_name)
+            except Exception as e:  # noqa: BLE001
+                self.events.binding_result(current, E.BINDING_FAILED, [], f"failed to get node {node_name}")
+                self._cleanup_stale(current)
+                return {"Error": str(e)}
+
+        def fail(e):
+            self.release_all_devices(node, current)
+            self.events.binding_result(current, E.BINDING_FAILED, [], e)
+            return {"Error": str(e) if e else ""}
+
+        try:
+            self.acquire_node_locks(node, current)
+        except Exception as e:  # noqa: BLE001
+            return fail(e)
+        try:
+            util.patch_pod_annotations(current, {T.DEVICE_BIND_PHASE: T.DEVICE_BIND_ALLOCATING,
+                                                 T.BIND_TIME_ANNOTATION: str(int(time.time()))})
+            self.client.bind(ns, pod_name, node_name, uid)
+        except Exception as e:  # noqa: BLE001
+            return fail(e)
+        self.events.binding_result(current, E.BINDING_SUCCEED, [node_name], None)
+        return {"Error": ""}
+
+    def _cleanup_stale(self, pod: dict):
+        pi = self.pod_manager.take_and_delete_pod(pod)
+        if pi and pi.devices:
+            self.quota_manager.rm_usage(pod, pi.devices)
+
+    # ---------------------------------------------------------------- filter
+    def filter(self, args: dict) -> dict:
+        pod = args.get("Pod") or args.get("pod")
+        node_names = args.get("NodeNames", args.get("nodenames"))
+        nodes = args.get("Nodes", args.get("nodes"))
+        reqs = D.resource_reqs(pod)
+        if not any(reqs):
+            return {"NodeNames": node_names, "FailedNodes": None, "Error": ""}
+        if nodes is not None:
+            return self._filter_simulation(pod, nodes, reqs)
+        pi = self.pod_manager.take_and_delete_pod(pod)
+        if pi:
+            self.quota_manager.rm_usage(pod, pi.devices)
+        usage, _, failed = self.get_nodes_usage(node_names or [], pod)
+        scores, failure = calc_score(usage, reqs, pod, failed, self.cfg.node_scheduler_policy)
+        if not scores.node_list:
+            for reason, ns_ in sorted(failure.items()):
+                self.events.filter_result(pod, E.FILTERING_FAILED, "",
+                                          f"{len(ns_)} nodes {reason}({','.join(sorted(ns_))})")
+            self.events.filter_result(pod, E.FILTERING_FAILED, "",
+                                      f"no available node, {len(node_names or [])} nodes do not meet")
+            return {"FailedNodes": failed, "NodeNames": None, "Error": ""}
+        scores.sort()
+        best = scores.node_list[-1]
+        annos = {T.ASSIGNED_NODE_ANNOTATION: best.node_id, T.ASSIGNED_TIME_ANNOTATION: str(int(time.time()))}
+        for dev in D.get_devices().values():
+            dev.patch_annotations(pod, annos, best.devices)
+        eff = collapse_init_container_usage(pod, best.devices)
+        added = self.pod_manager.add_pod(pod, best.node_id, eff)
+        if added:
+            self.quota_manager.add_usage(pod, eff)
+        try:
+            util.patch_pod_annotations(pod, annos)
+        except Exception as e:  # noqa: BLE001
+            self.events.filter_result(pod, E.FILTERING_FAILED, "", e)
+            if added:
+                self.quota_manager.rm_usage(pod, eff)
+            self.pod_manager.del_pod(pod)
+            return {"Error": str(e)}
+        msg = (f"find fit node({best.node_id}), {len(node_names or []) - len(scores.node_list)} nodes not fit, "
+               f"{len(scores.node_list)} nodes fit("
+               + ",".join(f"{n.node_id}:{n.score:.2f}" for n in scores.node_list) + ")")
+        self.events.filter_result(pod, E.FILTERING_SUCCEED, msg, None)
+        return {"NodeNames": [best.node_id], "FailedNodes": failed, "Error": ""}
+
+    def _filter_simulation(self, pod: dict, nodes, reqs) -> dict:
+        items = nodes.get("items", []) if isinstance(nodes, dict) else list(nodes)
+        usage, failed = self.get_simulation_nodes_usage(items, pod)
+        scores, _ = calc_score(usage, reqs, pod, failed, self.cfg.node_scheduler_policy)
+        if not scores.node_list:
+            return {"FailedNodes": failed, "Nodes": None, "Error": ""}
+        scores.sort()
+        best = scores.node_list[-1].node_id
+        chosen = [n for n in items if name_of(n) == best][:1]
+        return {"Nodes": {"items": chosen}, "FailedNodes": failed, "Error": ""}
