@@ -60,6 +60,10 @@ def main():
     ap.add_argument("--no-spatial", action="store_true", help="no HSA_CU_MASK (temporal governor)")
     ap.add_argument("--policy", default="default", choices=["default", "force", "disable"])
     ap.add_argument("--out", default=None, help="also write the JSON line here")
+    ap.add_argument("--hw-queues", type=int, default=1,
+                    help="GPU_MAX_HW_QUEUES per slice in the shim round (0 = HIP default)")
+    ap.add_argument("--child-env", action="append", default=[], metavar="K=V",
+                    help="extra environment for every slice process (experiments)")
     args = ap.parse_args()
 
     from k8s_vgpu_scheduler_amd.bench.slices import plan_slices, run_round, spawn_round
@@ -77,15 +81,23 @@ def main():
     child_args = ["--model", args.model, "--batch", str(args.batch), "--ctx", str(args.ctx),
                   "--steps", str(args.steps), "--warmup", str(args.warmup)]
 
+    extra_env = dict(kv.split("=", 1) for kv in args.child_env)
+
+    def with_env(specs):
+        for sp in specs:
+            sp.env.update(extra_env)
+        return specs
+
     # Spawn every slice process of both rounds BEFORE this process touches HIP.
     rounds = []
     if args.mode in ("both", "native"):
-        rounds.append(("native", spawn_round(plan_slices(args.slices, shim=False, gpumem_mib=None),
+        rounds.append(("native", spawn_round(with_env(plan_slices(args.slices, shim=False, gpumem_mib=None)),
                                              phys, work, log_dir, child_args, "native")))
     if args.mode in ("both", "shim"):
         rounds.append(("shim", spawn_round(
-            plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib,
-                        spatial=not args.no_spatial, policy=args.policy),
+            with_env(plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib,
+                                 spatial=not args.no_spatial, policy=args.policy,
+                                 hw_queues=args.hw_queues or None)),
             phys, work, log_dir, child_args, "shim")))
 
     import torch
@@ -140,7 +152,8 @@ def main():
                 "batch_per_slice": args.batch,
                 "gpumem_mib_per_slice": args.gpumem_mib,
                 "gpucores_per_slice": 100 // args.slices if args.slices > 1 else 100,
-                "isolation": "HSA_CU_MASK + libmivgpu" if not args.no_spatial else f"governor ({args.policy})",
+                "isolation": ("HSA_CU_MASK + libmivgpu" if not args.no_spatial else f"governor ({args.policy})")
+                + (f" + {args.hw_queues} HW queue/slice" if args.hw_queues and args.slices > 1 else ""),
             },
             "round": "shim" if "shim" in results else "native",
             "per_slice_tok_s_rank0": per_slice,

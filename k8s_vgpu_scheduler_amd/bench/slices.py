@@ -43,6 +43,11 @@ class SliceSpec:
     core_pct: int = 100
     shim: bool = True
     policy: str = "default"
+    # HW queues per slice process (GPU_MAX_HW_QUEUES).  HIP's default of 4 per
+    # process oversubscribes the hardware scheduler once several tenants share
+    # a GPU (measured: 4 slices 3.1k -> 6.4k tok/s with 1 queue each); the
+    # device plugin injects the same value for fractional pods.
+    hw_queues: int | None = None
     env: dict = field(default_factory=dict)
 
 
@@ -51,7 +56,7 @@ def cu_mask_string(ranges) -> str:
 
 
 def plan_slices(n: int, shim: bool, gpumem_mib: int | None, spatial: bool = True,
-                policy: str = "default") -> list[SliceSpec]:
+                policy: str = "default", hw_queues: int | None = 1) -> list[SliceSpec]:
     """Equal split of one GPU into n slices (CUs in contiguous, XCD-sized runs)."""
     specs = []
     per = (MI355X_CUS // n) // MI355X_XCDS * MI355X_XCDS   # whole 8-CU granules: XCD-balanced
@@ -59,7 +64,7 @@ def plan_slices(n: int, shim: bool, gpumem_mib: int | None, spatial: bool = True
         ranges = [(i * per, (i + 1) * per - 1)] if (shim and spatial and n > 1) else None
         specs.append(SliceSpec(index=i, gpumem_mib=gpumem_mib if shim else None, cu_ranges=ranges,
                                core_pct=max(1, 100 // n) if n > 1 else 100, shim=shim,
-                               policy=policy))
+                               policy=policy, hw_queues=hw_queues if (shim and n > 1) else None))
     return specs
 
 
@@ -78,6 +83,8 @@ def slice_env(spec: SliceSpec, physical_gpu: str | None, cache_dir: Path) -> dic
         env["GPU_CORE_UTILIZATION_POLICY"] = spec.policy
         if spec.cu_ranges:
             env["HSA_CU_MASK"] = "0:" + cu_mask_string(spec.cu_ranges)
+        if spec.hw_queues:
+            env["GPU_MAX_HW_QUEUES"] = str(spec.hw_queues)
     env.update(spec.env)
     return env
 

@@ -1,0 +1,283 @@
+"""Scheduler extender end-to-end on the fake API server (no GPU).
+
+Mirrors the reference's scheduler tests (pkg/scheduler/scheduler_test.go
+Test_Filter / Bind, score_test.go, register tests) for the MI355X backend.
+"""
+
+import pytest
+
+from k8s_vgpu_scheduler_amd.device import codec
+from k8s_vgpu_scheduler_amd.device.amd import cu_alloc
+from k8s_vgpu_scheduler_amd.device.amd.device import (CU_RANGES_ANNOS, IN_REQUEST_ANNOS, SUPPORT_ANNOS)
+from k8s_vgpu_scheduler_amd.device.quota import get_local_cache
+from k8s_vgpu_scheduler_amd.k8s.client import init_global_client
+from k8s_vgpu_scheduler_amd.k8s.fake import FakeCluster
+from k8s_vgpu_scheduler_amd.scheduler.config import SchedulerConfig, init_devices_with_config
+from k8s_vgpu_scheduler_amd.scheduler.scheduler import Scheduler
+from k8s_vgpu_scheduler_amd.testing import (MI355X_MEM_MIB, amd_container, amd_node, amd_pod, full_mesh_scores,
+                                            mi355x_devices)
+from k8s_vgpu_scheduler_amd.utils import types as T
+
+
+@pytest.fixture
+def cluster():
+    c = FakeCluster()
+    init_global_client(c)
+    init_devices_with_config()
+    get_local_cache().quotas.clear()
+    return c
+
+
+def make_sched(cluster, nodes, **cfg):
+    for n in nodes:
+        cluster.create("nodes", n)
+    s = Scheduler(cluster, SchedulerConfig(**cfg))
+    s.start()
+    s.register()
+    assert s.synced
+    return s
+
+
+def filt(s, cluster, pod, nodes):
+    cluster.create("pods", pod)
+    return s.filter({"Pod": cluster.get_pod("default", pod["metadata"]["name"]), "NodeNames": nodes})
+
+
+def test_single_slice_annotation_format(cluster):
+    s = make_sched(cluster, [amd_node("n1", n=1)])
+    res = filt(s, cluster, amd_pod("p1", mem=36864), ["n1"])
+    assert res["NodeNames"] == ["n1"] and not res["Error"]
+    annos = cluster.get_pod("default", "p1")["metadata"]["annotations"]
+    # gpucores omitted -> no CU reservation (time-shared)
+    assert annos[SUPPORT_ANNOS] == "n1-gpu0,AMD Instinct MI355X,36864,0:;"
+    assert annos[IN_REQUEST_ANNOS] == annos[SUPPORT_ANNOS]
+    assert annos[T.ASSIGNED_NODE_ANNOTATION] == "n1"
+    assert CU_RANGES_ANNOS not in annos
+    # label mirror of the node annotation (util.go:174-205)
+    assert cluster.get_pod("default", "p1")["metadata"]["labels"][T.ASSIGNED_NODE_ANNOTATION] == "n1"
+
+
+def test_gpucores_become_disjoint_xcd_balanced_cu_ranges(cluster):
+    s = make_sched(cluster, [amd_node("n1", n=1)])
+    topo = cu_alloc.CUTopology()
+    seen = 0
+    for i in range(4):
+        res = filt(s, cluster, amd_pod(f"p{i}", mem=36864, cores=25), ["n1"])
+        assert res["NodeNames"] == ["n1"], res
+        annos = cluster.get_pod("default", f"p{i}")["metadata"]["annotations"]
+        devs = codec.decode_container_devices(annos[SUPPORT_ANNOS].split(";")[0])
+        assert devs[0].usedcores == 64   # 25 % of 256 CUs
+        ranges = codec.decode_cu_ranges(annos[CU_RANGES_ANNOS])[0]["n1-gpu0"]
+        assert codec.ranges_count(ranges) == 64
+        assert cu_alloc.is_balanced(ranges, topo)
+        bm = cu_alloc.bitmap_from_ranges(ranges)
+        assert bm & seen == 0, "CU ranges overlap"
+        seen |= bm
+    # fifth 25 % pod cannot fit: all 256 CUs are spatially reserved
+    res = filt(s, cluster, amd_pod("p4", mem=1024, cores=25), ["n1"])
+    assert not res.get("NodeNames")
+    assert "CardInsufficientCore" in res["FailedNodes"]["n1"]
+
+
+def test_memory_hard_limit_capacity(cluster):
+    s = make_sched(cluster, [amd_node("n1", n=1)])
+    for i in range(8):  # 8 x 36 GiB = 288 GiB
+        assert filt(s, cluster, amd_pod(f"p{i}", mem=36864), ["n1"])["NodeNames"] == ["n1"]
+    res = filt(s, cluster, amd_pod("p9", mem=1), ["n1"])
+    assert "CardTimeSlicingExhausted" in res["FailedNodes"]["n1"] or \
+        "CardInsufficientMemory" in res["FailedNodes"]["n1"]
+
+
+def test_whole_card_default_and_exclusive(cluster):
+    s = make_sched(cluster, [amd_node("n1", n=2)])
+    pod = amd_pod("whole", gpu=1)  # no mem, no cores -> whole card
+    # webhook would default cores to 100; emulate via mutate
+    from k8s_vgpu_scheduler_amd.device import devices as D
+    D.get_devices()["AMD"].mutate_admission(pod["spec"]["containers"][0], pod)
+    res = filt(s, cluster, pod, ["n1"])
+    assert res["NodeNames"] == ["n1"]
+    annos = cluster.get_pod("default", "whole")["metadata"]["annotations"]
+    d = codec.decode_container_devices(annos[SUPPORT_ANNOS].split(";")[0])[0]
+    assert d.usedmem == MI355X_MEM_MIB and d.usedcores == 256
+    # a second pod can still land on the other GPU, but not on the same one
+    res = filt(s, cluster, amd_pod("small", mem=1024, cores=10), ["n1"])
+    d2 = codec.decode_container_devices(
+        cluster.get_pod("default", "small")["metadata"]["annotations"][SUPPORT_ANNOS].split(";")[0])[0]
+    assert d2.uuid != d.uuid
+
+
+@pytest.mark.parametrize("policy,expect_same", [("binpack", True), ("spread", False)])
+def test_gpu_policy_binpack_vs_spread(cluster, policy, expect_same):
+    s = make_sched(cluster, [amd_node("n1", n=4)])
+    a = amd_pod("a", mem=10000, annotations={T.GPU_POLICY_ANNOTATION: policy})
+    b = amd_pod("b", mem=10000, annotations={T.GPU_POLICY_ANNOTATION: policy})
+    filt(s, cluster, a, ["n1"])
+    filt(s, cluster, b, ["n1"])
+    ua = codec.decode_container_devices(cluster.get_pod("default", "a")["metadata"]["annotations"][SUPPORT_ANNOS].split(";")[0])[0].uuid
+    ub = codec.decode_container_devices(cluster.get_pod("default", "b")["metadata"]["annotations"][SUPPORT_ANNOS].split(";")[0])[0].uuid
+    assert (ua == ub) == expect_same
+
+
+@pytest.mark.parametrize("policy", ["binpack", "spread"])
+def test_node_policy(cluster, policy):
+    s = make_sched(cluster, [amd_node("n1", n=2), amd_node("n2", n=2)], node_scheduler_policy=policy)
+    filt(s, cluster, amd_pod("a", mem=100000), ["n1"])   # load n1
+    res = filt(s, cluster, amd_pod("b", mem=1000), ["n1", "n2"])
+    assert res["NodeNames"] == (["n1"] if policy == "binpack" else ["n2"])
+
+
+def test_mutex_policy_prefers_idle_gpu(cluster):
+    s = make_sched(cluster, [amd_node("n1", n=2)])
+    filt(s, cluster, amd_pod("a", mem=1000), ["n1"])
+    pm = {T.GPU_POLICY_ANNOTATION: "mutex"}
+    filt(s, cluster, amd_pod("b", mem=1000, annotations=pm), ["n1"])
+    res = filt(s, cluster, amd_pod("c", mem=1000, annotations=pm), ["n1"])
+    assert "ExclusiveDeviceAllocateConflict" in res["FailedNodes"]["n1"]
+
+
+def test_topology_aware_multi_gpu_picks_best_connected(cluster):
+    devs = mi355x_devices("n1", 4)
+    # gpu0-gpu1 link degraded; best pair among others
+    scores = full_mesh_scores(devs, 100, degraded={("n1-gpu0", "n1-gpu1"): 10, ("n1-gpu2", "n1-gpu3"): 10,
+                                                   ("n1-gpu0", "n1-gpu2"): 40})
+    s = make_sched(cluster, [amd_node("n1", n=4, scores=scores)])
+    pod = amd_pod("tp2", gpu=2, mem=1000, annotations={T.GPU_POLICY_ANNOTATION: "topology-aware"})
+    res = filt(s, cluster, pod, ["n1"])
+    assert res["NodeNames"] == ["n1"]
+    devs = codec.decode_container_devices(
+        cluster.get_pod("default", "tp2")["metadata"]["annotations"][SUPPORT_ANNOS].split(";")[0])
+    pair = sorted(d.uuid for d in devs)
+    assert scores[pair[0]][pair[1]] == 100
+
+
+def test_topology_node_score_prefers_healthy_xgmi(cluster):
+    good = mi355x_devices("good", 2)
+    bad = mi355x_devices("bad", 2)
+    s = make_sched(cluster, [amd_node("good", n=2, scores=full_mesh_scores(good, 100)),
+                             amd_node("bad", n=2, scores=full_mesh_scores(bad, 20))])
+    res = filt(s, cluster, amd_pod("tp2", gpu=2, mem=1000), ["good", "bad"])
+    assert res["NodeNames"] == ["good"]
+
+
+def test_uuid_and_type_selectors_and_cordon(cluster):
+    node = amd_node("n1", n=3, annotations={T.DEVICE_CORDON_ANNOTATION: "n1-gpu2"})
+    s = make_sched(cluster, [node])
+    res = filt(s, cluster, amd_pod("a", mem=10, annotations={"amd.com/use-gpu-uuid": "n1-gpu1"}), ["n1"])
+    assert codec.decode_container_devices(
+        cluster.get_pod("default", "a")["metadata"]["annotations"][SUPPORT_ANNOS].split(";")[0])[0].uuid == "n1-gpu1"
+    res = filt(s, cluster, amd_pod("b", mem=10, annotations={"amd.com/use-gpu-uuid": "n1-gpu2"}), ["n1"])
+    assert "CardCordoned" in res["FailedNodes"]["n1"]
+    res = filt(s, cluster, amd_pod("c", mem=10, annotations={"amd.com/nouse-gputype": "MI355X"}), ["n1"])
+    assert "CardTypeMismatch" in res["FailedNodes"]["n1"]
+
+
+def test_filter_is_idempotent_per_pod(cluster):
+    s = make_sched(cluster, [amd_node("n1", n=1, split=2)])
+    pod = amd_pod("a", mem=100000)
+    cluster.create("pods", pod)
+    for _ in range(3):  # kube-scheduler may retry the same pod
+        res = s.filter({"Pod": cluster.get_pod("default", "a"), "NodeNames": ["n1"]})
+        assert res["NodeNames"] == ["n1"]
+    assert len(s.pod_manager) == 1
+
+
+def test_init_container_peak_accounting(cluster):
+    s = make_sched(cluster, [amd_node("n1", n=1)])
+    pod = amd_pod("p", containers=[amd_container("app", mem=100000)],
+                  init=[amd_container("init", mem=200000)])
+    res = filt(s, cluster, pod, ["n1"])
+    assert res["NodeNames"] == ["n1"]
+    annos = cluster.get_pod("default", "p")["metadata"]["annotations"]
+    parts = annos[SUPPORT_ANNOS].split(";")
+    assert parts[0].startswith("n1-gpu0,") and ",200000," in parts[0]   # init first
+    assert ",100000," in parts[1]
+    # effective usage = max(init peak, app sum) = 200000
+    _, overall, _ = s.get_nodes_usage(["n1"], None)
+    d = overall["n1"].devices.device_lists[0].device
+    assert d.usedmem == 200000 and d.used == 1
+
+
+def test_quota_blocks_over_limit(cluster):
+    s = make_sched(cluster, [amd_node("n1", n=2)])
+    cluster.create("resourcequotas", {"metadata": {"name": "q", "namespace": "default"},
+                                      "spec": {"hard": {"limits.amd.com/gpumem": "50000",
+                                                        "limits.amd.com/gpucores": "30"}}})
+    assert filt(s, cluster, amd_pod("a", mem=40000, cores=10), ["n1"])["NodeNames"] == ["n1"]
+    res = filt(s, cluster, amd_pod("b", mem=20000, cores=10), ["n1"])
+    assert "ResourceQuotaNotFit" in res["FailedNodes"]["n1"]
+    res = filt(s, cluster, amd_pod("c", mem=1000, cores=25), ["n1"])
+    assert "ResourceQuotaNotFit" in res["FailedNodes"]["n1"]
+
+
+def test_simulation_filter_touches_no_cache(cluster):
+    s = make_sched(cluster, [amd_node("n1", n=1)])
+    tmpl = amd_node("tmpl", n=8)
+    pod = amd_pod("sim", mem=1000)
+    res = s.filter({"Pod": pod, "Nodes": {"items": [tmpl]}})
+    assert [n["metadata"]["name"] for n in res["Nodes"]["items"]] == ["tmpl"]
+    assert len(s.pod_manager) == 0
+    assert cluster.count("patch", "pods") == 0
+
+
+def test_bind_sets_phase_lock_and_node(cluster):
+    s = make_sched(cluster, [amd_node("n1", n=1)])
+    filt(s, cluster, amd_pod("a", mem=1000), ["n1"])
+    p = cluster.get_pod("default", "a")
+    res = s.bind({"PodName": "a", "PodNamespace": "default", "PodUID": p["metadata"]["uid"], "Node": "n1"})
+    assert res["Error"] == ""
+    p = cluster.get_pod("default", "a")
+    assert p["spec"]["nodeName"] == "n1"
+    assert p["metadata"]["annotations"][T.DEVICE_BIND_PHASE] == "allocating"
+    lock = cluster.get_node("n1")["metadata"]["annotations"][T.NODE_LOCK_KEY]
+    assert lock.endswith(",default,a")
+    # a second pod cannot bind while the lock is held
+    filt(s, cluster, amd_pod("b", mem=1000), ["n1"])
+    res = s.bind({"PodName": "b", "PodNamespace": "default", "Node": "n1"})
+    assert "locked" in res["Error"]
+
+
+def test_informer_rebuilds_state_after_restart(cluster):
+    s = make_sched(cluster, [amd_node("n1", n=1)])
+    filt(s, cluster, amd_pod("a", mem=30000, cores=25), ["n1"])
+    s.stop()
+    s2 = Scheduler(cluster, SchedulerConfig())
+    s2.start()
+    s2.register()
+    _, overall, _ = s2.get_nodes_usage(["n1"], None)
+    d = overall["n1"].devices.device_lists[0].device
+    assert d.usedmem == 30000 and d.usedcores == 64
+    assert bin(d.custominfo["cu_used"]).count("1") == 64
+
+
+def test_pod_deletion_releases_usage(cluster):
+    s = make_sched(cluster, [amd_node("n1", n=1, split=1)])
+    filt(s, cluster, amd_pod("a", mem=1000), ["n1"])
+    assert not filt(s, cluster, amd_pod("b", mem=1000), ["n1"]).get("NodeNames")
+    cluster.delete("pods", "a", "default")
+    assert filt(s, cluster, amd_pod("c", mem=1000), ["n1"])["NodeNames"] == ["n1"]
+
+
+def test_unregistered_and_unhealthy_nodes(cluster):
+    node = amd_node("n1", n=1, health=False)
+    s = make_sched(cluster, [node])
+    res = filt(s, cluster, amd_pod("a", mem=1000), ["n1", "ghost"])
+    assert res["FailedNodes"]["ghost"] == "node unregistered"
+    assert "CardNotHealth" in res["FailedNodes"]["n1"]
+
+
+def test_numa_bind_keeps_devices_on_one_numa(cluster):
+    s = make_sched(cluster, [amd_node("n1", n=4, numa_per=2)])
+    pod = amd_pod("p", gpu=2, mem=1000, annotations={"amd.com/numa-bind": "true"})
+    assert filt(s, cluster, pod, ["n1"])["NodeNames"] == ["n1"]
+    devs = codec.decode_container_devices(
+        cluster.get_pod("default", "p")["metadata"]["annotations"][SUPPORT_ANNOS].split(";")[0])
+    numas = {int(d.uuid[-1]) // 2 for d in devs}
+    assert len(numas) == 1
+
+
+def test_64_vgpus_on_8x8_node(cluster):
+    """BASELINE config 5: 8 slices/GPU x 8 MI355X = 64 schedulable vGPUs."""
+    s = make_sched(cluster, [amd_node("n1", n=8, split=8)])
+    for i in range(64):
+        assert filt(s, cluster, amd_pod(f"p{i}", mem=36864, cores=12), ["n1"])["NodeNames"] == ["n1"], i
+    assert not filt(s, cluster, amd_pod("p64", mem=1, cores=0), ["n1"]).get("NodeNames")
