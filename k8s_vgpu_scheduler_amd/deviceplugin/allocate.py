@@ -1,0 +1,140 @@
+"""Container environment, mounts and device nodes for an allocated vGPU slice.
+
+Reference contract: Allocate in pkg/device-plugin/nvidiadevice/nvinternal/plugin/
+server.go:747-912 (envs :833-847, mounts :848-897) plus the AMD protocol of
+docs/develop/amd-vgpu.md:47-104.  MI355X translation:
+
+  env  ROCR_VISIBLE_DEVICES   ROCr ids of the allocated GPUs, in allocation
+                              order (= container-local device index)
+       HSA_CU_MASK            ``i:ranges;...`` for devices with a CU partition
+       HIP_DEVICE_MEMORY_LIMIT_i  ``<MiB>m`` hard limit per local device
+       HIP_DEVICE_CORE_LIMIT  CU share in % (first device, for the governor)
+       GPU_MAX_HW_QUEUES      1 for shared (fractional) pods: HIP's default 4
+                              queues/process oversubscribes the HW scheduler
+                              when tenants share a GPU (measured, bench)
+       MIVGPU_SHARED_CACHE    $HOOK_PATH/vgpu/<uuid4>.cache
+       MIVGPU_DEVICE_UUIDS, MIVGPU_OVERSUBSCRIBE, MIVGPU_LOG_LEVEL,
+       GPU_CORE_UTILIZATION_POLICY=disable (with --disable-core-limit)
+  mounts libmivgpu.so (ro), the per-container cache dir (rw), /tmp/vgpulock,
+       /etc/ld.so.preload (ro) unless the container sets MIVGPU_DISABLE_CONTROL=true
+  devs /dev/kfd and the allocated /dev/dri/renderD<N> (+ card<M>) nodes
+"""
+
+from __future__ import annotations
+
+import os
+import uuid as _uuid
+from dataclasses import dataclass
+
+from k8s_vgpu_scheduler_amd.device.codec import format_ranges, ranges_count
+
+CONTAINER_LIB = "/usr/local/vgpu/libmivgpu.so"
+
+
+@dataclass
+class PluginConfig:
+    hook_path: str = "/usr/local/vgpu"
+    resource_name: str = "amd.com/gpu"
+    device_split_count: int = 8
+    device_memory_scaling: float = 1.0
+    device_core_scaling: float = 1.0
+    disable_core_limit: bool = False
+    log_level: str = ""
+    hw_queues_shared: int = 1
+    pass_device_specs: bool = True
+    enable_preferred_allocation: bool = True
+    filter_uuids: tuple = ()
+    filter_indexes: tuple = ()
+    enable_numa_topology: bool = False
+    node_name: str = ""
+
+
+def _truthy(v) -> bool:
+    return str(v).strip().lower() in ("1", "t", "true", "yes")
+
+
+def container_env(devreq: list, gpus: dict, cfg: PluginConfig, cache_file: str) -> dict:
+    """devreq: ContainerDevices of this container; gpus: uuid -> smi.GPUInfo."""
+    env = {}
+    rocr = []
+    masks = []
+    shared = False
+    for i, d in enumerate(devreq):
+        g = gpus.get(d.uuid)
+        rocr.append(g.rocr_id if g else d.uuid)
+        env[f"HIP_DEVICE_MEMORY_LIMIT_{i}"] = f"{d.usedmem}m"
+        total_cus = g.cus if g else 256
+        ranges = (d.custominfo or {}).get("cu_ranges")
+        if ranges and ranges_count(ranges) < total_cus:
+            masks.append(f"{i}:{format_ranges(ranges)}")
+            shared = True
+        if g and d.usedmem < int(g.memory_mib * cfg.device_memory_scaling):
+            shared = True
+        if 0 < d.usedcores < total_cus or d.usedcores == 0:
+            shared = True
+    env["ROCR_VISIBLE_DEVICES"] = ",".join(rocr)
+    if masks:
+        env["HSA_CU_MASK"] = ";".join(masks)
+    if devreq:
+        g0 = gpus.get(devreq[0].uuid)
+        total0 = g0.cus if g0 else 256
+        pct = 0 if devreq[0].usedcores == 0 else max(1, min(100, round(devreq[0].usedcores * 100 / total0)))
+        env["HIP_DEVICE_CORE_LIMIT"] = str(pct)
+    env["MIVGPU_SHARED_CACHE"] = cache_file
+    env["MIVGPU_DEVICE_UUIDS"] = ",".join(d.uuid for d in devreq)
+    if cfg.device_memory_scaling > 1:
+        env["MIVGPU_OVERSUBSCRIBE"] = "true"
+    if cfg.log_level:
+        env["MIVGPU_LOG_LEVEL"] = str(cfg.log_level)
+    if cfg.disable_core_limit:
+        env["GPU_CORE_UTILIZATION_POLICY"] = "disable"
+    if shared and cfg.hw_queues_shared:
+        env["GPU_MAX_HW_QUEUES"] = str(cfg.hw_queues_shared)
+    return env
+
+
+def allocate_container(pod: dict, ctr: dict, devreq: list, gpus: dict, cfg: PluginConfig,
+                       make_dirs: bool = True) -> dict:
+    """-> {"envs": {...}, "mounts": [...], "devices": [...]} for one container."""
+    hook = cfg.hook_path
+    cache_file = f"{hook}/vgpu/{_uuid.uuid4()}.cache"
+    envs = container_env(devreq, gpus, cfg, cache_file)
+    uid = (pod.get("metadata") or {}).get("uid", "")
+    host_dir = f"{hook}/vgpu/containers/{uid}_{ctr.get('name', '')}"
+    if make_dirs:
+        import shutil
+        shutil.rmtree(host_dir, ignore_errors=True)
+        for d in (host_dir, "/tmp/vgpulock"):
+            os.makedirs(d, exist_ok=True)
+            try:
+                os.chmod(d, 0o777)
+            except OSError:
+                pass
+    mounts = [
+        {"container_path": CONTAINER_LIB, "host_path": f"{hook}/vgpu/libmivgpu.so", "read_only": True},
+        {"container_path": f"{hook}/vgpu", "host_path": host_dir, "read_only": False},
+        {"container_path": "/tmp/vgpulock", "host_path": "/tmp/vgpulock", "read_only": False},
+    ]
+    disabled = any(e.get("name") == "MIVGPU_DISABLE_CONTROL" and _truthy(e.get("value", ""))
+                   for e in ctr.get("env") or [])
+    if not disabled:
+        mounts.append({"container_path": "/etc/ld.so.preload", "host_path": f"{hook}/vgpu/ld.so.preload",
+                       "read_only": True})
+    devices = []
+    if cfg.pass_device_specs:
+        devices.append({"container_path": "/dev/kfd", "host_path": "/dev/kfd", "permissions": "rw"})
+        for d in devreq:
+            g = gpus.get(d.uuid)
+            if g is None:
+                continue
+            if g.render_minor >= 0:
+                p = f"/dev/dri/renderD{g.render_minor}"
+                devices.append({"container_path": p, "host_path": p, "permissions": "rw"})
+            if g.card_minor >= 0:
+                p = f"/dev/dri/card{g.card_minor}"
+                devices.append({"container_path": p, "host_path": p, "permissions": "rw"})
+    return {"envs": envs, "mounts": mounts, "devices": devices}
+
+
+def ld_so_preload_contents() -> str:
+    return CONTAINER_LIB + "\n"

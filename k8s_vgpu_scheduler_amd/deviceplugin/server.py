@@ -1,0 +1,322 @@
+"""AMD (MI355X) kubelet device plugin: ListAndWatch / GetPreferredAllocation / Allocate.
+
+Reference: pkg/device-plugin/nvidiadevice/nvinternal/plugin/server.go:93-1014
+and util.go:94-414.  Protocol kept:
+  * the plugin advertises ``split`` replicas per GPU (``<uuid>::<n>``) under
+    ``amd.com/gpu`` (optionally with NUMA topology hints);
+  * ``Allocate`` is serialised node-wide; the pod is found through the node lock
+    / bind-phase annotations (``util.get_pending_pod``); the scheduler's
+    decision is decoded from ``hami.io/amd-devices-to-allocate`` (+ CU ranges),
+    the next non-empty container entry is popped (init containers first), the
+    env/mounts/device nodes are built (:mod:`.allocate`), the popped entries
+    are erased from the annotation, and when no AMD entries remain the pod is
+    marked ``bind-phase=success`` and the node lock released; any failure marks
+    ``failed`` and releases the lock;
+  * ``GetPreferredAllocation`` maps the annotated physical GPUs onto replica ids.
+``pod_allocation_try_success`` / ``pod_allocation_failed`` / ``get_pending_pod``
+are module-level so tests can swap them (server.go:84, util.go:371-407).
+"""
+
+from __future__ import annotations
+
+import logging
+import os
+import threading
+import time
+from concurrent import futures
+
+from k8s_vgpu_scheduler_amd.device import codec
+from k8s_vgpu_scheduler_amd.device.amd.device import AMD_DEVICE, CU_RANGES_ANNOS, IN_REQUEST_ANNOS, NODE_LOCK_AMD
+from k8s_vgpu_scheduler_amd.k8s.client import containers, get_client, init_containers
+from k8s_vgpu_scheduler_amd.smi import Backend, GPUInfo
+from k8s_vgpu_scheduler_amd.utils import nodelock, util
+from k8s_vgpu_scheduler_amd.utils import types as T
+
+from . import api
+from .allocate import PluginConfig, allocate_container
+from .register import filtered
+
+log = logging.getLogger(__name__)
+
+REPLICA_SEP = "::"
+
+
+def physical_id(replica_id: str) -> str:
+    return replica_id.split(REPLICA_SEP, 1)[0]
+
+
+# ----------------------------------------------------- swappable test seams
+def get_pending_pod(node_name: str) -> dict:
+    return util.get_pending_pod(node_name)
+
+
+def _update_phase_and_release(node_name: str, pod: dict, phase: str):
+    try:
+        util.patch_pod_annotations(pod, {T.DEVICE_BIND_PHASE: phase})
+    except Exception as e:  # noqa: BLE001
+        log.error("failed to patch bind-phase=%s on %s: %s", phase, pod["metadata"]["name"], e)
+    try:
+        nodelock.release_node_lock(node_name, NODE_LOCK_AMD, pod)
+    except Exception as e:  # noqa: BLE001
+        log.error("failed to release node lock on %s: %s", node_name, e)
+
+
+def pod_allocation_try_success(node_name: str, pod: dict):
+    """Release the lock only once every device type of the pod is allocated."""
+    md = pod["metadata"]
+    fresh = get_client().get_pod(md.get("namespace", "default"), md["name"])
+    remaining = ((fresh.get("metadata") or {}).get("annotations") or {}).get(IN_REQUEST_ANNOS, "")
+    if any(d for ctr in codec.decode_pod_devices({AMD_DEVICE: IN_REQUEST_ANNOS},
+                                                 {IN_REQUEST_ANNOS: remaining}).get(AMD_DEVICE, []) for d in ctr):
+        return False
+    _update_phase_and_release(node_name, fresh, T.DEVICE_BIND_SUCCESS)
+    return True
+
+
+def pod_allocation_failed(node_name: str, pod: dict):
+    _update_phase_and_release(node_name, pod, T.DEVICE_BIND_FAILED)
+
+
+def decode_pod_single_device(pod: dict) -> list:
+    annos = (pod.get("metadata") or {}).get("annotations") or {}
+    pd = codec.decode_pod_devices({AMD_DEVICE: IN_REQUEST_ANNOS}, annos).get(AMD_DEVICE)
+    if pd is None:
+        raise LookupError("device request not found")
+    return codec.attach_cu_ranges(pd, annos.get(CU_RANGES_ANNOS))
+
+
+def pop_next_container_devices(pod: dict, single: list):
+    """Pop the first non-empty container entry (init containers first)."""
+    n_init = len(init_containers(pod))
+    for i, ctr in enumerate(single):
+        if ctr:
+            single[i] = []
+            if i < n_init:
+                return init_containers(pod)[i], ctr
+            j = i - n_init
+            if j >= len(containers(pod)):
+                raise LookupError(f"container index {i} out of range (init={n_init}, regular={len(containers(pod))})")
+            return containers(pod)[j], ctr
+    raise LookupError("no pending device allocation found")
+
+
+def patch_erased_annotation(pod: dict, single: list):
+    enc = codec.encode_pod_single_device(single)
+    util.patch_pod_annotations(pod, {IN_REQUEST_ANNOS: enc})
+    pod["metadata"].setdefault("annotations", {})[IN_REQUEST_ANNOS] = enc
+
+
+class AllocationError(Exception):
+    pass
+
+
+# --------------------------------------------------------------------- plugin
+class AMDDevicePlugin:
+    def __init__(self, backend: Backend, cfg: PluginConfig, node_name: str,
+                 socket_dir: str = api.DEVICE_PLUGIN_PATH, socket_name: str = "mivgpu-amd.sock"):
+        self.backend, self.cfg, self.node = backend, cfg, node_name
+        self.gpus: list[GPUInfo] = filtered(backend.gpus(), cfg)
+        self.by_uuid = {g.uuid: g for g in self.gpus}
+        self.health = {g.uuid: True for g in self.gpus}
+        self._cv = threading.Condition()
+        self._gen = 0
+        self.apply_mutex = threading.Lock()
+        self.socket = os.path.join(socket_dir, socket_name)
+        self.server = None
+        self._stop = threading.Event()
+
+    # ----------------------------------------------------------- devices
+    def kubelet_devices(self) -> list:
+        out = []
+        for g in self.gpus:
+            state = api.HEALTHY if self.health.get(g.uuid, True) else api.UNHEALTHY
+            for i in range(self.cfg.device_split_count):
+                d = api.Device(ID=f"{g.uuid}{REPLICA_SEP}{i}", health=state)
+                if self.cfg.enable_numa_topology:
+                    d.topology.nodes.add(ID=g.numa)
+                out.append(d)
+        return out
+
+    def set_health(self, uuid: str, healthy: bool):
+        with self._cv:
+            if self.health.get(uuid) != healthy:
+                self.health[uuid] = healthy
+                self._gen += 1
+                self._cv.notify_all()
+
+    def health_loop(self, period: float = 5.0):
+        disabled = os.environ.get("DP_DISABLE_HEALTHCHECKS", "") in ("all", "*")
+        while not self._stop.wait(period):
+            if disabled:
+                continue
+            for g in self.gpus:
+                ok, why = self.backend.health(g)
+                if not ok and self.health.get(g.uuid, True):
+                    log.error("GPU %s unhealthy: %s", g.uuid, why)
+                self.set_health(g.uuid, ok)
+
+    # ----------------------------------------------------------- gRPC API
+    def GetDevicePluginOptions(self, request, context):  # noqa: N802
+        return api.DevicePluginOptions(pre_start_required=False,
+                                       get_preferred_allocation_available=self.cfg.enable_preferred_allocation)
+
+    def ListAndWatch(self, request, context):  # noqa: N802
+        gen = -1
+        while not self._stop.is_set():
+            with self._cv:
+                if gen == self._gen:
+                    self._cv.wait(timeout=1.0)
+                if gen == self._gen:
+                    if context is not None and not context.is_active():
+                        return
+                    continue
+                gen = self._gen
+            yield api.ListAndWatchResponse(devices=self.kubelet_devices())
+
+    def GetPreferredAllocation(self, request, context):  # noqa: N802
+        resp = api.PreferredAllocationResponse()
+        try:
+            pod = get_pending_pod(self.node)
+            single = decode_pod_single_device(pod)
+        except Exception:  # noqa: BLE001 -- no annotation: fall back to kubelet's order
+            pod, single = None, []
+        for creq in request.container_requests:
+            avail = list(creq.available_deviceIDs)
+            chosen = list(creq.must_include_deviceIDs)
+            want = []
+            for ctr in single:
+                if ctr:
+                    want = [d.uuid for d in ctr]
+                    break
+            for u in want:
+                if len(chosen) >= creq.allocation_size:
+                    break
+                for rid in avail:
+                    if rid not in chosen and physical_id(rid) == u and \
+                            all(physical_id(c) != u for c in chosen):
+                        chosen.append(rid)
+                        break
+            for rid in avail:
+                if len(chosen) >= creq.allocation_size:
+                    break
+                if rid not in chosen:
+                    chosen.append(rid)
+            resp.container_responses.add(deviceIDs=chosen[:creq.allocation_size])
+        return resp
+
+    def PreStartContainer(self, request, context):  # noqa: N802
+        return api.PreStartContainerResponse()
+
+    def allocate(self, container_requests: list[list[str]]) -> list[dict]:
+        """Core of Allocate; returns per-container dicts (envs/mounts/devices)."""
+        with self.apply_mutex:
+            pod = get_pending_pod(self.node)
+            try:
+                single = decode_pod_single_device(pod)
+            except Exception as e:
+                pod_allocation_failed(self.node, pod)
+                raise AllocationError(str(e)) from e
+            out = []
+            try:
+                for ids in container_requests:
+                    ctr, devreq = pop_next_container_devices(pod, single)
+                    if len(devreq) != len(ids):
+                        raise AllocationError("device number not matched")
+                    for d in devreq:
+                        if d.uuid not in self.by_uuid:
+                            raise AllocationError(f"allocated GPU {d.uuid} is not managed by this node")
+                        if not self.health.get(d.uuid, True):
+                            raise AllocationError(f"allocated GPU {d.uuid} is unhealthy")
+                    out.append(allocate_container(pod, ctr, devreq, self.by_uuid, self.cfg,
+                                                  make_dirs=not os.environ.get("MIVGPU_DP_DRY_RUN")))
+                patch_erased_annotation(pod, single)
+            except Exception:
+                pod_allocation_failed(self.node, pod)
+                raise
+            pod_allocation_try_success(self.node, pod)
+            return out
+
+    def Allocate(self, request, context):  # noqa: N802
+        import grpc
+
+        try:
+            res = self.allocate([list(r.devices_ids) for r in request.container_requests])
+        except Exception as e:  # noqa: BLE001
+            log.error("Allocate failed: %s", e)
+            if context is not None:
+                context.abort(grpc.StatusCode.UNKNOWN, str(e))
+            raise
+        resp = api.AllocateResponse()
+        for r in res:
+            c = resp.container_responses.add()
+            for k, v in r["envs"].items():
+                c.envs[k] = v
+            for m in r["mounts"]:
+                c.mounts.add(**m)
+            for d in r["devices"]:
+                c.devices.add(**d)
+        return resp
+
+    # --------------------------------------------------------- serve/register
+    def serve(self, max_workers: int = 8):
+        import grpc
+
+        try:
+            os.unlink(self.socket)
+        except FileNotFoundError:
+            pass
+        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers))
+        api.add_device_plugin_servicer(self.server, self)
+        self.server.add_insecure_port(f"unix://{self.socket}")
+        self.server.start()
+        return self.server
+
+    def register_with_kubelet(self, kubelet_socket: str = api.KUBELET_SOCKET, timeout: float = 10.0):
+        import grpc
+
+        with grpc.insecure_channel(f"unix://{kubelet_socket}") as ch:
+            grpc.channel_ready_future(ch).result(timeout=timeout)
+            api.RegistrationStub(ch).Register(api.RegisterRequest(
+                version=api.VERSION, endpoint=os.path.basename(self.socket), resource_name=self.cfg.resource_name,
+                options=api.DevicePluginOptions(
+                    get_preferred_allocation_available=self.cfg.enable_preferred_allocation)), timeout=timeout)
+
+    def start(self, kubelet_socket: str = api.KUBELET_SOCKET, register: bool = True):
+        self.serve()
+        if register:
+            self.register_with_kubelet(kubelet_socket)
+        threading.Thread(target=self.health_loop, name="health", daemon=True).start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+        with self._cv:
+            self._cv.notify_all()
+        if self.server is not None:
+            self.server.stop(grace=1)
+
+
+def run_with_restarts(make_plugin, kubelet_socket: str, max_restarts: int = 5, window_s: float = 3600.0,
+                      stop: threading.Event | None = None):
+    """server.go:518-566: restart a crashed plugin; >max_restarts within the window is fatal."""
+    stop = stop or threading.Event()
+    restarts: list[float] = []
+    while not stop.is_set():
+        plugin = make_plugin()
+        try:
+            plugin.start(kubelet_socket)
+            while not stop.wait(5.0):
+                if not os.path.exists(plugin.socket):
+                    raise RuntimeError("plugin socket disappeared (kubelet restarted?)")
+                if not os.path.exists(kubelet_socket):
+                    raise RuntimeError("kubelet socket disappeared")
+        except Exception as e:  # noqa: BLE001
+            log.error("device plugin crashed: %s", e)
+            now = time.time()
+            restarts = [t for t in restarts if now - t < window_s] + [now]
+            if len(restarts) > max_restarts:
+                raise RuntimeError(f"device plugin restarted more than {max_restarts} times within "
+                                   f"{window_s}s") from e
+            time.sleep(1.0)
+        finally:
+            plugin.stop()

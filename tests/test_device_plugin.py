@@ -1,0 +1,210 @@
+"""Device plugin: registration -> scheduler -> Allocate, end to end on the fake API server.
+
+Mirrors the reference's plugin tests (server_test.go:705-760 with swapped
+getPendingPod / podAllocation* seams, register tests) for AMD/MI355X.
+"""
+
+import os
+import tempfile
+import threading
+import time
+
+import grpc
+import pytest
+
+from k8s_vgpu_scheduler_amd.device import codec
+from k8s_vgpu_scheduler_amd.device.amd.device import (HANDSHAKE_ANNOS, IN_REQUEST_ANNOS, PAIR_SCORE_ANNOS,
+                                                      REGISTER_ANNOS)
+from k8s_vgpu_scheduler_amd.device.quota import get_local_cache
+from k8s_vgpu_scheduler_amd.deviceplugin import api
+from k8s_vgpu_scheduler_amd.deviceplugin import server as S
+from k8s_vgpu_scheduler_amd.deviceplugin.allocate import PluginConfig
+from k8s_vgpu_scheduler_amd.deviceplugin.register import Registrar
+from k8s_vgpu_scheduler_amd.k8s.client import init_global_client
+from k8s_vgpu_scheduler_amd.k8s.fake import FakeCluster, make_node
+from k8s_vgpu_scheduler_amd.scheduler.config import SchedulerConfig, init_devices_with_config
+from k8s_vgpu_scheduler_amd.scheduler.scheduler import Scheduler
+from k8s_vgpu_scheduler_amd.smi import FakeBackend
+from k8s_vgpu_scheduler_amd.testing import amd_container, amd_pod
+from k8s_vgpu_scheduler_amd.utils import types as T
+
+
+@pytest.fixture
+def env(monkeypatch):
+    monkeypatch.setenv("MIVGPU_DP_DRY_RUN", "1")
+    c = FakeCluster()
+    init_global_client(c)
+    init_devices_with_config()
+    get_local_cache().quotas.clear()
+    c.create("nodes", make_node("node1", capacity={"amd.com/gpu": "64"}))
+    backend = FakeBackend(n=8)
+    cfg = PluginConfig(hook_path=tempfile.mkdtemp(), device_split_count=8)
+    Registrar(backend, cfg, "node1").register_once()
+    sched = Scheduler(c, SchedulerConfig())
+    sched.start()
+    sched.register()
+    plugin = S.AMDDevicePlugin(backend, cfg, "node1", socket_dir=tempfile.mkdtemp())
+    return c, sched, plugin, backend
+
+
+def schedule(c, sched, pod):
+    c.create("pods", pod)
+    name = pod["metadata"]["name"]
+    res = sched.filter({"Pod": c.get_pod("default", name), "NodeNames": ["node1"]})
+    assert res["NodeNames"] == ["node1"], res
+    p = c.get_pod("default", name)
+    assert sched.bind({"PodName": name, "PodNamespace": "default", "PodUID": p["metadata"]["uid"],
+                       "Node": "node1"})["Error"] == ""
+    return c.get_pod("default", name)
+
+
+def test_registration_annotations(env):
+    c, sched, plugin, backend = env
+    annos = c.get_node("node1")["metadata"]["annotations"]
+    devs = codec.unmarshal_node_devices(annos[REGISTER_ANNOS])
+    assert len(devs) == 8 and devs[0].devmem == 294912 and devs[0].devcore == 256 and devs[0].count == 8
+    scores = codec.decode_pair_scores(annos[PAIR_SCORE_ANNOS])
+    assert scores["GPU-0000"]["GPU-0001"] == 100
+    # the scheduler's register() already asked again ("Requesting_<time>")
+    assert annos[HANDSHAKE_ANNOS].startswith("Requesting_")
+    assert len(plugin.kubelet_devices()) == 64
+
+
+def test_allocate_fractional_slice(env):
+    c, sched, plugin, backend = env
+    pod = schedule(c, sched, amd_pod("p", mem=36864, cores=25))
+    res = plugin.allocate([["GPU-0007::0"]])
+    e = res[0]["envs"]
+    assert e["HIP_DEVICE_MEMORY_LIMIT_0"] == "36864m"
+    assert e["HSA_CU_MASK"].startswith("0:")
+    assert codec.ranges_count(codec.parse_ranges(e["HSA_CU_MASK"][2:])) == 64
+    assert e["HIP_DEVICE_CORE_LIMIT"] == "25"
+    assert e["GPU_MAX_HW_QUEUES"] == "1"
+    assert e["ROCR_VISIBLE_DEVICES"].startswith("GPU-")
+    paths = {m["container_path"] for m in res[0]["mounts"]}
+    assert "/etc/ld.so.preload" in paths and "/usr/local/vgpu/libmivgpu.so" in paths
+    devs = {d["container_path"] for d in res[0]["devices"]}
+    assert "/dev/kfd" in devs and any(p.startswith("/dev/dri/renderD") for p in devs)
+    p = c.get_pod("default", "p")
+    assert p["metadata"]["annotations"][T.DEVICE_BIND_PHASE] == "success"
+    assert T.NODE_LOCK_KEY not in c.get_node("node1")["metadata"]["annotations"]
+    # the popped entry is erased from the to-allocate annotation
+    assert set(p["metadata"]["annotations"][IN_REQUEST_ANNOS]) <= {";"}
+
+
+def test_allocate_opt_out_skips_preload(env):
+    c, sched, plugin, backend = env
+    ctr = amd_container(mem=1000)
+    ctr["env"] = [{"name": "MIVGPU_DISABLE_CONTROL", "value": "true"}]
+    schedule(c, sched, amd_pod("p", containers=[ctr]))
+    res = plugin.allocate([["x"]])
+    assert "/etc/ld.so.preload" not in {m["container_path"] for m in res[0]["mounts"]}
+
+
+def test_multi_gpu_multi_container_pod(env):
+    c, sched, plugin, backend = env
+    pod = amd_pod("p", containers=[amd_container("a", gpu=2, mem=1000, cores=50), amd_container("b", mem=2000)],
+                  init=[amd_container("init", mem=500)])
+    schedule(c, sched, pod)
+    # kubelet calls Allocate once per container, init first
+    r_init = plugin.allocate([["i"]])
+    assert r_init[0]["envs"]["HIP_DEVICE_MEMORY_LIMIT_0"] == "500m"
+    assert c.get_pod("default", "p")["metadata"]["annotations"][T.DEVICE_BIND_PHASE] == "allocating"
+    r_a = plugin.allocate([["x", "y"]])
+    ea = r_a[0]["envs"]
+    assert len(ea["ROCR_VISIBLE_DEVICES"].split(",")) == 2
+    assert ea["HSA_CU_MASK"].count(";") == 1 and ea["HSA_CU_MASK"].split(";")[1].startswith("1:")
+    r_b = plugin.allocate([["z"]])
+    assert r_b[0]["envs"]["HIP_DEVICE_MEMORY_LIMIT_0"] == "2000m"
+    assert c.get_pod("default", "p")["metadata"]["annotations"][T.DEVICE_BIND_PHASE] == "success"
+
+
+def test_allocate_count_mismatch_marks_failed_and_unlocks(env):
+    c, sched, plugin, backend = env
+    schedule(c, sched, amd_pod("p", mem=1000))
+    with pytest.raises(S.AllocationError):
+        plugin.allocate([["a", "b"]])
+    p = c.get_pod("default", "p")
+    assert p["metadata"]["annotations"][T.DEVICE_BIND_PHASE] == "failed"
+    assert T.NODE_LOCK_KEY not in c.get_node("node1")["metadata"]["annotations"]
+
+
+def test_allocate_without_pending_pod(env):
+    c, sched, plugin, backend = env
+    with pytest.raises(LookupError):
+        plugin.allocate([["a"]])
+
+
+def test_health_change_marks_replicas_unhealthy(env):
+    c, sched, plugin, backend = env
+    backend.unhealthy.add("GPU-0003")
+    ok, _ = backend.health(plugin.gpus[3])
+    plugin.set_health("GPU-0003", ok)
+    bad = [d for d in plugin.kubelet_devices() if d.health == api.UNHEALTHY]
+    assert len(bad) == 8 and all(d.ID.startswith("GPU-0003") for d in bad)
+
+
+def test_preferred_allocation_follows_annotation(env):
+    c, sched, plugin, backend = env
+    schedule(c, sched, amd_pod("p", mem=1000))
+    target = codec.decode_container_devices(
+        c.get_pod("default", "p")["metadata"]["annotations"][IN_REQUEST_ANNOS].split(";")[0])[0].uuid
+    req = api.PreferredAllocationRequest()
+    cr = req.container_requests.add(allocation_size=1)
+    cr.available_deviceIDs.extend([d.ID for d in plugin.kubelet_devices()])
+    resp = plugin.GetPreferredAllocation(req, None)
+    assert S.physical_id(resp.container_responses[0].deviceIDs[0]) == target
+
+
+class _FakeKubelet:
+    def __init__(self):
+        self.requests = []
+
+    def Register(self, request, context):  # noqa: N802
+        self.requests.append(request)
+        return api.Empty()
+
+
+def test_grpc_register_list_and_allocate(env):
+    c, sched, plugin, backend = env
+    from concurrent import futures
+
+    kdir = tempfile.mkdtemp()
+    ksock = os.path.join(kdir, "kubelet.sock")
+    kubelet = _FakeKubelet()
+    ks = grpc.server(futures.ThreadPoolExecutor(max_workers=2))
+    api.add_registration_servicer(ks, kubelet)
+    ks.add_insecure_port(f"unix://{ksock}")
+    ks.start()
+    try:
+        plugin.start(kubelet_socket=ksock)
+        assert kubelet.requests[0].resource_name == "amd.com/gpu"
+        assert kubelet.requests[0].version == "v1beta1"
+        schedule(c, sched, amd_pod("p", mem=4096, cores=50))
+        with grpc.insecure_channel(f"unix://{plugin.socket}") as ch:
+            stub = api.DevicePluginStub(ch)
+            first = next(iter(stub.ListAndWatch(api.Empty(), timeout=5)))
+            assert len(first.devices) == 64
+            opts = stub.GetDevicePluginOptions(api.Empty())
+            assert opts.get_preferred_allocation_available
+            req = api.AllocateRequest()
+            req.container_requests.add(devices_ids=["GPU-0000::0"])
+            resp = stub.Allocate(req, timeout=5)
+            envs = dict(resp.container_responses[0].envs)
+            assert envs["HIP_DEVICE_MEMORY_LIMIT_0"] == "4096m"
+            assert codec.ranges_count(codec.parse_ranges(envs["HSA_CU_MASK"][2:])) == 128
+            # error path surfaces as a gRPC error
+            with pytest.raises(grpc.RpcError):
+                stub.Allocate(req, timeout=5)
+    finally:
+        plugin.stop()
+        ks.stop(0)
+
+
+def test_handshake_cycle(env):
+    """Scheduler writes Requesting_, the registrar answers Reported_."""
+    c, sched, plugin, backend = env
+    from k8s_vgpu_scheduler_amd.utils import util
+    util.patch_node_annotations("node1", {HANDSHAKE_ANNOS: "Requesting_2020-01-01 00:00:00"})
+    Registrar(backend, plugin.cfg, "node1").register_once()
+    assert c.get_node("node1")["metadata"]["annotations"][HANDSHAKE_ANNOS].startswith("Reported_")
