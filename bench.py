@@ -8,7 +8,9 @@ device plugin's environment (libmivgpu.so preloaded, HBM hard limit
 ``--gpumem-mib``, disjoint HSA_CU_MASK CU ranges = ``gpucores`` 100/slices %),
 each decoding a Qwen3-8B-shaped model (random init, synthetic KV context) at
 ``--batch`` sequences.  The same slices are first run natively (no shim, no
-limits, no masks): overhead = 1 - shim / native aggregate tokens/s.
+limits, no masks, same GPU_MAX_HW_QUEUES): overhead = 1 - shim / native
+aggregate tokens/s.  A third round runs natively with HIP's default 4 queues
+per process (naive sharing, what N plain pods get without the device plugin).
 
 ``value`` = whole-job aggregate decode tokens/s of the shim round over all
 GPUs and slices, timed over exactly ``--steps`` hipGraph-replayed decode steps
@@ -56,11 +58,12 @@ def main():
     ap.add_argument("--ctx", type=int, default=1024, help="KV context length at decode start")
     ap.add_argument("--gpumem-mib", type=int, default=36864, help="HBM hard limit per slice")
     ap.add_argument("--model", default="qwen3-8b", choices=["qwen3-8b", "qwen3-tiny"])
-    ap.add_argument("--mode", default="both", choices=["both", "shim", "native"])
+    ap.add_argument("--mode", default="all", choices=["all", "both", "shim", "native"],
+                    help="all = native (same queues) + native (HIP default queues) + shim rounds")
     ap.add_argument("--no-spatial", action="store_true", help="no HSA_CU_MASK (temporal governor)")
     ap.add_argument("--policy", default="default", choices=["default", "force", "disable"])
     ap.add_argument("--out", default=None, help="also write the JSON line here")
-    ap.add_argument("--hw-queues", type=int, default=1,
+    ap.add_argument("--hw-queues", type=int, default=2,
                     help="GPU_MAX_HW_QUEUES per slice in the shim round (0 = HIP default)")
     ap.add_argument("--child-env", action="append", default=[], metavar="K=V",
                     help="extra environment for every slice process (experiments)")
@@ -88,12 +91,25 @@ def main():
             sp.env.update(extra_env)
         return specs
 
-    # Spawn every slice process of both rounds BEFORE this process touches HIP.
+    def native_specs(queues):
+        specs = plan_slices(args.slices, shim=False, gpumem_mib=None)
+        for sp in specs:
+            if queues and args.slices > 1:
+                sp.env["GPU_MAX_HW_QUEUES"] = str(queues)
+        return with_env(specs)
+
+    # Spawn every slice process of every round BEFORE this process touches HIP.
+    # "native" uses the same HW-queue count as the shim round, so the overhead
+    # isolates the cost of the vGPU layer itself (shim + CU masks + limits);
+    # "native_hip_default" is naive sharing with HIP's default queue count.
     rounds = []
-    if args.mode in ("both", "native"):
-        rounds.append(("native", spawn_round(with_env(plan_slices(args.slices, shim=False, gpumem_mib=None)),
-                                             phys, work, log_dir, child_args, "native")))
-    if args.mode in ("both", "shim"):
+    if args.mode in ("all", "both", "native"):
+        rounds.append(("native", spawn_round(native_specs(args.hw_queues), phys, work, log_dir, child_args,
+                                             "native")))
+    if args.mode == "all" and args.slices > 1 and args.hw_queues:
+        rounds.append(("native_hip_default", spawn_round(native_specs(0), phys, work, log_dir, child_args,
+                                                         "native_hip_default")))
+    if args.mode in ("all", "both", "shim"):
         rounds.append(("shim", spawn_round(
             with_env(plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib,
                                  spatial=not args.no_spatial, policy=args.policy,
@@ -164,6 +180,10 @@ def main():
             nat = results["native"]["tok_s"]
             out["native_value"] = round(nat, 2)
             out["isolation_overhead_pct"] = round((1.0 - head["tok_s"] / nat) * 100.0, 2)
+        if "native_hip_default" in results:
+            nd = results["native_hip_default"]["tok_s"]
+            out["native_hip_default_queues_value"] = round(nd, 2)
+            out["speedup_vs_naive_sharing"] = round(head["tok_s"] / nd, 3)
         line = json.dumps(out)
         print(line, flush=True)
         if args.out:

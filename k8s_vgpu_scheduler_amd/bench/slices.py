@@ -45,8 +45,8 @@ class SliceSpec:
     policy: str = "default"
     # HW queues per slice process (GPU_MAX_HW_QUEUES).  HIP's default of 4 per
     # process oversubscribes the hardware scheduler once several tenants share
-    # a GPU (measured: 4 slices 3.1k -> 6.4k tok/s with 1 queue each); the
-    # device plugin injects the same value for fractional pods.
+    # a GPU (measured: 4 slices 4.5k -> 7.6k tok/s with 2 queues each, see
+    # profiles/slice_scaling.md); the device plugin injects the same value.
     hw_queues: int | None = None
     env: dict = field(default_factory=dict)
 
@@ -56,7 +56,7 @@ def cu_mask_string(ranges) -> str:
 
 
 def plan_slices(n: int, shim: bool, gpumem_mib: int | None, spatial: bool = True,
-                policy: str = "default", hw_queues: int | None = 1) -> list[SliceSpec]:
+                policy: str = "default", hw_queues: int | None = 2) -> list[SliceSpec]:
     """Equal split of one GPU into n slices (CUs in contiguous, XCD-sized runs)."""
     specs = []
     per = (MI355X_CUS // n) // MI355X_XCDS * MI355X_XCDS   # whole 8-CU granules: XCD-balanced

@@ -75,7 +75,7 @@ def main(argv=None):
     ap.add_argument("--device-memory-scaling", type=float, default=1.0)
     ap.add_argument("--device-core-scaling", type=float, default=1.0)
     ap.add_argument("--disable-core-limit", action="store_true")
-    ap.add_argument("--hw-queues", type=int, default=1, help="GPU_MAX_HW_QUEUES for shared pods (0 = HIP default)")
+    ap.add_argument("--hw-queues", type=int, default=2, help="GPU_MAX_HW_QUEUES for shared pods (0 = HIP default)")
     ap.add_argument("--hook-path", default=os.environ.get("HOOK_PATH", "/usr/local/vgpu"))
     ap.add_argument("--kubelet-socket", default=api.KUBELET_SOCKET)
     ap.add_argument("--socket-dir", default=api.DEVICE_PLUGIN_PATH)

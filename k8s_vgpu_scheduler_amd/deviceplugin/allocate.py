@@ -9,9 +9,10 @@ docs/develop/amd-vgpu.md:47-104.  MI355X translation:
        HSA_CU_MASK            ``i:ranges;...`` for devices with a CU partition
        HIP_DEVICE_MEMORY_LIMIT_i  ``<MiB>m`` hard limit per local device
        HIP_DEVICE_CORE_LIMIT  CU share in % (first device, for the governor)
-       GPU_MAX_HW_QUEUES      1 for shared (fractional) pods: HIP's default 4
+       GPU_MAX_HW_QUEUES      2 for shared (fractional) pods: HIP's default 4
                               queues/process oversubscribes the HW scheduler
-                              when tenants share a GPU (measured, bench)
+                              when tenants share a GPU (measured, see
+                              profiles/slice_scaling.md)
        MIVGPU_SHARED_CACHE    $HOOK_PATH/vgpu/<uuid4>.cache
        MIVGPU_DEVICE_UUIDS, MIVGPU_OVERSUBSCRIBE, MIVGPU_LOG_LEVEL,
        GPU_CORE_UTILIZATION_POLICY=disable (with --disable-core-limit)
@@ -40,7 +41,7 @@ class PluginConfig:
     device_core_scaling: float = 1.0
     disable_core_limit: bool = False
     log_level: str = ""
-    hw_queues_shared: int = 1
+    hw_queues_shared: int = 2
     pass_device_specs: bool = True
     enable_preferred_allocation: bool = True
     filter_uuids: tuple = ()

@@ -79,7 +79,7 @@ def test_allocate_fractional_slice(env):
     assert e["HSA_CU_MASK"].startswith("0:")
     assert codec.ranges_count(codec.parse_ranges(e["HSA_CU_MASK"][2:])) == 64
     assert e["HIP_DEVICE_CORE_LIMIT"] == "25"
-    assert e["GPU_MAX_HW_QUEUES"] == "1"
+    assert e["GPU_MAX_HW_QUEUES"] == "2"
     assert e["ROCR_VISIBLE_DEVICES"].startswith("GPU-")
     paths = {m["container_path"] for m in res[0]["mounts"]}
     assert "/etc/ld.so.preload" in paths and "/usr/local/vgpu/libmivgpu.so" in paths

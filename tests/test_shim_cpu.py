@@ -1,0 +1,174 @@
+"""libmivgpu.so on the CPU: interposition, quota, virtualisation, shared region.
+
+Runs the real shim against the mock HIP runtime (csrc/mockhip), through a
+driver linked like PyTorch (versioned HIP references), so every hook path is
+exercised natively without a GPU.  The reference tests the equivalent ABI
+from the Go side only (pkg/monitor/nvidia/v1/spec_test.go, cudevshr_test.go).
+"""
+
+import ctypes
+import json
+import os
+import signal
+import subprocess
+import threading
+import time
+
+import pytest
+
+from k8s_vgpu_scheduler_amd.monitor import region as R
+
+
+def run(native_build, tmp_path, *cmds, env=None, cache="c.cache", preload=True, timeout=60):
+    e = dict(os.environ)
+    e.update({"MOCKHIP_TOTAL_MIB": "65536", "MIVGPU_SHARED_CACHE": str(tmp_path / cache)})
+    if preload:
+        e["LD_PRELOAD"] = str(native_build["shim"])
+    e.update(env or {})
+    p = subprocess.run([str(native_build["driver"]), *map(str, cmds)], env=e, stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr
+    return [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+
+
+def test_abi_offsets_match_c_layout(native_build):
+    lib = ctypes.CDLL(str(native_build["shim"]))
+    lib.mivgpu_abi_offsetof.restype = ctypes.c_long
+    py = R.offsets()
+    for fid, off in py.items():
+        assert lib.mivgpu_abi_offsetof(fid) == off, f"field {fid}"
+    assert lib.mivgpu_abi_offsetof(99) == -1
+
+
+def test_parsers(native_build):
+    lib = ctypes.CDLL(str(native_build["shim"]))
+    lib.mivgpu_parse_size.restype = ctypes.c_ulonglong
+    assert lib.mivgpu_parse_size(b"36864m") == 36864 << 20
+    assert lib.mivgpu_parse_size(b"2g") == 2 << 30
+    assert lib.mivgpu_parse_size(b"4096") == 4096
+    f = lib.mivgpu_parse_cu_mask_count
+    assert f(b"0:0-63", 0) == 64
+    assert f(b"0:0-63;1:0-7,64-71", 1) == 16
+    assert f(b"0:0-63;1:0-7", 2) == 0
+
+
+def test_no_preload_is_native(native_build, tmp_path):
+    out = run(native_build, tmp_path, "alloc", 1000, "meminfo", preload=False)
+    assert out[0]["rc"] == 0 and out[1]["total_mib"] == 65536
+
+
+def test_hard_limit_and_virtual_meminfo(native_build, tmp_path):
+    out = run(native_build, tmp_path, "alloc", 30000, "meminfo", "alloc", 7000, "alloc", 6000, "props",
+              env={"HIP_DEVICE_MEMORY_LIMIT_0": "36864m"})
+    assert out[0]["rc"] == 0
+    assert out[1]["total_mib"] == 36864 and out[1]["free_mib"] == 6864
+    assert out[2]["rc"] == 2          # hipErrorOutOfMemory: would exceed the slice
+    assert out[3]["rc"] == 0
+    assert out[4]["total_mib"] == 36864 and out[4]["devtotal_mib"] == 36864
+
+
+def test_global_limit_env_and_free_restores(native_build, tmp_path):
+    out = run(native_build, tmp_path, "alloc", 800, "freeall", "alloc", 900, "usage",
+              env={"HIP_DEVICE_MEMORY_LIMIT": "1g"})
+    assert out[0]["rc"] == 0 and out[2]["rc"] == 0
+    assert out[3]["bytes"] == 900 << 20
+
+
+def test_vmm_and_async_paths_are_accounted(native_build, tmp_path):
+    out = run(native_build, tmp_path, "vmm", 500, "allocasync", 400, "usage", "vmm", 200, "freeall", "usage",
+              env={"HIP_DEVICE_MEMORY_LIMIT_0": "1000m"})
+    assert out[0]["rc"] == 0 and out[1]["rc"] == 0
+    assert out[2]["bytes"] == 900 << 20
+    assert out[3]["rc"] == 2
+    assert out[5]["bytes"] == 0
+
+
+def test_limit_is_shared_by_processes_of_a_container(native_build, tmp_path):
+    env = {"HIP_DEVICE_MEMORY_LIMIT_0": "1000m"}
+    e = dict(os.environ, MOCKHIP_TOTAL_MIB="65536", MIVGPU_SHARED_CACHE=str(tmp_path / "s.cache"),
+             LD_PRELOAD=str(native_build["shim"]), **env)
+    holder = subprocess.Popen([str(native_build["driver"]), "alloc", "700", "sleep", "3000"], env=e,
+                              stdout=subprocess.PIPE, text=True)
+    assert json.loads(holder.stdout.readline())["rc"] == 0
+    out = run(native_build, tmp_path, "alloc", 400, "alloc", 300, "meminfo", env=env, cache="s.cache")
+    assert out[0]["rc"] == 2 and out[1]["rc"] == 0 and out[2]["free_mib"] == 0
+    holder.wait(timeout=30)
+
+
+def test_dead_process_quota_is_reclaimed(native_build, tmp_path):
+    env = {"HIP_DEVICE_MEMORY_LIMIT_0": "1000m"}
+    e = dict(os.environ, MOCKHIP_TOTAL_MIB="65536", MIVGPU_SHARED_CACHE=str(tmp_path / "d.cache"),
+             LD_PRELOAD=str(native_build["shim"]), **env)
+    p = subprocess.Popen([str(native_build["driver"]), "alloc", "900", "sleep", "60000"], env=e,
+                         stdout=subprocess.PIPE, text=True)
+    assert json.loads(p.stdout.readline())["rc"] == 0
+    p.send_signal(signal.SIGKILL)   # no atexit: the slot stays behind
+    p.wait()
+    reg = R.SharedRegion(str(tmp_path / "d.cache"))
+    assert reg.dev_used(0) == 900 << 20
+    reg.close()
+    out = run(native_build, tmp_path, "alloc", 500, env=env, cache="d.cache")
+    assert out[0]["rc"] == 0
+
+
+def test_region_contents_visible_to_monitor(native_build, tmp_path):
+    e = dict(os.environ, MOCKHIP_TOTAL_MIB="65536", MIVGPU_SHARED_CACHE=str(tmp_path / "m.cache"),
+             LD_PRELOAD=str(native_build["shim"]), HIP_DEVICE_MEMORY_LIMIT_0="2g", HIP_DEVICE_CORE_LIMIT="25",
+             HSA_CU_MASK="0:0-63", HIP_TASK_PRIORITY="1", MIVGPU_DEVICE_UUIDS="GPU-abc")
+    p = subprocess.Popen([str(native_build["driver"]), "alloc", "300", "launch", "5", "sleep", "3000"], env=e,
+                         stdout=subprocess.PIPE, text=True)
+    json.loads(p.stdout.readline())
+    json.loads(p.stdout.readline())
+    reg = R.SharedRegion(str(tmp_path / "m.cache"))
+    assert reg.uuid(0) == "GPU-abc"
+    assert reg.memory_total(0) == 300 << 20
+    assert reg.memory_limit(0) == 2 << 30
+    assert reg.r.cu_limit[0] == 25 and reg.r.cu_mask_count[0] == 64
+    assert reg.priority() == 1
+    assert reg.recent_kernel() == 2       # set by the launch hook
+    assert reg.pids() == [p.pid]
+    reg.close()
+    p.wait(timeout=30)
+    reg = R.SharedRegion(str(tmp_path / "m.cache"))
+    assert reg.active_procs() == [] and reg.dev_used(0) == 0   # atexit released the slot
+    reg.close()
+
+
+def test_priority_block_parks_launches(native_build, tmp_path):
+    path = tmp_path / "b.cache"
+    R.SharedRegion.create(str(path)).close()
+    reg = R.SharedRegion(str(path))
+    reg.set_recent_kernel(-1)
+
+    def release():
+        time.sleep(0.6)
+        reg.set_recent_kernel(0)
+    threading.Thread(target=release).start()
+    t0 = time.time()
+    out = run(native_build, tmp_path, "launch", 3, cache="b.cache")
+    dt = time.time() - t0
+    assert out[0]["real_seen"] == 3 and dt >= 0.5
+    reg.close()
+
+
+def test_disable_control_env(native_build, tmp_path):
+    out = run(native_build, tmp_path, "alloc", 3000, "meminfo",
+              env={"HIP_DEVICE_MEMORY_LIMIT_0": "1000m", "MIVGPU_DISABLE_CONTROL": "true"})
+    assert out[0]["rc"] == 0 and out[1]["total_mib"] == 65536
+
+
+def test_oversubscribe_spills_to_host(native_build, tmp_path):
+    out = run(native_build, tmp_path, "alloc", 800, "alloc", 800, "usage", "freeall",
+              env={"HIP_DEVICE_MEMORY_LIMIT_0": "1000m", "MIVGPU_OVERSUBSCRIBE": "true"})
+    assert out[0]["rc"] == 0 and out[1]["rc"] == 0     # second one lands in host memory
+    assert out[2]["bytes"] == 800 << 20                 # only HBM use is charged
+    assert out[3]["errors"] == 0
+
+
+def test_multi_device_limits(native_build, tmp_path):
+    out = run(native_build, tmp_path, "device", 1, "alloc", 600, "meminfo", "device", 0, "alloc", 600,
+              env={"MOCKHIP_DEVICES": "2", "HIP_DEVICE_MEMORY_LIMIT_0": "1000m",
+                   "HIP_DEVICE_MEMORY_LIMIT_1": "500m"})
+    assert out[0]["rc"] == 0
+    assert out[1]["rc"] == 2 and out[2]["total_mib"] == 500
+    assert out[4]["rc"] == 0
