@@ -46,6 +46,8 @@ def child_matmul(args) -> dict:
         try:
             x = torch.empty(args.oom_probe_mib << 20, dtype=torch.uint8, device=dev)
             out["oom_probe"] = "allocated"
+            if args.hold_s:
+                time.sleep(args.hold_s)   # keep it resident while a sibling probes
             del x
         except torch.OutOfMemoryError:
             out["oom_probe"] = "oom"
@@ -108,6 +110,27 @@ def child_hwid(args) -> dict:
             "xccs": sorted({p[0] for p in places}), "places": places[:512]}
 
 
+def child_region(args) -> dict:
+    """Allocate through PyTorch under the shim and read the accounting back
+    through the monitor's shared-region reader (what vGPUmonitor sees)."""
+    import torch
+
+    from k8s_vgpu_scheduler_amd.monitor.region import SharedRegion
+
+    x = torch.empty(args.oom_probe_mib << 20, dtype=torch.uint8, device="cuda")
+    x.fill_(1)
+    torch.cuda.synchronize()
+    reg = SharedRegion(os.environ["MIVGPU_SHARED_CACHE"], writable=False)
+    me = [p for p in reg.active_procs() if p.pid == os.getpid()]
+    out = {"mode": "region", "dev_used_mib": reg.dev_used(0) >> 20, "limit_mib": reg.memory_limit(0) >> 20,
+           "procs": len(list(reg.active_procs())), "self_found": bool(me),
+           "self_buffer_mib": (me[0].used[0].buffer >> 20) if me else -1,
+           "launches": reg.launches(0), "uuid": reg.uuid(0)}
+    reg.close()
+    del x
+    return out
+
+
 def run_child(mode: str, env_extra: dict, shim: bool, extra_args=(), timeout=300) -> dict:
     env = dict(os.environ)
     if shim:
@@ -159,12 +182,14 @@ def main():
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--oom-probe-mib", type=int, default=0)
+    ap.add_argument("--hold-s", type=float, default=0.0)
     ap.add_argument("--out", default=None)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--hwid", action="store_true")
     args = ap.parse_args()
     if args.child:
-        fn = {"matmul": child_matmul, "stream": child_stream, "hwid": child_hwid}[args.child]
+        fn = {"matmul": child_matmul, "stream": child_stream, "hwid": child_hwid,
+              "region": child_region}[args.child]
         print(json.dumps(fn(args)), flush=True)
         return
     tmp = Path(os.environ.get("TMPDIR", "/tmp")) / f"mivgpu-probe-{os.getpid()}"
