@@ -23,9 +23,11 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--gemm", default="auto", choices=["auto", "skinny", "hipblaslt"])
     a = ap.parse_args()
     cfg = QWEN3_8B if a.model == "qwen3-8b" else QWEN3_TINY
-    dec = Qwen3Decoder(cfg, batch=a.batch, max_ctx=a.ctx + a.steps + a.warmup + 16)
+    skinny = {"auto": None, "skinny": True, "hipblaslt": False}[a.gemm]
+    dec = Qwen3Decoder(cfg, batch=a.batch, max_ctx=a.ctx + a.steps + a.warmup + 16, skinny=skinny)
     dec.fill_context(a.ctx)
     if not a.no_graph:
         dec.capture(warmup=1)
@@ -39,7 +41,7 @@ def main():
     dt = time.perf_counter() - t0
     weight_bytes = cfg.param_count() * 2
     kv_bytes = 2 * cfg.layers * a.batch * cfg.kv_heads * (a.ctx + a.warmup + a.steps // 2) * cfg.head_dim * 2
-    print(json.dumps({"batch": a.batch, "ctx": a.ctx, "ms_per_step": dt / a.steps * 1e3,
+    print(json.dumps({"batch": a.batch, "ctx": a.ctx, "skinny_gemm": dec.skinny, "ms_per_step": dt / a.steps * 1e3,
                       "tok_s": a.batch * a.steps / dt,
                       "hbm_gbps_lower_bound": (weight_bytes + kv_bytes) * a.steps / dt / 1e9}))
 

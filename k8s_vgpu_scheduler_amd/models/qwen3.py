@@ -5,7 +5,11 @@ The reference's only benchmark is vLLM serving Qwen3-8B bf16 at TP=1
 slice vs. natively.  This module is the MI355X-native stand-in for that
 workload: a Qwen3-8B-shaped decoder (GQA 32q/8kv x 128, per-head QK RMSNorm,
 NeoX RoPE theta 1e6, SwiGLU 12288, vocab 151936) whose decode step runs
-  * GEMMs on hipBLASLt (``F.linear``, the "plain library GEMM" path),
+  * the weight-streaming projections (gate_up with SiLU*up fused into its
+    epilogue, down, lm_head) on the hand-written skinny MFMA GEMM
+    (csrc/ops/skinny_gemm.hip) over fragment-packed weights, for batch <= 32;
+  * qkv / o_proj on hipBLASLt (``F.linear``), where the library is as fast at
+    these 33-50 MB shapes (profiles/gemm);
   * every other op on the hand-written gfx950 kernels of libmivgpu_ops.so,
   * the whole step captured in one hipGraph (launch overhead -> one replay).
 No network: weights are random normal(0, 0.02) of the exact architecture.
@@ -92,7 +96,7 @@ class Qwen3Decoder:
     """
 
     def __init__(self, cfg: Qwen3Config, batch: int, max_ctx: int, device="cuda",
-                 native: bool | None = None, seed: int = 0):
+                 native: bool | None = None, seed: int = 0, skinny: bool | None = None):
         self.cfg = cfg
         self.B = batch
         self.T = max_ctx
@@ -101,6 +105,17 @@ class Qwen3Decoder:
         if self.native:
             ops.require_native()
         self.w = Qwen3Weights(cfg, self.device, seed=seed)
+        shapes_ok = cfg.hidden % 64 == 0 and cfg.intermediate % 64 == 0 and cfg.vocab % 64 == 0
+        self.skinny = (self.native and batch <= 32 and shapes_ok) if skinny is None else skinny
+        if self.skinny:
+            # Keep only the packed copies (no duplicate 16 GB of weights).
+            for lw in self.w.layers:
+                lw["pgu"] = ops.PackedLinear(lw.pop("wgu"), silu_mul=True)
+                lw["pd"] = ops.PackedLinear(lw.pop("wd"))
+            self.p_lm = ops.PackedLinear(self.w.lm_head)
+            if not cfg.tie_embeddings:
+                self.w.lm_head = None
+            torch.cuda.empty_cache()
         dt = torch.bfloat16
         kvshape = (batch, cfg.kv_heads, max_ctx, cfg.head_dim)
         self.k_cache = [torch.zeros(kvshape, dtype=dt, device=self.device) for _ in range(cfg.layers)]
@@ -116,6 +131,8 @@ class Qwen3Decoder:
         self.q = torch.zeros(batch, cfg.heads, cfg.head_dim, dtype=dt, device=self.device)
         self.attn = torch.zeros(batch, cfg.heads * cfg.head_dim, dtype=dt, device=self.device)
         self.act = torch.zeros(batch, cfg.intermediate, dtype=dt, device=self.device)
+        self.mlp_out = torch.zeros(batch, h, dtype=dt, device=self.device)
+        self.logits = torch.zeros(batch, cfg.vocab, dtype=dt, device=self.device)
         self.o_part = torch.zeros(batch * cfg.heads * self.nsplit * cfg.head_dim, dtype=torch.float32,
                                   device=self.device)
         self.ml_part = torch.zeros(batch * cfg.heads * self.nsplit * 2, dtype=torch.float32,
@@ -167,18 +184,22 @@ class Qwen3Decoder:
                 ops.add_rmsnorm(o, self.res, lw["ln2"], cfg.eps, out=self.h)
             else:
                 self.h.copy_(ref.add_rmsnorm(o, self.res, lw["ln2"], cfg.eps))
-            gu = F.linear(self.h, lw["wgu"])
-            if self.native:
-                ops.silu_mul(gu, out=self.act)
+            if self.skinny:
+                lw["pgu"](self.h, out=self.act)          # gate_up GEMM + SiLU*up epilogue
+                d = lw["pd"](self.act, out=self.mlp_out)
             else:
-                self.act.copy_(ref.silu_mul(gu))
-            d = F.linear(self.act, lw["wd"])
+                gu = F.linear(self.h, lw["wgu"])
+                if self.native:
+                    ops.silu_mul(gu, out=self.act)
+                else:
+                    self.act.copy_(ref.silu_mul(gu))
+                d = F.linear(self.act, lw["wd"])
             nxt = w.layers[li + 1]["ln1"] if li + 1 < L else w.final_norm
             if self.native:
                 ops.add_rmsnorm(d, self.res, nxt, cfg.eps, out=self.h)
             else:
                 self.h.copy_(ref.add_rmsnorm(d, self.res, nxt, cfg.eps))
-        logits = F.linear(self.h, w.lm_head)
+        logits = self.p_lm(self.h, out=self.logits) if self.skinny else F.linear(self.h, w.lm_head)
         self.tokens.copy_(torch.argmax(logits, dim=-1))
         self.pos.add_(1)
         self.seqlens.add_(1)

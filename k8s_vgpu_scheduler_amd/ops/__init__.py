@@ -41,9 +41,14 @@ def lib():
         L.mivgpu_decode_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, f, vp]
         L.mivgpu_silu_mul.argtypes = [vp, vp, i, i, vp]
         L.mivgpu_hwid_probe.argtypes = [vp, i, vp]
+        L.mivgpu_pack_weight.argtypes = [vp, vp, i, i, vp]
+        L.mivgpu_skinny_gemm.argtypes = [vp, vp, vp, i, i, i, i, i, i, i, i, i, vp, vp, vp]
+        ip, lp = ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_longlong)
+        L.mivgpu_skinny_plan.argtypes = [i, i, i, i, ip, ip, ip, lp, ip]
         for fn in ("mivgpu_rmsnorm", "mivgpu_add_rmsnorm", "mivgpu_qk_norm_rope_kv",
                    "mivgpu_decode_attention", "mivgpu_silu_mul", "mivgpu_ops_attn_split",
-                   "mivgpu_hwid_probe"):
+                   "mivgpu_hwid_probe", "mivgpu_pack_weight", "mivgpu_skinny_gemm",
+                   "mivgpu_skinny_max_m", "mivgpu_skinny_plan"):
             getattr(L, fn).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -131,3 +136,83 @@ def hwid_probe(blocks: int = 4096) -> torch.Tensor:
     _check(lib().mivgpu_hwid_probe(_p(out), blocks, _stream()), "hwid_probe")
     torch.cuda.synchronize()
     return out.view(blocks, 2).cpu()
+
+
+# ------------------------------------------------------------ skinny GEMM --
+EPI_STORE, EPI_SILU_MUL = 0, 1
+
+
+def skinny_max_m() -> int:
+    return int(lib().mivgpu_skinny_max_m())
+
+
+def pack_weight(w: torch.Tensor) -> torch.Tensor:
+    """W[N, K] bf16 -> MFMA-fragment-packed copy (same byte size, flat bf16)."""
+    N, K = w.shape
+    if w.dtype != torch.bfloat16 or N % 32 or K % 64:
+        raise ValueError(f"pack_weight needs bf16 [N%32, K%64], got {tuple(w.shape)} {w.dtype}")
+    w = w.contiguous()
+    out = torch.empty(N * K, dtype=torch.bfloat16, device=w.device)
+    _check(lib().mivgpu_pack_weight(_p(w), _p(out), N, K, _stream()), "pack_weight")
+    return out
+
+
+def interleave_gate_up(w_gu: torch.Tensor) -> torch.Tensor:
+    """[2I, K] (gate rows then up rows) -> rows ordered gate[0:32], up[0:32], gate[32:64], ...
+    so n-tile pair (2c, 2c+1) of the packed weight is (gate, up) of channel block c."""
+    two_i, K = w_gu.shape
+    inter = two_i // 2
+    return w_gu.view(2, inter // 32, 32, K).transpose(0, 1).reshape(two_i, K)
+
+
+def skinny_plan(M: int, K: int, N: int, epi: int, nt: int = 0, ks: int = 0, S: int = 0) -> dict:
+    """Launch plan the kernel will use (0 = auto) and the scratch it needs."""
+    c = ctypes
+    v_nt, v_ks, v_s, v_t = c.c_int(nt), c.c_int(ks), c.c_int(S), c.c_int(0)
+    v_f = c.c_longlong(0)
+    _check(lib().mivgpu_skinny_plan(M, K, N, epi, c.byref(v_nt), c.byref(v_ks), c.byref(v_s), c.byref(v_f),
+                                    c.byref(v_t)), "skinny_plan")
+    return {"nt": v_nt.value, "ks": v_ks.value, "S": v_s.value, "scratch_floats": v_f.value,
+            "tickets": v_t.value}
+
+
+class PackedLinear:
+    """A weight held only in packed form, applied with the skinny MFMA GEMM.
+
+    Owns the zeroed fp32 slabs + tickets of the inter-workgroup split-K
+    (sized for the largest plan seen; the kernel leaves them zeroed, so graph
+    replays need no memset).  Not safe to call concurrently on two streams.
+    """
+
+    def __init__(self, w: torch.Tensor, silu_mul: bool = False):
+        self.N, self.K = w.shape
+        self.silu_mul = silu_mul
+        self.epi = EPI_SILU_MUL if silu_mul else EPI_STORE
+        self.wp = pack_weight(interleave_gate_up(w) if silu_mul else w)
+        self.scratch = None
+        self.tickets = None
+
+    @property
+    def out_features(self) -> int:
+        return self.N // 2 if self.silu_mul else self.N
+
+    def _ensure_scratch(self, floats: int, tickets: int, device):
+        if floats and (self.scratch is None or self.scratch.numel() < floats):
+            self.scratch = torch.zeros(floats, dtype=torch.float32, device=device)
+        if tickets and (self.tickets is None or self.tickets.numel() < tickets):
+            self.tickets = torch.zeros(tickets, dtype=torch.int32, device=device)
+
+    def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None, nt: int = 0, ks: int = 0, S: int = 0):
+        M = x.shape[0]
+        if x.dim() != 2 or x.shape[1] != self.K or x.stride(1) != 1:
+            raise ValueError(f"skinny_gemm: x must be [M, {self.K}] row-major, got {tuple(x.shape)}")
+        if out is None:
+            out = torch.empty(M, self.out_features, dtype=torch.bfloat16, device=x.device)
+        if 0 < M <= 128:
+            pl = skinny_plan(M, self.K, self.N, self.epi, nt, ks, S)
+            self._ensure_scratch(pl["scratch_floats"], pl["tickets"], x.device)
+        sp = _p(self.scratch) if self.scratch is not None else None
+        tp = _p(self.tickets) if self.tickets is not None else None
+        _check(lib().mivgpu_skinny_gemm(_p(self.wp), _p(x), _p(out), M, self.K, self.N, x.stride(0),
+                                        out.stride(0), self.epi, nt, ks, S, sp, tp, _stream()), "skinny_gemm")
+        return out

@@ -119,6 +119,25 @@ def test_decoder_native_matches_reference():
     _close(la, lb, 5e-2)
 
 
+@pytest.mark.parametrize("batch", [1, 5, 32])
+def test_decoder_skinny_path_matches(batch):
+    """Skinny MFMA GEMM path (packed gate_up+SiLU / down / lm_head) vs the
+    hipBLASLt path and the fp32 reference, same weights, over 3 decode steps."""
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
+
+    decs = [Qwen3Decoder(QWEN3_TINY, batch=batch, max_ctx=64, device="cuda", native=nat, seed=5, skinny=sk)
+            for nat, sk in ((True, True), (True, False), (False, False))]
+    assert decs[0].skinny and decs[0].w.lm_head is None and "wgu" not in decs[0].w.layers[0]
+    for d in decs:
+        d.fill_context(12)
+    for _ in range(3):
+        la, lb, lr = (d.step() for d in decs)
+        _close(la, lr, 5e-2)
+        _close(la, lb, 5e-2)
+        for d in decs[1:]:   # keep the token streams identical
+            d.tokens.copy_(decs[0].tokens)
+
+
 def test_decoder_graph_replay_advances_state():
     from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
 

@@ -1,0 +1,101 @@
+"""Skinny MFMA GEMM (csrc/ops/skinny_gemm.hip) against a plain fp32 PyTorch reference."""
+
+import pytest
+import torch
+
+from k8s_vgpu_scheduler_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(x, w):
+    return (x.float() @ w.float().t())
+
+
+def _close(got, ref, tol=2e-2):
+    err = (got.float() - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-6
+    assert err / scale < tol, (err, scale)
+
+
+@pytest.mark.parametrize("M", [1, 7, 32, 33, 64, 100, 128])
+@pytest.mark.parametrize("N,K", [(64, 64), (1024, 512), (4096, 4096), (6144, 4096), (4096, 12288)])
+def test_skinny_gemm_matches_fp32(M, N, K):
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) * 0.02).bfloat16()
+    lin = ops.PackedLinear(w)
+    _close(lin(x), _ref(x, w))
+
+
+@pytest.mark.parametrize("nt,ks,S", [(1, 1, 1), (1, 4, 1), (2, 2, 1), (2, 8, 1), (1, 4, 4), (2, 4, 2),
+                                     (1, 1, 8), (1, 8, 8), (2, 2, 3), (1, 4, 64)])
+@pytest.mark.parametrize("M", [1, 32, 100])
+def test_skinny_gemm_variants(nt, ks, S, M):
+    x = torch.randn(M, 4096, device="cuda").bfloat16()
+    w = (torch.randn(2048, 4096, device="cuda") * 0.02).bfloat16()
+    lin = ops.PackedLinear(w)
+    ref = _ref(x, w)
+    for _ in range(3):   # the split-K scratch must come back zeroed every call
+        _close(lin(x, nt=nt, ks=ks, S=S), ref)
+
+
+def test_split_k_under_graph_replay():
+    x = torch.randn(32, 4096, device="cuda").bfloat16()
+    w = (torch.randn(4096, 4096, device="cuda") * 0.02).bfloat16()
+    lin = ops.PackedLinear(w)
+    assert ops.skinny_plan(32, 4096, 4096, ops.EPI_STORE)["S"] > 1   # o_proj shape splits by default
+    out = torch.empty(32, 4096, device="cuda", dtype=torch.bfloat16)
+    lin(x, out=out, S=4)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        lin(x, out=out, S=4)
+    ref = _ref(x, w)
+    for i in range(5):
+        x.copy_(torch.randn(32, 4096, device="cuda").bfloat16())
+        ref = _ref(x, w)
+        g.replay()
+        torch.cuda.synchronize()
+        _close(out, ref)
+
+
+def test_exact_on_integers():
+    """Small integers are exact in bf16 and fp32: any k-permutation mismatch between
+    the packed W and the X fragments shows up as a wrong element."""
+    x = torch.randint(-3, 4, (32, 256), device="cuda").bfloat16()
+    w = torch.randint(-3, 4, (96, 256), device="cuda").bfloat16()
+    got = ops.PackedLinear(w)(x).float()
+    # the fp32 sum is exact; the kernel rounds it to bf16 once (RNE), like this
+    assert torch.equal(got, (x.float() @ w.float().t()).bfloat16().float())
+
+
+@pytest.mark.parametrize("M", [1, 32, 64, 128])
+@pytest.mark.parametrize("S", [0, 1, 4])
+def test_fused_silu_mul(M, S):
+    inter, K = 1024, 512
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(2 * inter, K, device="cuda") * 0.05).bfloat16()
+    got = ops.PackedLinear(w, silu_mul=True)(x, S=S)
+    gu = _ref(x, w).bfloat16().float()
+    ref = torch.nn.functional.silu(gu[:, :inter]) * gu[:, inter:]
+    assert got.shape == (M, inter)
+    _close(got, ref)
+
+
+def test_strided_x_and_out():
+    x_big = torch.randn(32, 1024 + 64, device="cuda").bfloat16()
+    x = x_big[:, :1024]
+    w = (torch.randn(256, 1024, device="cuda") * 0.02).bfloat16()
+    out_big = torch.zeros(32, 512, device="cuda", dtype=torch.bfloat16)
+    ops.PackedLinear(w)(x, out=out_big[:, :256])
+    _close(out_big[:, :256], _ref(x, w))
+    assert out_big[:, 256:].abs().max().item() == 0
+
+
+def test_rejects_bad_shapes():
+    with pytest.raises(ValueError):
+        ops.pack_weight(torch.zeros(33, 64, device="cuda", dtype=torch.bfloat16))
+    lin = ops.PackedLinear(torch.zeros(64, 64, device="cuda", dtype=torch.bfloat16))
+    with pytest.raises(RuntimeError):
+        lin(torch.zeros(129, 64, device="cuda", dtype=torch.bfloat16))
