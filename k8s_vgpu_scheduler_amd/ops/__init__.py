@@ -44,11 +44,17 @@ def lib():
         L.mivgpu_pack_weight.argtypes = [vp, vp, i, i, vp]
         L.mivgpu_skinny_gemm.argtypes = [vp, vp, vp, i, i, i, i, i, i, i, i, i, vp, vp, vp]
         ip, lp = ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_longlong)
+        L.mivgpu_mfma_burn.argtypes = [vp, i, i, ctypes.c_uint, vp]
+        L.mivgpu_mfma_burn_flops.argtypes = [i, i]
+        L.mivgpu_mfma_burn_flops.restype = ctypes.c_double
+        L.mivgpu_stream_copy.argtypes = [vp, vp, ctypes.c_longlong, i, vp]
+        L.mivgpu_stream_read.argtypes = [vp, ctypes.c_longlong, vp, i, vp]
         L.mivgpu_skinny_plan.argtypes = [i, i, i, i, ip, ip, ip, lp, ip]
         for fn in ("mivgpu_rmsnorm", "mivgpu_add_rmsnorm", "mivgpu_qk_norm_rope_kv",
                    "mivgpu_decode_attention", "mivgpu_silu_mul", "mivgpu_ops_attn_split",
                    "mivgpu_hwid_probe", "mivgpu_pack_weight", "mivgpu_skinny_gemm",
-                   "mivgpu_skinny_max_m", "mivgpu_skinny_plan"):
+                   "mivgpu_skinny_max_m", "mivgpu_skinny_plan", "mivgpu_mfma_burn",
+                   "mivgpu_stream_copy", "mivgpu_stream_read"):
             getattr(L, fn).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -136,6 +142,33 @@ def hwid_probe(blocks: int = 4096) -> torch.Tensor:
     _check(lib().mivgpu_hwid_probe(_p(out), blocks, _stream()), "hwid_probe")
     torch.cuda.synchronize()
     return out.view(blocks, 2).cpu()
+
+
+# ------------------------------------------------------- load generators --
+def mfma_burn(blocks: int, iters: int, out: torch.Tensor | None = None, seed: int = 1) -> torch.Tensor:
+    """Matrix-core load: `blocks` x 4 waves x 8 MFMA chains x `iters` (see loadgen.hip)."""
+    out = torch.empty(blocks * 256, dtype=torch.float32, device="cuda") if out is None else out
+    _check(lib().mivgpu_mfma_burn(_p(out), blocks, iters, seed, _stream()), "mfma_burn")
+    return out
+
+
+def mfma_burn_flops(blocks: int, iters: int) -> float:
+    return float(lib().mivgpu_mfma_burn_flops(blocks, iters))
+
+
+def stream_copy(src: torch.Tensor, dst: torch.Tensor, blocks: int = 0):
+    nbytes = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() < nbytes:
+        raise ValueError("stream_copy: dst too small")
+    _check(lib().mivgpu_stream_copy(_p(src), _p(dst), nbytes, blocks, _stream()), "stream_copy")
+
+
+def stream_read(src: torch.Tensor, out: torch.Tensor | None = None, blocks: int = 0) -> torch.Tensor:
+    """HBM read-only sweep; returns the sum of all 32-bit words as uint64 (in an int64 tensor)."""
+    out = torch.zeros(1, dtype=torch.int64, device=src.device) if out is None else out
+    _check(lib().mivgpu_stream_read(_p(src), src.numel() * src.element_size(), _p(out), blocks, _stream()),
+           "stream_read")
+    return out
 
 
 # ------------------------------------------------------------ skinny GEMM --

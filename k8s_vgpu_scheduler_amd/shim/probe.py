@@ -98,6 +98,46 @@ def child_stream(args) -> dict:
     return {"mode": "stream", "gbps": 2 * x.numel() * 4 * args.iters / dt / 1e9, "seconds": dt}
 
 
+def _timed(fn, iters: int) -> float:
+    import torch
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+def child_mfma(args) -> dict:
+    """Hand-written matrix-core load (csrc/ops/loadgen.hip): exact FLOP count."""
+    from k8s_vgpu_scheduler_amd import ops
+
+    blocks, inner = 256 * 4, 2048
+    out = ops.mfma_burn(blocks, inner)
+    dt = _timed(lambda: ops.mfma_burn(blocks, inner, out=out), args.iters)
+    res = {"mode": "mfma", "tflops": ops.mfma_burn_flops(blocks, inner) * args.iters / dt / 1e12, "seconds": dt,
+           "finite": bool(out.isfinite().all().item())}
+    res.update(gate_stats())
+    return res
+
+
+def child_hipstream(args) -> dict:
+    """Hand-written HBM stream copy (csrc/ops/loadgen.hip)."""
+    import torch
+
+    from k8s_vgpu_scheduler_amd import ops
+
+    nbytes = args.n << 20
+    src = torch.empty(nbytes // 4, dtype=torch.int32, device="cuda").random_()
+    dst = torch.empty_like(src)
+    dt = _timed(lambda: ops.stream_copy(src, dst), args.iters)
+    res = {"mode": "hipstream", "gbps": 2 * nbytes * args.iters / dt / 1e9, "seconds": dt,
+           "exact": bool(torch.equal(src, dst))}
+    res.update(gate_stats())
+    return res
+
+
 def child_hwid(args) -> dict:
     """Which XCD / SE / CU ids does a grid touch under the current HSA_CU_MASK?"""
     from k8s_vgpu_scheduler_amd import ops
@@ -189,7 +229,7 @@ def main():
     args = ap.parse_args()
     if args.child:
         fn = {"matmul": child_matmul, "stream": child_stream, "hwid": child_hwid,
-              "region": child_region}[args.child]
+              "region": child_region, "mfma": child_mfma, "hipstream": child_hipstream}[args.child]
         print(json.dumps(fn(args)), flush=True)
         return
     tmp = Path(os.environ.get("TMPDIR", "/tmp")) / f"mivgpu-probe-{os.getpid()}"

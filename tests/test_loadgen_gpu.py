@@ -1,0 +1,68 @@
+"""Hand-written load generators (csrc/ops/loadgen.hip) and the isolation
+behaviour they are used to measure: CU partitions and the governor."""
+
+import os
+import tempfile
+
+import pytest
+import torch
+
+from k8s_vgpu_scheduler_amd import ops
+from k8s_vgpu_scheduler_amd.shim.probe import run_child
+
+pytestmark = pytest.mark.gpu
+
+
+def test_stream_copy_exact():
+    src = torch.empty((64 << 20) // 4, dtype=torch.int32, device="cuda").random_()
+    dst = torch.zeros_like(src)
+    ops.stream_copy(src, dst)
+    assert torch.equal(src, dst)
+    tail = torch.arange(1000, dtype=torch.int32, device="cuda")      # 4000 B: tail loop only
+    out = torch.zeros_like(tail)
+    ops.stream_copy(tail, out)
+    assert torch.equal(tail, out)
+    with pytest.raises(RuntimeError):
+        ops.stream_copy(src[:3], dst[:3])                             # 12 B: not 16-byte sized
+
+
+def test_stream_read_checksum_exact():
+    src = torch.empty((32 << 20) // 4, dtype=torch.int32, device="cuda").random_()
+    got = ops.stream_read(src).item() & (2 ** 64 - 1)
+    exp = int((src.cpu().numpy().view("uint32").astype("uint64")).sum()) & (2 ** 64 - 1)
+    assert got == exp
+
+
+def test_mfma_burn_runs_at_matrix_core_rate():
+    r = run_child("mfma", {}, False, ["--iters", "20"])
+    assert r["rc"] == 0, r.get("stderr")
+    assert r["finite"]
+    assert r["tflops"] > 500, r     # dense bf16 peak is ~2.5 PF/s
+
+
+def test_cu_partition_scales_matrix_core_throughput():
+    full = run_child("mfma", {}, False, ["--iters", "20"])
+    quarter = run_child("mfma", {"HSA_CU_MASK": "0:0-63"}, False, ["--iters", "20"])
+    assert full["rc"] == 0 and quarter["rc"] == 0
+    ratio = quarter["tflops"] / full["tflops"]
+    assert 0.18 <= ratio <= 0.32, ratio
+
+
+def test_governor_duty_cycle_on_handwritten_load():
+    tmp = tempfile.mkdtemp(prefix="mivgpu-lg-")
+    full = run_child("mfma", {}, False, ["--iters", "60"])
+    half = run_child("mfma", {"MIVGPU_SHARED_CACHE": os.path.join(tmp, "g.cache"), "HIP_DEVICE_CORE_LIMIT": "50",
+                              "GPU_CORE_UTILIZATION_POLICY": "force"}, True, ["--iters", "60"])
+    assert full["rc"] == 0 and half["rc"] == 0, half.get("stderr")
+    ratio = half["tflops"] / full["tflops"]
+    assert 0.35 <= ratio <= 0.65, ratio
+    assert half["gates"] > 0
+
+
+def test_hipstream_under_shim_has_no_overhead():
+    tmp = tempfile.mkdtemp(prefix="mivgpu-lg-")
+    base = run_child("hipstream", {}, False, ["--n", "1024", "--iters", "20"])
+    shim = run_child("hipstream", {"MIVGPU_SHARED_CACHE": os.path.join(tmp, "s.cache")}, True,
+                     ["--n", "1024", "--iters", "20"])
+    assert base["rc"] == 0 and shim["rc"] == 0 and base["exact"] and shim["exact"]
+    assert shim["gbps"] >= 0.95 * base["gbps"], (shim["gbps"], base["gbps"])
