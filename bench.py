@@ -175,11 +175,15 @@ def main():
             "per_slice_tok_s_rank0": per_slice,
             "slice_fairness_min_over_max": round(min(per_slice) / max(per_slice), 3) if per_slice else None,
             "slice_mem_total_mib": [rd["mem_total_mib"] for rd in head["ready"]],
+            "tpot_ms_p50_rank0": [round(d.get("tpot_ms_p50", 0), 3) for d in head["done"]],
+            "tpot_ms_p99_rank0": [round(d.get("tpot_ms_p99", 0), 3) for d in head["done"]],
         }
         if "native" in results and "shim" in results:
             nat = results["native"]["tok_s"]
             out["native_value"] = round(nat, 2)
             out["isolation_overhead_pct"] = round((1.0 - head["tok_s"] / nat) * 100.0, 2)
+            nd = results["native"]["done"]
+            out["native_tpot_ms_p50_rank0"] = [round(d.get("tpot_ms_p50", 0), 3) for d in nd]
         if "native_hip_default" in results:
             nd = results["native_hip_default"]["tok_s"]
             out["native_hip_default_queues_value"] = round(nd, 2)

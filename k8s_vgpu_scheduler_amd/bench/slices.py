@@ -46,7 +46,7 @@ class SliceSpec:
     # HW queues per slice process (GPU_MAX_HW_QUEUES).  HIP's default of 4 per
     # process oversubscribes the hardware scheduler once several tenants share
     # a GPU (measured: 4 slices 4.5k -> 7.6k tok/s with 2 queues each, see
-    # profiles/slice_scaling.md); the device plugin injects the same value.
+    # profiles/README.md §2); the device plugin injects the same value.
     hw_queues: int | None = None
     env: dict = field(default_factory=dict)
 
@@ -171,14 +171,20 @@ def child_main(argv):
     print("READY " + json.dumps(ready), flush=True)
     if sys.stdin.readline().strip() != "GO":
         return 0
+    # per-step completion events: time per output token (TPOT) of this slice
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    evs[0].record()
+    for i in range(a.steps):
         dec.step()
+        evs[i + 1].record()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    print("DONE " + json.dumps({"seconds": dt, "tokens": a.batch * a.steps,
-                                "tok_s": a.batch * a.steps / dt}), flush=True)
+    tpot = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(a.steps))
+    print("DONE " + json.dumps({"seconds": dt, "tokens": a.batch * a.steps, "tok_s": a.batch * a.steps / dt,
+                                "tpot_ms_p50": tpot[len(tpot) // 2],
+                                "tpot_ms_p99": tpot[min(len(tpot) - 1, int(0.99 * len(tpot)))]}), flush=True)
     return 0
 
 

@@ -83,6 +83,8 @@ def main(argv=None):
     ap.add_argument("--log-level", default="", help="MIVGPU_LOG_LEVEL injected into containers")
     ap.add_argument("--smi-backend", default=None, choices=[None, "amdsmi", "sysfs", "fake"])
     ap.add_argument("--enable-numa-topology", action="store_true")
+    ap.add_argument("--device-list-strategy", default="envvar", choices=["envvar", "cdi-annotations", "cdi-cri"])
+    ap.add_argument("--cdi-spec-dir", default="/var/run/cdi")
     ap.add_argument("--kubeconfig", default=None)
     ap.add_argument("-v", type=int, default=2)
     a = ap.parse_args(argv)
@@ -94,10 +96,14 @@ def main(argv=None):
     cfg = PluginConfig(hook_path=a.hook_path, resource_name=a.resource_name, device_split_count=a.device_split_count,
                        device_memory_scaling=a.device_memory_scaling, device_core_scaling=a.device_core_scaling,
                        disable_core_limit=a.disable_core_limit, log_level=a.log_level, hw_queues_shared=a.hw_queues,
-                       enable_numa_topology=a.enable_numa_topology, node_name=a.node_name)
+                       enable_numa_topology=a.enable_numa_topology, node_name=a.node_name,
+                       device_list_strategy=a.device_list_strategy)
     cfg = apply_node_config(cfg, a.node_config, a.node_name)
     install_shim(a.hook_path)
     backend = detect(a.smi_backend)
+    if cfg.device_list_strategy != "envvar":
+        from k8s_vgpu_scheduler_amd.deviceplugin import cdi
+        log.info("wrote CDI spec %s", cdi.write_spec(cdi.build_spec(backend.gpus(), cfg.cdi_kind), a.cdi_spec_dir))
     reg = Registrar(backend, cfg, a.node_name)
     threading.Thread(target=reg.watch_and_register, name="register", daemon=True).start()
     run_with_restarts(lambda: AMDDevicePlugin(backend, cfg, a.node_name, a.socket_dir), a.kubelet_socket)

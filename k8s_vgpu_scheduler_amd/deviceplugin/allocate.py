@@ -12,7 +12,7 @@ docs/develop/amd-vgpu.md:47-104.  MI355X translation:
        GPU_MAX_HW_QUEUES      2 for shared (fractional) pods: HIP's default 4
                               queues/process oversubscribes the HW scheduler
                               when tenants share a GPU (measured, see
-                              profiles/slice_scaling.md)
+                              profiles/README.md §2)
        MIVGPU_SHARED_CACHE    $HOOK_PATH/vgpu/<uuid4>.cache
        MIVGPU_DEVICE_UUIDS, MIVGPU_OVERSUBSCRIBE, MIVGPU_LOG_LEVEL,
        GPU_CORE_UTILIZATION_POLICY=disable (with --disable-core-limit)
@@ -48,6 +48,10 @@ class PluginConfig:
     filter_indexes: tuple = ()
     enable_numa_topology: bool = False
     node_name: str = ""
+    # envvar: device specs in the response; cdi-cri: CDI device names;
+    # cdi-annotations: CDI names in a per-container annotation (deviceplugin/cdi.py)
+    device_list_strategy: str = "envvar"
+    cdi_kind: str = "amd.com/gpu"
 
 
 def _truthy(v) -> bool:
@@ -122,7 +126,11 @@ def allocate_container(pod: dict, ctr: dict, devreq: list, gpus: dict, cfg: Plug
         mounts.append({"container_path": "/etc/ld.so.preload", "host_path": f"{hook}/vgpu/ld.so.preload",
                        "read_only": True})
     devices = []
-    if cfg.pass_device_specs:
+    cdi_names = []
+    if cfg.device_list_strategy in ("cdi-cri", "cdi-annotations"):
+        from k8s_vgpu_scheduler_amd.deviceplugin.cdi import qualified_name
+        cdi_names = [qualified_name(cfg.cdi_kind, d.uuid) for d in devreq]
+    elif cfg.pass_device_specs:
         devices.append({"container_path": "/dev/kfd", "host_path": "/dev/kfd", "permissions": "rw"})
         for d in devreq:
             g = gpus.get(d.uuid)
@@ -134,7 +142,13 @@ def allocate_container(pod: dict, ctr: dict, devreq: list, gpus: dict, cfg: Plug
             if g.card_minor >= 0:
                 p = f"/dev/dri/card{g.card_minor}"
                 devices.append({"container_path": p, "host_path": p, "permissions": "rw"})
-    return {"envs": envs, "mounts": mounts, "devices": devices}
+    out = {"envs": envs, "mounts": mounts, "devices": devices}
+    if cfg.device_list_strategy == "cdi-cri":
+        out["cdi_devices"] = cdi_names
+    elif cfg.device_list_strategy == "cdi-annotations":
+        from k8s_vgpu_scheduler_amd.deviceplugin.cdi import annotation_key
+        out["annotations"] = {annotation_key(ctr.get("name", "")): ",".join(cdi_names)}
+    return out
 
 
 def ld_so_preload_contents() -> str:

@@ -255,6 +255,10 @@ class AMDDevicePlugin:
                 c.mounts.add(**m)
             for d in r["devices"]:
                 c.devices.add(**d)
+            for name in r.get("cdi_devices", ()):
+                c.cdi_devices.add(name=name)
+            for k, v in r.get("annotations", {}).items():
+                c.annotations[k] = v
         return resp
 
     # --------------------------------------------------------- serve/register

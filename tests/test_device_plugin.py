@@ -4,6 +4,7 @@ Mirrors the reference's plugin tests (server_test.go:705-760 with swapped
 getPendingPod / podAllocation* seams, register tests) for AMD/MI355X.
 """
 
+import json
 import os
 import tempfile
 import threading
@@ -208,3 +209,33 @@ def test_handshake_cycle(env):
     util.patch_node_annotations("node1", {HANDSHAKE_ANNOS: "Requesting_2020-01-01 00:00:00"})
     Registrar(backend, plugin.cfg, "node1").register_once()
     assert c.get_node("node1")["metadata"]["annotations"][HANDSHAKE_ANNOS].startswith("Reported_")
+
+
+def test_cdi_spec_and_strategies(env, tmp_path):
+    from k8s_vgpu_scheduler_amd.deviceplugin import cdi
+
+    c, sched, plugin, backend = env
+    spec = cdi.build_spec(backend.gpus())
+    cdi.validate_spec(spec)
+    p = cdi.write_spec(spec, str(tmp_path))
+    assert p.name == "amd.com-gpu.json"
+    doc = json.loads(p.read_text())
+    assert doc["containerEdits"]["deviceNodes"] == [{"path": "/dev/kfd"}]
+    assert {d["name"] for d in doc["devices"]} >= {"GPU-0000", "0"}
+    with pytest.raises(ValueError):
+        cdi.validate_spec({**spec, "kind": "gpu"})
+
+    plugin.cfg.device_list_strategy = "cdi-cri"
+    schedule(c, sched, amd_pod("p", mem=1000))
+    req = api.AllocateRequest()
+    req.container_requests.add(devices_ids=["x"])
+    resp = plugin.Allocate(req, None)
+    cr = resp.container_responses[0]
+    assert [d.name for d in cr.cdi_devices] == [f"amd.com/gpu={S.physical_id(cr.envs['MIVGPU_DEVICE_UUIDS'])}"]
+    assert len(cr.devices) == 0          # device nodes come from the CDI spec
+
+    plugin.cfg.device_list_strategy = "cdi-annotations"
+    schedule(c, sched, amd_pod("q", mem=1000))
+    resp = plugin.Allocate(req, None)
+    ann = dict(resp.container_responses[0].annotations)
+    assert list(ann) == ["cdi.k8s.io/mivgpu_main"] and ann["cdi.k8s.io/mivgpu_main"].startswith("amd.com/gpu=")

@@ -281,3 +281,15 @@ def test_64_vgpus_on_8x8_node(cluster):
     for i in range(64):
         assert filt(s, cluster, amd_pod(f"p{i}", mem=36864, cores=12), ["n1"])["NodeNames"] == ["n1"], i
     assert not filt(s, cluster, amd_pod("p64", mem=1, cores=0), ["n1"]).get("NodeNames")
+
+
+def test_scheduler_bench_policies():
+    """bench/scheduler.py on a 2-node cluster: everything placed, spread touches more GPUs."""
+    from k8s_vgpu_scheduler_amd.bench import scheduler as SB
+
+    bp = SB.run(2, 24, "binpack", "binpack")
+    sp = SB.run(2, 24, "spread", "spread")
+    assert bp["pods_placed"] + bp["pods_rejected"] == 24 and bp["pods_placed"] >= 20
+    assert sp["gpus_touched"] >= bp["gpus_touched"]
+    assert sp["nodes_touched"] == 2
+    assert bp["filter_ms_p50"] is not None and bp["bind_ms_p50"] is not None
