@@ -47,6 +47,8 @@ def apply_node_config(cfg: PluginConfig, path: str, node: str) -> PluginConfig:
             cfg.device_core_scaling = float(nc["devicecorescaling"])
         if "hwqueues" in nc:
             cfg.hw_queues_shared = int(nc["hwqueues"])
+        if "partitions" in nc:
+            cfg.partitions = {int(k): str(v).upper() for k, v in (nc["partitions"] or {}).items()}
         if "enablegetpreferredallocation" in nc:
             cfg.enable_preferred_allocation = bool(nc["enablegetpreferredallocation"])
         fd = nc.get("filterdevices") or {}
@@ -85,6 +87,8 @@ def main(argv=None):
     ap.add_argument("--enable-numa-topology", action="store_true")
     ap.add_argument("--device-list-strategy", default="envvar", choices=["envvar", "cdi-annotations", "cdi-cri"])
     ap.add_argument("--cdi-spec-dir", default="/var/run/cdi")
+    ap.add_argument("--enable-partition-manager", action="store_true",
+                    help="reconcile compute-partition modes from mivgpu.io/partition-request")
     ap.add_argument("--kubeconfig", default=None)
     ap.add_argument("-v", type=int, default=2)
     a = ap.parse_args(argv)
@@ -106,7 +110,18 @@ def main(argv=None):
         log.info("wrote CDI spec %s", cdi.write_spec(cdi.build_spec(backend.gpus(), cfg.cdi_kind), a.cdi_spec_dir))
     reg = Registrar(backend, cfg, a.node_name)
     threading.Thread(target=reg.watch_and_register, name="register", daemon=True).start()
-    run_with_restarts(lambda: AMDDevicePlugin(backend, cfg, a.node_name, a.socket_dir), a.kubelet_socket)
+    reload = threading.Event()
+    if a.enable_partition_manager or cfg.partitions:
+        from k8s_vgpu_scheduler_amd.deviceplugin.partition import PartitionManager
+
+        pm = PartitionManager(backend, a.node_name, static=cfg.partitions)
+
+        def on_change():
+            reg.register_once()
+            reload.set()
+        threading.Thread(target=pm.watch, args=(on_change,), name="partitions", daemon=True).start()
+    run_with_restarts(lambda: AMDDevicePlugin(backend, cfg, a.node_name, a.socket_dir), a.kubelet_socket,
+                      reload=reload)
     return 0
 
 

@@ -32,7 +32,7 @@ from k8s_vgpu_scheduler_amd.device import common as R
 from k8s_vgpu_scheduler_amd.device import devices as D
 from k8s_vgpu_scheduler_amd.device.init_container import collapse_init_container_usage
 from k8s_vgpu_scheduler_amd.device.quota import get_local_cache
-from k8s_vgpu_scheduler_amd.device.types import (ContainerDevice, ContainerDeviceRequest, DeviceInfo,
+from k8s_vgpu_scheduler_amd.device.types import (MODE_SHARED, ContainerDevice, ContainerDeviceRequest, DeviceInfo,
                                                  DeviceUsage, NodeInfo, ResourceNames)
 from k8s_vgpu_scheduler_amd.k8s import quantity
 from k8s_vgpu_scheduler_amd.k8s.client import containers
@@ -56,6 +56,10 @@ AMD_NO_USE = "amd.com/nouse-gputype"
 AMD_USE_UUID = "amd.com/use-gpu-uuid"
 AMD_NO_USE_UUID = "amd.com/nouse-gpu-uuid"
 AMD_NUMA_BIND = "amd.com/numa-bind"
+# Pod annotation restricting the device mode: "hami-core" (shared SPX GPU),
+# or a compute-partition mode "dpx" / "qpx" / "cpx" (comma list allowed).
+AMD_VGPU_MODE = "amd.com/vgpu-mode"
+CUS_PER_XCD = 32      # MI355X: 8 XCDs x 32 CUs
 NODE_LOCK_AMD = T.NODE_LOCK_KEY
 
 CORE_POLICIES = ("default", "force", "disable")
@@ -156,7 +160,11 @@ class AMDDevices(D.Devices):
         util.HANDSHAKE_ANNOS.setdefault(AMD_DEVICE, HANDSHAKE_ANNOS)
 
     def cu_topology(self, total: int) -> cu_alloc.CUTopology:
-        xcds = self.cfg.xcds_per_device if total % max(1, self.cfg.xcds_per_device) == 0 else 1
+        """XCDs a device spans: 8 for a whole MI355X (SPX), fewer for a compute
+        partition (DPX 4 / QPX 2 / CPX 1 XCD of 32 CUs each)."""
+        xcds = max(1, min(self.cfg.xcds_per_device, total // CUS_PER_XCD))
+        if total % xcds:
+            xcds = 1
         return cu_alloc.CUTopology(total=total, xcds=xcds, layout=self.cfg.cu_layout)
 
     # ------------------------------------------------------------ identity
@@ -393,6 +401,9 @@ class AMDDevices(D.Devices):
         is_mutex = util.policy_contains(policy, T.GPU_POLICY_MUTEX)
         numa_bind = str(annos.get(AMD_NUMA_BIND, "")).lower() in ("1", "t", "true")
         cordoned = cordoned_devices(node_info)
+        want_modes = {m.strip().lower() for m in annos.get(AMD_VGPU_MODE, "").split(",") if m.strip()}
+        if "spx" in want_modes or "shared" in want_modes:
+            want_modes |= {MODE_SHARED}
         tmp: list[ContainerDevice] = []
         prevnuma = -1
 
@@ -408,6 +419,9 @@ class AMDDevices(D.Devices):
                 continue
             if k.type.upper() != AMD_DEVICE or not D.check_type(annos, dev.type, AMD_IN_USE, AMD_NO_USE):
                 bump(R.CARD_TYPE_MISMATCH)
+                continue
+            if want_modes and (dev.mode or MODE_SHARED).lower() not in want_modes:
+                bump(R.MODE_NOT_FIT)
                 continue
             if numa_bind and prevnuma != dev.numa:
                 if k.nums != orig:

@@ -25,7 +25,7 @@ from __future__ import annotations
 
 import os
 import uuid as _uuid
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 from k8s_vgpu_scheduler_amd.device.codec import format_ranges, ranges_count
 
@@ -52,6 +52,7 @@ class PluginConfig:
     # cdi-annotations: CDI names in a per-container annotation (deviceplugin/cdi.py)
     device_list_strategy: str = "envvar"
     cdi_kind: str = "amd.com/gpu"
+    partitions: dict = field(default_factory=dict)   # physical GPU index -> SPX/DPX/QPX/CPX
 
 
 def _truthy(v) -> bool:

@@ -70,6 +70,10 @@ class Registrar:
         return annos
 
     def register_once(self, gpus: list[GPUInfo] | None = None) -> bool:
+        from k8s_vgpu_scheduler_amd.deviceplugin.partition import is_applying
+
+        if is_applying():          # GPUs are being re-partitioned: the device list is in flux
+            return False
         gpus = gpus if gpus is not None else self.backend.gpus()
         annos = self.annotations(gpus)
         node = util.get_node(self.node)

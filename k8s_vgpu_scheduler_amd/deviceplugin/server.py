@@ -146,8 +146,10 @@ class AMDDevicePlugin:
 
     def health_loop(self, period: float = 5.0):
         disabled = os.environ.get("DP_DISABLE_HEALTHCHECKS", "") in ("all", "*")
+        from k8s_vgpu_scheduler_amd.deviceplugin.partition import is_applying
+
         while not self._stop.wait(period):
-            if disabled:
+            if disabled or is_applying():    # a partition reconfiguration is resetting GPUs
                 continue
             for g in self.gpus:
                 ok, why = self.backend.health(g)
@@ -301,15 +303,22 @@ class AMDDevicePlugin:
 
 
 def run_with_restarts(make_plugin, kubelet_socket: str, max_restarts: int = 5, window_s: float = 3600.0,
-                      stop: threading.Event | None = None):
-    """server.go:518-566: restart a crashed plugin; >max_restarts within the window is fatal."""
+                      stop: threading.Event | None = None, reload: threading.Event | None = None):
+    """server.go:518-566: restart a crashed plugin; >max_restarts within the window is fatal.
+    Setting `reload` (device list changed, e.g. a new compute-partition mode)
+    restarts the endpoint without counting as a crash."""
     stop = stop or threading.Event()
+    reload = reload or threading.Event()
     restarts: list[float] = []
     while not stop.is_set():
         plugin = make_plugin()
         try:
             plugin.start(kubelet_socket)
-            while not stop.wait(5.0):
+            while not stop.wait(1.0):
+                if reload.is_set():
+                    reload.clear()
+                    log.info("device list changed: re-registering the plugin with the kubelet")
+                    break
                 if not os.path.exists(plugin.socket):
                     raise RuntimeError("plugin socket disappeared (kubelet restarted?)")
                 if not os.path.exists(kubelet_socket):

@@ -38,7 +38,22 @@ class GPUInfo:
     healthy: bool = True
     compute_partition: str = "SPX"
     memory_partition: str = "NPS1"
+    physical_index: int = -1     # physical GPU this (partition) device belongs to; -1 = index
+    partition_index: int = 0
     extra: dict = field(default_factory=dict)
+
+    @property
+    def physical(self) -> int:
+        return self.index if self.physical_index < 0 else self.physical_index
+
+
+# MI355X compute-partition modes: logical GPUs per physical GPU (XCDs split evenly).
+PARTITION_MODES = {"SPX": 1, "DPX": 2, "QPX": 4, "CPX": 8}
+MEMORY_MODES = ("NPS1", "NPS2")
+
+
+class PartitionError(RuntimeError):
+    pass
 
 
 @dataclass
@@ -69,6 +84,10 @@ class Backend:
 
     def processes(self, g: GPUInfo) -> list[dict]:
         return []
+
+    def set_compute_partition(self, physical_index: int, mode: str) -> None:
+        """Reconfigure one physical GPU (must be idle; needs privileges)."""
+        raise PartitionError(f"{self.name}: compute partitioning not supported")
 
     def shutdown(self):
         pass
@@ -127,7 +146,35 @@ class AmdSmiBackend(Backend):
                         compute_partition=str(part))
             self._by_uuid[g.uuid] = h
             out.append(g)
+        # partitions of one physical GPU share domain:bus:device, differ in function
+        phys: dict[str, int] = {}
+        for g in out:
+            key = g.bdf.rsplit(".", 1)[0] if g.bdf else f"idx{g.index}"
+            g.partition_index = sum(1 for o in out[: g.index] if (o.bdf.rsplit(".", 1)[0] if o.bdf else "") == key)
+            g.physical_index = phys.setdefault(key, len(phys))
         return out
+
+    def set_compute_partition(self, physical_index: int, mode: str) -> None:
+        mode = mode.upper()
+        if mode not in PARTITION_MODES:
+            raise PartitionError(f"unknown compute partition {mode}")
+        gs = [g for g in self.gpus() if g.physical == physical_index]
+        if not gs:
+            raise PartitionError(f"no physical GPU {physical_index}")
+        enum = getattr(self.m, "AmdSmiComputePartitionType", None)
+        try:
+            self.m.amdsmi_set_gpu_compute_partition(self._h(gs[0]), getattr(enum, mode) if enum else mode)
+        except Exception as e:  # noqa: BLE001
+            raise PartitionError(f"amd-smi set compute partition {mode} on GPU {physical_index}: {e}") from e
+        self.handles = self.m.amdsmi_get_processor_handles()
+        self._by_uuid = {}
+
+    def processes(self, g):
+        try:
+            return [dict(p) if isinstance(p, dict) else {"pid": p}
+                    for p in self.m.amdsmi_get_gpu_process_list(self._h(g))]
+        except Exception:  # noqa: BLE001
+            return []
 
     def _h(self, g):
         return self._by_uuid.get(g.uuid) or self.handles[g.index]
@@ -243,6 +290,18 @@ class SysfsBackend(Backend):
     def link(self, a, b):
         return LinkInfo("XGMI", 1, 1)
 
+    def set_compute_partition(self, physical_index: int, mode: str) -> None:
+        mode = mode.upper()
+        if mode not in PARTITION_MODES:
+            raise PartitionError(f"unknown compute partition {mode}")
+        cards = sorted(Path("/sys/class/drm").glob("card*/device/current_compute_partition"))
+        if physical_index >= len(cards):
+            raise PartitionError(f"no compute-partition sysfs node for GPU {physical_index}")
+        try:
+            cards[physical_index].write_text(mode + "\n")
+        except OSError as e:
+            raise PartitionError(f"write {cards[physical_index]}: {e}") from e
+
 
 # ---------------------------------------------------------------------- fake
 class FakeBackend(Backend):
@@ -256,15 +315,43 @@ class FakeBackend(Backend):
         self.numa_per = numa_per
         self.used: dict[str, int] = {}
         self.util: dict[str, dict] = {}
+        self.modes: dict[int, str] = {i: "SPX" for i in range(n)}
+        self.procs: dict[str, list] = {}
+        self.partition_calls: list[tuple[int, str]] = []
 
     def gpus(self):
-        return [GPUInfo(index=i, uuid=f"{self.prefix}-{i:04x}", rocr_id=f"{self.prefix}-{i:04x}",
-                        memory_mib=self.memory_mib, cus=self.cus, numa=i // self.numa_per if self.numa_per else 0,
-                        bdf=f"0000:{0x11 + i:02x}:00.0", render_minor=128 + i, card_minor=i)
-                for i in range(self.n)]
+        out = []
+        for i in range(self.n):
+            mode = self.modes.get(i, "SPX")
+            parts = PARTITION_MODES[mode]
+            for j in range(parts):
+                uid = f"{self.prefix}-{i:04x}" if parts == 1 else f"{self.prefix}-{i:04x}-{mode.lower()}{j}"
+                k = len(out)
+                out.append(GPUInfo(index=k, uuid=uid, rocr_id=uid, memory_mib=self.memory_mib // parts,
+                                   cus=self.cus // parts, xcds=8 // parts,
+                                   numa=i // self.numa_per if self.numa_per else 0,
+                                   bdf=f"0000:{0x11 + i:02x}:00.{j}", render_minor=128 + k, card_minor=k,
+                                   compute_partition=mode, physical_index=i, partition_index=j))
+        return out
+
+    def processes(self, g):
+        return list(self.procs.get(g.uuid, []))
+
+    def set_compute_partition(self, physical_index: int, mode: str) -> None:
+        mode = mode.upper()
+        if mode not in PARTITION_MODES:
+            raise PartitionError(f"unknown compute partition {mode}")
+        if physical_index not in self.modes:
+            raise PartitionError(f"no physical GPU {physical_index}")
+        if any(self.procs.get(g.uuid) for g in self.gpus() if g.physical == physical_index):
+            raise PartitionError(f"GPU {physical_index} busy")
+        self.partition_calls.append((physical_index, mode))
+        self.modes[physical_index] = mode
 
     def link(self, a, b):
-        key = tuple(sorted((a.index, b.index)))
+        if a.physical == b.physical:
+            return LinkInfo("XGMI", 0, 8)          # partitions of one package: on-die
+        key = tuple(sorted((a.physical, b.physical)))
         if key in self.degraded:
             return LinkInfo("XGMI", 1, 1, self.degraded[key])
         return LinkInfo("XGMI", 1, 1)
