@@ -106,7 +106,11 @@ class Qwen3Decoder:
             ops.require_native()
         self.w = Qwen3Weights(cfg, self.device, seed=seed)
         shapes_ok = cfg.hidden % 64 == 0 and cfg.intermediate % 64 == 0 and cfg.vocab % 64 == 0
-        self.skinny = (self.native and batch <= 32 and shapes_ok) if skinny is None else skinny
+        if skinny is None:
+            import os
+            skinny = os.environ.get("MIVGPU_SKINNY_GEMM", "1") != "0"
+            skinny = skinny and self.native and batch <= 32 and shapes_ok
+        self.skinny = skinny
         if self.skinny:
             # Keep only the packed copies (no duplicate 16 GB of weights).
             for lw in self.w.layers:

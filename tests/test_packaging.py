@@ -127,3 +127,15 @@ def test_examples_admit_and_schedule(name, pod):
         assert got["NodeNames"] in (None, []) and "n1" in got["FailedNodes"]
     else:
         assert got["NodeNames"] == ["n1"], (name, got)
+
+
+def test_dashboard_queries_exported_series():
+    dash = json.loads((ROOT / "dashboards/mivgpu-mi355x.json").read_text())
+    src = ((ROOT / "k8s_vgpu_scheduler_amd/scheduler/metrics.py").read_text()
+           + (ROOT / "k8s_vgpu_scheduler_amd/monitor/metrics.py").read_text())
+    exported = set(re.findall(r'"((?:hami|mivgpu)_[a-z_]+)"', src))
+    used = set()
+    for p in dash["panels"]:
+        for t in p["targets"]:
+            used |= set(re.findall(r"\b((?:hami|mivgpu)_[a-z_]+)", t["expr"]))
+    assert used and used <= exported, used - exported
