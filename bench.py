@@ -18,7 +18,7 @@ per slice between a barrier + torch.cuda.synchronize() on both sides (max
 over ranks).  The reference publishes no number -> vs_baseline
 is null; the native round is the comparison point.
 
-    python bench.py --gpus 1 --steps 20 --warmup 5
+    python bench.py --gpus 1 --steps 100 --warmup 10
     torchrun --nproc-per-node 8 bench.py --gpus 8 ...
 """
 
@@ -51,8 +51,12 @@ def physical_gpu_for(local_rank: int) -> str:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # Timed decode steps per slice.  Steps are cheap next to model load (one
+    # step = one token per sequence, ~16 ms at 4 slices); 100 keeps a single
+    # scheduling hiccup (seen once: ~190 ms on one of 8 slices) from
+    # dominating the slowest slice's wall time.
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--slices", type=int, default=4, help="vGPU slices (pods) per GPU")
     ap.add_argument("--batch", type=int, default=32, help="decode sequences per slice")
     ap.add_argument("--ctx", type=int, default=1024, help="KV context length at decode start")

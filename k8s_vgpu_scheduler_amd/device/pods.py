@@ -7,10 +7,11 @@ to app-containers-only so an informer resync cannot re-inflate it.
 
 from __future__ import annotations
 
-import copy
 import logging
 import threading
 from dataclasses import dataclass, field
+
+from k8s_vgpu_scheduler_amd.utils.jcopy import jcopy
 
 from .types import copy_pod_devices
 
@@ -41,8 +42,9 @@ class PodInfo:
         return self.pod["metadata"].get("annotations") or {}
 
     def deepcopy(self) -> "PodInfo":
-        return PodInfo(copy.deepcopy(self.pod), self.node_id, copy_pod_devices(self.devices),
-                       self.init_released)
+        # `pod` is a private copy taken in add_pod/update_pod and only ever
+        # replaced, never mutated, so snapshots share it.
+        return PodInfo(self.pod, self.node_id, copy_pod_devices(self.devices), self.init_released)
 
 
 def _uid(pod: dict) -> str:
@@ -61,10 +63,10 @@ class PodManager:
             k = _uid(pod)
             pi = self._pods.get(k)
             if pi is None:
-                self._pods[k] = PodInfo(copy.deepcopy(pod), node_id, copy_pod_devices(devices))
+                self._pods[k] = PodInfo(jcopy(pod), node_id, copy_pod_devices(devices))
                 log.info("pod added %s/%s node=%s", pod["metadata"].get("namespace"), pod["metadata"]["name"], node_id)
                 return True
-            pi.pod = copy.deepcopy(pod)
+            pi.pod = jcopy(pod)
             pi.node_id = node_id
             if not pi.init_released:
                 pi.devices = copy_pod_devices(devices)
@@ -74,7 +76,7 @@ class PodManager:
         with self._mu:
             pi = self._pods.get(_uid(pod))
             if pi:
-                pi.pod = copy.deepcopy(pod)
+                pi.pod = jcopy(pod)
 
     def del_pod(self, pod: dict):
         with self._mu:

@@ -10,9 +10,10 @@ analogue, CPX/NPS compute partitions, is reported via ``mode``).
 
 from __future__ import annotations
 
-import copy
 from dataclasses import dataclass, field
 from typing import Any
+
+from k8s_vgpu_scheduler_amd.utils.jcopy import jcopy
 
 # Mode string of a device shared by libmivgpu time/CU slicing (the AMD analogue
 # of the reference's "hami-core" mode, nvidia/device.go:62).
@@ -54,7 +55,9 @@ class DeviceInfo:
                    custominfo=dict(d.get("custominfo") or {}))
 
     def deepcopy(self) -> "DeviceInfo":
-        return copy.deepcopy(self)
+        return DeviceInfo(self.id, self.index, self.count, self.devmem, self.devcore, self.type, self.numa,
+                          self.mode, self.health, self.devicevendor, jcopy(self.custominfo),
+                          jcopy(self.pair_scores))
 
 
 @dataclass
@@ -87,7 +90,7 @@ class DeviceUsage:
                            usedmem=self.usedmem, totalmem=self.totalmem, totalcore=self.totalcore,
                            usedcores=self.usedcores, mode=self.mode, numa=self.numa, type=self.type,
                            health=self.health, pod_infos=list(self.pod_infos),
-                           custominfo=copy.deepcopy(self.custominfo))
+                           custominfo=jcopy(self.custominfo))
 
 
 @dataclass
@@ -102,7 +105,7 @@ class ContainerDevice:
 
     def deepcopy(self) -> "ContainerDevice":
         return ContainerDevice(self.idx, self.uuid, self.type, self.usedmem, self.usedcores,
-                               self.slots, copy.deepcopy(self.custominfo))
+                               self.slots, jcopy(self.custominfo))
 
 
 @dataclass
@@ -135,8 +138,10 @@ class NodeInfo:
     devices: dict = field(default_factory=dict)   # vendor -> list[DeviceInfo]
 
     def deepcopy(self) -> "NodeInfo":
-        return NodeInfo(self.id, copy.deepcopy(self.node),
-                        {k: [d.deepcopy() for d in v] for k, v in self.devices.items()})
+        # The node object is replaced wholesale on every informer update and is
+        # never mutated in place, so snapshots share it; only the device
+        # records (whose usage fields the scorer updates) are copied.
+        return NodeInfo(self.id, self.node, {k: [d.deepcopy() for d in v] for k, v in self.devices.items()})
 
 
 @dataclass

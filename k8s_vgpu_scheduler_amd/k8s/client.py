@@ -9,9 +9,10 @@ pkg/util/client/client.go:58-107 (``InitGlobalClient`` / ``GetClient``).
 
 from __future__ import annotations
 
-import copy
 import threading
 from typing import Callable, Iterable, Optional
+
+from k8s_vgpu_scheduler_amd.utils.jcopy import jcopy
 
 KINDS = ("nodes", "pods", "resourcequotas", "events", "leases")
 NAMESPACED = {"pods", "resourcequotas", "events", "leases"}
@@ -110,15 +111,15 @@ class KubeClient:
 def merge_patch(target, patch):
     """RFC 7386 JSON merge patch (None deletes a key)."""
     if not isinstance(patch, dict):
-        return copy.deepcopy(patch)
-    out = copy.deepcopy(target) if isinstance(target, dict) else {}
+        return jcopy(patch)
+    out = jcopy(target) if isinstance(target, dict) else {}
     for k, v in patch.items():
         if v is None:
             out.pop(k, None)
         elif isinstance(v, dict):
             out[k] = merge_patch(out.get(k), v)
         else:
-            out[k] = copy.deepcopy(v)
+            out[k] = jcopy(v)
     return out
 
 

@@ -14,12 +14,13 @@ Faithful where the control plane depends on it:
 
 from __future__ import annotations
 
-import copy
 import itertools
 import threading
 import time
 import uuid
 from typing import Callable, Optional
+
+from k8s_vgpu_scheduler_amd.utils.jcopy import jcopy
 
 from .client import (NAMESPACED, AlreadyExists, ApiError, Conflict, KubeClient, NotFound,
                      match_fields, match_labels, merge_patch)
@@ -64,7 +65,7 @@ class FakeCluster(KubeClient):
             if ns and (obj.get("metadata") or {}).get("namespace") != ns:
                 continue
             try:
-                h(etype, copy.deepcopy(obj), copy.deepcopy(old) if old else None)
+                h(etype, jcopy(obj), jcopy(old) if old else None)
             except Exception:  # a broken handler must not break the API server
                 import logging
                 logging.getLogger(__name__).exception("watch handler failed")
@@ -81,7 +82,7 @@ class FakeCluster(KubeClient):
             o = self._store(kind).get(self._key(kind, name, namespace))
             if o is None:
                 raise NotFound(f"{kind} {namespace or ''}/{name} not found")
-            return copy.deepcopy(o)
+            return jcopy(o)
 
     def list(self, kind, namespace=None, label_selector=None, field_selector=None):
         with self._lock:
@@ -92,13 +93,13 @@ class FakeCluster(KubeClient):
                 if namespace and kind in NAMESPACED and ns != namespace:
                     continue
                 if match_labels(o, label_selector) and match_fields(o, field_selector):
-                    out.append(copy.deepcopy(o))
+                    out.append(jcopy(o))
             return out
 
     def create(self, kind, obj, namespace=None):
         events = []
         with self._lock:
-            obj = copy.deepcopy(obj)
+            obj = jcopy(obj)
             md = obj.setdefault("metadata", {})
             if kind in NAMESPACED:
                 md["namespace"] = namespace or md.get("namespace") or "default"
@@ -113,12 +114,12 @@ class FakeCluster(KubeClient):
                 raise AlreadyExists(f"{kind} {md['name']} exists")
             self._bump(obj)
             self._store(kind)[key] = obj
-            events.append((kind, "ADDED", copy.deepcopy(obj), None))
+            events.append((kind, "ADDED", jcopy(obj), None))
         for e in events:
             self._notify(*e)
         if after:
             raise after
-        return copy.deepcopy(obj)
+        return jcopy(obj)
 
     def update(self, kind, obj, namespace=None):
         with self._lock:
@@ -133,7 +134,7 @@ class FakeCluster(KubeClient):
             rv = md.get("resourceVersion")
             if rv and rv != cur["metadata"]["resourceVersion"]:
                 raise Conflict(f"{kind} {md.get('name')}: resourceVersion {rv} is stale")
-            new = copy.deepcopy(obj)
+            new = jcopy(obj)
             new.setdefault("metadata", {})["uid"] = cur["metadata"].get("uid")
             self._bump(new)
             self._store(kind)[key] = new
@@ -141,7 +142,7 @@ class FakeCluster(KubeClient):
         self._notify(kind, "MODIFIED", new, old)
         if after:
             raise after
-        return copy.deepcopy(new)
+        return jcopy(new)
 
     def patch(self, kind, name, patch, namespace=None):
         with self._lock:
@@ -163,7 +164,7 @@ class FakeCluster(KubeClient):
         self._notify(kind, "MODIFIED", new, old)
         if after:
             raise after
-        return copy.deepcopy(new)
+        return jcopy(new)
 
     def delete(self, kind, name, namespace=None):
         with self._lock:

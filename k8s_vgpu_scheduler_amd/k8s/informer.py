@@ -9,10 +9,11 @@ matching the reference's deep-copy discipline (nodes.go:71-106).
 
 from __future__ import annotations
 
-import copy
 import logging
 import threading
 from typing import Callable, Optional
+
+from k8s_vgpu_scheduler_amd.utils.jcopy import jcopy
 
 from .client import KubeClient, NAMESPACED, match_labels
 
@@ -50,14 +51,14 @@ class Informer:
         for on_add, on_update, on_delete in self._handlers:
             try:
                 if etype == "ADDED" and on_add:
-                    on_add(copy.deepcopy(obj))
+                    on_add(jcopy(obj))
                 elif etype == "MODIFIED":
                     if prev is None and on_add:
-                        on_add(copy.deepcopy(obj))
+                        on_add(jcopy(obj))
                     elif on_update:
-                        on_update(copy.deepcopy(prev if prev is not None else old), copy.deepcopy(obj))
+                        on_update(jcopy(prev if prev is not None else old), jcopy(obj))
                 elif etype == "DELETED" and on_delete:
-                    on_delete(copy.deepcopy(prev or obj))
+                    on_delete(jcopy(prev or obj))
             except Exception:
                 log.exception("%s informer handler failed", self.kind)
 
@@ -86,10 +87,10 @@ class Informer:
     def get(self, name: str, namespace: str | None = None) -> dict | None:
         with self._mu:
             o = self._cache.get((namespace if self.kind in NAMESPACED else "", name))
-            return copy.deepcopy(o) if o is not None else None
+            return jcopy(o) if o is not None else None
 
     def list(self, label_selector: dict | None = None, namespace: str | None = None) -> list[dict]:
         with self._mu:
             items = list(self._cache.items())
-        return [copy.deepcopy(o) for (ns, _), o in items
+        return [jcopy(o) for (ns, _), o in items
                 if (namespace is None or ns == namespace) and match_labels(o, label_selector)]

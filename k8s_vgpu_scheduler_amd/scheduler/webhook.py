@@ -15,12 +15,12 @@ Order of checks (kept from the reference):
 from __future__ import annotations
 
 import base64
-import copy
 import json
 import logging
 
 from k8s_vgpu_scheduler_amd.device import devices as D
 from k8s_vgpu_scheduler_amd.device.quota import get_local_cache
+from k8s_vgpu_scheduler_amd.utils.jcopy import jcopy
 
 log = logging.getLogger(__name__)
 
@@ -94,7 +94,7 @@ class Webhook:
 
     def admit(self, pod: dict) -> tuple[bool, str, dict | None, int]:
         """-> (allowed, message, mutated_pod_or_None, http_code_for_errors)"""
-        pod = copy.deepcopy(pod)
+        pod = jcopy(pod)
         spec = pod.setdefault("spec", {})
         if not spec.get("containers"):
             return False, "pod has no containers", None, 403
