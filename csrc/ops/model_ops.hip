@@ -16,6 +16,7 @@
 // All tensors bf16 (raw uint16 bits) unless noted; fp32 accumulation.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 typedef uint16_t bf16_t;
 
@@ -176,7 +177,11 @@ qk_norm_rope_kv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict_
 constexpr int ATT_SPLIT = 256;
 constexpr int ATT_D = 128;
 
-template <int G>
+// PF (load scheduling): 0 = one dependent K / V load per loop trip (lowest
+// VGPRs, highest occupancy); 1 = every K and V load of the thread issued up
+// front; 2 = K up front, V issued right after the scores (before the softmax
+// barrier).  Chosen per launch by mivgpu_decode_attention (measured).
+template <int G, int PF>
 __global__ void __launch_bounds__(256)
 decode_attn_partial_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k_cache,
                            const bf16_t* __restrict__ v_cache, const int* __restrict__ seqlens,
@@ -203,23 +208,64 @@ decode_attn_partial_kernel(const bf16_t* __restrict__ q, const bf16_t* __restric
   const bf16_t* kb = k_cache + ((size_t)b * Hkv + hk) * (size_t)max_ctx * ATT_D;
   const bf16_t* vb = v_cache + ((size_t)b * Hkv + hk) * (size_t)max_ctx * ATT_D;
 
+  const int lane = t & 63, wave = t >> 6;
+  const int sub = lane & 7;       // 16-dim chunk of a key row (scores)
+  const int krow = lane >> 3;     // key within a wave-iteration (scores)
+  const int r = t >> 4, c = t & 15;  // P.V: row group, 8-dim column chunk
+  constexpr int KIT = ATT_SPLIT / 32;   // score iterations per wave
+  constexpr int VIT = ATT_SPLIT / 16;   // P.V rows per thread
+  // Out-of-range rows are clamped to row j0 and their results discarded (no
+  // branches around loads).  q is loaded first: vmcnt retires in order.
+  uint4 qreg[G][2];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const uint4* qp = reinterpret_cast<const uint4*>(q + (part_base + g) * ATT_D + sub * 16);
+    qreg[g][0] = qp[0];
+    qreg[g][1] = qp[1];
+  }
+  uint4 kreg[PF ? KIT : 1][2];
+  uint4 vreg[PF ? VIT : 1];
+  auto load_k = [&](int i, uint4* dst) {
+    const int jj = wave * 8 + krow + 32 * i;
+    const uint4* kp = reinterpret_cast<const uint4*>(kb + (size_t)(j0 + (jj < n ? jj : 0)) * ATT_D + sub * 16);
+    dst[0] = kp[0];
+    dst[1] = kp[1];
+  };
+  auto load_v = [&](int i) {
+    const int jj = r + 16 * i;
+    return *reinterpret_cast<const uint4*>(vb + (size_t)(j0 + (jj < n ? jj : 0)) * ATT_D + c * 8);
+  };
+  if constexpr (PF >= 1) {
+#pragma unroll
+    for (int i = 0; i < KIT; ++i) load_k(i, kreg[i]);
+  }
+  if constexpr (PF == 1) {
+#pragma unroll
+    for (int i = 0; i < VIT; ++i) vreg[i] = load_v(i);
+  }
+  if constexpr (PF >= 1) __builtin_amdgcn_sched_barrier(0);   // keep the batch ahead of its uses
+
   // ---- scores
   {
-    const int lane = t & 63, wave = t >> 6;
-    const int sub = lane & 7;       // 16-dim chunk
-    const int krow = lane >> 3;     // key within the wave-iteration
     float qf[G][16];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const uint4* qp = reinterpret_cast<const uint4*>(q + (part_base + g) * ATT_D + sub * 16);
-      unpack8(qp[0], &qf[g][0]);
-      unpack8(qp[1], &qf[g][8]);
+      unpack8(qreg[g][0], &qf[g][0]);
+      unpack8(qreg[g][1], &qf[g][8]);
     }
-    for (int jj = wave * 8 + krow; jj < n; jj += 32) {
-      const uint4* kp = reinterpret_cast<const uint4*>(kb + (size_t)(j0 + jj) * ATT_D + sub * 16);
+#pragma unroll
+    for (int i = 0; i < KIT; ++i) {
+      const int jj = wave * 8 + krow + 32 * i;
+      uint4 kk[2];
+      if constexpr (PF >= 1) {
+        kk[0] = kreg[i][0];
+        kk[1] = kreg[i][1];
+      } else {
+        load_k(i, kk);
+      }
       float kf[16];
-      unpack8(kp[0], &kf[0]);
-      unpack8(kp[1], &kf[8]);
+      unpack8(kk[0], &kf[0]);
+      unpack8(kk[1], &kf[8]);
       float acc[G];
 #pragma unroll
       for (int g = 0; g < G; ++g) {
@@ -231,11 +277,15 @@ decode_attn_partial_kernel(const bf16_t* __restrict__ q, const bf16_t* __restric
         a += __shfl_xor(a, 4, 64);
         acc[g] = a;
       }
-      if (sub == 0) {
+      if (sub == 0 && jj < n) {
 #pragma unroll
         for (int g = 0; g < G; ++g) s_p[g][jj] = acc[g] * scale;
       }
     }
+  }
+  if constexpr (PF == 2) {
+#pragma unroll
+    for (int i = 0; i < VIT; ++i) vreg[i] = load_v(i);   // in flight across the softmax
   }
   __syncthreads();
 
@@ -266,21 +316,27 @@ decode_attn_partial_kernel(const bf16_t* __restrict__ q, const bf16_t* __restric
     for (int g = 0; g < G; ++g) lsum[g] = s_red[4][g] + s_red[5][g] + s_red[6][g] + s_red[7][g];
   }
 
-  // ---- P.V: group r = t>>4 walks rows r, r+16, ...; column chunk c = t&15
-  const int r = t >> 4, c = t & 15;
+  // ---- P.V: group r = t>>4 owns rows r, r+16, ...; column chunk c = t&15
   float acc[G][8];
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[g][e] = 0.f;
-  for (int jj = r; jj < n; jj += 16) {
-    float vf[8];
-    unpack8(*reinterpret_cast<const uint4*>(vb + (size_t)(j0 + jj) * ATT_D + c * 8), vf);
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const float p = s_p[g][jj];
+  for (int i = 0; i < VIT; ++i) {
+    const int jj = r + 16 * i;
+    if (jj < n) {
+      float vf[8];
+      if constexpr (PF >= 1)
+        unpack8(vreg[i], vf);
+      else
+        unpack8(load_v(i), vf);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[g][e] = fmaf(p, vf[e], acc[g][e]);
+      for (int g = 0; g < G; ++g) {
+        const float p = s_p[g][jj];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[g][e] = fmaf(p, vf[e], acc[g][e]);
+      }
     }
   }
   // Cross-group reduction through LDS, one half of D at a time (16 KB for G=4).
@@ -374,6 +430,8 @@ int mivgpu_qk_norm_rope_kv(const void* qkv, const void* qw, const void* kw, cons
   return (int)hipGetLastError();
 }
 
+extern "C" int mivgpu_ops_visible_cus();
+
 // Workspace: o_part = B*Hq*nsplit*128 floats, ml_part = B*Hq*nsplit*2 floats.
 int mivgpu_decode_attention(const void* q, const void* k_cache, const void* v_cache,
                             const int* seqlens, void* out, void* o_part, void* ml_part, int B,
@@ -382,13 +440,39 @@ int mivgpu_decode_attention(const void* q, const void* k_cache, const void* v_ca
   if (head_dim != ATT_D || Hq % Hkv || nsplit <= 0 || B <= 0) return -1;
   const int G = Hq / Hkv;
   dim3 grid(nsplit, Hkv, B);
+  // Load scheduling variant (see the kernel); MIVGPU_ATTN_PF overrides for experiments.
+  static const int pf_env = [] {
+    const char* e = getenv("MIVGPU_ATTN_PF");
+    return e ? atoi(e) : -1;
+  }();
+  // PF=0 keeps the most workgroups resident (5 per CU at G=4): best when the
+  // whole grid fits at once (full MI355X).  When a CU partition must run many
+  // rounds of workgroups (a 64- or 32-CU slice), PF=2 hides HBM latency
+  // inside each workgroup: 90 -> 73 us at 64 CUs, 160 -> 132 us at 32 CUs
+  // (bench/attention.py, profiles/attention_variants.json).
+  static const int cus = mivgpu_ops_visible_cus();
+  const int resident0 = G <= 2 ? 8 : (G == 4 ? 5 : 3);
+  const int pf = pf_env >= 0 ? pf_env : ((long long)grid.x * grid.y * grid.z > (long long)cus * resident0 ? 2 : 0);
+#define MIVGPU_ATTN_LAUNCH(GG, PP)                                                                          \
+  hipLaunchKernelGGL((decode_attn_partial_kernel<GG, PP>), grid, dim3(256), 0, s, (const bf16_t*)q,        \
+                     (const bf16_t*)k_cache, (const bf16_t*)v_cache, seqlens, (float*)o_part,              \
+                     (float*)ml_part, Hq, Hkv, max_ctx, nsplit, scale)
+#define MIVGPU_ATTN_G(GG)                            \
+  case GG:                                           \
+    if (pf == 1) MIVGPU_ATTN_LAUNCH(GG, 1);          \
+    else if (pf == 2) MIVGPU_ATTN_LAUNCH(GG, 2);     \
+    else MIVGPU_ATTN_LAUNCH(GG, 0);                  \
+    break;
   switch (G) {
-    case 1: hipLaunchKernelGGL(decode_attn_partial_kernel<1>, grid, dim3(256), 0, s, (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, seqlens, (float*)o_part, (float*)ml_part, Hq, Hkv, max_ctx, nsplit, scale); break;
-    case 2: hipLaunchKernelGGL(decode_attn_partial_kernel<2>, grid, dim3(256), 0, s, (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, seqlens, (float*)o_part, (float*)ml_part, Hq, Hkv, max_ctx, nsplit, scale); break;
-    case 4: hipLaunchKernelGGL(decode_attn_partial_kernel<4>, grid, dim3(256), 0, s, (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, seqlens, (float*)o_part, (float*)ml_part, Hq, Hkv, max_ctx, nsplit, scale); break;
-    case 8: hipLaunchKernelGGL(decode_attn_partial_kernel<8>, grid, dim3(256), 0, s, (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, seqlens, (float*)o_part, (float*)ml_part, Hq, Hkv, max_ctx, nsplit, scale); break;
-    default: return -2;
+    MIVGPU_ATTN_G(1)
+    MIVGPU_ATTN_G(2)
+    MIVGPU_ATTN_G(4)
+    MIVGPU_ATTN_G(8)
+    default:
+      return -1;
   }
+#undef MIVGPU_ATTN_G
+#undef MIVGPU_ATTN_LAUNCH
   hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(Hq, B), dim3(ATT_D), 0, s,
                      (const float*)o_part, (const float*)ml_part, (bf16_t*)out, Hq, nsplit);
   return (int)hipGetLastError();
@@ -405,5 +489,42 @@ int mivgpu_silu_mul(const void* gate_up, void* out, int rows, int inter, hipStre
 }
 
 int mivgpu_ops_attn_split() { return ATT_SPLIT; }
+
+// CUs this process can run on: the HSA_CU_MASK bits of the current device
+// (a vGPU slice's partition, "i:lo-hi,..;j:..") or, without a mask, the
+// device's CU count.  Kernel variants whose best schedule depends on the
+// number of resident workgroups per CU key off this.
+int mivgpu_ops_visible_cus() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  const char* m = getenv("HSA_CU_MASK");
+  if (m && *m) {
+    const char* p = m;
+    while (*p) {
+      char* end = nullptr;
+      const long idx = strtol(p, &end, 10);
+      if (end == p || *end != ':') break;
+      p = end + 1;
+      int count = 0;
+      while (*p && *p != ';') {
+        const long lo = strtol(p, &end, 10);
+        if (end == p) break;
+        long hi = lo;
+        p = end;
+        if (*p == '-') {
+          hi = strtol(p + 1, &end, 10);
+          p = end;
+        }
+        if (hi >= lo) count += (int)(hi - lo + 1);
+        if (*p == ',') ++p;
+      }
+      if (idx == dev && count > 0) return count;
+      if (*p == ';') ++p;
+    }
+  }
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  return cus;
+}
 
 }  // extern "C"

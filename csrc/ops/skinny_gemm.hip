@@ -307,19 +307,28 @@ hipError_t launch_mt(int mt, int ks, const Args& a, hipStream_t s) {
 
 int mt_of(int M) { return M <= 32 ? 1 : (M <= 64 ? 2 : 4); }
 
+}  // namespace
+extern "C" int mivgpu_ops_visible_cus();   // model_ops.hip
+namespace {
+
 // Default plan, from bench/gemm.py --sweep on MI355X (profiles/gemm):
 //  * nt = 2 (X fragments reused twice) once there are >= 384 tile pairs;
 //  * many groups (gate_up, lm_head): single-wave workgroups, no split (12
 //    independent waves per CU hide each other's prologue/epilogue);
 //  * few groups (qkv 192, o/down 128): 2 waves per workgroup, and S = 2 when
 //    <= 128 groups so that more CUs stream.
+//  * a CU partition of <= 96 CUs (a vGPU slice): nt = 2, 2 waves per
+//    workgroup, no inter-workgroup split (down 68 -> 57 us, o_proj 27 -> 25 us
+//    at 64 CUs vs hipBLASLt; splitting only adds combine traffic there).
 void plan(int M, int K, int N, int epi, int* nt, int* ks, int* S) {
+  static const int cus = mivgpu_ops_visible_cus();
   const int mt = mt_of(M);
+  const bool slice = cus <= 96;
   if (epi == EPI_SILU_MUL) *nt = 2;
-  if (*nt != 1 && *nt != 2) *nt = (mt < 4 && (N / 64) >= 384) ? 2 : 1;
+  if (*nt != 1 && *nt != 2) *nt = (mt < 4 && ((N / 64) >= 384 || (slice && (N / 64) >= 32))) ? 2 : 1;
   const int groups = (N / 32) / *nt, KB = K / 64;
-  if (*ks <= 0) *ks = groups >= 384 ? 1 : 2;
-  if (*S <= 0) *S = (groups <= 128 && KB >= 4 * *ks) ? 2 : 1;
+  if (*ks <= 0) *ks = slice ? 2 : (groups >= 384 ? 1 : 2);
+  if (*S <= 0) *S = (!slice && groups <= 128 && KB >= 4 * *ks) ? 2 : 1;
 }
 
 }  // namespace

@@ -111,10 +111,15 @@ class Qwen3Decoder:
             skinny = os.environ.get("MIVGPU_SKINNY_GEMM", "1") != "0"
             skinny = skinny and self.native and batch <= 32 and shapes_ok
         self.skinny = skinny
+        # gate_up (+SiLU) on the skinny kernel only with >= 128 CUs: in a
+        # 64-CU slice hipBLASLt streams this 201 MB shape faster (78 vs 101 us,
+        # profiles/gemm_cu64.json) while down / lm_head still win.
+        self.skinny_gate_up = skinny and ops.visible_cus() >= 128
         if self.skinny:
             # Keep only the packed copies (no duplicate 16 GB of weights).
             for lw in self.w.layers:
-                lw["pgu"] = ops.PackedLinear(lw.pop("wgu"), silu_mul=True)
+                if self.skinny_gate_up:
+                    lw["pgu"] = ops.PackedLinear(lw.pop("wgu"), silu_mul=True)
                 lw["pd"] = ops.PackedLinear(lw.pop("wd"))
             self.p_lm = ops.PackedLinear(self.w.lm_head)
             if not cfg.tie_embeddings:
@@ -189,7 +194,10 @@ class Qwen3Decoder:
             else:
                 self.h.copy_(ref.add_rmsnorm(o, self.res, lw["ln2"], cfg.eps))
             if self.skinny:
-                lw["pgu"](self.h, out=self.act)          # gate_up GEMM + SiLU*up epilogue
+                if self.skinny_gate_up:
+                    lw["pgu"](self.h, out=self.act)      # gate_up GEMM + SiLU*up epilogue
+                else:
+                    ops.silu_mul(F.linear(self.h, lw["wgu"]), out=self.act)
                 d = lw["pd"](self.act, out=self.mlp_out)
             else:
                 gu = F.linear(self.h, lw["wgu"])

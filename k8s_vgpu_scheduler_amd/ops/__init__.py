@@ -54,7 +54,7 @@ def lib():
                    "mivgpu_decode_attention", "mivgpu_silu_mul", "mivgpu_ops_attn_split",
                    "mivgpu_hwid_probe", "mivgpu_pack_weight", "mivgpu_skinny_gemm",
                    "mivgpu_skinny_max_m", "mivgpu_skinny_plan", "mivgpu_mfma_burn",
-                   "mivgpu_stream_copy", "mivgpu_stream_read"):
+                   "mivgpu_stream_copy", "mivgpu_stream_read", "mivgpu_ops_visible_cus"):
             getattr(L, fn).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -112,6 +112,11 @@ def qk_norm_rope_kv(qkv, q_norm_w, k_norm_w, pos, q_out, k_cache, v_cache, n_q_h
     _check(lib().mivgpu_qk_norm_rope_kv(_p(qkv), _p(q_norm_w), _p(k_norm_w), _p(pos), _p(q_out),
                                         _p(k_cache), _p(v_cache), B, n_q_heads, n_kv_heads, head_dim,
                                         max_ctx, eps, theta, _stream()), "qk_norm_rope_kv")
+
+
+def visible_cus() -> int:
+    """CUs this process runs on (its HSA_CU_MASK partition, else the whole GPU)."""
+    return int(lib().mivgpu_ops_visible_cus())
 
 
 def attn_split() -> int:

@@ -149,3 +149,39 @@ def test_decoder_graph_replay_advances_state():
         d.step()
     torch.cuda.synchronize()
     assert torch.equal(d.pos, p0 + 3)
+
+
+_ATTN_CHILD = r"""
+import math, torch
+from k8s_vgpu_scheduler_amd import ops
+from k8s_vgpu_scheduler_amd.ops import reference as ref
+B, Hq, Hkv, D, T = 5, 32, 8, 128, 700
+k = torch.randn(B, Hkv, T, D, device="cuda").bfloat16()
+v = torch.randn(B, Hkv, T, D, device="cuda").bfloat16()
+q = torch.randn(B, Hq, D, device="cuda").bfloat16()
+seqlens = torch.tensor([1, 255, 256, 513, 700], dtype=torch.int32, device="cuda")
+nsplit = math.ceil(T / ops.attn_split())
+out = torch.empty(B, Hq * D, device="cuda", dtype=torch.bfloat16)
+o_part = torch.empty(B * Hq * nsplit * D, device="cuda")
+ml = torch.empty(B * Hq * nsplit * 2, device="cuda")
+ops.decode_attention(q, k, v, seqlens, out, o_part, ml, Hq, Hkv, D, nsplit, 1 / math.sqrt(D))
+exp = ref.decode_attention(q, k, v, seqlens, Hq, Hkv, D, 1 / math.sqrt(D)).view(B, -1)
+print("ERR", ((out.float() - exp).abs().max() / exp.abs().max()).item())
+"""
+
+
+@pytest.mark.parametrize("pf", ["0", "1", "2"])
+@pytest.mark.parametrize("mask", ["", "0:0-63"])
+def test_decode_attention_load_variants(pf, mask):
+    import os
+    import subprocess
+    import sys
+
+    env = dict(os.environ, MIVGPU_ATTN_PF=pf)
+    env.pop("HSA_CU_MASK", None)
+    if mask:
+        env["HSA_CU_MASK"] = mask
+    r = subprocess.run([sys.executable, "-c", _ATTN_CHILD], env=env, capture_output=True, text=True, timeout=300)
+    line = next((x for x in r.stdout.splitlines() if x.startswith("ERR ")), None)
+    assert r.returncode == 0 and line, r.stderr[-800:]
+    assert float(line.split()[1]) < 2e-2
