@@ -180,7 +180,10 @@ constexpr int ATT_D = 128;
 // PF (load scheduling): 0 = one dependent K / V load per loop trip (lowest
 // VGPRs, highest occupancy); 1 = every K and V load of the thread issued up
 // front; 2 = K up front, V issued right after the scores (before the softmax
-// barrier).  Chosen per launch by mivgpu_decode_attention (measured).
+// barrier).  Chosen per launch by mivgpu_decode_attention (measured).  A
+// streaming flash-decoding variant (one workgroup walking 64/128-key blocks
+// with an online softmax and double-buffered K/V) measured 2x slower in a
+// 64-CU slice: profiles/attention_streaming_negative.json.
 template <int G, int PF>
 __global__ void __launch_bounds__(256)
 decode_attn_partial_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k_cache,
@@ -368,13 +371,14 @@ decode_attn_partial_kernel(const bf16_t* __restrict__ q, const bf16_t* __restric
 // grid = (Hq, B), 128 threads (one per output dim).
 __global__ void __launch_bounds__(128)
 decode_attn_combine_kernel(const float* __restrict__ o_part, const float* __restrict__ ml_part,
-                           bf16_t* __restrict__ out, int Hq, int nsplit) {
+                           bf16_t* __restrict__ out, int Hq, int nsplit, int count) {
+  // nsplit = workspace stride, count = splits actually written (<= nsplit)
   const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
   const size_t base = (size_t)b * Hq + h;
   float M = -INFINITY;
-  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ml_part[(base * nsplit + s) * 2]);
+  for (int s = 0; s < count; ++s) M = fmaxf(M, ml_part[(base * nsplit + s) * 2]);
   float num = 0.f, den = 0.f;
-  for (int s = 0; s < nsplit; ++s) {
+  for (int s = 0; s < count; ++s) {
     const float ms = ml_part[(base * nsplit + s) * 2];
     if (ms == -INFINITY) continue;
     const float w = __expf(ms - M);
@@ -474,7 +478,7 @@ int mivgpu_decode_attention(const void* q, const void* k_cache, const void* v_ca
 #undef MIVGPU_ATTN_G
 #undef MIVGPU_ATTN_LAUNCH
   hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(Hq, B), dim3(ATT_D), 0, s,
-                     (const float*)o_part, (const float*)ml_part, (bf16_t*)out, Hq, nsplit);
+                     (const float*)o_part, (const float*)ml_part, (bf16_t*)out, Hq, nsplit, nsplit);
   return (int)hipGetLastError();
 }
 
