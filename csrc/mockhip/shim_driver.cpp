@@ -11,6 +11,9 @@
 //   usage            mivgpu_process_usage(0) via dlsym
 //   sleep <ms>
 //   device <i>       hipSetDevice
+//   stress <threads> <iters> <max MiB>
+//                    threads doing random hipMalloc/hipFree and
+//                    hipMemCreate/hipMemRelease (sanitizer + race tests)
 #include <hip/hip_runtime_api.h>
 
 #include <dlfcn.h>
@@ -19,7 +22,50 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <atomic>
+#include <random>
+#include <thread>
 #include <vector>
+
+static void stress_thread(int seed, int iters, int max_mib, std::atomic<long>* allocs, std::atomic<long>* ooms,
+                          std::atomic<long>* errors) {
+  std::mt19937 rng(seed);
+  std::vector<void*> bufs;
+  std::vector<hipMemGenericAllocationHandle_t> handles;
+  for (int k = 0; k < iters; ++k) {
+    const int op = rng() % 4;
+    const size_t mib = 1 + rng() % max_mib;
+    if (op == 0 || (op == 1 && bufs.empty())) {
+      void* p = nullptr;
+      hipError_t rc = hipMalloc(&p, mib << 20);
+      if (rc == hipSuccess) { bufs.push_back(p); ++*allocs; }
+      else if (rc == hipErrorOutOfMemory) ++*ooms;
+      else ++*errors;
+    } else if (op == 1) {
+      const size_t i = rng() % bufs.size();
+      if (hipFree(bufs[i]) != hipSuccess) ++*errors;
+      bufs[i] = bufs.back();
+      bufs.pop_back();
+    } else if (op == 2 || handles.empty()) {
+      hipMemGenericAllocationHandle_t h{};
+      hipMemAllocationProp prop{};
+      prop.type = hipMemAllocationTypePinned;
+      prop.location.type = hipMemLocationTypeDevice;
+      prop.location.id = 0;
+      hipError_t rc = hipMemCreate(&h, mib << 20, &prop, 0);
+      if (rc == hipSuccess) { handles.push_back(h); ++*allocs; }
+      else if (rc == hipErrorOutOfMemory) ++*ooms;
+      else ++*errors;
+    } else {
+      const size_t i = rng() % handles.size();
+      if (hipMemRelease(handles[i]) != hipSuccess) ++*errors;
+      handles[i] = handles.back();
+      handles.pop_back();
+    }
+  }
+  for (void* p : bufs) if (hipFree(p) != hipSuccess) ++*errors;
+  for (auto h : handles) if (hipMemRelease(h) != hipSuccess) ++*errors;
+}
 
 extern "C" hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_tR0600*, int);
 
@@ -79,6 +125,16 @@ int main(int argc, char** argv) {
       printf("{\"op\":\"usage\",\"bytes\":%lld}\n", f ? f(0) : -2ll);
     } else if (!strcmp(c, "sleep")) {
       usleep((useconds_t)strtoul(argv[++i], nullptr, 10) * 1000);
+    } else if (!strcmp(c, "stress")) {
+      const int nt = atoi(argv[++i]), iters = atoi(argv[++i]), max_mib = atoi(argv[++i]);
+      std::atomic<long> allocs{0}, ooms{0}, errors{0};
+      std::vector<std::thread> ts;
+      for (int k = 0; k < nt; ++k)
+        ts.emplace_back(stress_thread, (int)getpid() * 131 + k, iters, max_mib, &allocs, &ooms, &errors);
+      for (auto& t : ts) t.join();
+      auto f = (long long (*)(int))dlsym(RTLD_DEFAULT, "mivgpu_process_usage");
+      printf("{\"op\":\"stress\",\"allocs\":%ld,\"ooms\":%ld,\"errors\":%ld,\"usage_after\":%lld}\n",
+             allocs.load(), ooms.load(), errors.load(), f ? f(0) : -2ll);
     } else if (!strcmp(c, "device")) {
       int d = atoi(argv[++i]);
       printf("{\"op\":\"device\",\"rc\":%d}\n", (int)hipSetDevice(d));

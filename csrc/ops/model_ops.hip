@@ -174,7 +174,10 @@ qk_norm_rope_kv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict_
 //   P.V   : 16 lanes per key row (8 dims each, one 16-B load), 16 rows at once
 // Partials (unnormalised O, running max m, sum l) go to fp32 workspace; the
 // combine kernel merges splits.  G <= 8 supported (Qwen3-8B: G = 4).
-constexpr int ATT_SPLIT = 256;
+#ifndef MIVGPU_ATT_SPLIT
+#define MIVGPU_ATT_SPLIT 256
+#endif
+constexpr int ATT_SPLIT = MIVGPU_ATT_SPLIT;   // keys per partial workgroup
 constexpr int ATT_D = 128;
 
 // PF (load scheduling): 0 = one dependent K / V load per loop trip (lowest

@@ -16,7 +16,8 @@ from pathlib import Path
 
 import torch
 
-_LIB_PATH = Path(__file__).resolve().parents[1] / "lib" / "libmivgpu_ops.so"
+# MIVGPU_OPS_LIB points experiments at an alternative build of the same library.
+_LIB_PATH = Path(os.environ.get("MIVGPU_OPS_LIB") or Path(__file__).resolve().parents[1] / "lib" / "libmivgpu_ops.so")
 _lib = None
 
 
