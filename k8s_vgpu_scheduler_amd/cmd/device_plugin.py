@@ -15,6 +15,7 @@ import json
 import logging
 import os
 import shutil
+import signal
 import threading
 from pathlib import Path
 
@@ -111,6 +112,8 @@ def main(argv=None):
     reg = Registrar(backend, cfg, a.node_name)
     threading.Thread(target=reg.watch_and_register, name="register", daemon=True).start()
     reload = threading.Event()
+    # SIGHUP: re-register with the kubelet (reference: main.go:305-337)
+    signal.signal(signal.SIGHUP, lambda *_: reload.set())
     if a.enable_partition_manager or cfg.partitions:
         from k8s_vgpu_scheduler_amd.deviceplugin.partition import PartitionManager
 

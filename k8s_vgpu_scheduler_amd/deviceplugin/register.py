@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import datetime as _dt
 import logging
+import os
 import threading
 
 from k8s_vgpu_scheduler_amd.device import codec
@@ -55,7 +56,10 @@ class Registrar:
         devs = api_devices(self.backend, gpus, self.cfg)
         annos = {REGISTER_ANNOS: codec.marshal_node_devices(devs)}
         fg = filtered(gpus, self.cfg)
-        if len(fg) > 1:
+        # ENABLE_TOPOLOGY_SCORE (reference register.go:279): on by default for
+        # MI355X, whose xGMI pair scores drive multi-GPU placement
+        topo = os.environ.get("ENABLE_TOPOLOGY_SCORE", "true").strip().lower() not in ("0", "false", "no")
+        if topo and len(fg) > 1:
             scores = pair_scores(self.backend, fg)
             bad = topology.is_asymmetric(scores)
             if bad:

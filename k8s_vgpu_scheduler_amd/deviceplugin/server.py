@@ -145,7 +145,12 @@ class AMDDevicePlugin:
                 self._cv.notify_all()
 
     def health_loop(self, period: float = 5.0):
-        disabled = os.environ.get("DP_DISABLE_HEALTHCHECKS", "") in ("all", "*")
+        # DP_DISABLE_HEALTHCHECKS: "all" / "*" or a list of checks ("ecc");
+        # DP_ENABLE_HEALTHCHECKS re-enables listed ones (reference rm/health.go:46-55)
+        off = {x.strip().lower() for x in os.environ.get("DP_DISABLE_HEALTHCHECKS", "").split(",") if x.strip()}
+        on = {x.strip().lower() for x in os.environ.get("DP_ENABLE_HEALTHCHECKS", "").split(",") if x.strip()}
+        disabled = bool(off & {"all", "*"}) and not on
+        self.backend.skip_checks = (off - on) - {"all", "*"}
         from k8s_vgpu_scheduler_amd.deviceplugin.partition import is_applying
 
         while not self._stop.wait(period):

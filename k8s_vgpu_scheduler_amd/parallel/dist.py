@@ -46,6 +46,11 @@ def init_distributed(backend: str | None = None, timeout_s: float = 600.0) -> Di
         import datetime
 
         kw = {"device_id": device} if backend == "nccl" else {}
+        # MIVGPU_DIST_INIT (e.g. file:///tmp/rdzv) overrides env:// rendezvous:
+        # tests use a file store so parallel runs never race for a TCP port
+        init = os.environ.get("MIVGPU_DIST_INIT")
+        if init:
+            kw["init_method"] = init
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return DistEnv(rank, world, local, backend, device)

@@ -51,6 +51,10 @@ class SchedulerCollector:
         overview = _g("hami_node_gpu_overview", "GPU overview on a certain node",
                       ["node", "device_uuid", "device_index", "device_cores", "device_memory_limit", "device_type"])
         mem_pct = _g("hami_node_gpu_memory_allocated_ratio", "GPU memory allocated ratio on a certain node", dl)
+        # MI355X counterpart of hami_node_gpu_mig_instance_info: one series per
+        # compute-partition device (mode dpx/qpx/cpx), value = its CU count
+        part = _g("hami_node_gpu_partition_info", "Compute-partition devices (SPX/DPX/QPX/CPX) on a node",
+                  ["node", "device_uuid", "device_index", "mode", "device_type"])
         legacy = []
         if self.legacy:
             ll = ["nodeid", "deviceuuid", "deviceidx", "devicetype"]
@@ -71,11 +75,13 @@ class SchedulerCollector:
                                     mib_to_bytes(d.usedmem))
                 if d.totalmem > 0:
                     mem_pct.add_metric([node_id, d.id, idx, d.type, ZONE], d.usedmem / d.totalmem)
+                if d.mode and d.mode != "hami-core":
+                    part.add_metric([node_id, d.id, idx, d.mode, d.type, ZONE], float(d.totalcore))
                 if self.legacy:
                     legacy[0].add_metric([node_id, d.id, idx, d.type, ZONE], mib_to_bytes(d.totalmem))
                     legacy[1].add_metric([node_id, d.id, idx, d.type, ZONE], float(d.totalcore))
                     legacy[2].add_metric([node_id, d.id, idx, d.type, ZONE], float(d.used))
-        yield from (mem_limit, core_limit, mem_alloc, shared, core_alloc, overview, mem_pct, *legacy)
+        yield from (mem_limit, core_limit, mem_alloc, shared, core_alloc, overview, mem_pct, part, *legacy)
 
         q_used = _g("hami_resource_quota_used", "resource quota used", ["namespace", "quota_name", "limit"])
         q_limit = _g("hami_resource_quota_limit", "resource quota limit", ["namespace", "quota_name"])

@@ -21,7 +21,8 @@ def _free_port() -> int:
 
 def _worker(rank, world, port, out, extra):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
-                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                       "MIVGPU_DIST_INIT": f"file://{out}.rdzv"})
     rc = C.main(["--backend", "gloo", "--max-bytes", str(64 << 10), "--iters", "3", "--warmup", "1",
                  "--out", out, *extra])
     if rc != 0:

@@ -152,3 +152,16 @@ def test_parse_request():
     assert P.parse_request("") == {}
     with pytest.raises(ValueError):
         P.parse_request("0=NPS2")
+
+
+def test_partition_metric_and_topology_env(env, monkeypatch):
+    from k8s_vgpu_scheduler_amd.scheduler.metrics import SchedulerCollector
+    c, sched, backend, cfg, reg, _ = env
+    fams = {f.name: f for f in SchedulerCollector(sched).collect()}
+    samples = fams["hami_node_gpu_partition_info"].samples
+    assert len(samples) == 8 and all(s.labels["mode"] == "cpx" and s.value == 32 for s in samples)
+    from k8s_vgpu_scheduler_amd.device.amd.device import PAIR_SCORE_ANNOS
+    monkeypatch.setenv("ENABLE_TOPOLOGY_SCORE", "false")
+    assert PAIR_SCORE_ANNOS not in reg.annotations(backend.gpus())
+    monkeypatch.delenv("ENABLE_TOPOLOGY_SCORE")
+    assert PAIR_SCORE_ANNOS in reg.annotations(backend.gpus())
