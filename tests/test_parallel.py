@@ -45,7 +45,8 @@ def test_collectives_exact_on_gloo(world, tmp_path):
     assert doc["all_correct"]
     for r in doc["results"]:
         assert r["bytes"] % (4 * world) == 0
-        assert r["busbw_gbps"] == pytest.approx(r["algbw_gbps"] * C.BUS_FACTOR[r["op"]](world), rel=1e-2, abs=1e-3)
+        # both figures are rounded to 3 decimals: allow that rounding
+        assert r["busbw_gbps"] == pytest.approx(r["algbw_gbps"] * C.BUS_FACTOR[r["op"]](world), rel=1e-2, abs=2.5e-3)
 
 
 def test_placement_verdict_fails_below_expectation(tmp_path):
