@@ -6,6 +6,7 @@ OOM, shared-region accounting read by vGPUmonitor, SM-limit duty cycling) and
 the CU-partition placement that replaces MPS/MIG on MI355X.
 """
 
+import json
 import os
 import tempfile
 
@@ -78,3 +79,55 @@ def test_shim_overhead_unlimited(tmp):
                   ["--n", "8192", "--iters", "100"])
     assert base["rc"] == 0 and r["rc"] == 0
     assert r["tflops"] >= 0.97 * base["tflops"], (r["tflops"], base["tflops"])
+
+
+_IPC_CHILD = r"""
+import os, sys, json
+import torch
+import torch.multiprocessing as mp
+
+
+def consumer(q, done):
+    t = q.get()                                  # opened through hipIpcOpenMemHandle
+    ok = bool(torch.equal(t, torch.arange(1 << 20, device="cuda", dtype=torch.float32)))
+    t.mul_(2)                                    # write through the shared mapping
+    torch.cuda.synchronize()
+    done.put(ok)
+
+
+if __name__ == "__main__":
+    mp.set_start_method("spawn")
+    q, done = mp.Queue(), mp.Queue()
+    p = mp.Process(target=consumer, args=(q, done))
+    p.start()
+    t = torch.arange(1 << 20, device="cuda", dtype=torch.float32)
+    q.put(t)
+    ok = done.get(timeout=120)
+    p.join(timeout=120)
+    torch.cuda.synchronize()
+    seen = bool(torch.equal(t, 2 * torch.arange(1 << 20, device="cuda", dtype=torch.float32)))
+    print("IPC " + json.dumps({"consumer_ok": ok, "writeback_seen": seen, "rc": p.exitcode}), flush=True)
+"""
+
+
+def test_cuda_ipc_works_under_shim(tmp):
+    """The reference's libvgpu breaks CUDA IPC (examples/nvidia/vllm_cross_vgpu.yaml:99-102);
+    hipIpcGetMemHandle/hipIpcOpenMemHandle must keep working under libmivgpu.so so
+    RCCL and PyTorch tensor sharing do."""
+    import subprocess
+    import sys
+
+    from k8s_vgpu_scheduler_amd.shim import shim_env
+
+    script = os.path.join(tmp, "ipc_child.py")
+    with open(script, "w") as f:
+        f.write(_IPC_CHILD)
+    env = dict(os.environ)
+    env.update(shim_env())
+    env.update({"MIVGPU_SHARED_CACHE": os.path.join(tmp, "ipc.cache"), "HIP_DEVICE_MEMORY_LIMIT_0": "8192m",
+                "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    r = subprocess.run([sys.executable, script], env=env, capture_output=True, text=True, timeout=300)
+    line = next((x for x in r.stdout.splitlines() if x.startswith("IPC ")), None)
+    assert r.returncode == 0 and line, r.stderr[-2000:]
+    res = json.loads(line[4:])
+    assert res == {"consumer_ok": True, "writeback_seen": True, "rc": 0}, res
