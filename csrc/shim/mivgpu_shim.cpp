@@ -85,6 +85,63 @@ inline uint64_t coarse_ns() {
   return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
 
+// ------------------------------------------------------------------ roctx --
+// MIVGPU_ROCTX=1 puts the shim's own decisions on the profiler timeline
+// (rocprofv3 --marker-trace), next to the tenant's kernels: OOM denials, host
+// spills, governor gates, priority parking.  The library is dlopen'ed only
+// when asked for, so the default path carries one null-pointer test.
+struct Roctx {
+  void (*mark)(const char*) = nullptr;
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+};
+Roctx g_roctx;
+
+void roctx_init(const char* hip_dir) {
+  const char* on = getenv("MIVGPU_ROCTX");
+  if (!on || !(!strcmp(on, "1") || !strcasecmp(on, "true"))) return;
+  const char* lib = getenv("MIVGPU_ROCTX_LIB");
+  void* h = nullptr;
+  if (lib && *lib) {
+    h = dlopen(lib, RTLD_NOW | RTLD_GLOBAL);
+  } else {
+    h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h && hip_dir) {  // next to the HIP runtime (/opt/rocm/lib) when not on the loader path
+      char path[1024];
+      snprintf(path, sizeof(path), "%s/librocprofiler-sdk-roctx.so.1", hip_dir);
+      h = dlopen(path, RTLD_NOW | RTLD_GLOBAL);
+    }
+  }
+  if (!h) {
+    mlog(1, "MIVGPU_ROCTX set but no roctx library could be loaded: %s", dlerror());
+    return;
+  }
+  g_roctx.mark = reinterpret_cast<void (*)(const char*)>(dlsym(h, "roctxMarkA"));
+  g_roctx.push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+  g_roctx.pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+  if (!g_roctx.mark || !g_roctx.push || !g_roctx.pop) g_roctx = Roctx{};
+}
+
+__attribute__((format(printf, 1, 2))) void tmark(const char* fmt, ...) {
+  if (__builtin_expect(!g_roctx.mark, 1)) return;
+  char buf[256];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_roctx.mark(buf);
+}
+
+struct TRange {
+  bool on;
+  explicit TRange(const char* name) : on(g_roctx.push != nullptr) {
+    if (on) g_roctx.push(name);
+  }
+  ~TRange() {
+    if (on) g_roctx.pop();
+  }
+};
+
 // ------------------------------------------------------ re-entrancy guard --
 thread_local int t_depth = 0;
 struct Guard {
@@ -465,6 +522,16 @@ std::atomic<bool> g_ready{false};
 void bootstrap() {
   Guard g;
   load_config();
+  {
+    Dl_info di;
+    char dir[1024] = {0};
+    if (real_hipGetDevice() && dladdr(reinterpret_cast<void*>(real_hipGetDevice()), &di) && di.dli_fname) {
+      snprintf(dir, sizeof(dir), "%s", di.dli_fname);
+      char* slash = strrchr(dir, '/');
+      if (slash) *slash = 0; else dir[0] = 0;
+    }
+    roctx_init(dir[0] ? dir : nullptr);
+  }
   int n = 0;
   if (real_hipGetDeviceCount() && real_hipGetDeviceCount()(&n) == hipSuccess) g_num_devices = n;
   if (g_num_devices > MIVGPU_MAX_DEVICES) g_num_devices = MIVGPU_MAX_DEVICES;
@@ -473,6 +540,9 @@ void bootstrap() {
   }
   atexit(on_exit_release);
   for (int d = 0; d < g_num_devices; ++d) {
+    if (g_cfg.mem_limit[d] || g_cfg.cu_limit < 100 || g_cfg.cu_mask_count[d])
+      tmark("mivgpu:config dev=%d limit_mib=%llu cu_limit=%d cu_mask=%d", d,
+            (unsigned long long)(g_cfg.mem_limit[d] >> 20), g_cfg.cu_limit, g_cfg.cu_mask_count[d]);
     if (g_cfg.mem_limit[d])
       mlog(3, "device %d: HBM limit %llu MiB, CU limit %d%%, CU mask %d CUs", d,
            (unsigned long long)(g_cfg.mem_limit[d] >> 20), g_cfg.cu_limit, g_cfg.cu_mask_count[d]);
@@ -569,6 +639,9 @@ bool reserve(int dev, uint64_t bytes, AllocKind kind) {
       if (n == 0) break;
     }
   }
+  tmark("mivgpu:oom dev=%d req_mib=%llu used_mib=%llu limit_mib=%llu", dev, (unsigned long long)(bytes >> 20),
+        (unsigned long long)(__atomic_load_n(&g_region->dev_used[dev], __ATOMIC_RELAXED) >> 20),
+        (unsigned long long)(lim >> 20));
   mlog(1, "device %d: allocation of %llu MiB exceeds the slice (%llu / %llu MiB in use)", dev,
        (unsigned long long)(bytes >> 20),
        (unsigned long long)(__atomic_load_n(&g_region->dev_used[dev], __ATOMIC_RELAXED) >> 20),
@@ -620,6 +693,7 @@ hipError_t guarded_alloc(void** ptr, uint64_t bytes, Call&& call) {
         if (real_hipHostGetDevicePointer()) real_hipHostGetDevicePointer()(&dptr, h, 0);
         *ptr = dptr;
         track(dptr, bytes, dev, K_HOST_SPILL);
+        tmark("mivgpu:host-spill dev=%d mib=%llu", dev, (unsigned long long)(bytes >> 20));
         return hipSuccess;
       }
     }
@@ -685,6 +759,7 @@ namespace {
 
 bool gate_init_locked(int dev, DeviceGate& G) {
   G.tried = true;
+  TRange r("mivgpu:governor-init");
   if (!real_hipModuleLoadData() || !real_hipModuleGetFunction() || !real_hipModuleLaunchKernel())
     return false;
   if (real_hipModuleLoadData()(&G.module, mivgpu_governor_hsaco) != hipSuccess) {
@@ -752,6 +827,7 @@ void enqueue_gate_locked(int dev, DeviceGate& G, int slot, hipStream_t stream, u
   void* hs = G.host_stats;
   void* args[] = {&state, &hs, &submit_dev, &slot_arg, &rate_ppm, &cap, &hold};
   real_hipModuleLaunchKernel()(G.gate_fn, 1, 1, 1, 64, 1, 1, 0, stream, args, nullptr);
+  tmark("mivgpu:gate dev=%d slot=%d rate_pct=%u", dev, slot, rate_ppm / 10000u);
   S.last_gate_host_ns = now;
   if (g_slot >= 0 && hs) {
     const uint64_t* h = static_cast<const uint64_t*>(hs);
@@ -878,6 +954,7 @@ inline void on_launch(hipStream_t stream) {
   int rk = __atomic_load_n(&g_region->recent_kernel, __ATOMIC_RELAXED);
   if (__builtin_expect(rk < 0, 0)) {
     // Priority blocking requested by the node monitor: park until released.
+    TRange r("mivgpu:priority-block");
     uint64_t t0 = coarse_ns();
     while (__atomic_load_n(&g_region->recent_kernel, __ATOMIC_RELAXED) < 0) {
       usleep(1000);

@@ -19,4 +19,4 @@ def native_build():
     from k8s_vgpu_scheduler_amd.utils import build
     build.build_shim()
     mock_lib, driver = build.build_mock()
-    return {"shim": build.SHIM_SO, "mock_lib": mock_lib, "driver": driver}
+    return {"shim": build.SHIM_SO, "mock_lib": mock_lib, "driver": driver, "roctx": build.MOCK_ROCTX}

@@ -172,3 +172,34 @@ def test_multi_device_limits(native_build, tmp_path):
     assert out[0]["rc"] == 0
     assert out[1]["rc"] == 2 and out[2]["total_mib"] == 500
     assert out[4]["rc"] == 0
+
+
+def test_roctx_markers_for_shim_decisions(native_build, tmp_path):
+    """MIVGPU_ROCTX=1: OOM denials, host spills and priority
+    parking show up as roctx markers/ranges; without it nothing is emitted."""
+    trace = tmp_path / "roctx.txt"
+    env = {"HIP_DEVICE_MEMORY_LIMIT_0": "1000m", "MIVGPU_ROCTX": "1",
+           "MIVGPU_ROCTX_LIB": str(native_build["roctx"]), "MOCK_ROCTX_OUT": str(trace)}
+    out = run(native_build, tmp_path, "alloc", 800, "alloc", 800, env=env)
+    assert out[0]["rc"] == 0 and out[1]["rc"] == 2
+    lines = trace.read_text().splitlines()
+    assert "mark mivgpu:config dev=0 limit_mib=1000 cu_limit=100 cu_mask=0" in lines
+    assert "mark mivgpu:oom dev=0 req_mib=800 used_mib=800 limit_mib=1000" in lines
+    run(native_build, tmp_path, "alloc", 800, "alloc", 800, cache="s.cache",
+        env={**env, "MIVGPU_OVERSUBSCRIBE": "true"})
+    assert "mark mivgpu:host-spill dev=0 mib=800" in trace.read_text().splitlines()
+    # priority parking is a range around the wait
+    path = tmp_path / "p.cache"
+    R.SharedRegion.create(str(path)).close()
+    reg = R.SharedRegion(str(path))
+    reg.set_recent_kernel(-1)
+    threading.Timer(0.3, lambda: reg.set_recent_kernel(0)).start()
+    trace.unlink()
+    run(native_build, tmp_path, "launch", 2, cache="p.cache", env=env)
+    lines = trace.read_text().splitlines()
+    assert lines.count("push mivgpu:priority-block") == 1 and lines.count("pop ") == 1
+    reg.close()
+    trace.unlink()
+    run(native_build, tmp_path, "alloc", 800, "alloc", 800, cache="q.cache",
+        env={**env, "MIVGPU_ROCTX": "0"})
+    assert not trace.exists()

@@ -131,3 +131,43 @@ def test_cuda_ipc_works_under_shim(tmp):
     assert r.returncode == 0 and line, r.stderr[-2000:]
     res = json.loads(line[4:])
     assert res == {"consumer_ok": True, "writeback_seen": True, "rc": 0}, res
+
+
+def test_roctx_markers_on_rocprofv3_timeline(tmp):
+    """MIVGPU_ROCTX=1 under rocprofv3 --marker-trace: the shim's decisions
+    (config, governor init, gates, OOM denial) are on the same timeline as
+    the tenant's kernels and the gate kernel."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import sys
+
+    from k8s_vgpu_scheduler_amd.shim import shim_env
+
+    rocprof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    out_dir = os.path.join(tmp, "roctx_prof")
+    env = dict(os.environ)
+    env.update(shim_env())
+    env.update({"MIVGPU_SHARED_CACHE": os.path.join(tmp, "roctx.cache"), "HIP_DEVICE_MEMORY_LIMIT_0": "4096m",
+                "HIP_DEVICE_CORE_LIMIT": "50", "GPU_CORE_UTILIZATION_POLICY": "force", "MIVGPU_ROCTX": "1",
+                "TMPDIR": "/tmp"})
+    cmd = [rocprof, "--marker-trace", "--kernel-trace", "--output-format", "csv", "-d", out_dir, "--",
+           sys.executable, "-m", "k8s_vgpu_scheduler_amd.shim.probe", "--child", "matmul",
+           "--n", "4096", "--iters", "20", "--oom-probe-mib", "5000"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    markers = glob.glob(os.path.join(out_dir, "**", "*marker_api_trace.csv"), recursive=True)
+    kernels = glob.glob(os.path.join(out_dir, "**", "*kernel_trace.csv"), recursive=True)
+    assert markers and kernels, sorted(glob.glob(os.path.join(out_dir, "**"), recursive=True))
+    # rocprofv3 puts a marker's text in the Function column; take every cell so a
+    # column rename cannot hide it
+    rows = [row for f in markers for row in csv.DictReader(open(f))]
+    msgs = [v for row in rows for v in row.values() if isinstance(v, str) and v.startswith("mivgpu:")]
+    assert msgs, rows[:3]
+    assert any(m.startswith("mivgpu:config dev=0 limit_mib=4096 cu_limit=50") for m in msgs), msgs[:20]
+    assert "mivgpu:governor-init" in msgs
+    assert sum(m.startswith("mivgpu:gate dev=0") for m in msgs) > 0
+    assert any(m.startswith("mivgpu:oom dev=0 req_mib=5000") for m in msgs), msgs[:20]
+    names = [row.get("Kernel_Name", "") for f in kernels for row in csv.DictReader(open(f))]
+    assert any("mivgpu_gate" in n for n in names)
