@@ -118,6 +118,7 @@ class AMDDevicePlugin:
         self.gpus: list[GPUInfo] = filtered(backend.gpus(), cfg)
         self.by_uuid = {g.uuid: g for g in self.gpus}
         self.health = {g.uuid: True for g in self.gpus}
+        self.event_unhealthy: dict[str, str] = {}    # uuid -> reason, set by device events
         self._cv = threading.Condition()
         self._gen = 0
         self.apply_mutex = threading.Lock()
@@ -144,23 +145,76 @@ class AMDDevicePlugin:
                 self._gen += 1
                 self._cv.notify_all()
 
+    # event kinds that make a GPU unhealthy by default; "vmfault" is an
+    # application fault (the XID 13/31/43 class the reference skips) and only
+    # counts when DP_ENABLE_HEALTHCHECKS names it
+    FATAL_EVENTS = {"gpu_pre_reset"}
+    APP_EVENTS = {"vmfault"}
+
     def health_loop(self, period: float = 5.0):
-        # DP_DISABLE_HEALTHCHECKS: "all" / "*" or a list of checks ("ecc");
-        # DP_ENABLE_HEALTHCHECKS re-enables listed ones (reference rm/health.go:46-55)
+        """rm/health.go:checkHealth, AMD form: block up to `period` on amd-smi
+        event notifications (the XID event set), then poll RAS/ECC.  A reset
+        event on a physical GPU marks it and all of its compute partitions
+        unhealthy until the post-reset event; an event the backend cannot place
+        marks every GPU.
+
+        DP_DISABLE_HEALTHCHECKS: "all" / "*" or a list of checks ("ecc",
+        "events", "reset"); DP_ENABLE_HEALTHCHECKS re-enables listed ones and can
+        make application faults fatal ("vmfault") (reference rm/health.go:46-55)."""
         off = {x.strip().lower() for x in os.environ.get("DP_DISABLE_HEALTHCHECKS", "").split(",") if x.strip()}
         on = {x.strip().lower() for x in os.environ.get("DP_ENABLE_HEALTHCHECKS", "").split(",") if x.strip()}
         disabled = bool(off & {"all", "*"}) and not on
         self.backend.skip_checks = (off - on) - {"all", "*"}
+        fatal = set(self.FATAL_EVENTS) | (on & self.APP_EVENTS)
+        if "reset" in self.backend.skip_checks:
+            fatal.discard("gpu_pre_reset")
+        use_events = "events" not in self.backend.skip_checks
         from k8s_vgpu_scheduler_amd.deviceplugin.partition import is_applying
 
-        while not self._stop.wait(period):
+        while not self._stop.is_set():
+            events, failed = None, False
+            if use_events and not disabled:
+                try:
+                    events = self.backend.wait_health_events(self.gpus, period)
+                except Exception as e:  # noqa: BLE001 -- health.go: a failed wait marks all devices
+                    log.error("waiting for GPU events failed: %s; marking all devices unhealthy", e)
+                    events, failed = [], True
+                    for g in self.gpus:
+                        self.event_unhealthy[g.uuid] = f"event wait failed: {e}"
+                    self._stop.wait(period)
+            if events is None and self._stop.wait(period):
+                break
+            if self._stop.is_set():
+                break
             if disabled or is_applying():    # a partition reconfiguration is resetting GPUs
                 continue
+            if events is not None and not failed:
+                # a wait that works again clears the marks a failed one left
+                for u in [u for u, r in self.event_unhealthy.items() if r.startswith("event wait failed")]:
+                    del self.event_unhealthy[u]
+            for ev in events or ():
+                self._apply_event(ev, fatal)
             for g in self.gpus:
                 ok, why = self.backend.health(g)
+                if ok and g.uuid in self.event_unhealthy:
+                    ok, why = False, self.event_unhealthy[g.uuid]
                 if not ok and self.health.get(g.uuid, True):
                     log.error("GPU %s unhealthy: %s", g.uuid, why)
                 self.set_health(g.uuid, ok)
+
+    def _apply_event(self, ev, fatal: set):
+        targets = [g for g in self.gpus if ev.physical is None or g.physical == ev.physical]
+        if ev.kind == "gpu_post_reset":
+            for g in targets:
+                if self.event_unhealthy.pop(g.uuid, None) is not None:
+                    log.info("GPU %s back after reset", g.uuid)
+            return
+        if ev.kind not in fatal:
+            log.info("skipping GPU event %s on %s: %s", ev.kind,
+                     "all" if ev.physical is None else ev.physical, ev.message)
+            return
+        for g in targets:
+            self.event_unhealthy[g.uuid] = f"{ev.kind}: {ev.message}".rstrip(": ")
 
     # ----------------------------------------------------------- gRPC API
     def GetDevicePluginOptions(self, request, context):  # noqa: N802

@@ -16,6 +16,8 @@ from __future__ import annotations
 import logging
 import os
 import re
+import threading
+import time
 from dataclasses import dataclass, field
 from pathlib import Path
 
@@ -64,9 +66,28 @@ class LinkInfo:
     max_bw_gbps: float | None = None
 
 
+@dataclass
+class HealthEvent:
+    """One amd-smi event notification (the AMD analog of an NVML XID event).
+    ``kind`` is the lower-case AmdSmiEvtNotificationType name; ``physical`` is
+    the physical GPU index it was raised on (None: unknown device)."""
+    kind: str
+    physical: int | None
+    message: str = ""
+
+
+# kinds the device plugin subscribes to (AmdSmiEvtNotificationType names)
+HEALTH_EVENT_KINDS = ("vmfault", "thermal_throttle", "gpu_pre_reset", "gpu_post_reset")
+
+
 class Backend:
     name = "base"
     skip_checks: set = set()     # health checks disabled via DP_DISABLE_HEALTHCHECKS
+
+    def wait_health_events(self, gpus: list[GPUInfo], timeout_s: float) -> list[HealthEvent] | None:
+        """Block up to ``timeout_s`` for device events.  None = this backend has
+        no event source (the caller sleeps and polls instead)."""
+        return None
 
     def gpus(self) -> list[GPUInfo]:
         raise NotImplementedError
@@ -108,7 +129,29 @@ def pair_scores(backend: Backend, gpus: list[GPUInfo]) -> dict[str, dict[str, in
     return out
 
 
+def _group_physical(out: list[GPUInfo]) -> list[GPUInfo]:
+    """Partitions of one physical GPU share domain:bus:device and differ in
+    the PCI function: number the physical GPUs and the partitions inside each."""
+    phys: dict[str, int] = {}
+    for g in out:
+        key = g.bdf.rsplit(".", 1)[0] if g.bdf else f"idx{g.index}"
+        g.partition_index = sum(1 for o in out[: g.index] if (o.bdf.rsplit(".", 1)[0] if o.bdf else "") == key)
+        g.physical_index = phys.setdefault(key, len(phys))
+    return out
+
+
 # ------------------------------------------------------------------- amd-smi
+def _handle_key(h) -> int | None:
+    """amd-smi processor handles come back as ctypes pointers or plain ints."""
+    if h is None:
+        return None
+    v = getattr(h, "value", h)
+    try:
+        return int(v) if v is not None else None
+    except (TypeError, ValueError):
+        return None
+
+
 class AmdSmiBackend(Backend):
     name = "amdsmi"
 
@@ -147,13 +190,7 @@ class AmdSmiBackend(Backend):
                         compute_partition=str(part))
             self._by_uuid[g.uuid] = h
             out.append(g)
-        # partitions of one physical GPU share domain:bus:device, differ in function
-        phys: dict[str, int] = {}
-        for g in out:
-            key = g.bdf.rsplit(".", 1)[0] if g.bdf else f"idx{g.index}"
-            g.partition_index = sum(1 for o in out[: g.index] if (o.bdf.rsplit(".", 1)[0] if o.bdf else "") == key)
-            g.physical_index = phys.setdefault(key, len(phys))
-        return out
+        return _group_physical(out)
 
     def set_compute_partition(self, physical_index: int, mode: str) -> None:
         mode = mode.upper()
@@ -197,6 +234,50 @@ class AmdSmiBackend(Backend):
             return LinkInfo(tname, int(lt.get("hops", 1) or 1), 1, bw)
         except Exception:  # noqa: BLE001
             return LinkInfo("NONE", 0, 0)
+
+    def wait_health_events(self, gpus, timeout_s):
+        m = self.m
+        if getattr(self, "_evt_handles", None) is None:
+            # one registration per physical GPU (partitions share the package's events)
+            self._evt_handles = {}
+            mask = 0
+            for k in HEALTH_EVENT_KINDS:
+                mask |= 1 << (int(getattr(m.AmdSmiEvtNotificationType, k.upper())) - 1)
+            for g in gpus:
+                if g.physical in self._evt_handles.values():
+                    continue
+                h = self._h(g)
+                try:
+                    m.amdsmi_init_gpu_event_notification(h)
+                    m.amdsmi_set_gpu_event_notification_mask(h, mask)
+                    self._evt_handles[_handle_key(h)] = g.physical
+                except Exception as e:  # noqa: BLE001 -- e.g. no permission on /dev/kfd events
+                    log.warning("GPU %s: amd-smi event notification unavailable (%s); ECC polling only",
+                                g.uuid, e)
+        if not self._evt_handles:
+            return None
+        t0 = time.monotonic()
+        try:
+            res = m.amdsmi_get_gpu_event_notification(int(timeout_s * 1000))
+        except Exception as e:  # noqa: BLE001
+            # an idle card answers the wait with NO_DATA (measured on MI355X) or a timeout
+            code = getattr(e, "get_error_code", lambda: None)()
+            if "NO_DATA" in str(e) or "TIMEOUT" in str(e).upper() or code in (
+                    getattr(m.amdsmi_wrapper, "AMDSMI_STATUS_NO_DATA", -1),
+                    getattr(m.amdsmi_wrapper, "AMDSMI_STATUS_TIMEOUT", -1)):
+                # keep the "block up to timeout_s" contract even if the answer came early
+                time.sleep(max(0.0, timeout_s - (time.monotonic() - t0)))
+                return []
+            raise
+        out = []
+        names = {int(v): v.name.lower() for v in m.AmdSmiEvtNotificationType}
+        for d in res.get("data", []):
+            kind = names.get(int(d.get("event", 0)), "none")
+            if kind == "none":
+                continue
+            out.append(HealthEvent(kind, self._evt_handles.get(_handle_key(d.get("processor_handle"))),
+                                   str(d.get("message", ""))))
+        return out
 
     def health(self, g):
         if "ecc" in getattr(self, "skip_checks", set()):
@@ -263,13 +344,25 @@ def _rocr_id_from_kfd(node_id) -> str | None:
 
 # --------------------------------------------------------------------- sysfs
 class SysfsBackend(Backend):
-    """KFD topology only: GPUs are nodes with simd_count > 0."""
+    """KFD topology (GPUs are nodes with simd_count > 0) joined with the DRM
+    render node's PCI device for NUMA node, BDF, card minor and partition mode."""
     name = "sysfs"
 
-    def __init__(self, root: Path = KFD_TOPO):
-        self.root = root
+    def __init__(self, root: Path = KFD_TOPO, drm: Path = Path("/sys/class/drm")):
+        self.root, self.drm = root, drm
         if not root.exists():
             raise RuntimeError(f"{root} not present")
+
+    def _pci(self, render_minor: int) -> Path | None:
+        d = self.drm / f"renderD{render_minor}" / "device"
+        return d if d.exists() else None
+
+    @staticmethod
+    def _read(p: Path, default: str = "") -> str:
+        try:
+            return p.read_text().strip()
+        except OSError:
+            return default
 
     def gpus(self):
         out = []
@@ -284,11 +377,25 @@ class SysfsBackend(Backend):
             for b in (n / "mem_banks").glob("*"):
                 mp = _kfd_props(b)
                 mem += mp.get("size_in_bytes", 0)
+            minor = p.get("drm_render_minor", -1)
+            numa, bdf, card, part, name = 0, "", -1, "SPX", "AMD Instinct MI355X"
+            dev = self._pci(minor)
+            if dev is not None:
+                try:
+                    numa = max(0, int(self._read(dev / "numa_node", "0") or 0))
+                except ValueError:
+                    numa = 0
+                bdf = os.path.basename(os.path.realpath(dev))
+                cards = [c.name for c in (dev / "drm").glob("card*")] if (dev / "drm").exists() else []
+                card = int(cards[0][4:]) if cards and cards[0][4:].isdigit() else -1
+                part = self._read(dev / "current_compute_partition", "SPX") or "SPX"
+                name = self._read(dev / "product_name") or name
             idx = len(out)
             out.append(GPUInfo(index=idx, uuid=f"GPU-{uid:016x}" if uid else f"kfd-{n.name}",
-                               rocr_id=f"GPU-{uid:016x}" if uid else str(idx), memory_mib=mem >> 20, cus=cus,
-                               numa=max(0, p.get("cpu_core_id_base", 0) and 0), render_minor=p.get("drm_render_minor", -1)))
-        return out
+                               rocr_id=f"GPU-{uid:016x}" if uid else str(idx), name=name, memory_mib=mem >> 20,
+                               cus=cus, numa=numa, bdf=bdf, render_minor=minor, card_minor=card,
+                               compute_partition=part.upper()))
+        return _group_physical(out)
 
     def link(self, a, b):
         return LinkInfo("XGMI", 1, 1)
@@ -297,13 +404,15 @@ class SysfsBackend(Backend):
         mode = mode.upper()
         if mode not in PARTITION_MODES:
             raise PartitionError(f"unknown compute partition {mode}")
-        cards = sorted(Path("/sys/class/drm").glob("card*/device/current_compute_partition"))
-        if physical_index >= len(cards):
+        gs = [g for g in self.gpus() if g.physical == physical_index and g.partition_index == 0]
+        dev = self._pci(gs[0].render_minor) if gs else None
+        if dev is None:
             raise PartitionError(f"no compute-partition sysfs node for GPU {physical_index}")
+        node = dev / "current_compute_partition"
         try:
-            cards[physical_index].write_text(mode + "\n")
+            node.write_text(mode + "\n")
         except OSError as e:
-            raise PartitionError(f"write {cards[physical_index]}: {e}") from e
+            raise PartitionError(f"write {node}: {e}") from e
 
 
 # ---------------------------------------------------------------------- fake
@@ -321,6 +430,23 @@ class FakeBackend(Backend):
         self.modes: dict[int, str] = {i: "SPX" for i in range(n)}
         self.procs: dict[str, list] = {}
         self.partition_calls: list[tuple[int, str]] = []
+        self.events: list[HealthEvent] = []
+        self._events_cv = threading.Condition()
+        self.event_source = True
+
+    def inject_event(self, kind: str, physical: int | None, message: str = ""):
+        with self._events_cv:
+            self.events.append(HealthEvent(kind, physical, message))
+            self._events_cv.notify_all()
+
+    def wait_health_events(self, gpus, timeout_s):
+        if not self.event_source:
+            return None
+        with self._events_cv:
+            if not self.events:
+                self._events_cv.wait(timeout_s)
+            out, self.events = self.events, []
+        return out
 
     def gpus(self):
         out = []

@@ -145,6 +145,87 @@ def test_health_change_marks_replicas_unhealthy(env):
     assert len(bad) == 8 and all(d.ID.startswith("GPU-0003") for d in bad)
 
 
+def _health_loop(plugin):
+    t = threading.Thread(target=plugin.health_loop, kwargs={"period": 0.05}, daemon=True)
+    t.start()
+    return t
+
+
+def _until(cond, timeout=5.0):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if cond():
+            return True
+        time.sleep(0.02)
+    return False
+
+
+def test_reset_event_marks_all_partitions_until_post_reset(env, monkeypatch):
+    """rm/health.go: an XID-class event marks the device (and every MIG child of
+    its parent) unhealthy; on MI355X a GPU reset event covers every compute
+    partition of the package, and the post-reset event brings them back."""
+    c, sched, plugin, backend = env
+    backend.set_compute_partition(2, "CPX")
+    plugin = S.AMDDevicePlugin(backend, plugin.cfg, "node1", socket_dir=tempfile.mkdtemp())
+    monkeypatch.setattr("k8s_vgpu_scheduler_amd.deviceplugin.partition.is_applying", lambda *a: False)
+    part2 = {g.uuid for g in plugin.gpus if g.physical == 2}
+    assert len(part2) == 8
+    _health_loop(plugin)
+    backend.inject_event("gpu_pre_reset", 2, "ring gfx_0.0.0 timeout")
+    assert _until(lambda: {u for u, ok in plugin.health.items() if not ok} == part2)
+    assert plugin.event_unhealthy[next(iter(part2))] == "gpu_pre_reset: ring gfx_0.0.0 timeout"
+    backend.inject_event("gpu_post_reset", 2)
+    assert _until(lambda: all(plugin.health.values()))
+    # an application page fault is not a device fault by default
+    backend.inject_event("vmfault", 5, "pasid 0x8001")
+    backend.inject_event("thermal_throttle", None)
+    time.sleep(0.3)
+    assert all(plugin.health.values())
+    # an event the backend cannot place marks every GPU
+    backend.inject_event("gpu_pre_reset", None)
+    assert _until(lambda: not any(plugin.health.values()))
+    plugin.stop()
+
+
+def test_health_check_env_lists(env, monkeypatch):
+    c, sched, plugin, backend = env
+    monkeypatch.setattr("k8s_vgpu_scheduler_amd.deviceplugin.partition.is_applying", lambda *a: False)
+    monkeypatch.setenv("DP_ENABLE_HEALTHCHECKS", "vmfault")
+    _health_loop(plugin)
+    backend.inject_event("vmfault", 1, "pasid 0x8001")
+    assert _until(lambda: plugin.health["GPU-0001"] is False)
+    plugin.stop()
+    monkeypatch.delenv("DP_ENABLE_HEALTHCHECKS")
+    monkeypatch.setenv("DP_DISABLE_HEALTHCHECKS", "reset")
+    p2 = S.AMDDevicePlugin(backend, plugin.cfg, "node1", socket_dir=tempfile.mkdtemp())
+    _health_loop(p2)
+    backend.inject_event("gpu_pre_reset", 3)
+    time.sleep(0.3)
+    assert all(p2.health.values())
+    p2.stop()
+
+
+def test_failed_event_wait_marks_all_then_recovers(env, monkeypatch):
+    c, sched, plugin, backend = env
+    monkeypatch.setattr("k8s_vgpu_scheduler_amd.deviceplugin.partition.is_applying", lambda *a: False)
+    calls = {"n": 0}
+    real = backend.wait_health_events
+
+    def flaky(gpus, timeout_s):
+        calls["n"] += 1
+        if calls["n"] == 1:
+            raise RuntimeError("AMDSMI_STATUS_DRIVER_NOT_LOADED")
+        return real(gpus, timeout_s)
+    backend.wait_health_events = flaky
+    seen = []
+    real_set = plugin.set_health
+    plugin.set_health = lambda u, ok: (seen.append((u, ok)), real_set(u, ok))
+    _health_loop(plugin)
+    assert _until(lambda: calls["n"] >= 3 and all(plugin.health.values()))
+    assert {u for u, ok in seen if not ok} == {g.uuid for g in plugin.gpus}   # all marked once
+    plugin.stop()
+
+
 def test_preferred_allocation_follows_annotation(env):
     c, sched, plugin, backend = env
     schedule(c, sched, amd_pod("p", mem=1000))
