@@ -3,7 +3,7 @@
 PYTHON ?= python3
 VERSION ?= 0.1.0
 
-.PHONY: all native shim ops mock test test-gpu bench image clean
+.PHONY: all native shim ops mock test test-gpu verify bench image clean
 
 all: native
 
@@ -24,6 +24,9 @@ test:
 
 test-gpu:
 	$(PYTHON) -m pytest tests/ -x -q -m gpu
+
+verify:
+	$(PYTHON) hack/verify.py all -v
 
 bench:
 	$(PYTHON) bench.py

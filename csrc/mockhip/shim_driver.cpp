@@ -88,7 +88,7 @@ int main(int argc, char** argv) {
       prop.type = hipMemAllocationTypePinned;
       prop.location.type = hipMemLocationTypeDevice;
       int d = 0;
-      hipGetDevice(&d);
+      (void)hipGetDevice(&d);
       prop.location.id = d;
       hipError_t rc = hipMemCreate(&h, mib << 20, &prop, 0);
       printf("{\"op\":\"vmm\",\"mib\":%zu,\"rc\":%d}\n", mib, (int)rc);
@@ -107,15 +107,15 @@ int main(int argc, char** argv) {
              t >> 20);
     } else if (!strcmp(c, "props")) {
       hipDeviceProp_tR0600 p;
-      hipGetDevicePropertiesR0600(&p, 0);
+      (void)hipGetDevicePropertiesR0600(&p, 0);
       size_t tm = 0;
-      hipDeviceTotalMem(&tm, 0);
+      (void)hipDeviceTotalMem(&tm, 0);
       printf("{\"op\":\"props\",\"total_mib\":%zu,\"devtotal_mib\":%zu}\n", p.totalGlobalMem >> 20,
              tm >> 20);
     } else if (!strcmp(c, "launch")) {
       long n = strtol(argv[++i], nullptr, 10);
       static char dummy;
-      for (long k = 0; k < n; ++k) hipLaunchKernel(&dummy, dim3(1), dim3(64), nullptr, 0, nullptr);
+      for (long k = 0; k < n; ++k) (void)hipLaunchKernel(&dummy, dim3(1), dim3(64), nullptr, 0, nullptr);
       auto f = (unsigned long long (*)(void))dlsym(RTLD_DEFAULT, "mivgpu_launch_count");
       auto g = (unsigned long long (*)(void))dlsym(RTLD_DEFAULT, "mockhip_launch_count");
       printf("{\"op\":\"launch\",\"n\":%ld,\"shim_seen\":%llu,\"real_seen\":%llu}\n", n,

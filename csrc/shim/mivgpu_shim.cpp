@@ -556,7 +556,7 @@ inline void ensure_init() {
 
 inline int current_device() {
   int d = 0;
-  if (real_hipGetDevice()) real_hipGetDevice()(&d);
+  if (real_hipGetDevice()) (void)real_hipGetDevice()(&d);  // on failure: device 0
   if (d < 0 || d >= MIVGPU_MAX_DEVICES) d = 0;
   return d;
 }
@@ -690,7 +690,8 @@ hipError_t guarded_alloc(void** ptr, uint64_t bytes, Call&& call) {
       void* h = nullptr;
       if (real_hipHostMalloc()(&h, bytes, hipHostMallocMapped) == hipSuccess) {
         void* dptr = h;
-        if (real_hipHostGetDevicePointer()) real_hipHostGetDevicePointer()(&dptr, h, 0);
+        // mapped host memory is addressable by its host pointer if this fails
+        if (real_hipHostGetDevicePointer()) (void)real_hipHostGetDevicePointer()(&dptr, h, 0);
         *ptr = dptr;
         track(dptr, bytes, dev, K_HOST_SPILL);
         tmark("mivgpu:host-spill dev=%d mib=%llu", dev, (unsigned long long)(bytes >> 20));
@@ -713,7 +714,7 @@ bool release_tracked(void* p) {
   AllocRec r;
   if (!p || !untrack(reinterpret_cast<uintptr_t>(p), &r)) return false;
   if (r.kind == K_HOST_SPILL) {
-    if (real_hipHostFree()) real_hipHostFree()(p);
+    if (real_hipHostFree() && real_hipHostFree()(p) != hipSuccess) mlog(1, "host-spill free of %p failed", p);
     return true;
   }
   account_sub(r.dev, r.size, (AllocKind)r.kind);
@@ -771,7 +772,7 @@ bool gate_init_locked(int dev, DeviceGate& G) {
     return false;
   // State lives in device memory; it is not charged to the tenant's quota.
   if (real_hipMalloc()(&G.state, 4096) != hipSuccess) return false;
-  if (real_hipMemset()) real_hipMemset()(G.state, 0, 4096);
+  if (!real_hipMemset() || real_hipMemset()(G.state, 0, 4096) != hipSuccess) return false;
   if (real_hipHostMalloc()(&G.host_stats, kHostStatsBytes, hipHostMallocCoherent | hipHostMallocMapped) !=
       hipSuccess)
     G.host_stats = nullptr;
@@ -789,7 +790,7 @@ bool gate_init_locked(int dev, DeviceGate& G) {
     if (real_hipModuleLaunchKernel()(G.clock_fn, 1, 1, 1, 64, 1, 1, 0, nullptr, args, nullptr) !=
         hipSuccess)
       return false;
-    real_hipStreamSynchronize()(nullptr);
+    if (real_hipStreamSynchronize()(nullptr) != hipSuccess) return false;
     uint64_t t1 = mono_ns();
     if (t1 - t0 < best_span && *G.clock_host) {
       best_span = t1 - t0;
@@ -826,7 +827,11 @@ void enqueue_gate_locked(int dev, DeviceGate& G, int slot, hipStream_t stream, u
   void* state = G.state;
   void* hs = G.host_stats;
   void* args[] = {&state, &hs, &submit_dev, &slot_arg, &rate_ppm, &cap, &hold};
-  real_hipModuleLaunchKernel()(G.gate_fn, 1, 1, 1, 64, 1, 1, 0, stream, args, nullptr);
+  if (real_hipModuleLaunchKernel()(G.gate_fn, 1, 1, 1, 64, 1, 1, 0, stream, args, nullptr) != hipSuccess) {
+    static std::atomic<bool> warned{false};
+    if (!warned.exchange(true)) mlog(1, "device %d: governor gate launch failed; this batch is not throttled", dev);
+    return;
+  }
   tmark("mivgpu:gate dev=%d slot=%d rate_pct=%u", dev, slot, rate_ppm / 10000u);
   S.last_gate_host_ns = now;
   if (g_slot >= 0 && hs) {
@@ -871,7 +876,8 @@ void* stamper_main(void* arg) {
   DeviceGate& G = g_gates[dev];
   {
     Guard g;  // our own HIP calls must never re-enter the hooks' accounting
-    if (real_hipSetDevice()) real_hipSetDevice()(dev);
+    if (real_hipSetDevice() && real_hipSetDevice()(dev) != hipSuccess)
+      mlog(1, "device %d: governor stamper could not select the device", dev);
   }
   for (;;) {
     usleep(500);
