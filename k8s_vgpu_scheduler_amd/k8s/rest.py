@@ -19,7 +19,7 @@ from pathlib import Path
 import requests
 import yaml
 
-from .client import ApiError, Conflict, KubeClient, NotFound, Unauthorized
+from .client import AlreadyExists, ApiError, Conflict, KubeClient, NotFound, Unauthorized
 
 log = logging.getLogger(__name__)
 
@@ -131,7 +131,7 @@ class RestClient(KubeClient):
             if r.status_code == 404:
                 raise NotFound(msg)
             if r.status_code == 409:
-                raise Conflict(msg)
+                raise AlreadyExists(msg) if reason == "AlreadyExists" else Conflict(msg)
             if r.status_code == 401:
                 raise Unauthorized(msg)
             raise ApiError(r.status_code, reason or r.reason, msg)

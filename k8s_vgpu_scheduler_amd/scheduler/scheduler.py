@@ -89,7 +89,7 @@ class Scheduler:
 
     def start(self):
         self.pods_inf.add_event_handler(self.on_add_pod, self.on_update_pod, self.on_del_pod)
-        self.nodes_inf.add_event_handler(lambda n: self._notify.set(), None, self.on_del_node)
+        self.nodes_inf.add_event_handler(lambda n: self._notify.set(), self.on_update_node, self.on_del_node)
         self.quota_inf.add_event_handler(self.quota_manager.add_quota,
                                          lambda o, n: self.quota_manager.update_quota(o, n),
                                          self.quota_manager.del_quota)
@@ -121,6 +121,20 @@ class Scheduler:
                 self.register()
             except Exception:  # noqa: BLE001
                 log.exception("register failed")
+
+    @staticmethod
+    def _device_annos(node: dict | None) -> dict:
+        anns = ((node or {}).get("metadata") or {}).get("annotations") or {}
+        return {k: v for k, v in anns.items() if k.startswith("hami.io/node-")}
+
+    def on_update_node(self, old: dict, new: dict):
+        """The reference wakes registration on node add only (scheduler.go:371-374) and
+        otherwise waits for the 15 s ticker; a changed device-registration or
+        handshake annotation wakes it now, so a GPU the device plugin just
+        registered is schedulable within one watch event.  Status heartbeats
+        do not touch these annotations and do not wake it."""
+        if self._device_annos(old) != self._device_annos(new):
+            self._notify.set()
 
     # ------------------------------------------------------------- pod events
     def on_add_pod(self, pod: dict):

@@ -1,0 +1,77 @@
+"""End to end across process and protocol boundaries (the reference's test/e2e
+tier): the real scheduler, device plugin and monitor binaries
+against an HTTP API server, driven the way kube-apiserver (webhook),
+kube-scheduler (extender /filter, /bind) and the kubelet (device-plugin gRPC)
+drive them.  The "container" is the shim-preloaded mock-HIP driver, so the
+HBM limit, the shared region and the monitor's per-pod metrics are real.
+The GPU variant of this test (tests/test_e2e_gpu.py) runs a PyTorch workload
+on the MI355X instead."""
+
+import subprocess
+
+import pytest
+
+from k8s_vgpu_scheduler_amd.device import codec
+from k8s_vgpu_scheduler_amd.e2e.harness import E2ECluster, container_env, samples, wait_for
+from k8s_vgpu_scheduler_amd.testing import amd_pod
+
+MIB = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def cluster(tmp_path_factory, native_build):
+    with E2ECluster(str(tmp_path_factory.mktemp("e2e")), fake_gpus=2, split=4) as cl:
+        yield cl
+
+
+def test_binaries_register_the_node(cluster):
+    anns = cluster.api.cluster.get("nodes", "node1")["metadata"]["annotations"]
+    devs = codec.unmarshal_node_devices(anns["hami.io/node-amd-register"])
+    assert len(devs) == 2 and all(d.count == 4 and d.devcore == 256 for d in devs)
+    st = cluster.api.cluster.get("nodes", "node1")["status"]
+    assert st["allocatable"]["amd.com/gpu"] == "8"          # kubelet saw 2 GPUs x 4 replicas
+    assert {m for m, _ in cluster.api.requests} >= {"GET", "PATCH"}   # all through HTTP
+
+
+def test_pod_lifecycle(cluster, native_build):
+    cl = cluster
+    pod = cl.submit(amd_pod("vgpu-a", mem=8192, cores=25))
+    assert pod["spec"]["schedulerName"] == "hami-scheduler"        # set by the webhook
+    assert cl.schedule("default", "vgpu-a") == "node1"
+    allocs = cl.start_containers("default", "vgpu-a")
+    envs = allocs[0]["envs"]
+    assert envs["HIP_DEVICE_MEMORY_LIMIT_0"] == "8192m" and envs["GPU_MAX_HW_QUEUES"] == "2"
+    assert codec.ranges_count(codec.parse_ranges(envs["HSA_CU_MASK"].split(":", 1)[1])) == 64
+    anns = cl.api.cluster.get("pods", "vgpu-a", "default")["metadata"]["annotations"]
+    assert anns["hami.io/bind-phase"] == "success"
+
+    # the container: shim preloaded through the mounts, limit enforced, region visible to the monitor
+    env = container_env(allocs[0])
+    env["MOCKHIP_TOTAL_MIB"] = "65536"
+    proc = subprocess.Popen([str(native_build["driver"]), "alloc", "3000", "meminfo", "alloc", "6000",
+                             "sleep", "6000"], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        def used():
+            return [v for l, v in samples(cl.metrics("mon_metrics"), "hami_vgpu_memory_used_bytes")
+                    if l.get("pod") == "vgpu-a"]
+        vals = wait_for(used, 30, "monitor to report the container's HBM use")
+        assert vals[0] == 3000 * MIB
+        lim = [v for l, v in samples(cl.metrics("mon_metrics"), "hami_vgpu_memory_limit_bytes")
+               if l.get("pod") == "vgpu-a"]
+        assert lim == [8192 * MIB]
+    finally:
+        out, err = proc.communicate(timeout=30)
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert '"total_mib":8192' in lines[1] and '"rc":2' in lines[2], (out, err)   # 6000 more MiB: OOM
+
+    alloc = [v for l, v in samples(cl.metrics("sched_metrics"), "hami_vgpu_memory_allocated_bytes")
+             if l.get("pod") == "vgpu-a"]
+    assert alloc == [8192 * MIB]
+    # a pod that fits nowhere is filtered out, with the reason recorded
+    cl.submit(amd_pod("too-big", mem=400000))
+    assert cl.schedule("default", "too-big") is None
+    # deleting the pod releases its share in the scheduler
+    cl.delete_pod("default", "vgpu-a")
+    wait_for(lambda: not [1 for l, v in samples(cl.metrics("sched_metrics"), "hami_vgpu_memory_allocated_bytes")
+                          if l.get("pod") == "vgpu-a"], 30, "scheduler to release the pod")
+    assert all(v is None for v in cl.alive().values()), cl.alive()

@@ -1,0 +1,83 @@
+"""End to end on the MI355X: the real binaries with amd-smi discovery, a pod
+scheduled through the extender and allocated through the kubelet gRPC path,
+and a PyTorch workload started with exactly the environment Allocate returned
+(shim preloaded as /etc/ld.so.preload would, mounts resolved to host paths).
+Checks, inside the "container": the HBM limit seen by torch, OOM beyond it,
+confinement to the granted 64 CUs across all 8 XCDs; outside it: the
+monitor's per-pod HBM metric and the scheduler's allocation metric."""
+
+import json
+import subprocess
+import sys
+
+import pytest
+
+from k8s_vgpu_scheduler_amd.device import codec
+from k8s_vgpu_scheduler_amd.e2e.harness import REPO, E2ECluster, container_env, samples, wait_for
+from k8s_vgpu_scheduler_amd.testing import amd_pod
+
+pytestmark = pytest.mark.gpu
+MIB = 1 << 20
+
+
+def _probe(env, mode, *args, wait=True):
+    cmd = [sys.executable, "-m", "k8s_vgpu_scheduler_amd.shim.probe", "--child", mode, *args]
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=str(REPO))
+    if not wait:
+        return p
+    out, err = p.communicate(timeout=300)
+    res = {"rc": p.returncode}
+    for line in out.splitlines():
+        if line.startswith("{"):
+            res.update(json.loads(line))
+    assert p.returncode == 0, err[-3000:]
+    return res
+
+
+@pytest.fixture(scope="module")
+def cluster(tmp_path_factory):
+    from k8s_vgpu_scheduler_amd.utils import build
+    build.build_all()
+    with E2ECluster(str(tmp_path_factory.mktemp("e2e-gpu")), smi_backend="amdsmi", split=4) as cl:
+        yield cl
+
+
+def test_pod_on_mi355x_end_to_end(cluster):
+    cl = cluster
+    devs = codec.unmarshal_node_devices(
+        cl.api.cluster.get("nodes", "node1")["metadata"]["annotations"]["hami.io/node-amd-register"])
+    assert devs and devs[0].devcore == 256 and devs[0].devmem > 280_000
+    cl.submit(amd_pod("llm-a", mem=36864, cores=25))
+    assert cl.schedule("default", "llm-a") == "node1"
+    alloc = cl.start_containers("default", "llm-a")[0]
+    assert any(d["host_path"] == "/dev/kfd" for d in alloc["devices"])
+    env = container_env(alloc)
+    env["PYTHONPATH"] = str(REPO)
+
+    holder = _probe(env, "matmul", "--n", "2048", "--iters", "5", "--oom-probe-mib", "20000", "--hold-s", "20",
+                    wait=False)
+    try:
+        def used():
+            return [v for l, v in samples(cl.metrics("mon_metrics"), "hami_vgpu_memory_used_bytes")
+                    if l.get("pod") == "llm-a" and v >= 20000 * MIB]
+        wait_for(used, 240, "the monitor to see the pod's 20 GiB")
+        lim = [v for l, v in samples(cl.metrics("mon_metrics"), "hami_vgpu_memory_limit_bytes")
+               if l.get("pod") == "llm-a"]
+        assert lim == [36864 * MIB]
+        host = [v for l, v in samples(cl.metrics("mon_metrics"), "hami_host_gpu_memory_used_bytes")]
+        assert host and max(host) >= 20000 * MIB
+    finally:
+        out, err = holder.communicate(timeout=300)
+    r = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert holder.returncode == 0 and r["mem_total_mib"] == 36864 and r["oom_probe"] == "allocated", err[-2000:]
+
+    over = _probe(env, "matmul", "--n", "1024", "--iters", "2", "--oom-probe-mib", "40000")
+    assert over["oom_probe"] == "oom"
+    hw = _probe(env, "hwid")
+    assert hw["distinct"] == 64 and hw["xccs"] == list(range(8)), hw
+
+    alloc_m = [v for l, v in samples(cl.metrics("sched_metrics"), "hami_vgpu_memory_allocated_bytes")
+               if l.get("pod") == "llm-a"]
+    assert alloc_m == [36864 * MIB]
+    cl.delete_pod("default", "llm-a")
+    assert all(v is None for v in cl.alive().values()), cl.alive()
