@@ -45,6 +45,10 @@ class NodeManager:
                 raise LookupError(f"node {node_id} not found")
             return n.deepcopy()
 
+    def node_ids(self) -> list[str]:
+        with self._mu:
+            return list(self._nodes)
+
     def list_nodes(self) -> dict[str, NodeInfo]:
         with self._mu:
             return {k: v.deepcopy() for k, v in self._nodes.items()}

@@ -252,6 +252,16 @@ class Scheduler:
                     for d in nodedevs:
                         info.devices.setdefault(d.devicevendor or vendor, []).append(d)
                     self.nodes.add_node(name, info)
+            # A delete event can land between the list above and add_node (the
+            # reference's register/onDelNode race, register_race_test.go:37-56):
+            # the node would be re-added after on_del_node removed it and never
+            # leave the cache.  Every pass therefore drops cached nodes the
+            # lister no longer returns, so the cache converges on the next pass.
+            listed = set(names)
+            for stale in [n for n in self.nodes.node_ids() if n not in listed]:
+                log.info("dropping node %s: no longer listed", stale)
+                self.nodes.rm_node(stale)
+                self.overview.pop(stale, None)
             _, overall, _ = self.get_nodes_usage(names, None)
             self.overview = overall
             self.synced = True

@@ -70,6 +70,12 @@ def test_pod_lifecycle(cluster, native_build):
     # a pod that fits nowhere is filtered out, with the reason recorded
     cl.submit(amd_pod("too-big", mem=400000))
     assert cl.schedule("default", "too-big") is None
+    # ...and stays Pending with a FilteringFailed event (test/e2e/pod/test_pod.go:108-122)
+    evs = wait_for(lambda: [e for e in cl.api.cluster.list("events", "default")
+                            if (e.get("involvedObject") or {}).get("name") == "too-big"
+                            and e.get("reason") == "FilteringFailed"], 10, "FilteringFailed event")
+    assert evs[0]["type"] == "Warning" and "node1" in evs[0]["message"], evs[0]
+    assert not cl.api.cluster.get("pods", "too-big", "default")["spec"].get("nodeName")
     # deleting the pod releases its share in the scheduler
     cl.delete_pod("default", "vgpu-a")
     wait_for(lambda: not [1 for l, v in samples(cl.metrics("sched_metrics"), "hami_vgpu_memory_allocated_bytes")
