@@ -31,6 +31,7 @@
 //    removes the separate activation kernel and the [M, 2I] round trip.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 typedef uint16_t bf16_t;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
@@ -55,6 +56,23 @@ constexpr int unroll_of(int mt, int nt) {
   return 128 / (16 * (mt + nt)) >= 4 ? 4 : (128 / (16 * (mt + nt)) >= 2 ? 2 : 1);
 }
 
+// Double-buffered schedule (DB): two groups of U k-blocks, the next one's loads
+// issued before the current one's MFMAs, so at least one group is always in
+// flight.  Both buffers live in registers: 2*U*(MT+NT)*16 VGPRs <= 256.
+constexpr int unroll_db(int mt, int nt) {
+  return 256 / (32 * (mt + nt)) >= 4 ? 4 : (256 / (32 * (mt + nt)) >= 2 ? 2 : 1);
+}
+
+// Strides (in 16-byte chunks) of the packed W between consecutive n-tiles and
+// consecutive k-blocks.  Tile-major: a tile's k-blocks are contiguous.
+// K-block-major: a k-block's tiles are contiguous, so the waves of a launch,
+// all near the same k-block, read one contiguous front that spreads over every
+// HBM channel, instead of as many separate streams as there are waves.
+struct WStride {
+  size_t tile;
+  size_t kb;
+};
+
 template <int MT, int NT>
 struct Frag {
   u32x4_t a[MT][4];
@@ -66,11 +84,11 @@ struct Frag {
 // loads (a predicated load hides from the compiler's vmcnt bookkeeping and
 // serialises the pipeline).
 template <int MT, int NT>
-__device__ __forceinline__ void load_kblock(Frag<MT, NT>& f, const u32x4_t* __restrict__ wp, size_t wstride_tile,
+__device__ __forceinline__ void load_kblock(Frag<MT, NT>& f, const u32x4_t* __restrict__ wp, WStride ws,
                                             const bf16_t* const* xrow, int kb, int lane) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const u32x4_t* src = wp + t * wstride_tile + (size_t)kb * 256 + lane;
+    const u32x4_t* src = wp + t * ws.tile + (size_t)kb * ws.kb + lane;
 #pragma unroll
     for (int j = 0; j < 4; ++j) f.b[t][j] = __builtin_nontemporal_load(src + j * 64);
   }
@@ -78,7 +96,42 @@ __device__ __forceinline__ void load_kblock(Frag<MT, NT>& f, const u32x4_t* __re
   for (int m = 0; m < MT; ++m) {
     const u32x4_t* src = (const u32x4_t*)(xrow[m] + kb * 64);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) f.a[m][j] = src[j];
+    for (int j = 0; j < 4; ++j) {
+#ifdef MIVGPU_SKINNY_NOX_EXPERIMENT  // throughput experiment only: X from registers, results meaningless
+      f.a[m][j] = (u32x4_t){(unsigned)kb, (unsigned)j, (unsigned)m, (unsigned)(uintptr_t)src};
+#else
+      f.a[m][j] = src[j];
+#endif
+    }
+  }
+}
+
+// Split halves of load_kblock for the double-buffered schedule: W (HBM
+// stream) and X (L2-resident) fragments.
+template <int MT, int NT>
+__device__ __forceinline__ void load_w_kblock(Frag<MT, NT>& f, const u32x4_t* __restrict__ wp, WStride ws,
+                                              int kb, int lane) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const u32x4_t* src = wp + t * ws.tile + (size_t)kb * ws.kb + lane;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f.b[t][j] = __builtin_nontemporal_load(src + j * 64);
+  }
+}
+
+template <int MT, int NT>
+__device__ __forceinline__ void load_x_kblock(Frag<MT, NT>& f, const bf16_t* const* xrow, int kb) {
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const u32x4_t* src = (const u32x4_t*)(xrow[m] + kb * 64);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#ifdef MIVGPU_SKINNY_NOX_EXPERIMENT
+      f.a[m][j] = (u32x4_t){(unsigned)kb, (unsigned)j, (unsigned)m, (unsigned)(uintptr_t)src};
+#else
+      f.a[m][j] = src[j];
+#endif
+    }
   }
 }
 
@@ -143,10 +196,22 @@ __device__ __forceinline__ void epilogue(Get get, bf16_t* __restrict__ y, int M,
   }
 }
 
-template <int MT, int NT, int KS, int EPI>
+// Scheduling + compiler barrier: sched_barrier pins the machine schedule, the
+// empty asm with a memory clobber keeps IR passes from hoisting the next
+// buffer's (restrict, hence freely movable) loads above the MFMAs still reading
+// the registers they would overwrite -- which forces renamed registers and
+// loop-end copies that wait for every load (vmcnt(0)).
+#define DB_FENCE()                          \
+  do {                                      \
+    __builtin_amdgcn_sched_barrier(0);      \
+    asm volatile("" ::: "memory");          \
+  } while (0)
+
+template <int MT, int NT, int KS, int EPI, bool DB>
 __global__ void __launch_bounds__(64 * KS)
 skinny_gemm_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int M,
-                   int K, int N, int ldx, int ldy, int S, float* __restrict__ scratch, int* __restrict__ tickets) {
+                   int K, int N, int ldx, int ldy, int S, float* __restrict__ scratch, int* __restrict__ tickets,
+                   int kmajor) {
   __shared__ float red[MT * NT * 16 * 64];
   __shared__ int last;
   const int tid = threadIdx.x;
@@ -155,8 +220,8 @@ skinny_gemm_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
   const int KB = K >> 6;
   const int group = blockIdx.x / S, split = blockIdx.x % S;
   const int tile0 = group * NT;
-  const size_t wstride_tile = (size_t)KB * 256;  // 16-byte chunks per n-tile
-  const u32x4_t* wbase = wp + (size_t)tile0 * wstride_tile;
+  const WStride ws = kmajor ? WStride{256, (size_t)(N >> 5) * 256} : WStride{(size_t)KB * 256, 256};
+  const u32x4_t* wbase = wp + (size_t)tile0 * ws.tile;
 
   for (int i = tid; i < MT * NT * 16 * 64; i += 64 * KS) red[i] = 0.f;
 
@@ -176,24 +241,85 @@ skinny_gemm_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[m][t][e] = 0.f;
 
-  // Groups of U k-blocks: every load of the group is issued before the first
-  // MFMA, which then consume them in order behind decreasing vmcnt waits.
-  // (A rotated one-ahead pipeline gets re-serialised by the compiler.)
-  constexpr int U = unroll_of(MT, NT);
   int kb = kb0;
-  for (; kb + U <= kb1; kb += U) {
-    Frag<MT, NT> f[U];
+  if constexpr (DB) {
+    // W (the HBM stream) alternates between two register buffers, the next
+    // group's loads issued before the current group's MFMAs, with no branch
+    // around a load in the steady state.  X comes from L2 just in time for its
+    // group and is issued *before* the W prefetch (vmcnt retires in issue
+    // order: waiting for X must not wait for the prefetch), so no X fragment is
+    // loop-carried (a loop-carried X buffer gets
+    // renamed by the register allocator and copied back at the loop end behind
+    // a vmcnt(0) that drains the whole pipeline).  The last one or two groups
+    // are peeled.
+    constexpr int U = unroll_db(MT, NT);
+    const int G = (kb1 - kb0) / U;
+    if (G > 0) {
+      Frag<MT, NT> fa[U], fb[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) load_kblock<MT, NT>(f[u], wbase, wstride_tile, xrow, kb + u, lane);
-    // keep the whole group in flight: the occupancy-driven scheduler would
-    // otherwise sink loads behind MFMAs (≈2 loads in flight per wave)
-    __builtin_amdgcn_sched_barrier(0);
+      for (int u = 0; u < U; ++u) load_w_kblock<MT, NT>(fa[u], wbase, ws, kb + u, lane);
+      int g = 0;
+      for (; g + 3 <= G; g += 2, kb += 2 * U) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) mma_kblock<MT, NT>(f[u], acc);
+        for (int u = 0; u < U; ++u) load_x_kblock<MT, NT>(fa[u], xrow, kb + u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) load_w_kblock<MT, NT>(fb[u], wbase, ws, kb + U + u, lane);
+        DB_FENCE();
+#pragma unroll
+        for (int u = 0; u < U; ++u) mma_kblock<MT, NT>(fa[u], acc);
+        DB_FENCE();
+#pragma unroll
+        for (int u = 0; u < U; ++u) load_x_kblock<MT, NT>(fb[u], xrow, kb + U + u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) load_w_kblock<MT, NT>(fa[u], wbase, ws, kb + 2 * U + u, lane);
+        DB_FENCE();
+#pragma unroll
+        for (int u = 0; u < U; ++u) mma_kblock<MT, NT>(fb[u], acc);
+        DB_FENCE();
+      }
+      if (G - g == 2) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) load_x_kblock<MT, NT>(fa[u], xrow, kb + u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) load_w_kblock<MT, NT>(fb[u], wbase, ws, kb + U + u, lane);
+        DB_FENCE();
+#pragma unroll
+        for (int u = 0; u < U; ++u) mma_kblock<MT, NT>(fa[u], acc);
+        DB_FENCE();
+#pragma unroll
+        for (int u = 0; u < U; ++u) load_x_kblock<MT, NT>(fb[u], xrow, kb + U + u);
+        DB_FENCE();
+#pragma unroll
+        for (int u = 0; u < U; ++u) mma_kblock<MT, NT>(fb[u], acc);
+        kb += 2 * U;
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) load_x_kblock<MT, NT>(fa[u], xrow, kb + u);
+        DB_FENCE();
+#pragma unroll
+        for (int u = 0; u < U; ++u) mma_kblock<MT, NT>(fa[u], acc);
+        kb += U;
+      }
+    }
+  } else {
+    // Groups of U k-blocks: every load of the group is issued before the first
+    // MFMA, which then consume them in order behind decreasing vmcnt waits.
+    // (A rotated one-ahead pipeline gets re-serialised by the compiler.)
+    constexpr int U = unroll_of(MT, NT);
+    for (; kb + U <= kb1; kb += U) {
+      Frag<MT, NT> f[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) load_kblock<MT, NT>(f[u], wbase, ws, xrow, kb + u, lane);
+      // keep the whole group in flight: the occupancy-driven scheduler would
+      // otherwise sink loads behind MFMAs (≈2 loads in flight per wave)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < U; ++u) mma_kblock<MT, NT>(f[u], acc);
+    }
   }
   for (; kb < kb1; ++kb) {
     Frag<MT, NT> f;
-    load_kblock<MT, NT>(f, wbase, wstride_tile, xrow, kb, lane);
+    load_kblock<MT, NT>(f, wbase, ws, xrow, kb, lane);
     mma_kblock<MT, NT>(f, acc);
   }
   __syncthreads();  // red[] zeroed
@@ -241,15 +367,223 @@ skinny_gemm_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
   if (tid == 0) tickets[group] = 0;
 }
 
+// ============================================================================
+// Wide workgroups: WV waves own different n-tiles over the SAME k-range, so the
+// workgroup needs each X k-block once.  X is loaded cooperatively with fully
+// coalesced 16-byte loads (row-major, 8 cache lines per KiB instead of 32)
+// into a padded, double-buffered LDS tile, and each wave reads its MFMA
+// A-operands with ds_read_b128.  Measured at 64 CUs, the per-wave X loads of
+// the kernel above (each instruction touches 32 rows x 32 B) are what limits
+// it: with X taken out of the loop the same W stream runs 1.5-1.6x faster
+// (profiles/gemm_cu64_nox.json).  W stays double-buffered in registers (the
+// next group's loads issued before the current group's MFMAs); one barrier per
+// group hands the next X tile over.  No LDS reduction: every wave finishes its
+// own tiles from its accumulators; inter-workgroup split S as above.
+constexpr int unroll_wide(int nt) { return nt >= 4 ? 1 : (nt == 2 ? 2 : 4); }
+
+template <int NT>
+struct WFrag {
+  u32x4_t b[NT][4];
+};
+
+template <int NT, int U>
+__device__ __forceinline__ void wide_load_w(WFrag<NT> (&f)[U], const u32x4_t* __restrict__ wp, WStride ws, int kb,
+                                            int lane) {
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const u32x4_t* src = wp + t * ws.tile + (size_t)(kb + u) * ws.kb + lane;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) f[u].b[t][j] = __builtin_nontemporal_load(src + j * 64);
+    }
+}
+
+// X[MT*32 rows][U*64 k] of k-blocks kb.. as MT*U*256 16-byte chunks, row-major,
+// XC per thread (rows >= M re-read row M-1: never stored, no masks).
+template <int MT, int U, int XC>
+__device__ __forceinline__ void wide_load_x(u32x4_t (&xr)[XC], const bf16_t* __restrict__ x, int M, int ldx, int kb,
+                                            int tid, int nthreads) {
+#pragma unroll
+  for (int i = 0; i < XC; ++i) {
+    const int c = tid + i * nthreads;
+    const int row = c / (U * 8), c8 = c % (U * 8);
+    xr[i] = *(const u32x4_t*)(x + (size_t)min(row, M - 1) * ldx + kb * 64 + c8 * 8);
+  }
+}
+
+template <int MT, int U, int XC, int PITCH>
+__device__ __forceinline__ void wide_store_x(bf16_t* xs, const u32x4_t (&xr)[XC], int tid, int nthreads) {
+#pragma unroll
+  for (int i = 0; i < XC; ++i) {
+    const int c = tid + i * nthreads;
+    const int row = c / (U * 8), c8 = c % (U * 8);
+    *(u32x4_t*)(xs + row * PITCH + c8 * 8) = xr[i];
+  }
+}
+
+template <int MT, int NT, int U, int PITCH>
+__device__ __forceinline__ void wide_mma(const WFrag<NT> (&f)[U], const bf16_t* xs, f32x16_t (&acc)[MT][NT], int r,
+                                         int h) {
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const u32x4_t a = *(const u32x4_t*)(xs + (m * 32 + r) * PITCH + u * 64 + 32 * h + 8 * j);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                              __builtin_bit_cast(bf16x8_t, f[u].b[t][j]), acc[m][t],
+                                                              0, 0, 0);
+      }
+}
+
+// One group: (prefetch the next group's X then W,) MFMAs of this group from
+// `cur` + LDS buffer `xc`, (then stage the prefetched X into `xn` and hand it
+// over with the barrier).  X is issued before W: vmcnt retires in issue
+// order, so staging X never waits for the W prefetch.
+template <int MT, int NT, int U, int XC, int PITCH, bool PREFETCH>
+__device__ __forceinline__ void wide_step(const WFrag<NT> (&cur)[U], WFrag<NT> (&nxt)[U], const bf16_t* xc,
+                                          bf16_t* xn, f32x16_t (&acc)[MT][NT], const u32x4_t* __restrict__ wbase,
+                                          WStride ws, const bf16_t* __restrict__ x, int M, int ldx, int kb, int tid,
+                                          int nthreads, int lane, int r, int h) {
+  u32x4_t xr[XC];
+  if constexpr (PREFETCH) {
+    wide_load_x<MT, U, XC>(xr, x, M, ldx, kb + U, tid, nthreads);
+    wide_load_w<NT, U>(nxt, wbase, ws, kb + U, lane);
+  }
+  DB_FENCE();
+  wide_mma<MT, NT, U, PITCH>(cur, xc, acc, r, h);
+  DB_FENCE();
+  if constexpr (PREFETCH) {
+    wide_store_x<MT, U, XC, PITCH>(xn, xr, tid, nthreads);
+    __syncthreads();
+  }
+}
+
+// 32x32x16 accumulator element e of lane (r, h): row (e&3) + 8*(e>>2) + 4h, column r.
+__device__ __forceinline__ int acc_row(int e, int h) { return (e & 3) + 8 * (e >> 2) + 4 * h; }
+
+template <int MT, int NT, int EPI, class Get>
+__device__ __forceinline__ void wide_epilogue(Get get, bf16_t* __restrict__ y, int M, int ldy, int tile0,
+                                              int vgroup, int r, int h) {
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = m * 32 + acc_row(e, h);
+      if (row >= M) continue;
+      if constexpr (EPI == EPI_STORE) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) y[(size_t)row * ldy + (size_t)(tile0 + t) * 32 + r] = f2bf(get(m, t, e));
+      } else if constexpr (NT == 2) {  // SiLU(gate)*up: tile pair (gate, up) of channel block `vgroup`
+        const float g = round_bf(get(m, 0, e)), u = round_bf(get(m, 1, e));
+        y[(size_t)row * ldy + (size_t)vgroup * 32 + r] = f2bf(g / (1.f + __expf(-g)) * u);
+      }
+    }
+}
+
+template <int MT, int NT, int WV, int EPI>
+__global__ void __launch_bounds__(64 * WV)
+skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int M,
+                   int K, int N, int ldx, int ldy, int S, float* __restrict__ scratch, int* __restrict__ tickets,
+                   int kmajor) {
+  static_assert(EPI != EPI_SILU_MUL || NT == 2, "SiLU*up pairs a gate tile with an up tile");
+  constexpr int U = unroll_wide(NT);
+  constexpr int PITCH = U * 64 + 8;                 // +16 B per row: conflict-free ds_read_b128
+  constexpr int XBUF = MT * 32 * PITCH;
+  constexpr int NTHREADS = 64 * WV;
+  constexpr int XC = MT * U * 256 / NTHREADS;       // X chunks per thread per group
+  static_assert(XC * NTHREADS == MT * U * 256, "X tile must split evenly over the workgroup");
+  __shared__ __attribute__((aligned(16))) bf16_t xs[2 * XBUF];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int KB = K >> 6;
+  const int wg = blockIdx.x / S, split = blockIdx.x % S;
+  const int vgroup = wg * WV + wave;
+  const int tile0 = vgroup * NT;
+  const WStride ws = kmajor ? WStride{256, (size_t)(N >> 5) * 256} : WStride{(size_t)KB * 256, 256};
+  const u32x4_t* wbase = wp + (size_t)tile0 * ws.tile;
+  const int kb0 = (int)((long long)KB * split / S), kb1 = (int)((long long)KB * (split + 1) / S);
+  const int G = (kb1 - kb0) / U;                    // the plan makes (kb1 - kb0) a multiple of U, >= U
+
+  f32x16_t acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[m][t][e] = 0.f;
+
+  WFrag<NT> fa[U], fb[U];
+  {
+    u32x4_t xr[XC];
+    wide_load_x<MT, U, XC>(xr, x, M, ldx, kb0, tid, NTHREADS);
+    wide_load_w<NT, U>(fa, wbase, ws, kb0, lane);
+    wide_store_x<MT, U, XC, PITCH>(xs, xr, tid, NTHREADS);
+    __syncthreads();
+  }
+  int g = 0, kb = kb0;
+  for (; g + 3 <= G; g += 2, kb += 2 * U) {
+    wide_step<MT, NT, U, XC, PITCH, true>(fa, fb, xs, xs + XBUF, acc, wbase, ws, x, M, ldx, kb, tid, NTHREADS, lane,
+                                          r, h);
+    wide_step<MT, NT, U, XC, PITCH, true>(fb, fa, xs + XBUF, xs, acc, wbase, ws, x, M, ldx, kb + U, tid, NTHREADS,
+                                          lane, r, h);
+  }
+  if (G - g == 2) {
+    wide_step<MT, NT, U, XC, PITCH, true>(fa, fb, xs, xs + XBUF, acc, wbase, ws, x, M, ldx, kb, tid, NTHREADS, lane,
+                                          r, h);
+    wide_step<MT, NT, U, XC, PITCH, false>(fb, fa, xs + XBUF, xs, acc, wbase, ws, x, M, ldx, kb + U, tid, NTHREADS,
+                                           lane, r, h);
+  } else {
+    wide_step<MT, NT, U, XC, PITCH, false>(fa, fb, xs, xs + XBUF, acc, wbase, ws, x, M, ldx, kb, tid, NTHREADS, lane,
+                                           r, h);
+  }
+
+  if (S == 1) {
+    wide_epilogue<MT, NT, EPI>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, vgroup, r, h);
+    return;
+  }
+  // Inter-workgroup split, per wave: add the tile into this wave-group's fp32
+  // slab (lane-major, so the adds and the final reads are coalesced), drain,
+  // take a ticket; the last of the S arrivals finishes and re-zeroes.
+  constexpr int SLAB = MT * NT * 16 * 64;
+  float* sc = scratch + (size_t)vgroup * SLAB;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) atomicAdd(sc + ((m * NT + t) * 16 + e) * 64 + lane, acc[m][t][e]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int ticket = 0;
+  if (lane == 0) ticket = atomicAdd(tickets + vgroup, 1);
+  ticket = __shfl(ticket, 0, 64);
+  if (ticket != S - 1) return;
+  wide_epilogue<MT, NT, EPI>(
+      [&](int m, int t, int e) {
+        return __hip_atomic_load(sc + ((m * NT + t) * 16 + e) * 64 + lane, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      },
+      y, M, ldy, tile0, vgroup, r, h);
+#pragma unroll
+  for (int i = 0; i < SLAB / 64; ++i) sc[i * 64 + lane] = 0.f;
+  if (lane == 0) tickets[vgroup] = 0;
+}
+
 // Pack W[N][K] (row-major bf16) into the fragment order above.
-__global__ void pack_weight_kernel(const bf16_t* __restrict__ w, u32x4_t* __restrict__ wp, int N, int K) {
-  const size_t KB = K >> 6;
-  const size_t total = (size_t)(N >> 5) * KB * 256;
+__global__ void pack_weight_kernel(const bf16_t* __restrict__ w, u32x4_t* __restrict__ wp, int N, int K,
+                                   int kmajor) {
+  const size_t KB = K >> 6, NTL = N >> 5;
+  const size_t total = NTL * KB * 256;
   for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (size_t)gridDim.x * blockDim.x) {
     const int l = q & 63;
     const int j = (q >> 6) & 3;
-    const size_t tk = q >> 8;  // t*KB + kb
-    const size_t t = tk / KB, kb = tk % KB;
+    const size_t tk = q >> 8;  // t*KB + kb (tile-major) or kb*NTL + t (k-block-major)
+    const size_t t = kmajor ? tk % NTL : tk / KB, kb = kmajor ? tk / NTL : tk % KB;
     const size_t row = t * 32 + (l & 31);
     const size_t col = kb * 64 + 32 * (l >> 5) + 8 * j;
     wp[q] = *(const u32x4_t*)(w + row * K + col);
@@ -263,14 +597,21 @@ struct Args {
   int M, K, N, ldx, ldy, S;
   float* scratch;
   int* tickets;
+  bool db;
+  int kmajor;
 };
 
 template <int MT, int NT, int KS, int EPI>
 hipError_t launch(const Args& a, hipStream_t s) {
   const int groups = (a.N / 32) / NT;
-  hipLaunchKernelGGL((skinny_gemm_kernel<MT, NT, KS, EPI>), dim3(groups * a.S), dim3(64 * KS), 0, s,
-                     (const u32x4_t*)a.wp, (const bf16_t*)a.x, (bf16_t*)a.y, a.M, a.K, a.N, a.ldx, a.ldy, a.S,
-                     a.scratch, a.tickets);
+  if (a.db)
+    hipLaunchKernelGGL((skinny_gemm_kernel<MT, NT, KS, EPI, true>), dim3(groups * a.S), dim3(64 * KS), 0, s,
+                       (const u32x4_t*)a.wp, (const bf16_t*)a.x, (bf16_t*)a.y, a.M, a.K, a.N, a.ldx, a.ldy, a.S,
+                       a.scratch, a.tickets, a.kmajor);
+  else
+    hipLaunchKernelGGL((skinny_gemm_kernel<MT, NT, KS, EPI, false>), dim3(groups * a.S), dim3(64 * KS), 0, s,
+                       (const u32x4_t*)a.wp, (const bf16_t*)a.x, (bf16_t*)a.y, a.M, a.K, a.N, a.ldx, a.ldy, a.S,
+                       a.scratch, a.tickets, a.kmajor);
   return hipGetLastError();
 }
 
@@ -284,6 +625,7 @@ template <int MT, int NT, int EPI>
 hipError_t launch_ks(int ks, const Args& a, hipStream_t s) {
   constexpr int KSM = ks_max(MT, NT);
   if (ks > KSM) ks = KSM;
+  if (a.db && ks > 4) ks = 4;   // two register buffers: 8 waves per workgroup would spill
   switch (ks) {
     case 1: return launch<MT, NT, 1, EPI>(a, s);
     case 2: return launch<MT, NT, 2, EPI>(a, s);
@@ -301,6 +643,33 @@ hipError_t launch_mt(int mt, int ks, const Args& a, hipStream_t s) {
     case 1: return launch_ks<1, NT, EPI>(ks, a, s);
     case 2: return launch_ks<2, NT, EPI>(ks, a, s);
     case 4: return launch_ks<4, NT, EPI>(ks, a, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int MT, int NT, int EPI>
+hipError_t launch_wide(int wv, const Args& a, hipStream_t s) {
+  const int blocks = (a.N / 32) / NT / wv * a.S;
+#define MIVGPU_LAUNCH_WIDE(WV)                                                                                \
+  hipLaunchKernelGGL((skinny_wide_kernel<MT, NT, WV, EPI>), dim3(blocks), dim3(64 * WV), 0, s,               \
+                     (const u32x4_t*)a.wp, (const bf16_t*)a.x, (bf16_t*)a.y, a.M, a.K, a.N, a.ldx, a.ldy, a.S, \
+                     a.scratch, a.tickets, a.kmajor)
+  switch (wv) {
+    case 1: MIVGPU_LAUNCH_WIDE(1); break;
+    case 2: MIVGPU_LAUNCH_WIDE(2); break;
+    case 4: MIVGPU_LAUNCH_WIDE(4); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef MIVGPU_LAUNCH_WIDE
+  return hipGetLastError();
+}
+
+template <int NT, int EPI>
+hipError_t launch_wide_mt(int mt, int wv, const Args& a, hipStream_t s) {
+  switch (mt) {
+    case 1: return launch_wide<1, NT, EPI>(wv, a, s);
+    case 2: return launch_wide<2, NT, EPI>(wv, a, s);
+    case 4: return launch_wide<4, NT, EPI>(wv, a, s);
   }
   return hipErrorInvalidValue;
 }
@@ -331,6 +700,82 @@ void plan(int M, int K, int N, int epi, int* nt, int* ks, int* S) {
   if (*S <= 0) *S = (!slice && groups <= 128 && KB >= 4 * *ks) ? 2 : 1;
 }
 
+// Double-buffered schedule: MIVGPU_SKINNY_DB=0/1 forces it (A/B runs);
+// default off until measured per partition size.
+bool use_db() {
+  static const int v = [] {
+    const char* e = getenv("MIVGPU_SKINNY_DB");
+    return e && *e ? atoi(e) : -1;
+  }();
+  return v > 0;
+}
+
+// Packed-W layout: MIVGPU_SKINNY_KMAJOR=0/1 (read once per process; packing
+// and the GEMM must agree, so both read it here).
+bool use_kmajor() {
+  static const int v = [] {
+    const char* e = getenv("MIVGPU_SKINNY_KMAJOR");
+    return e && *e ? atoi(e) : -1;
+  }();
+  return v > 0;
+}
+
+constexpr int unroll_wide_host(int nt) { return nt >= 4 ? 1 : (nt == 2 ? 2 : 4); }
+
+// Wide plan (bench/gemm.py --sweep at 64 and 256 CUs, profiles/gemm_wide_*):
+//  * one tile per wave (X shared by the workgroup's waves, not by a wave's
+//    tiles), except SiLU*up, which pairs a gate with an up tile;
+//  * a CU partition (<= 96 CUs): no split, 2 waves per workgroup, 4 when there
+//    are >= 16 wave-groups per CU (lm_head: 422 vs 491 us at 64 CUs);
+//  * the whole chip: S = 4 with 2 waves when <= 128 wave-groups (o_proj,
+//    down), else no split with 2 waves.
+// Values > 0 are requests; false when the wide kernel cannot run them (the
+// caller falls back to the classic kernel).
+bool plan_wide(int K, int N, int epi, int* nt, int* wv, int* S) {
+  static const int cus = mivgpu_ops_visible_cus();
+  const bool slice = cus <= 96;
+  const int ntiles = N / 32, KB = K / 64;
+  if (epi == EPI_SILU_MUL) {
+    if (*nt > 0 && *nt != 2) return false;
+    *nt = 2;
+  }
+  if (*nt <= 0) *nt = 1;
+  if (*nt != 1 && *nt != 2) return false;
+  const int vgroups = ntiles / *nt;
+  const bool auto_s = *S <= 0;
+  if (auto_s) *S = (!slice && vgroups <= 128) ? 4 : 1;
+  if (*wv <= 0) {
+    *wv = (slice && vgroups >= 16 * cus) ? 4 : 2;
+    while (*wv > 1 && ntiles % (*nt * *wv)) *wv /= 2;
+  }
+  if ((*wv != 1 && *wv != 2 && *wv != 4) || ntiles % (*nt * *wv)) return false;
+  const int U = unroll_wide_host(*nt);
+  if (auto_s && *S > 1 && (KB % (*S * U) || KB / *S < U)) *S = 1;   // auto split that does not fit: none
+  return *S >= 1 && KB % (*S * U) == 0 && KB / *S >= U;
+}
+
+// Kernel choice: 1 = classic, 2 = wide; 0 = auto = wide where it can run
+// (MIVGPU_SKINNY_WIDE=0/1 forces one for A/B runs).  An infeasible wide request
+// falls back to classic.  Resolves nt/ks/S for the kernel chosen.
+int resolve(int M, int K, int N, int epi, int* nt, int* ks, int* S, int variant) {
+  if (variant == 0) {
+    static const int env = [] {
+      const char* e = getenv("MIVGPU_SKINNY_WIDE");
+      return e && *e ? atoi(e) : -1;
+    }();
+    variant = env >= 0 ? (env ? 2 : 1) : 2;   // wide unless forced off
+  }
+  if (variant == 2) {
+    int a = *nt, b = *ks, c = *S;
+    if (plan_wide(K, N, epi, &a, &b, &c)) {
+      *nt = a, *ks = b, *S = c;
+      return 2;
+    }
+  }
+  plan(M, K, N, epi, nt, ks, S);
+  return 1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -342,9 +787,9 @@ int mivgpu_skinny_max_m() { return 128; }
 // *scratch_floats fp32 elements and *tickets ints, both zero-initialised by the
 // caller once (the kernel leaves them zeroed).
 int mivgpu_skinny_plan(int M, int K, int N, int epi, int* nt, int* ks, int* S, long long* scratch_floats,
-                       int* tickets) {
+                       int* tickets, int* variant) {
   if (M <= 0 || M > 128 || K <= 0 || (K & 63) || N <= 0 || (N & 31)) return (int)hipErrorInvalidValue;
-  plan(M, K, N, epi, nt, ks, S);
+  *variant = resolve(M, K, N, epi, nt, ks, S, *variant);
   const int groups = (N / 32) / *nt;
   *scratch_floats = *S > 1 ? (long long)groups * (mt_of(M) * 32) * (*nt * 32) : 0;
   *tickets = *S > 1 ? groups : 0;
@@ -358,26 +803,42 @@ int mivgpu_pack_weight(const void* w, void* wp, int N, int K, hipStream_t s) {
   if (N <= 0 || K <= 0 || (N & 31) || (K & 63)) return (int)hipErrorInvalidValue;
   const size_t total = (size_t)(N >> 5) * (K >> 6) * 256;
   const int blocks = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
-  hipLaunchKernelGGL(pack_weight_kernel, dim3(blocks), dim3(256), 0, s, (const bf16_t*)w, (u32x4_t*)wp, N, K);
+  hipLaunchKernelGGL(pack_weight_kernel, dim3(blocks), dim3(256), 0, s, (const bf16_t*)w, (u32x4_t*)wp, N, K,
+                     use_kmajor() ? 1 : 0);
   return (int)hipGetLastError();
 }
 
 // epi: 0 = store Y[M][N] (ldy >= N);  1 = SiLU(gate)*up -> Y[M][N/2] for an
-// interleaved gate/up weight.  nt/ks/S: 0 = auto (see mivgpu_skinny_plan);
+// interleaved gate/up weight.  variant: 0 auto, 1 classic, 2 wide workgroups
+// (ks = waves per workgroup there).  nt/ks/S: 0 = auto (see mivgpu_skinny_plan);
 // scratch/tickets must hold what mivgpu_skinny_plan reports for the same
 // arguments when S > 1.
 int mivgpu_skinny_gemm(const void* wp, const void* x, void* y, int M, int K, int N, int ldx, int ldy, int epi,
-                       int nt, int ks, int S, float* scratch, int* tickets, hipStream_t s) {
+                       int nt, int ks, int S, int variant, float* scratch, int* tickets, hipStream_t s) {
   if (M <= 0 || M > 128 || K <= 0 || (K & 63) || N <= 0 || (N & 31) || ldx < K || (ldx & 7) || (ldy & 7))
     return (int)hipErrorInvalidValue;
   if (epi != EPI_STORE && epi != EPI_SILU_MUL) return (int)hipErrorInvalidValue;
-  plan(M, K, N, epi, &nt, &ks, &S);
+  if (resolve(M, K, N, epi, &nt, &ks, &S, variant) == 2) {
+    if (epi == EPI_SILU_MUL && ldy < N / 2) return (int)hipErrorInvalidValue;
+    if (epi == EPI_STORE && ldy < N) return (int)hipErrorInvalidValue;
+    if (S > 1 && (scratch == nullptr || tickets == nullptr)) return (int)hipErrorInvalidValue;
+    const Args a{wp, x, y, M, K, N, ldx, ldy, S, scratch, tickets, false, use_kmajor() ? 1 : 0};
+    const int mt = mt_of(M);
+    hipError_t e;
+    if (epi == EPI_SILU_MUL)
+      e = launch_wide_mt<2, EPI_SILU_MUL>(mt, ks, a, s);
+    else if (nt == 2)
+      e = launch_wide_mt<2, EPI_STORE>(mt, ks, a, s);
+    else
+      e = launch_wide_mt<1, EPI_STORE>(mt, ks, a, s);
+    return (int)e;
+  }
   if ((N / 32) % nt || S < 1 || S > K / 64) return (int)hipErrorInvalidValue;
   if (epi == EPI_STORE && ldy < N) return (int)hipErrorInvalidValue;
   if (epi == EPI_SILU_MUL && ldy < N / 2) return (int)hipErrorInvalidValue;
   if (S > 1 && (scratch == nullptr || tickets == nullptr)) return (int)hipErrorInvalidValue;
   if (ks != 1 && ks != 2 && ks != 4 && ks != 8) return (int)hipErrorInvalidValue;
-  const Args a{wp, x, y, M, K, N, ldx, ldy, S, scratch, tickets};
+  const Args a{wp, x, y, M, K, N, ldx, ldy, S, scratch, tickets, use_db(), use_kmajor() ? 1 : 0};
   const int mt = mt_of(M);
   hipError_t e;
   if (epi == EPI_SILU_MUL)

@@ -84,22 +84,29 @@ def main():
                     torch.matmul(x, ws[i % ncopy].t(), out=yl)
             t_lib = _time(lib_fn, a.reps)
             t_sk = _time(lambda i: lins[i % ncopy](x, out=out), a.reps)
+            t_wide = _time(lambda i: lins[i % ncopy](x, out=out, variant=ops.VARIANT_WIDE), a.reps)
             row = {"plan": ops.skinny_plan(M, K, N, lin.epi), "shape": name, "M": M, "N": N, "K": K, "fused_silu": silu,
+                   "wide_plan": ops.skinny_plan(M, K, N, lin.epi, variant=ops.VARIANT_WIDE),
+                   "wide_us": round(t_wide, 2), "wide_TBps": round(wbytes / t_wide / 1e6, 3),
                    "hipblaslt_us": round(t_lib, 2), "skinny_us": round(t_sk, 2),
                    "hipblaslt_TBps": round(wbytes / t_lib / 1e6, 3), "skinny_TBps": round(wbytes / t_sk / 1e6, 3),
                    "speedup": round(t_lib / t_sk, 3), "weight_copies": ncopy}
             if a.sweep and M == 32:
                 sw = {}
-                for nt in (1, 2):
-                    for ks in (1, 2, 4, 8):
-                        for S in (1, 2, 4, 8, 16):
-                            if (silu and nt == 1) or S > K // 64 // ks:
-                                continue
-                            try:
-                                sw[f"nt{nt}_ks{ks}_S{S}"] = round(_time(
-                                    lambda i: lins[i % ncopy](x, out=out, nt=nt, ks=ks, S=S), a.reps), 2)
-                            except RuntimeError as e:
-                                sw[f"nt{nt}_ks{ks}_S{S}"] = str(e)[:40]
+                for variant, tag, kss in ((ops.VARIANT_CLASSIC, "", (1, 2, 4, 8)), (ops.VARIANT_WIDE, "wide_", (1, 2, 4))):
+                    for nt in (1, 2):
+                        for ks in kss:
+                            for S in (1, 2, 4, 8, 16):
+                                if (silu and nt == 1) or S > K // 64 // ks:
+                                    continue
+                                if ops.skinny_plan(M, K, N, lin.epi, nt, ks, S, variant)["variant"] != variant:
+                                    continue      # the wide kernel cannot run this split
+                                try:
+                                    sw[f"{tag}nt{nt}_ks{ks}_S{S}"] = round(_time(
+                                        lambda i: lins[i % ncopy](x, out=out, nt=nt, ks=ks, S=S, variant=variant),
+                                        a.reps), 2)
+                                except RuntimeError as e:
+                                    sw[f"{tag}nt{nt}_ks{ks}_S{S}"] = str(e)[:40]
                 best = min((v, k) for k, v in sw.items() if isinstance(v, float))
                 row["sweep_best"] = {"config": best[1], "us": best[0]}
                 row["sweep_us"] = sw

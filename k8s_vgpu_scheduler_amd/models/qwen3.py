@@ -6,10 +6,11 @@ slice vs. natively.  This module is the MI355X-native stand-in for that
 workload: a Qwen3-8B-shaped decoder (GQA 32q/8kv x 128, per-head QK RMSNorm,
 NeoX RoPE theta 1e6, SwiGLU 12288, vocab 151936) whose decode step runs
   * the weight-streaming projections (gate_up with SiLU*up fused into its
-    epilogue, down, lm_head) on the hand-written skinny MFMA GEMM
-    (csrc/ops/skinny_gemm.hip) over fragment-packed weights, for batch <= 32;
-  * qkv / o_proj on hipBLASLt (``F.linear``), where the library is as fast at
-    these 33-50 MB shapes (profiles/gemm);
+    epilogue, down, lm_head, and o_proj inside a CU partition) on the
+    hand-written skinny MFMA GEMM (csrc/ops/skinny_gemm.hip, wide workgroups
+    sharing an LDS X tile) over fragment-packed weights, for batch <= 32;
+  * qkv (and o_proj on the whole chip) on hipBLASLt (``F.linear``), where the
+    library is as fast at these 33-50 MB shapes (profiles/gemm_wide_*);
   * every other op on the hand-written gfx950 kernels of libmivgpu_ops.so,
   * the whole step captured in one hipGraph (launch overhead -> one replay).
 No network: weights are random normal(0, 0.02) of the exact architecture.
@@ -111,15 +112,19 @@ class Qwen3Decoder:
             skinny = os.environ.get("MIVGPU_SKINNY_GEMM", "1") != "0"
             skinny = skinny and self.native and batch <= 32 and shapes_ok
         self.skinny = skinny
-        # gate_up (+SiLU) on the skinny kernel only with >= 128 CUs: in a
-        # 64-CU slice hipBLASLt streams this 201 MB shape faster (78 vs 101 us,
-        # profiles/gemm_cu64.json) while down / lm_head still win.
-        self.skinny_gate_up = skinny and ops.visible_cus() >= 128
+        # The wide-workgroup skinny kernel (X staged once per workgroup in LDS)
+        # beats hipBLASLt on gate_up (+SiLU fused), down and lm_head at 64 and
+        # 256 CUs, and on o_proj inside a CU partition; qkv stays on hipBLASLt
+        # (profiles/gemm_wide_*.json).
+        self.skinny_gate_up = skinny
+        self.skinny_o = skinny and ops.visible_cus() <= 96
         if self.skinny:
             # Keep only the packed copies (no duplicate 16 GB of weights).
             for lw in self.w.layers:
                 if self.skinny_gate_up:
                     lw["pgu"] = ops.PackedLinear(lw.pop("wgu"), silu_mul=True)
+                if self.skinny_o:
+                    lw["po"] = ops.PackedLinear(lw.pop("wo"))
                 lw["pd"] = ops.PackedLinear(lw.pop("wd"))
             self.p_lm = ops.PackedLinear(self.w.lm_head)
             if not cfg.tie_embeddings:
@@ -141,6 +146,7 @@ class Qwen3Decoder:
         self.attn = torch.zeros(batch, cfg.heads * cfg.head_dim, dtype=dt, device=self.device)
         self.act = torch.zeros(batch, cfg.intermediate, dtype=dt, device=self.device)
         self.mlp_out = torch.zeros(batch, h, dtype=dt, device=self.device)
+        self.o_out = torch.zeros(batch, h, dtype=dt, device=self.device)
         self.logits = torch.zeros(batch, cfg.vocab, dtype=dt, device=self.device)
         self.o_part = torch.zeros(batch * cfg.heads * self.nsplit * cfg.head_dim, dtype=torch.float32,
                                   device=self.device)
@@ -188,7 +194,7 @@ class Qwen3Decoder:
                 self.attn.copy_(ref.decode_attention(self.q, self.k_cache[li], self.v_cache[li],
                                                      self.seqlens, cfg.heads, cfg.kv_heads,
                                                      cfg.head_dim, self.scale).view(self.B, -1))
-            o = F.linear(self.attn, lw["wo"])
+            o = lw["po"](self.attn, out=self.o_out) if self.skinny_o else F.linear(self.attn, lw["wo"])
             if self.native:
                 ops.add_rmsnorm(o, self.res, lw["ln2"], cfg.eps, out=self.h)
             else:

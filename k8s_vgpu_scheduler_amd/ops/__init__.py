@@ -43,14 +43,14 @@ def lib():
         L.mivgpu_silu_mul.argtypes = [vp, vp, i, i, vp]
         L.mivgpu_hwid_probe.argtypes = [vp, i, vp]
         L.mivgpu_pack_weight.argtypes = [vp, vp, i, i, vp]
-        L.mivgpu_skinny_gemm.argtypes = [vp, vp, vp, i, i, i, i, i, i, i, i, i, vp, vp, vp]
+        L.mivgpu_skinny_gemm.argtypes = [vp, vp, vp, i, i, i, i, i, i, i, i, i, i, vp, vp, vp]
         ip, lp = ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_longlong)
         L.mivgpu_mfma_burn.argtypes = [vp, i, i, ctypes.c_uint, vp]
         L.mivgpu_mfma_burn_flops.argtypes = [i, i]
         L.mivgpu_mfma_burn_flops.restype = ctypes.c_double
         L.mivgpu_stream_copy.argtypes = [vp, vp, ctypes.c_longlong, i, vp]
         L.mivgpu_stream_read.argtypes = [vp, ctypes.c_longlong, vp, i, vp]
-        L.mivgpu_skinny_plan.argtypes = [i, i, i, i, ip, ip, ip, lp, ip]
+        L.mivgpu_skinny_plan.argtypes = [i, i, i, i, ip, ip, ip, lp, ip, ip]
         for fn in ("mivgpu_rmsnorm", "mivgpu_add_rmsnorm", "mivgpu_qk_norm_rope_kv",
                    "mivgpu_decode_attention", "mivgpu_silu_mul", "mivgpu_ops_attn_split",
                    "mivgpu_hwid_probe", "mivgpu_pack_weight", "mivgpu_skinny_gemm",
@@ -204,15 +204,21 @@ def interleave_gate_up(w_gu: torch.Tensor) -> torch.Tensor:
     return w_gu.view(2, inter // 32, 32, K).transpose(0, 1).reshape(two_i, K)
 
 
-def skinny_plan(M: int, K: int, N: int, epi: int, nt: int = 0, ks: int = 0, S: int = 0) -> dict:
-    """Launch plan the kernel will use (0 = auto) and the scratch it needs."""
+VARIANT_AUTO, VARIANT_CLASSIC, VARIANT_WIDE = 0, 1, 2
+
+
+def skinny_plan(M: int, K: int, N: int, epi: int, nt: int = 0, ks: int = 0, S: int = 0, variant: int = 0) -> dict:
+    """Launch plan the kernel will use (0 = auto) and the scratch it needs.
+    variant: 1 classic (ks = waves splitting K inside a workgroup), 2 wide
+    workgroups (ks = waves sharing one LDS X tile); 0 = auto.  The returned
+    variant is the kernel that will run (an infeasible wide plan falls back)."""
     c = ctypes
-    v_nt, v_ks, v_s, v_t = c.c_int(nt), c.c_int(ks), c.c_int(S), c.c_int(0)
+    v_nt, v_ks, v_s, v_t, v_v = c.c_int(nt), c.c_int(ks), c.c_int(S), c.c_int(0), c.c_int(variant)
     v_f = c.c_longlong(0)
     _check(lib().mivgpu_skinny_plan(M, K, N, epi, c.byref(v_nt), c.byref(v_ks), c.byref(v_s), c.byref(v_f),
-                                    c.byref(v_t)), "skinny_plan")
+                                    c.byref(v_t), c.byref(v_v)), "skinny_plan")
     return {"nt": v_nt.value, "ks": v_ks.value, "S": v_s.value, "scratch_floats": v_f.value,
-            "tickets": v_t.value}
+            "tickets": v_t.value, "variant": v_v.value}
 
 
 class PackedLinear:
@@ -241,17 +247,19 @@ class PackedLinear:
         if tickets and (self.tickets is None or self.tickets.numel() < tickets):
             self.tickets = torch.zeros(tickets, dtype=torch.int32, device=device)
 
-    def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None, nt: int = 0, ks: int = 0, S: int = 0):
+    def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None, nt: int = 0, ks: int = 0, S: int = 0,
+                 variant: int = 0):
         M = x.shape[0]
         if x.dim() != 2 or x.shape[1] != self.K or x.stride(1) != 1:
             raise ValueError(f"skinny_gemm: x must be [M, {self.K}] row-major, got {tuple(x.shape)}")
         if out is None:
             out = torch.empty(M, self.out_features, dtype=torch.bfloat16, device=x.device)
         if 0 < M <= 128:
-            pl = skinny_plan(M, self.K, self.N, self.epi, nt, ks, S)
+            pl = skinny_plan(M, self.K, self.N, self.epi, nt, ks, S, variant)
             self._ensure_scratch(pl["scratch_floats"], pl["tickets"], x.device)
         sp = _p(self.scratch) if self.scratch is not None else None
         tp = _p(self.tickets) if self.tickets is not None else None
         _check(lib().mivgpu_skinny_gemm(_p(self.wp), _p(x), _p(out), M, self.K, self.N, x.stride(0),
-                                        out.stride(0), self.epi, nt, ks, S, sp, tp, _stream()), "skinny_gemm")
+                                        out.stride(0), self.epi, nt, ks, S, variant, sp, tp, _stream()),
+               "skinny_gemm")
         return out

@@ -18,14 +18,45 @@ def _close(got, ref, tol=2e-2):
     assert err / scale < tol, (err, scale)
 
 
+@pytest.mark.parametrize("variant", [ops.VARIANT_CLASSIC, ops.VARIANT_WIDE])
 @pytest.mark.parametrize("M", [1, 7, 32, 33, 64, 100, 128])
 @pytest.mark.parametrize("N,K", [(64, 64), (1024, 512), (4096, 4096), (6144, 4096), (4096, 12288)])
-def test_skinny_gemm_matches_fp32(M, N, K):
+def test_skinny_gemm_matches_fp32(M, N, K, variant):
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
     x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
     w = (torch.randn(N, K, device="cuda", generator=g) * 0.02).bfloat16()
     lin = ops.PackedLinear(w)
-    _close(lin(x), _ref(x, w))
+    if variant == ops.VARIANT_WIDE and K >= 512:      # K = 64 is a single k-block: classic fallback
+        assert ops.skinny_plan(M, K, N, ops.EPI_STORE, variant=variant)["variant"] == ops.VARIANT_WIDE
+    for _ in range(2):   # split-K scratch must come back zeroed
+        _close(lin(x, variant=variant), _ref(x, w))
+
+
+@pytest.mark.parametrize("nt,wv,S", [(1, 1, 1), (1, 4, 1), (2, 2, 1), (2, 4, 1), (1, 4, 4), (2, 4, 2),
+                                     (2, 1, 8), (1, 2, 16), (2, 4, 32)])
+@pytest.mark.parametrize("M", [1, 32, 100])
+def test_wide_variants(nt, wv, S, M):
+    x = torch.randn(M, 4096, device="cuda").bfloat16()
+    w = (torch.randn(2048, 4096, device="cuda") * 0.02).bfloat16()
+    lin = ops.PackedLinear(w)
+    pl = ops.skinny_plan(M, 4096, 2048, ops.EPI_STORE, nt, wv, S, ops.VARIANT_WIDE)
+    assert pl["variant"] == ops.VARIANT_WIDE and (pl["nt"], pl["ks"], pl["S"]) == (nt, wv, S)
+    ref = _ref(x, w)
+    for _ in range(3):
+        _close(lin(x, nt=nt, ks=wv, S=S, variant=ops.VARIANT_WIDE), ref)
+
+
+def test_wide_lm_head_shape_and_fallbacks():
+    # 151936 rows = 4748 tiles: not a multiple of 8 -> one tile per wave
+    assert ops.skinny_plan(32, 4096, 151936, ops.EPI_STORE, variant=ops.VARIANT_WIDE)["nt"] == 1
+    # a split that leaves no whole group per workgroup falls back to the classic kernel
+    assert ops.skinny_plan(32, 4096, 2048, ops.EPI_STORE, 1, 4, 64, ops.VARIANT_WIDE)["variant"] == ops.VARIANT_CLASSIC
+    # 1187 tiles (odd): one tile per wave, one wave per workgroup
+    x = torch.randn(32, 4096, device="cuda").bfloat16()
+    w = (torch.randn(37984, 4096, device="cuda") * 0.02).bfloat16()
+    pl = ops.skinny_plan(32, 4096, 37984, ops.EPI_STORE, variant=ops.VARIANT_WIDE)
+    assert (pl["variant"], pl["nt"], pl["ks"]) == (ops.VARIANT_WIDE, 1, 1)
+    _close(ops.PackedLinear(w)(x, variant=ops.VARIANT_WIDE), _ref(x, w))
 
 
 @pytest.mark.parametrize("nt,ks,S", [(1, 1, 1), (1, 4, 1), (2, 2, 1), (2, 8, 1), (1, 4, 4), (2, 4, 2),
@@ -44,7 +75,8 @@ def test_split_k_under_graph_replay():
     x = torch.randn(32, 4096, device="cuda").bfloat16()
     w = (torch.randn(4096, 4096, device="cuda") * 0.02).bfloat16()
     lin = ops.PackedLinear(w)
-    assert ops.skinny_plan(32, 4096, 4096, ops.EPI_STORE)["S"] > 1   # o_proj shape splits by default
+    # the o_proj shape splits by default on the whole chip; a CU partition (<= 96 CUs) does not split
+    assert (ops.skinny_plan(32, 4096, 4096, ops.EPI_STORE)["S"] > 1) == (ops.visible_cus() > 96)
     out = torch.empty(32, 4096, device="cuda", dtype=torch.bfloat16)
     lin(x, out=out, S=4)
     torch.cuda.synchronize()
@@ -63,20 +95,23 @@ def test_split_k_under_graph_replay():
 def test_exact_on_integers():
     """Small integers are exact in bf16 and fp32: any k-permutation mismatch between
     the packed W and the X fragments shows up as a wrong element."""
-    x = torch.randint(-3, 4, (32, 256), device="cuda").bfloat16()
-    w = torch.randint(-3, 4, (96, 256), device="cuda").bfloat16()
-    got = ops.PackedLinear(w)(x).float()
-    # the fp32 sum is exact; the kernel rounds it to bf16 once (RNE), like this
-    assert torch.equal(got, (x.float() @ w.float().t()).bfloat16().float())
+    x = torch.randint(-3, 4, (32, 512), device="cuda").bfloat16()
+    w = torch.randint(-3, 4, (256, 512), device="cuda").bfloat16()
+    for variant in (ops.VARIANT_CLASSIC, ops.VARIANT_WIDE):
+        assert ops.skinny_plan(32, 512, 256, ops.EPI_STORE, variant=variant)["variant"] == variant
+        got = ops.PackedLinear(w)(x, variant=variant).float()
+        # the fp32 sum is exact; the kernel rounds it to bf16 once (RNE), like this
+        assert torch.equal(got, (x.float() @ w.float().t()).bfloat16().float())
 
 
+@pytest.mark.parametrize("variant", [ops.VARIANT_CLASSIC, ops.VARIANT_WIDE])
 @pytest.mark.parametrize("M", [1, 32, 64, 128])
 @pytest.mark.parametrize("S", [0, 1, 4])
-def test_fused_silu_mul(M, S):
+def test_fused_silu_mul(M, S, variant):
     inter, K = 1024, 512
     x = torch.randn(M, K, device="cuda").bfloat16()
     w = (torch.randn(2 * inter, K, device="cuda") * 0.05).bfloat16()
-    got = ops.PackedLinear(w, silu_mul=True)(x, S=S)
+    got = ops.PackedLinear(w, silu_mul=True)(x, S=S, variant=variant)
     gu = _ref(x, w).bfloat16().float()
     ref = torch.nn.functional.silu(gu[:, :inter]) * gu[:, inter:]
     assert got.shape == (M, inter)
