@@ -726,12 +726,13 @@ constexpr int unroll_wide_host(int nt) { return nt >= 4 ? 1 : (nt == 2 ? 2 : 4);
 //  * one tile per wave (X shared by the workgroup's waves, not by a wave's
 //    tiles), except SiLU*up, which pairs a gate with an up tile;
 //  * a CU partition (<= 96 CUs): no split, 2 waves per workgroup, 4 when there
-//    are >= 16 wave-groups per CU (lm_head: 422 vs 491 us at 64 CUs);
+//    are >= 16 wave-groups per CU (lm_head: 422 vs 491 us at 64 CUs) or more
+//    than 32 rows (2-wave workgroups of 2-4 M-tiles spill);
 //  * the whole chip: S = 4 with 2 waves when <= 128 wave-groups (o_proj,
 //    down), else no split with 2 waves.
 // Values > 0 are requests; false when the wide kernel cannot run them (the
 // caller falls back to the classic kernel).
-bool plan_wide(int K, int N, int epi, int* nt, int* wv, int* S) {
+bool plan_wide(int M, int K, int N, int epi, int* nt, int* wv, int* S) {
   static const int cus = mivgpu_ops_visible_cus();
   const bool slice = cus <= 96;
   const int ntiles = N / 32, KB = K / 64;
@@ -745,7 +746,8 @@ bool plan_wide(int K, int N, int epi, int* nt, int* wv, int* S) {
   const bool auto_s = *S <= 0;
   if (auto_s) *S = (!slice && vgroups <= 128) ? 4 : 1;
   if (*wv <= 0) {
-    *wv = (slice && vgroups >= 16 * cus) ? 4 : 2;
+    // > 32 rows: 4 waves (2-wave workgroups of 2-4 M-tiles spill registers)
+    *wv = (M > 32 || (slice && vgroups >= 16 * cus)) ? 4 : 2;
     while (*wv > 1 && ntiles % (*nt * *wv)) *wv /= 2;
   }
   if ((*wv != 1 && *wv != 2 && *wv != 4) || ntiles % (*nt * *wv)) return false;
@@ -763,11 +765,13 @@ int resolve(int M, int K, int N, int epi, int* nt, int* ks, int* S, int variant)
       const char* e = getenv("MIVGPU_SKINNY_WIDE");
       return e && *e ? atoi(e) : -1;
     }();
-    variant = env >= 0 ? (env ? 2 : 1) : 2;   // wide unless forced off
+    // wide unless forced off; above 64 rows (4 M-tiles) it is not measured
+    // to win (profiles/gemm_wide_plan_full.json), so the classic kernel runs
+    variant = env >= 0 ? (env ? 2 : 1) : (M <= 64 ? 2 : 1);
   }
   if (variant == 2) {
     int a = *nt, b = *ks, c = *S;
-    if (plan_wide(K, N, epi, &a, &b, &c)) {
+    if (plan_wide(M, K, N, epi, &a, &b, &c)) {
       *nt = a, *ks = b, *S = c;
       return 2;
     }
