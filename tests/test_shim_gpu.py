@@ -152,6 +152,9 @@ def test_roctx_markers_on_rocprofv3_timeline(tmp):
     env.update({"MIVGPU_SHARED_CACHE": os.path.join(tmp, "roctx.cache"), "HIP_DEVICE_MEMORY_LIMIT_0": "4096m",
                 "HIP_DEVICE_CORE_LIMIT": "50", "GPU_CORE_UTILIZATION_POLICY": "force", "MIVGPU_ROCTX": "1",
                 "TMPDIR": "/tmp"})
+    # rocprofv3 runs from /tmp (its scratch files): put the package on the path
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env["PYTHONPATH"] = repo + os.pathsep + env.get("PYTHONPATH", "")
     cmd = [rocprof, "--marker-trace", "--kernel-trace", "--output-format", "csv", "-d", out_dir, "--",
            sys.executable, "-m", "k8s_vgpu_scheduler_amd.shim.probe", "--child", "matmul",
            "--n", "4096", "--iters", "20", "--oom-probe-mib", "5000"]
