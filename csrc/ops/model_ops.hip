@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 typedef uint16_t bf16_t;
 
@@ -118,6 +119,7 @@ rmsnorm_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ res, const bf1
 // ------------------------------------------- QK-norm + RoPE + KV append ----
 // grid = (B, Hq + 2*Hkv); one wave per (token, head).  D = 128: lane l owns
 // elements l and l+64, which is exactly a NeoX rotate-half pair.
+template <bool PACKED>
 __global__ void __launch_bounds__(64)
 qk_norm_rope_kv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ qw,
                        const bf16_t* __restrict__ kw, const int* __restrict__ pos,
@@ -137,9 +139,16 @@ qk_norm_rope_kv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict_
   if (h >= Hq + Hkv) {  // V head: plain copy into the cache
     if (!in_range) return;
     const int hv = h - Hq - Hkv;
-    bf16_t* dst = v_cache + (((size_t)b * Hkv + hv) * max_ctx + p) * D;
-    dst[l] = f2bf(x0);
-    dst[l + 64] = f2bf(x1);
+    if (PACKED) {  // V group [dt 8][q 4][r 16][e 8]: key = 8q + e, dim = 16dt + r
+      bf16_t* grp = v_cache + ((size_t)b * Hkv + hv) * (size_t)max_ctx * D + (size_t)(p >> 5) * (32 * D);
+      const int kq = (p & 31) >> 3, ke = p & 7;
+      grp[(((l >> 4) * 4 + kq) * 16 + (l & 15)) * 8 + ke] = f2bf(x0);
+      grp[((((l + 64) >> 4) * 4 + kq) * 16 + (l & 15)) * 8 + ke] = f2bf(x1);
+    } else {
+      bf16_t* dst = v_cache + (((size_t)b * Hkv + hv) * max_ctx + p) * D;
+      dst[l] = f2bf(x0);
+      dst[l + 64] = f2bf(x1);
+    }
     return;
   }
   const bool is_q = h < Hq;
@@ -160,6 +169,14 @@ qk_norm_rope_kv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict_
   } else {
     if (!in_range) return;
     const int hk = h - Hq;
+    if (PACKED) {  // K group [t 2][s 4][q 4][r 16][e 8]: key = 8(r/4) + 4t + r%4, dim = 32s + 8q + e
+      bf16_t* grp = k_cache + ((size_t)b * Hkv + hk) * (size_t)max_ctx * D + (size_t)(p >> 5) * (32 * D);
+      const int k = p & 31;
+      const int kt = (k >> 2) & 1, kr = 4 * (k >> 3) + (k & 3);
+      grp[(((kt * 4 + (l >> 5)) * 4 + ((l >> 3) & 3)) * 16 + kr) * 8 + (l & 7)] = f2bf(o0);
+      grp[(((kt * 4 + ((l + 64) >> 5)) * 4 + (((l + 64) >> 3) & 3)) * 16 + kr) * 8 + (l & 7)] = f2bf(o1);
+      return;
+    }
     dst = k_cache + (((size_t)b * Hkv + hk) * max_ctx + p) * D;
   }
   dst[l] = f2bf(o0);
@@ -371,6 +388,172 @@ decode_attn_partial_kernel(const bf16_t* __restrict__ q, const bf16_t* __restric
   }
 }
 
+// ------------------------------------------- MFMA decode attention (default) --
+// Same partial/combine contract as above, but QK^T and P.V run on
+// v_mfma_f32_16x16x32_bf16, and K and V live in a FRAGMENT-PACKED cache: each
+// 32-key group of a (batch, kv-head) is 8 KB of K followed (in its own
+// tensor) by 8 KB of V, laid out so that every load instruction of a wave is
+// one linear 1 KB read that lands exactly in the MFMA operand registers:
+//   K group: [t 2][s 4][q 4][r 16][e 8]   key = 8*(r/4) + 4t + r%4, dim = 32s + 8q + e
+//   V group: [dt 8][q 4][r 16][e 8]       key = 8q + e,              dim = 16dt + r
+// (lane l = 16q + r reads element block l of every 1 KB slab).  The VALU
+// kernel spends ~1.7k vector instructions per wave per 64 keys on unpack +
+// FMA + shuffles, 30-40 % of its time in a 64- or 32-CU slice; here a wave's
+// 32 keys cost 16 MFMAs and ~60 VALU instructions.
+//
+// grid = (nsplit, Hkv, B), WAVES x 64 threads, 32 keys (one group) per wave:
+//   scores S^T = K (32 keys x 128) . Q^T (128 x G): 2 key tiles x 4 k-steps;
+//     the packing gives lane l the 8 contiguous keys 8*(l/16) .. +8 of query
+//     l%16 in its two C tiles.
+//   local softmax per wave (max/sum over its 32 keys, no barrier).
+//   O^T = V^T (128 x 32 keys) . P^T (32 keys x G): 8 dim tiles; A operand =
+//     the V slab, B operand = the lane's own 8 probabilities (bf16).
+//   one LDS merge of the WAVES per-wave (m, l, O) triples -> partial.
+// All 20 loads of a wave (Q, 8 K, 8 V slabs: 16 KB) are issued before the first
+// MFMA; a wave past the sequence end reads the split's first group (valid
+// memory) and masks everything.
+constexpr int ATT_KPW = 32;            // keys per wave = one packed group
+constexpr int ATT_GROUP = ATT_KPW * ATT_D;   // elements per packed group (K or V)
+
+template <int G, int WAVES, bool NT>
+__global__ void __launch_bounds__(WAVES * 64)
+decode_attn_mfma_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k_pack,
+                        const bf16_t* __restrict__ v_pack, const int* __restrict__ seqlens,
+                        float* __restrict__ o_part, float* __restrict__ ml_part, int Hq, int Hkv,
+                        int max_ctx, int nsplit, float scale_log2) {
+  typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+  typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+  constexpr int SPLIT = WAVES * ATT_KPW;
+  constexpr int DP = ATT_D + 4;   // padded LDS row
+  const int split = blockIdx.x;
+  const int hk = blockIdx.y;
+  const int b = blockIdx.z;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const int r16 = lane & 15, q4 = lane >> 4;
+  const int L = min(seqlens[b], max_ctx);
+  const int j0 = split * SPLIT;
+  const int n = min(SPLIT, L - j0);
+  const size_t part_base = ((size_t)b * Hq + (size_t)hk * G);
+  if (n <= 0) {
+    if (t < G) {
+      ml_part[((part_base + t) * nsplit + split) * 2 + 0] = -INFINITY;
+      ml_part[((part_base + t) * nsplit + split) * 2 + 1] = 0.f;
+    }
+    return;
+  }
+  __shared__ float s_o[WAVES][G][DP];
+  __shared__ float s_m[WAVES][G];
+  __shared__ float s_l[WAVES][G];
+
+  const int wj0 = j0 + wave * ATT_KPW;   // first key of this wave
+  const int wn = min(ATT_KPW, L - wj0);   // valid keys of this wave (may be <= 0)
+  const int grp = (wn > 0 ? wj0 : j0) / ATT_KPW;
+  const size_t gbase = ((size_t)b * Hkv + hk) * (size_t)max_ctx * ATT_D + (size_t)grp * ATT_GROUP;
+
+  // Q as the B operand: lane -> query r16, dims 32*s + 8*q4 .. +8.  Columns
+  // r16 >= G load a duplicate query: MFMA columns are independent, and only
+  // columns < G are ever stored.
+  uint4 qr[4];
+  {
+    const int g = r16 < G ? r16 : 0;
+    const uint4* qp = reinterpret_cast<const uint4*>(q + (part_base + g) * ATT_D + 8 * q4);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qr[s] = qp[4 * s];
+  }
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+  const u32x4_t* kp = reinterpret_cast<const u32x4_t*>(k_pack + gbase) + lane;
+  const u32x4_t* vp = reinterpret_cast<const u32x4_t*>(v_pack + gbase) + lane;
+  u32x4_t kr[2][4];
+  u32x4_t vr[8];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) kr[tt][s] = NT ? __builtin_nontemporal_load(kp + 64 * (4 * tt + s)) : kp[64 * (4 * tt + s)];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) vr[dt] = NT ? __builtin_nontemporal_load(vp + 64 * dt) : vp[64 * dt];
+  // keep all loads ahead of the first MFMA (the scheduler would otherwise
+  // sink the V loads below the softmax to save registers: 16 KB in flight
+  // per wave is the point of this kernel)
+  __builtin_amdgcn_sched_barrier(0);
+
+  // ---- scores (raw dot products; scale folded into the exp2)
+  f32x4_t sc[2];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    sc[tt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      sc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, kr[tt][s]),
+                                                      __builtin_bit_cast(bf16x8_t, qr[s]), sc[tt], 0, 0, 0);
+  }
+  // ---- local softmax: lane holds keys 8*q4 + 4*tt + i of query r16
+  float p[8];
+  float m = -INFINITY;
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool ok = (8 * q4 + 4 * tt + i) < wn;
+      p[4 * tt + i] = ok ? sc[tt][i] : -INFINITY;
+      m = fmaxf(m, p[4 * tt + i]);
+    }
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float lsum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    p[j] = m == -INFINITY ? 0.f : exp2f((p[j] - m) * scale_log2);
+    lsum += p[j];
+  }
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  bf16x8_t pb;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) pb[j] = (__bf16)p[j];
+
+  // ---- P.V: C tile dt, lane l, reg i -> dim 16*dt + 4*q4 + i, query r16
+  f32x4_t o[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+    o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, vr[dt]), pb,
+                                                    f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+  if (r16 < G) {
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s_o[wave][r16][16 * dt + 4 * q4 + i] = o[dt][i];
+    if (q4 == 0) {
+      s_m[wave][r16] = m;
+      s_l[wave][r16] = lsum;
+    }
+  }
+  __syncthreads();
+  // ---- merge the waves: partial relative to the split max (base-2 scaled)
+  for (int idx = t; idx < G * ATT_D; idx += WAVES * 64) {
+    const int g = idx / ATT_D, d = idx % ATT_D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) M = fmaxf(M, s_m[w][g]);
+    float num = 0.f, den = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) {
+        const float mw = s_m[w][g];
+        const float f = mw == -INFINITY ? 0.f : exp2f((mw - M) * scale_log2);
+        num += f * s_o[w][g][d];
+        den += f * s_l[w][g];
+      }
+    }
+    o_part[((part_base + g) * nsplit + split) * ATT_D + d] = num;
+    if (d == 0) {
+      // the combine kernel works in natural-log units of the scaled scores
+      ml_part[((part_base + g) * nsplit + split) * 2 + 0] = M == -INFINITY ? -INFINITY : M * scale_log2 * 0.69314718f;
+      ml_part[((part_base + g) * nsplit + split) * 2 + 1] = den;
+    }
+  }
+}
+
 // grid = (Hq, B), 128 threads (one per output dim).
 __global__ void __launch_bounds__(128)
 decode_attn_combine_kernel(const float* __restrict__ o_part, const float* __restrict__ ml_part,
@@ -426,14 +609,51 @@ int mivgpu_add_rmsnorm(const void* x, void* res, const void* w, void* out, int r
   return (int)hipGetLastError();
 }
 
+// Decode-attention implementation, read once per process: 0 = the VALU
+// split-K kernel (row-major K and V caches), 8 / 4 = the MFMA kernel with 8
+// (default) or 4 waves per workgroup (fragment-packed caches).
+// MIVGPU_ATTN_KERNEL=mfma|mfma4|valu; MIVGPU_ATTN_NT=1|0 picks the MFMA
+// kernel's K/V load policy (nontemporal by default: every byte is read once).
+// Measured (Qwen3-8B, B=32, ctx 1024, profiles/attention_mfma.json):
+//   256 / 64 / 32 CUs: VALU 34.6 / 73.1 / 132 us, MFMA-8 nt 28.7 / 52.4 / 92.4 us.
+static int attn_impl() {
+  static const int impl = [] {
+    const char* e = getenv("MIVGPU_ATTN_KERNEL");
+    if (!e || !*e || !strcmp(e, "mfma")) return 8;
+    if (!strcmp(e, "mfma4")) return 4;
+    if (!strcmp(e, "valu")) return 0;
+    return 8;
+  }();
+  return impl;
+}
+
+static int attn_nt() {
+  static const int nt = [] {
+    const char* e = getenv("MIVGPU_ATTN_NT");
+    return e ? atoi(e) : 1;
+  }();
+  return nt;
+}
+
+// 1 = fragment-packed K/V caches (32-key groups), 0 = row-major [B][Hkv][T][D]
+int mivgpu_ops_kv_packed() { return attn_impl() != 0; }
+
 int mivgpu_qk_norm_rope_kv(const void* qkv, const void* qw, const void* kw, const int* pos,
                            void* q_out, void* k_cache, void* v_cache, int B, int Hq, int Hkv,
                            int head_dim, int max_ctx, float eps, float theta, hipStream_t s) {
   if (head_dim != 128 || B <= 0) return -1;
-  hipLaunchKernelGGL(qk_norm_rope_kv_kernel, dim3(B, Hq + 2 * Hkv), dim3(64), 0, s,
-                     (const bf16_t*)qkv, (const bf16_t*)qw, (const bf16_t*)kw, pos,
-                     (bf16_t*)q_out, (bf16_t*)k_cache, (bf16_t*)v_cache, Hq, Hkv, max_ctx, eps,
-                     theta);
+  if (attn_impl()) {
+    if (max_ctx % ATT_KPW) return -1;
+    hipLaunchKernelGGL(qk_norm_rope_kv_kernel<true>, dim3(B, Hq + 2 * Hkv), dim3(64), 0, s,
+                       (const bf16_t*)qkv, (const bf16_t*)qw, (const bf16_t*)kw, pos,
+                       (bf16_t*)q_out, (bf16_t*)k_cache, (bf16_t*)v_cache, Hq, Hkv, max_ctx, eps,
+                       theta);
+  } else {
+    hipLaunchKernelGGL(qk_norm_rope_kv_kernel<false>, dim3(B, Hq + 2 * Hkv), dim3(64), 0, s,
+                       (const bf16_t*)qkv, (const bf16_t*)qw, (const bf16_t*)kw, pos,
+                       (bf16_t*)q_out, (bf16_t*)k_cache, (bf16_t*)v_cache, Hq, Hkv, max_ctx, eps,
+                       theta);
+  }
   return (int)hipGetLastError();
 }
 
@@ -447,6 +667,41 @@ int mivgpu_decode_attention(const void* q, const void* k_cache, const void* v_ca
   if (head_dim != ATT_D || Hq % Hkv || nsplit <= 0 || B <= 0) return -1;
   const int G = Hq / Hkv;
   dim3 grid(nsplit, Hkv, B);
+  if (attn_impl()) {
+    const int waves = attn_impl();
+    // the workspace must cover every key: nsplit * split >= max_ctx
+    if (max_ctx % ATT_KPW || (long long)nsplit * waves * ATT_KPW < max_ctx) return -1;
+    const bool nt = attn_nt() != 0;
+    const float scale_log2 = scale * 1.44269504f;
+#define MIVGPU_ATTN_MFMA(GG, WW, NN)                                                                      \
+  hipLaunchKernelGGL((decode_attn_mfma_kernel<GG, WW, NN>), grid, dim3(WW * 64), 0, s, (const bf16_t*)q, \
+                     (const bf16_t*)k_cache, (const bf16_t*)v_cache, seqlens, (float*)o_part,             \
+                     (float*)ml_part, Hq, Hkv, max_ctx, nsplit, scale_log2)
+#define MIVGPU_ATTN_MFMA_G(GG)                                  \
+  case GG:                                                      \
+    if (waves == 8) {                                           \
+      if (nt) MIVGPU_ATTN_MFMA(GG, 8, true);                    \
+      else MIVGPU_ATTN_MFMA(GG, 8, false);                      \
+    } else {                                                    \
+      if (nt) MIVGPU_ATTN_MFMA(GG, 4, true);                    \
+      else MIVGPU_ATTN_MFMA(GG, 4, false);                      \
+    }                                                           \
+    break;
+    switch (G) {
+      MIVGPU_ATTN_MFMA_G(1)
+      MIVGPU_ATTN_MFMA_G(2)
+      MIVGPU_ATTN_MFMA_G(4)
+      MIVGPU_ATTN_MFMA_G(8)
+      MIVGPU_ATTN_MFMA_G(16)
+      default:
+        return -1;
+    }
+#undef MIVGPU_ATTN_MFMA_G
+#undef MIVGPU_ATTN_MFMA
+    hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(Hq, B), dim3(ATT_D), 0, s,
+                       (const float*)o_part, (const float*)ml_part, (bf16_t*)out, Hq, nsplit, nsplit);
+    return (int)hipGetLastError();
+  }
   // Load scheduling variant (see the kernel); MIVGPU_ATTN_PF overrides for experiments.
   static const int pf_env = [] {
     const char* e = getenv("MIVGPU_ATTN_PF");
@@ -495,7 +750,7 @@ int mivgpu_silu_mul(const void* gate_up, void* out, int rows, int inter, hipStre
   return (int)hipGetLastError();
 }
 
-int mivgpu_ops_attn_split() { return ATT_SPLIT; }
+int mivgpu_ops_attn_split() { return attn_impl() ? attn_impl() * ATT_KPW : ATT_SPLIT; }
 
 // CUs this process can run on: the HSA_CU_MASK bits of the current device
 // (a vGPU slice's partition, "i:lo-hi,..;j:..") or, without a mask, the

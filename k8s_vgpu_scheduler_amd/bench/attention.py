@@ -1,5 +1,6 @@
-"""Decode-attention microbenchmark (csrc/ops/model_ops.hip) across load-
-scheduling variants and CU partitions.
+"""Decode-attention microbenchmark (csrc/ops/model_ops.hip): the MFMA kernel
+(4 / 8 waves) and the VALU kernel's load-scheduling variants, across CU
+partitions.
 
 Qwen3-8B shape: B=32 sequences, 32 query / 8 KV heads x 128, context 1024.
 Each call reads K+V of one layer (134 MB); calls rotate over ``--layers`` KV
@@ -30,8 +31,9 @@ def child(a):
 
     B, Hq, Hkv, D = a.batch, 32, 8, 128
     T = a.ctx + 16
-    ks = [torch.randn(B, Hkv, T, D, device="cuda").bfloat16() for _ in range(a.layers)]
-    vs = [torch.randn(B, Hkv, T, D, device="cuda").bfloat16() for _ in range(a.layers)]
+    T = -(-T // 32) * 32
+    ks = [ops.k_to_cache_layout(torch.randn(B, Hkv, T, D, device="cuda").bfloat16()) for _ in range(a.layers)]
+    vs = [ops.v_to_cache_layout(torch.randn(B, Hkv, T, D, device="cuda").bfloat16()) for _ in range(a.layers)]
     q = torch.randn(B, Hq, D, device="cuda").bfloat16()
     seqlens = torch.full((B,), a.ctx, dtype=torch.int32, device="cuda")
     nsplit = math.ceil(T / ops.attn_split())
@@ -60,7 +62,9 @@ def child(a):
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1000 / a.reps
     kv_bytes = 2 * B * Hkv * a.ctx * D * 2
-    print(json.dumps({"pf": os.environ.get("MIVGPU_ATTN_PF", "auto"), "cu_mask": os.environ.get("HSA_CU_MASK", ""),
+    print(json.dumps({"kernel": os.environ.get("MIVGPU_ATTN_KERNEL", "mfma"), "split": ops.attn_split(),
+                      "nt": os.environ.get("MIVGPU_ATTN_NT", "1"),
+                      "pf": os.environ.get("MIVGPU_ATTN_PF", "auto"), "cu_mask": os.environ.get("HSA_CU_MASK", ""),
                       "us": round(us, 2), "kv_TBps": round(kv_bytes / us / 1e6, 3)}), flush=True)
 
 
@@ -71,7 +75,8 @@ def main():
     ap.add_argument("--ctx", type=int, default=1024)
     ap.add_argument("--layers", type=int, default=8)
     ap.add_argument("--reps", type=int, default=64)
-    ap.add_argument("--variants", default="0,1,2")
+    ap.add_argument("--variants", default="mfma,mfma4,valu:auto",
+                    help="mfma | mfma4 | mfma:cached | mfma4:cached | valu:<pf> with pf in 0,1,2,auto")
     ap.add_argument("--masks", default=",0:0-63,0:0-31")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -79,10 +84,15 @@ def main():
         return child(a)
     rows = []
     for mask in a.masks.split(","):
-        for pf in a.variants.split(","):
-            env = dict(os.environ, MIVGPU_ATTN_PF=pf)
-            if pf == "auto":            # the library's own CU-aware choice
-                env.pop("MIVGPU_ATTN_PF")
+        for var in a.variants.split(","):
+            kernel, _, opt = var.partition(":")
+            env = dict(os.environ, MIVGPU_ATTN_KERNEL=kernel)
+            env.pop("MIVGPU_ATTN_PF", None)
+            env.pop("MIVGPU_ATTN_NT", None)
+            if opt == "cached":
+                env["MIVGPU_ATTN_NT"] = "0"
+            elif opt and opt != "auto":     # auto = the library's own CU-aware choice
+                env["MIVGPU_ATTN_PF"] = opt
             env.pop("HSA_CU_MASK", None)
             if mask:
                 env["HSA_CU_MASK"] = mask
@@ -90,7 +100,7 @@ def main():
                                 "--batch", str(a.batch), "--ctx", str(a.ctx), "--layers", str(a.layers),
                                 "--reps", str(a.reps)], env=env, capture_output=True, text=True, timeout=600)
             line = next((x for x in r.stdout.splitlines() if x.startswith("{")), None)
-            row = json.loads(line) if line else {"pf": pf, "cu_mask": mask, "error": r.stderr[-500:]}
+            row = json.loads(line) if line else {"variant": var, "cu_mask": mask, "error": r.stderr[-500:]}
             print(json.dumps(row), flush=True)
             rows.append(row)
     if a.out:

@@ -100,9 +100,10 @@ class Qwen3Decoder:
                  native: bool | None = None, seed: int = 0, skinny: bool | None = None):
         self.cfg = cfg
         self.B = batch
-        self.T = max_ctx
         self.device = torch.device(device)
         self.native = (self.device.type == "cuda") if native is None else native
+        # KV length padded to whole 32-key groups (the packed KV layout)
+        self.T = -(-max_ctx // 32) * 32
         if self.native:
             ops.require_native()
         self.w = Qwen3Weights(cfg, self.device, seed=seed)
@@ -131,13 +132,18 @@ class Qwen3Decoder:
                 self.w.lm_head = None
             torch.cuda.empty_cache()
         dt = torch.bfloat16
-        kvshape = (batch, cfg.kv_heads, max_ctx, cfg.head_dim)
-        self.k_cache = [torch.zeros(kvshape, dtype=dt, device=self.device) for _ in range(cfg.layers)]
-        self.v_cache = [torch.zeros(kvshape, dtype=dt, device=self.device) for _ in range(cfg.layers)]
+        kvshape = (batch, cfg.kv_heads, self.T, cfg.head_dim)
+        # K/V in the attention kernel's layout (fragment-packed 32-key groups
+        # for the MFMA kernel: ops.kv_cache_shape); the fp32 reference path
+        # keeps [B, Hkv, T, D] rows.
+        self.kv_native_layout = self.native and ops.kv_packed()
+        pshape = ops.kv_cache_shape(*kvshape) if self.native else kvshape
+        self.k_cache = [torch.zeros(pshape, dtype=dt, device=self.device) for _ in range(cfg.layers)]
+        self.v_cache = [torch.zeros(pshape, dtype=dt, device=self.device) for _ in range(cfg.layers)]
         self.tokens = torch.zeros(batch, dtype=torch.long, device=self.device)
         self.pos = torch.zeros(batch, dtype=torch.int32, device=self.device)
         self.seqlens = torch.ones(batch, dtype=torch.int32, device=self.device)
-        self.nsplit = max(1, math.ceil(max_ctx / (ops.attn_split() if self.native else 256)))
+        self.nsplit = max(1, math.ceil(self.T / (ops.attn_split() if self.native else 256)))
         h = cfg.hidden
         # Static activation buffers (graph-capture friendly).
         self.res = torch.zeros(batch, h, dtype=dt, device=self.device)
@@ -161,9 +167,19 @@ class Qwen3Decoder:
         assert 0 < ctx_len < self.T
         g = torch.Generator(device=self.device)
         g.manual_seed(seed)
+        shape = (self.B, self.cfg.kv_heads, ctx_len, self.cfg.head_dim)
+        full = torch.zeros(self.B, self.cfg.kv_heads, self.T, self.cfg.head_dim, dtype=torch.bfloat16,
+                           device=self.device)
         for kc, vc in zip(self.k_cache, self.v_cache):
-            kc[:, :, :ctx_len].normal_(0, 1.0, generator=g)
-            vc[:, :, :ctx_len].normal_(0, 1.0, generator=g)
+            # drawn in the logical [B, Hkv, ctx, D] order whatever the cache
+            # layout, so native and reference decoders see the same context
+            for c, to_layout in ((kc, ops.k_to_cache_layout), (vc, ops.v_to_cache_layout)):
+                x = torch.randn(shape, generator=g, device=self.device, dtype=torch.float32).to(c.dtype)
+                if self.kv_native_layout:
+                    full[:, :, :ctx_len] = x
+                    c.copy_(to_layout(full))
+                else:
+                    c[:, :, :ctx_len] = x
         self.pos.fill_(ctx_len)
         self.seqlens.fill_(ctx_len + 1)
         self.tokens.copy_(torch.randint(0, self.cfg.vocab, (self.B,), generator=g, device=self.device))

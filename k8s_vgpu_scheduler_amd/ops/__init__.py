@@ -55,7 +55,8 @@ def lib():
                    "mivgpu_decode_attention", "mivgpu_silu_mul", "mivgpu_ops_attn_split",
                    "mivgpu_hwid_probe", "mivgpu_pack_weight", "mivgpu_skinny_gemm",
                    "mivgpu_skinny_max_m", "mivgpu_skinny_plan", "mivgpu_mfma_burn",
-                   "mivgpu_stream_copy", "mivgpu_stream_read", "mivgpu_ops_visible_cus"):
+                   "mivgpu_stream_copy", "mivgpu_stream_read", "mivgpu_ops_visible_cus",
+                   "mivgpu_ops_kv_packed"):
             getattr(L, fn).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -106,10 +107,21 @@ def add_rmsnorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: float,
     return out
 
 
+def _check_kv(k_cache, v_cache, B, n_kv_heads, head_dim):
+    """Host-side check that both caches are in the layout the kernels index; returns T."""
+    T = k_cache.shape[2] * (32 if kv_packed() else 1)
+    want = kv_cache_shape(B, n_kv_heads, T, head_dim)
+    if tuple(k_cache.shape) != want or tuple(v_cache.shape) != want \
+            or not (k_cache.is_contiguous() and v_cache.is_contiguous()):
+        raise ValueError(f"KV cache shapes {tuple(k_cache.shape)} / {tuple(v_cache.shape)} do not match "
+                         f"the kernels' layout {want} (contiguous)")
+    return T
+
+
 def qk_norm_rope_kv(qkv, q_norm_w, k_norm_w, pos, q_out, k_cache, v_cache, n_q_heads, n_kv_heads,
                     head_dim, eps, theta):
     B = qkv.shape[0]
-    max_ctx = k_cache.shape[2]
+    max_ctx = _check_kv(k_cache, v_cache, B, n_kv_heads, head_dim)
     _check(lib().mivgpu_qk_norm_rope_kv(_p(qkv), _p(q_norm_w), _p(k_norm_w), _p(pos), _p(q_out),
                                         _p(k_cache), _p(v_cache), B, n_q_heads, n_kv_heads, head_dim,
                                         max_ctx, eps, theta, _stream()), "qk_norm_rope_kv")
@@ -121,13 +133,83 @@ def visible_cus() -> int:
 
 
 def attn_split() -> int:
+    """Keys per decode-attention partial workgroup (size the workspace with it)."""
     return int(lib().mivgpu_ops_attn_split())
+
+
+def kv_packed() -> bool:
+    """True when the KV caches are fragment-packed (the MFMA attention kernel,
+    MIVGPU_ATTN_KERNEL != valu): per (batch, kv-head), 32-key groups of 4096
+    elements laid out as the MFMA operands (csrc/ops/model_ops.hip)."""
+    return bool(lib().mivgpu_ops_kv_packed())
+
+
+def kv_cache_shape(B: int, Hkv: int, T: int, D: int) -> tuple:
+    """Shape of a K or V cache of logical size [B, Hkv, T, D] in the kernels' layout."""
+    if kv_packed():
+        if T % 32 or D != 128:
+            raise ValueError(f"packed KV cache needs T % 32 == 0 and D == 128 (T={T}, D={D})")
+        return (B, Hkv, T // 32, 32 * D)
+    return (B, Hkv, T, D)
+
+
+# Logical [B, H, T, D] viewed as [B, H, g, key factors..., dim factors...] and
+# permuted into the packed group order (see the kernel's layout comment):
+#   K: key = 8a + 4t + c, dim = 32s + 8q + e -> [t][s][q][a c][e]
+#   V: key = 8q + e,      dim = 16dt + r    -> [dt][q][r][e]
+def _k_pack_view(k):
+    B, H, T, D = k.shape
+    return k.reshape(B, H, T // 32, 4, 2, 4, 4, 4, 8).permute(0, 1, 2, 4, 6, 7, 3, 5, 8)
+
+
+def _v_pack_view(v):
+    B, H, T, D = v.shape
+    return v.reshape(B, H, T // 32, 4, 8, 8, 16).permute(0, 1, 2, 5, 3, 6, 4)
+
+
+def k_to_cache_layout(k: torch.Tensor) -> torch.Tensor:
+    """Logical [B, Hkv, T, D] K -> contiguous copy in the kernels' layout."""
+    if not kv_packed():
+        return k.contiguous()
+    B, H, T, D = k.shape
+    return _k_pack_view(k).contiguous().view(kv_cache_shape(B, H, T, D))
+
+
+def v_to_cache_layout(v: torch.Tensor) -> torch.Tensor:
+    """Logical [B, Hkv, T, D] V -> contiguous copy in the kernels' layout."""
+    if not kv_packed():
+        return v.contiguous()
+    B, H, T, D = v.shape
+    return _v_pack_view(v).contiguous().view(kv_cache_shape(B, H, T, D))
+
+
+def k_from_cache_layout(k: torch.Tensor, D: int = 128) -> torch.Tensor:
+    """Kernel-layout K cache -> logical [B, Hkv, T, D]."""
+    if not kv_packed():
+        return k
+    B, H, G, _ = k.shape
+    out = torch.empty(B, H, G * 32, D, dtype=k.dtype, device=k.device)
+    _k_pack_view(out).copy_(k.view(B, H, G, 2, 4, 4, 4, 4, 8))
+    return out
+
+
+def v_from_cache_layout(v: torch.Tensor, D: int = 128) -> torch.Tensor:
+    """Kernel-layout V cache -> logical [B, Hkv, T, D]."""
+    if not kv_packed():
+        return v
+    B, H, G, _ = v.shape
+    out = torch.empty(B, H, G * 32, D, dtype=v.dtype, device=v.device)
+    _v_pack_view(out).copy_(v.view(B, H, G, 8, 4, 16, 8))
+    return out
 
 
 def decode_attention(q, k_cache, v_cache, seqlens, out, o_part, ml_part, n_q_heads, n_kv_heads,
                      head_dim, nsplit, scale):
     B = q.shape[0]
-    max_ctx = k_cache.shape[2]
+    max_ctx = _check_kv(k_cache, v_cache, B, n_kv_heads, head_dim)
+    need = B * n_q_heads * nsplit
+    if nsplit * attn_split() < max_ctx or o_part.numel() < need * head_dim or ml_part.numel() < need * 2:
+        raise ValueError(f"attention workspace too small for nsplit={nsplit}, max_ctx={max_ctx}")
     _check(lib().mivgpu_decode_attention(_p(q), _p(k_cache), _p(v_cache), _p(seqlens), _p(out),
                                          _p(o_part), _p(ml_part), B, n_q_heads, n_kv_heads, head_dim,
                                          max_ctx, nsplit, scale, _stream()), "decode_attention")

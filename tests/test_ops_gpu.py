@@ -52,24 +52,45 @@ def test_qk_norm_rope_kv(ops, B, Hq, Hkv):
     kw = (1 + 0.1 * torch.randn(D, device="cuda")).to(torch.bfloat16)
     pos = torch.tensor([0, 5, 63, 17][:B], dtype=torch.int32, device="cuda")
     q1 = torch.empty(B, Hq, D, device="cuda", dtype=torch.bfloat16)
-    k1 = torch.zeros(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
+    k1 = torch.zeros(ops.kv_cache_shape(B, Hkv, T, D), device="cuda", dtype=torch.bfloat16)
     v1 = torch.zeros_like(k1)
-    q2, k2, v2 = q1.clone(), k1.clone(), v1.clone()
+    q2 = q1.clone()
+    k2 = torch.zeros(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
+    v2 = torch.zeros_like(k2)
     ops.qk_norm_rope_kv(qkv, qw, kw, pos, q1, k1, v1, Hq, Hkv, D, 1e-6, 1e6)
     ref.qk_norm_rope_kv(qkv, qw, kw, pos, q2, k2, v2, Hq, Hkv, D, 1e-6, 1e6)
     torch.cuda.synchronize()
     _close(q1, q2, 2e-2)
-    _close(k1, k2, 2e-2)
-    _close(v1, v2, 1e-3)
+    # K/V land in the attention kernel's layout (fragment-packed for the MFMA kernel)
+    _close(ops.k_from_cache_layout(k1), k2, 2e-2)
+    _close(ops.v_from_cache_layout(v1), v2, 1e-3)
+
+
+def test_kv_layout_roundtrip(ops):
+    k = torch.randn(2, 3, 96, 128, device="cuda").bfloat16()
+    assert torch.equal(ops.k_from_cache_layout(ops.k_to_cache_layout(k)), k)
+    assert torch.equal(ops.v_from_cache_layout(ops.v_to_cache_layout(k)), k)
+    if ops.kv_packed():
+        # one lane's 16-byte K fragment: key 8*(r/4) + 4t + r%4, dims 32s + 8q .. +8
+        pk = ops.k_to_cache_layout(k)
+        t, s, q, r = 1, 2, 3, 6
+        off = (((t * 4 + s) * 4 + q) * 16 + r) * 8
+        key = 8 * (r // 4) + 4 * t + r % 4
+        assert torch.equal(pk[1, 2, 1, off:off + 8], k[1, 2, 32 + key, 32 * s + 8 * q:32 * s + 8 * q + 8])
+        # one lane's V fragment: keys 8q .. +8 of dim 16dt + r
+        pv = ops.v_to_cache_layout(k)
+        dt, q, r = 5, 2, 11
+        off = ((dt * 4 + q) * 16 + r) * 8
+        assert torch.equal(pv[0, 1, 2, off:off + 8], k[0, 1, 64 + 8 * q:64 + 8 * q + 8, 16 * dt + r])
 
 
 def test_qk_norm_rope_kv_out_of_range_pos_is_dropped(ops):
-    B, Hq, Hkv, D, T = 2, 8, 2, 128, 16
+    B, Hq, Hkv, D, T = 2, 8, 2, 128, 32
     qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
     w = torch.ones(D, device="cuda", dtype=torch.bfloat16)
     pos = torch.tensor([T, T + 100], dtype=torch.int32, device="cuda")
     q = torch.empty(B, Hq, D, device="cuda", dtype=torch.bfloat16)
-    k = torch.zeros(B, Hkv, T, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.zeros(ops.kv_cache_shape(B, Hkv, T, D), device="cuda", dtype=torch.bfloat16)
     v = torch.zeros_like(k)
     ops.qk_norm_rope_kv(qkv, w, w, pos, q, k, v, Hq, Hkv, D, 1e-6, 1e6)
     torch.cuda.synchronize()
@@ -78,8 +99,9 @@ def test_qk_norm_rope_kv_out_of_range_pos_is_dropped(ops):
 
 @pytest.mark.parametrize("B,Hq,Hkv,T,lens", [
     (2, 32, 8, 1024, [1, 1000]),
-    (3, 32, 8, 600, [257, 256, 599]),
-    (2, 8, 8, 300, [300, 7]),
+    (3, 32, 8, 608, [257, 256, 599]),
+    (2, 8, 8, 320, [300, 7]),
+    (2, 32, 8, 1152, [1031, 1152]),
     (1, 16, 2, 2048, [2048]),
 ])
 def test_decode_attention(ops, B, Hq, Hkv, T, lens):
@@ -95,7 +117,8 @@ def test_decode_attention(ops, B, Hq, Hkv, T, lens):
     o_part = torch.empty(B * Hq * nsplit * D, device="cuda", dtype=torch.float32)
     ml = torch.empty(B * Hq * nsplit * 2, device="cuda", dtype=torch.float32)
     scale = 1 / math.sqrt(D)
-    ops.decode_attention(q, k, v, seqlens, out, o_part, ml, Hq, Hkv, D, nsplit, scale)
+    ops.decode_attention(q, ops.k_to_cache_layout(k), ops.v_to_cache_layout(v), seqlens, out, o_part, ml, Hq, Hkv,
+                         D, nsplit, scale)
     exp = ref.decode_attention(q, k, v, seqlens, Hq, Hkv, D, scale)
     _close(out.view(B, Hq, D), exp, 2e-2)
 
@@ -155,7 +178,7 @@ _ATTN_CHILD = r"""
 import math, torch
 from k8s_vgpu_scheduler_amd import ops
 from k8s_vgpu_scheduler_amd.ops import reference as ref
-B, Hq, Hkv, D, T = 5, 32, 8, 128, 700
+B, Hq, Hkv, D, T = 5, 32, 8, 128, 704
 k = torch.randn(B, Hkv, T, D, device="cuda").bfloat16()
 v = torch.randn(B, Hkv, T, D, device="cuda").bfloat16()
 q = torch.randn(B, Hq, D, device="cuda").bfloat16()
@@ -164,24 +187,36 @@ nsplit = math.ceil(T / ops.attn_split())
 out = torch.empty(B, Hq * D, device="cuda", dtype=torch.bfloat16)
 o_part = torch.empty(B * Hq * nsplit * D, device="cuda")
 ml = torch.empty(B * Hq * nsplit * 2, device="cuda")
-ops.decode_attention(q, k, v, seqlens, out, o_part, ml, Hq, Hkv, D, nsplit, 1 / math.sqrt(D))
+ops.decode_attention(q, ops.k_to_cache_layout(k), ops.v_to_cache_layout(v), seqlens, out, o_part, ml, Hq, Hkv,
+                     D, nsplit, 1 / math.sqrt(D))
 exp = ref.decode_attention(q, k, v, seqlens, Hq, Hkv, D, 1 / math.sqrt(D)).view(B, -1)
-print("ERR", ((out.float() - exp).abs().max() / exp.abs().max()).item())
+print("ERR", ((out.float() - exp).abs().max() / exp.abs().max()).item(), ops.attn_split(), int(ops.kv_packed()))
 """
 
 
-@pytest.mark.parametrize("pf", ["0", "1", "2"])
+@pytest.mark.parametrize("variant", ["valu:0", "valu:1", "valu:2", "mfma", "mfma4", "mfma:cached"])
 @pytest.mark.parametrize("mask", ["", "0:0-63"])
-def test_decode_attention_load_variants(pf, mask):
+def test_decode_attention_variants(variant, mask):
+    """Every decode-attention implementation (VALU kernel with its three load
+    schedules, MFMA kernel with 8 / 4 waves, nontemporal or cached K/V loads)
+    in a fresh process, whole GPU and a 64-CU partition."""
     import os
     import subprocess
     import sys
 
-    env = dict(os.environ, MIVGPU_ATTN_PF=pf)
+    kernel, _, opt = variant.partition(":")
+    env = dict(os.environ, MIVGPU_ATTN_KERNEL=kernel)
+    env.pop("MIVGPU_ATTN_NT", None)
+    if opt == "cached":
+        env["MIVGPU_ATTN_NT"] = "0"
+    elif opt:
+        env["MIVGPU_ATTN_PF"] = opt
     env.pop("HSA_CU_MASK", None)
     if mask:
         env["HSA_CU_MASK"] = mask
     r = subprocess.run([sys.executable, "-c", _ATTN_CHILD], env=env, capture_output=True, text=True, timeout=300)
     line = next((x for x in r.stdout.splitlines() if x.startswith("ERR ")), None)
     assert r.returncode == 0 and line, r.stderr[-800:]
-    assert float(line.split()[1]) < 2e-2
+    _, err, split, packed = line.split()
+    assert float(err) < 2e-2
+    assert (int(split), int(packed)) == {"valu": (256, 0), "mfma": (256, 1), "mfma4": (128, 1)}[kernel]
