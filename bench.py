@@ -106,19 +106,23 @@ def main():
     # "native" uses the same HW-queue count as the shim round, so the overhead
     # isolates the cost of the vGPU layer itself (shim + CU masks + limits);
     # "native_hip_default" is naive sharing with HIP's default queue count.
+    # Round order: the headline (shim) first, the naive-sharing round last.  A
+    # round that oversubscribes the hardware queues (8 slices x HIP's default 4
+    # queues) was seen to leave the next round on the GPU unfair (one 8-slice
+    # shim round behind it: fairness 0.51, 6.3k tok/s; alone: 0.99, 8.2k).
     rounds = []
-    if args.mode in ("all", "both", "native"):
-        rounds.append(("native", spawn_round(native_specs(args.hw_queues), phys, work, log_dir, child_args,
-                                             "native")))
-    if args.mode == "all" and args.slices > 1 and args.hw_queues:
-        rounds.append(("native_hip_default", spawn_round(native_specs(0), phys, work, log_dir, child_args,
-                                                         "native_hip_default")))
     if args.mode in ("all", "both", "shim"):
         rounds.append(("shim", spawn_round(
             with_env(plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib,
                                  spatial=not args.no_spatial, policy=args.policy,
                                  hw_queues=args.hw_queues or None)),
             phys, work, log_dir, child_args, "shim")))
+    if args.mode in ("all", "both", "native"):
+        rounds.append(("native", spawn_round(native_specs(args.hw_queues), phys, work, log_dir, child_args,
+                                             "native")))
+    if args.mode == "all" and args.slices > 1 and args.hw_queues:
+        rounds.append(("native_hip_default", spawn_round(native_specs(0), phys, work, log_dir, child_args,
+                                                         "native_hip_default")))
 
     import torch
     import torch.distributed as dist

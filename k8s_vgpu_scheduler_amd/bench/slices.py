@@ -174,6 +174,7 @@ def child_main(argv):
     # per-step completion events: time per output token (TPOT) of this slice
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
     torch.cuda.synchronize()
+    t_start = time.time()
     t0 = time.perf_counter()
     evs[0].record()
     for i in range(a.steps):
@@ -183,6 +184,7 @@ def child_main(argv):
     dt = time.perf_counter() - t0
     tpot = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(a.steps))
     print("DONE " + json.dumps({"seconds": dt, "tokens": a.batch * a.steps, "tok_s": a.batch * a.steps / dt,
+                                "t_start": t_start, "t_end": t_start + dt,
                                 "tpot_ms_p50": tpot[len(tpot) // 2],
                                 "tpot_ms_p99": tpot[min(len(tpot) - 1, int(0.99 * len(tpot)))]}), flush=True)
     return 0
