@@ -57,45 +57,52 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 }
 
 // ----------------------------------------------------------------- RMSNorm --
-// One 256-thread workgroup per row; each thread owns dim/256 contiguous
-// elements loaded as 16-byte vectors (dim % 2048 == 0 for the fast path; a
-// scalar tail loop handles any dim % 8 == 0).
+// One 256-thread workgroup per row; thread t owns the 16-byte vectors t,
+// t+256, ... (dim % 8 == 0, dim <= 8192).  Every load of the row (x, the
+// residual, the norm weight) is issued up front from clamped addresses, so a
+// row costs one memory round trip before the reduction instead of one per
+// vector (a tiny kernel like this is pure latency: 5.1 -> see profiles).
 template <bool ADD>
 __global__ void __launch_bounds__(256)
 rmsnorm_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ res, const bf16_t* __restrict__ w,
                bf16_t* __restrict__ out, int dim, float eps) {
   const int row = blockIdx.x;
   const int t = threadIdx.x;
-  const bf16_t* xr = x + (size_t)row * dim;
-  bf16_t* rr = res + (size_t)row * dim;
-  bf16_t* orow = out + (size_t)row * dim;
+  const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * dim);
+  uint4* rr = reinterpret_cast<uint4*>(res + (size_t)row * dim);
+  uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * dim);
+  const uint4* wv = reinterpret_cast<const uint4*>(w);
   __shared__ float red[4];
   constexpr int MAXV = 4;  // up to 4 x 8 elements per thread (dim <= 8192)
-  float v[MAXV][8];
   const int nvec = dim / 8;
+  uint4 xa[MAXV], xb[MAXV], wa[MAXV];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = min(t + k * 256, nvec - 1);
+    xa[k] = xr[vi];
+    if (ADD) xb[k] = rr[vi];
+    wa[k] = wv[vi];
+  }
+  float v[MAXV][8];
   float ss = 0.f;
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) {
     const int vi = t + k * 256;
-    if (vi < nvec) {
-      float a[8];
-      if (ADD) {
-        float b[8];
-        unpack8(reinterpret_cast<const uint4*>(xr)[vi], a);
-        unpack8(reinterpret_cast<const uint4*>(rr)[vi], b);
+    float a[8];
+    unpack8(xa[k], a);
+    if (ADD) {
+      float c[8];
+      unpack8(xb[k], c);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) a[e] += b[e];
-        reinterpret_cast<uint4*>(rr)[vi] = pack8(a);
-        // Normalise the bf16-rounded residual, exactly what is stored.
-        unpack8(reinterpret_cast<const uint4*>(rr)[vi], a);
-      } else {
-        unpack8(reinterpret_cast<const uint4*>(xr)[vi], a);
-      }
+      for (int e = 0; e < 8; ++e) a[e] += c[e];
+      const uint4 packed = pack8(a);
+      if (vi < nvec) rr[vi] = packed;
+      unpack8(packed, a);   // normalise the bf16-rounded residual, exactly what is stored
+    }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        v[k][e] = a[e];
-        ss += a[e] * a[e];
-      }
+    for (int e = 0; e < 8; ++e) {
+      v[k][e] = a[e];
+      if (vi < nvec) ss += a[e] * a[e];
     }
   }
   ss = wave_sum(ss);
@@ -108,10 +115,10 @@ rmsnorm_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ res, const bf1
     const int vi = t + k * 256;
     if (vi < nvec) {
       float wf[8], o[8];
-      unpack8(reinterpret_cast<const uint4*>(w)[vi], wf);
+      unpack8(wa[k], wf);
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = v[k][e] * inv * wf[e];
-      reinterpret_cast<uint4*>(orow)[vi] = pack8(o);
+      orow[vi] = pack8(o);
     }
   }
 }
@@ -554,22 +561,327 @@ decode_attn_mfma_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__
   }
 }
 
+// ------------------------------------ fused decode attention (one launch) --
+// decode_attn_mfma_kernel with the neighbouring launches folded in (the
+// combine only with COMBINE, see attn_fused_mode for the measured trade-off):
+//   * QK-norm + RoPE + KV append (was qk_norm_rope_kv_kernel): waves 0..G-1
+//     normalise + rotate the workgroup's G query heads straight from the qkv
+//     GEMM output into LDS, wave G the new key, wave G+1 copies the new value
+//     (one wave per head, lane l owns the rotate-half pair l, l+64).  Only the
+//     workgroup whose split holds the new position writes K/V into the packed
+//     cache, and the wave that owns that 32-key group patches its already
+//     loaded K/V fragments from LDS (no other workgroup reads that key).
+//   * the split combine (was decode_attn_combine_kernel): partials are
+//     published with write-through (sc1) stores; after every storing wave's
+//     vmcnt(0) and a workgroup barrier, one lane bumps the (b, kv-head)
+//     arrival counter (agent-scope atomic); the workgroup whose add returns
+//     nsplit-1 is the last one: it resets the counter and merges all splits
+//     with sc1 loads (MI355X_MICROARCH.md, "Hand-offs measured with sc1
+//     loads", row 1).  Every workgroup arrives, empty splits included.
+// The qkv/weight loads are issued before the K/V loads so the prep math does
+// not wait behind the 16 KB of K/V (vmcnt retires in order).
+template <int G, int WAVES, bool NT, bool COMBINE>
+__global__ void __launch_bounds__(WAVES * 64)
+decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ qnw,
+                         const bf16_t* __restrict__ knw, const int* __restrict__ pos,
+                         const int* __restrict__ seqlens, bf16_t* __restrict__ k_pack,
+                         bf16_t* __restrict__ v_pack, bf16_t* __restrict__ out,
+                         float* __restrict__ o_part, float* __restrict__ ml_part,
+                         int* __restrict__ counters, int Hq, int Hkv, int max_ctx, int nsplit,
+                         float scale_log2, float eps, float log2_theta) {
+  typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+  typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+  constexpr int D = ATT_D;
+  constexpr int SPLIT = WAVES * ATT_KPW;
+  constexpr int DP = D + 4;
+  const int split = blockIdx.x;
+  const int hk = blockIdx.y;
+  const int b = blockIdx.z;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const int r16 = lane & 15, q4 = lane >> 4;
+  const int L = min(seqlens[b], max_ctx);
+  const int p = pos[b];
+  const int j0 = split * SPLIT;
+  const int n = min(SPLIT, L - j0);
+  const size_t part_base = ((size_t)b * Hq + (size_t)hk * G);
+  __shared__ float s_o[WAVES][G][DP];
+  __shared__ float s_m[WAVES][G];
+  __shared__ float s_l[WAVES][G];
+  __shared__ __attribute__((aligned(16))) bf16_t s_q[G][D];
+  __shared__ __attribute__((aligned(16))) bf16_t s_kv[2][D];   // new key (normed, rotated), new value
+  __shared__ int s_last;
+
+  if (n > 0) {
+    const bool owner = p >= j0 && p < j0 + SPLIT && p < max_ctx;   // this split appends the new key
+    // ---- prep loads (issued first)
+    // Unconditional loads from clamped, always-valid addresses, issued before
+    // the K/V loads: their wait must not sit behind 16 KB of K/V.
+    const int row = wave < G + 2 ? wave : -1;   // q heads 0..G-1, k, v
+    const int rr = row < 0 ? 0 : row;
+    const int hsrc = rr < G ? hk * G + rr : (rr == G ? Hq + hk : Hq + Hkv + hk);
+    const bf16_t* src = qkv + (size_t)b * (Hq + 2 * Hkv) * D + (size_t)hsrc * D;
+    const bf16_t* nw = rr < G ? qnw : knw;
+    const bf16_t raw_x0 = src[lane], raw_x1 = src[lane + 64];
+    const bf16_t raw_w0 = nw[lane], raw_w1 = nw[lane + 64];
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- K/V loads of this wave's 32-key group (as decode_attn_mfma_kernel)
+    const int wj0 = j0 + wave * ATT_KPW;
+    const int wn = min(ATT_KPW, L - wj0);
+    const int grp = (wn > 0 ? wj0 : j0) / ATT_KPW;
+    const size_t head = ((size_t)b * Hkv + hk) * (size_t)max_ctx * D;
+    const u32x4_t* kp = reinterpret_cast<const u32x4_t*>(k_pack + head + (size_t)grp * ATT_GROUP) + lane;
+    const u32x4_t* vp = reinterpret_cast<const u32x4_t*>(v_pack + head + (size_t)grp * ATT_GROUP) + lane;
+    u32x4_t kr[2][4];
+    u32x4_t vr[8];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        kr[tt][s] = NT ? __builtin_nontemporal_load(kp + 64 * (4 * tt + s)) : kp[64 * (4 * tt + s)];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) vr[dt] = NT ? __builtin_nontemporal_load(vp + 64 * dt) : vp[64 * dt];
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- prep math: RMSNorm + NeoX RoPE (q, k), copy (v).  Computed by every
+    // wave, outside any branch: a use inside a branch lets LLVM sink the loads
+    // into it, behind the K/V loads (then their wait drains all 16 KB).
+    float x0 = bf2f(raw_x0), x1 = bf2f(raw_x1);
+    {
+      const float w0 = bf2f(raw_w0), w1 = bf2f(raw_w1);
+      const float ss = wave_sum(x0 * x0 + x1 * x1);
+      const float inv = rsqrtf(ss / (float)D + eps);
+      const float n0 = x0 * inv * w0, n1 = x1 * inv * w1;
+      const float inv_freq = exp2f(-(2.0f * (float)lane / (float)D) * log2_theta);
+      float sn, cs;
+      sincosf((float)p * inv_freq, &sn, &cs);
+      if (rr <= G) {   // q heads and the key; the value is copied as is
+        x0 = n0 * cs - n1 * sn;
+        x1 = n1 * cs + n0 * sn;
+      }
+    }
+    if (row >= 0 && (row < G || owner)) {
+      const bf16_t h0 = f2bf(x0), h1 = f2bf(x1);
+      if (row < G) {
+        s_q[row][lane] = h0;
+        s_q[row][lane + 64] = h1;
+      } else {
+        const int which = row - G;   // 0 = k, 1 = v
+        s_kv[which][lane] = h0;
+        s_kv[which][lane + 64] = h1;
+        bf16_t* grpp = (which ? v_pack : k_pack) + head + (size_t)(p >> 5) * ATT_GROUP;
+        const int k = p & 31;
+        if (which == 0) {   // K group [t][s][q][r][e]
+          const int kt = (k >> 2) & 1, kr_ = 4 * (k >> 3) + (k & 3);
+          grpp[(((kt * 4 + (lane >> 5)) * 4 + ((lane >> 3) & 3)) * 16 + kr_) * 8 + (lane & 7)] = h0;
+          grpp[(((kt * 4 + ((lane + 64) >> 5)) * 4 + (((lane + 64) >> 3) & 3)) * 16 + kr_) * 8 + (lane & 7)] = h1;
+        } else {            // V group [dt][q][r][e]
+          const int kq = k >> 3, ke = k & 7;
+          grpp[(((lane >> 4) * 4 + kq) * 16 + (lane & 15)) * 8 + ke] = h0;
+          grpp[((((lane + 64) >> 4) * 4 + kq) * 16 + (lane & 15)) * 8 + ke] = h1;
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- Q operand from LDS; the wave owning the new key patches its fragments
+    u32x4_t qr[4];
+    {
+      const int g = r16 < G ? r16 : 0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) qr[s] = *reinterpret_cast<const u32x4_t*>(&s_q[g][32 * s + 8 * q4]);
+    }
+    if (owner && p >= wj0 && p < wj0 + ATT_KPW) {
+      const int k = p & 31;
+      const int kt = (k >> 2) & 1, kr_ = 4 * (k >> 3) + (k & 3);
+      if (r16 == kr_) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+          if (tt == kt) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) kr[tt][s] = *reinterpret_cast<const u32x4_t*>(&s_kv[0][32 * s + 8 * q4]);
+          }
+      }
+      if (q4 == (k >> 3)) {
+        const int ke = k & 7;
+        const unsigned sh = (ke & 1) * 16, keep = 0xffff0000u >> sh;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          const unsigned nv = (unsigned)s_kv[1][16 * dt + r16] << sh;
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (c == (ke >> 1)) vr[dt][c] = (vr[dt][c] & keep) | nv;
+        }
+      }
+    }
+
+    // ---- scores, local softmax, P.V (as decode_attn_mfma_kernel)
+    f32x4_t sc[2];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      sc[tt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        sc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, kr[tt][s]),
+                                                        __builtin_bit_cast(bf16x8_t, qr[s]), sc[tt], 0, 0, 0);
+    }
+    float pr[8];
+    float m = -INFINITY;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool ok = (8 * q4 + 4 * tt + i) < wn;
+        pr[4 * tt + i] = ok ? sc[tt][i] : -INFINITY;
+        m = fmaxf(m, pr[4 * tt + i]);
+      }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float lsum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      pr[j] = m == -INFINITY ? 0.f : exp2f((pr[j] - m) * scale_log2);
+      lsum += pr[j];
+    }
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    bf16x8_t pb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pb[j] = (__bf16)pr[j];
+    f32x4_t o[8];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, vr[dt]), pb,
+                                                      f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    if (r16 < G) {
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s_o[wave][r16][16 * dt + 4 * q4 + i] = o[dt][i];
+      if (q4 == 0) {
+        s_m[wave][r16] = m;
+        s_l[wave][r16] = lsum;
+      }
+    }
+    __syncthreads();
+    // ---- this split's partial, published write-through (sc1)
+    for (int idx = t; idx < G * D; idx += WAVES * 64) {
+      const int g = idx / D, d = idx % D;
+      float M = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) M = fmaxf(M, s_m[w][g]);
+      float num = 0.f, den = 0.f;
+      if (M != -INFINITY) {
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) {
+          const float mw = s_m[w][g];
+          const float f = mw == -INFINITY ? 0.f : exp2f((mw - M) * scale_log2);
+          num += f * s_o[w][g][d];
+          den += f * s_l[w][g];
+        }
+      }
+      const float mn = M == -INFINITY ? -INFINITY : M * scale_log2 * 0.69314718f;
+      float* op = &o_part[((part_base + g) * nsplit + split) * D + d];
+      float* mp = &ml_part[((part_base + g) * nsplit + split) * 2];
+      if constexpr (COMBINE) {   // write-through: read back by another CU in this launch
+        __hip_atomic_store(op, num, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == 0) {
+          __hip_atomic_store(mp, mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(mp + 1, den, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
+        *op = num;
+        if (d == 0) {
+          mp[0] = mn;
+          mp[1] = den;
+        }
+      }
+    }
+  } else if (t < G) {   // empty split: neutral partial
+    float* mp = &ml_part[((part_base + t) * nsplit + split) * 2];
+    if constexpr (COMBINE) {
+      __hip_atomic_store(mp, -INFINITY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(mp + 1, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      mp[0] = -INFINITY;
+      mp[1] = 0.f;
+    }
+  }
+  if constexpr (!COMBINE) return;
+
+  // ---- arrival: every storing wave drained, then one add per workgroup
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* cnt = counters + (size_t)b * Hkv + hk;
+  if (t == 0) {
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == nsplit - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (t == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // ready for the next launch
+  // ---- last workgroup of (b, kv-head): merge the nsplit partials (sc1
+  // loads), 8 splits per batch so each batch is one memory round trip
+  // (a loop of dependent loads here costs a round trip per split).
+  constexpr int MS = 8;
+  for (int idx = t; idx < G * D; idx += WAVES * 64) {
+    const int g = idx / D, d = idx % D;
+    const size_t base = part_base + g;
+    float M = -INFINITY, num = 0.f, den = 0.f;
+    for (int s0 = 0; s0 < nsplit; s0 += MS) {
+      float mv[MS], lv[MS], ov[MS];
+#pragma unroll
+      for (int i = 0; i < MS; ++i) {
+        const int sp = s0 + i < nsplit ? s0 + i : s0;
+        mv[i] = __hip_atomic_load(&ml_part[(base * nsplit + sp) * 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lv[i] = __hip_atomic_load(&ml_part[(base * nsplit + sp) * 2 + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ov[i] = __hip_atomic_load(&o_part[(base * nsplit + sp) * D + d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+#pragma unroll
+      for (int i = 0; i < MS; ++i) {
+        if (s0 + i >= nsplit || mv[i] == -INFINITY) continue;
+        const float nm = fmaxf(M, mv[i]);
+        const float a = M == -INFINITY ? 0.f : __expf(M - nm), w = __expf(mv[i] - nm);
+        num = num * a + w * ov[i];
+        den = den * a + w * lv[i];
+        M = nm;
+      }
+    }
+    out[base * D + d] = f2bf(den > 0.f ? num / den : 0.f);
+  }
+}
+
 // grid = (Hq, B), 128 threads (one per output dim).
 __global__ void __launch_bounds__(128)
 decode_attn_combine_kernel(const float* __restrict__ o_part, const float* __restrict__ ml_part,
                            bf16_t* __restrict__ out, int Hq, int nsplit, int count) {
   // nsplit = workspace stride, count = splits actually written (<= nsplit)
+  // Loads batched 8 splits at a time (one memory round trip per batch) with
+  // an online merge; a max pass followed by a weighted pass costs a dependent
+  // round trip per split.
   const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
   const size_t base = (size_t)b * Hq + h;
-  float M = -INFINITY;
-  for (int s = 0; s < count; ++s) M = fmaxf(M, ml_part[(base * nsplit + s) * 2]);
-  float num = 0.f, den = 0.f;
-  for (int s = 0; s < count; ++s) {
-    const float ms = ml_part[(base * nsplit + s) * 2];
-    if (ms == -INFINITY) continue;
-    const float w = __expf(ms - M);
-    den += w * ml_part[(base * nsplit + s) * 2 + 1];
-    num += w * o_part[(base * nsplit + s) * ATT_D + d];
+  constexpr int MS = 8;
+  float M = -INFINITY, num = 0.f, den = 0.f;
+  for (int s0 = 0; s0 < count; s0 += MS) {
+    float mv[MS], lv[MS], ov[MS];
+#pragma unroll
+    for (int i = 0; i < MS; ++i) {
+      const int sp = s0 + i < count ? s0 + i : s0;
+      mv[i] = ml_part[(base * nsplit + sp) * 2];
+      lv[i] = ml_part[(base * nsplit + sp) * 2 + 1];
+      ov[i] = o_part[(base * nsplit + sp) * ATT_D + d];
+    }
+#pragma unroll
+    for (int i = 0; i < MS; ++i) {
+      if (s0 + i >= count || mv[i] == -INFINITY) continue;
+      const float nm = fmaxf(M, mv[i]);
+      const float a = M == -INFINITY ? 0.f : __expf(M - nm), w = __expf(mv[i] - nm);
+      num = num * a + w * ov[i];
+      den = den * a + w * lv[i];
+      M = nm;
+    }
   }
   out[base * ATT_D + d] = f2bf(den > 0.f ? num / den : 0.f);
 }
@@ -625,6 +937,21 @@ static int attn_impl() {
     return 8;
   }();
   return impl;
+}
+
+// MIVGPU_ATTN_FUSED (read by mivgpu_decode_attention_fused): 1 (default) =
+// prep + attention in one launch, then the combine kernel; 2 = the combine
+// folded in as well (last-arriving workgroup).  Measured decode step, batch
+// 32 (profiles/README.md section 13): whole GPU 4.93 (unfused) / 4.86 (1) /
+// 4.95 ms (2); 64-CU slice 8.88 / 8.87 / 9.65 ms -- the per-workgroup
+// arrival atomic (a full memory round trip before the slot frees) and the
+// last arriver's merge on the critical path cost more than the combine launch.
+static int attn_fused_mode() {
+  static const int m = [] {
+    const char* e = getenv("MIVGPU_ATTN_FUSED");
+    return e && *e ? atoi(e) : 1;
+  }();
+  return m;
 }
 
 static int attn_nt() {
@@ -737,6 +1064,66 @@ int mivgpu_decode_attention(const void* q, const void* k_cache, const void* v_ca
 #undef MIVGPU_ATTN_LAUNCH
   hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(Hq, B), dim3(ATT_D), 0, s,
                      (const float*)o_part, (const float*)ml_part, (bf16_t*)out, Hq, nsplit, nsplit);
+  return (int)hipGetLastError();
+}
+
+// One-launch decode attention step for one layer (fragment-packed caches only):
+// QK-norm + RoPE of the G query heads and the new key, KV append at pos[b],
+// GQA attention over seqlens[b] keys, split combine.  counters: B*Hkv ints,
+// zero before the first call; every launch leaves them zero.  Launches that
+// share `counters` must not run concurrently.
+int mivgpu_decode_attention_fused(const void* qkv, const void* q_norm_w, const void* k_norm_w,
+                                  const int* pos, const int* seqlens, void* k_cache, void* v_cache,
+                                  void* out, void* o_part, void* ml_part, int* counters, int B, int Hq,
+                                  int Hkv, int head_dim, int max_ctx, int nsplit, float scale, float eps,
+                                  float theta, hipStream_t s) {
+  if (!attn_impl() || head_dim != ATT_D || Hq % Hkv || nsplit <= 0 || B <= 0) return -1;
+  const int G = Hq / Hkv;
+  const int waves = attn_impl();
+  if (max_ctx % ATT_KPW || (long long)nsplit * waves * ATT_KPW < max_ctx || G + 2 > waves) return -1;
+  const bool nt = attn_nt() != 0;
+  const float scale_log2 = scale * 1.44269504f;
+  const float log2_theta = log2f(theta);
+  dim3 grid(nsplit, Hkv, B);
+  const bool comb = attn_fused_mode() >= 2;
+#define MIVGPU_ATTN_FUSED2(GG, WW, NN, CC)                                                                     \
+  hipLaunchKernelGGL((decode_attn_fused_kernel<GG, WW, NN, CC>), grid, dim3(WW * 64), 0, s,                  \
+                     (const bf16_t*)qkv, (const bf16_t*)q_norm_w, (const bf16_t*)k_norm_w, pos, seqlens,     \
+                     (bf16_t*)k_cache, (bf16_t*)v_cache, (bf16_t*)out, (float*)o_part, (float*)ml_part,      \
+                     counters, Hq, Hkv, max_ctx, nsplit, scale_log2, eps, log2_theta)
+#define MIVGPU_ATTN_FUSED(GG, WW, NN)                      \
+  do {                                                     \
+    if (comb) MIVGPU_ATTN_FUSED2(GG, WW, NN, true);        \
+    else MIVGPU_ATTN_FUSED2(GG, WW, NN, false);            \
+  } while (0)
+#define MIVGPU_ATTN_FUSED_G(GG)                                  \
+  case GG:                                                       \
+    if (waves == 8) {                                            \
+      if (nt) MIVGPU_ATTN_FUSED(GG, 8, true);                    \
+      else MIVGPU_ATTN_FUSED(GG, 8, false);                      \
+    } else {                                                     \
+      if (nt) MIVGPU_ATTN_FUSED(GG, 4, true);                    \
+      else MIVGPU_ATTN_FUSED(GG, 4, false);                      \
+    }                                                            \
+    break;
+  switch (G) {
+    MIVGPU_ATTN_FUSED_G(1)
+    MIVGPU_ATTN_FUSED_G(2)
+    MIVGPU_ATTN_FUSED_G(4)
+    case 6:
+      if (waves != 8) return -1;
+      if (nt) MIVGPU_ATTN_FUSED(6, 8, true);
+      else MIVGPU_ATTN_FUSED(6, 8, false);
+      break;
+    default:
+      return -1;
+  }
+#undef MIVGPU_ATTN_FUSED_G
+#undef MIVGPU_ATTN_FUSED
+#undef MIVGPU_ATTN_FUSED2
+  if (!comb)
+    hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(Hq, B), dim3(ATT_D), 0, s, (const float*)o_part,
+                       (const float*)ml_part, (bf16_t*)out, Hq, nsplit, nsplit);
   return (int)hipGetLastError();
 }
 

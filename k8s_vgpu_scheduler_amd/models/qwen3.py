@@ -158,6 +158,14 @@ class Qwen3Decoder:
                                   device=self.device)
         self.ml_part = torch.zeros(batch * cfg.heads * self.nsplit * 2, dtype=torch.float32,
                                    device=self.device)
+        # One launch per layer for QK-norm + RoPE + KV append + attention +
+        # split combine (csrc/ops/model_ops.hip decode_attn_fused_kernel);
+        # MIVGPU_ATTN_FUSED=0 runs the three separate kernels.
+        import os
+        self.attn_fused = (self.native and os.environ.get("MIVGPU_ATTN_FUSED", "1") != "0"
+                           and ops.attn_fused_ok(cfg.heads, cfg.kv_heads, cfg.head_dim))
+        self.attn_counters = (torch.zeros(batch * cfg.kv_heads, dtype=torch.int32, device=self.device)
+                              if self.attn_fused else None)
         self.graph = None
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
 
@@ -196,7 +204,12 @@ class Qwen3Decoder:
             self.h.copy_(ref.rmsnorm(self.res, w.layers[0]["ln1"], cfg.eps))
         for li, lw in enumerate(w.layers):
             qkv = F.linear(self.h, lw["wqkv"])
-            if self.native:
+            if self.attn_fused:
+                ops.decode_attention_fused(qkv, lw["q_norm"], lw["k_norm"], self.pos, self.seqlens,
+                                           self.k_cache[li], self.v_cache[li], self.attn, self.o_part,
+                                           self.ml_part, self.attn_counters, cfg.heads, cfg.kv_heads,
+                                           cfg.head_dim, self.nsplit, self.scale, cfg.eps, cfg.rope_theta)
+            elif self.native:
                 ops.qk_norm_rope_kv(qkv, lw["q_norm"], lw["k_norm"], self.pos, self.q,
                                     self.k_cache[li], self.v_cache[li], cfg.heads, cfg.kv_heads,
                                     cfg.head_dim, cfg.eps, cfg.rope_theta)

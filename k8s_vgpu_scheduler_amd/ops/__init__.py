@@ -40,6 +40,8 @@ def lib():
         L.mivgpu_add_rmsnorm.argtypes = [vp, vp, vp, vp, i, i, f, vp]
         L.mivgpu_qk_norm_rope_kv.argtypes = [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, f, f, vp]
         L.mivgpu_decode_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, f, vp]
+        L.mivgpu_decode_attention_fused.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i,
+                                                     i, f, f, f, vp]
         L.mivgpu_silu_mul.argtypes = [vp, vp, i, i, vp]
         L.mivgpu_hwid_probe.argtypes = [vp, i, vp]
         L.mivgpu_pack_weight.argtypes = [vp, vp, i, i, vp]
@@ -56,7 +58,7 @@ def lib():
                    "mivgpu_hwid_probe", "mivgpu_pack_weight", "mivgpu_skinny_gemm",
                    "mivgpu_skinny_max_m", "mivgpu_skinny_plan", "mivgpu_mfma_burn",
                    "mivgpu_stream_copy", "mivgpu_stream_read", "mivgpu_ops_visible_cus",
-                   "mivgpu_ops_kv_packed"):
+                   "mivgpu_ops_kv_packed", "mivgpu_decode_attention_fused"):
             getattr(L, fn).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -213,6 +215,35 @@ def decode_attention(q, k_cache, v_cache, seqlens, out, o_part, ml_part, n_q_hea
     _check(lib().mivgpu_decode_attention(_p(q), _p(k_cache), _p(v_cache), _p(seqlens), _p(out),
                                          _p(o_part), _p(ml_part), B, n_q_heads, n_kv_heads, head_dim,
                                          max_ctx, nsplit, scale, _stream()), "decode_attention")
+    return out
+
+
+def attn_fused_ok(n_q_heads: int, n_kv_heads: int, head_dim: int = 128) -> bool:
+    """The one-launch attention (decode_attention_fused) needs the packed KV
+    layout and one wave per query head of a group + 2 (key, value)."""
+    G = n_q_heads // n_kv_heads
+    return (kv_packed() and head_dim == 128 and n_q_heads % n_kv_heads == 0 and G in (1, 2, 4, 6)
+            and attn_split() // 32 >= G + 2)
+
+
+def decode_attention_fused(qkv, q_norm_w, k_norm_w, pos, seqlens, k_cache, v_cache, out, o_part, ml_part,
+                           counters, n_q_heads, n_kv_heads, head_dim, nsplit, scale, eps, theta):
+    """One launch per layer: QK-norm + RoPE (q heads, new key), KV append at
+    pos[b], attention over seqlens[b] keys, split combine -> out [B, Hq*D].
+    counters: B*Hkv int32, zero before the first call (left zero after)."""
+    B = qkv.shape[0]
+    max_ctx = _check_kv(k_cache, v_cache, B, n_kv_heads, head_dim)
+    need = B * n_q_heads * nsplit
+    if nsplit * attn_split() < max_ctx or o_part.numel() < need * head_dim or ml_part.numel() < need * 2:
+        raise ValueError(f"attention workspace too small for nsplit={nsplit}, max_ctx={max_ctx}")
+    if counters.dtype != torch.int32 or counters.numel() < B * n_kv_heads:
+        raise ValueError("counters must be int32 with B * n_kv_heads entries")
+    if qkv.shape[1] != (n_q_heads + 2 * n_kv_heads) * head_dim or not qkv.is_contiguous():
+        raise ValueError(f"qkv shape {tuple(qkv.shape)} does not match the head counts")
+    _check(lib().mivgpu_decode_attention_fused(_p(qkv), _p(q_norm_w), _p(k_norm_w), _p(pos), _p(seqlens),
+                                               _p(k_cache), _p(v_cache), _p(out), _p(o_part), _p(ml_part),
+                                               _p(counters), B, n_q_heads, n_kv_heads, head_dim, max_ctx,
+                                               nsplit, scale, eps, theta, _stream()), "decode_attention_fused")
     return out
 
 

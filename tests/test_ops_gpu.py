@@ -220,3 +220,151 @@ def test_decode_attention_variants(variant, mask):
     _, err, split, packed = line.split()
     assert float(err) < 2e-2
     assert (int(split), int(packed)) == {"valu": (256, 0), "mfma": (256, 1), "mfma4": (128, 1)}[kernel]
+
+
+def _fused_case(ops, B, Hq, Hkv, T, pos_list, seed=0):
+    D = 128
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", generator=g).bfloat16()
+    qw = (1 + 0.1 * torch.randn(D, device="cuda", generator=g)).bfloat16()
+    kw = (1 + 0.1 * torch.randn(D, device="cuda", generator=g)).bfloat16()
+    k = torch.randn(B, Hkv, T, D, device="cuda", generator=g).bfloat16()
+    v = torch.randn(B, Hkv, T, D, device="cuda", generator=g).bfloat16()
+    pos = torch.tensor(pos_list, dtype=torch.int32, device="cuda")
+    seqlens = pos + 1
+    return qkv, qw, kw, k, v, pos, seqlens
+
+
+@pytest.mark.parametrize("B,Hq,Hkv,T,pos_list", [
+    (4, 32, 8, 1056, [0, 31, 32, 1000]),        # first key, group edges, deep context
+    (3, 32, 8, 544, [255, 256, 543]),           # split edges (256 keys / workgroup), last slot
+    (2, 8, 4, 320, [100, 7]),                    # G = 2
+    (2, 16, 16, 96, [50, 95]),                   # G = 1 (MHA)
+])
+def test_decode_attention_fused(ops, B, Hq, Hkv, T, pos_list):
+    """QK-norm + RoPE + KV append + attention + combine in one launch vs the
+    fp32 reference chain (ref.qk_norm_rope_kv -> ref.decode_attention)."""
+    if not ops.attn_fused_ok(Hq, Hkv):
+        pytest.skip("fused attention needs the packed MFMA kernel")
+    D = 128
+    qkv, qw, kw, k, v, pos, seqlens = _fused_case(ops, B, Hq, Hkv, T, pos_list)
+    kc, vc = ops.k_to_cache_layout(k), ops.v_to_cache_layout(v)
+    nsplit = math.ceil(T / ops.attn_split())
+    out = torch.empty(B, Hq * D, device="cuda", dtype=torch.bfloat16)
+    o_part = torch.empty(B * Hq * nsplit * D, device="cuda")
+    ml = torch.empty(B * Hq * nsplit * 2, device="cuda")
+    cnt = torch.zeros(B * Hkv, dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(D)
+    ops.decode_attention_fused(qkv, qw, kw, pos, seqlens, kc, vc, out, o_part, ml, cnt, Hq, Hkv, D, nsplit,
+                               scale, 1e-6, 1e6)
+    q_ref = torch.empty(B, Hq, D, device="cuda", dtype=torch.bfloat16)
+    k_ref, v_ref = k.clone(), v.clone()
+    ref.qk_norm_rope_kv(qkv, qw, kw, pos, q_ref, k_ref, v_ref, Hq, Hkv, D, 1e-6, 1e6)
+    exp = ref.decode_attention(q_ref, k_ref, v_ref, seqlens, Hq, Hkv, D, scale)
+    torch.cuda.synchronize()
+    _close(out.view(B, Hq, D), exp, 2e-2)
+    # the new key/value landed in the packed caches, nothing else changed
+    _close(ops.k_from_cache_layout(kc), k_ref, 2e-2)
+    assert torch.equal(ops.v_from_cache_layout(vc), v_ref)
+    assert int(cnt.abs().sum()) == 0, "arrival counters must be left at zero"
+
+
+_FUSED_CHILD = r"""
+import math, torch
+from k8s_vgpu_scheduler_amd import ops
+from k8s_vgpu_scheduler_amd.ops import reference as ref
+B, Hq, Hkv, D, T = 3, 32, 8, 128, 800
+g = torch.Generator(device="cuda").manual_seed(1)
+qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda", generator=g).bfloat16()
+qw = (1 + 0.1 * torch.randn(D, device="cuda", generator=g)).bfloat16()
+kw = (1 + 0.1 * torch.randn(D, device="cuda", generator=g)).bfloat16()
+k = torch.randn(B, Hkv, T, D, device="cuda", generator=g).bfloat16()
+v = torch.randn(B, Hkv, T, D, device="cuda", generator=g).bfloat16()
+pos = torch.tensor([5, 511, 796], dtype=torch.int32, device="cuda")
+seqlens = pos + 1
+kc, vc = ops.k_to_cache_layout(k), ops.v_to_cache_layout(v)
+nsplit = math.ceil(T / ops.attn_split())
+out = torch.empty(B, Hq * D, device="cuda", dtype=torch.bfloat16)
+o_part = torch.empty(B * Hq * nsplit * D, device="cuda")
+ml = torch.empty(B * Hq * nsplit * 2, device="cuda")
+cnt = torch.zeros(B * Hkv, dtype=torch.int32, device="cuda")
+err = 0.0
+for it in range(3):
+    ops.decode_attention_fused(qkv, qw, kw, pos, seqlens, kc, vc, out, o_part, ml, cnt, Hq, Hkv, D, nsplit,
+                               1 / math.sqrt(D), 1e-6, 1e6)
+    q_ref = torch.empty(B, Hq, D, device="cuda", dtype=torch.bfloat16)
+    ref.qk_norm_rope_kv(qkv, qw, kw, pos, q_ref, k, v, Hq, Hkv, D, 1e-6, 1e6)
+    exp = ref.decode_attention(q_ref, k, v, seqlens, Hq, Hkv, D, 1 / math.sqrt(D)).view(B, -1)
+    err = max(err, ((out.float() - exp.float()).abs().max() / exp.float().abs().max()).item())
+    qkv = torch.randn_like(qkv)
+    pos += 1
+    seqlens += 1
+torch.cuda.synchronize()
+print("ERR", err, int(cnt.abs().sum()))
+"""
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("mask", ["", "0:0-63"])
+def test_decode_attention_fused_modes(mode, mask):
+    """Both fusion modes (separate combine kernel / last-arriver combine) in a
+    fresh process, whole GPU and a 64-CU partition, 3 launches in a row."""
+    import os
+    import subprocess
+    import sys
+
+    env = dict(os.environ, MIVGPU_ATTN_FUSED=mode)
+    env.pop("HSA_CU_MASK", None)
+    if mask:
+        env["HSA_CU_MASK"] = mask
+    r = subprocess.run([sys.executable, "-c", _FUSED_CHILD], env=env, capture_output=True, text=True, timeout=300)
+    line = next((x for x in r.stdout.splitlines() if x.startswith("ERR ")), None)
+    assert r.returncode == 0 and line, r.stderr[-800:]
+    _, err, cnt = line.split()
+    assert float(err) < 2e-2 and int(cnt) == 0
+
+
+def test_decode_attention_fused_repeated_launches(ops):
+    """Back-to-back launches (the decoder's 36 layers x N steps) reuse one
+    counter array: each launch's last workgroup resets it."""
+    B, Hq, Hkv, T, D = 3, 32, 8, 608, 128
+    if not ops.attn_fused_ok(Hq, Hkv):
+        pytest.skip("fused attention needs the packed MFMA kernel")
+    qkv, qw, kw, k, v, pos, seqlens = _fused_case(ops, B, Hq, Hkv, T, [300, 511, 17], seed=3)
+    kc, vc = ops.k_to_cache_layout(k), ops.v_to_cache_layout(v)
+    k_ref, v_ref = k.clone(), v.clone()
+    nsplit = math.ceil(T / ops.attn_split())
+    out = torch.empty(B, Hq * D, device="cuda", dtype=torch.bfloat16)
+    o_part = torch.empty(B * Hq * nsplit * D, device="cuda")
+    ml = torch.empty(B * Hq * nsplit * 2, device="cuda")
+    cnt = torch.zeros(B * Hkv, dtype=torch.int32, device="cuda")
+    q_ref = torch.empty(B, Hq, D, device="cuda", dtype=torch.bfloat16)
+    for step in range(4):
+        qkv = torch.randn_like(qkv)
+        ops.decode_attention_fused(qkv, qw, kw, pos, seqlens, kc, vc, out, o_part, ml, cnt, Hq, Hkv, D, nsplit,
+                                   1 / math.sqrt(D), 1e-6, 1e6)
+        ref.qk_norm_rope_kv(qkv, qw, kw, pos, q_ref, k_ref, v_ref, Hq, Hkv, D, 1e-6, 1e6)
+        exp = ref.decode_attention(q_ref, k_ref, v_ref, seqlens, Hq, Hkv, D, 1 / math.sqrt(D))
+        _close(out.view(B, Hq, D), exp, 2e-2)
+        pos += 1
+        seqlens += 1
+    torch.cuda.synchronize()
+    assert int(cnt.abs().sum()) == 0
+
+
+def test_decoder_fused_matches_unfused():
+    """Whole tiny decoder, 4 steps: the one-launch attention vs the three
+    separate kernels, same weights and context."""
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
+
+    a = Qwen3Decoder(QWEN3_TINY, batch=3, max_ctx=96, device="cuda", native=True, seed=4)
+    b = Qwen3Decoder(QWEN3_TINY, batch=3, max_ctx=96, device="cuda", native=True, seed=4)
+    if not a.attn_fused:
+        pytest.skip("fused attention not selected")
+    b.attn_fused = False
+    a.fill_context(30)
+    b.fill_context(30)
+    for _ in range(4):
+        la, lb = a.step(), b.step()
+        _close(la, lb, 3e-2)
+        b.tokens.copy_(a.tokens)
