@@ -48,7 +48,19 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 }
 __device__ __forceinline__ float round_bf(float f) { return __uint_as_float((uint32_t)f2bf(f) << 16); }
 
-enum { EPI_STORE = 0, EPI_SILU_MUL = 1 };
+enum { EPI_STORE = 0, EPI_SILU_MUL = 1, EPI_RESID = 2 };
+
+// Row-norm fusion (wide kernel):
+//  * EPI_RESID: Y is the residual stream, updated in place, Y = bf16(Y + X.W^T),
+//    and each wave-group writes its columns' share of every row's sum of
+//    squares of the new Y to ss_out[vgroup * SS_ROWS + row] (plain stores: no
+//    atomics, no zeroing; one slot per wave-group).
+//  * row scale: with rs_part != nullptr the accumulator of row m is multiplied
+//    by rsqrt(sum_p rs_part[p * SS_ROWS + m] * rs_inv_dim + rs_eps) before the
+//    epilogue.  Together with an RMSNorm weight folded into W's columns this
+//    is Y = RMSNorm(X) . W^T, with the norm's reduction done by the producer
+//    of X and its scale applied here: no separate RMSNorm launch.
+constexpr int SS_ROWS = 128;
 
 // k-blocks per load group: ~128 VGPRs of fragments in flight per wave
 // (16 VGPRs per M- or N-tile per k-block).
@@ -468,28 +480,108 @@ __device__ __forceinline__ int acc_row(int e, int h) { return (e & 3) + 8 * (e >
 
 template <int MT, int NT, int EPI, class Get>
 __device__ __forceinline__ void wide_epilogue(Get get, bf16_t* __restrict__ y, int M, int ldy, int tile0,
-                                              int vgroup, int r, int h) {
+                                              int vgroup, int r, int h, const float* rs, float* __restrict__ ss_out,
+                                              const bf16_t* res_lds) {
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int row = m * 32 + acc_row(e, h);
+      if constexpr (EPI == EPI_RESID) {
+        // per row: update, then sum the squares over the 32 columns (lanes r)
+        // of this half right away (one live value, not 16 per lane)
+        float sq = 0.f;
+        if (row < M) {
+          const float sc = rs ? rs[row] : 1.f;
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            // the old residual was prefetched into this wave's LDS tile (row, 32t + r)
+            const bf16_t old = res_lds[((m * NT + t) * 32 + (row - m * 32)) * 32 + r];
+            const float v = round_bf(__uint_as_float((uint32_t)old << 16) + get(m, t, e) * sc);
+            y[(size_t)row * ldy + (size_t)(tile0 + t) * 32 + r] = f2bf(v);
+            sq += v * v;
+          }
+        }
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) sq += __shfl_xor(sq, o, 64);
+        if (r == 0) ss_out[(size_t)vgroup * SS_ROWS + row] = sq;
+        continue;
+      }
       if (row >= M) continue;
+      const float sc = rs ? rs[row] : 1.f;
       if constexpr (EPI == EPI_STORE) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) y[(size_t)row * ldy + (size_t)(tile0 + t) * 32 + r] = f2bf(get(m, t, e));
+        for (int t = 0; t < NT; ++t) y[(size_t)row * ldy + (size_t)(tile0 + t) * 32 + r] = f2bf(get(m, t, e) * sc);
       } else if constexpr (NT == 2) {  // SiLU(gate)*up: tile pair (gate, up) of channel block `vgroup`
-        const float g = round_bf(get(m, 0, e)), u = round_bf(get(m, 1, e));
+        const float g = round_bf(get(m, 0, e) * sc), u = round_bf(get(m, 1, e) * sc);
         y[(size_t)row * ldy + (size_t)vgroup * 32 + r] = f2bf(g / (1.f + __expf(-g)) * u);
       }
     }
+}
+
+// Row scales of the workgroup's MT*32 rows from the producer's per-wave-group
+// sum-of-squares slots, in two halves so the loads overlap the W stream:
+// rs_issue() issues one 16-byte load per (slot, 4 rows) -- RS_LMAX per thread
+// -- before the first X/W loads; rs_finish() (after them, from every thread)
+// reduces in registers, across lanes and through LDS (its internal barrier
+// publishes s_rs).  vmcnt retires in issue order, so the reduction waits for
+// the slot loads only.
+constexpr int RS_LMAX = 8;
+
+template <int MT, int NTHREADS>
+__device__ __forceinline__ void rs_issue(float4 (&v)[RS_LMAX], const float* __restrict__ part, int nparts, int tid) {
+  constexpr int RC = MT * 8;                 // float4 chunks per slot (MT*32 rows)
+  constexpr int PER = NTHREADS / RC;         // slots read in parallel
+  static_assert(NTHREADS % RC == 0, "row chunks must tile the workgroup");
+  const int rc = tid % RC, p0 = tid / RC;
+#pragma unroll
+  for (int i = 0; i < RS_LMAX; ++i) {
+    const int pp = p0 + i * PER;
+    v[i] = pp < nparts ? *(const float4*)(part + (size_t)pp * SS_ROWS + 4 * rc) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+template <int MT, int NTHREADS>
+__device__ __forceinline__ void rs_finish(const float4 (&v)[RS_LMAX], float inv_dim, float eps, float* s_rs,
+                                          float* s_tmp, int tid) {
+  constexpr int RC = MT * 8;
+  constexpr int WV = NTHREADS / 64;
+  const int rc = tid % RC;
+  float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < RS_LMAX; ++i) {
+    sum.x += v[i].x; sum.y += v[i].y; sum.z += v[i].z; sum.w += v[i].w;
+  }
+  // threads with the same rc: lanes rc + RC*j of each wave, then across waves
+#pragma unroll
+  for (int o = RC; o < 64; o <<= 1) {
+    sum.x += __shfl_xor(sum.x, o, 64);
+    sum.y += __shfl_xor(sum.y, o, 64);
+    sum.z += __shfl_xor(sum.z, o, 64);
+    sum.w += __shfl_xor(sum.w, o, 64);
+  }
+  if ((tid & 63) < RC) {
+    const int w = tid >> 6;
+    s_tmp[(w * RC + rc) * 4 + 0] = sum.x;
+    s_tmp[(w * RC + rc) * 4 + 1] = sum.y;
+    s_tmp[(w * RC + rc) * 4 + 2] = sum.z;
+    s_tmp[(w * RC + rc) * 4 + 3] = sum.w;
+  }
+  __syncthreads();
+  if (tid < MT * 32) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < WV; ++w) t += s_tmp[w * RC * 4 + tid];
+    s_rs[tid] = rsqrtf(t * inv_dim + eps);
+  }
 }
 
 template <int MT, int NT, int WV, int EPI>
 __global__ void __launch_bounds__(64 * WV)
 skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int M,
                    int K, int N, int ldx, int ldy, int S, float* __restrict__ scratch, int* __restrict__ tickets,
-                   int kmajor) {
+                   int kmajor, const float* __restrict__ rs_part, int rs_nparts, float rs_inv_dim, float rs_eps,
+                   float* __restrict__ ss_out) {
   static_assert(EPI != EPI_SILU_MUL || NT == 2, "SiLU*up pairs a gate tile with an up tile");
   constexpr int U = unroll_wide(NT);
   constexpr int PITCH = U * 64 + 8;                 // +16 B per row: conflict-free ds_read_b128
@@ -498,6 +590,12 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
   constexpr int XC = MT * U * 256 / NTHREADS;       // X chunks per thread per group
   static_assert(XC * NTHREADS == MT * U * 256, "X tile must split evenly over the workgroup");
   __shared__ __attribute__((aligned(16))) bf16_t xs[2 * XBUF];
+  // row scales (not for EPI_RESID: that epilogue is the producer of the sums)
+  constexpr bool RS = EPI != EPI_RESID;
+  __shared__ float s_rs[MT * 32];
+  __shared__ float s_rtmp[RS ? WV * MT * 32 : 1];
+  // EPI_RESID: each wave's residual tile [m][t][32 rows][32 cols], prefetched by LDS-DMA
+  __shared__ __attribute__((aligned(16))) bf16_t s_res[EPI == EPI_RESID ? WV * MT * NT * 32 * 32 : 2];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
@@ -519,10 +617,38 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
       for (int e = 0; e < 16; ++e) acc[m][t][e] = 0.f;
 
   WFrag<NT> fa[U], fb[U];
+  // Row-scale slot loads are issued first and reduced after the first X/W
+  // loads are in flight (vmcnt retires in order: the reduction waits only for
+  // them); the barrier below publishes s_rs.
+  const float* rs = (RS && rs_part) ? s_rs : nullptr;
+  bf16_t* res_lds = s_res + (EPI == EPI_RESID ? wave * (MT * NT * 32 * 32) : 0);
   {
+    // row-scale slot loads and the residual tile's LDS-DMA first: older than
+    // the X loads, so the X wait below covers them as well
+    float4 rsv[RS ? RS_LMAX : 1];
+    if constexpr (RS) {
+      if (rs_part) rs_issue<MT, NTHREADS>(rsv, rs_part, rs_nparts, tid);
+    }
+    if constexpr (EPI == EPI_RESID) {
+      // tile (m, t): 32 rows x 64 B, 4 rows per instruction, lane = (row, 4-byte column pair)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int row = m * 32 + 4 * i + (lane >> 4);
+            const bf16_t* g = y + (size_t)min(row, M - 1) * ldy + (size_t)(tile0 + t) * 32 + 2 * (lane & 15);
+            __builtin_amdgcn_global_load_lds(g, res_lds + ((m * NT + t) * 32 + 4 * i) * 32, 4, 0, 0);
+          }
+    }
     u32x4_t xr[XC];
     wide_load_x<MT, U, XC>(xr, x, M, ldx, kb0, tid, NTHREADS);
     wide_load_w<NT, U>(fa, wbase, ws, kb0, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (RS) {
+      if (rs_part) rs_finish<MT, NTHREADS>(rsv, rs_inv_dim, rs_eps, s_rs, s_rtmp, tid);
+    }
     wide_store_x<MT, U, XC, PITCH>(xs, xr, tid, NTHREADS);
     __syncthreads();
   }
@@ -543,8 +669,10 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
                                            r, h);
   }
 
+  if constexpr (EPI == EPI_RESID) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // residual tile landed
   if (S == 1) {
-    wide_epilogue<MT, NT, EPI>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, vgroup, r, h);
+    wide_epilogue<MT, NT, EPI>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, vgroup, r, h,
+                               rs, ss_out, res_lds);
     return;
   }
   // Inter-workgroup split, per wave: add the tile into this wave-group's fp32
@@ -568,7 +696,7 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
         return __hip_atomic_load(sc + ((m * NT + t) * 16 + e) * 64 + lane, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
       },
-      y, M, ldy, tile0, vgroup, r, h);
+      y, M, ldy, tile0, vgroup, r, h, rs, ss_out, res_lds);
 #pragma unroll
   for (int i = 0; i < SLAB / 64; ++i) sc[i * 64 + lane] = 0.f;
   if (lane == 0) tickets[vgroup] = 0;
@@ -599,6 +727,11 @@ struct Args {
   int* tickets;
   bool db;
   int kmajor;
+  const float* rs_part = nullptr;   // row-norm fusion (wide kernel only)
+  int rs_nparts = 0;
+  float rs_inv_dim = 0.f;
+  float rs_eps = 0.f;
+  float* ss_out = nullptr;
 };
 
 template <int MT, int NT, int KS, int EPI>
@@ -653,7 +786,7 @@ hipError_t launch_wide(int wv, const Args& a, hipStream_t s) {
 #define MIVGPU_LAUNCH_WIDE(WV)                                                                                \
   hipLaunchKernelGGL((skinny_wide_kernel<MT, NT, WV, EPI>), dim3(blocks), dim3(64 * WV), 0, s,               \
                      (const u32x4_t*)a.wp, (const bf16_t*)a.x, (bf16_t*)a.y, a.M, a.K, a.N, a.ldx, a.ldy, a.S, \
-                     a.scratch, a.tickets, a.kmajor)
+                     a.scratch, a.tickets, a.kmajor, a.rs_part, a.rs_nparts, a.rs_inv_dim, a.rs_eps, a.ss_out)
   switch (wv) {
     case 1: MIVGPU_LAUNCH_WIDE(1); break;
     case 2: MIVGPU_LAUNCH_WIDE(2); break;
@@ -670,6 +803,15 @@ hipError_t launch_wide_mt(int mt, int wv, const Args& a, hipStream_t s) {
     case 1: return launch_wide<1, NT, EPI>(wv, a, s);
     case 2: return launch_wide<2, NT, EPI>(wv, a, s);
     case 4: return launch_wide<4, NT, EPI>(wv, a, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int NT>
+hipError_t launch_wide_resid(int mt, int wv, const Args& a, hipStream_t s) {
+  switch (mt) {
+    case 1: return launch_wide<1, NT, EPI_RESID>(wv, a, s);
+    case 2: return launch_wide<2, NT, EPI_RESID>(wv, a, s);
   }
   return hipErrorInvalidValue;
 }
@@ -812,6 +954,10 @@ int mivgpu_pack_weight(const void* w, void* wp, int N, int K, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+int mivgpu_skinny_gemm_norm(const void* wp, const void* x, void* y, int M, int K, int N, int ldx, int ldy, int epi,
+                            int nt, int ks, int S, int variant, float* scratch, int* tickets, const float* rs_part,
+                            int rs_nparts, float rs_inv_dim, float rs_eps, float* ss_out, hipStream_t s);
+
 // epi: 0 = store Y[M][N] (ldy >= N);  1 = SiLU(gate)*up -> Y[M][N/2] for an
 // interleaved gate/up weight.  variant: 0 auto, 1 classic, 2 wide workgroups
 // (ks = waves per workgroup there).  nt/ks/S: 0 = auto (see mivgpu_skinny_plan);
@@ -822,21 +968,52 @@ int mivgpu_skinny_gemm(const void* wp, const void* x, void* y, int M, int K, int
   if (M <= 0 || M > 128 || K <= 0 || (K & 63) || N <= 0 || (N & 31) || ldx < K || (ldx & 7) || (ldy & 7))
     return (int)hipErrorInvalidValue;
   if (epi != EPI_STORE && epi != EPI_SILU_MUL) return (int)hipErrorInvalidValue;
-  if (resolve(M, K, N, epi, &nt, &ks, &S, variant) == 2) {
+  return mivgpu_skinny_gemm_norm(wp, x, y, M, K, N, ldx, ldy, epi, nt, ks, S, variant, scratch, tickets, nullptr, 0,
+                                 0.f, 0.f, nullptr, s);
+}
+
+// mivgpu_skinny_gemm plus the row-norm fusion of the wide kernel (see
+// EPI_RESID / SS_ROWS above): epi 2 = residual update with sum-of-squares
+// slots ss_out[(N/32/nt) * 128]; rs_part != nullptr = row scales from rs_nparts
+// such slots (rs_inv_dim = 1/normalised dim).  Either requires the wide kernel
+// (hipErrorInvalidValue when the plan resolves to the classic one).
+int mivgpu_skinny_gemm_norm(const void* wp, const void* x, void* y, int M, int K, int N, int ldx, int ldy, int epi,
+                            int nt, int ks, int S, int variant, float* scratch, int* tickets, const float* rs_part,
+                            int rs_nparts, float rs_inv_dim, float rs_eps, float* ss_out, hipStream_t s) {
+  if (M <= 0 || M > 128 || K <= 0 || (K & 63) || N <= 0 || (N & 31) || ldx < K || (ldx & 7) || (ldy & 7))
+    return (int)hipErrorInvalidValue;
+  if (epi != EPI_STORE && epi != EPI_SILU_MUL && epi != EPI_RESID) return (int)hipErrorInvalidValue;
+  const bool fused = rs_part != nullptr || epi == EPI_RESID;
+  if (epi == EPI_RESID && ss_out == nullptr) return (int)hipErrorInvalidValue;
+  if (rs_part != nullptr && rs_nparts <= 0) return (int)hipErrorInvalidValue;
+  if (resolve(M, K, N, epi == EPI_RESID ? EPI_STORE : epi, &nt, &ks, &S, fused ? 2 : variant) == 2) {
     if (epi == EPI_SILU_MUL && ldy < N / 2) return (int)hipErrorInvalidValue;
-    if (epi == EPI_STORE && ldy < N) return (int)hipErrorInvalidValue;
+    if (epi != EPI_SILU_MUL && ldy < N) return (int)hipErrorInvalidValue;
     if (S > 1 && (scratch == nullptr || tickets == nullptr)) return (int)hipErrorInvalidValue;
-    const Args a{wp, x, y, M, K, N, ldx, ldy, S, scratch, tickets, false, use_kmajor() ? 1 : 0};
+    Args a{wp, x, y, M, K, N, ldx, ldy, S, scratch, tickets, false, use_kmajor() ? 1 : 0};
+    a.rs_part = rs_part;
+    a.rs_nparts = rs_nparts;
+    a.rs_inv_dim = rs_inv_dim;
+    a.rs_eps = rs_eps;
+    a.ss_out = ss_out;
     const int mt = mt_of(M);
+    // rs_issue reads RS_LMAX slots per thread in one batch
+    // rs_issue reads RS_LMAX slots per thread in one batch; the residual epilogue takes no row scale
+    if (rs_part != nullptr && (epi == EPI_RESID || rs_nparts > 64 * ks * RS_LMAX / (mt * 8)))
+      return (int)hipErrorInvalidValue;
+    if (epi == EPI_RESID && mt > 2) return (int)hipErrorInvalidValue;   // LDS: residual tiles of <= 64 rows
     hipError_t e;
     if (epi == EPI_SILU_MUL)
       e = launch_wide_mt<2, EPI_SILU_MUL>(mt, ks, a, s);
+    else if (epi == EPI_RESID)
+      e = nt == 2 ? launch_wide_resid<2>(mt, ks, a, s) : launch_wide_resid<1>(mt, ks, a, s);
     else if (nt == 2)
       e = launch_wide_mt<2, EPI_STORE>(mt, ks, a, s);
     else
       e = launch_wide_mt<1, EPI_STORE>(mt, ks, a, s);
     return (int)e;
   }
+  if (fused) return (int)hipErrorInvalidValue;   // the classic kernel has no row-norm fusion
   if ((N / 32) % nt || S < 1 || S > K / 64) return (int)hipErrorInvalidValue;
   if (epi == EPI_STORE && ldy < N) return (int)hipErrorInvalidValue;
   if (epi == EPI_SILU_MUL && ldy < N / 2) return (int)hipErrorInvalidValue;

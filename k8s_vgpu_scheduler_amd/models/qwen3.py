@@ -119,15 +119,31 @@ class Qwen3Decoder:
         # (profiles/gemm_wide_*.json).
         self.skinny_gate_up = skinny
         self.skinny_o = skinny and ops.visible_cus() <= 96
+        # Row-norm fusion (MIVGPU_NORM_FUSED=1; off by default): every
+        # projection on the wide kernel; the RMSNorm weights are folded into
+        # the columns of qkv / gate_up / lm_head, o_proj and down update the
+        # residual stream in their epilogue and write per-row sums of squares,
+        # and the next projection applies rsqrt(mean + eps) per row in its
+        # epilogue -- no add+RMSNorm launches (csrc/ops/skinny_gemm.hip).
+        # Measured: 64-CU slice 8.85 vs 8.87 ms/step, whole GPU 4.97 vs 4.92
+        # (qkv and o_proj are slower on the wide kernel than on hipBLASLt
+        # there), profiles/README.md section 14.
+        import os
+        self.norm_fused = skinny and os.environ.get("MIVGPU_NORM_FUSED", "0") == "1"
+        if self.norm_fused:
+            self.skinny_o = True
         if self.skinny:
             # Keep only the packed copies (no duplicate 16 GB of weights).
             for lw in self.w.layers:
-                if self.skinny_gate_up:
+                if self.norm_fused:
+                    lw["pqkv"] = ops.PackedLinear(lw.pop("wqkv"), col_scale=lw["ln1"])
+                    lw["pgu"] = ops.PackedLinear(lw.pop("wgu"), silu_mul=True, col_scale=lw["ln2"])
+                elif self.skinny_gate_up:
                     lw["pgu"] = ops.PackedLinear(lw.pop("wgu"), silu_mul=True)
                 if self.skinny_o:
                     lw["po"] = ops.PackedLinear(lw.pop("wo"))
                 lw["pd"] = ops.PackedLinear(lw.pop("wd"))
-            self.p_lm = ops.PackedLinear(self.w.lm_head)
+            self.p_lm = ops.PackedLinear(self.w.lm_head, col_scale=self.w.final_norm if self.norm_fused else None)
             if not cfg.tie_embeddings:
                 self.w.lm_head = None
             torch.cuda.empty_cache()
@@ -154,6 +170,13 @@ class Qwen3Decoder:
         self.mlp_out = torch.zeros(batch, h, dtype=dt, device=self.device)
         self.o_out = torch.zeros(batch, h, dtype=dt, device=self.device)
         self.logits = torch.zeros(batch, cfg.vocab, dtype=dt, device=self.device)
+        if self.norm_fused:
+            l0 = self.w.layers[0]
+            self.slots_o, self.slots_d = l0["po"].slots(batch), l0["pd"].slots(batch)
+            n = max(self.slots_o, self.slots_d, 1) * ops.SS_ROWS
+            self.ss_a = torch.zeros(n, dtype=torch.float32, device=self.device)   # before qkv / lm_head
+            self.ss_b = torch.zeros(n, dtype=torch.float32, device=self.device)   # before gate_up
+            self.qkv_buf = torch.zeros(batch, cfg.qkv_dim, dtype=dt, device=self.device)
         self.o_part = torch.zeros(batch * cfg.heads * self.nsplit * cfg.head_dim, dtype=torch.float32,
                                   device=self.device)
         self.ml_part = torch.zeros(batch * cfg.heads * self.nsplit * 2, dtype=torch.float32,
@@ -193,7 +216,46 @@ class Qwen3Decoder:
         self.tokens.copy_(torch.randint(0, self.cfg.vocab, (self.B,), generator=g, device=self.device))
 
     # -------------------------------------------------------------- step --
+    def _attention(self, li, lw, qkv):
+        cfg = self.cfg
+        if self.attn_fused:
+            ops.decode_attention_fused(qkv, lw["q_norm"], lw["k_norm"], self.pos, self.seqlens,
+                                       self.k_cache[li], self.v_cache[li], self.attn, self.o_part,
+                                       self.ml_part, self.attn_counters, cfg.heads, cfg.kv_heads,
+                                       cfg.head_dim, self.nsplit, self.scale, cfg.eps, cfg.rope_theta)
+        else:
+            ops.qk_norm_rope_kv(qkv, lw["q_norm"], lw["k_norm"], self.pos, self.q,
+                                self.k_cache[li], self.v_cache[li], cfg.heads, cfg.kv_heads,
+                                cfg.head_dim, cfg.eps, cfg.rope_theta)
+            ops.decode_attention(self.q, self.k_cache[li], self.v_cache[li], self.seqlens,
+                                 self.attn, self.o_part, self.ml_part, cfg.heads, cfg.kv_heads,
+                                 cfg.head_dim, self.nsplit, self.scale)
+
+    def _step_norm_fused(self):
+        """Decode step with the row-norm fusion: six launches per layer
+        (qkv, attention, combine, o_proj+residual, gate_up+SiLU, down+residual)."""
+        cfg, w = self.cfg, self.w
+        h, eps = cfg.hidden, cfg.eps
+        self.res.copy_(F.embedding(self.tokens, w.embed))
+        # the first norm's sums of squares (one slot), later ones come from the epilogues
+        self.ss_a.view(-1, ops.SS_ROWS)[0, :self.B].copy_(self.res.float().pow(2).sum(-1))
+        na = 1
+        for li, lw in enumerate(w.layers):
+            qkv = lw["pqkv"].norm_call(self.res, out=self.qkv_buf, row_scale=(self.ss_a, na, h, eps))
+            self._attention(li, lw, qkv)
+            lw["po"].norm_call(self.attn, out=self.res, residual=True, ss_out=self.ss_b)
+            lw["pgu"].norm_call(self.res, out=self.act, row_scale=(self.ss_b, self.slots_o, h, eps))
+            lw["pd"].norm_call(self.act, out=self.res, residual=True, ss_out=self.ss_a)
+            na = self.slots_d
+        logits = self.p_lm.norm_call(self.res, out=self.logits, row_scale=(self.ss_a, na, h, eps))
+        self.tokens.copy_(torch.argmax(logits, dim=-1))
+        self.pos.add_(1)
+        self.seqlens.add_(1)
+        return logits
+
     def _step_impl(self):
+        if self.norm_fused:
+            return self._step_norm_fused()
         cfg, w = self.cfg, self.w
         x = F.embedding(self.tokens, w.embed)
         self.res.copy_(x)
@@ -204,18 +266,8 @@ class Qwen3Decoder:
             self.h.copy_(ref.rmsnorm(self.res, w.layers[0]["ln1"], cfg.eps))
         for li, lw in enumerate(w.layers):
             qkv = F.linear(self.h, lw["wqkv"])
-            if self.attn_fused:
-                ops.decode_attention_fused(qkv, lw["q_norm"], lw["k_norm"], self.pos, self.seqlens,
-                                           self.k_cache[li], self.v_cache[li], self.attn, self.o_part,
-                                           self.ml_part, self.attn_counters, cfg.heads, cfg.kv_heads,
-                                           cfg.head_dim, self.nsplit, self.scale, cfg.eps, cfg.rope_theta)
-            elif self.native:
-                ops.qk_norm_rope_kv(qkv, lw["q_norm"], lw["k_norm"], self.pos, self.q,
-                                    self.k_cache[li], self.v_cache[li], cfg.heads, cfg.kv_heads,
-                                    cfg.head_dim, cfg.eps, cfg.rope_theta)
-                ops.decode_attention(self.q, self.k_cache[li], self.v_cache[li], self.seqlens,
-                                     self.attn, self.o_part, self.ml_part, cfg.heads, cfg.kv_heads,
-                                     cfg.head_dim, self.nsplit, self.scale)
+            if self.native:
+                self._attention(li, lw, qkv)
             else:
                 ref.qk_norm_rope_kv(qkv, lw["q_norm"], lw["k_norm"], self.pos, self.q,
                                     self.k_cache[li], self.v_cache[li], cfg.heads, cfg.kv_heads,

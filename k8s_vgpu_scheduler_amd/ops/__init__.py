@@ -46,6 +46,7 @@ def lib():
         L.mivgpu_hwid_probe.argtypes = [vp, i, vp]
         L.mivgpu_pack_weight.argtypes = [vp, vp, i, i, vp]
         L.mivgpu_skinny_gemm.argtypes = [vp, vp, vp, i, i, i, i, i, i, i, i, i, i, vp, vp, vp]
+        L.mivgpu_skinny_gemm_norm.argtypes = [vp, vp, vp, i, i, i, i, i, i, i, i, i, i, vp, vp, vp, i, f, f, vp, vp]
         ip, lp = ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_longlong)
         L.mivgpu_mfma_burn.argtypes = [vp, i, i, ctypes.c_uint, vp]
         L.mivgpu_mfma_burn_flops.argtypes = [i, i]
@@ -58,7 +59,7 @@ def lib():
                    "mivgpu_hwid_probe", "mivgpu_pack_weight", "mivgpu_skinny_gemm",
                    "mivgpu_skinny_max_m", "mivgpu_skinny_plan", "mivgpu_mfma_burn",
                    "mivgpu_stream_copy", "mivgpu_stream_read", "mivgpu_ops_visible_cus",
-                   "mivgpu_ops_kv_packed", "mivgpu_decode_attention_fused"):
+                   "mivgpu_ops_kv_packed", "mivgpu_decode_attention_fused", "mivgpu_skinny_gemm_norm"):
             getattr(L, fn).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -334,18 +335,30 @@ def skinny_plan(M: int, K: int, N: int, epi: int, nt: int = 0, ks: int = 0, S: i
             "tickets": v_t.value, "variant": v_v.value}
 
 
+EPI_RESID = 2
+SS_ROWS = 128   # rows per sum-of-squares slot (csrc/ops/skinny_gemm.hip SS_ROWS)
+
+
 class PackedLinear:
     """A weight held only in packed form, applied with the skinny MFMA GEMM.
 
     Owns the zeroed fp32 slabs + tickets of the inter-workgroup split-K
     (sized for the largest plan seen; the kernel leaves them zeroed, so graph
     replays need no memset).  Not safe to call concurrently on two streams.
+
+    ``col_scale`` (an RMSNorm weight of length K) is folded into W's columns
+    before packing, so ``norm_call(x, row_scale=...)`` computes
+    RMSNorm(x) . W^T with the norm's row scales applied in the epilogue.
     """
 
-    def __init__(self, w: torch.Tensor, silu_mul: bool = False):
+    def __init__(self, w: torch.Tensor, silu_mul: bool = False, col_scale: torch.Tensor | None = None):
         self.N, self.K = w.shape
         self.silu_mul = silu_mul
         self.epi = EPI_SILU_MUL if silu_mul else EPI_STORE
+        if col_scale is not None:
+            if col_scale.shape != (self.K,):
+                raise ValueError(f"col_scale must be [{self.K}], got {tuple(col_scale.shape)}")
+            w = (w.float() * col_scale.float()[None, :]).to(w.dtype)
         self.wp = pack_weight(interleave_gate_up(w) if silu_mul else w)
         self.scratch = None
         self.tickets = None
@@ -375,4 +388,42 @@ class PackedLinear:
         _check(lib().mivgpu_skinny_gemm(_p(self.wp), _p(x), _p(out), M, self.K, self.N, x.stride(0),
                                         out.stride(0), self.epi, nt, ks, S, variant, sp, tp, _stream()),
                "skinny_gemm")
+        return out
+
+    def slots(self, M: int) -> int:
+        """Sum-of-squares slots a residual call (``norm_call(residual=True)``)
+        writes: one per wave-group of the wide plan."""
+        return (self.N // 32) // skinny_plan(M, self.K, self.N, EPI_RESID, variant=VARIANT_WIDE)["nt"]
+
+    def norm_call(self, x: torch.Tensor, out: torch.Tensor, row_scale: tuple | None = None,
+                  residual: bool = False, ss_out: torch.Tensor | None = None, ks: int = 0, S: int = 0):
+        """Wide-kernel call with the row-norm fusion (csrc/ops/skinny_gemm.hip):
+        * ``row_scale=(slots, nparts, dim, eps)``: multiply row m of X.W^T by
+          rsqrt(sum of the nparts sum-of-squares slots / dim + eps);
+        * ``residual=True``: ``out`` is the residual stream, updated in place
+          (out += X.W^T), and ``ss_out`` receives ``slots(M)`` slots of the new
+          rows' sums of squares ([slots * SS_ROWS] fp32)."""
+        M = x.shape[0]
+        if x.dim() != 2 or x.shape[1] != self.K or x.stride(1) != 1 or not 0 < M <= 128:
+            raise ValueError(f"skinny_gemm: x must be [M <= 128, {self.K}] row-major, got {tuple(x.shape)}")
+        epi = EPI_RESID if residual else self.epi
+        if residual and (self.silu_mul or ss_out is None or ss_out.numel() < self.slots(M) * SS_ROWS
+                         or tuple(out.shape) != (M, self.N)):
+            raise ValueError("residual call needs out [M, N], ss_out of slots(M) * SS_ROWS floats, no SiLU")
+        pl = skinny_plan(M, self.K, self.N, epi, 0, ks, S, variant=VARIANT_WIDE)
+        if pl["variant"] != VARIANT_WIDE:
+            raise ValueError(f"row-norm fusion needs the wide kernel; plan {pl}")
+        self._ensure_scratch(pl["scratch_floats"], pl["tickets"], x.device)
+        sp = _p(self.scratch) if self.scratch is not None else None
+        tp = _p(self.tickets) if self.tickets is not None else None
+        rs, nparts, inv_dim, eps = None, 0, 0.0, 0.0
+        if row_scale is not None:
+            part, nparts, dim, eps = row_scale
+            if part.dtype != torch.float32 or part.numel() < nparts * SS_ROWS or nparts <= 0:
+                raise ValueError("row_scale slots must be fp32 [nparts * SS_ROWS]")
+            rs, inv_dim = _p(part), 1.0 / dim
+        _check(lib().mivgpu_skinny_gemm_norm(_p(self.wp), _p(x), _p(out), M, self.K, self.N, x.stride(0),
+                                             out.stride(0), epi, 0, ks, S, VARIANT_WIDE, sp, tp, rs, nparts,
+                                             inv_dim, eps, _p(ss_out) if residual else None, _stream()),
+               "skinny_gemm_norm")
         return out

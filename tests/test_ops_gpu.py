@@ -368,3 +368,20 @@ def test_decoder_fused_matches_unfused():
         la, lb = a.step(), b.step()
         _close(la, lb, 3e-2)
         b.tokens.copy_(a.tokens)
+
+
+def test_decoder_norm_fused_matches_reference(monkeypatch):
+    """Row-norm fusion (MIVGPU_NORM_FUSED=1): folded RMSNorm weights, residual
+    epilogues and row scales, 3 steps against the fp32 reference decoder."""
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
+
+    monkeypatch.setenv("MIVGPU_NORM_FUSED", "1")
+    a = Qwen3Decoder(QWEN3_TINY, batch=5, max_ctx=64, device="cuda", native=True, seed=6)
+    assert a.norm_fused and "pqkv" in a.w.layers[0]
+    b = Qwen3Decoder(QWEN3_TINY, batch=5, max_ctx=64, device="cuda", native=False, seed=6)
+    a.fill_context(12)
+    b.fill_context(12)
+    for _ in range(3):
+        la, lb = a.step(), b.step()
+        _close(la, lb, 5e-2)
+        b.tokens.copy_(a.tokens)

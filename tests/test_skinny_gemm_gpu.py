@@ -134,3 +134,65 @@ def test_rejects_bad_shapes():
     lin = ops.PackedLinear(torch.zeros(64, 64, device="cuda", dtype=torch.bfloat16))
     with pytest.raises(RuntimeError):
         lin(torch.zeros(129, 64, device="cuda", dtype=torch.bfloat16))
+
+
+def _rms_ref(x, w, eps=1e-6):
+    xf = x.float()
+    return xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+
+
+@pytest.mark.parametrize("S", [0, 1, 4])
+@pytest.mark.parametrize("M", [1, 5, 32, 48])
+def test_row_norm_fusion_chain(M, S):
+    """o_proj-like residual call (res += X.W^T, per-slot sums of squares) then
+    a gate_up-like call that applies RMSNorm through folded column weights and
+    row scales from those slots, vs. add + RMSNorm + GEMM in fp32."""
+    g = torch.Generator(device="cuda").manual_seed(M * 13 + S)
+    K, N1, N2 = 4096, 4096, 2048
+    res = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    wo = (torch.randn(N1, K, device="cuda", generator=g) * 0.02).bfloat16()
+    wn = (1 + 0.1 * torch.randn(K, device="cuda", generator=g)).bfloat16()
+    wg = (torch.randn(N2, K, device="cuda", generator=g) * 0.02).bfloat16()
+    po = ops.PackedLinear(wo)
+    pg = ops.PackedLinear(wg, col_scale=wn)
+    slots = po.slots(M)
+    ss = torch.full((slots * ops.SS_ROWS,), float("nan"), device="cuda")   # every used slot must be written
+    r1 = res.clone()
+    for _ in range(2):   # split-K scratch / tickets must come back clean
+        r1.copy_(res)
+        po.norm_call(x, out=r1, residual=True, ss_out=ss, S=S)
+        exp_res = res.float() + _ref(x, wo)
+        _close(r1, exp_res)
+        got_ss = ss.view(slots, ops.SS_ROWS)[:, :M].sum(0)
+        _close(got_ss, r1.float().pow(2).sum(-1), 1e-3)
+        y = torch.empty(M, N2, device="cuda", dtype=torch.bfloat16)
+        pg.norm_call(r1, out=y, row_scale=(ss, slots, K, 1e-6), S=S)
+        _close(y, _rms_ref(r1, wn) @ wg.float().t())
+
+
+@pytest.mark.parametrize("M", [1, 32])
+def test_row_scale_with_silu_and_single_slot(M):
+    """The decoder's first norm (one slot from torch) into the SiLU*up epilogue."""
+    K, inter = 1024, 2048
+    res = torch.randn(M, K, device="cuda").bfloat16()
+    wn = (1 + 0.1 * torch.randn(K, device="cuda")).bfloat16()
+    wgu = (torch.randn(2 * inter, K, device="cuda") * 0.05).bfloat16()
+    ss = torch.zeros(ops.SS_ROWS, device="cuda")
+    ss[:M] = res.float().pow(2).sum(-1)
+    lin = ops.PackedLinear(wgu, silu_mul=True, col_scale=wn)
+    y = torch.empty(M, inter, device="cuda", dtype=torch.bfloat16)
+    lin.norm_call(res, out=y, row_scale=(ss, 1, K, 1e-6))
+    gu = _rms_ref(res, wn).bfloat16().float() @ wgu.float().t()
+    g, u = gu[:, :inter], gu[:, inter:]
+    _close(y, torch.nn.functional.silu(g) * u, 3e-2)
+
+
+def test_norm_call_rejects_bad_arguments():
+    lin = ops.PackedLinear((torch.randn(2048, 4096, device="cuda") * 0.02).bfloat16())
+    x = torch.randn(4, 4096, device="cuda").bfloat16()
+    out = torch.empty(4, 2048, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(ValueError):
+        lin.norm_call(x, out=out, residual=True)          # no ss_out
+    with pytest.raises(ValueError):
+        lin.norm_call(x, out=out, row_scale=(torch.zeros(8, device="cuda"), 1, 4096, 1e-6))   # slots too small
