@@ -818,6 +818,16 @@ hipError_t launch_wide_resid(int mt, int wv, const Args& a, hipStream_t s) {
 
 int mt_of(int M) { return M <= 32 ? 1 : (M <= 64 ? 2 : 4); }
 
+// Partition-size plan switch: the "slice" plans (no inter-workgroup split,
+// fatter workgroups) apply at <= MIVGPU_SLICE_PLAN_CUS visible CUs (default 96).
+bool slice_plan(int cus) {
+  static const int limit = [] {
+    const char* e = getenv("MIVGPU_SLICE_PLAN_CUS");
+    return e && *e ? atoi(e) : 96;
+  }();
+  return cus <= limit;
+}
+
 }  // namespace
 extern "C" int mivgpu_ops_visible_cus();   // model_ops.hip
 namespace {
@@ -834,7 +844,7 @@ namespace {
 void plan(int M, int K, int N, int epi, int* nt, int* ks, int* S) {
   static const int cus = mivgpu_ops_visible_cus();
   const int mt = mt_of(M);
-  const bool slice = cus <= 96;
+  const bool slice = slice_plan(cus);
   if (epi == EPI_SILU_MUL) *nt = 2;
   if (*nt != 1 && *nt != 2) *nt = (mt < 4 && ((N / 64) >= 384 || (slice && (N / 64) >= 32))) ? 2 : 1;
   const int groups = (N / 32) / *nt, KB = K / 64;
@@ -876,7 +886,7 @@ constexpr int unroll_wide_host(int nt) { return nt >= 4 ? 1 : (nt == 2 ? 2 : 4);
 // caller falls back to the classic kernel).
 bool plan_wide(int M, int K, int N, int epi, int* nt, int* wv, int* S) {
   static const int cus = mivgpu_ops_visible_cus();
-  const bool slice = cus <= 96;
+  const bool slice = slice_plan(cus);
   const int ntiles = N / 32, KB = K / 64;
   if (epi == EPI_SILU_MUL) {
     if (*nt > 0 && *nt != 2) return false;

@@ -107,6 +107,7 @@ class Qwen3Decoder:
         if self.native:
             ops.require_native()
         self.w = Qwen3Weights(cfg, self.device, seed=seed)
+        import os
         shapes_ok = cfg.hidden % 64 == 0 and cfg.intermediate % 64 == 0 and cfg.vocab % 64 == 0
         if skinny is None:
             import os
@@ -118,7 +119,7 @@ class Qwen3Decoder:
         # 256 CUs, and on o_proj inside a CU partition; qkv stays on hipBLASLt
         # (profiles/gemm_wide_*.json).
         self.skinny_gate_up = skinny
-        self.skinny_o = skinny and ops.visible_cus() <= 96
+        self.skinny_o = skinny and ops.visible_cus() <= int(os.environ.get("MIVGPU_SLICE_PLAN_CUS", "96"))
         # Row-norm fusion (MIVGPU_NORM_FUSED=1; off by default): every
         # projection on the wide kernel; the RMSNorm weights are folded into
         # the columns of qkv / gate_up / lm_head, o_proj and down update the
