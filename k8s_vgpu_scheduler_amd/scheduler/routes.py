@@ -47,10 +47,19 @@ def make_handler(scheduler, webhook, profiling: bool = False):
             self.wfile.write(body)
 
         def _body(self):
-            n = int(self.headers.get("Content-Length") or 0)
+            """Request body, None when absent; b"" marks one over the 1 MiB cap
+            (route.go's MaxBytesReader), which is left unread: the connection
+            is closed after the reply instead of parsing its tail as a request."""
+            try:
+                n = int(self.headers.get("Content-Length") or 0)
+            except ValueError:
+                n = 0
             if n <= 0:
                 return None
-            return self.rfile.read(min(n, MAX_BODY))
+            if n > MAX_BODY:
+                self.close_connection = True
+                return b""
+            return self.rfile.read(n)
 
         def do_GET(self):  # noqa: N802
             if self.path == "/healthz":
@@ -68,6 +77,8 @@ def make_handler(scheduler, webhook, profiling: bool = False):
             raw = self._body()
             if raw is None:
                 return self._text(400, "Please send a request body")
+            if raw == b"":
+                return self._text(413, "request body too large")
             try:
                 args = json.loads(raw)
             except ValueError as e:
