@@ -67,9 +67,10 @@ class SharedRegion:
                             mmap.PROT_READ | (mmap.PROT_WRITE if writable else 0))
         self.r = Region.from_buffer(self.mm) if writable else Region.from_buffer_copy(self.mm)
         self.writable = writable
-        if self.r.magic != MAGIC:
-            self.close()
-            raise ValueError(f"{path}: bad magic {self.r.magic:#x}")
+        magic = int(self.r.magic)
+        if magic != MAGIC:
+            self.close()   # drops self.r: report the value read before
+            raise ValueError(f"{path}: bad magic {magic:#x}")
 
     @classmethod
     def create(cls, path: str, num_devices: int = 1, mem_limit: int = 0, cu_limit: int = 100) -> "SharedRegion":
