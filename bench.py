@@ -71,6 +71,9 @@ def main():
                     help="GPU_MAX_HW_QUEUES per slice in the shim round (0 = HIP default)")
     ap.add_argument("--child-env", action="append", default=[], metavar="K=V",
                     help="extra environment for every slice process (experiments)")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu = rehearse the harness without a GPU: gloo barriers, CPU reference decoder in "
+                         "the slice processes (results are not MI355X numbers)")
     args = ap.parse_args()
 
     from k8s_vgpu_scheduler_amd.bench.slices import plan_slices, run_round, spawn_round
@@ -86,7 +89,8 @@ def main():
     log_dir = Path(os.environ.get("MIVGPU_BENCH_LOGS", work))
     log_dir.mkdir(parents=True, exist_ok=True)
     child_args = ["--model", args.model, "--batch", str(args.batch), "--ctx", str(args.ctx),
-                  "--steps", str(args.steps), "--warmup", str(args.warmup)]
+                  "--steps", str(args.steps), "--warmup", str(args.warmup), "--device", args.device]
+    cpu = args.device == "cpu"
 
     extra_env = dict(kv.split("=", 1) for kv in args.child_env)
 
@@ -127,22 +131,28 @@ def main():
     import torch
     import torch.distributed as dist
 
+    dev = "cpu" if cpu else "cuda"
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        if cpu:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
         barrier = dist.barrier
     else:
-        torch.cuda.set_device(0)
+        if not cpu:
+            torch.cuda.set_device(0)
         barrier = None
 
     def sync():
-        torch.cuda.synchronize()
+        if not cpu:
+            torch.cuda.synchronize()
 
     results = {}
     for name, procs in rounds:
         r = run_round(procs, barrier=barrier, sync=sync)
-        wall = torch.tensor([r["wall_s"]], dtype=torch.float64, device="cuda")
-        toks = torch.tensor([float(r["tokens"])], dtype=torch.float64, device="cuda")
+        wall = torch.tensor([r["wall_s"]], dtype=torch.float64, device=dev)
+        toks = torch.tensor([float(r["tokens"])], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(wall, op=dist.ReduceOp.MAX)
             dist.all_reduce(toks, op=dist.ReduceOp.SUM)
@@ -165,7 +175,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if not cpu else "fp32-reference (CPU rehearsal)",
             "data": "synthetic (random-init weights, random KV context)",
             "config": {
                 "model": "Qwen3-8B" if args.model == "qwen3-8b" else "Qwen3-tiny",

@@ -95,6 +95,9 @@ class SliceProc:
         for k in ("LD_PRELOAD", "HSA_CU_MASK", "HIP_DEVICE_CORE_LIMIT"):
             full.pop(k, None)
         full.update(env)
+        # the child runs `-m k8s_vgpu_scheduler_amd...`: importable from any cwd
+        root = str(Path(__file__).resolve().parents[2])
+        full["PYTHONPATH"] = root + (os.pathsep + full["PYTHONPATH"] if full.get("PYTHONPATH") else "")
         if env.get("ROCR_VISIBLE_DEVICES") is not None:
             full.pop("HIP_VISIBLE_DEVICES", None)
             full.pop("CUDA_VISIBLE_DEVICES", None)
@@ -146,6 +149,8 @@ def child_main(argv):
     ap.add_argument("--ctx", type=int, default=1024)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu = harness rehearsal (fp32 reference path, no GPU)")
     a = ap.parse_args(argv)
     cmd = sys.stdin.readline().strip()
     if cmd != "LOAD":
@@ -155,6 +160,8 @@ def child_main(argv):
     from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_8B, QWEN3_TINY, Qwen3Decoder
 
     cfg = {"qwen3-8b": QWEN3_8B, "qwen3-tiny": QWEN3_TINY}[a.model]
+    if a.device == "cpu":
+        return _child_cpu(a, cfg, Qwen3Decoder)
     t_load = time.time()
     max_ctx = a.ctx + a.warmup + a.steps + 16
     dec = Qwen3Decoder(cfg, batch=a.batch, max_ctx=max_ctx, device="cuda")
@@ -186,6 +193,35 @@ def child_main(argv):
     print("DONE " + json.dumps({"seconds": dt, "tokens": a.batch * a.steps, "tok_s": a.batch * a.steps / dt,
                                 "t_start": t_start, "t_end": t_start + dt,
                                 "tpot_ms_p50": tpot[len(tpot) // 2],
+                                "tpot_ms_p99": tpot[min(len(tpot) - 1, int(0.99 * len(tpot)))]}), flush=True)
+    return 0
+
+
+def _child_cpu(a, cfg, Qwen3Decoder):
+    """The same LOAD/READY/GO/DONE protocol on the CPU reference decoder, so
+    the multi-rank harness (spawn, barriers, MAX wall, token sum, JSON line)
+    can be rehearsed without a GPU (tests/test_bench_harness.py)."""
+    t_load = time.time()
+    dec = Qwen3Decoder(cfg, batch=a.batch, max_ctx=a.ctx + a.warmup + a.steps + 16, device="cpu", native=False)
+    dec.fill_context(a.ctx)
+    for _ in range(a.warmup):
+        dec.step()
+    print("READY " + json.dumps({"load_s": round(time.time() - t_load, 2), "mem_total_mib": 0, "mem_free_mib": 0,
+                                 "allocated_mib": 0, "cus": 0, "preload": os.environ.get("LD_PRELOAD", ""),
+                                 "cu_mask": os.environ.get("HSA_CU_MASK", "")}), flush=True)
+    if sys.stdin.readline().strip() != "GO":
+        return 0
+    t_start = time.time()
+    t0 = time.perf_counter()
+    tpot = []
+    for _ in range(a.steps):
+        s0 = time.perf_counter()
+        dec.step()
+        tpot.append((time.perf_counter() - s0) * 1e3)
+    dt = time.perf_counter() - t0
+    tpot.sort()
+    print("DONE " + json.dumps({"seconds": dt, "tokens": a.batch * a.steps, "tok_s": a.batch * a.steps / dt,
+                                "t_start": t_start, "t_end": t_start + dt, "tpot_ms_p50": tpot[len(tpot) // 2],
                                 "tpot_ms_p99": tpot[min(len(tpot) - 1, int(0.99 * len(tpot)))]}), flush=True)
     return 0
 
