@@ -71,6 +71,8 @@ def main():
                     help="GPU_MAX_HW_QUEUES per slice in the shim round (0 = HIP default)")
     ap.add_argument("--child-env", action="append", default=[], metavar="K=V",
                     help="extra environment for every slice process (experiments)")
+    ap.add_argument("--no-collectives", action="store_true",
+                    help="skip the untimed all-reduce check between the bench ranks (N > 1)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = rehearse the harness without a GPU: gloo barriers, CPU reference decoder in "
                          "the slice processes (results are not MI355X numbers)")
@@ -161,6 +163,19 @@ def main():
         r["tok_s"] = toks.item() / wall.item()
         results[name] = r
 
+    # N > 1: after the timed rounds (slice processes gone), an untimed RCCL
+    # all-reduce between the ranks: exact result + busBW over xGMI, the data
+    # plane a multi-GPU pod placed by the topology score runs on
+    # (parallel/collectives.py).  Reported next to the headline, never in it.
+    coll = None
+    if world > 1 and not args.no_collectives:
+        from k8s_vgpu_scheduler_amd.parallel.collectives import measure
+        from k8s_vgpu_scheduler_amd.parallel.dist import DistEnv
+        env = DistEnv(rank, world, local_rank, "gloo" if cpu else "nccl",
+                      torch.device("cpu" if cpu else f"cuda:{local_rank}"))
+        sizes = (64 << 10, 1 << 20) if cpu else (1 << 20, 16 << 20, 256 << 20)
+        coll = [measure("all_reduce", nb, env, iters=10, warmup=3) for nb in sizes]
+
     if rank == 0:
         head = results.get("shim") or results["native"]
         per_slice = [round(d["tok_s"], 1) for d in head["done"]]
@@ -206,6 +221,10 @@ def main():
             nd = results["native_hip_default"]["tok_s"]
             out["native_hip_default_queues_value"] = round(nd, 2)
             out["speedup_vs_naive_sharing"] = round(head["tok_s"] / nd, 3)
+        if coll:
+            out["allreduce_between_gpus"] = [{k: r[k] for k in ("bytes", "us", "busbw_gbps", "correct")}
+                                              for r in coll]
+            out["allreduce_peak_busbw_gbps"] = max(r["busbw_gbps"] for r in coll)
         line = json.dumps(out)
         print(line, flush=True)
         if args.out:

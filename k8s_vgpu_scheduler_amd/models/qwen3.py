@@ -120,6 +120,10 @@ class Qwen3Decoder:
         # (profiles/gemm_wide_*.json).
         self.skinny_gate_up = skinny
         self.skinny_o = skinny and ops.visible_cus() <= int(os.environ.get("MIVGPU_SLICE_PLAN_CUS", "96"))
+        # qkv joins them in small partitions: at 32 CUs (an 8-slice pod)
+        # hipBLASLt takes 50.7 us vs 40.7 on the wide kernel; at 64 CUs it is
+        # 27.9 vs 29.6 (profiles/cu32/, profiles/gemm_wide_plan_cu64.json).
+        self.skinny_qkv = skinny and ops.visible_cus() <= int(os.environ.get("MIVGPU_QKV_WIDE_CUS", "48"))
         # Row-norm fusion (MIVGPU_NORM_FUSED=1; off by default): every
         # projection on the wide kernel; the RMSNorm weights are folded into
         # the columns of qkv / gate_up / lm_head, o_proj and down update the
@@ -139,8 +143,11 @@ class Qwen3Decoder:
                 if self.norm_fused:
                     lw["pqkv"] = ops.PackedLinear(lw.pop("wqkv"), col_scale=lw["ln1"])
                     lw["pgu"] = ops.PackedLinear(lw.pop("wgu"), silu_mul=True, col_scale=lw["ln2"])
-                elif self.skinny_gate_up:
-                    lw["pgu"] = ops.PackedLinear(lw.pop("wgu"), silu_mul=True)
+                else:
+                    if self.skinny_gate_up:
+                        lw["pgu"] = ops.PackedLinear(lw.pop("wgu"), silu_mul=True)
+                    if self.skinny_qkv:
+                        lw["pqkv"] = ops.PackedLinear(lw.pop("wqkv"))
                 if self.skinny_o:
                     lw["po"] = ops.PackedLinear(lw.pop("wo"))
                 lw["pd"] = ops.PackedLinear(lw.pop("wd"))
@@ -171,13 +178,14 @@ class Qwen3Decoder:
         self.mlp_out = torch.zeros(batch, h, dtype=dt, device=self.device)
         self.o_out = torch.zeros(batch, h, dtype=dt, device=self.device)
         self.logits = torch.zeros(batch, cfg.vocab, dtype=dt, device=self.device)
+        if self.norm_fused or self.skinny_qkv:
+            self.qkv_buf = torch.zeros(batch, cfg.qkv_dim, dtype=dt, device=self.device)
         if self.norm_fused:
             l0 = self.w.layers[0]
             self.slots_o, self.slots_d = l0["po"].slots(batch), l0["pd"].slots(batch)
             n = max(self.slots_o, self.slots_d, 1) * ops.SS_ROWS
             self.ss_a = torch.zeros(n, dtype=torch.float32, device=self.device)   # before qkv / lm_head
             self.ss_b = torch.zeros(n, dtype=torch.float32, device=self.device)   # before gate_up
-            self.qkv_buf = torch.zeros(batch, cfg.qkv_dim, dtype=dt, device=self.device)
         self.o_part = torch.zeros(batch * cfg.heads * self.nsplit * cfg.head_dim, dtype=torch.float32,
                                   device=self.device)
         self.ml_part = torch.zeros(batch * cfg.heads * self.nsplit * 2, dtype=torch.float32,
@@ -266,7 +274,7 @@ class Qwen3Decoder:
         else:
             self.h.copy_(ref.rmsnorm(self.res, w.layers[0]["ln1"], cfg.eps))
         for li, lw in enumerate(w.layers):
-            qkv = F.linear(self.h, lw["wqkv"])
+            qkv = lw["pqkv"](self.h, out=self.qkv_buf) if self.skinny_qkv else F.linear(self.h, lw["wqkv"])
             if self.native:
                 self._attention(li, lw, qkv)
             else:

@@ -39,3 +39,10 @@ def test_bench_json_contract_cpu_rehearsal(nproc):
     tokens = nproc * 2 * 2 * 3
     assert out["value"] == pytest.approx(tokens / (out["ms_per_step"] * 3 / 1000), rel=0.02)
     assert len(out["per_slice_tok_s_rank0"]) == 2
+    if nproc > 1:
+        # the untimed all-reduce between ranks: exact, and reported beside the headline
+        ar = out["allreduce_between_gpus"]
+        assert [r["bytes"] for r in ar] == [64 << 10, 1 << 20] and all(r["correct"] for r in ar)
+        assert out["allreduce_peak_busbw_gbps"] == max(r["busbw_gbps"] for r in ar) > 0
+    else:
+        assert "allreduce_between_gpus" not in out

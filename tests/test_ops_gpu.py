@@ -385,3 +385,20 @@ def test_decoder_norm_fused_matches_reference(monkeypatch):
         la, lb = a.step(), b.step()
         _close(la, lb, 5e-2)
         b.tokens.copy_(a.tokens)
+
+
+def test_decoder_qkv_on_wide_kernel_matches_reference(monkeypatch):
+    """Small-partition plan (qkv on the wide skinny kernel, forced here on the
+    whole GPU with MIVGPU_QKV_WIDE_CUS): 3 steps against the fp32 reference."""
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
+
+    monkeypatch.setenv("MIVGPU_QKV_WIDE_CUS", "100000")
+    a = Qwen3Decoder(QWEN3_TINY, batch=7, max_ctx=64, device="cuda", native=True, seed=8)
+    assert a.skinny_qkv and "pqkv" in a.w.layers[0] and "wqkv" not in a.w.layers[0]
+    b = Qwen3Decoder(QWEN3_TINY, batch=7, max_ctx=64, device="cuda", native=False, seed=8)
+    a.fill_context(12)
+    b.fill_context(12)
+    for _ in range(3):
+        la, lb = a.step(), b.step()
+        _close(la, lb, 5e-2)
+        b.tokens.copy_(a.tokens)
