@@ -6,8 +6,11 @@
 // carries.  "Device memory" is host malloc bounded by MOCKHIP_TOTAL_MIB.
 #include <hip/hip_runtime_api.h>
 
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <mutex>
@@ -31,6 +34,28 @@ int ndev() {
   const char* n = getenv("MOCKHIP_DEVICES");
   return n ? atoi(n) : 1;
 }
+// KFD's per-process VRAM file, simulated when MOCKHIP_KFD_SYSFS is set:
+// <root>/proc/<MOCKHIP_KFD_PID or getpid()>/vram_<MOCKHIP_KFD_GPU_ID + dev>
+// = runtime "context" bytes (mockhip_set_kfd_context) + live allocations.
+// MOCKHIP_KFD_PID != getpid() stands for a container's pid namespace.
+size_t kfd_context[16] = {0};
+void kfd_publish_locked(int dev) {
+  const char* root = getenv("MOCKHIP_KFD_SYSFS");
+  if (!root) return;
+  const char* gid = getenv("MOCKHIP_KFD_GPU_ID");
+  const char* kp = getenv("MOCKHIP_KFD_PID");
+  const int pid = kp ? atoi(kp) : (int)getpid();
+  char path[512];
+  snprintf(path, sizeof(path), "%s/proc", root);
+  mkdir(path, 0755);
+  snprintf(path, sizeof(path), "%s/proc/%d", root, pid);
+  mkdir(path, 0755);
+  snprintf(path, sizeof(path), "%s/proc/%d/vram_%d", root, pid, (gid ? atoi(gid) : 1) + dev);
+  FILE* f = fopen(path, "w");
+  if (!f) return;
+  fprintf(f, "%zu\n", kfd_context[dev] + used_bytes[dev]);
+  fclose(f);
+}
 hipError_t do_alloc(void** p, size_t sz) {
   std::lock_guard<std::mutex> lk(mu);
   if (used_bytes[cur_dev] + sz > total_bytes()) return hipErrorOutOfMemory;
@@ -39,6 +64,7 @@ hipError_t do_alloc(void** p, size_t sz) {
   if (!m) return hipErrorOutOfMemory;
   allocs[m] = sz;
   used_bytes[cur_dev] += sz;
+  kfd_publish_locked(cur_dev);
   *p = m;
   return hipSuccess;
 }
@@ -48,12 +74,18 @@ hipError_t do_free(void* p) {
   auto it = allocs.find(p);
   if (it == allocs.end()) return hipErrorInvalidValue;
   used_bytes[cur_dev] -= it->second;
+  kfd_publish_locked(cur_dev);
   allocs.erase(it);
   free(p);
   return hipSuccess;
 }
 }  // namespace
 
+EXPORT void mockhip_set_kfd_context(unsigned long long mib) {
+  std::lock_guard<std::mutex> lk(mu);
+  kfd_context[cur_dev] = (size_t)mib << 20;
+  kfd_publish_locked(cur_dev);
+}
 EXPORT hipError_t hipGetDeviceCount(int* n) { *n = ndev(); return hipSuccess; }
 EXPORT hipError_t hipGetDevice(int* d) { *d = cur_dev; return hipSuccess; }
 EXPORT hipError_t hipSetDevice(int d) {
@@ -115,7 +147,12 @@ EXPORT hipError_t hipGetDevicePropertiesR0000(void* p, int) {
   *reinterpret_cast<size_t*>(static_cast<char*>(p) + 256) = total_bytes();
   return hipSuccess;
 }
-EXPORT hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t, int) { *v = 0; return hipSuccess; }
+// PCI location of mock device d: domain 0, bus 0x75 + 0x10 * d, device 0
+// (what the shim matches against the KFD topology in context accounting).
+EXPORT hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t a, int dev) {
+  *v = a == hipDeviceAttributePciBusId ? 0x75 + 0x10 * dev : 0;
+  return hipSuccess;
+}
 EXPORT hipError_t hipLaunchKernel(const void*, dim3, dim3, void**, size_t, hipStream_t) {
   launches++;
   return hipSuccess;

@@ -10,6 +10,8 @@
 //   launch <n>       n x hipLaunchKernel
 //   usage            mivgpu_process_usage(0) via dlsym
 //   sleep <ms>
+//   kfdctx <MiB>     runtime VRAM outside the hooks in the mock's simulated
+//                    KFD per-process file (MOCKHIP_KFD_SYSFS), for context accounting
 //   device <i>       hipSetDevice
 //   stress <threads> <iters> <max MiB>
 //                    threads doing random hipMalloc/hipFree and
@@ -20,6 +22,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -123,6 +126,13 @@ int main(int argc, char** argv) {
     } else if (!strcmp(c, "usage")) {
       auto f = (long long (*)(int))dlsym(RTLD_DEFAULT, "mivgpu_process_usage");
       printf("{\"op\":\"usage\",\"bytes\":%lld}\n", f ? f(0) : -2ll);
+    } else if (!strcmp(c, "kfdctx")) {
+      // runtime bytes outside the allocator hooks, as KFD would count them
+      auto f = (void (*)(unsigned long long))dlsym(RTLD_DEFAULT, "mockhip_set_kfd_context");
+      const unsigned long long mib = strtoull(argv[++i], nullptr, 10);
+      if (f) f(mib);
+      printf("{\"op\":\"kfdctx\",\"ok\":%d}\n", f ? 1 : 0);
+      usleep(30000);  // past the shim's 20 ms refresh interval
     } else if (!strcmp(c, "sleep")) {
       usleep((useconds_t)strtoul(argv[++i], nullptr, 10) * 1000);
     } else if (!strcmp(c, "stress")) {

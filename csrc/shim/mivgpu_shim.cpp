@@ -46,12 +46,15 @@
 #include <sys/stat.h>
 #include <sys/types.h>
 #include <time.h>
+#include <dirent.h>
 #include <unistd.h>
 
 #include <atomic>
 #include <cstddef>
 #include <mutex>
 #include <unordered_map>
+#include <utility>
+#include <vector>
 
 #include "mivgpu/shared_region.h"
 
@@ -228,6 +231,8 @@ REAL_DECL(hipError_t, hipStreamSynchronize_spt, "hip_5.2", (hipStream_t))
 REAL_DECL(hipError_t, hipDeviceSynchronize, "hip_4.2", (void))
 REAL_DECL(hipError_t, hipStreamBeginCapture, "hip_4.3", (hipStream_t, hipStreamCaptureMode))
 REAL_DECL(hipError_t, hipStreamBeginCapture_spt, "hip_5.3", (hipStream_t, hipStreamCaptureMode))
+REAL_DECL(hipError_t, hipStreamEndCapture, "hip_4.3", (hipStream_t, hipGraph_t*))
+REAL_DECL(hipError_t, hipStreamEndCapture_spt, "hip_5.3", (hipStream_t, hipGraph_t*))
 REAL_DECL(hipError_t, hipSetDevice, "hip_4.2", (int))
 REAL_DECL(hipError_t, hipMemset, "hip_4.2", (void*, int, size_t))
 
@@ -240,6 +245,8 @@ struct Config {
   int priority = 1;
   bool oversubscribe = false;
   bool disabled = false;
+  bool account_context = true;  // count runtime/code-object VRAM (KFD per-process view) in the quota
+  char kfd_sysfs[256] = "/sys/class/kfd/kfd";
   uint64_t gate_min_interval_ns = 200000;  // >= 200 us of host submission per gate
   int64_t gate_cap_ns = 20000000;          // 20 ms burst
   int64_t gate_max_hold_ns = 100000000;    // 100 ms per gate, bounds every spin
@@ -325,6 +332,10 @@ void load_config() {
   if (pri) g_cfg.priority = atoi(pri);
   const char* ov = getenv("MIVGPU_OVERSUBSCRIBE");
   g_cfg.oversubscribe = ov && (!strcmp(ov, "1") || !strcasecmp(ov, "true"));
+  const char* ac = getenv("MIVGPU_ACCOUNT_CONTEXT");
+  g_cfg.account_context = !(ac && (!strcmp(ac, "0") || !strcasecmp(ac, "false")));
+  const char* kfd = getenv("MIVGPU_KFD_SYSFS");
+  if (kfd && *kfd) snprintf(g_cfg.kfd_sysfs, sizeof(g_cfg.kfd_sysfs), "%s", kfd);
   const char* gi = getenv("MIVGPU_GATE_INTERVAL_US");
   if (gi) g_cfg.gate_min_interval_ns = (uint64_t)atoll(gi) * 1000ull;
   const char* cap = getenv("MIVGPU_GATE_BURST_US");
@@ -613,11 +624,181 @@ void account_sub(int dev, uint64_t bytes, AllocKind kind) {
   }
 }
 
+// ------------------------------------------------ context / code-object VRAM --
+// VRAM a process holds outside the hooked allocators -- HIP/ROCr pools,
+// kernarg and signal buffers, code objects, scratch -- is invisible to the
+// hooks (SURVEY.md 7.5 "memory accounting truthfulness"; the reference's
+// libvgpu reconciles the same gap against NVML).  KFD publishes the process's
+// total VRAM per GPU in <kfd>/proc/<pid>/vram_<gpu_id>; the shim charges
+// context = that - (buffer + vmm) to the slot and to the container's quota,
+// so the hard limit covers everything the process holds on the device.
+// Refreshed at most every 20 ms, from the allocation and meminfo hooks.
+struct CtxDev {
+  int gpu_id = -2;        // KFD gpu_id of the HIP device (-2 unresolved, -1 unavailable)
+  int kfd_pid = -2;       // KFD's name for this process (-2 unresolved, -1 unavailable)
+  uint64_t last_ns = 0;
+};
+CtxDev g_ctx[MIVGPU_MAX_DEVICES];
+std::mutex g_ctx_mu;
+// Stream captures in flight (begin/end hooks): the pid probe below frees
+// memory, which a global-mode capture forbids, so it waits for none.
+std::atomic<int> g_captures{0};
+
+bool read_u64_file(const char* path, uint64_t* out) {
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return false;
+  char buf[64];
+  ssize_t n = read(fd, buf, sizeof(buf) - 1);
+  close(fd);
+  if (n <= 0) return false;
+  buf[n] = 0;
+  char* end = nullptr;
+  unsigned long long v = strtoull(buf, &end, 10);
+  if (end == buf) return false;
+  *out = v;
+  return true;
+}
+
+// KFD topology node of HIP device `dev`: match the PCI domain and bus/device
+// (location_id = bus << 8 | device << 3 | function) against every GPU node;
+// an ambiguous match (several nodes behind one function) leaves it unknown.
+int resolve_kfd_gpu_id(int dev) {
+  if (!real_hipDeviceGetAttribute()) return -1;
+  int bus = 0, slot = 0, domain = 0;
+  if (real_hipDeviceGetAttribute()(&bus, hipDeviceAttributePciBusId, dev) != hipSuccess ||
+      real_hipDeviceGetAttribute()(&slot, hipDeviceAttributePciDeviceId, dev) != hipSuccess ||
+      real_hipDeviceGetAttribute()(&domain, hipDeviceAttributePciDomainId, dev) != hipSuccess)
+    return -1;
+  int found = -1, matches = 0;
+  for (int node = 0; node < 256; ++node) {
+    char path[512];
+    snprintf(path, sizeof(path), "%s/topology/nodes/%d/properties", g_cfg.kfd_sysfs, node);
+    FILE* f = fopen(path, "re");
+    if (!f) {
+      if (node > 0) break;  // nodes are numbered densely from 0
+      continue;
+    }
+    long long loc = -1, dom = -1;
+    char key[96];
+    long long val;
+    while (fscanf(f, "%95s %lld", key, &val) == 2) {
+      if (!strcmp(key, "location_id")) loc = val;
+      else if (!strcmp(key, "domain")) dom = val;
+    }
+    fclose(f);
+    uint64_t gid = 0;
+    snprintf(path, sizeof(path), "%s/topology/nodes/%d/gpu_id", g_cfg.kfd_sysfs, node);
+    if (!read_u64_file(path, &gid) || gid == 0) continue;  // CPU node
+    if (loc < 0 || (loc >> 8) != bus || ((loc >> 3) & 0x1f) != slot || (dom >= 0 && dom != domain)) continue;
+    ++matches;
+    found = (int)gid;
+  }
+  return matches == 1 ? found : -1;
+}
+
+// KFD names /proc/<pid> by the host pid, which a process in a container's pid
+// namespace does not know (the monitor fills slot->hostpid when it runs with
+// hostPID; before that, or without it, the shim finds itself): snapshot
+// vram_<gpu_id> of every KFD process, make one distinctive allocation through
+// the real allocator, and keep the single process whose VRAM grew by exactly
+// that much.  Three attempts with different sizes; ambiguity -> unavailable.
+int probe_kfd_pid(int gpu_id) {
+  if (!real_hipMalloc() || !real_hipFree()) return -1;
+  char dir[512];
+  snprintf(dir, sizeof(dir), "%s/proc", g_cfg.kfd_sysfs);
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    std::vector<std::pair<int, uint64_t>> before;
+    DIR* d = opendir(dir);
+    if (!d) return -1;
+    while (struct dirent* e = readdir(d)) {
+      char* end = nullptr;
+      long pid = strtol(e->d_name, &end, 10);
+      if (end == e->d_name || *end || pid <= 0) continue;
+      char path[640];
+      uint64_t v = 0;
+      snprintf(path, sizeof(path), "%s/%ld/vram_%d", dir, pid, gpu_id);
+      if (read_u64_file(path, &v)) before.emplace_back((int)pid, v);
+    }
+    closedir(d);
+    if (before.empty()) return -1;
+    const uint64_t probe = (64ull + 6ull * (uint64_t)attempt) << 20;
+    void* p = nullptr;
+    if (real_hipMalloc()(&p, probe) != hipSuccess || !p) return -1;
+    int found = -1, hits = 0;
+    for (auto& pv : before) {
+      char path[640];
+      uint64_t v = 0;
+      snprintf(path, sizeof(path), "%s/%d/vram_%d", dir, pv.first, gpu_id);
+      if (read_u64_file(path, &v) && v >= pv.second + probe && v < pv.second + probe + (4ull << 20)) {
+        found = pv.first;
+        ++hits;
+      }
+    }
+    (void)real_hipFree()(p);
+    if (hits == 1) return found;
+  }
+  return -1;
+}
+
+void refresh_context(int dev, bool force) {
+  if (!g_cfg.account_context || !g_region || g_slot < 0 || dev < 0 || dev >= MIVGPU_MAX_DEVICES) return;
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  CtxDev& c = g_ctx[dev];
+  uint64_t now = coarse_ns();
+  if (c.gpu_id == -1 || (!force && c.last_ns && now - c.last_ns < 20000000ull)) return;
+  c.last_ns = now;
+  if (c.gpu_id == -2) {
+    c.gpu_id = resolve_kfd_gpu_id(dev);
+    if (c.gpu_id < 0) {
+      mlog(3, "device %d: no KFD node matched; runtime VRAM not charged to the quota", dev);
+      return;
+    }
+  }
+  mivgpu_proc_slot_t* s = &g_region->procs[g_slot];
+  int pid = __atomic_load_n(&s->hostpid, __ATOMIC_RELAXED);  // the monitor's mapping wins
+  if (pid <= 0) {
+    if (c.kfd_pid == -2) {
+      if (g_captures.load(std::memory_order_acquire) > 0) return;
+      c.kfd_pid = probe_kfd_pid(c.gpu_id);
+      if (c.kfd_pid < 0) {
+        mlog(3, "device %d: own KFD process entry not identified; runtime VRAM not charged", dev);
+      } else {
+        int zero = 0;
+        __atomic_compare_exchange_n(&s->hostpid, &zero, c.kfd_pid, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
+      }
+    }
+    pid = c.kfd_pid;
+  }
+  if (pid <= 0) return;
+  char path[512];
+  uint64_t vram = 0;
+  snprintf(path, sizeof(path), "%s/proc/%d/vram_%d", g_cfg.kfd_sysfs, pid, c.gpu_id);
+  if (!read_u64_file(path, &vram)) return;
+  mivgpu_mem_t* m = &s->used[dev];
+  uint64_t hooked = __atomic_load_n(&m->buffer, __ATOMIC_RELAXED) + __atomic_load_n(&m->vmm, __ATOMIC_RELAXED);
+  uint64_t ctx = vram > hooked ? vram - hooked : 0;
+  uint64_t old = __atomic_exchange_n(&m->context, ctx, __ATOMIC_RELAXED);
+  if (ctx == old) return;
+  if (ctx > old) {
+    uint64_t d = ctx - old;
+    __atomic_fetch_add(&g_region->dev_used[dev], d, __ATOMIC_RELAXED);
+    uint64_t t = __atomic_add_fetch(&m->total, d, __ATOMIC_RELAXED);
+    uint64_t pk = __atomic_load_n(&m->peak, __ATOMIC_RELAXED);
+    while (t > pk && !__atomic_compare_exchange_n(&m->peak, &pk, t, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+    }
+  } else {
+    uint64_t d = old - ctx;
+    __atomic_fetch_sub(&g_region->dev_used[dev], d, __ATOMIC_RELAXED);
+    __atomic_fetch_sub(&m->total, d, __ATOMIC_RELAXED);
+  }
+}
+
 // Reserve `bytes` on `dev` against the quota before calling the real
 // allocator.  Returns false if the slice is exhausted.
 bool reserve(int dev, uint64_t bytes, AllocKind kind) {
   uint64_t lim = limit_of(dev);
   if (!g_region) return true;
+  refresh_context(dev, false);
   if (lim == 0) {
     account_add(dev, bytes, kind);
     return true;
@@ -1104,6 +1285,7 @@ MIVGPU_EXPORT hipError_t hipMemGetInfo(size_t* free_b, size_t* total_b) {
   int dev = current_device();
   uint64_t lim = limit_of(dev);
   if (lim && g_region) {
+    refresh_context(dev, false);
     uint64_t used = __atomic_load_n(&g_region->dev_used[dev], __ATOMIC_RELAXED);
     uint64_t vfree = used >= lim ? 0 : lim - used;
     if (free_b) *free_b = vfree < *free_b ? vfree : *free_b;
@@ -1228,7 +1410,9 @@ MIVGPU_EXPORT hipError_t hipStreamBeginCapture(hipStream_t stream, hipStreamCapt
   Guard g;
   DeviceGate& G = g_gates[current_device()];
   std::lock_guard<std::mutex> lk(G.mu);
-  return real_hipStreamBeginCapture()(stream, mode);
+  hipError_t rc = real_hipStreamBeginCapture()(stream, mode);
+  if (rc == hipSuccess) g_captures.fetch_add(1, std::memory_order_acq_rel);
+  return rc;
 }
 
 MIVGPU_EXPORT hipError_t hipStreamBeginCapture_spt(hipStream_t stream, hipStreamCaptureMode mode) {
@@ -1236,7 +1420,22 @@ MIVGPU_EXPORT hipError_t hipStreamBeginCapture_spt(hipStream_t stream, hipStream
   Guard g;
   DeviceGate& G = g_gates[current_device()];
   std::lock_guard<std::mutex> lk(G.mu);
-  return real_hipStreamBeginCapture_spt()(stream, mode);
+  hipError_t rc = real_hipStreamBeginCapture_spt()(stream, mode);
+  if (rc == hipSuccess) g_captures.fetch_add(1, std::memory_order_acq_rel);
+  return rc;
+}
+
+// A capture ends (successfully or invalidated) with hipStreamEndCapture.
+MIVGPU_EXPORT hipError_t hipStreamEndCapture(hipStream_t stream, hipGraph_t* graph) {
+  hipError_t rc = real_hipStreamEndCapture()(stream, graph);
+  if (g_captures.load(std::memory_order_acquire) > 0) g_captures.fetch_sub(1, std::memory_order_acq_rel);
+  return rc;
+}
+
+MIVGPU_EXPORT hipError_t hipStreamEndCapture_spt(hipStream_t stream, hipGraph_t* graph) {
+  hipError_t rc = real_hipStreamEndCapture_spt()(stream, graph);
+  if (g_captures.load(std::memory_order_acquire) > 0) g_captures.fetch_sub(1, std::memory_order_acq_rel);
+  return rc;
 }
 
 MIVGPU_EXPORT hipError_t hipStreamSynchronize(hipStream_t stream) {

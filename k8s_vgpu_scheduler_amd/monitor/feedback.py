@@ -15,6 +15,7 @@ from __future__ import annotations
 import logging
 import threading
 
+from .hostpid import fill_host_pids
 from .lister import ContainerLister
 
 log = logging.getLogger(__name__)
@@ -85,6 +86,7 @@ def watch_and_feedback(lister: ContainerLister, stop: threading.Event, period: f
             continue
         try:
             lister.update()
+            fill_host_pids(lister.list_containers())
             observe(lister)
         except Exception:  # noqa: BLE001
             log.exception("feedback iteration failed")

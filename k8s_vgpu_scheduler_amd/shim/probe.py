@@ -160,11 +160,21 @@ def child_region(args) -> dict:
     x = torch.empty(args.oom_probe_mib << 20, dtype=torch.uint8, device="cuda")
     x.fill_(1)
     torch.cuda.synchronize()
+    time.sleep(0.05)                   # past the shim's 20 ms runtime-VRAM refresh interval
+    torch.cuda.mem_get_info()          # the meminfo hook refreshes the context charge
     reg = SharedRegion(os.environ["MIVGPU_SHARED_CACHE"], writable=False)
     me = [p for p in reg.active_procs() if p.pid == os.getpid()]
+    # KFD names the entry by the host pid, which the shim published in the slot
+    kfd = Path("/sys/class/kfd/kfd/proc") / str(me[0].hostpid if me and me[0].hostpid else os.getpid())
+    kfd_vram = sum(int(f.read_text()) for f in kfd.glob("vram_*")) if kfd.is_dir() else -1
     out = {"mode": "region", "dev_used_mib": reg.dev_used(0) >> 20, "limit_mib": reg.memory_limit(0) >> 20,
            "procs": len(list(reg.active_procs())), "self_found": bool(me),
            "self_buffer_mib": (me[0].used[0].buffer >> 20) if me else -1,
+           "self_vmm": me[0].used[0].vmm if me else -1,
+           "self_context": me[0].used[0].context if me else -1,
+           "self_total": me[0].used[0].total if me else -1,
+           "self_buffer": me[0].used[0].buffer if me else -1,
+           "kfd_vram": kfd_vram, "hostpid": me[0].hostpid if me else -1,
            "launches": reg.launches(0), "uuid": reg.uuid(0)}
     reg.close()
     del x

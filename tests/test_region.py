@@ -175,3 +175,40 @@ def test_lister_missing_hook_path(tmp_path):
 def test_region_file_size_matches_struct(tmp_path):
     d = _mk(tmp_path, "u1", "a")
     assert os.path.getsize(d / "r.cache") == REGION_SIZE
+
+
+def _fake_proc(root, pid, nspids, cgroup):
+    d = root / str(pid)
+    d.mkdir(parents=True)
+    (d / "status").write_text(f"Name:\tpython\nPid:\t{pid}\nNSpid:\t" + "\t".join(map(str, nspids)) + "\n")
+    (d / "cgroup").write_text(cgroup)
+
+
+def test_host_pids_filled_from_nspid_and_pod_cgroup(region, tmp_path):
+    """The monitor maps slot pids (container pid namespace) to host pids: the
+    NSpid tail must equal the slot pid and the cgroup must name the pod UID."""
+    from types import SimpleNamespace
+
+    from k8s_vgpu_scheduler_amd.monitor.hostpid import fill_host_pids
+
+    uid = "3f1c2b7a-0d1e-4a5b-9c8d-112233445566"
+    proc = tmp_path / "proc"
+    # cgroupfs layout, pid 7 inside the container = host 4107
+    _fake_proc(proc, 4107, [4107, 7], f"0::/kubepods/burstable/pod{uid}/abc123\n")
+    # systemd layout (dashes -> underscores), pid 8 = host 4108
+    _fake_proc(proc, 4108, [4108, 8], f"0::/kubepods.slice/kubepods-pod{uid.replace('-', '_')}.slice/cri-x\n")
+    # same container pid 9 in two pods: only the one in our pod may match
+    _fake_proc(proc, 4109, [4109, 9], f"0::/kubepods/pod{uid}/c1\n")
+    _fake_proc(proc, 5109, [5109, 9], "0::/kubepods/podffffffff-0000-0000-0000-000000000000/c2\n")
+    # pid 10 twice in our pod (ambiguous): left unfilled
+    _fake_proc(proc, 4110, [4110, 10], f"0::/kubepods/pod{uid}/c1\n")
+    _fake_proc(proc, 4210, [4210, 10], f"0::/kubepods/pod{uid}/c3\n")
+    (proc / "self").mkdir()
+    for i, pid in enumerate((7, 8, 9, 10, 11)):
+        _proc(region, i, pid)
+    region.r.procs[5].pid, region.r.procs[5].status, region.r.procs[5].hostpid = 12, 1, 999  # already known
+    region.r.procnum = 6
+    c = SimpleNamespace(pod_uid=uid, region=region)
+    assert fill_host_pids([c], proc_root=str(proc)) == 3
+    assert [region.r.procs[i].hostpid for i in range(6)] == [4107, 4108, 4109, 0, 0, 999]
+    assert fill_host_pids([c], proc_root=str(proc)) == 0      # nothing new to fill

@@ -203,3 +203,67 @@ def test_roctx_markers_for_shim_decisions(native_build, tmp_path):
     run(native_build, tmp_path, "alloc", 800, "alloc", 800, cache="q.cache",
         env={**env, "MIVGPU_ROCTX": "0"})
     assert not trace.exists()
+
+
+def _fake_kfd(root, gpu_nodes):
+    """KFD sysfs with a CPU node 0 and GPU nodes [(gpu_id, location_id, domain)]."""
+    n0 = root / "topology" / "nodes" / "0"
+    n0.mkdir(parents=True)
+    (n0 / "gpu_id").write_text("0\n")
+    (n0 / "properties").write_text("cpu_cores_count 64\nsimd_count 0\nlocation_id 0\ndomain 0\n")
+    for i, (gid, loc, dom) in enumerate(gpu_nodes, start=1):
+        n = root / "topology" / "nodes" / str(i)
+        n.mkdir(parents=True)
+        (n / "gpu_id").write_text(f"{gid}\n")
+        (n / "properties").write_text(f"cpu_cores_count 0\nsimd_count 1024\nlocation_id {loc}\ndomain {dom}\n")
+    return root
+
+
+def _kfd_env(kfd, gid=4242, kpid=987654, limit="4096m"):
+    # MOCKHIP_KFD_PID != the driver's pid: the process runs in a "pid namespace"
+    return {"HIP_DEVICE_MEMORY_LIMIT_0": limit, "MIVGPU_KFD_SYSFS": str(kfd), "MOCKHIP_KFD_SYSFS": str(kfd),
+            "MOCKHIP_KFD_GPU_ID": str(gid), "MOCKHIP_KFD_PID": str(kpid)}
+
+
+def test_runtime_vram_charged_to_the_quota(native_build, tmp_path):
+    """VRAM outside the hooked allocators (KFD's per-process total minus the
+    hooked bytes: context, code objects, scratch) counts against the slice.
+    The shim finds its own KFD entry (named by a host pid it cannot see) with
+    a probe allocation, among decoy processes on the same GPU."""
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0), (5151, 0x85 << 8, 0)])
+    for pid, gid, v in ((111, 4242, 5 << 30), (222, 5151, 1 << 30), (333, 4242, 0)):
+        (kfd / "proc" / str(pid)).mkdir(parents=True)
+        (kfd / "proc" / str(pid) / f"vram_{gid}").write_text(f"{v}\n")
+    e = dict(os.environ, MOCKHIP_TOTAL_MIB="65536", MIVGPU_SHARED_CACHE=str(tmp_path / "ctx.cache"),
+             LD_PRELOAD=str(native_build["shim"]), **_kfd_env(kfd))
+    p = subprocess.Popen([str(native_build["driver"]), "kfdctx", "600", "alloc", "1000", "meminfo", "alloc", "2600",
+                          "alloc", "2400", "usage", "sleep", "3000"], env=e, stdout=subprocess.PIPE, text=True)
+    out = [json.loads(p.stdout.readline()) for _ in range(6)]
+    assert out[0]["ok"] == 1 and out[1]["rc"] == 0
+    assert out[2]["total_mib"] == 4096 and out[2]["free_mib"] == 4096 - 1600   # 600 MiB of context charged
+    assert out[3]["rc"] == 2                                                   # 1600 + 2600 > 4096
+    assert out[4]["rc"] == 0
+    assert out[5]["bytes"] == (1000 + 600 + 2400) << 20
+    reg = R.SharedRegion(str(tmp_path / "ctx.cache"))
+    me = reg.active_procs()[0]
+    assert me.hostpid == 987654                       # published for the monitor
+    assert me.used[0].context == 600 << 20 and me.used[0].buffer == 3400 << 20
+    reg.close()
+    p.wait(timeout=30)
+
+
+def test_runtime_vram_accounting_off_or_unresolvable(native_build, tmp_path):
+    # opt-out
+    kfd = _fake_kfd(tmp_path / "kfd1", [(4242, 0x75 << 8, 0)])
+    env = dict(_kfd_env(kfd), MIVGPU_ACCOUNT_CONTEXT="0")
+    out = run(native_build, tmp_path, "kfdctx", 600, "alloc", 1000, "meminfo", env=env, cache="o.cache")
+    assert out[2]["free_mib"] == 3096
+    # two KFD nodes behind one PCI function (ambiguous): nothing charged
+    kfd = _fake_kfd(tmp_path / "kfd2", [(4242, 0x75 << 8, 0), (4343, 0x75 << 8, 0)])
+    out = run(native_build, tmp_path, "kfdctx", 600, "alloc", 1000, "meminfo", env=_kfd_env(kfd), cache="a.cache")
+    assert out[2]["free_mib"] == 3096
+    # no KFD process entry for the device (e.g. sysfs not mounted): nothing charged
+    kfd = _fake_kfd(tmp_path / "kfd3", [(4242, 0x75 << 8, 0)])
+    out = run(native_build, tmp_path, "alloc", 1000, "meminfo",
+              env={"HIP_DEVICE_MEMORY_LIMIT_0": "4096m", "MIVGPU_KFD_SYSFS": str(kfd)}, cache="b.cache")
+    assert out[1]["free_mib"] == 3096

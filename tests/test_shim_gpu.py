@@ -46,10 +46,28 @@ def test_allocation_accounting_visible_to_monitor(tmp):
     assert r["uuid"] == "GPU-test"
 
 
+def test_runtime_vram_charged_as_context(tmp):
+    """Runtime / code-object VRAM (KFD's per-process total minus the hooked
+    allocations) is charged to the slot's context field and the quota."""
+    cache = os.path.join(tmp, "ctx.cache")
+    r = run_child("region", {"MIVGPU_SHARED_CACHE": cache, "HIP_DEVICE_MEMORY_LIMIT_0": "8192m"}, True,
+                  ["--oom-probe-mib", "512"])
+    assert r["rc"] == 0, r.get("stderr")
+    print(json.dumps({k: r[k] for k in ("hostpid", "kfd_vram", "self_buffer", "self_vmm", "self_context",
+                                        "self_total")}))
+    assert r["hostpid"] > 0, "the shim did not identify its KFD process entry"
+    assert r["kfd_vram"] > 0
+    assert r["self_context"] > 0
+    assert r["self_total"] == r["self_buffer"] + r["self_vmm"] + r["self_context"]
+    # the charge is KFD's view: within 64 MiB of it (allocations may land between the two reads)
+    assert abs(r["self_total"] - r["kfd_vram"]) <= 64 << 20
+
+
 def test_two_processes_share_one_container_limit(tmp):
     cache = os.path.join(tmp, "c.cache")
-    env = {"MIVGPU_SHARED_CACHE": cache, "HIP_DEVICE_MEMORY_LIMIT_0": "3072m"}
+    env = {"MIVGPU_SHARED_CACHE": cache, "HIP_DEVICE_MEMORY_LIMIT_0": "4096m"}
     # each holds 2 GiB for 8 s after probing: the container-wide limit admits one
+    # (each process also carries ~0.5 GiB of runtime VRAM, charged as context)
     outs = run_parallel("matmul", [env, env], True, ["--n", "1024", "--iters", "5",
                                                      "--oom-probe-mib", "2048", "--hold-s", "8"])
     assert all(o["rc"] == 0 for o in outs), outs
