@@ -828,6 +828,16 @@ bool slice_plan(int cus) {
   return cus <= limit;
 }
 
+// Half-GPU partitions (97-160 CUs) get their own wide-kernel wave counts
+// (MIVGPU_WIDE_MID_PLAN=0 restores the whole-chip ones for A/B runs).
+bool mid_plan(int cus, bool slice) {
+  static const int on = [] {
+    const char* e = getenv("MIVGPU_WIDE_MID_PLAN");
+    return e && *e ? atoi(e) : 1;
+  }();
+  return on && !slice && cus <= 160;
+}
+
 }  // namespace
 extern "C" int mivgpu_ops_visible_cus();   // model_ops.hip
 namespace {
@@ -900,6 +910,13 @@ bool plan_wide(int M, int K, int N, int epi, int* nt, int* wv, int* S) {
   if (*wv <= 0) {
     // > 32 rows: 4 waves (2-wave workgroups of 2-4 M-tiles spill registers)
     *wv = (M > 32 || (slice && vgroups >= 16 * cus)) ? 4 : 2;
+    if (M <= 32 && mid_plan(cus, slice)) {
+      // 97-160 CUs (a half-GPU slice), bench/gemm.py --sweep at 128 CUs
+      // (profiles/cu128/sweep_cu128.json): lm_head 4 waves 255 vs 287 us,
+      // down (S = 4) 4 waves 29.4 vs 32.5, gate_up+SiLU 1 wave 47.7 vs 53.0.
+      if (vgroups >= 16 * cus || (vgroups <= 128 && *S > 1)) *wv = 4;
+      else if (epi == EPI_SILU_MUL) *wv = 1;
+    }
     while (*wv > 1 && ntiles % (*nt * *wv)) *wv /= 2;
   }
   if ((*wv != 1 && *wv != 2 && *wv != 4) || ntiles % (*nt * *wv)) return false;

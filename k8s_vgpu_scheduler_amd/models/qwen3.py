@@ -120,10 +120,10 @@ class Qwen3Decoder:
         # (profiles/gemm_wide_*.json).
         self.skinny_gate_up = skinny
         self.skinny_o = skinny and ops.visible_cus() <= int(os.environ.get("MIVGPU_SLICE_PLAN_CUS", "96"))
-        # qkv joins them in small partitions: at 32 CUs (an 8-slice pod)
-        # hipBLASLt takes 50.7 us vs 40.7 on the wide kernel; at 64 CUs it is
-        # 27.9 vs 29.6 (profiles/cu32/, profiles/gemm_wide_plan_cu64.json).
-        self.skinny_qkv = skinny and ops.visible_cus() <= int(os.environ.get("MIVGPU_QKV_WIDE_CUS", "48"))
+        # qkv joins them in partitions: hipBLASLt vs wide kernel at 32 CUs
+        # 50.7 vs 40.7 us, 64 CUs 27.9 vs 29.6, 128 CUs 20.9 vs 17.5, whole
+        # GPU 15.2 vs 17.0 (profiles/cu32/, cu128/, gemm_wide_plan_*.json).
+        self.skinny_qkv = skinny and ops.visible_cus() <= int(os.environ.get("MIVGPU_QKV_WIDE_CUS", "160"))
         # Row-norm fusion (MIVGPU_NORM_FUSED=1; off by default): every
         # projection on the wide kernel; the RMSNorm weights are folded into
         # the columns of qkv / gate_up / lm_head, o_proj and down update the

@@ -196,3 +196,45 @@ def test_norm_call_rejects_bad_arguments():
         lin.norm_call(x, out=out, residual=True)          # no ss_out
     with pytest.raises(ValueError):
         lin.norm_call(x, out=out, row_scale=(torch.zeros(8, device="cuda"), 1, 4096, 1e-6))   # slots too small
+
+
+_MID_CHILD = r"""
+import json, torch
+from k8s_vgpu_scheduler_amd import ops
+from k8s_vgpu_scheduler_amd.ops import reference as ref
+out = {"cus": ops.visible_cus()}
+x = torch.randn(32, 4096, device="cuda").bfloat16()
+for name, N, K, silu in (("gate_up", 24576, 4096, True), ("down", 4096, 12288, False), ("lm", 65536, 4096, False)):
+    w = (torch.randn(N, K, device="cuda") * 0.02).bfloat16()
+    lin = ops.PackedLinear(w, silu_mul=silu)
+    xx = x if K == 4096 else torch.randn(32, K, device="cuda").bfloat16()
+    pl = ops.skinny_plan(32, K, N, lin.epi)
+    y = lin(xx).float()
+    r = xx.float() @ w.float().t()
+    if silu:
+        r = ref.silu_mul(r.bfloat16()).float()
+    out[name] = {"plan": [pl["variant"], pl["nt"], pl["ks"], pl["S"]],
+                 "err": ((y - r).abs().max() / r.abs().max()).item()}
+print("RESULT " + json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("mid", ["1", "0"])
+def test_half_gpu_partition_plans(mid):
+    """128-CU partition (2 slices per GPU): the mid-partition wave counts
+    (MIVGPU_WIDE_MID_PLAN) are chosen and compute the same as fp32."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    env = dict(os.environ, HSA_CU_MASK="0:0-127", MIVGPU_WIDE_MID_PLAN=mid)
+    r = subprocess.run([sys.executable, "-c", _MID_CHILD], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][0][7:])
+    assert out["cus"] == 128
+    want = {"1": {"gate_up": [2, 2, 1, 1], "down": [2, 1, 4, 4], "lm": [2, 1, 4, 1]},
+            "0": {"gate_up": [2, 2, 2, 1], "down": [2, 1, 2, 4], "lm": [2, 1, 2, 1]}}[mid]
+    for k, plan in want.items():
+        assert out[k]["plan"] == plan, (k, out[k])
+        assert out[k]["err"] < 2e-2, (k, out[k])
