@@ -887,9 +887,10 @@ constexpr int unroll_wide_host(int nt) { return nt >= 4 ? 1 : (nt == 2 ? 2 : 4);
 // Wide plan (bench/gemm.py --sweep at 64 and 256 CUs, profiles/gemm_wide_*):
 //  * one tile per wave (X shared by the workgroup's waves, not by a wave's
 //    tiles), except SiLU*up, which pairs a gate with an up tile;
-//  * a CU partition (<= 96 CUs): no split, 2 waves per workgroup, 4 when there
+//  * a CU partition (<= 96 CUs): no split, 4 waves per workgroup when there
 //    are >= 16 wave-groups per CU (lm_head: 422 vs 491 us at 64 CUs) or more
-//    than 32 rows (2-wave workgroups of 2-4 M-tiles spill);
+//    than 32 rows (2-wave workgroups of 2-4 M-tiles spill), otherwise 2 or 4
+//    by CU balance (below);
 //  * the whole chip: S = 4 with 2 waves when <= 128 wave-groups (o_proj,
 //    down), else no split with 2 waves.
 // Values > 0 are requests; false when the wide kernel cannot run them (the
@@ -910,6 +911,17 @@ bool plan_wide(int M, int K, int N, int epi, int* nt, int* wv, int* S) {
   if (*wv <= 0) {
     // > 32 rows: 4 waves (2-wave workgroups of 2-4 M-tiles spill registers)
     *wv = (M > 32 || (slice && vgroups >= 16 * cus)) ? 4 : 2;
+    if (M <= 32 && slice && vgroups < 16 * cus) {
+      // Slice partitions, bench/gemm.py --sweep (profiles/sweeps/): keep the
+      // workgroup count a multiple of the CU count where that is possible.
+      //  * <= 48 CUs (8 slices): 4 waves when vgroups/4 fills every CU equally
+      //    (o_proj 25.3 vs 28.0 us, gate_up 121 vs 132, down 69 vs 79 at 32
+      //    CUs), else 2 (qkv: 48 workgroups on 32 CUs lose to 96);
+      //  * 49-96 CUs (4 slices): 2 waves when vgroups/2 fills the CUs equally
+      //    (o_proj, gate_up, down at 64 CUs), else 4 (qkv 25.9 vs 29.4 us).
+      if (cus <= 48) *wv = (vgroups % 4 == 0 && (vgroups / 4) % cus == 0) ? 4 : 2;
+      else *wv = (vgroups % 2 == 0 && (vgroups / 2) % cus == 0) ? 2 : 4;
+    }
     if (M <= 32 && mid_plan(cus, slice)) {
       // 97-160 CUs (a half-GPU slice), bench/gemm.py --sweep at 128 CUs
       // (profiles/cu128/sweep_cu128.json): lm_head 4 waves 255 vs 287 us,

@@ -238,3 +238,37 @@ def test_half_gpu_partition_plans(mid):
     for k, plan in want.items():
         assert out[k]["plan"] == plan, (k, out[k])
         assert out[k]["err"] < 2e-2, (k, out[k])
+
+
+_SLICE_PLANS_CHILD = r"""
+import json
+from k8s_vgpu_scheduler_amd import ops
+shapes = {"qkv": (6144, 4096, 0), "o_proj": (4096, 4096, 0), "gate_up": (24576, 4096, 1), "down": (4096, 12288, 0),
+          "lm_head": (151936, 4096, 0)}
+out = {"cus": ops.visible_cus()}
+for k, (N, K, epi) in shapes.items():
+    pl = ops.skinny_plan(32, K, N, epi)
+    out[k] = [pl["variant"], pl["nt"], pl["ks"], pl["S"]]
+print("RESULT " + json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("mask,want", [
+    ("0:0-31", {"qkv": [2, 1, 2, 1], "o_proj": [2, 1, 4, 1], "gate_up": [2, 2, 4, 1], "down": [2, 1, 4, 1],
+                "lm_head": [2, 1, 4, 1]}),
+    ("0:0-63", {"qkv": [2, 1, 4, 1], "o_proj": [2, 1, 2, 1], "gate_up": [2, 2, 2, 1], "down": [2, 1, 2, 1],
+                "lm_head": [2, 1, 4, 1]}),
+])
+def test_slice_partition_plans(mask, want):
+    """Auto plans of the Qwen3-8B projections in the 8-slice and 4-slice
+    partitions (the measured table in skinny_gemm.hip plan_wide)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    r = subprocess.run([sys.executable, "-c", _SLICE_PLANS_CHILD], env=dict(os.environ, HSA_CU_MASK=mask),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][0][7:])
+    assert {k: out[k] for k in want} == want
