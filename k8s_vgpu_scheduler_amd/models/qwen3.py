@@ -6,11 +6,12 @@ slice vs. natively.  This module is the MI355X-native stand-in for that
 workload: a Qwen3-8B-shaped decoder (GQA 32q/8kv x 128, per-head QK RMSNorm,
 NeoX RoPE theta 1e6, SwiGLU 12288, vocab 151936) whose decode step runs
   * the weight-streaming projections (gate_up with SiLU*up fused into its
-    epilogue, down, lm_head, and o_proj inside a CU partition) on the
-    hand-written skinny MFMA GEMM (csrc/ops/skinny_gemm.hip, wide workgroups
-    sharing an LDS X tile) over fragment-packed weights, for batch <= 32;
-  * qkv (and o_proj on the whole chip) on hipBLASLt (``F.linear``), where the
-    library is as fast at these 33-50 MB shapes (profiles/gemm_wide_*);
+    epilogue, down, lm_head; o_proj inside a CU partition of <= 96 CUs, qkv
+    in one of <= 160) on the hand-written skinny MFMA GEMM
+    (csrc/ops/skinny_gemm.hip, wide workgroups sharing an LDS X tile) over
+    fragment-packed weights, for batch <= 32;
+  * qkv and o_proj on the whole chip on hipBLASLt (``F.linear``), where the
+    library is faster at these 33-50 MB shapes (profiles/gemm_wide_*, cu128/);
   * every other op on the hand-written gfx950 kernels of libmivgpu_ops.so,
   * the whole step captured in one hipGraph (launch overhead -> one replay).
 No network: weights are random normal(0, 0.02) of the exact architecture.
@@ -19,6 +20,7 @@ No network: weights are random normal(0, 0.02) of the exact architecture.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -107,10 +109,8 @@ class Qwen3Decoder:
         if self.native:
             ops.require_native()
         self.w = Qwen3Weights(cfg, self.device, seed=seed)
-        import os
         shapes_ok = cfg.hidden % 64 == 0 and cfg.intermediate % 64 == 0 and cfg.vocab % 64 == 0
         if skinny is None:
-            import os
             skinny = os.environ.get("MIVGPU_SKINNY_GEMM", "1") != "0"
             skinny = skinny and self.native and batch <= 32 and shapes_ok
         self.skinny = skinny
@@ -133,7 +133,6 @@ class Qwen3Decoder:
         # Measured: 64-CU slice 8.85 vs 8.87 ms/step, whole GPU 4.97 vs 4.92
         # (qkv and o_proj are slower on the wide kernel than on hipBLASLt
         # there), profiles/README.md section 14.
-        import os
         self.norm_fused = skinny and os.environ.get("MIVGPU_NORM_FUSED", "0") == "1"
         if self.norm_fused:
             self.skinny_o = True
@@ -193,7 +192,6 @@ class Qwen3Decoder:
         # One launch per layer for QK-norm + RoPE + KV append + attention +
         # split combine (csrc/ops/model_ops.hip decode_attn_fused_kernel);
         # MIVGPU_ATTN_FUSED=0 runs the three separate kernels.
-        import os
         self.attn_fused = (self.native and os.environ.get("MIVGPU_ATTN_FUSED", "1") != "0"
                            and ops.attn_fused_ok(cfg.heads, cfg.kv_heads, cfg.head_dim))
         self.attn_counters = (torch.zeros(batch * cfg.kv_heads, dtype=torch.int32, device=self.device)
