@@ -36,7 +36,7 @@ def child(args) -> dict:
 
     from k8s_vgpu_scheduler_amd import ops
 
-    bufs = [torch.ones(GIB // 2, dtype=torch.int16, device="cuda") for _ in range(4)]
+    bufs = [torch.ones(GIB // 2, dtype=torch.int16, device="cuda") for _ in range(args.gib)]
     out = torch.zeros(1, dtype=torch.int64, device="cuda")
     cus = ops.visible_cus()
     res = {"cus": cus, "mask": os.environ.get("HSA_CU_MASK", "")}
@@ -72,7 +72,7 @@ def child(args) -> dict:
                 ops.stream_read(b, out, blocks)
         e1.record()
         torch.cuda.synchronize()
-        best[bpc] = round(20 * GIB / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+        best[bpc] = round(5 * len(bufs) * GIB / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
     res["gbps_by_blocks_per_cu"] = best
     res["gbps"] = max(best.values())
     return res
@@ -101,20 +101,30 @@ def main(argv=None) -> int:
     ap.add_argument("--shared", action="store_true")
     ap.add_argument("--window-s", type=float, default=3.0)
     ap.add_argument("--blocks-per-cu", type=int, default=8)
+    ap.add_argument("--gib", type=int, default=4,
+                    help="working set per process in GiB (a decode slice streams ~20 GiB per step)")
+    ap.add_argument("--shared-bpc", type=int, default=0,
+                    help="blocks per CU in the shared rows (0 = the best single-process value)")
+    ap.add_argument("--shared-only", default="", help="comma list of process counts: only these shared rows")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     if a.child:
         print(json.dumps(child(a)), flush=True)
         return 0
-    doc = {"single": {}, "shared": {}}
+    doc = {"single": {}, "shared": {}, "gib_per_process": a.gib}
+    counts = [int(x) for x in a.shared_only.split(",") if x] or [2, 4, 8]
     for cus in (256, 128, 64, 32):
-        r = _collect(_spawn(None if cus == 256 else _mask(cus), []))
+        if a.shared_only and 256 // cus not in counts:
+            continue
+        r = _collect(_spawn(None if cus == 256 else _mask(cus), ["--gib", str(a.gib)]))
         doc["single"][cus] = r
         print(f"single {cus:3d} CUs: {r['gbps']:.0f} GB/s {r['gbps_by_blocks_per_cu']}", flush=True)
-    for n in (2, 4, 8):
+    for n in counts:
         cus = 256 // n
-        bpc = max(doc["single"][cus]["gbps_by_blocks_per_cu"], key=doc["single"][cus]["gbps_by_blocks_per_cu"].get)
-        ps = [_spawn(_mask(cus, i), ["--shared", "--window-s", str(a.window_s), "--blocks-per-cu", str(bpc)])
+        bpc = a.shared_bpc or max(doc["single"][cus]["gbps_by_blocks_per_cu"],
+                                  key=doc["single"][cus]["gbps_by_blocks_per_cu"].get)
+        ps = [_spawn(_mask(cus, i), ["--shared", "--window-s", str(a.window_s), "--blocks-per-cu", str(bpc),
+                                     "--gib", str(a.gib)])
               for i in range(n)]
         for p in ps:                          # every child initialised and warm
             line = p.stdout.readline()
@@ -127,7 +137,7 @@ def main(argv=None) -> int:
         rs = [_collect(p) for p in ps]
         span = max(r["t1"] for r in rs) - min(r["t0"] for r in rs)
         agg = sum(r["bytes"] for r in rs) / span / 1e9
-        doc["shared"][n] = {"cus_each": cus, "per_process_gbps": [round(r["gbps"], 1) for r in rs],
+        doc["shared"][n] = {"cus_each": cus, "blocks_per_cu": int(bpc), "per_process_gbps": [round(r["gbps"], 1) for r in rs],
                             "aggregate_gbps": round(agg, 1)}
         print(f"shared {n} x {cus} CUs: aggregate {agg:.0f} GB/s, each {[round(r['gbps']) for r in rs]}",
               flush=True)

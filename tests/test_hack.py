@@ -44,3 +44,31 @@ def test_native_check_flags_cuda_isms(tmp_path, monkeypatch):
     monkeypatch.setattr(V, "ROOT", tmp_path)
     errs = V.check_native()
     assert len(errs) == 2 and "platform branch" in errs[0] and "warp-32" in errs[1], errs
+
+
+def test_pmcsum_merges_passes_and_scales_fetch(tmp_path):
+    """utils/pmcsum: per-kernel means over --pmc passes, FETCH_SIZE doubled
+    (gfx950 tallies 128-B requests at 64 B), bandwidth from each pass's times."""
+    from k8s_vgpu_scheduler_amd.utils import pmcsum
+
+    hdr = ('"Correlation_Id","Dispatch_Id","Agent_Id","Queue_Id","Process_Id","Thread_Id","Grid_Size","Kernel_Id",'
+           '"Kernel_Name","Workgroup_Size","LDS_Block_Size","Scratch_Size","VGPR_Count","Accum_VGPR_Count",'
+           '"SGPR_Count","Counter_Name","Counter_Value","Start_Timestamp","End_Timestamp"\n')
+
+    def row(d, name, cn, v, t0, t1):
+        return f'{d},{d},"Agent 2",1,1,1,64,1,"{name}",64,0,0,8,0,8,"{cn}",{v},{t0},{t1}\n'
+
+    a = tmp_path / "a.csv"
+    a.write_text(hdr + row(1, "void gemm_kernel<1>(float*)", "FETCH_SIZE", 1000.0, 0, 1000)
+                 + row(2, "void gemm_kernel<1>(float*)", "FETCH_SIZE", 1000.0, 5000, 6000)
+                 + row(3, "void at::native::fill(float*)", "FETCH_SIZE", 9.0, 0, 10))
+    b = tmp_path / "b.csv"
+    b.write_text(hdr + row(1, "void gemm_kernel<1>(float*)", "SQ_WAVES", 64.0, 0, 3000)
+                 + row(2, "void gemm_kernel<1>(float*)", "SQ_WAVES", 32.0, 0, 1000))
+    rows = pmcsum.summarise(pmcsum.load([str(a), str(b)]))
+    assert [r["kernel"] for r in rows] == ["gemm_kernel<1>"]          # one-off init kernels dropped
+    r = rows[0]
+    assert r["dispatches"] == 2 and r["SQ_WAVES"] == 48.0 and r["FETCH_SIZE"] == 1000.0
+    assert r["read_MB"] == round(2 * 1000 * 1024 / 1e6, 2)
+    assert r["read_GBps"] == round(2 * 2000 * 1024 / 2000, 1)          # bytes / ns over pass a only
+    assert "| gemm_kernel<1> | 2 |" in pmcsum.to_markdown(rows)
