@@ -110,3 +110,22 @@ def test_metrics_series_and_labels(tmp_path):
     assert 'hami_host_gpu_memory_used_bytes{device_index="0",device_type="AMD Instinct MI355X",device_uuid="GPU-0000",node="node1"} 1.073741824e+09' in text
     assert "hami_container_last_kernel_elapsed_seconds" in text
     assert "mivgpu_container_throttled_seconds_total" in text
+
+
+def test_context_bytes_split_out_of_the_usage(tmp_path):
+    """Runtime VRAM the shim charges as context shows in hami_vgpu_memory_context_bytes,
+    inside the used total, and not in the buffer series."""
+    r = make_container(tmp_path, "u2", "main", uuid="GPU-0002", used=0, limit=4 << 30)
+    p = r.r.procs[0]
+    p.used[0].buffer, p.used[0].context = 1 << 30, 490 << 20
+    p.used[0].total = (1 << 30) + (490 << 20)
+    r.close()
+    lister = ContainerLister(str(tmp_path), lambda: [pod("u2", "p2", "ns2")])
+    lister.update()
+    reg = CollectorRegistry()
+    reg.register(MonitorCollector(lister, FakeBackend(n=1), "node1"))
+    text = generate_latest(reg).decode()
+    lab = '{container="main",device_uuid="GPU-0002",namespace="ns2",pod="p2",vdevice_index="0"}'
+    assert f"hami_vgpu_memory_context_bytes{lab} 5.1380224e+08" in text
+    assert f"hami_vgpu_memory_buffer_bytes{lab} 1.073741824e+09" in text
+    assert f"hami_vgpu_memory_used_bytes{lab} 1.587544064e+09" in text
