@@ -246,6 +246,7 @@ struct Config {
   bool oversubscribe = false;
   bool disabled = false;
   bool account_context = true;  // count runtime/code-object VRAM (KFD per-process view) in the quota
+  uint64_t context_refresh_ns = 20000000;  // at most one KFD read per 20 ms (forced before an OOM)
   char kfd_sysfs[256] = "/sys/class/kfd/kfd";
   uint64_t gate_min_interval_ns = 200000;  // >= 200 us of host submission per gate
   int64_t gate_cap_ns = 20000000;          // 20 ms burst
@@ -334,6 +335,8 @@ void load_config() {
   g_cfg.oversubscribe = ov && (!strcmp(ov, "1") || !strcasecmp(ov, "true"));
   const char* ac = getenv("MIVGPU_ACCOUNT_CONTEXT");
   g_cfg.account_context = !(ac && (!strcmp(ac, "0") || !strcasecmp(ac, "false")));
+  const char* crm = getenv("MIVGPU_CONTEXT_REFRESH_MS");
+  if (crm && *crm) g_cfg.context_refresh_ns = (uint64_t)atoll(crm) * 1000000ull;
   const char* kfd = getenv("MIVGPU_KFD_SYSFS");
   if (kfd && *kfd) snprintf(g_cfg.kfd_sysfs, sizeof(g_cfg.kfd_sysfs), "%s", kfd);
   const char* gi = getenv("MIVGPU_GATE_INTERVAL_US");
@@ -740,25 +743,28 @@ int probe_kfd_pid(int gpu_id) {
   return -1;
 }
 
-void refresh_context(int dev, bool force) {
-  if (!g_cfg.account_context || !g_region || g_slot < 0 || dev < 0 || dev >= MIVGPU_MAX_DEVICES) return;
+// Returns true when the context charge went down (a forced refresh before an
+// OOM verdict: the charge read between a hooked free's accounting and the real
+// free can briefly count the freed buffer as context).
+bool refresh_context(int dev, bool force) {
+  if (!g_cfg.account_context || !g_region || g_slot < 0 || dev < 0 || dev >= MIVGPU_MAX_DEVICES) return false;
   std::lock_guard<std::mutex> lk(g_ctx_mu);
   CtxDev& c = g_ctx[dev];
   uint64_t now = coarse_ns();
-  if (c.gpu_id == -1 || (!force && c.last_ns && now - c.last_ns < 20000000ull)) return;
+  if (c.gpu_id == -1 || (!force && c.last_ns && now - c.last_ns < g_cfg.context_refresh_ns)) return false;
   c.last_ns = now;
   if (c.gpu_id == -2) {
     c.gpu_id = resolve_kfd_gpu_id(dev);
     if (c.gpu_id < 0) {
       mlog(3, "device %d: no KFD node matched; runtime VRAM not charged to the quota", dev);
-      return;
+      return false;
     }
   }
   mivgpu_proc_slot_t* s = &g_region->procs[g_slot];
   int pid = __atomic_load_n(&s->hostpid, __ATOMIC_RELAXED);  // the monitor's mapping wins
   if (pid <= 0) {
     if (c.kfd_pid == -2) {
-      if (g_captures.load(std::memory_order_acquire) > 0) return;
+      if (g_captures.load(std::memory_order_acquire) > 0) return false;
       c.kfd_pid = probe_kfd_pid(c.gpu_id);
       if (c.kfd_pid < 0) {
         mlog(3, "device %d: own KFD process entry not identified; runtime VRAM not charged", dev);
@@ -769,16 +775,16 @@ void refresh_context(int dev, bool force) {
     }
     pid = c.kfd_pid;
   }
-  if (pid <= 0) return;
+  if (pid <= 0) return false;
   char path[512];
   uint64_t vram = 0;
   snprintf(path, sizeof(path), "%s/proc/%d/vram_%d", g_cfg.kfd_sysfs, pid, c.gpu_id);
-  if (!read_u64_file(path, &vram)) return;
+  if (!read_u64_file(path, &vram)) return false;
   mivgpu_mem_t* m = &s->used[dev];
   uint64_t hooked = __atomic_load_n(&m->buffer, __ATOMIC_RELAXED) + __atomic_load_n(&m->vmm, __ATOMIC_RELAXED);
   uint64_t ctx = vram > hooked ? vram - hooked : 0;
   uint64_t old = __atomic_exchange_n(&m->context, ctx, __ATOMIC_RELAXED);
-  if (ctx == old) return;
+  if (ctx == old) return false;
   if (ctx > old) {
     uint64_t d = ctx - old;
     __atomic_fetch_add(&g_region->dev_used[dev], d, __ATOMIC_RELAXED);
@@ -786,11 +792,12 @@ void refresh_context(int dev, bool force) {
     uint64_t pk = __atomic_load_n(&m->peak, __ATOMIC_RELAXED);
     while (t > pk && !__atomic_compare_exchange_n(&m->peak, &pk, t, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
     }
-  } else {
-    uint64_t d = old - ctx;
-    __atomic_fetch_sub(&g_region->dev_used[dev], d, __ATOMIC_RELAXED);
-    __atomic_fetch_sub(&m->total, d, __ATOMIC_RELAXED);
+    return false;
   }
+  uint64_t d = old - ctx;
+  __atomic_fetch_sub(&g_region->dev_used[dev], d, __ATOMIC_RELAXED);
+  __atomic_fetch_sub(&m->total, d, __ATOMIC_RELAXED);
+  return true;
 }
 
 // Reserve `bytes` on `dev` against the quota before calling the real
@@ -813,11 +820,12 @@ bool reserve(int dev, uint64_t bytes, AllocKind kind) {
         return true;
       }
     }
-    if (attempt == 0) {  // maybe a dead process still holds quota
+    if (attempt == 0) {  // a dead process may still hold quota, or our context charge be stale
       lock_region();
       int n = reclaim_dead_locked();
       unlock_region();
-      if (n == 0) break;
+      bool shrank = refresh_context(dev, true);
+      if (n == 0 && !shrank) break;
     }
   }
   tmark("mivgpu:oom dev=%d req_mib=%llu used_mib=%llu limit_mib=%llu", dev, (unsigned long long)(bytes >> 20),

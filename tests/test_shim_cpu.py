@@ -267,3 +267,15 @@ def test_runtime_vram_accounting_off_or_unresolvable(native_build, tmp_path):
     out = run(native_build, tmp_path, "alloc", 1000, "meminfo",
               env={"HIP_DEVICE_MEMORY_LIMIT_0": "4096m", "MIVGPU_KFD_SYSFS": str(kfd)}, cache="b.cache")
     assert out[1]["free_mib"] == 3096
+
+
+def test_stale_context_charge_is_refreshed_before_oom(native_build, tmp_path):
+    """With refreshes rate-limited, a context charge that has since shrunk must
+    not cause an OOM: the shim re-reads KFD before denying an allocation."""
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
+    env = dict(_kfd_env(kfd), MIVGPU_CONTEXT_REFRESH_MS="600000")
+    out = run(native_build, tmp_path, "kfdctx", 2000, "alloc", 1000, "kfdctx", 0, "alloc", 2500, "usage",
+              env=env, cache="stale.cache")
+    assert out[1]["rc"] == 0
+    assert out[3]["rc"] == 0                              # 2000 stale + 1000 + 2500 > 4096, fresh 0 + 3500 fits
+    assert out[4]["bytes"] == 3500 << 20

@@ -72,3 +72,31 @@ def test_sanitized_stress(kind, tmp_path):
         assert rc == 0 and res is not None, err[-2000:]
         assert res["errors"] == 0 and res["usage_after"] == 0, res
     _check_region_clean(cache)
+
+
+@pytest.mark.parametrize("kind", ["plain", "thread"])
+def test_stress_with_runtime_vram_accounting(kind, native_build, tmp_path):
+    """Concurrent alloc/free with the KFD context accounting active (the mock
+    runtime publishes its per-process VRAM file): no sanitizer reports, no
+    errors, and the shared region is clean once every process has exited."""
+    from tests.test_shim_cpu import _fake_kfd
+
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
+    env = {"MIVGPU_KFD_SYSFS": str(kfd), "MOCKHIP_KFD_SYSFS": str(kfd), "MOCKHIP_KFD_GPU_ID": "4242",
+           "MIVGPU_CONTEXT_REFRESH_MS": "1",
+           "TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1:report_signal_unsafe=0"}
+    if kind == "plain":
+        driver, shim, extra = native_build["driver"], native_build["shim"], ()
+    else:
+        try:
+            b = build.build_sanitized(kind)
+        except RuntimeError as e:
+            pytest.skip(f"{kind} sanitizer build unavailable: {e}")
+        driver, shim, extra = b["driver"], b["shim"], (b["runtime"],)
+    cache = tmp_path / "k.cache"
+    outs = _stress(driver, shim, cache, procs=2, threads=4, iters=200, preload_extra=extra, extra_env=env)
+    for rc, res, err in outs:
+        assert "WARNING: ThreadSanitizer" not in err, err[-4000:]
+        assert rc == 0 and res is not None, err[-2000:]
+        assert res["errors"] == 0 and res["allocs"] > 0, res
+    _check_region_clean(cache)
