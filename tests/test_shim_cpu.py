@@ -279,3 +279,35 @@ def test_stale_context_charge_is_refreshed_before_oom(native_build, tmp_path):
     assert out[1]["rc"] == 0
     assert out[3]["rc"] == 0                              # 2000 stale + 1000 + 2500 > 4096, fresh 0 + 3500 fits
     assert out[4]["bytes"] == 3500 << 20
+
+
+def _board(path):
+    import struct
+    raw = open(path, "rb").read()
+    return [struct.unpack_from("<QQ", raw, 16 * i) for i in range(len(raw) // 16)]
+
+
+def test_share_board_counts_tenants_per_physical_gpu(native_build, tmp_path):
+    """Every shimmed process stamps its launches into one board per physical
+    GPU (PCI location) in the node-wide lock dir; slots are released at exit."""
+    lock = tmp_path / "vgpulock"
+    e = dict(os.environ, MOCKHIP_TOTAL_MIB="65536", LD_PRELOAD=str(native_build["shim"]), MIVGPU_LOCK_DIR=str(lock))
+    ps = []
+    for i in range(3):
+        env = dict(e, MIVGPU_SHARED_CACHE=str(tmp_path / f"t{i}.cache"))   # three containers
+        ps.append(subprocess.Popen([str(native_build["driver"]), "launch", "3", "sleep", "2500"], env=env,
+                                   stdout=subprocess.PIPE, text=True))
+    for p in ps:
+        json.loads(p.stdout.readline())
+    board = lock / "mivgpu-board-0000-75-00"          # the mock's device 0: domain 0, bus 0x75, device 0
+    slots = [s for s in _board(board) if s[0]]
+    assert len(slots) == 3 and len({t for t, _ in slots}) == 3
+    assert max(t for _, t in slots) - min(t for _, t in slots) < 2 * 10 ** 9
+    for p in ps:
+        p.wait(timeout=30)
+    assert [s for s in _board(board) if s[0]] == []  # released at exit
+    # opt-out: no board
+    lock2 = tmp_path / "lock2"
+    run(native_build, tmp_path, "launch", 2, env={"MIVGPU_LOCK_DIR": str(lock2), "MIVGPU_SHARE_BOARD": "0"},
+        cache="o.cache")
+    assert not lock2.exists() or not any(lock2.iterdir())

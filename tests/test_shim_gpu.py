@@ -192,3 +192,27 @@ def test_roctx_markers_on_rocprofv3_timeline(tmp):
     assert any(m.startswith("mivgpu:oom dev=0 req_mib=5000") for m in msgs), msgs[:20]
     names = [row.get("Kernel_Name", "") for f in kernels for row in csv.DictReader(open(f))]
     assert any("mivgpu_gate" in n for n in names)
+
+
+def _bench(args, timeout=240):
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+def test_governor_share_board_under_concurrency(tmp):
+    """Two 50 % tenants under the temporal governor on one GPU: with the
+    cross-tenant board each is refilled for the GPU time it actually gets
+    (wall time / tenants), so together they are not throttled to half the GPU."""
+    common = ["--slices", "2", "--no-spatial", "--policy", "force", "--mode", "shim", "--steps", "40",
+              "--warmup", "5"]
+    on = _bench(common)
+    off = _bench(common + ["--child-env", "MIVGPU_SHARE_BOARD=0"])
+    print(json.dumps({"board": on["value"], "no_board": off["value"], "fairness": on["slice_fairness_min_over_max"]}))
+    assert on["value"] > 1.3 * off["value"]
+    assert on["slice_fairness_min_over_max"] > 0.8
