@@ -208,11 +208,26 @@ def _bench(args, timeout=240):
 def test_governor_share_board_under_concurrency(tmp):
     """Two 50 % tenants under the temporal governor on one GPU: with the
     cross-tenant board each is refilled for the GPU time it actually gets
-    (wall time / tenants), so together they are not throttled to half the GPU."""
-    common = ["--slices", "2", "--no-spatial", "--policy", "force", "--mode", "shim", "--steps", "40",
-              "--warmup", "5"]
-    on = _bench(common)
-    off = _bench(common + ["--child-env", "MIVGPU_SHARE_BOARD=0"])
-    print(json.dumps({"board": on["value"], "no_board": off["value"], "fairness": on["slice_fairness_min_over_max"]}))
-    assert on["value"] > 1.3 * off["value"]
+    (wall time / tenants), so together they run like two unthrottled slices
+    instead of being held to half the GPU (without the board: 4.2-6.0k vs
+    8.0k tok/s, profiles/governor_board/)."""
+    common = ["--slices", "2", "--no-spatial", "--mode", "shim", "--steps", "40", "--warmup", "5"]
+    free = _bench(common)
+    on = _bench(common + ["--policy", "force"])
+    print(json.dumps({"board": on["value"], "unthrottled": free["value"],
+                      "fairness": on["slice_fairness_min_over_max"]}))
+    assert on["value"] >= 0.85 * free["value"]
     assert on["slice_fairness_min_over_max"] > 0.8
+
+
+def test_governor_holds_graph_decode_to_its_limit(tmp):
+    """A hipGraph decode slice under the temporal governor at 50 % runs at about
+    half its unthrottled rate, also with the host far ahead of the GPU (queue
+    backpressure: launch calls in flight must not be mistaken for idleness)."""
+    common = ["--slices", "1", "--mode", "shim", "--steps", "150", "--warmup", "5"]
+    full = _bench(common)
+    half = _bench(common + ["--child-env", "HIP_DEVICE_CORE_LIMIT=50",
+                            "--child-env", "GPU_CORE_UTILIZATION_POLICY=force"])
+    ratio = half["value"] / full["value"]
+    print(json.dumps({"full": full["value"], "half": half["value"], "ratio": round(ratio, 3)}))
+    assert 0.42 <= ratio <= 0.58, ratio
