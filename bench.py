@@ -208,6 +208,7 @@ def main():
             "per_slice_tok_s_rank0": per_slice,
             "slice_fairness_min_over_max": round(min(per_slice) / max(per_slice), 3) if per_slice else None,
             "slice_mem_total_mib": [rd["mem_total_mib"] for rd in head["ready"]],
+            "slice_runtime_vram_charged_mib": [rd.get("context_mib") for rd in head["ready"]],
             "tpot_ms_p50_rank0": [round(d.get("tpot_ms_p50", 0), 3) for d in head["done"]],
             "tpot_ms_p99_rank0": [round(d.get("tpot_ms_p99", 0), 3) for d in head["done"]],
         }

@@ -736,7 +736,10 @@ int probe_kfd_pid(int gpu_id) {
     }
     closedir(d);
     if (before.empty()) return -1;
-    const uint64_t probe = (64ull + 6ull * (uint64_t)attempt) << 20;
+    // per-process sizes (64-298 MiB in 6 MiB steps): tenants that start
+    // together and probe at the same instant still see distinct deltas
+    const uint64_t seed = (mono_ns() >> 10) ^ ((uint64_t)getpid() * 0x9E3779B97F4A7C15ull);
+    const uint64_t probe = (64ull + 6ull * ((seed + 17ull * (uint64_t)attempt) % 40ull)) << 20;
     void* p = nullptr;
     if (real_hipMalloc()(&p, probe) != hipSuccess || !p) return -1;
     int found = -1, hits = 0;

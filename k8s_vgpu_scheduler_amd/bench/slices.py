@@ -175,6 +175,16 @@ def child_main(argv):
              "mem_free_mib": free >> 20, "allocated_mib": torch.cuda.memory_allocated() >> 20,
              "cus": torch.cuda.get_device_properties(0).multi_processor_count,
              "preload": os.environ.get("LD_PRELOAD", ""), "cu_mask": os.environ.get("HSA_CU_MASK", "")}
+    cache = os.environ.get("MIVGPU_SHARED_CACHE")
+    if cache and os.environ.get("LD_PRELOAD") and os.path.exists(cache):
+        # what the shim charged beyond the hooked allocations (runtime VRAM)
+        from k8s_vgpu_scheduler_amd.monitor.region import SharedRegion
+
+        reg = SharedRegion(cache, writable=False)
+        me = [p for p in reg.active_procs() if p.pid == os.getpid()]
+        ready["context_mib"] = (me[0].used[0].context >> 20) if me else None
+        ready["kfd_entry_found"] = bool(me and me[0].hostpid)
+        reg.close()
     print("READY " + json.dumps(ready), flush=True)
     if sys.stdin.readline().strip() != "GO":
         return 0
