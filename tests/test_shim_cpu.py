@@ -311,3 +311,26 @@ def test_share_board_counts_tenants_per_physical_gpu(native_build, tmp_path):
     run(native_build, tmp_path, "launch", 2, env={"MIVGPU_LOCK_DIR": str(lock2), "MIVGPU_SHARE_BOARD": "0"},
         cache="o.cache")
     assert not lock2.exists() or not any(lock2.iterdir())
+
+
+def test_share_board_reclaims_silent_slots(native_build, tmp_path):
+    """A full board whose slots all went silent long ago (crashed tenants that
+    never released them): a new tenant takes one over, and frees it at exit."""
+    import struct
+
+    lock = tmp_path / "vgpulock"
+    lock.mkdir()
+    board = lock / "mivgpu-board-0000-75-00"
+    board.write_bytes(b"".join(struct.pack("<QQ", 1000 + i, 1) for i in range(64)))   # stamped at t = 1 ns
+    e = dict(os.environ, MOCKHIP_TOTAL_MIB="65536", LD_PRELOAD=str(native_build["shim"]), MIVGPU_LOCK_DIR=str(lock),
+             MIVGPU_SHARED_CACHE=str(tmp_path / "r.cache"))
+    p = subprocess.Popen([str(native_build["driver"]), "launch", "2", "sleep", "2000"], env=e, stdout=subprocess.PIPE,
+                         text=True)
+    json.loads(p.stdout.readline())
+    slots = _board(board)
+    fresh = [i for i, (tok, last) in enumerate(slots) if last > 1]
+    assert len(fresh) == 1 and slots[fresh[0]][0] not in range(1000, 1064)   # one stale slot taken over
+    p.wait(timeout=30)
+    slots = _board(board)
+    assert slots[fresh[0]][0] == 0                                          # released at exit
+    assert sum(1 for tok, _ in slots if tok) == 63                           # the other stale slots untouched
