@@ -233,6 +233,7 @@ REAL_DECL(hipError_t, hipStreamBeginCapture, "hip_4.3", (hipStream_t, hipStreamC
 REAL_DECL(hipError_t, hipStreamBeginCapture_spt, "hip_5.3", (hipStream_t, hipStreamCaptureMode))
 REAL_DECL(hipError_t, hipStreamEndCapture, "hip_4.3", (hipStream_t, hipGraph_t*))
 REAL_DECL(hipError_t, hipStreamEndCapture_spt, "hip_5.3", (hipStream_t, hipGraph_t*))
+REAL_DECL(hipError_t, hipDeviceGetPCIBusId, "hip_4.2", (char*, int, int))
 REAL_DECL(hipError_t, hipSetDevice, "hip_4.2", (int))
 REAL_DECL(hipError_t, hipMemset, "hip_4.2", (void*, int, size_t))
 
@@ -847,17 +848,27 @@ BoardSlot* board_map(int dev) {
   std::lock_guard<std::mutex> lk(g_board_mu);
   st = b.state.load(std::memory_order_acquire);
   if (st != 0) return st > 0 ? b.slots : nullptr;
-  int bus = 0, slot = 0, domain = 0;
-  bool ok = g_cfg.share_board && real_hipDeviceGetAttribute() &&
-            real_hipDeviceGetAttribute()(&bus, hipDeviceAttributePciBusId, dev) == hipSuccess &&
-            real_hipDeviceGetAttribute()(&slot, hipDeviceAttributePciDeviceId, dev) == hipSuccess &&
-            real_hipDeviceGetAttribute()(&domain, hipDeviceAttributePciDomainId, dev) == hipSuccess;
+  // One board per GPU (per compute partition: the PCI function), named by its
+  // PCI location -- container-local device indices differ between tenants.
+  unsigned domain = 0, bus = 0, slot = 0, fn = 0;
+  bool ok = false;
+  if (g_cfg.share_board) {
+    char id[64] = {0};
+    if (real_hipDeviceGetPCIBusId() && real_hipDeviceGetPCIBusId()(id, (int)sizeof(id) - 1, dev) == hipSuccess)
+      ok = sscanf(id, "%x:%x:%x.%x", &domain, &bus, &slot, &fn) == 4;
+    int b = 0, d = 0, dm = 0;
+    if (!ok && real_hipDeviceGetAttribute() &&
+        real_hipDeviceGetAttribute()(&b, hipDeviceAttributePciBusId, dev) == hipSuccess &&
+        real_hipDeviceGetAttribute()(&d, hipDeviceAttributePciDeviceId, dev) == hipSuccess &&
+        real_hipDeviceGetAttribute()(&dm, hipDeviceAttributePciDomainId, dev) == hipSuccess) {
+      domain = (unsigned)dm, bus = (unsigned)b, slot = (unsigned)d, fn = 0;
+      ok = true;
+    }
+  }
   if (ok) {
-    // one board per physical GPU, named by its PCI location (container-local
-    // device indices differ between tenants)
     char path[512];
     mkdir(g_cfg.lock_dir, 0777);
-    snprintf(path, sizeof(path), "%s/mivgpu-board-%04x-%02x-%02x", g_cfg.lock_dir, domain, bus, slot);
+    snprintf(path, sizeof(path), "%s/mivgpu-board-%04x-%02x-%02x-%x", g_cfg.lock_dir, domain, bus, slot, fn);
     int fd = open(path, O_RDWR | O_CREAT | O_CLOEXEC, 0666);
     if (fd >= 0) {
       (void)fchmod(fd, 0666);

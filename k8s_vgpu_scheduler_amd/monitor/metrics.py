@@ -12,6 +12,8 @@ import time
 
 from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily
 
+from .board import active_tenants, board_path
+
 CTR_LABELS = ["namespace", "pod", "container", "vdevice_index", "device_uuid"]
 
 
@@ -29,14 +31,20 @@ class MonitorCollector:
         host_mc = GaugeMetricFamily("hami_host_gpu_memory_controller_utilization_ratio",
                                     "GPU memory controller utilization ratio (0-100)",
                                     labels=["device_index", "device_uuid", "device_type"])
+        tenants = GaugeMetricFamily("mivgpu_host_gpu_active_tenants",
+                                    "Shimmed processes that launched work on the GPU in the last second "
+                                    "(the governor's share board)", labels=["node", "device_index", "device_uuid"])
         if self.backend is not None:
             for g in self.backend.gpus():
+                bp = board_path(g.bdf) if g.bdf else None
+                if bp is not None and bp.exists():
+                    tenants.add_metric([self.node, str(g.index), g.uuid], float(active_tenants(bp)))
                 u = self.backend.utilization(g)
                 host_mem.add_metric([self.node, str(g.index), g.uuid, g.name],
                                     float(self.backend.memory_used_mib(g)) * 1024 * 1024)
                 host_util.add_metric([self.node, str(g.index), g.uuid, g.name], float(u.get("gfx", 0)))
                 host_mc.add_metric([str(g.index), g.uuid, g.name], float(u.get("umc", 0)))
-        yield from (host_mem, host_util, host_mc)
+        yield from (host_mem, host_util, host_mc, tenants)
 
         used = GaugeMetricFamily("hami_vgpu_memory_used_bytes", "vGPU device memory usage in bytes", labels=CTR_LABELS)
         limit = GaugeMetricFamily("hami_vgpu_memory_limit_bytes", "vGPU device memory limit in bytes",

@@ -129,3 +129,27 @@ def test_context_bytes_split_out_of_the_usage(tmp_path):
     assert f"hami_vgpu_memory_context_bytes{lab} 5.1380224e+08" in text
     assert f"hami_vgpu_memory_buffer_bytes{lab} 1.073741824e+09" in text
     assert f"hami_vgpu_memory_used_bytes{lab} 1.587544064e+09" in text
+
+
+def test_active_tenants_from_the_share_board(tmp_path, monkeypatch):
+    """mivgpu_host_gpu_active_tenants counts board slots stamped in the last second."""
+    import struct
+
+    from k8s_vgpu_scheduler_amd.monitor import board as B
+
+    monkeypatch.setenv("MIVGPU_LOCK_DIR", str(tmp_path / "lock"))
+    (tmp_path / "lock").mkdir()
+    be = FakeBackend(n=2)
+    g0 = be.gpus()[0]
+    path = B.board_path(g0.bdf)
+    assert path.name == "mivgpu-board-0000-11-00-0"
+    now = B.now_ns()
+    slots = [(7, now - 10 ** 8), (8, now - 5 * 10 ** 8), (9, now - 5 * 10 ** 9), (0, now)] + [(0, 0)] * 60
+    path.write_bytes(b"".join(struct.pack("<QQ", t, l) for t, l in slots))
+    assert B.active_tenants(path, at_ns=now) == 2
+    lister = ContainerLister(str(tmp_path), lambda: [])
+    reg = CollectorRegistry()
+    reg.register(MonitorCollector(lister, be, "node1"))
+    text = generate_latest(reg).decode()
+    assert 'mivgpu_host_gpu_active_tenants{device_index="0",device_uuid="GPU-0000",node="node1"} 2.0' in text
+    assert 'device_index="1"' not in text.split("mivgpu_host_gpu_active_tenants")[-1]   # no board, no series

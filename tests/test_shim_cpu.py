@@ -299,7 +299,7 @@ def test_share_board_counts_tenants_per_physical_gpu(native_build, tmp_path):
                                    stdout=subprocess.PIPE, text=True))
     for p in ps:
         json.loads(p.stdout.readline())
-    board = lock / "mivgpu-board-0000-75-00"          # the mock's device 0: domain 0, bus 0x75, device 0
+    board = lock / "mivgpu-board-0000-75-00-0"          # the mock's device 0: domain 0, bus 0x75, device 0
     slots = [s for s in _board(board) if s[0]]
     assert len(slots) == 3 and len({t for t, _ in slots}) == 3
     assert max(t for _, t in slots) - min(t for _, t in slots) < 2 * 10 ** 9
@@ -320,7 +320,7 @@ def test_share_board_reclaims_silent_slots(native_build, tmp_path):
 
     lock = tmp_path / "vgpulock"
     lock.mkdir()
-    board = lock / "mivgpu-board-0000-75-00"
+    board = lock / "mivgpu-board-0000-75-00-0"
     board.write_bytes(b"".join(struct.pack("<QQ", 1000 + i, 1) for i in range(64)))   # stamped at t = 1 ns
     e = dict(os.environ, MOCKHIP_TOTAL_MIB="65536", LD_PRELOAD=str(native_build["shim"]), MIVGPU_LOCK_DIR=str(lock),
              MIVGPU_SHARED_CACHE=str(tmp_path / "r.cache"))
