@@ -867,7 +867,7 @@ BoardSlot* board_map(int dev) {
   }
   if (ok) {
     char path[512];
-    mkdir(g_cfg.lock_dir, 0777);
+    if (mkdir(g_cfg.lock_dir, 0777) == 0) (void)chmod(g_cfg.lock_dir, 0777);   // shared by every tenant (umask)
     snprintf(path, sizeof(path), "%s/mivgpu-board-%04x-%02x-%02x-%x", g_cfg.lock_dir, domain, bus, slot, fn);
     int fd = open(path, O_RDWR | O_CREAT | O_CLOEXEC, 0666);
     if (fd >= 0) {
