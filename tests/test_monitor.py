@@ -153,3 +153,29 @@ def test_active_tenants_from_the_share_board(tmp_path, monkeypatch):
     text = generate_latest(reg).decode()
     assert 'mivgpu_host_gpu_active_tenants{device_index="0",device_uuid="GPU-0000",node="node1"} 2.0' in text
     assert 'device_index="1"' not in text.split("mivgpu_host_gpu_active_tenants")[-1]   # no board, no series
+
+
+def test_feedback_loop_fills_host_pids(tmp_path, monkeypatch):
+    """watch_and_feedback maps every new slot to its host pid on each pass."""
+    import threading
+
+    from k8s_vgpu_scheduler_amd.monitor import hostpid
+
+    uid = "11111111-2222-3333-4444-555555555555"
+    r = make_container(tmp_path, uid, "main")
+    r.r.procs[0].pid = 42
+    r.close()
+    monkeypatch.setattr(hostpid, "scan", lambda proc_root="/proc": [(90042, 42, f"0::/kubepods/pod{uid}/c\n")])
+    lister = ContainerLister(str(tmp_path), lambda: [pod(uid, "p")])
+    stop = threading.Event()
+    t = threading.Thread(target=feedback.watch_and_feedback, args=(lister, stop, 0.05), daemon=True)
+    t.start()
+    deadline = time.time() + 10
+    while time.time() < deadline:
+        cs = lister.list_containers()
+        if cs and cs[0].region.r.procs[0].hostpid == 90042:
+            break
+        time.sleep(0.05)
+    stop.set()
+    t.join(timeout=5)
+    assert lister.list_containers()[0].region.r.procs[0].hostpid == 90042
