@@ -23,6 +23,7 @@ mode, i.e. one HIP device per XCD), which is why the planner never promises it.
 
 from __future__ import annotations
 
+import functools
 from dataclasses import dataclass
 
 
@@ -79,8 +80,13 @@ def free_cus(used_bitmap: int, topo: CUTopology) -> int:
     return topo.total - bin(used_bitmap & ((1 << topo.total) - 1)).count("1")
 
 
+@functools.lru_cache(maxsize=64)
+def _granule_masks(topo: CUTopology) -> tuple[int, ...]:
+    return tuple(sum(1 << c for c in topo.granule_cus(k)) for k in range(topo.granules))
+
+
 def _granule_free(used_bitmap: int, topo: CUTopology, k: int) -> bool:
-    return all(not (used_bitmap >> c) & 1 for c in topo.granule_cus(k))
+    return not used_bitmap & _granule_masks(topo)[k]
 
 
 def pick(used_bitmap: int, n: int, topo: CUTopology) -> list[tuple[int, int]] | None:
@@ -91,7 +97,7 @@ def pick(used_bitmap: int, n: int, topo: CUTopology) -> list[tuple[int, int]] | 
     need = -(-n // topo.xcds)
     if need > topo.granules:
         return None
-    free = [k for k in range(topo.granules) if _granule_free(used_bitmap, topo, k)]
+    free = [k for k, m in enumerate(_granule_masks(topo)) if not used_bitmap & m]
     if len(free) < need:
         return None
     # runs of consecutive free granules

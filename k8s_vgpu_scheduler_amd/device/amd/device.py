@@ -377,6 +377,8 @@ class AMDDevices(D.Devices):
         return int(math.ceil(d.usedcores * 100 / total))
 
     def _fit_quota(self, pod, tmp: list, allocated: dict, uuid: str, memreq: int, cu: int, total: int) -> bool:
+        if not get_local_cache().fit_key(pod["metadata"].get("namespace", "default")):
+            return True     # no explicit limit in the namespace: skip the hypothetical collapse
         hypo = {t: [list(c) for c in single] for t, single in (allocated or {}).items()}
         cur = list(tmp) + [ContainerDevice(uuid=uuid, type=AMD_DEVICE, usedmem=memreq, usedcores=cu)]
         hypo.setdefault(AMD_DEVICE, []).append(cur)

@@ -51,6 +51,16 @@ class QuotaManager:
                 return False
         return True
 
+    def fit_key(self, ns: str) -> tuple:
+        """Everything ``fit_quota`` reads for ``ns``: () when the namespace has
+        no explicit limit (every fit passes), else the limited entries.  A
+        Filter result computed under one key is valid under an equal key."""
+        with self._mu:
+            dq = self.quotas.get(ns)
+            if not dq:
+                return ()
+            return tuple(sorted((k, q.used, q.limit) for k, q in dq.items() if q.limit_set))
+
     @staticmethod
     def _count(pd: dict) -> dict[str, int]:
         res: dict[str, int] = {}

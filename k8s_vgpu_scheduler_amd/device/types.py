@@ -90,7 +90,9 @@ class DeviceUsage:
                            usedmem=self.usedmem, totalmem=self.totalmem, totalcore=self.totalcore,
                            usedcores=self.usedcores, mode=self.mode, numa=self.numa, type=self.type,
                            health=self.health, pod_infos=list(self.pod_infos),
-                           custominfo=jcopy(self.custominfo))
+                           # values are replaced, never mutated in place (pair
+                           # scores, the cu_used bitmap): a shallow copy suffices
+                           custominfo=dict(self.custominfo))
 
 
 @dataclass

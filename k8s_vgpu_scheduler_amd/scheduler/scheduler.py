@@ -8,9 +8,20 @@ Reference: pkg/scheduler/scheduler.go:60-1209.  Behavioural contract kept:
     every node's registration annotation, checks backend health (handshake),
     cleans unhealthy/zero-device nodes and marks the cache ``synced``;
   * ``filter`` is idempotent per pod (take-and-delete previous reservation),
-    rebuilds per-device usage from ALL cached pods, scores every candidate,
-    picks the best node, patches ``hami.io/vgpu-node``/``-time`` plus backend
-    annotations and reserves the usage immediately;
+    scores every candidate, picks the best node, patches
+    ``hami.io/vgpu-node``/``-time`` plus backend annotations and reserves the
+    usage immediately;
+  * beyond the reference (which re-derives every node's usage from every pod
+    and scores nodes in goroutines, score.go:360-419): one usage view per
+    node, rebuilt only when that node's pods or registration change, and a
+    memo of per-node Fit results keyed by (node usage generation, the pod's
+    scheduling-relevant spec, the namespace's quota state).  Between two
+    Filters only the node that received the last pod changes, so a Filter
+    over N nodes re-fits ~1 node instead of N (Filter p99 at 100 nodes:
+    112-152 ms -> see profiles/scheduler_bench_100.json).  Nodes whose
+    device state is identical (every empty node of a fresh cluster) share one
+    Fit result under device-id renaming, so even a new pod shape fits once per
+    distinct node state, not once per node;
   * CA simulation (``Nodes`` given) touches no cache;
   * ``bind`` takes every backend's node lock transactionally (sorted, with
     rollback; PodGroup members retry until --node-lock-retry-timeout), marks
@@ -19,10 +30,12 @@ Reference: pkg/scheduler/scheduler.go:60-1209.  Behavioural contract kept:
 
 from __future__ import annotations
 
+import json
 import logging
 import os
 import threading
 import time
+from collections import OrderedDict
 
 from k8s_vgpu_scheduler_amd.device import codec
 from k8s_vgpu_scheduler_amd.device import devices as D
@@ -30,18 +43,19 @@ from k8s_vgpu_scheduler_amd.device.init_container import (app_containers_only_de
                                                           collapse_init_container_usage)
 from k8s_vgpu_scheduler_amd.device.pods import PodManager
 from k8s_vgpu_scheduler_amd.device.quota import get_local_cache
-from k8s_vgpu_scheduler_amd.device.types import DeviceUsage, NodeInfo
+from k8s_vgpu_scheduler_amd.device.types import DeviceUsage, NodeInfo, copy_pod_devices
 from k8s_vgpu_scheduler_amd.k8s.client import KubeClient, annotations, name_of, ns_of
 from k8s_vgpu_scheduler_amd.k8s.informer import Informer
 from k8s_vgpu_scheduler_amd.utils import nodelock, util
 from k8s_vgpu_scheduler_amd.utils import types as T
 from k8s_vgpu_scheduler_amd.utils.leaderelection import DummyLeaderManager, LeaderManager
+from k8s_vgpu_scheduler_amd.utils.weights import weights_for_pod
 
 from . import events as E
 from .config import SchedulerConfig
 from .nodes import NodeManager
-from .policy import DeviceListsScore, DeviceUsageList
-from .score import NodeUsage, calc_score
+from .policy import DeviceListsScore, DeviceUsageList, NodeScoreList
+from .score import NodeUsage, calc_score, record_result, resolve_node_policy, score_node_safe
 
 log = logging.getLogger(__name__)
 
@@ -54,6 +68,35 @@ def _decode_allocation(pod: dict) -> dict:
         key = getattr(dev, "CU_RANGES_ANNOS", None) or "hami.io/amd-cu-ranges"
         codec.attach_cu_ranges(single, annotations(pod).get(key))
     return raw
+
+
+# Annotations the scheduler / device plugin write as OUTPUT of a Filter or Bind;
+# they never influence Fit and are left out of the memo key.
+_OUTPUT_ANNOTATIONS = frozenset({T.ASSIGNED_NODE_ANNOTATION, T.ASSIGNED_TIME_ANNOTATION, T.BIND_TIME_ANNOTATION,
+                                 T.DEVICE_BIND_PHASE})
+_MEMO_MAX = 16384
+
+
+def _output_annotation(key: str) -> bool:
+    if key in _OUTPUT_ANNOTATIONS:
+        return True
+    if key in D.IN_REQUEST_DEVICES.values() or key in D.SUPPORT_DEVICES.values():
+        return True
+    return any(getattr(dev, "CU_RANGES_ANNOS", None) == key for dev in D.get_devices().values()) or \
+        key == "hami.io/amd-cu-ranges"
+
+
+def fit_signature(pod: dict) -> str:
+    """Everything of ``pod`` that Fit and the node score read: namespace,
+    per-container resources (+ init-container restart policy), annotations
+    other than the scheduler's own outputs."""
+    md = pod.get("metadata") or {}
+    spec = pod.get("spec") or {}
+    annos = {k: v for k, v in (md.get("annotations") or {}).items() if not _output_annotation(k)}
+    return json.dumps([md.get("namespace", "default"), annos,
+                       [c.get("resources") for c in spec.get("containers") or []],
+                       [(c.get("resources"), c.get("restartPolicy")) for c in spec.get("initContainers") or []]],
+                      sort_keys=True, default=str)
 
 
 class Scheduler:
@@ -76,6 +119,14 @@ class Scheduler:
                                         on_started=self._notify.set, on_stopped=self._lost_leadership)
         else:
             self.leader = DummyLeaderManager(True)
+        # node -> ((registration gen, pods gen), NodeUsage with policy-free device list)
+        self._usage_cache: dict[str, tuple[tuple, NodeUsage]] = {}
+        self._score_memo: OrderedDict = OrderedDict()
+        self._cache_mu = threading.Lock()
+        self.memo_hits = 0
+        self.memo_misses = 0
+        self.memo_class_hits = 0
+        self.memoize = True     # False: fit every candidate from scratch (tests compare the two)
         self.pods_inf = Informer(client, "pods")
         self.nodes_inf = Informer(client, "nodes")
         self.quota_inf = Informer(client, "resourcequotas")
@@ -292,9 +343,14 @@ class Scheduler:
             return {k: v.deepcopy() for k, v in self.overview.items()}
 
     # --------------------------------------------------------------- usage
-    def build_node_usage(self, info: NodeInfo, pod: dict | None) -> NodeUsage:
+    @staticmethod
+    def _pod_list_policy(pod: dict | None) -> tuple[str, bool]:
         policy = util.get_gpu_scheduler_policy_by_pod(D.gpu_scheduler_policy(), pod)
         numa = str(annotations(pod or {}).get("amd.com/numa-bind", "")).lower() in ("1", "t", "true")
+        return policy, numa
+
+    def build_node_usage(self, info: NodeInfo, pod: dict | None) -> NodeUsage:
+        policy, numa = self._pod_list_policy(pod)
         lst = DeviceUsageList([], policy, numa)
         for vendor_devs in info.devices.values():
             for d in vendor_devs:
@@ -307,17 +363,10 @@ class Scheduler:
                     pod_infos=[], custominfo=ci)))
         return NodeUsage(info.node, info, lst)
 
-    def get_nodes_usage(self, node_names: list | None, pod: dict | None):
-        overall: dict[str, NodeUsage] = {}
-        failed: dict[str, str] = {}
-        all_nodes = self.nodes.list_nodes()
-        for nid, info in all_nodes.items():
-            overall[nid] = self.build_node_usage(info, pod)
-        for p in self.pod_manager.list_pods_info():
-            usage = overall.get(p.node_id)
-            if usage is None:
-                continue
-            by_id = {dl.device.id: dl.device for dl in usage.devices.device_lists}
+    @staticmethod
+    def _apply_pods(usage: NodeUsage, pods) -> None:
+        by_id = {dl.device.id: dl.device for dl in usage.devices.device_lists}
+        for p in pods:
             for single in p.devices.values():
                 for ctr in single:
                     for cd in ctr:
@@ -334,15 +383,132 @@ class Scheduler:
                         if r:
                             from k8s_vgpu_scheduler_amd.device.amd.cu_alloc import bitmap_from_ranges
                             d.custominfo["cu_used"] = d.custominfo.get("cu_used", 0) | bitmap_from_ranges(r)
+
+    @staticmethod
+    def _shape(usage: NodeUsage) -> tuple[tuple, tuple]:
+        """(shape, device ids in list order).  Two nodes with equal shapes are
+        interchangeable for Fit up to renaming their device ids: same devices
+        in the same order, same usage, CU bitmaps, pair-score matrix (by
+        position) and cordons."""
+        devs = [dl.device for dl in usage.devices.device_lists]
+        pos = {d.id: i for i, d in enumerate(devs)}
+        from k8s_vgpu_scheduler_amd.device.amd.device import cordoned_devices
+        cordon = cordoned_devices(usage.node_info)
+        shape = tuple((d.index, d.type, d.count, d.totalmem, d.totalcore, d.mode, d.numa, d.health, d.used,
+                       d.usedmem, d.usedcores, d.custominfo.get("cu_used", 0), d.id in cordon,
+                       tuple(sorted((pos.get(k, -1), v) for k, v in (d.custominfo.get("pair_scores") or {}).items())))
+                      for d in devs)
+        return shape, tuple(d.id for d in devs)
+
+    def _cached_usage(self, node_id: str) -> tuple | None:
+        """(generation key, shared base usage, shape, device ids) of a registered
+        node, rebuilt only when its registration or its pods changed.  The
+        NodeUsage is shared: copy it before fitting into it."""
+        ref = self.nodes.get_node_ref(node_id)
+        if ref is None:
+            return None
+        ngen, info = ref
+        with self._cache_mu:
+            hit = self._usage_cache.get(node_id)
+        if hit is not None and hit[0] == (ngen, self.pod_manager.node_generation(node_id)):
+            return hit
+        pgen, pods = self.pod_manager.pods_on_node(node_id)
+        key = (ngen, pgen)
+        usage = self.build_node_usage(info, None)
+        self._apply_pods(usage, pods)
+        shape, ids = self._shape(usage)
+        entry = (key, usage, shape, ids)
+        with self._cache_mu:
+            self._usage_cache[node_id] = entry
+        return entry
+
+    @staticmethod
+    def _rename(hit: tuple, node_id: str, node: dict, src_ids: tuple, dst_ids: tuple) -> tuple:
+        """A class-memo result fitted on an equal-shaped node, moved to ``node_id``."""
+        sc, reason = hit
+        if sc is None:
+            return hit
+        m = dict(zip(src_ids, dst_ids))
+        devs = copy_pod_devices(sc.devices)
+        for single in devs.values():
+            for ctr in single:
+                for cd in ctr:
+                    cd.uuid = m.get(cd.uuid, cd.uuid)
+        return type(sc)(node_id, node, devs, sc.score), reason
+
+    def _usage_for_pod(self, base: NodeUsage, pod: dict | None) -> NodeUsage:
+        policy, numa = self._pod_list_policy(pod)
+        return NodeUsage(base.node, base.node_info,
+                         DeviceUsageList([DeviceListsScore(dl.device.deepcopy()) for dl in base.devices.device_lists],
+                                         policy, numa))
+
+    def get_nodes_usage(self, node_names: list | None, pod: dict | None):
+        overall: dict[str, NodeUsage] = {}
+        failed: dict[str, str] = {}
+        ids = self.nodes.node_ids()
+        for nid in ids:
+            c = self._cached_usage(nid)
+            if c is not None:
+                overall[nid] = self._usage_for_pod(c[1], pod)
+        with self._cache_mu:
+            for stale in [n for n in self._usage_cache if n not in overall]:
+                del self._usage_cache[stale]
         if node_names is None:
             return {}, overall, failed
         cache = {}
         for n in node_names:
-            if n not in all_nodes:
+            if n not in overall:
                 failed[n] = "node unregistered"
                 continue
             cache[n] = overall[n]
         return cache, overall, failed
+
+    def score_candidates(self, node_names: list, pod: dict, reqs: list):
+        """Fit ``pod`` on every candidate node; per-node results come from the
+        memo when neither the node nor the namespace quota changed since the
+        same pod shape was last fitted there.
+        -> (NodeScoreList, failure reasons, failed nodes)."""
+        weights = weights_for_pod(pod)
+        policy = resolve_node_policy(pod, self.cfg.node_scheduler_policy)
+        res = NodeScoreList(node_list=[], policy=policy)
+        failure: dict[str, list] = {}
+        failed: dict[str, str] = {}
+        sig = (fit_signature(pod), D.gpu_scheduler_policy(), self.cfg.node_scheduler_policy,
+               tuple(id(d) for d in D.get_devices().values()),   # a config reload re-creates the backends
+               self.quota_manager.fit_key((pod.get("metadata") or {}).get("namespace", "default")))
+        # UUID selectors name concrete devices: equal-shaped nodes stop being interchangeable
+        annos = annotations(pod)
+        by_class = not any(k in annos for k in ("amd.com/use-gpu-uuid", "amd.com/nouse-gpu-uuid"))
+        for n in node_names:
+            c = self._cached_usage(n)
+            if c is None:
+                failed[n] = "node unregistered"
+                continue
+            key = (n, c[0], sig)
+            ckey = (c[2], sig) if by_class else None
+            with self._cache_mu:
+                hit = self._score_memo.get(key)
+                if hit is not None:
+                    self._score_memo.move_to_end(key)
+                    self.memo_hits += 1
+                elif ckey is not None:
+                    tmpl = self._score_memo.get(ckey)
+                    if tmpl is not None:
+                        self._score_memo.move_to_end(ckey)
+                        hit = self._rename(tmpl[0], n, c[1].node, tmpl[1], c[3])
+                        self._score_memo[key] = hit
+                        self.memo_class_hits += 1
+            if hit is None:
+                hit = score_node_safe(n, self._usage_for_pod(c[1], pod), reqs, pod, policy, weights)
+                with self._cache_mu:
+                    self.memo_misses += 1
+                    self._score_memo[key] = hit
+                    if ckey is not None:
+                        self._score_memo[ckey] = (hit, c[3])
+                    while len(self._score_memo) > _MEMO_MAX:
+                        self._score_memo.popitem(last=False)
+            record_result(res, failure, failed, n, hit[0], hit[1])
+        return res, failure, failed
 
     def get_simulation_nodes_usage(self, nodes: list[dict], pod: dict):
         cand, failed = {}, {}
@@ -456,8 +622,11 @@ class Scheduler:
         pi = self.pod_manager.take_and_delete_pod(pod)
         if pi:
             self.quota_manager.rm_usage(pod, pi.devices)
-        usage, _, failed = self.get_nodes_usage(node_names or [], pod)
-        scores, failure = calc_score(usage, reqs, pod, failed, self.cfg.node_scheduler_policy)
+        if self.memoize:
+            scores, failure, failed = self.score_candidates(list(node_names or []), pod, reqs)
+        else:
+            usage, _, failed = self.get_nodes_usage(node_names or [], pod)
+            scores, failure = calc_score(usage, reqs, pod, failed, self.cfg.node_scheduler_policy)
         if not scores.node_list:
             for reason, ns_ in sorted(failure.items()):
                 self.events.filter_result(pod, E.FILTERING_FAILED, "",
@@ -467,6 +636,8 @@ class Scheduler:
             return {"FailedNodes": failed, "NodeNames": None, "Error": ""}
         scores.sort()
         best = scores.node_list[-1]
+        # memo entries are shared: hand the winner's allocation out as a copy
+        best = type(best)(best.node_id, best.node, copy_pod_devices(best.devices), best.score)
         annos = {T.ASSIGNED_NODE_ANNOTATION: best.node_id, T.ASSIGNED_TIME_ANNOTATION: str(int(time.time()))}
         for dev in D.get_devices().values():
             dev.patch_annotations(pod, annos, best.devices)

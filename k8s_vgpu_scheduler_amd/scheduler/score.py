@@ -179,6 +179,27 @@ def resolve_node_policy(pod: dict, default: str) -> str:
     return annos.get(T.NODE_POLICY_ANNOTATION, default)
 
 
+def record_result(res: "NodeScoreList", failure: dict, failed: dict, node_id: str, s, reason: str):
+    """Fold one node's (score | None, reason) into the Filter aggregates."""
+    if s is None:
+        failed[node_id] = reason
+        for r in R.parse_reason(reason) or {reason: 1}:
+            failure.setdefault(r, []).append(node_id)
+    else:
+        res.node_list.append(s)
+
+
+def score_node_safe(node_id: str, usage: NodeUsage, reqs: list, pod: dict, policy: str,
+                    weights: DeviceScoringWeights):
+    """score_node that turns an exception into a per-node failure (one bad
+    node must not fail the pod)."""
+    try:
+        return score_node(node_id, usage, reqs, pod, policy, weights)
+    except Exception as e:  # noqa: BLE001
+        log.exception("scoring node %s failed", node_id)
+        return None, f"scoring error: {e}"
+
+
 def calc_score(nodes: dict, reqs: list, pod: dict, failed: dict, default_node_policy: str):
     """-> (NodeScoreList, failure_reasons {reason: [nodes]})."""
     weights = weights_for_pod(pod)
@@ -186,16 +207,6 @@ def calc_score(nodes: dict, reqs: list, pod: dict, failed: dict, default_node_po
     res = NodeScoreList(node_list=[], policy=policy)
     failure: dict[str, list] = {}
     for node_id, usage in nodes.items():
-        try:
-            s, reason = score_node(node_id, usage, reqs, pod, policy, weights)
-        except Exception as e:  # noqa: BLE001 -- one bad node must not fail the pod
-            log.exception("scoring node %s failed", node_id)
-            failed[node_id] = f"scoring error: {e}"
-            continue
-        if s is None:
-            failed[node_id] = reason
-            for r in R.parse_reason(reason) or {reason: 1}:
-                failure.setdefault(r, []).append(node_id)
-        else:
-            res.node_list.append(s)
+        s, reason = score_node_safe(node_id, usage, reqs, pod, policy, weights)
+        record_result(res, failure, failed, node_id, s, reason)
     return res, failure

@@ -202,10 +202,13 @@ def test_device_usage_deepcopy_is_independent():
     d = DeviceUsage(id="g0", count=8, totalmem=10, totalcore=256, custominfo={"cu_used": 3, "x": [1]},
                     pod_infos=["p"])
     c = d.deepcopy()
-    c.custominfo["x"].append(2)
+    # custominfo values are replaced, never mutated in place (the Fit path
+    # rebinds cu_used; pair scores are read-only): rebinding stays private
+    c.custominfo["cu_used"] |= 4
+    c.custominfo["x"] = [1, 2]
     c.pod_infos.append("q")
     c.used = 5
-    assert d.custominfo["x"] == [1] and d.pod_infos == ["p"] and d.used == 0
+    assert d.custominfo == {"cu_used": 3, "x": [1]} and d.pod_infos == ["p"] and d.used == 0
 
 
 # ==================================================================== admission
