@@ -65,6 +65,11 @@ def main():
     ap.add_argument("--mode", default="all", choices=["all", "both", "shim", "native"],
                     help="all = native (same queues) + native (HIP default queues) + shim rounds")
     ap.add_argument("--no-spatial", action="store_true", help="no HSA_CU_MASK (temporal governor)")
+    ap.add_argument("--active-slices", type=int, default=0,
+                    help="run only the first K of the --slices planned slices (same masks/limits; 0 = all)")
+    ap.add_argument("--monitor", type=float, default=0.0, metavar="SECONDS",
+                    help="run the node monitor's feedback pass (priority + utilization_switch) over the shim "
+                         "rounds' regions every SECONDS while they run (0 = off)")
     ap.add_argument("--policy", default="default", choices=["default", "force", "disable"])
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     ap.add_argument("--hw-queues", type=int, default=2,
@@ -99,7 +104,7 @@ def main():
     def with_env(specs):
         for sp in specs:
             sp.env.update(extra_env)
-        return specs
+        return specs[:args.active_slices] if args.active_slices > 0 else specs
 
     def native_specs(queues):
         specs = plan_slices(args.slices, shim=False, gpumem_mib=None)
@@ -123,6 +128,13 @@ def main():
                                  spatial=not args.no_spatial, policy=args.policy,
                                  hw_queues=args.hw_queues or None)),
             phys, work, log_dir, child_args, "shim")))
+    if args.mode == "all" and args.slices > 1 and not args.no_spatial:
+        # the same slices time-shared by the governor gate instead of CU masks
+        # (BASELINE config 3: "4 pods x 25% gpucores, CU-throttle governor kernel")
+        rounds.append(("temporal", spawn_round(
+            with_env(plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib, spatial=False,
+                                 policy="force", hw_queues=args.hw_queues or None)),
+            phys, work / "temporal", log_dir, child_args, "temporal")))
     if args.mode in ("all", "both", "native"):
         rounds.append(("native", spawn_round(native_specs(args.hw_queues), phys, work, log_dir, child_args,
                                              "native")))
@@ -152,7 +164,13 @@ def main():
 
     results = {}
     for name, procs in rounds:
+        mon = None
+        if args.monitor > 0 and name in ("shim", "temporal"):
+            from k8s_vgpu_scheduler_amd.bench.slices import RoundMonitor
+            mon = RoundMonitor([p.cache for p in procs], args.monitor).start()
         r = run_round(procs, barrier=barrier, sync=sync)
+        if mon is not None:
+            r["monitor"] = mon.stop()
         wall = torch.tensor([r["wall_s"]], dtype=torch.float64, device=dev)
         toks = torch.tensor([float(r["tokens"])], dtype=torch.float64, device=dev)
         if world > 1:
@@ -212,12 +230,29 @@ def main():
             "tpot_ms_p50_rank0": [round(d.get("tpot_ms_p50", 0), 3) for d in head["done"]],
             "tpot_ms_p99_rank0": [round(d.get("tpot_ms_p99", 0), 3) for d in head["done"]],
         }
+        if any("gov_gates" in d or "share_pct" in d for d in head["done"]):
+            out["governor_rank0"] = [{k: d.get(k) for k in ("gov_charged_ms", "gov_held_ms", "gov_gates",
+                                                            "share_pct", "util_pct")} for d in head["done"]]
         if "native" in results and "shim" in results:
             nat = results["native"]["tok_s"]
             out["native_value"] = round(nat, 2)
             out["isolation_overhead_pct"] = round((1.0 - head["tok_s"] / nat) * 100.0, 2)
             nd = results["native"]["done"]
             out["native_tpot_ms_p50_rank0"] = [round(d.get("tpot_ms_p50", 0), 3) for d in nd]
+        if "temporal" in results:
+            tr = results["temporal"]
+            tps = [round(d["tok_s"], 1) for d in tr["done"]]
+            out["temporal_value"] = round(tr["tok_s"], 2)
+            out["temporal_per_slice_tok_s_rank0"] = tps
+            out["temporal_fairness_min_over_max"] = round(min(tps) / max(tps), 3) if tps else None
+            out["temporal_isolation"] = f"governor gate (force, {100 // args.slices} % each, occupancy-charged)"
+            out["temporal_governor_rank0"] = [{k: d.get(k) for k in ("gov_charged_ms", "gov_held_ms", "gov_gates",
+                                                                     "share_pct", "util_pct")} for d in tr["done"]]
+            if "native" in results:
+                out["temporal_overhead_pct"] = round((1.0 - tr["tok_s"] / results["native"]["tok_s"]) * 100.0, 2)
+        for nm in ("shim", "temporal"):
+            if nm in results and "monitor" in results[nm]:
+                out[f"{nm}_monitor"] = results[nm]["monitor"]
         if "native_hip_default" in results:
             nd = results["native_hip_default"]["tok_s"]
             out["native_hip_default_queues_value"] = round(nd, 2)

@@ -1,4 +1,4 @@
-// mivgpu shared-region ABI (version 1.0).
+// mivgpu shared-region ABI (version 1.1; 1.1 names two spare util fields).
 //
 // One file-backed region per container, mmap'd MAP_SHARED by every process of
 // the container that loads libmivgpu.so and, from the host side, by the node's
@@ -31,7 +31,7 @@ extern "C" {
 
 #define MIVGPU_MAGIC 0x4D495647u /* 'MIVG' */
 #define MIVGPU_MAJOR 1
-#define MIVGPU_MINOR 0
+#define MIVGPU_MINOR 1
 #define MIVGPU_MAX_DEVICES 16
 #define MIVGPU_MAX_PROCS 1024
 #define MIVGPU_UUID_LEN 96
@@ -56,8 +56,11 @@ typedef struct {
   uint64_t busy_ns;       /* GPU busy time measured by the governor gate    */
   uint64_t throttled_ns;  /* time gate kernels held the stream              */
   uint64_t gates;         /* gate kernels enqueued                          */
-  uint64_t util_pct;      /* last computed utilisation, percent             */
-  uint64_t unused[3];
+  uint64_t util_pct;      /* GPU share received over the last >= 0.5 s, %   */
+  uint64_t share_ns;      /* GPU time received: integral of the process's   */
+                          /* share of resident wavefronts (KFD occupancy)   */
+  uint64_t occupancy;     /* last KFD cu_occupancy sample of the process    */
+  uint64_t share_ppm;     /* governor's measured share while contending, ppm */
 } mivgpu_util_t; /* 64 B */
 
 typedef struct {

@@ -10,11 +10,24 @@
 // stream, in front of a user launch, at most once per `min interval` of host
 // submission.  The gate
 //   1. reads the 100 MHz constant clock (s_memrealtime -> 10 ns ticks),
-//   2. debits the stream's GPU-busy time since its previous gate from a bucket
-//      shared by every stream of the process on this device,
-//   3. refills the bucket at `rate_ppm` of wall time (the container's CU share),
+//   2. debits the GPU time the process received since this stream's previous
+//      gate from a bucket shared by all its streams on this device: the
+//      stream's busy wall time (in-order stream => everything between
+//      max(previous gate exit, first submission) and now was its work),
+//      weighted by the process's share of the GPU while busy.  The share is
+//      measured by the shim's sampler from KFD's per-process wave counts
+//      (SPI_CSQ_WF_ACTIVE_COUNT): own / (own + every other process) averaged
+//      over the samples in which the process was contending, published in
+//      host memory and read here at execution time.  A tenant alone is
+//      charged its wall time, N tenants time-sliced or co-resident are each
+//      charged ~1/N, a CU-masked tenant at most its CU fraction -- the
+//      analogue of HAMi-core charging NVML per-process SM utilisation.
+//      Without a KFD view the share is 1 (plain wall time),
+//   3. refills the bucket at `rate_ppm` of wall time (the container's share),
 //   4. if the bucket is in debt, holds the stream on-device (s_sleep loop)
-//      until the debt is repaid -- other tenants' queues run meanwhile.
+//      until the debt is repaid -- other tenants' queues run meanwhile -- and
+//      publishes the hold's end so the sampler does not count the gate's own
+//      resident wave as consumption.
 // No host thread ever blocks, launches stay asynchronous, and graph replays are
 // gated by the same mechanism.  Every spin is bounded (max_hold_ns), so a gate
 // can never wedge a queue.
@@ -23,6 +36,8 @@
 // of different streams can run on different XCDs, so every access to the
 // shared state is an agent-scope atomic, the critical section is bracketed by
 // acquire/release on the lock word, and only lane 0 of one wave touches it.
+// Host memory (fine-grained, coherent) is read and written with system-scope
+// atomics only.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -53,8 +68,10 @@ struct mivgpu_gate_host_stats {
   long long last_now_ns;
   long long last_tokens_ns;
   long long last_hold_ns;
-  unsigned long long pad[2];
+  unsigned long long share_ppm;  // HOST-written: the process's measured GPU share, ppm
+  unsigned long long pad;
   mivgpu_gate_trace_entry trace[MIVGPU_GATE_TRACE];  // ring, index = gates % N
+  long long hold_end_ns[MIVGPU_GATE_SLOTS];          // device ns at which a slot's hold ends
 };
 
 __device__ __forceinline__ long long rt_ns() {
@@ -76,7 +93,7 @@ __device__ __forceinline__ void astoreu(unsigned long long* p, unsigned long lon
 
 extern "C" __global__ void __launch_bounds__(64)
 mivgpu_gate(mivgpu_gate_state* st, mivgpu_gate_host_stats* hs, long long submit_ns,
-            int slot, unsigned int rate_ppm, long long cap_ns, long long max_hold_ns) {
+            int slot, unsigned int rate_ppm, long long cap_ns, long long max_hold_ns, int occupancy) {
   if (threadIdx.x != 0) return;
   if (slot < 0 || slot >= MIVGPU_GATE_SLOTS) slot = 0;
   if (rate_ppm == 0) rate_ppm = 1;
@@ -106,15 +123,19 @@ mivgpu_gate(mivgpu_gate_state* st, mivgpu_gate_host_stats* hs, long long submit_
   tokens += (long long)(((__int128)elapsed * rate_ppm) / 1000000);
   if (tokens > cap_ns) tokens = cap_ns;
 
-  // GPU time this stream consumed since its previous gate.  The stream is
-  // in-order, so everything between max(previous gate exit, first submission
-  // after it) and `now` was the stream's own work.
+  // Busy wall time of this stream since its previous gate.
   // submit_ns < 0: nothing was submitted on this stream since its previous
   // gate, so the time since then was idle, not busy.
   const long long prev_exit = aload(&st->slot_exit_ns[slot]);
   long long begin = prev_exit > submit_ns ? prev_exit : submit_ns;
   if (submit_ns < 0 || begin <= 0 || begin > now) begin = now;
-  const long long busy = now - begin;
+  long long busy = now - begin;
+  if (occupancy && hs) {
+    // weight by the measured share (ppm; 0 = no sample yet -> wall time)
+    unsigned long long share =
+        __hip_atomic_load(&hs->share_ppm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (share > 0 && share < 1000000ull) busy = (long long)(((__int128)busy * (long long)share) / 1000000);
+  }
   tokens -= busy;
   // Bound the debt to one burst: a single mis-measured interval can never
   // stall a tenant for longer than cap / rate.
@@ -155,6 +176,7 @@ mivgpu_gate(mivgpu_gate_state* st, mivgpu_gate_host_stats* hs, long long submit_
     e->hold_ns = hold;
     e->tokens_ns = tokens;
     e->slot = slot;
+    __hip_atomic_store(&hs->hold_end_ns[slot], t_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 
   // Hold the stream on-device.  ~3.4 us per s_sleep(127) at 2.4 GHz; bounded

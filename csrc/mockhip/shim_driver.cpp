@@ -13,6 +13,8 @@
 //   kfdctx <MiB>     runtime VRAM outside the hooks in the mock's simulated
 //                    KFD per-process file (MOCKHIP_KFD_SYSFS), for context accounting
 //   device <i>       hipSetDevice
+//   hsainit          hsa_init (interposed by the shim) + the HSA_CU_MASK /
+//                    ROCR_VISIBLE_DEVICES ROCr would read
 //   stress <threads> <iters> <max MiB>
 //                    threads doing random hipMalloc/hipFree and
 //                    hipMemCreate/hipMemRelease (sanitizer + race tests)
@@ -133,6 +135,14 @@ int main(int argc, char** argv) {
       if (f) f(mib);
       printf("{\"op\":\"kfdctx\",\"ok\":%d}\n", f ? 1 : 0);
       usleep(30000);  // past the shim's 20 ms refresh interval
+    } else if (!strcmp(c, "hsainit")) {
+      // what ROCr would see: HIP calls hsa_init, which the shim interposes
+      auto f = (int (*)(void))dlsym(RTLD_DEFAULT, "hsa_init");
+      int rc = f ? f() : -1;
+      const char* m = getenv("HSA_CU_MASK");
+      const char* v = getenv("ROCR_VISIBLE_DEVICES");
+      printf("{\"op\":\"hsainit\",\"hooked\":%d,\"rc\":%d,\"mask\":\"%s\",\"visible\":\"%s\"}\n", f ? 1 : 0, rc,
+             m ? m : "", v ? v : "");
     } else if (!strcmp(c, "sleep")) {
       usleep((useconds_t)strtoul(argv[++i], nullptr, 10) * 1000);
     } else if (!strcmp(c, "stress")) {

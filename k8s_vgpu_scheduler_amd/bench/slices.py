@@ -89,6 +89,52 @@ def slice_env(spec: SliceSpec, physical_gpu: str | None, cache_dir: Path) -> dic
     return env
 
 
+class RoundMonitor:
+    """The node monitor's feedback pass (monitor/feedback.py observe: priority
+    blocking + utilization_switch) over a round's slice regions, every
+    ``period`` s on a thread -- the production loop runs every 5 s over the
+    regions of all containers on the node."""
+
+    class _C:
+        def __init__(self, region):
+            self.region = region
+
+    def __init__(self, caches: list, period: float):
+        import threading
+        self.caches, self.period = [c for c in caches if c], period
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._run, name="round-monitor", daemon=True)
+        self.passes = 0
+        self.switch_seen = 0
+
+    def start(self):
+        self._th.start()
+        return self
+
+    def _run(self):
+        from k8s_vgpu_scheduler_amd.monitor.feedback import observe
+        from k8s_vgpu_scheduler_amd.monitor.region import SharedRegion
+        regions = {}
+        while not self._stop.wait(self.period):
+            for c in self.caches:
+                if c not in regions and os.path.exists(c):
+                    try:
+                        regions[c] = SharedRegion(c)
+                    except (OSError, ValueError):
+                        pass
+            cs = [self._C(r) for r in regions.values()]
+            observe(type("L", (), {"list_containers": lambda _self: cs})())
+            self.passes += 1
+            self.switch_seen += sum(1 for x in cs if x.region.utilization_switch() == 1)
+        for r in regions.values():
+            r.close()
+
+    def stop(self) -> dict:
+        self._stop.set()
+        self._th.join(timeout=10)
+        return {"period_s": self.period, "passes": self.passes, "switch_on_slice_passes": self.switch_seen}
+
+
 class SliceProc:
     def __init__(self, spec: SliceSpec, env: dict, args: list, log_path: Path):
         full = dict(os.environ)
@@ -102,6 +148,7 @@ class SliceProc:
             full.pop("HIP_VISIBLE_DEVICES", None)
             full.pop("CUDA_VISIBLE_DEVICES", None)
         self.spec = spec
+        self.cache = env.get("MIVGPU_SHARED_CACHE")
         self.log = open(log_path, "w")
         self.p = subprocess.Popen(
             [sys.executable, "-m", "k8s_vgpu_scheduler_amd.bench.slices", "--child", *args],
@@ -200,11 +247,38 @@ def child_main(argv):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     tpot = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(a.steps))
-    print("DONE " + json.dumps({"seconds": dt, "tokens": a.batch * a.steps, "tok_s": a.batch * a.steps / dt,
-                                "t_start": t_start, "t_end": t_start + dt,
-                                "tpot_ms_p50": tpot[len(tpot) // 2],
-                                "tpot_ms_p99": tpot[min(len(tpot) - 1, int(0.99 * len(tpot)))]}), flush=True)
+    done = {"seconds": dt, "tokens": a.batch * a.steps, "tok_s": a.batch * a.steps / dt,
+            "t_start": t_start, "t_end": t_start + dt,
+            "tpot_ms_p50": tpot[len(tpot) // 2],
+            "tpot_ms_p99": tpot[min(len(tpot) - 1, int(0.99 * len(tpot)))]}
+    done.update(_governor_stats())
+    print("DONE " + json.dumps(done), flush=True)
     return 0
+
+
+def _governor_stats() -> dict:
+    """This slice's governor counters (shim ABI) and measured GPU share (region)."""
+    import ctypes
+    out = {}
+    if not os.environ.get("LD_PRELOAD"):
+        return out
+    try:
+        lib = ctypes.CDLL(None)
+        b, h, g = ctypes.c_ulonglong(), ctypes.c_ulonglong(), ctypes.c_ulonglong()
+        if lib.mivgpu_gate_stats(0, ctypes.byref(b), ctypes.byref(h), ctypes.byref(g)) == 0:
+            out.update({"gov_charged_ms": round(b.value / 1e6, 1), "gov_held_ms": round(h.value / 1e6, 1),
+                        "gov_gates": g.value})
+    except (OSError, AttributeError):
+        pass
+    cache = os.environ.get("MIVGPU_SHARED_CACHE")
+    if cache and os.path.exists(cache):
+        from k8s_vgpu_scheduler_amd.monitor.region import SharedRegion
+        reg = SharedRegion(cache, writable=False)
+        me = [p for p in reg.active_procs() if p.pid == os.getpid()]
+        if me:
+            out.update({"share_pct": round(me[0].util[0].share_ppm / 1e4, 1), "util_pct": me[0].util[0].util_pct})
+        reg.close()
+    return out
 
 
 def _child_cpu(a, cfg, Qwen3Decoder):
@@ -237,6 +311,7 @@ def _child_cpu(a, cfg, Qwen3Decoder):
 
 
 def spawn_round(specs, physical_gpu, cache_dir: Path, log_dir: Path, child_args, tag: str):
+    cache_dir.mkdir(parents=True, exist_ok=True)
     procs = []
     for s in specs:
         env = slice_env(s, physical_gpu, cache_dir)

@@ -1,8 +1,11 @@
 """``mivgpu-monitor``: node vGPU monitor (metrics :9394 + priority feedback loop).
 
 Reference: cmd/vGPUmonitor/main.go:57-172, feedback.go, metrics.go.  Validates
-HOOK_PATH, lists this node's pods (field selector spec.nodeName) for the
-container lister, serves Prometheus, and runs the 5 s feedback loop.
+HOOK_PATH, watches this node's pods only (server-side field selector
+spec.nodeName, pkg/monitor/nvidia/cudevshr.go:308) for the container lister,
+samples KFD wave occupancy, serves Prometheus (``--legacy-metrics`` adds the
+pre-2.x series), and runs the 5 s feedback loop -- paused while the device
+plugin holds the compute-partition apply lock (main.go:79-109).
 """
 
 from __future__ import annotations
@@ -19,6 +22,7 @@ from k8s_vgpu_scheduler_amd.k8s.informer import Informer
 from k8s_vgpu_scheduler_amd.monitor.feedback import watch_and_feedback
 from k8s_vgpu_scheduler_amd.monitor.lister import ContainerLister
 from k8s_vgpu_scheduler_amd.monitor.metrics import MonitorCollector
+from k8s_vgpu_scheduler_amd.monitor.occupancy import OccupancySampler
 from k8s_vgpu_scheduler_amd.smi import detect
 from k8s_vgpu_scheduler_amd.utils.logsetup import setup_logging
 
@@ -30,6 +34,10 @@ def main(argv=None):
     ap.add_argument("--hook-path", default=os.environ.get("HOOK_PATH", "/usr/local/vgpu"))
     ap.add_argument("--kubeconfig", default=None)
     ap.add_argument("--smi-backend", default=None)
+    ap.add_argument("--legacy-metrics", action="store_true",
+                    help="also export the pre-2.x metric names (HostGPUMemoryUsage, vGPU_device_memory_*, ...)")
+    ap.add_argument("--occupancy-period", type=float, default=0.05,
+                    help="seconds between KFD wave-occupancy samples (0 = off)")
     ap.add_argument("-v", type=int, default=2)
     a = ap.parse_args(argv)
     setup_logging(a.v)
@@ -38,22 +46,46 @@ def main(argv=None):
         raise SystemExit(f"HOOK_PATH {a.hook_path} does not exist")
     from k8s_vgpu_scheduler_amd.k8s.rest import RestClient
     client = init_global_client(RestClient.from_env(a.kubeconfig))
-    inf = Informer(client, "pods")
+    inf = Informer(client, "pods", field_selector={"spec.nodeName": a.node_name})
     inf.start()
-    pods = (lambda: [p for p in inf.list() if (p.get("spec") or {}).get("nodeName") == a.node_name])
-    lister = ContainerLister(a.hook_path, pods)
+    lister = ContainerLister(a.hook_path, inf.list)
     try:
         backend = detect(a.smi_backend)
     except RuntimeError as e:
         log.warning("no amd-smi backend (%s): host metrics disabled", e)
         backend = None
+    occ = OccupancySampler(period_s=a.occupancy_period).start() if a.occupancy_period > 0 else None
     reg = CollectorRegistry()
-    reg.register(MonitorCollector(lister, backend, a.node_name))
+    reg.register(MonitorCollector(lister, backend, a.node_name, occupancy=occ, legacy=a.legacy_metrics))
     host, _, port = a.metrics_bind_address.rpartition(":")
     start_http_server(int(port), addr=host or "0.0.0.0", registry=reg)
     stop = threading.Event()
-    watch_and_feedback(lister, stop)
+    pause = threading.Event()
+    threading.Thread(target=watch_partition_lock, args=(pause, stop), name="partition-lock", daemon=True).start()
+    watch_and_feedback(lister, stop, pause=pause)
     return 0
+
+
+def watch_partition_lock(pause: threading.Event, stop: threading.Event, lock_path: str | None = None,
+                         poll: float = 1.0):
+    """Mirror the device plugin's partition apply lock into ``pause``."""
+    from k8s_vgpu_scheduler_amd.deviceplugin.partition import APPLY_LOCK, is_applying
+    log = logging.getLogger("mivgpu.monitor")
+    path = lock_path or APPLY_LOCK
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+    except OSError:   # read-only mount of the device plugin's lock dir
+        pass
+    while True:
+        busy = is_applying(path)
+        if busy and not pause.is_set():
+            log.info("partition apply lock %s present: feedback paused", path)
+            pause.set()
+        elif not busy and pause.is_set():
+            log.info("partition apply lock released: feedback resumed")
+            pause.clear()
+        if stop.wait(poll):
+            return
 
 
 if __name__ == "__main__":

@@ -16,8 +16,17 @@ docs/develop/amd-vgpu.md:47-104.  MI355X translation:
        MIVGPU_SHARED_CACHE    $HOOK_PATH/vgpu/<uuid4>.cache
        MIVGPU_DEVICE_UUIDS, MIVGPU_OVERSUBSCRIBE, MIVGPU_LOG_LEVEL,
        GPU_CORE_UTILIZATION_POLICY=disable (with --disable-core-limit)
-  mounts libmivgpu.so (ro), the per-container cache dir (rw), /tmp/vgpulock,
-       /etc/ld.so.preload (ro) unless the container sets MIVGPU_DISABLE_CONTROL=true
+  mounts libmivgpu.so (ro), the per-container cache dir (rw), the grant file
+       (ro, LIMITS_PATH), /etc/ld.so.preload (ro) unless the container sets
+       MIVGPU_DISABLE_CONTROL=true
+
+The grant file repeats the policy settings of ``env`` (limits, CU mask, core
+limit/policy, visible devices, region path).  It is written on the host and
+mounted read-only, and the shim takes the grant from it alone, so a tenant
+that unsets or rewrites those variables before the runtime starts still gets
+exactly its allocation (the shim re-asserts HSA_CU_MASK / ROCR_VISIBLE_DEVICES
+right before ROCr reads them); the monitor reconciles each shared region's
+limits against the same host file (monitor/feedback.py).
   devs /dev/kfd and the allocated /dev/dri/renderD<N> (+ card<M>) nodes
 """
 
@@ -30,6 +39,30 @@ from dataclasses import dataclass, field
 from k8s_vgpu_scheduler_amd.device.codec import format_ranges, ranges_count
 
 CONTAINER_LIB = "/usr/local/vgpu/libmivgpu.so"
+LIMITS_PATH = "/etc/mivgpu/limits.conf"     # fixed in the shim (kLimitsPath)
+# env keys that form the grant (the shim's is_grant_key list)
+GRANT_KEYS = ("HIP_DEVICE_MEMORY_LIMIT", "HIP_DEVICE_CORE_LIMIT", "HSA_CU_MASK", "GPU_CORE_UTILIZATION_POLICY",
+              "HIP_TASK_PRIORITY", "MIVGPU_OVERSUBSCRIBE", "MIVGPU_SHARED_CACHE", "MIVGPU_DEVICE_UUIDS",
+              "ROCR_VISIBLE_DEVICES")
+
+
+def limits_host_path(hook_path: str, pod_uid: str, ctr_name: str) -> str:
+    """Host location of a container's grant file (outside the container's rw mounts)."""
+    return f"{hook_path}/vgpu/limits/{pod_uid}_{ctr_name}.conf"
+
+
+def grant_text(env: dict) -> str:
+    keys = [k for k in env if k in GRANT_KEYS or k.startswith("HIP_DEVICE_MEMORY_LIMIT_")]
+    return "".join(f"{k}={env[k]}\n" for k in sorted(keys))
+
+
+def parse_grant(text: str) -> dict:
+    out = {}
+    for line in text.splitlines():
+        k, sep, v = line.partition("=")
+        if sep and k and not k.startswith("#"):
+            out[k] = v
+    return out
 
 
 @dataclass
@@ -107,19 +140,25 @@ def allocate_container(pod: dict, ctr: dict, devreq: list, gpus: dict, cfg: Plug
     envs = container_env(devreq, gpus, cfg, cache_file)
     uid = (pod.get("metadata") or {}).get("uid", "")
     host_dir = f"{hook}/vgpu/containers/{uid}_{ctr.get('name', '')}"
+    limits = limits_host_path(hook, uid, ctr.get("name", ""))
     if make_dirs:
         import shutil
         shutil.rmtree(host_dir, ignore_errors=True)
-        for d in (host_dir, "/tmp/vgpulock"):
-            os.makedirs(d, exist_ok=True)
-            try:
-                os.chmod(d, 0o777)
-            except OSError:
-                pass
+        os.makedirs(host_dir, exist_ok=True)
+        try:
+            os.chmod(host_dir, 0o777)
+        except OSError:
+            pass
+        os.makedirs(os.path.dirname(limits), exist_ok=True)
+        tmp = limits + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(grant_text(envs))
+        os.chmod(tmp, 0o444)
+        os.replace(tmp, limits)
     mounts = [
         {"container_path": CONTAINER_LIB, "host_path": f"{hook}/vgpu/libmivgpu.so", "read_only": True},
         {"container_path": f"{hook}/vgpu", "host_path": host_dir, "read_only": False},
-        {"container_path": "/tmp/vgpulock", "host_path": "/tmp/vgpulock", "read_only": False},
+        {"container_path": LIMITS_PATH, "host_path": limits, "read_only": True},
     ]
     disabled = any(e.get("name") == "MIVGPU_DISABLE_CONTROL" and _truthy(e.get("value", ""))
                    for e in ctr.get("env") or [])

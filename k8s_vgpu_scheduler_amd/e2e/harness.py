@@ -193,6 +193,17 @@ def container_env(alloc: dict, base: dict | None = None) -> dict:
     mounts = alloc["mounts"]
     if "MIVGPU_SHARED_CACHE" in env:
         env["MIVGPU_SHARED_CACHE"] = host_path(env["MIVGPU_SHARED_CACHE"], mounts)
+    from k8s_vgpu_scheduler_amd.deviceplugin.allocate import LIMITS_PATH, grant_text, parse_grant
+    grant = next((m for m in mounts if m["container_path"] == LIMITS_PATH), None)
+    if grant is not None:
+        # the shim reads the grant from the read-only mount; on the host the
+        # same file (with its region path mapped) is named by MIVGPU_LIMITS_FILE
+        g = parse_grant(Path(grant["host_path"]).read_text())
+        if "MIVGPU_SHARED_CACHE" in g:
+            g["MIVGPU_SHARED_CACHE"] = host_path(g["MIVGPU_SHARED_CACHE"], mounts)
+        hp = Path(grant["host_path"] + ".host")
+        hp.write_text(grant_text(g))
+        env["MIVGPU_LIMITS_FILE"] = str(hp)
     preload = next((m for m in mounts if m["container_path"] == "/etc/ld.so.preload"), None)
     if preload is not None:
         libs = [host_path(l.strip(), mounts) for l in Path(preload["host_path"]).read_text().splitlines()

@@ -82,9 +82,11 @@ class KubeClient:
         raise NotImplementedError
 
     def watch(self, kind: str, handler: Callable[[str, dict, Optional[dict]], None],
-              namespace: str | None = None) -> Callable[[], None]:
+              namespace: str | None = None, field_selector: dict | None = None) -> Callable[[], None]:
         """Subscribe to ADDED/MODIFIED/DELETED events; returns an unsubscribe fn.
-        handler(event_type, obj, old_obj)."""
+        handler(event_type, obj, old_obj).  With ``field_selector`` only objects
+        matching it are delivered (an object leaving the selection arrives as
+        DELETED, one entering it as ADDED)."""
         raise NotImplementedError
 
     # -- typed conveniences -------------------------------------------------

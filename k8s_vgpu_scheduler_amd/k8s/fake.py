@@ -61,11 +61,21 @@ class FakeCluster(KubeClient):
         return after
 
     def _notify(self, kind, etype, obj, old):
-        for ns, h in list(self._watchers.get(kind, [])):
+        for ns, h, fs in list(self._watchers.get(kind, [])):
             if ns and (obj.get("metadata") or {}).get("namespace") != ns:
                 continue
+            et = etype
+            if fs:
+                # a field-selected watch sees an object enter (ADDED) and leave
+                # (DELETED) the selection, as the API server's filtered watch does
+                now_in = match_fields(obj, fs)
+                was_in = old is not None and match_fields(old, fs)
+                if et == "MODIFIED" and now_in != was_in:
+                    et = "ADDED" if now_in else "DELETED"
+                elif not now_in and not (et == "DELETED" and was_in):
+                    continue
             try:
-                h(etype, jcopy(obj), jcopy(old) if old else None)
+                h(et, jcopy(obj), jcopy(old) if old else None)
             except Exception:  # a broken handler must not break the API server
                 import logging
                 logging.getLogger(__name__).exception("watch handler failed")
@@ -188,9 +198,9 @@ class FakeCluster(KubeClient):
                 raise Conflict(f"pod {pod_name} is already assigned to a node")
         self.patch("pods", pod_name, {"spec": {"nodeName": node}}, namespace)
 
-    def watch(self, kind, handler, namespace=None):
+    def watch(self, kind, handler, namespace=None, field_selector=None):
         with self._lock:
-            entry = (namespace, handler)
+            entry = (namespace, handler, field_selector)
             self._watchers.setdefault(kind, []).append(entry)
 
         def stop():

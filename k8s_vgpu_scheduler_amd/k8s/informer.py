@@ -21,8 +21,12 @@ log = logging.getLogger(__name__)
 
 
 class Informer:
-    def __init__(self, client: KubeClient, kind: str, namespace: str | None = None):
+    def __init__(self, client: KubeClient, kind: str, namespace: str | None = None,
+                 field_selector: dict | None = None):
+        """``field_selector`` scopes the cache server-side, e.g. the node agents'
+        ``{"spec.nodeName": node}`` (pkg/monitor/nvidia/cudevshr.go:308)."""
         self.client, self.kind, self.namespace = client, kind, namespace
+        self.field_selector = field_selector
         self._cache: dict[tuple, dict] = {}
         self._mu = threading.RLock()
         self._handlers: list[tuple] = []
@@ -66,8 +70,14 @@ class Informer:
         if self._stop:
             return
         # Subscribe first, then list, so no event between the two is lost.
-        self._stop = self.client.watch(self.kind, self._dispatch, self.namespace)
-        for o in self.client.list(self.kind, self.namespace):
+        if self.field_selector:
+            self._stop = self.client.watch(self.kind, self._dispatch, self.namespace,
+                                           field_selector=self.field_selector)
+            listed = self.client.list(self.kind, self.namespace, field_selector=self.field_selector)
+        else:
+            self._stop = self.client.watch(self.kind, self._dispatch, self.namespace)
+            listed = self.client.list(self.kind, self.namespace)
+        for o in listed:
             key = self._key(o)
             with self._mu:
                 known = key in self._cache

@@ -181,8 +181,9 @@ class RestClient(KubeClient):
             body["metadata"]["uid"] = uid
         self._req("POST", self._url("pods", pod_name, namespace, "binding"), json=body)
 
-    def watch(self, kind, handler, namespace=None):
+    def watch(self, kind, handler, namespace=None, field_selector=None):
         stop = threading.Event()
+        sel = {"fieldSelector": self._selector(field_selector)} if field_selector else {}
 
         def loop():
             rv = None
@@ -190,7 +191,7 @@ class RestClient(KubeClient):
             while not stop.is_set():
                 try:
                     if rv is None:
-                        body = self._req("GET", self._url(kind, namespace=namespace))
+                        body = self._req("GET", self._url(kind, namespace=namespace), params=dict(sel))
                         rv = body["metadata"].get("resourceVersion")
                         fresh = {}
                         for it in body.get("items", []):
@@ -202,7 +203,7 @@ class RestClient(KubeClient):
                                 handler("DELETED", old, None)
                         known = fresh
                     params = {"watch": "1", "resourceVersion": rv, "timeoutSeconds": "300",
-                              "allowWatchBookmarks": "true"}
+                              "allowWatchBookmarks": "true", **sel}
                     self.throttle.wait()
                     with self.s.get(self._url(kind, namespace=namespace), params=params, stream=True,
                                     timeout=(self.timeout, 330)) as r:

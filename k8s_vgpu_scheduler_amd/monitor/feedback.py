@@ -17,6 +17,7 @@ import threading
 
 from .hostpid import fill_host_pids
 from .lister import ContainerLister
+from .region import MAX_DEVICES
 
 log = logging.getLogger(__name__)
 
@@ -79,14 +80,104 @@ def observe(lister: ContainerLister):
     return ut
 
 
+_SIZE_MULT = {"k": 1 << 10, "m": 1 << 20, "g": 1 << 30, "t": 1 << 40}
+
+
+def parse_size(v: str | None) -> int:
+    """The shim's parse_size: ``4096m`` -> bytes (plain numbers are bytes)."""
+    if not v:
+        return 0
+    v = v.strip()
+    mult = _SIZE_MULT.get(v[-1:].lower(), 1)
+    try:
+        return int(float(v[:-1] if mult > 1 else v) * mult)
+    except ValueError:
+        return 0
+
+
+def mask_count(mask: str | None, idx: int) -> int:
+    """CUs granted to local device ``idx`` by an HSA_CU_MASK value."""
+    for part in (mask or "").split(";"):
+        dev, sep, ranges = part.partition(":")
+        if not sep or dev.strip() != str(idx):
+            continue
+        n = 0
+        for r in ranges.split(","):
+            a, _, b = r.partition("-")
+            try:
+                n += int(b or a) - int(a) + 1
+            except ValueError:
+                return 0
+        return n
+    return 0
+
+
+def expected_region(grant: dict) -> dict:
+    """Region fields a grant file (deviceplugin/allocate.py) implies."""
+    allmem = parse_size(grant.get("HIP_DEVICE_MEMORY_LIMIT"))
+    try:
+        core = int(grant.get("HIP_DEVICE_CORE_LIMIT", "100"))
+    except ValueError:
+        core = 100
+    core = core if 1 <= core <= 100 else 100
+    pol = {"force": 1, "disable": 2}.get(grant.get("GPU_CORE_UTILIZATION_POLICY", "").lower(), 0)
+    try:
+        prio = int(grant.get("HIP_TASK_PRIORITY", "1"))
+    except ValueError:
+        prio = 1
+    return {"mem_limit": [parse_size(grant.get(f"HIP_DEVICE_MEMORY_LIMIT_{i}")) or allmem
+                          for i in range(MAX_DEVICES)],
+            "cu_limit": core, "cu_mask": [mask_count(grant.get("HSA_CU_MASK"), i) for i in range(MAX_DEVICES)],
+            "core_policy": pol, "priority": prio}
+
+
+def reconcile_limits(lister: ContainerLister) -> int:
+    """Put every region's limits back to the container's grant.
+
+    The region file sits in a directory the container mounts read-write, so a
+    tenant can rewrite ``mem_limit``/``cu_limit``/``cu_mask_count``/policy in
+    it; the grant file (written by Allocate on the host, mounted read-only)
+    is the authority.  Returns the number of fields corrected."""
+    from k8s_vgpu_scheduler_amd.deviceplugin.allocate import parse_grant
+    fixed = 0
+    limits_dir = lister.base.parent / "limits"
+    for c in lister.list_containers():
+        path = limits_dir / f"{c.pod_uid}_{c.container}.conf"
+        try:
+            grant = parse_grant(path.read_text())
+        except OSError:
+            continue
+        want = expected_region(grant)
+        r = c.region.r
+        for i in range(c.region.device_num()):
+            for field, val in (("mem_limit", want["mem_limit"][i]), ("cu_limit", want["cu_limit"]),
+                               ("cu_mask_count", want["cu_mask"][i])):
+                arr = getattr(r, field)
+                if int(arr[i]) != val:
+                    log.warning("%s/%s: region %s[%d]=%d differs from the grant %d; restored",
+                                c.pod_uid, c.container, field, i, int(arr[i]), val)
+                    arr[i] = val
+                    fixed += 1
+        for field in ("core_policy", "priority"):
+            if int(getattr(r, field)) != want[field]:
+                log.warning("%s/%s: region %s=%d differs from the grant %d; restored", c.pod_uid, c.container,
+                            field, int(getattr(r, field)), want[field])
+                setattr(r, field, want[field])
+                fixed += 1
+    return fixed
+
+
 def watch_and_feedback(lister: ContainerLister, stop: threading.Event, period: float = 5.0,
                        pause: threading.Event | None = None):
+    """The 5 s loop; skipped while ``pause`` is set (a compute-partition apply
+    is in progress, cmd/vGPUmonitor/main.go:79-109)."""
     while not stop.wait(period):
         if pause is not None and pause.is_set():
             continue
         try:
             lister.update()
             fill_host_pids(lister.list_containers())
+            reconcile_limits(lister)
             observe(lister)
         except Exception:  # noqa: BLE001
             log.exception("feedback iteration failed")

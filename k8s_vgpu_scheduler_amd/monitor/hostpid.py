@@ -68,15 +68,18 @@ def fill_host_pids(containers, proc_root: str = "/proc", procs=None) -> int:
         for i in range(min(r.procnum, len(r.procs))):
             s = r.procs[i]
             if s.status == 1 and s.pid > 0 and s.hostpid == 0:
-                pending.append((c, s))
+                pending.append((c, s, s.pid, s.start_ns))
     if not pending:
         return 0
     procs = scan(proc_root) if procs is None else procs
     filled = 0
-    for c, s in pending:
+    for c, s, pid, start in pending:
         forms = _uid_forms(c.pod_uid)
-        hits = [hp for hp, nsp, cg in procs if nsp == s.pid and any(f"pod{f}" in cg for f in forms)]
-        if len(hits) == 1:
+        hits = [hp for hp, nsp, cg in procs if nsp == pid and any(f"pod{f}" in cg for f in forms)]
+        # the slot may have been freed and reused by another process during the
+        # /proc scan: write only if it still holds the process that was matched
+        # (same pid and start time, still active, still unmapped)
+        if len(hits) == 1 and s.status == 1 and s.pid == pid and s.start_ns == start and s.hostpid == 0:
             s.hostpid = hits[0]
             filled += 1
     return filled

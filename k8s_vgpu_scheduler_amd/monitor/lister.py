@@ -91,6 +91,10 @@ class ContainerLister:
                 if age > self.resync:
                     log.info("removing stale container dir %s", d)
                     shutil.rmtree(d, ignore_errors=True)
+                    try:   # the container's grant file (deviceplugin/allocate.py)
+                        (self.base.parent / "limits" / f"{d.name}.conf").unlink()
+                    except OSError:
+                        pass
                 continue
             with self._mu:
                 known = d.name in self.containers

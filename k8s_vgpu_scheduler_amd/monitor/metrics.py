@@ -2,8 +2,15 @@
 
 Host series come from amd-smi (the NVML replacement), container series from
 the shim's shared regions; names and labels match the reference so the HAMi
-dashboards keep working.  MI355X extras: governor busy/throttled time and CU
-mask size per container.
+dashboards keep working.  MI355X extras: governor busy/throttled time, CU
+mask size and partition identity per container, active tenants per GPU from
+KFD wave occupancy.  ``legacy=True`` also emits the pre-2.x series names
+(cmd/vGPUmonitor/metrics.go:133-212, ``--legacy-metrics``).
+
+Container utilisation (``hami_container_device_utilization_ratio``) is the
+GPU share the container's processes received -- their share of the resident
+wavefronts, integrated by the shim (``util_pct``) or, when no shim process
+reports one, sampled by the monitor itself from KFD (monitor/occupancy.py).
 """
 
 from __future__ import annotations
@@ -12,16 +19,28 @@ import time
 
 from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily
 
-from .board import active_tenants, board_path
+from .occupancy import gpu_ids_by_bdf
 
 CTR_LABELS = ["namespace", "pod", "container", "vdevice_index", "device_uuid"]
+LEGACY_CTR_LABELS = ["podnamespace", "podname", "ctrname", "vdeviceid", "deviceuuid"]
+LEGACY_HOST_LABELS = ["nodeid", "deviceidx", "deviceuuid", "devicetype"]
 
 
 class MonitorCollector:
-    def __init__(self, lister, backend=None, node_name: str = ""):
+    def __init__(self, lister, backend=None, node_name: str = "", occupancy=None, legacy: bool = False):
         self.lister = lister
         self.backend = backend
         self.node = node_name
+        self.occ = occupancy      # monitor.occupancy.OccupancySampler (hostPID view) or None
+        self.legacy = legacy
+        self._gpu_ids: dict[str, int] | None = None
+
+    def _gpu_id(self, bdf: str) -> int | None:
+        if self.occ is None or not bdf:
+            return None
+        if self._gpu_ids is None or bdf not in self._gpu_ids:
+            self._gpu_ids = gpu_ids_by_bdf(self.occ.root)
+        return self._gpu_ids.get(bdf)
 
     def collect(self):
         host_mem = GaugeMetricFamily("hami_host_gpu_memory_used_bytes", "GPU device memory usage in bytes",
@@ -32,19 +51,29 @@ class MonitorCollector:
                                     "GPU memory controller utilization ratio (0-100)",
                                     labels=["device_index", "device_uuid", "device_type"])
         tenants = GaugeMetricFamily("mivgpu_host_gpu_active_tenants",
-                                    "Shimmed processes that launched work on the GPU in the last second "
-                                    "(the governor's share board)", labels=["node", "device_index", "device_uuid"])
+                                    "Processes with wavefronts resident on the GPU in the sampling window "
+                                    "(KFD cu_occupancy)", labels=["node", "device_index", "device_uuid"])
+        l_mem = GaugeMetricFamily("HostGPUMemoryUsage", "GPU device memory usage", labels=LEGACY_HOST_LABELS)
+        l_util = GaugeMetricFamily("HostCoreUtilization", "GPU core utilization", labels=LEGACY_HOST_LABELS)
+        gpus = {}
         if self.backend is not None:
             for g in self.backend.gpus():
-                bp = board_path(g.bdf) if g.bdf else None
-                if bp is not None and bp.exists():
-                    tenants.add_metric([self.node, str(g.index), g.uuid], float(active_tenants(bp)))
+                gpus[g.uuid] = g
+                gid = self._gpu_id(g.bdf)
+                n = self.occ.active_tenants(gid) if gid is not None else None
+                if n is not None:
+                    tenants.add_metric([self.node, str(g.index), g.uuid], float(n))
                 u = self.backend.utilization(g)
-                host_mem.add_metric([self.node, str(g.index), g.uuid, g.name],
-                                    float(self.backend.memory_used_mib(g)) * 1024 * 1024)
+                mem_b = float(self.backend.memory_used_mib(g)) * 1024 * 1024
+                host_mem.add_metric([self.node, str(g.index), g.uuid, g.name], mem_b)
                 host_util.add_metric([self.node, str(g.index), g.uuid, g.name], float(u.get("gfx", 0)))
                 host_mc.add_metric([str(g.index), g.uuid, g.name], float(u.get("umc", 0)))
+                if self.legacy:
+                    l_mem.add_metric([self.node, str(g.index), g.uuid, g.name], mem_b)
+                    l_util.add_metric([self.node, str(g.index), g.uuid, g.name], float(u.get("gfx", 0)))
         yield from (host_mem, host_util, host_mc, tenants)
+        if self.legacy:
+            yield from (l_mem, l_util)
 
         used = GaugeMetricFamily("hami_vgpu_memory_used_bytes", "vGPU device memory usage in bytes", labels=CTR_LABELS)
         limit = GaugeMetricFamily("hami_vgpu_memory_limit_bytes", "vGPU device memory limit in bytes",
@@ -67,6 +96,20 @@ class MonitorCollector:
                                    "Time the governor held the container's streams", labels=CTR_LABELS)
         cumask = GaugeMetricFamily("mivgpu_container_cu_mask_cus", "CUs granted through HSA_CU_MASK",
                                    labels=CTR_LABELS)
+        part = GaugeMetricFamily("mivgpu_container_partition_info",
+                                 "Compute-partition identity of a container allocation (the MI355X analogue "
+                                 "of hami_mig_device_info)",
+                                 labels=CTR_LABELS + ["compute_partition", "memory_partition", "partition_index",
+                                                      "physical_index", "cus"])
+        l_used = GaugeMetricFamily("vGPU_device_memory_usage_in_bytes", "vGPU device usage", labels=LEGACY_CTR_LABELS)
+        l_limit = GaugeMetricFamily("vGPU_device_memory_limit_in_bytes", "vGPU device limit",
+                                    labels=LEGACY_CTR_LABELS)
+        l_desc = GaugeMetricFamily("Device_memory_desc_of_container", "Container device memory description",
+                                   labels=LEGACY_CTR_LABELS + ["context", "module", "data", "offset"])
+        l_cutil = GaugeMetricFamily("Device_utilization_desc_of_container",
+                                    "Container device utilization description", labels=LEGACY_CTR_LABELS)
+        l_lastk = GaugeMetricFamily("Device_last_kernel_of_container", "Container device last kernel description",
+                                    labels=LEGACY_CTR_LABELS)
         now = time.time()
         for c in self.lister.list_containers():
             r = c.region
@@ -82,12 +125,42 @@ class MonitorCollector:
                 ctx.add_metric(lab, float(r.memory_field(i, "context")))
                 mod.add_metric(lab, float(r.memory_field(i, "module")))
                 buf.add_metric(lab, float(r.memory_field(i, "buffer") + r.memory_field(i, "vmm")))
-                util = sum(p.util[i].util_pct for p in r.active_procs())
-                dutil.add_metric(lab, float(util))
+                util = float(self._container_util(r, i, gpus.get(r.uuid(i))))
+                dutil.add_metric(lab, util)
                 lkt = r.last_kernel_time()
                 if lkt > 0:
                     lastk.add_metric(lab, max(0.0, now - lkt))
+                g = gpus.get(r.uuid(i))
+                if g is not None:
+                    part.add_metric(lab + [g.compute_partition, g.memory_partition, str(g.partition_index),
+                                           str(g.physical), str(g.cus)], 1.0)
+                if self.legacy:
+                    ctx_b, mod_b = r.memory_field(i, "context"), r.memory_field(i, "module")
+                    data_b = r.memory_field(i, "buffer") + r.memory_field(i, "vmm")
+                    l_used.add_metric(lab, float(total))
+                    l_limit.add_metric(lab, float(r.memory_limit(i)))
+                    l_desc.add_metric(lab + [str(ctx_b), str(mod_b), str(data_b),
+                                             str(max(0, total - ctx_b - mod_b - data_b))], float(total))
+                    l_cutil.add_metric(lab, util)
+                    if lkt > 0:
+                        l_lastk.add_metric(lab, max(0.0, now - lkt))
                 busy.add_metric(lab, r.busy_ns(i) / 1e9)
                 held.add_metric(lab, sum(p.util[i].throttled_ns for p in r.active_procs()) / 1e9)
                 cumask.add_metric(lab, float(r.r.cu_mask_count[i]))
-        yield from (used, limit, dmem, dutil, lastk, ctx, mod, buf, busy, held, cumask)
+        yield from (used, limit, dmem, dutil, lastk, ctx, mod, buf, busy, held, cumask, part)
+        if self.legacy:
+            yield from (l_used, l_limit, l_desc, l_cutil, l_lastk)
+
+    def _container_util(self, r, i: int, g) -> float:
+        """Percent of the GPU the container's processes received: the shims'
+        own occupancy integral when any reports one, else the monitor's KFD
+        sample of the processes' host pids."""
+        procs = r.active_procs()
+        if any(p.util[i].share_ns for p in procs):
+            return float(min(100, sum(p.util[i].util_pct for p in procs)))
+        gid = self._gpu_id(g.bdf) if g is not None else None
+        pids = [p.hostpid for p in procs if p.hostpid > 0]
+        if gid is None or not pids:
+            return 0.0
+        v = self.occ.share_pct(gid, pids)
+        return round(v, 1) if v is not None else 0.0

@@ -27,7 +27,8 @@ class MemT(C.Structure):
 
 class UtilT(C.Structure):
     _fields_ = [("launches", C.c_uint64), ("busy_ns", C.c_uint64), ("throttled_ns", C.c_uint64),
-                ("gates", C.c_uint64), ("util_pct", C.c_uint64), ("unused", C.c_uint64 * 3)]
+                ("gates", C.c_uint64), ("util_pct", C.c_uint64), ("share_ns", C.c_uint64),
+                ("occupancy", C.c_uint64), ("share_ppm", C.c_uint64)]
 
 
 class ProcSlot(C.Structure):
@@ -80,7 +81,7 @@ class SharedRegion:
         fd = os.open(path, os.O_RDWR)
         mm = mmap.mmap(fd, REGION_SIZE, mmap.MAP_SHARED)
         r = Region.from_buffer(mm)
-        r.major_version, r.minor_version, r.initialized = 1, 0, 1
+        r.major_version, r.minor_version, r.initialized = 1, 1, 1
         r.num_devices = num_devices
         for d in range(MAX_DEVICES):
             r.mem_limit[d] = mem_limit

@@ -21,6 +21,7 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
 log = logging.getLogger(__name__)
 MAX_BODY = 1024 * 1024
+DRAIN_LIMIT = 16 * MAX_BODY   # oversized bodies up to this are drained before the 413
 
 
 def make_handler(scheduler, webhook, profiling: bool = False):
@@ -48,8 +49,9 @@ def make_handler(scheduler, webhook, profiling: bool = False):
 
         def _body(self):
             """Request body, None when absent; b"" marks one over the 1 MiB cap
-            (route.go's MaxBytesReader), which is left unread: the connection
-            is closed after the reply instead of parsing its tail as a request."""
+            (route.go's MaxBytesReader).  A moderately oversized body is read
+            and discarded so the client, still sending, gets the 413 instead
+            of a broken pipe; either way the connection closes after the reply."""
             try:
                 n = int(self.headers.get("Content-Length") or 0)
             except ValueError:
@@ -58,6 +60,13 @@ def make_handler(scheduler, webhook, profiling: bool = False):
                 return None
             if n > MAX_BODY:
                 self.close_connection = True
+                if n <= DRAIN_LIMIT:
+                    left = n
+                    while left > 0:
+                        chunk = self.rfile.read(min(left, 1 << 16))
+                        if not chunk:
+                            break
+                        left -= len(chunk)
                 return b""
             return self.rfile.read(n)
 

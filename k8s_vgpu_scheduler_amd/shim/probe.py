@@ -150,6 +150,22 @@ def child_hwid(args) -> dict:
             "xccs": sorted({p[0] for p in places}), "places": places[:512]}
 
 
+def child_light(args) -> dict:
+    """A light tenant: one tiny kernel every 50 ms for --hold-s seconds (an
+    inference server idling between requests)."""
+    import torch
+
+    x = torch.zeros(1024, device="cuda")
+    n = 0
+    t_end = time.time() + args.hold_s
+    while time.time() < t_end:
+        x.add_(1)
+        torch.cuda.synchronize()
+        n += 1
+        time.sleep(0.05)
+    return {"mode": "light", "kernels": n}
+
+
 def child_region(args) -> dict:
     """Allocate through PyTorch under the shim and read the accounting back
     through the monitor's shared-region reader (what vGPUmonitor sees)."""
@@ -236,10 +252,19 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--hwid", action="store_true")
+    ap.add_argument("--hostile", action="store_true",
+                    help="child: rewrite the grant in the environment before the runtime starts "
+                         "(all CUs, 200 GiB, control disabled) -- the grant file must still win")
     args = ap.parse_args()
+    if args.child and args.hostile:
+        os.environ.pop("HIP_DEVICE_MEMORY_LIMIT_0", None)
+        os.environ["HIP_DEVICE_MEMORY_LIMIT"] = "200g"
+        os.environ["HSA_CU_MASK"] = "0:0-255"
+        os.environ["MIVGPU_DISABLE_CONTROL"] = "1"
     if args.child:
         fn = {"matmul": child_matmul, "stream": child_stream, "hwid": child_hwid,
-              "region": child_region, "mfma": child_mfma, "hipstream": child_hipstream}[args.child]
+              "region": child_region, "mfma": child_mfma, "hipstream": child_hipstream,
+              "light": child_light}[args.child]
         print(json.dumps(fn(args)), flush=True)
         return
     tmp = Path(os.environ.get("TMPDIR", "/tmp")) / f"mivgpu-probe-{os.getpid()}"

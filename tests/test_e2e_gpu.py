@@ -71,6 +71,29 @@ def test_pod_on_mi355x_end_to_end(cluster):
     r = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
     assert holder.returncode == 0 and r["mem_total_mib"] == 36864 and r["oom_probe"] == "allocated", err[-2000:]
 
+    # container utilisation (hami_container_device_utilization_ratio): a busy
+    # matmul pod next to this pod while it only holds memory
+    cl.submit(amd_pod("busy-b", mem=16384, cores=75))   # 192 CUs: can hold up to 75 % of the GPU
+    assert cl.schedule("default", "busy-b") == "node1"
+    env_b = container_env(cl.start_containers("default", "busy-b")[0])
+    env_b["PYTHONPATH"] = str(REPO)
+    holder2 = _probe(env, "matmul", "--n", "1024", "--iters", "2", "--oom-probe-mib", "1024", "--hold-s", "40",
+                     wait=False)
+    busy = _probe(env_b, "matmul", "--n", "8192", "--iters", "40000", wait=False)
+    try:
+        def util(pod):
+            return [v for l, v in samples(cl.metrics("mon_metrics"), "hami_container_device_utilization_ratio")
+                    if l.get("pod") == pod]
+        wait_for(lambda: [v for v in util("busy-b") if v > 50], 120, "the busy pod's utilisation above 50 %")
+        idle = util("llm-a")
+        assert idle and max(idle) < 5, idle
+    finally:
+        busy.kill()
+        busy.communicate()
+        holder2.kill()
+        holder2.communicate()
+    cl.delete_pod("default", "busy-b")
+
     over = _probe(env, "matmul", "--n", "1024", "--iters", "2", "--oom-probe-mib", "40000")
     assert over["oom_probe"] == "oom"
     hw = _probe(env, "hwid")

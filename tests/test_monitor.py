@@ -131,28 +131,179 @@ def test_context_bytes_split_out_of_the_usage(tmp_path):
     assert f"hami_vgpu_memory_used_bytes{lab} 1.587544064e+09" in text
 
 
-def test_active_tenants_from_the_share_board(tmp_path, monkeypatch):
-    """mivgpu_host_gpu_active_tenants counts board slots stamped in the last second."""
-    import struct
+def fake_kfd(root, occ: dict, bdf_loc=(0x11 << 8), gpu_id=4242):
+    """A KFD sysfs tree: one GPU node at PCI 0000:11:00.0 (FakeBackend GPU 0) and
+    ``occ`` = {host pid: cu_occupancy} on it."""
+    n = root / "topology" / "nodes" / "2"
+    n.mkdir(parents=True)
+    (n / "gpu_id").write_text(f"{gpu_id}\n")
+    (n / "properties").write_text(f"simd_count 1024\nsimd_per_cu 4\nlocation_id {bdf_loc}\ndomain 0\n")
+    cpu = root / "topology" / "nodes" / "0"
+    cpu.mkdir(parents=True)
+    (cpu / "gpu_id").write_text("0\n")
+    for pid, v in occ.items():
+        d = root / "proc" / str(pid) / f"stats_{gpu_id}"
+        d.mkdir(parents=True)
+        (d / "cu_occupancy").write_text(f"{v}\n")
+    return gpu_id
 
-    from k8s_vgpu_scheduler_amd.monitor import board as B
 
-    monkeypatch.setenv("MIVGPU_LOCK_DIR", str(tmp_path / "lock"))
-    (tmp_path / "lock").mkdir()
-    be = FakeBackend(n=2)
-    g0 = be.gpus()[0]
-    path = B.board_path(g0.bdf)
-    assert path.name == "mivgpu-board-0000-11-00-0"
-    now = B.now_ns()
-    slots = [(7, now - 10 ** 8), (8, now - 5 * 10 ** 8), (9, now - 5 * 10 ** 9), (0, now)] + [(0, 0)] * 60
-    path.write_bytes(b"".join(struct.pack("<QQ", t, l) for t, l in slots))
-    assert B.active_tenants(path, at_ns=now) == 2
+def test_active_tenants_from_kfd_wave_occupancy(tmp_path):
+    """mivgpu_host_gpu_active_tenants counts the processes with waves resident on
+    the GPU (KFD cu_occupancy) in the sampling window."""
+    from k8s_vgpu_scheduler_amd.monitor.occupancy import OccupancySampler, gpu_ids_by_bdf
+
+    kfd = tmp_path / "kfd"
+    gid = fake_kfd(kfd, {100: 12, 101: 0, 102: 4})
+    assert gpu_ids_by_bdf(kfd) == {"0000:11:00.0": gid}
+    occ = OccupancySampler(root=kfd)
+    occ.sample_once()
+    assert occ.active_tenants(gid) == 2
+    assert occ.share_pct(gid, [100]) == 75.0
     lister = ContainerLister(str(tmp_path), lambda: [])
     reg = CollectorRegistry()
-    reg.register(MonitorCollector(lister, be, "node1"))
+    reg.register(MonitorCollector(lister, FakeBackend(n=2), "node1", occupancy=occ))
     text = generate_latest(reg).decode()
     assert 'mivgpu_host_gpu_active_tenants{device_index="0",device_uuid="GPU-0000",node="node1"} 2.0' in text
-    assert 'device_index="1"' not in text.split("mivgpu_host_gpu_active_tenants")[-1]   # no board, no series
+    assert 'device_index="1"' not in text.split("mivgpu_host_gpu_active_tenants")[-1]   # no KFD node, no series
+
+
+def test_container_utilization_from_shim_or_kfd(tmp_path):
+    """hami_container_device_utilization_ratio: the shim's own occupancy share
+    (util_pct) when it reports one, else the monitor's KFD sample of the
+    container's host pids (metrics.go:468-497 exports DeviceSmUtil)."""
+    from k8s_vgpu_scheduler_amd.monitor.occupancy import OccupancySampler
+
+    kfd = tmp_path / "kfd"
+    fake_kfd(kfd, {100: 12, 102: 4})
+    occ = OccupancySampler(root=kfd)
+    occ.sample_once()
+    busy = make_container(tmp_path, "u1", "main", uuid="GPU-0000")
+    busy.r.procs[0].hostpid = 100                    # no shim util: monitor's KFD share 12 / 16
+    busy.close()
+    rep = make_container(tmp_path, "u2", "main", uuid="GPU-0000")
+    rep.r.procs[0].util[0].share_ns, rep.r.procs[0].util[0].util_pct = 5 * 10 ** 9, 40
+    rep.close()
+    idle = make_container(tmp_path, "u3", "main", uuid="GPU-0000")
+    idle.r.procs[0].hostpid = 999                    # holds the GPU, no waves
+    idle.close()
+    lister = ContainerLister(str(tmp_path), lambda: [pod("u1", "busy"), pod("u2", "rep"), pod("u3", "idle")])
+    lister.update()
+    reg = CollectorRegistry()
+    reg.register(MonitorCollector(lister, FakeBackend(n=1), "node1", occupancy=occ))
+    text = generate_latest(reg).decode()
+
+    def util(p):
+        pre = f'hami_container_device_utilization_ratio{{container="main",device_uuid="GPU-0000",namespace="default",pod="{p}",vdevice_index="0"}} '
+        return float(text.split(pre)[1].split()[0])
+    assert util("busy") == 75.0
+    assert util("rep") == 40.0
+    assert util("idle") == 0.0
+
+
+def test_partition_info_and_legacy_series(tmp_path):
+    """Per-container partition identity (the hami_mig_device_info analogue) and
+    the --legacy-metrics names (cmd/vGPUmonitor/metrics.go:133-212)."""
+    make_container(tmp_path, "u1", "main", uuid="GPU-0001-cpx3", used=300 << 20, limit=2 << 30).close()
+    lister = ContainerLister(str(tmp_path), lambda: [pod("u1", "p1", "ns1")])
+    lister.update()
+    be = FakeBackend(n=2)
+    be.modes[1] = "CPX"
+    reg = CollectorRegistry()
+    reg.register(MonitorCollector(lister, be, "node1", legacy=True))
+    text = generate_latest(reg).decode()
+    assert ('mivgpu_container_partition_info{compute_partition="CPX",container="main",cus="32",'
+            'device_uuid="GPU-0001-cpx3",memory_partition="NPS1",namespace="ns1",partition_index="3",'
+            'physical_index="1",pod="p1",vdevice_index="0"} 1.0') in text
+    assert 'vGPU_device_memory_usage_in_bytes{ctrname="main",deviceuuid="GPU-0001-cpx3",podname="p1",podnamespace="ns1",vdeviceid="0"} 3.145728e+08' in text
+    assert 'vGPU_device_memory_limit_in_bytes{' in text
+    assert 'Device_memory_desc_of_container{context="0",ctrname="main",data="314572800"' in text
+    assert 'HostGPUMemoryUsage{deviceidx="0"' in text and "HostCoreUtilization{" in text
+    reg2 = CollectorRegistry()
+    reg2.register(MonitorCollector(lister, be, "node1"))
+    assert "HostGPUMemoryUsage" not in generate_latest(reg2).decode()
+
+
+def test_region_limits_reconciled_against_the_grant(tmp_path):
+    """A tenant that rewrites its region's limits (the region file is in a
+    read-write mount) is put back to the grant the device plugin wrote."""
+    from k8s_vgpu_scheduler_amd.deviceplugin.allocate import grant_text
+
+    make_container(tmp_path, "u1", "main", limit=1 << 30).close()
+    limits = tmp_path / "vgpu" / "limits"
+    limits.mkdir(parents=True)
+    (limits / "u1_main.conf").write_text(grant_text({
+        "HIP_DEVICE_MEMORY_LIMIT_0": "1024m", "HSA_CU_MASK": "0:0-63", "HIP_DEVICE_CORE_LIMIT": "25",
+        "MIVGPU_SHARED_CACHE": "/usr/local/vgpu/x.cache", "NOT_A_GRANT_KEY": "1"}))
+    assert "NOT_A_GRANT_KEY" not in (limits / "u1_main.conf").read_text()
+    lister = ContainerLister(str(tmp_path), lambda: [pod("u1", "p1")])
+    lister.update()
+    r = lister.list_containers()[0].region
+    r.r.cu_limit[0], r.r.cu_mask_count[0] = 25, 64
+    assert feedback.reconcile_limits(lister) == 0          # consistent: nothing to do
+    r.r.mem_limit[0], r.r.cu_limit[0], r.r.cu_mask_count[0], r.r.core_policy = 64 << 30, 100, 0, 2
+    assert feedback.reconcile_limits(lister) == 4
+    assert (r.r.mem_limit[0], r.r.cu_limit[0], r.r.cu_mask_count[0], r.r.core_policy) == (1 << 30, 25, 64, 0)
+
+
+def test_feedback_pauses_while_a_partition_apply_holds_the_lock(tmp_path):
+    """cmd/vGPUmonitor/main.go:79-109: no feedback pass while the device plugin
+    reconfigures compute partitions."""
+    import threading
+
+    from k8s_vgpu_scheduler_amd.cmd.monitor import watch_partition_lock
+
+    lock = tmp_path / "lockdir" / "partition-apply.lock"
+    lock.parent.mkdir()
+    pause, stop = threading.Event(), threading.Event()
+    t = threading.Thread(target=watch_partition_lock, args=(pause, stop, str(lock), 0.02), daemon=True)
+    t.start()
+    lock.write_text("applying")
+    deadline = time.time() + 5
+    while not pause.is_set() and time.time() < deadline:
+        time.sleep(0.02)
+    assert pause.is_set()
+    # a paused loop does not touch the regions
+    make_container(tmp_path, "a", "c", priority=1, recent=2).close()
+    make_container(tmp_path, "b", "c", priority=1, recent=2).close()
+    lister = ContainerLister(str(tmp_path), lambda: [pod("a", "a"), pod("b", "b")])
+    lister.update()
+    fb_stop = threading.Event()
+    fb = threading.Thread(target=feedback.watch_and_feedback, args=(lister, fb_stop, 0.02, pause), daemon=True)
+    fb.start()
+    time.sleep(0.3)
+    assert all(c.region.utilization_switch() == 0 for c in lister.list_containers())
+    lock.unlink()
+    deadline = time.time() + 5
+    while time.time() < deadline and not all(c.region.utilization_switch() == 1 for c in lister.list_containers()):
+        time.sleep(0.02)
+    assert not pause.is_set()
+    assert all(c.region.utilization_switch() == 1 for c in lister.list_containers())
+    stop.set()
+    fb_stop.set()
+
+
+def test_node_scoped_pod_informer():
+    """The monitor watches only its node's pods (field selector spec.nodeName,
+    pkg/monitor/nvidia/cudevshr.go:308); a pod bound to the node later enters
+    the cache, one deleted leaves it."""
+    from k8s_vgpu_scheduler_amd.k8s.fake import FakeCluster
+    from k8s_vgpu_scheduler_amd.k8s.informer import Informer
+
+    kc = FakeCluster()
+    mk = lambda n, node: {"metadata": {"name": n, "namespace": "d", "uid": n}, "spec": {"nodeName": node}}  # noqa: E731
+    kc.create("pods", mk("here", "n1"))
+    kc.create("pods", mk("there", "n2"))
+    kc.create("pods", mk("pending", ""))
+    inf = Informer(kc, "pods", field_selector={"spec.nodeName": "n1"})
+    inf.start()
+    assert [p["metadata"]["name"] for p in inf.list()] == ["here"]
+    kc.patch("pods", "pending", {"spec": {"nodeName": "n1"}}, "d")
+    assert sorted(p["metadata"]["name"] for p in inf.list()) == ["here", "pending"]
+    kc.patch("pods", "there", {"metadata": {"labels": {"x": "1"}}}, "d")   # other node: never seen
+    assert "there" not in [p["metadata"]["name"] for p in inf.list()]
+    kc.delete("pods", "here", "d")
+    assert [p["metadata"]["name"] for p in inf.list()] == ["pending"]
 
 
 def test_feedback_loop_fills_host_pids(tmp_path, monkeypatch):

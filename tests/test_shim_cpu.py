@@ -215,7 +215,8 @@ def _fake_kfd(root, gpu_nodes):
         n = root / "topology" / "nodes" / str(i)
         n.mkdir(parents=True)
         (n / "gpu_id").write_text(f"{gid}\n")
-        (n / "properties").write_text(f"cpu_cores_count 0\nsimd_count 1024\nlocation_id {loc}\ndomain {dom}\n")
+        (n / "properties").write_text(f"cpu_cores_count 0\nsimd_count 1024\nsimd_per_cu 4\nlocation_id {loc}\n"
+                                      f"domain {dom}\n")
     return root
 
 
@@ -281,56 +282,100 @@ def test_stale_context_charge_is_refreshed_before_oom(native_build, tmp_path):
     assert out[4]["bytes"] == 3500 << 20
 
 
-def _board(path):
-    import struct
-    raw = open(path, "rb").read()
-    return [struct.unpack_from("<QQ", raw, 16 * i) for i in range(len(raw) // 16)]
+def _occ(kfd, pid, gid, v):
+    d = kfd / "proc" / str(pid) / f"stats_{gid}"
+    d.mkdir(parents=True, exist_ok=True)
+    (d / "cu_occupancy").write_text(f"{v}\n")
 
 
-def test_share_board_counts_tenants_per_physical_gpu(native_build, tmp_path):
-    """Every shimmed process stamps its launches into one board per physical
-    GPU (PCI location) in the node-wide lock dir; slots are released at exit."""
-    lock = tmp_path / "vgpulock"
-    e = dict(os.environ, MOCKHIP_TOTAL_MIB="65536", LD_PRELOAD=str(native_build["shim"]), MIVGPU_LOCK_DIR=str(lock))
-    ps = []
-    for i in range(3):
-        env = dict(e, MIVGPU_SHARED_CACHE=str(tmp_path / f"t{i}.cache"))   # three containers
-        ps.append(subprocess.Popen([str(native_build["driver"]), "launch", "3", "sleep", "2500"], env=env,
-                                   stdout=subprocess.PIPE, text=True))
-    for p in ps:
+def _sample_util(native_build, tmp_path, kfd, cache, extra_env=None, wait_s=1.3):
+    e = dict(os.environ, MOCKHIP_TOTAL_MIB="65536", MIVGPU_SHARED_CACHE=str(tmp_path / cache),
+             LD_PRELOAD=str(native_build["shim"]), **_kfd_env(kfd), **(extra_env or {}))
+    # kfdctx 0: the KFD process entry exists (as it does once a process opens the GPU)
+    p = subprocess.Popen([str(native_build["driver"]), "kfdctx", "0", "alloc", "100", "launch", "3", "sleep", "3000"],
+                         env=e, stdout=subprocess.PIPE, text=True)
+    for _ in range(3):
         json.loads(p.stdout.readline())
-    board = lock / "mivgpu-board-0000-75-00-0"          # the mock's device 0: domain 0, bus 0x75, device 0
-    slots = [s for s in _board(board) if s[0]]
-    assert len(slots) == 3 and len({t for t, _ in slots}) == 3
-    assert max(t for _, t in slots) - min(t for _, t in slots) < 2 * 10 ** 9
-    for p in ps:
-        p.wait(timeout=30)
-    assert [s for s in _board(board) if s[0]] == []  # released at exit
-    # opt-out: no board
-    lock2 = tmp_path / "lock2"
-    run(native_build, tmp_path, "launch", 2, env={"MIVGPU_LOCK_DIR": str(lock2), "MIVGPU_SHARE_BOARD": "0"},
-        cache="o.cache")
-    assert not lock2.exists() or not any(lock2.iterdir())
-
-
-def test_share_board_reclaims_silent_slots(native_build, tmp_path):
-    """A full board whose slots all went silent long ago (crashed tenants that
-    never released them): a new tenant takes one over, and frees it at exit."""
-    import struct
-
-    lock = tmp_path / "vgpulock"
-    lock.mkdir()
-    board = lock / "mivgpu-board-0000-75-00-0"
-    board.write_bytes(b"".join(struct.pack("<QQ", 1000 + i, 1) for i in range(64)))   # stamped at t = 1 ns
-    e = dict(os.environ, MOCKHIP_TOTAL_MIB="65536", LD_PRELOAD=str(native_build["shim"]), MIVGPU_LOCK_DIR=str(lock),
-             MIVGPU_SHARED_CACHE=str(tmp_path / "r.cache"))
-    p = subprocess.Popen([str(native_build["driver"]), "launch", "2", "sleep", "2000"], env=e, stdout=subprocess.PIPE,
-                         text=True)
-    json.loads(p.stdout.readline())
-    slots = _board(board)
-    fresh = [i for i, (tok, last) in enumerate(slots) if last > 1]
-    assert len(fresh) == 1 and slots[fresh[0]][0] not in range(1000, 1064)   # one stale slot taken over
+    t0 = time.monotonic()
+    time.sleep(wait_s)
+    reg = R.SharedRegion(str(tmp_path / cache))
+    u = reg.active_procs()[0].util[0]
+    out = {"util_pct": u.util_pct, "share_ns": u.share_ns, "occupancy": u.occupancy,
+           "elapsed_ns": int((time.monotonic() - t0) * 1e9)}
+    reg.close()
     p.wait(timeout=30)
-    slots = _board(board)
-    assert slots[fresh[0]][0] == 0                                          # released at exit
-    assert sum(1 for tok, _ in slots if tok) == 63                           # the other stale slots untouched
+    return out
+
+
+def test_occupancy_sampler_measures_the_gpu_share(native_build, tmp_path):
+    """The shim samples KFD's per-process wave counts (cu_occupancy) of itself
+    and of every other process on its GPU and integrates its share of the
+    resident waves: own 30 vs neighbours 10 -> 75 % of the GPU received,
+    published as util_pct / share_ns for the monitor and the gate kernel."""
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0), (5151, 0x85 << 8, 0)])
+    _occ(kfd, 987654, 4242, 30)      # this process (the mock's KFD pid)
+    _occ(kfd, 111, 4242, 10)         # a neighbour on the same GPU
+    _occ(kfd, 222, 5151, 500)        # a process on another GPU: not a competitor
+    _occ(kfd, 333, 4242, 0)          # an idle neighbour: costs nothing
+    r = _sample_util(native_build, tmp_path, kfd, "occ.cache")
+    assert r["occupancy"] == 30
+    assert 70 <= r["util_pct"] <= 76, r
+    # the integral grows at ~0.75 GPU-ns per ns
+    assert 0.5 * 0.75 * r["elapsed_ns"] <= r["share_ns"] <= 0.75 * (r["elapsed_ns"] + 1.5e9), r
+
+
+def test_occupancy_share_capped_by_the_cu_mask(native_build, tmp_path):
+    """A CU-masked tenant cannot hold more of the GPU than its CUs: alone on the
+    GPU with a 64-of-256-CU mask it is charged 25 %, not 100 %."""
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
+    _occ(kfd, 987654, 4242, 8)
+    r = _sample_util(native_build, tmp_path, kfd, "mask.cache", {"HSA_CU_MASK": "0:0-63"})
+    assert 23 <= r["util_pct"] <= 26, r
+    unmasked = _sample_util(native_build, tmp_path, kfd, "nomask.cache")
+    assert unmasked["util_pct"] >= 97, unmasked
+
+
+def test_occupancy_sampler_off_without_kfd_or_opted_out(native_build, tmp_path):
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
+    _occ(kfd, 987654, 4242, 30)
+    r = _sample_util(native_build, tmp_path, kfd, "off.cache", {"MIVGPU_OCCUPANCY": "0"}, wait_s=0.8)
+    assert r["share_ns"] == 0 and r["util_pct"] == 0
+
+
+def _grant(tmp_path, **kv):
+    f = tmp_path / "limits.conf"
+    f.write_text("".join(f"{k}={v}\n" for k, v in kv.items()))
+    return str(f)
+
+
+def test_grant_file_overrides_a_rewritten_environment(native_build, tmp_path):
+    """The device plugin's read-only grant file is the only source of the
+    limits: a tenant that raises HIP_DEVICE_MEMORY_LIMIT_0, sets
+    MIVGPU_DISABLE_CONTROL or points MIVGPU_SHARED_CACHE at a private region
+    still gets its 1 GiB."""
+    cache = tmp_path / "granted.cache"
+    grant = _grant(tmp_path, HIP_DEVICE_MEMORY_LIMIT_0="1024m", MIVGPU_SHARED_CACHE=str(cache))
+    env = {"MIVGPU_LIMITS_FILE": grant, "HIP_DEVICE_MEMORY_LIMIT_0": "64g", "MIVGPU_DISABLE_CONTROL": "1"}
+    out = run(native_build, tmp_path, "meminfo", "alloc", 2000, "alloc", 900, env=env, cache="private.cache")
+    assert out[0]["total_mib"] == 1024
+    assert out[1]["rc"] == 2 and out[2]["rc"] == 0
+    assert cache.exists() and not (tmp_path / "private.cache").exists()
+    # without a grant file the environment is the configuration
+    out = run(native_build, tmp_path, "meminfo", env={"HIP_DEVICE_MEMORY_LIMIT_0": "2048m"}, cache="env.cache")
+    assert out[0]["total_mib"] == 2048
+
+
+def test_cu_mask_reasserted_before_rocr_reads_it(native_build, tmp_path):
+    """hsa_init is interposed: the granted HSA_CU_MASK / ROCR_VISIBLE_DEVICES
+    are back in the environment when ROCr reads them, whatever the tenant set."""
+    grant = _grant(tmp_path, HSA_CU_MASK="0:64-127", ROCR_VISIBLE_DEVICES="GPU-60126e549ca79192",
+                   HIP_DEVICE_MEMORY_LIMIT_0="1024m")
+    out = run(native_build, tmp_path, "hsainit",
+              env={"MIVGPU_LIMITS_FILE": grant, "HSA_CU_MASK": "0:0-255", "ROCR_VISIBLE_DEVICES": "0,1"})
+    assert out[0]["hooked"] == 1
+    assert out[0]["mask"] == "0:64-127" and out[0]["visible"] == "GPU-60126e549ca79192"
+    e = {k: v for k, v in os.environ.items() if k != "HSA_CU_MASK"}
+    e.update({"MIVGPU_LIMITS_FILE": grant, "MOCKHIP_TOTAL_MIB": "65536", "LD_PRELOAD": str(native_build["shim"]),
+              "MIVGPU_SHARED_CACHE": str(tmp_path / "u.cache")})
+    p = subprocess.run([str(native_build["driver"]), "hsainit"], env=e, stdout=subprocess.PIPE, text=True, timeout=60)
+    assert json.loads(p.stdout.splitlines()[0])["mask"] == "0:64-127"   # unset by the tenant: restored
