@@ -604,7 +604,14 @@ bool open_region() {
   return true;
 }
 
+// Set first thing at exit: the background threads (governor stamper,
+// occupancy sampler) stop issuing HIP calls before the runtime tears down.
+std::atomic<bool> g_exiting{false};
+void quiesce_background_threads();
+
 void on_exit_release() {
+  g_exiting.store(true, std::memory_order_release);
+  quiesce_background_threads();
   if (!g_region || g_slot < 0) return;
   lock_region();
   reclaim_slot_locked(g_slot);
@@ -1285,6 +1292,7 @@ void* occ_main(void*) {
     bool fast = false;
     for (int d = 0; d < g_num_devices; ++d) fast |= t - g_last_gate_ns[d].load(std::memory_order_relaxed) < 1000000000ull;
     usleep((useconds_t)((fast ? g_cfg.occ_period_ns : g_cfg.occ_idle_period_ns) / 1000));
+    if (g_exiting.load(std::memory_order_acquire)) return nullptr;
     Guard g;
     const uint64_t now = mono_ns();
     for (int d = 0; d < g_num_devices; ++d) {
@@ -1387,6 +1395,16 @@ constexpr uint64_t kStampIdleNs = 1000000;  // 1 ms
 void enqueue_gate_locked(int dev, DeviceGate& G, int slot, hipStream_t stream, uint64_t now);
 bool stream_capturing(hipStream_t stream);
 
+// Wait out a stamper that is inside an enqueue (it holds G.mu), so no gate
+// launch races the runtime's teardown; later passes see g_exiting and stop.
+void quiesce_background_threads() {
+  for (int d = 0; d < MIVGPU_MAX_DEVICES; ++d) {
+    DeviceGate& G = g_gates[d];
+    if (!G.stamper_started) continue;
+    std::lock_guard<std::mutex> lk(G.mu);
+  }
+}
+
 void* stamper_main(void* arg) {
   const int dev = (int)(intptr_t)arg;
   DeviceGate& G = g_gates[dev];
@@ -1399,6 +1417,7 @@ void* stamper_main(void* arg) {
     usleep(500);
     Guard g;
     std::lock_guard<std::mutex> lk(G.mu);
+    if (g_exiting.load(std::memory_order_acquire)) return nullptr;
     const uint64_t now = mono_ns();
     for (int i = 0; i < 64; ++i) {
       GateSlot& S = G.slots[i];

@@ -50,12 +50,16 @@ def test_cu_partition_scales_matrix_core_throughput():
 
 def test_governor_duty_cycle_on_handwritten_load():
     tmp = tempfile.mkdtemp(prefix="mivgpu-lg-")
-    full = run_child("mfma", {}, False, ["--iters", "60"])
+    probe = run_child("mfma", {}, False, ["--iters", "60"])
+    assert probe["rc"] == 0, probe.get("stderr")
+    # ~1.5 s of work unthrottled: the bucket's 100 ms burst is a small part of it
+    iters = str(max(60, int(60 * 1.5 / max(probe["seconds"], 1e-3))))
+    full = run_child("mfma", {}, False, ["--iters", iters])
     half = run_child("mfma", {"MIVGPU_SHARED_CACHE": os.path.join(tmp, "g.cache"), "HIP_DEVICE_CORE_LIMIT": "50",
-                              "GPU_CORE_UTILIZATION_POLICY": "force"}, True, ["--iters", "60"])
+                              "GPU_CORE_UTILIZATION_POLICY": "force"}, True, ["--iters", iters])
     assert full["rc"] == 0 and half["rc"] == 0, half.get("stderr")
     ratio = half["tflops"] / full["tflops"]
-    assert 0.35 <= ratio <= 0.65, ratio
+    assert 0.42 <= ratio <= 0.6, ratio
     assert half["gates"] > 0
 
 
