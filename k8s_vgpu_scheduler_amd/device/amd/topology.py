@@ -9,7 +9,10 @@ same and the scorer's job is to (a) prefer xGMI over PCIe peers (mixed or
 partitioned systems) and (b) steer around degraded links, measured as the
 min/max xGMI bandwidth amd-smi reports.  Pair score:
 
-    xGMI:  100 * links * min(1, bw_GBps / nominal_GBps)   (nominal 64 GB/s per link per direction)
+    xGMI:  100 * links * min(1, bw_GBps / nominal_GBps) / hops
+           (nominal 76 GB/s per link per direction: KFD io_link min = max
+           bandwidth 76000 MB/s on every GPU pair of a healthy 8 x MI355X
+           node, = amd-smi link_metrics 608 Gb/s; tests/fixtures/mi355x_8gpu_kfd_links.json)
     PCIe:  20 same NUMA node, 10 cross-socket
     none:  0
 """
@@ -18,7 +21,7 @@ from __future__ import annotations
 
 from itertools import combinations
 
-XGMI_NOMINAL_GBPS = 64.0
+XGMI_NOMINAL_GBPS = 76.0
 
 
 def pair_score(link_type: str, hops: int = 1, links: int = 1, bw_gbps: float | None = None,

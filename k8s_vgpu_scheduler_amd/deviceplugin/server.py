@@ -361,34 +361,86 @@ class AMDDevicePlugin:
             self.server.stop(grace=1)
 
 
+def _sock_id(path: str):
+    """(inode, ctime) of a socket file, None if absent: a re-created socket
+    (kubelet restart) has a new identity even at the same path."""
+    try:
+        st = os.stat(path)
+    except OSError:
+        return None
+    return (st.st_ino, st.st_ctime_ns)
+
+
 def run_with_restarts(make_plugin, kubelet_socket: str, max_restarts: int = 5, window_s: float = 3600.0,
-                      stop: threading.Event | None = None, reload: threading.Event | None = None):
-    """server.go:518-566: restart a crashed plugin; >max_restarts within the window is fatal.
-    Setting `reload` (device list changed, e.g. a new compute-partition mode)
-    restarts the endpoint without counting as a crash."""
+                      stop: threading.Event | None = None, reload: threading.Event | None = None,
+                      poll_s: float = 1.0, restart_grace_s: float = 10.0, stats: dict | None = None):
+    """Keep the plugin registered with the kubelet.
+
+    * A kubelet restart is not a crash (main.go:305-337 restarts the plugins
+      when the kubelet socket is re-created): the kubelet wipes the
+      device-plugins directory, our socket included, and creates a new
+      kubelet.sock; the plugin waits for it and re-registers.
+    * ``reload`` (the device list changed, e.g. a new compute-partition mode)
+      re-registers without counting as a crash.
+    * Anything else that stops the plugin is a crash; more than
+      ``max_restarts`` within ``window_s`` is fatal (server.go:518-566).
+    ``stats`` (optional) counts crashes / kubelet restarts / reloads."""
     stop = stop or threading.Event()
     reload = reload or threading.Event()
+    stats = stats if stats is not None else {}
+    for k in ("crashes", "kubelet_restarts", "reloads", "registrations"):
+        stats.setdefault(k, 0)
     restarts: list[float] = []
+    waiting_logged = False
     while not stop.is_set():
+        kubelet_id = _sock_id(kubelet_socket)
+        if kubelet_id is None:
+            if not waiting_logged:
+                log.info("waiting for the kubelet socket %s", kubelet_socket)
+                waiting_logged = True
+            stop.wait(poll_s)
+            continue
+        waiting_logged = False
         plugin = make_plugin()
         try:
             plugin.start(kubelet_socket)
-            while not stop.wait(1.0):
+            stats["registrations"] += 1
+            while not stop.wait(poll_s):
                 if reload.is_set():
                     reload.clear()
+                    stats["reloads"] += 1
                     log.info("device list changed: re-registering the plugin with the kubelet")
                     break
+                if _sock_id(kubelet_socket) != kubelet_id:
+                    stats["kubelet_restarts"] += 1
+                    log.info("kubelet socket %s gone or re-created (kubelet restart): re-registering",
+                             kubelet_socket)
+                    break
                 if not os.path.exists(plugin.socket):
-                    raise RuntimeError("plugin socket disappeared (kubelet restarted?)")
-                if not os.path.exists(kubelet_socket):
-                    raise RuntimeError("kubelet socket disappeared")
+                    # the kubelet removes plugin sockets when it restarts, possibly
+                    # before its own socket is re-created: give it a grace period
+                    deadline = time.monotonic() + restart_grace_s
+                    while time.monotonic() < deadline and _sock_id(kubelet_socket) == kubelet_id:
+                        if stop.wait(min(poll_s, 0.2)):
+                            return
+                    if _sock_id(kubelet_socket) != kubelet_id:
+                        stats["kubelet_restarts"] += 1
+                        log.info("kubelet restarted (plugin socket removed, kubelet socket re-created)")
+                        break
+                    raise RuntimeError("plugin socket disappeared while the kubelet kept running")
         except Exception as e:  # noqa: BLE001
-            log.error("device plugin crashed: %s", e)
-            now = time.time()
-            restarts = [t for t in restarts if now - t < window_s] + [now]
-            if len(restarts) > max_restarts:
-                raise RuntimeError(f"device plugin restarted more than {max_restarts} times within "
-                                   f"{window_s}s") from e
-            time.sleep(1.0)
+            if _sock_id(kubelet_socket) is None or _sock_id(kubelet_socket) != kubelet_id:
+                # registration raced a kubelet restart: not the plugin's fault
+                stats["kubelet_restarts"] += 1
+                log.info("kubelet went away during registration (%s); waiting for it", e)
+            else:
+                stats["crashes"] += 1
+                log.error("device plugin crashed: %s", e)
+                now = time.time()
+                restarts = [t for t in restarts if now - t < window_s] + [now]
+                if len(restarts) > max_restarts:
+                    raise RuntimeError(f"device plugin restarted more than {max_restarts} times within "
+                                       f"{window_s}s") from e
+                stop.wait(poll_s)
         finally:
             plugin.stop()

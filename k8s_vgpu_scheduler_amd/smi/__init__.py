@@ -63,7 +63,34 @@ class LinkInfo:
     type: str        # "XGMI" | "PCIE" | "NONE"
     hops: int = 1
     links: int = 1
-    max_bw_gbps: float | None = None
+    max_bw_gbps: float | None = None    # per direction; a degraded link reports less than nominal
+    weight: int | None = None           # KFD io_link weight (lower = closer: xGMI 15, PCIe 20 on MI355X)
+
+
+# KFD io_link types (kfd_crat.h CRAT_IOLINK_TYPE_*); measured on an 8 x MI355X
+# node (scripts/probe/topology_probe.py, tests/fixtures/mi355x_8gpu_kfd_links.json):
+# GPU<->GPU type 11 (xGMI), weight 15, min = max bandwidth 76000 MB/s (= the
+# 608 Gb/s per link amd-smi link_metrics reports); GPU<->CPU type 2 (PCIe),
+# weight 20, 64000 MB/s.
+KFD_IOLINK_PCIE, KFD_IOLINK_XGMI = 2, 11
+
+
+def kfd_link(root: Path, node_a: str, node_b: str) -> LinkInfo | None:
+    """The io_link from KFD topology node ``node_a`` to ``node_b`` (None: none)."""
+    base = root / str(node_a) / "io_links"
+    try:
+        entries = list(base.iterdir())
+    except OSError:
+        return None
+    for e in entries:
+        p = _kfd_props(e)
+        if str(p.get("node_to")) != str(node_b):
+            continue
+        t = p.get("type")
+        kind = "XGMI" if t == KFD_IOLINK_XGMI else ("PCIE" if t == KFD_IOLINK_PCIE else "NONE")
+        bws = [v for v in (p.get("min_bandwidth"), p.get("max_bandwidth")) if v]
+        return LinkInfo(kind, 1, 1, (min(bws) / 1000.0) if bws else None, p.get("weight"))   # MB/s -> GB/s
+    return None
 
 
 @dataclass
@@ -140,6 +167,62 @@ def _group_physical(out: list[GPUInfo]) -> list[GPUInfo]:
     return out
 
 
+# ------------------------------------------------------------ device identity
+# One identity whatever the backend (amd-smi published
+# "AMD Radeon Graphics" and its own UUID format while sysfs published the
+# board name and GPU-<unique_id>, so a node falling back from one backend to
+# the other changed every device id under live allocations):
+#   uuid = rocr_id = "GPU-<KFD unique_id, 16 lower-case hex>", the id ROCr
+#          accepts in ROCR_VISIBLE_DEVICES (docs/develop/amd-vgpu.md:174-180;
+#          amd-smi reports the same value as enumeration_info.hip_uuid and,
+#          on MI355X, as asic_serial);
+#   name = the board's product name (amd-smi board_info.product_name = sysfs
+#          product_name, "AMD Instinct MI355 OAM"), never the generic
+#          "AMD Radeon Graphics" libdrm answers when its id table is missing.
+GENERIC_NAMES = {"", "amd radeon graphics", "n/a", "na", "unknown"}
+DEVICE_ID_NAMES = {0x75A3: "AMD Instinct MI355X", 0x75A0: "AMD Instinct MI350X", 0x74A1: "AMD Instinct MI300X",
+                   0x74A5: "AMD Instinct MI325X"}
+
+
+def canonical_name(*candidates, device_id: int | None = None) -> str:
+    for c in candidates:
+        if c and str(c).strip().lower() not in GENERIC_NAMES:
+            return str(c).strip()
+    return DEVICE_ID_NAMES.get(device_id or 0, "AMD Instinct MI355X")
+
+
+def rocr_uuid(unique_id) -> str | None:
+    """``GPU-<16 hex>`` from a KFD unique_id / asic serial (int or hex string)."""
+    if unique_id in (None, "", 0, "0"):
+        return None
+    try:
+        v = int(unique_id, 16) if isinstance(unique_id, str) else int(unique_id)
+    except ValueError:
+        return None
+    return f"GPU-{v:016x}" if v else None
+
+
+def _dedupe_partition_ids(out: list[GPUInfo]) -> list[GPUInfo]:
+    """Compute partitions of one package may share the package's unique id:
+    suffix ``-<mode><partition>`` (and address them by index) so every
+    schedulable device keeps a distinct id."""
+    seen: dict[str, int] = {}
+    for g in out:
+        seen[g.uuid] = seen.get(g.uuid, 0) + 1
+    for g in out:
+        if seen[g.uuid] > 1:
+            g.uuid = f"{g.uuid}-{g.compute_partition.lower()}{g.partition_index}"
+            g.rocr_id = str(g.index)
+    return out
+
+
+def _sysfs_product_name(bdf: str) -> str:
+    try:
+        return Path(f"/sys/bus/pci/devices/{bdf}/product_name").read_text().strip()
+    except OSError:
+        return ""
+
+
 # ------------------------------------------------------------------- amd-smi
 def _handle_key(h) -> int | None:
     """amd-smi processor handles come back as ctypes pointers or plain ints."""
@@ -172,8 +255,8 @@ class AmdSmiBackend(Backend):
                     return getattr(m, fn)(h, *a)
                 except Exception:  # noqa: BLE001
                     return default
-            uuid = q("amdsmi_get_gpu_device_uuid", default=f"gpu-{i}")
             asic = q("amdsmi_get_gpu_asic_info", default={}) or {}
+            board = q("amdsmi_get_gpu_board_info", default={}) or {}
             total = q("amdsmi_get_gpu_memory_total", m.AmdSmiMemoryType.VRAM, default=0) or 0
             numa = q("amdsmi_topo_get_numa_node_number", default=0) or 0
             bdf = q("amdsmi_get_gpu_device_bdf", default="") or ""
@@ -181,16 +264,26 @@ class AmdSmiBackend(Backend):
             kfd = q("amdsmi_get_gpu_kfd_info", default={}) or {}
             part = q("amdsmi_get_gpu_compute_partition", default="SPX") or "SPX"
             cus = int(asic.get("num_of_compute_units") or asic.get("num_compute_units") or 256)
-            rocr = _rocr_id_from_kfd(kfd.get("node_id")) or str(i)
-            g = GPUInfo(index=i, uuid=str(uuid), rocr_id=rocr,
-                        name=str(asic.get("market_name") or "AMD Instinct MI355X"),
+            rocr = (_rocr_id_from_kfd(kfd.get("node_id")) or
+                    (str(enum.get("hip_uuid")).lower() if str(enum.get("hip_uuid", "")).startswith("GPU-") else None)
+                    or rocr_uuid(asic.get("asic_serial")))
+            uuid = rocr or str(q("amdsmi_get_gpu_device_uuid", default=f"gpu-{i}"))
+            try:
+                did = int(str(asic.get("device_id", "0")), 0)
+            except ValueError:
+                did = 0
+            g = GPUInfo(index=i, uuid=uuid, rocr_id=rocr or str(i),
+                        name=canonical_name(board.get("product_name"), asic.get("market_name"),
+                                            _sysfs_product_name(str(bdf)), device_id=did),
                         memory_mib=int(total) // (1 << 20), cus=cus, numa=max(0, int(numa)), bdf=str(bdf),
                         render_minor=int(enum.get("drm_render", -1) if isinstance(enum.get("drm_render"), int) else -1),
                         card_minor=int(enum.get("drm_card", -1) if isinstance(enum.get("drm_card"), int) else -1),
-                        compute_partition=str(part))
-            self._by_uuid[g.uuid] = h
-            out.append(g)
-        return _group_physical(out)
+                        compute_partition=str(part),
+                        extra={"kfd_node": kfd.get("node_id"), "gpu_id": kfd.get("kfd_id")})
+            out.append((g, h))
+        gs = _dedupe_partition_ids(_group_physical([g for g, _ in out]))
+        self._by_uuid = {g.uuid: h for g, h in zip(gs, (h for _, h in out))}
+        return gs
 
     def set_compute_partition(self, physical_index: int, mode: str) -> None:
         mode = mode.upper()
@@ -218,22 +311,36 @@ class AmdSmiBackend(Backend):
         return self._by_uuid.get(g.uuid) or self.handles[g.index]
 
     def link(self, a, b):
+        """Link type from the AmdSmiLinkType enum (PCIE = 1, XGMI = 2 in this
+        amd-smi; the names are resolved, not the numbers), hops, KFD weight and
+        the min/max bandwidth (MB/s, the KFD io_link unit) -- the weaker bound
+        counts, so a degraded link scores lower.  Falls back to the KFD io_links
+        when amd-smi cannot answer for a pair."""
         m = self.m
+        enum = getattr(m, "AmdSmiLinkType", None)
+        xgmi = int(getattr(enum, "AMDSMI_LINK_TYPE_XGMI", 2)) if enum is not None else 2
+        pcie = int(getattr(enum, "AMDSMI_LINK_TYPE_PCIE", 1)) if enum is not None else 1
         try:
             lt = m.amdsmi_topo_get_link_type(self._h(a), self._h(b))
-            t = lt.get("type")
-            xgmi = getattr(getattr(m, "AmdSmiLinkType", None), "XGMI", None)
-            pcie = getattr(getattr(m, "AmdSmiLinkType", None), "PCIE", None)
-            tname = "XGMI" if (t == xgmi or t == 2) else ("PCIE" if (t == pcie or t == 1) else "NONE")
-            bw = None
-            try:
-                mm = m.amdsmi_get_minmax_bandwidth_between_processors(self._h(a), self._h(b))
-                bw = mm.get("max_bandwidth", 0) / 1000.0 or None   # MB/s -> GB/s
-            except Exception:  # noqa: BLE001
-                pass
-            return LinkInfo(tname, int(lt.get("hops", 1) or 1), 1, bw)
+            t = int(lt.get("type"))
         except Exception:  # noqa: BLE001
-            return LinkInfo("NONE", 0, 0)
+            kl = kfd_link(KFD_TOPO, a.extra.get("kfd_node"), b.extra.get("kfd_node")) \
+                if a.extra.get("kfd_node") is not None else None
+            return kl or LinkInfo("NONE", 0, 0)
+        tname = "XGMI" if t == xgmi else ("PCIE" if t == pcie else "NONE")
+        weight = None
+        try:
+            weight = int(m.amdsmi_topo_get_link_weight(self._h(a), self._h(b)))
+        except Exception:  # noqa: BLE001
+            pass
+        bw = None
+        try:
+            mm = m.amdsmi_get_minmax_bandwidth_between_processors(self._h(a), self._h(b))
+            vals = [v for v in (mm.get("min_bandwidth"), mm.get("max_bandwidth")) if v]
+            bw = min(vals) / 1000.0 if vals else None     # MB/s -> GB/s
+        except Exception:  # noqa: BLE001
+            pass
+        return LinkInfo(tname, int(lt.get("hops", 1) or 1), 1, bw, weight)
 
     def wait_health_events(self, gpus, timeout_s):
         m = self.m
@@ -302,12 +409,6 @@ class AmdSmiBackend(Backend):
             return {"gfx": float(a.get("gfx_activity") or 0), "umc": float(a.get("umc_activity") or 0)}
         except Exception:  # noqa: BLE001
             return {"gfx": 0.0, "umc": 0.0}
-
-    def processes(self, g):
-        try:
-            return list(self.m.amdsmi_get_gpu_process_list(self._h(g)))
-        except Exception:  # noqa: BLE001
-            return []
 
     def shutdown(self):
         try:
@@ -389,16 +490,27 @@ class SysfsBackend(Backend):
                 cards = [c.name for c in (dev / "drm").glob("card*")] if (dev / "drm").exists() else []
                 card = int(cards[0][4:]) if cards and cards[0][4:].isdigit() else -1
                 part = self._read(dev / "current_compute_partition", "SPX") or "SPX"
-                name = self._read(dev / "product_name") or name
+                name = canonical_name(self._read(dev / "product_name"), device_id=p.get("device_id"))
             idx = len(out)
-            out.append(GPUInfo(index=idx, uuid=f"GPU-{uid:016x}" if uid else f"kfd-{n.name}",
-                               rocr_id=f"GPU-{uid:016x}" if uid else str(idx), name=name, memory_mib=mem >> 20,
-                               cus=cus, numa=numa, bdf=bdf, render_minor=minor, card_minor=card,
-                               compute_partition=part.upper()))
-        return _group_physical(out)
+            rid = rocr_uuid(uid)
+            gid = None
+            try:
+                gid = int((n / "gpu_id").read_text().strip() or 0)
+            except (OSError, ValueError):
+                pass
+            out.append(GPUInfo(index=idx, uuid=rid or f"kfd-{n.name}", rocr_id=rid or str(idx), name=name,
+                               memory_mib=mem >> 20, cus=cus, numa=numa, bdf=bdf, render_minor=minor,
+                               card_minor=card, compute_partition=part.upper(),
+                               extra={"kfd_node": n.name, "gpu_id": gid}))
+        return _dedupe_partition_ids(_group_physical(out))
 
     def link(self, a, b):
-        return LinkInfo("XGMI", 1, 1)
+        """From the KFD io_links (type, weight, bandwidth); partitions of one
+        package talk on-die."""
+        if a.physical == b.physical and a.bdf and b.bdf:
+            return LinkInfo("XGMI", 0, 8)
+        kl = kfd_link(self.root, a.extra.get("kfd_node"), b.extra.get("kfd_node"))
+        return kl or LinkInfo("NONE", 0, 0)
 
     def set_compute_partition(self, physical_index: int, mode: str) -> None:
         mode = mode.upper()

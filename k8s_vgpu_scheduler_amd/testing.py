@@ -66,3 +66,60 @@ def amd_pod(name: str, namespace: str = "default", containers: list | None = Non
     ctrs = containers if containers is not None else [amd_container(**ctr_kw)]
     return make_pod(name, namespace, containers=ctrs, init_containers=init, annotations=annotations,
                     labels=labels, uid=uid or f"uid-{namespace}-{name}")
+
+
+def write_mi355x_sysfs(root, n: int = 8, degraded: dict | None = None, pcie_pairs=(), serial_base: int = 0xAE8C1614E27CC400,
+                       numa_per: int = 4, product: str = "AMD Instinct MI355 OAM") -> tuple:
+    """A KFD topology + DRM/PCI sysfs tree of one 8 x MI355X node, shaped like
+    the one measured on the hardware (tests/fixtures/mi355x_8gpu_kfd_links.json):
+    CPU nodes 0-1, GPU nodes 2..n+1, each GPU with one PCIe io_link to its
+    socket (type 2, weight 20, 64000 MB/s) and one xGMI io_link to every peer
+    (type 11, weight 15, 76000 MB/s).  ``degraded`` = {(i, j): MB/s} lowers a
+    pair's xGMI bandwidth; ``pcie_pairs`` turns pairs into PCIe peers.
+    Returns (kfd_nodes_dir, drm_dir)."""
+    import os
+    from pathlib import Path
+
+    root = Path(root)
+    kfd, drm, pci = root / "kfd" / "topology" / "nodes", root / "drm", root / "pci"
+    degraded = {tuple(sorted(k)): v for k, v in (degraded or {}).items()}
+    pcie = {tuple(sorted(p)) for p in pcie_pairs}
+    buses = [0x05, 0x15, 0x65, 0x75, 0x85, 0x95, 0xE5, 0xF5][:n] + [0x100 + i for i in range(max(0, n - 8))]
+    for c in range(2):
+        d = kfd / str(c)
+        (d / "io_links").mkdir(parents=True)
+        (d / "gpu_id").write_text("0\n")
+        (d / "properties").write_text("cpu_cores_count 64\nsimd_count 0\nlocation_id 0\ndomain 0\n")
+    for i in range(n):
+        node = kfd / str(2 + i)
+        (node / "mem_banks" / "0").mkdir(parents=True)
+        minor = 128 + 8 * i
+        (node / "gpu_id").write_text(f"{16000 + 1111 * i}\n")
+        (node / "properties").write_text(
+            f"cpu_cores_count 0\nsimd_count 1024\nsimd_per_cu 4\nlocation_id {buses[i] << 8}\ndomain 0\n"
+            f"unique_id {serial_base + i}\ndevice_id 30115\ndrm_render_minor {minor}\nnum_xcc 8\n")
+        (node / "mem_banks" / "0" / "properties").write_text(f"heap_type 1\nsize_in_bytes {288 << 30}\n")
+        links = [(i // numa_per if numa_per else 0, 2, 20, 64000)]
+        for j in range(n):
+            if j == i:
+                continue
+            key = tuple(sorted((i, j)))
+            if key in pcie:
+                links.append((2 + j, 2, 40, 64000))
+            else:
+                bw = degraded.get(key, 76000)
+                links.append((2 + j, 11, 15, bw))
+        for k, (to, t, w, bw) in enumerate(links):
+            ld = node / "io_links" / str(k)
+            ld.mkdir(parents=True)
+            ld.joinpath("properties").write_text(
+                f"type {t}\nnode_from {2 + i}\nnode_to {to}\nweight {w}\nmin_bandwidth {bw if t == 11 else 0}\n"
+                f"max_bandwidth {bw}\n")
+        dev = pci / f"0000:{buses[i]:02x}:00.0"
+        (dev / "drm" / f"card{i}").mkdir(parents=True)
+        (dev / "numa_node").write_text(f"{i // numa_per if numa_per else 0}\n")
+        (dev / "current_compute_partition").write_text("SPX\n")
+        (dev / "product_name").write_text(product + "\n")
+        (drm / f"renderD{minor}").mkdir(parents=True)
+        os.symlink(dev, drm / f"renderD{minor}" / "device")
+    return kfd, drm

@@ -3,26 +3,21 @@
 The extender does not run its own election: it watches the Lease that
 kube-scheduler (running in the same pod) holds and is leader iff the lease's
 ``holderIdentity`` starts with this pod's hostname and the lease has not
-expired.  ``DummyLeaderManager`` is used when election is disabled.
+expired.  Expiry is judged on THIS process's clock -- the local monotonic time
+the lease record was last observed to change plus ``leaseDurationSeconds``
+(leaderelection.go:100-104,176-181) -- never on the server-written
+``renewTime``, so a node whose wall clock is skewed against the API server can
+neither keep serving as a stale leader nor refuse as a live one.
+``DummyLeaderManager`` is used when election is disabled.
 """
 
 from __future__ import annotations
 
-import datetime as _dt
 import logging
 import threading
+import time
 
 log = logging.getLogger(__name__)
-
-
-def _parse_time(s: str | None) -> _dt.datetime | None:
-    if not s:
-        return None
-    s = s.replace("Z", "+00:00")
-    try:
-        return _dt.datetime.fromisoformat(s)
-    except ValueError:
-        return None
 
 
 class DummyLeaderManager:
@@ -37,35 +32,42 @@ class DummyLeaderManager:
 
 
 class LeaderManager:
-    def __init__(self, hostname: str, namespace: str, name: str, on_started=None, on_stopped=None):
+    def __init__(self, hostname: str, namespace: str, name: str, on_started=None, on_stopped=None,
+                 clock=time.monotonic):
         self.hostname, self.namespace, self.name = hostname, namespace, name
         self.on_started, self.on_stopped = on_started, on_stopped
+        self.clock = clock
         self._lease: dict | None = None
+        self._observed = 0.0       # local clock when the lease record was last seen to change
         self._was_leader = False
         self._mu = threading.Lock()
 
-    def _valid(self, lease: dict, now: _dt.datetime) -> bool:
-        spec = lease.get("spec") or {}
-        holder = spec.get("holderIdentity") or ""
-        if not holder.startswith(self.hostname):
-            return False
-        renew = _parse_time(spec.get("renewTime")) or _parse_time(spec.get("acquireTime"))
-        dur = spec.get("leaseDurationSeconds") or 0
-        if renew is None:
-            return False
-        if renew.tzinfo is None:
-            renew = renew.replace(tzinfo=_dt.timezone.utc)
-        return now <= renew + _dt.timedelta(seconds=int(dur))
+    def _holder(self, lease: dict | None) -> bool:
+        holder = ((lease or {}).get("spec") or {}).get("holderIdentity") or ""
+        return bool(holder) and holder.startswith(self.hostname)
 
-    def is_leader(self, now: _dt.datetime | None = None) -> bool:
-        now = now or _dt.datetime.now(_dt.timezone.utc)
+    def is_leader(self, now: float | None = None) -> bool:
+        """``now``: local monotonic seconds (default: the clock now)."""
+        now = self.clock() if now is None else now
         with self._mu:
-            lease = self._lease
-        return bool(lease) and self._valid(lease, now)
+            lease, seen = self._lease, self._observed
+        if not lease or not self._holder(lease):
+            return False
+        dur = (lease.get("spec") or {}).get("leaseDurationSeconds")
+        if not dur:
+            return False
+        return now < seen + int(dur)
 
     def _update(self, lease: dict | None):
         with self._mu:
+            prev = self._lease
             self._lease = lease
+            # a record that changed (a renewal bumps renewTime / resourceVersion)
+            # restarts the local expiry window; a resync of the same record does not
+            if lease is None:
+                self._observed = 0.0
+            elif prev is None or _record(prev) != _record(lease):
+                self._observed = self.clock()
         leader = self.is_leader()
         if leader and not self._was_leader and self.on_started:
             self.on_started()
@@ -89,3 +91,10 @@ class LeaderManager:
     def _mine(self, lease: dict) -> bool:
         md = lease.get("metadata") or {}
         return md.get("name") == self.name and md.get("namespace", self.namespace) == self.namespace
+
+
+def _record(lease: dict) -> tuple:
+    spec = lease.get("spec") or {}
+    md = lease.get("metadata") or {}
+    return (spec.get("holderIdentity"), spec.get("renewTime"), spec.get("acquireTime"),
+            spec.get("leaseTransitions"), md.get("resourceVersion"))

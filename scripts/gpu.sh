@@ -1,0 +1,65 @@
+#!/usr/bin/env bash
+# One parameterised runner for the GPU-box measurements (replaces the round-1
+# one-off scripts/gpu_*.sh; their commands live on in git history).  Run on a
+# MI355X box, e.g. through gpurun:
+#     gpurun --timeout 1200 -- 'bash scripts/gpu.sh full'
+# Suites (each step has its own time limit; the first failure ends the run):
+#   full        GPU test suite + smoke + default bench (all rounds)
+#   bench [N..] bench.py --slices N for each N (default 1 2 4 8), all rounds
+#   governor    governor GPU tests + bench (spatial, temporal, native rounds)
+#   busyshare   rocprofv3 busy share of governed tenants (scripts/probe/governor_busyshare.py)
+#   probes      KFD occupancy + topology probes (scripts/probe/*.py)
+#   kernels     rocprofv3 --kernel-trace --stats of one 64-CU slice decode step
+#   pmc         PMC passes over a 64-CU decode step (one counter group per pass)
+#   membw       partition read ceilings (bench/membw.py)
+# Results go to gpurun_out/<suite>/ (copy the ones to keep into profiles/).
+set -o pipefail
+suite=${1:-full}; shift || true
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+out=$R/gpurun_out/$suite; mkdir -p "$out"
+cd "$R"
+
+step() {  # step <seconds> <log name> <command...>
+  local t=$1 name=$2; shift 2
+  echo "[gpu.sh] $suite/$name: $*"
+  timeout -k 10 "$t" "$@" > "$out/$name.log" 2>&1
+  local rc=$?
+  [ $rc -eq 0 ] || { echo "[gpu.sh] $name failed rc=$rc (see $out/$name.log)"; exit $rc; }
+}
+
+case $suite in
+  full)
+    timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > "$out/gpu_tests.log" 2>&1
+    rc=$?; [ $rc -le 1 ] || exit $rc
+    step 200 smoke python -u -c "import __graft_entry__ as g; g.smoke()"
+    step 400 bench python -u bench.py --out "$out/bench.json"
+    exit $rc ;;
+  bench)
+    for n in ${@:-1 2 4 8}; do step 400 "s$n" python -u bench.py --slices "$n" --out "$out/s$n.json"; done ;;
+  governor)
+    step 900 tests python -u -m pytest tests/test_shim_gpu.py -v -s --timeout 300 --timeout-method thread \
+      -k "governor or temporal or masked or heavy or launch or grant"
+    step 400 bench python -u bench.py --out "$out/bench.json" ;;
+  busyshare)
+    step 500 busyshare python -u scripts/probe/governor_busyshare.py ;;
+  probes)
+    step 120 kfd_matmul python -u scripts/probe/kfd_occupancy.py
+    step 500 kfd_decode python -u scripts/probe/kfd_decode_occupancy.py
+    step 120 topology python -u scripts/probe/topology_probe.py ;;
+  kernels)
+    cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
+    HSA_CU_MASK=0:0-63 step 240 prof_cu64 rocprofv3 --kernel-trace --stats -d "$out/prof_cu64" -o run -- \
+      python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 20 ;;
+  pmc)
+    cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R HSA_CU_MASK=0:0-63
+    dec="python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 3 --warmup 1 --no-graph"
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$out/a" -o run -- $dec > "$out/a.log" 2>&1 || exit 1
+    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS \
+      --kernel-trace --output-format csv -d "$out/b" -o run -- $dec > "$out/b.log" 2>&1 || exit 1 ;;
+  membw)
+    for b in 2 4 8 16; do
+      step 300 "membw8_b$b" python -u -m k8s_vgpu_scheduler_amd.bench.membw --gib 20 --shared-only 8 --shared-bpc "$b" \
+        --out "$out/membw8_b$b.json"
+    done ;;
+  *) echo "unknown suite $suite"; exit 2 ;;
+esac

@@ -35,6 +35,7 @@ def test_bench_json_contract_cpu_rehearsal(nproc):
     assert out["config"]["parallelism"] == f"dp{nproc} x 2 vGPU slices/GPU"
     assert out["round"] == "shim" and out["value"] > 0
     assert "native_value" in out and "native_hip_default_queues_value" in out
+    assert out["temporal_value"] > 0 and len(out["temporal_per_slice_tok_s_rank0"]) == 2   # the governor round
     # value is the whole-job aggregate: tokens of every slice on every rank / max wall
     tokens = nproc * 2 * 2 * 3
     assert out["value"] == pytest.approx(tokens / (out["ms_per_step"] * 3 / 1000), rel=0.02)
@@ -46,3 +47,17 @@ def test_bench_json_contract_cpu_rehearsal(nproc):
         assert out["allreduce_peak_busbw_gbps"] == max(r["busbw_gbps"] for r in ar) > 0
     else:
         assert "allreduce_between_gpus" not in out
+
+
+@pytest.mark.parametrize("nproc", [4, 8])
+def test_bench_json_contract_at_4_and_8_ranks(nproc):
+    """The driver's 1/2/4/8 scaling curve, rehearsed at 4 and 8 ranks (one
+    slice per rank, shim + native rounds, to fit the CPU container)."""
+    out = _run(["--gpus", str(nproc), "--device", "cpu", "--model", "qwen3-tiny", "--slices", "1", "--batch", "2",
+                "--ctx", "16", "--steps", "2", "--warmup", "1", "--mode", "both"], nproc)
+    assert out["n_gpus"] == nproc and out["config"]["global_batch"] == nproc * 2
+    assert out["config"]["parallelism"] == f"dp{nproc} x 1 vGPU slices/GPU"
+    tokens = nproc * 2 * 2
+    assert out["value"] == pytest.approx(tokens / (out["ms_per_step"] * 2 / 1000), rel=0.02)
+    ar = out["allreduce_between_gpus"]
+    assert all(r["correct"] for r in ar)

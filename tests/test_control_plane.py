@@ -347,20 +347,51 @@ def test_http_routes_filter_bind_webhook_health(cluster):
 
 # --------------------------------------------------------- leader election
 def test_passive_leader_election():
-    now = dt.datetime.now(dt.timezone.utc)
     events = []
+    clock = [1000.0]
     lm = LeaderManager("sched-0", "kube-system", "hami-scheduler", on_started=lambda: events.append("up"),
-                       on_stopped=lambda: events.append("down"))
-    lease = {"metadata": {"name": "hami-scheduler", "namespace": "kube-system"},
+                       on_stopped=lambda: events.append("down"), clock=lambda: clock[0])
+    now = dt.datetime.now(dt.timezone.utc)
+    lease = {"metadata": {"name": "hami-scheduler", "namespace": "kube-system", "resourceVersion": "1"},
              "spec": {"holderIdentity": "sched-0_abc", "leaseDurationSeconds": 15,
                       "renewTime": now.strftime("%Y-%m-%dT%H:%M:%S.%fZ")}}
     lm.on_add(lease)
     assert lm.is_leader() and events == ["up"]
     other = json.loads(json.dumps(lease))
     other["spec"]["holderIdentity"] = "sched-1_def"
+    other["metadata"]["resourceVersion"] = "2"
     lm.on_update(lease, other)
     assert not lm.is_leader() and events == ["up", "down"]
-    assert not lm.is_leader(now + dt.timedelta(seconds=60))
+
+
+def test_lease_validity_uses_the_local_observation_clock():
+    """leaderelection.go:100-104,176-181: a lease is valid for
+    leaseDurationSeconds after THIS process last saw it change; the server's
+    renewTime (possibly skewed against the local clock) is not consulted."""
+    clock = [500.0]
+    lm = LeaderManager("sched-0", "kube-system", "hami-scheduler", clock=lambda: clock[0])
+    skewed = (dt.datetime.now(dt.timezone.utc) - dt.timedelta(hours=3)).strftime("%Y-%m-%dT%H:%M:%S.%fZ")
+    lease = {"metadata": {"name": "hami-scheduler", "namespace": "kube-system", "resourceVersion": "7"},
+             "spec": {"holderIdentity": "sched-0_abc", "leaseDurationSeconds": 15, "renewTime": skewed}}
+    lm.on_add(lease)
+    assert lm.is_leader()                     # the server clock is 3 h behind: still the leader
+    clock[0] += 14.0
+    assert lm.is_leader()
+    lm.on_update(lease, json.loads(json.dumps(lease)))   # informer resync of the same record
+    clock[0] += 2.0
+    assert not lm.is_leader()                 # not renewed within 15 s of local time: stale
+    renewed = json.loads(json.dumps(lease))
+    renewed["metadata"]["resourceVersion"] = "8"
+    renewed["spec"]["renewTime"] = skewed     # even with the same (skewed) timestamp format
+    lm.on_update(lease, renewed)
+    assert lm.is_leader()
+    future = (dt.datetime.now(dt.timezone.utc) + dt.timedelta(hours=3)).strftime("%Y-%m-%dT%H:%M:%S.%fZ")
+    ahead = json.loads(json.dumps(renewed))
+    ahead["metadata"]["resourceVersion"] = "9"
+    ahead["spec"]["renewTime"] = future       # a server clock 3 h ahead does not extend the lease
+    lm.on_update(renewed, ahead)
+    clock[0] += 16.0
+    assert not lm.is_leader()
 
 
 def test_follower_does_not_register(cluster):

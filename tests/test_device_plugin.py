@@ -283,6 +283,71 @@ def test_grpc_register_list_and_allocate(env):
         ks.stop(0)
 
 
+def _kubelet(ksock):
+    from concurrent import futures
+    k = _FakeKubelet()
+    srv = grpc.server(futures.ThreadPoolExecutor(max_workers=2))
+    api.add_registration_servicer(srv, k)
+    srv.add_insecure_port(f"unix://{ksock}")
+    srv.start()
+    return k, srv
+
+
+def test_kubelet_restarts_do_not_consume_the_crash_budget(env):
+    """main.go:305-337: a kubelet restart (device-plugins dir wiped, a new
+    kubelet.sock) re-registers the plugin; six of them with a crash budget of
+    one leave the plugin running.  A plugin socket removed while the kubelet
+    keeps running is a crash."""
+    import threading
+    import time as _t
+
+    c, sched, plugin, backend = env
+    kdir = tempfile.mkdtemp()
+    ksock = os.path.join(kdir, "kubelet.sock")
+    sock_dir = tempfile.mkdtemp()
+    kubelets = [_kubelet(ksock)]
+    stats, stop = {}, threading.Event()
+    errors = []
+
+    def loop():
+        try:
+            S.run_with_restarts(lambda: S.AMDDevicePlugin(backend, plugin.cfg, "node1", socket_dir=sock_dir), ksock,
+                                max_restarts=1, stop=stop, poll_s=0.05, restart_grace_s=0.5, stats=stats)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    t = threading.Thread(target=loop, daemon=True)
+    t.start()
+
+    def wait(cond, what, timeout=10.0):
+        deadline = _t.time() + timeout
+        while _t.time() < deadline and not cond():
+            _t.sleep(0.02)
+        assert cond(), (what, stats, errors)
+
+    wait(lambda: stats.get("registrations") == 1, "first registration")
+    for i in range(6):
+        k, srv = kubelets[-1]
+        srv.stop(0)
+        for f in os.listdir(sock_dir):                  # the kubelet wipes the plugin sockets ...
+            os.unlink(os.path.join(sock_dir, f))
+        if os.path.exists(ksock):
+            os.unlink(ksock)
+        _t.sleep(0.1)
+        kubelets.append(_kubelet(ksock))                # ... and comes back with a new socket
+        wait(lambda: stats.get("registrations") == i + 2, f"re-registration {i + 1}")
+        assert kubelets[-1][0].requests and kubelets[-1][0].requests[0].resource_name == "amd.com/gpu"
+    assert stats["crashes"] == 0 and stats["kubelet_restarts"] >= 6 and t.is_alive() and not errors
+    # a genuine crash: the plugin socket vanishes, the kubelet does not restart
+    for f in os.listdir(sock_dir):
+        os.unlink(os.path.join(sock_dir, f))
+    wait(lambda: stats["crashes"] == 1, "crash counted")
+    stop.set()
+    t.join(timeout=10)
+    for _, srv in kubelets:
+        srv.stop(0)
+
+
 def test_handshake_cycle(env):
     """Scheduler writes Requesting_, the registrar answers Reported_."""
     c, sched, plugin, backend = env

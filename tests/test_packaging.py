@@ -139,3 +139,61 @@ def test_dashboard_queries_exported_series():
         for t in p["targets"]:
             used |= set(re.findall(r"\b((?:hami|mivgpu)_[a-z_]+)", t["expr"]))
     assert used and used <= exported, used - exported
+
+
+# pip distribution that provides each importable top-level module
+_DIST = {"grpc": "grpcio", "google": "protobuf", "yaml": "pyyaml", "prometheus_client": "prometheus_client",
+         "requests": "requests", "amdsmi": "/opt/rocm/share/amd_smi"}
+
+
+def _reachable_third_party(entry_points):
+    """Top-level third-party modules imported (anywhere, transitively within the
+    package) by the given entry-point modules."""
+    import ast
+    import sys
+
+    pkg = "k8s_vgpu_scheduler_amd"
+    std = set(sys.stdlib_module_names)
+    seen, ext, todo = set(), {}, list(entry_points)
+
+    def modfile(name):
+        p = ROOT / name.replace(".", "/")
+        return p / "__init__.py" if (p / "__init__.py").exists() else (p.with_suffix(".py") if p.with_suffix(
+            ".py").exists() else None)
+    while todo:
+        m = todo.pop()
+        if m in seen:
+            continue
+        seen.add(m)
+        f = modfile(m)
+        if f is None:
+            continue
+        base = m if f.name == "__init__.py" else m.rsplit(".", 1)[0]
+        for node in ast.walk(ast.parse(f.read_text())):
+            names = []
+            if isinstance(node, ast.Import):
+                names = [a.name for a in node.names]
+            elif isinstance(node, ast.ImportFrom):
+                mod = node.module or ""
+                if node.level:
+                    parts = base.split(".")
+                    mod = ".".join(parts[:len(parts) - node.level + 1] + ([mod] if mod else []))
+                names = [mod] + [f"{mod}.{a.name}" for a in node.names]
+            for n in names:
+                top = n.split(".")[0] if n else ""
+                if top == pkg:
+                    todo.append(n)
+                elif top and top not in std:
+                    ext.setdefault(top, set()).add(m)
+    return ext
+
+
+def test_runtime_image_installs_every_import():
+    """the runtime stage must install every third-party
+    module reachable from the scheduler, device-plugin and monitor binaries."""
+    ext = _reachable_third_party([f"k8s_vgpu_scheduler_amd.cmd.{b}" for b in ("scheduler", "device_plugin", "monitor")])
+    docker = (ROOT / "docker" / "Dockerfile").read_text()
+    runtime = docker[docker.rindex("FROM "):]
+    missing = {m: sorted(by) for m, by in ext.items() if _DIST.get(m, m) not in runtime}
+    assert not missing, f"runtime image lacks {missing}"
+    assert {"grpc", "prometheus_client", "requests", "yaml"} <= set(ext)
