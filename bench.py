@@ -129,6 +129,14 @@ def main():
                                  hw_queues=args.hw_queues or None)),
             phys, work, log_dir, child_args, "shim")))
     if args.mode == "all" and args.slices > 1 and not args.no_spatial:
+        # the same CU masks and queues without libmivgpu.so: what the shim
+        # itself costs (the overhead vs native also contains the
+        # partitioning's own benefit)
+        bare = plan_slices(args.slices, shim=True, gpumem_mib=None, hw_queues=args.hw_queues or None)
+        for sp in bare:
+            sp.shim = False
+        rounds.append(("masked_noshim", spawn_round(with_env(bare), phys, work / "bare", log_dir, child_args,
+                                                    "masked_noshim")))
         # the same slices time-shared by the governor gate instead of CU masks
         # (BASELINE config 3: "4 pods x 25% gpucores, CU-throttle governor kernel")
         rounds.append(("temporal", spawn_round(
@@ -239,6 +247,10 @@ def main():
             out["isolation_overhead_pct"] = round((1.0 - head["tok_s"] / nat) * 100.0, 2)
             nd = results["native"]["done"]
             out["native_tpot_ms_p50_rank0"] = [round(d.get("tpot_ms_p50", 0), 3) for d in nd]
+        if "masked_noshim" in results and "shim" in results:
+            bare = results["masked_noshim"]["tok_s"]
+            out["masked_noshim_value"] = round(bare, 2)
+            out["shim_overhead_pct"] = round((1.0 - head["tok_s"] / bare) * 100.0, 2)
         if "temporal" in results:
             tr = results["temporal"]
             tps = [round(d["tok_s"], 1) for d in tr["done"]]

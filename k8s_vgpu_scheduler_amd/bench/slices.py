@@ -81,10 +81,12 @@ def slice_env(spec: SliceSpec, physical_gpu: str | None, cache_dir: Path) -> dic
         if spec.core_pct < 100:
             env["HIP_DEVICE_CORE_LIMIT"] = str(spec.core_pct)
         env["GPU_CORE_UTILIZATION_POLICY"] = spec.policy
-        if spec.cu_ranges:
-            env["HSA_CU_MASK"] = "0:" + cu_mask_string(spec.cu_ranges)
-        if spec.hw_queues:
-            env["GPU_MAX_HW_QUEUES"] = str(spec.hw_queues)
+    # the partition and queue count are properties of the slice, with or
+    # without the shim (the "masked, no shim" round isolates the shim's cost)
+    if spec.cu_ranges:
+        env["HSA_CU_MASK"] = "0:" + cu_mask_string(spec.cu_ranges)
+    if spec.hw_queues:
+        env["GPU_MAX_HW_QUEUES"] = str(spec.hw_queues)
     env.update(spec.env)
     return env
 

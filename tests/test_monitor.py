@@ -66,6 +66,24 @@ def test_lister_skips_corrupt_cache(tmp_path):
     assert lister.list_containers() == []
 
 
+def test_lister_refuses_planted_symlinks_and_fifos(tmp_path):
+    """The cache directory is writable by the container: a region "file" that
+    is a symlink to a host file or a FIFO must never be mapped (let alone
+    written) by the privileged monitor."""
+    victim = tmp_path / "host_file"
+    victim.write_bytes(b"\1" * (REGION_SIZE + 10))
+    d = tmp_path / "vgpu" / "containers" / "u9_c"
+    d.mkdir(parents=True)
+    os.symlink(victim, d / "x.cache")
+    f = tmp_path / "vgpu" / "containers" / "u8_c"
+    f.mkdir(parents=True)
+    os.mkfifo(f / "y.cache")
+    lister = ContainerLister(str(tmp_path), None)
+    lister.update()
+    assert lister.list_containers() == []
+    assert victim.read_bytes() == b"\1" * (REGION_SIZE + 10)
+
+
 def test_feedback_blocks_lower_priority(tmp_path):
     hi = make_container(tmp_path, "h", "c", priority=0, recent=2)
     lo = make_container(tmp_path, "l", "c", priority=1, recent=2)

@@ -51,13 +51,18 @@ def test_detect_finds_the_mi355x(backends):
 def test_backends_agree(backends):
     ok = {k: v for k, v in backends.items() if isinstance(v, smi.Backend)}
     assert ok, backends
-    views = {k: sorted((g.render_minor, g.cus, g.numa, g.bdf.lower(), g.compute_partition.upper(),
-                        g.memory_mib // 1024) for g in v.gpus()) for k, v in ok.items()}
+    views = {k: sorted((g.render_minor, g.cus, g.numa, g.bdf.lower(), g.compute_partition.upper(), g.uuid,
+                        g.rocr_id, g.name, g.memory_mib // 1024) for g in v.gpus()) for k, v in ok.items()}
+    for v in views.values():
+        for g in v:
+            # one identity scheme: GPU-<16 hex KFD unique id>, the board product name
+            assert g[5].startswith("GPU-") and len(g[5]) == 20 and g[6] == g[5], g
+            assert g[7].startswith("AMD Instinct MI35") and "Radeon" not in g[7], g
     if len(views) == 2:
         a, s = views["amdsmi"], views["sysfs"]
-        # same render nodes, CU counts, NUMA nodes, PCI addresses and partition modes
-        assert [x[:5] for x in a] == [x[:5] for x in s], views
-        assert all(abs(x[5] - y[5]) <= 2 for x, y in zip(a, s)), views
+        # same render nodes, CU counts, NUMA nodes, PCI addresses, partition modes, ids and names
+        assert [x[:8] for x in a] == [x[:8] for x in s], views
+        assert all(abs(x[8] - y[8]) <= 2 for x, y in zip(a, s)), views
 
 
 def test_health_usage_and_events(backends):
