@@ -252,9 +252,14 @@ class AMDDevices(D.Devices):
         cv = _rv(ctr, c.resource_core_name)
         if cv is not None:
             cc, ok = quantity.as_int64(cv)
-            if not ok or cc < 0 or cc > 100:
+            if not ok or cc < 0:
                 log.error("amd core request %r rejected (container %s)", cv, ctr.get("name"))
                 return ContainerDeviceRequest()
+            if cc > 100:
+                # the reference clamps in Fit (nvidia/device.go:772-776): the pod
+                # still needs its GPU, as a whole card
+                log.error("amd core request %r exceeds 100 (container %s); using 100", cv, ctr.get("name"))
+                cc = 100
             cores = cc
         return ContainerDeviceRequest(nums=n, type=AMD_DEVICE, memreq=mem, mem_percentage_req=mem_pct,
                                       coresreq=cores)

@@ -267,7 +267,7 @@ def test_config_rejects_unknown_core_policy():
     ({"gpu": 1, "mem_pct": 250}, (1, 0, 100, 0)),               # clamped
     ({"gpu": 1, "cores": 25}, (1, 0, 100, 25)),
     ({"gpu": 0}, (0, 0, 101, 0)),                               # no request
-    ({"gpu": 1, "cores": 130}, (0, 0, 101, 0)),                 # invalid -> no request
+    ({"gpu": 1, "cores": 130}, (1, 0, 100, 100)),               # > 100 clamps to a whole card (device.go:772)
 ])
 def test_generate_resource_requests(kw, expect):
     r = amd().generate_resource_requests(amd_container(**kw))
