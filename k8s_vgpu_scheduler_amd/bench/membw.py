@@ -25,8 +25,24 @@ import time
 GIB = 1 << 30
 
 
-def _mask(cus: int, slot: int = 0) -> str:
-    """XCD-balanced partition: `cus` consecutive mask bits (8-CU granules)."""
+LAYOUT = "balanced"
+
+
+def _mask(cus: int, slot: int = 0, layout: str | None = None) -> str:
+    """CU partition ``slot`` of ``cus`` CUs.  ``balanced``: consecutive mask bits
+    = the same number of CUs on every XCD (CU i lives on XCD i % 8);
+    ``xcd``: whole XCDs (cus / 32 of them), the CPX-like layout in which tenants
+    would share no XCD.  Measured on MI355X in SPX mode (profiles/README.md
+    §23): an ``xcd`` mask is silently dropped -- a queue dispatches to every
+    XCD, so a mask that leaves an XCD without CUs is not applied and the
+    process runs on all 256 CUs.  XCD-exclusive tenants need a compute
+    partition mode (CPX/DPX/QPX), not a CU mask."""
+    layout = layout or LAYOUT
+    if layout == "xcd" and cus % 32 == 0:
+        k = cus // 32
+        xcds = range(slot * k, slot * k + k)
+        ids = sorted(x + 8 * j for x in xcds for j in range(32))
+        return "0:" + ",".join(f"{c}-{c}" for c in ids)
     lo = slot * cus
     return f"0:{lo}-{lo + cus - 1}"
 
@@ -106,12 +122,16 @@ def main(argv=None) -> int:
     ap.add_argument("--shared-bpc", type=int, default=0,
                     help="blocks per CU in the shared rows (0 = the best single-process value)")
     ap.add_argument("--shared-only", default="", help="comma list of process counts: only these shared rows")
+    ap.add_argument("--layout", default="balanced", choices=["balanced", "xcd"],
+                    help="CU partition layout: XCD-balanced (default) or whole XCDs per partition")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
+    global LAYOUT
+    LAYOUT = a.layout
     if a.child:
         print(json.dumps(child(a)), flush=True)
         return 0
-    doc = {"single": {}, "shared": {}, "gib_per_process": a.gib}
+    doc = {"single": {}, "shared": {}, "gib_per_process": a.gib, "layout": a.layout}
     counts = [int(x) for x in a.shared_only.split(",") if x] or [2, 4, 8]
     for cus in (256, 128, 64, 32):
         if a.shared_only and 256 // cus not in counts:
