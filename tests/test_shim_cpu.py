@@ -379,3 +379,38 @@ def test_cu_mask_reasserted_before_rocr_reads_it(native_build, tmp_path):
               "MIVGPU_SHARED_CACHE": str(tmp_path / "u.cache")})
     p = subprocess.run([str(native_build["driver"]), "hsainit"], env=e, stdout=subprocess.PIPE, text=True, timeout=60)
     assert json.loads(p.stdout.splitlines()[0])["mask"] == "0:64-127"   # unset by the tenant: restored
+
+
+@pytest.mark.parametrize("mask,policy,switch,gated", [
+    ("", "force", 0, True),               # no partition, forced: time-sliced
+    ("", "default", 0, True),             # no partition: the governor is the only limit
+    ("0:0-63", "default", 0, False),      # 64 / 256 CUs = the 25 % limit: the mask holds it
+    ("0:0-63", "default", 1, False),      # ... even when the monitor switches the limit on
+    ("0:0-63", "force", 0, False),        # ... and under force (no double throttle)
+    ("0:0-71", "default", 1, False),      # within one 8-CU granule of the limit
+    ("0:0-127", "default", 1, True),      # 50 % of the CUs for a 25 % limit: time-slice the rest
+    ("0:0-127", "default", 0, False),     # ... but only when contended (default policy)
+    ("0:0-127", "disable", 1, False),     # policy disable: never
+])
+def test_governor_engages_only_where_the_mask_does_not_hold_the_limit(native_build, tmp_path, mask, policy,
+                                                                      switch, gated):
+    """gate_wanted(): a CU mask no wider than the core limit already enforces it
+    in hardware, so the governor must not time-slice that tenant (VERDICT r1:
+    masked slices were double-throttled once the monitor's utilization_switch
+    went on).  The governor-init range marks the first gate attempt."""
+    trace = tmp_path / "roctx.txt"
+    cache = tmp_path / "g.cache"
+    R.SharedRegion.create(str(cache), cu_limit=25).close()
+    reg = R.SharedRegion(str(cache))
+    reg.set_utilization_switch(switch)
+    reg.r.core_policy = {"default": 0, "force": 1, "disable": 2}[policy]
+    for d in range(R.MAX_DEVICES):
+        reg.r.cu_mask_count[d] = int(mask.split("-")[1]) + 1 if mask else 0
+    reg.close()
+    env = {"HIP_DEVICE_CORE_LIMIT": "25", "GPU_CORE_UTILIZATION_POLICY": policy, "MIVGPU_ROCTX": "1",
+           "MIVGPU_ROCTX_LIB": str(native_build["roctx"]), "MOCK_ROCTX_OUT": str(trace)}
+    if mask:
+        env["HSA_CU_MASK"] = mask
+    run(native_build, tmp_path, "launch", 3, cache="g.cache", env=env)
+    lines = trace.read_text().splitlines() if trace.exists() else []
+    assert ("push mivgpu:governor-init" in lines) == gated, lines
