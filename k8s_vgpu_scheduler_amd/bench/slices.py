@@ -88,6 +88,14 @@ def slice_env(spec: SliceSpec, physical_gpu: str | None, cache_dir: Path) -> dic
     if spec.hw_queues:
         env["GPU_MAX_HW_QUEUES"] = str(spec.hw_queues)
     env.update(spec.env)
+    if spec.shim:
+        # as in a pod: the grant also goes to a read-only file the shim takes it
+        # from (deviceplugin/allocate.py; MIVGPU_LIMITS_FILE stands in for the
+        # /etc/mivgpu/limits.conf mount)
+        from k8s_vgpu_scheduler_amd.deviceplugin.allocate import grant_text
+        grant = cache_dir / f"slice{spec.index}.grant"
+        grant.write_text(grant_text(env))
+        env["MIVGPU_LIMITS_FILE"] = str(grant)
     return env
 
 

@@ -43,7 +43,9 @@ LIMITS_PATH = "/etc/mivgpu/limits.conf"     # fixed in the shim (kLimitsPath)
 # env keys that form the grant (the shim's is_grant_key list)
 GRANT_KEYS = ("HIP_DEVICE_MEMORY_LIMIT", "HIP_DEVICE_CORE_LIMIT", "HSA_CU_MASK", "GPU_CORE_UTILIZATION_POLICY",
               "HIP_TASK_PRIORITY", "MIVGPU_OVERSUBSCRIBE", "MIVGPU_SHARED_CACHE", "MIVGPU_DEVICE_UUIDS",
-              "ROCR_VISIBLE_DEVICES")
+              "ROCR_VISIBLE_DEVICES", "MIVGPU_ACCOUNT_CONTEXT", "MIVGPU_KFD_SYSFS", "MIVGPU_OCCUPANCY",
+              "MIVGPU_OCC_PERIOD_US", "MIVGPU_GATE_INTERVAL_US", "MIVGPU_GATE_BURST_US", "MIVGPU_SHARE_TAU_MS",
+              "MIVGPU_DISABLE_CONTROL")
 
 
 def limits_host_path(hook_path: str, pod_uid: str, ctr_name: str) -> str:

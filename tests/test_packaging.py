@@ -197,3 +197,16 @@ def test_runtime_image_installs_every_import():
     missing = {m: sorted(by) for m, by in ext.items() if _DIST.get(m, m) not in runtime}
     assert not missing, f"runtime image lacks {missing}"
     assert {"grpc", "prometheus_client", "requests", "yaml"} <= set(ext)
+
+
+def test_grant_keys_match_the_shim():
+    """The device plugin writes exactly the settings the shim takes from the
+    grant file (is_grant_key in csrc/shim/mivgpu_shim.cpp)."""
+    import re
+
+    from k8s_vgpu_scheduler_amd.deviceplugin.allocate import GRANT_KEYS
+    src = (ROOT / "csrc" / "shim" / "mivgpu_shim.cpp").read_text()
+    body = src[src.index("bool is_grant_key(const char* key)"):]
+    body = body[:body.index("for (const char* k : kKeys)")]
+    shim_keys = set(re.findall(r'"([A-Z_]+)"', body))
+    assert shim_keys == set(GRANT_KEYS), shim_keys ^ set(GRANT_KEYS)
