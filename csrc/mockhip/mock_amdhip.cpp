@@ -55,6 +55,16 @@ void kfd_publish_locked(int dev) {
   if (!f) return;
   fprintf(f, "%zu\n", kfd_context[dev] + used_bytes[dev]);
   fclose(f);
+  // with MOCKHIP_KFD_OCC=1, also the per-process wave count the occupancy
+  // sampler reads: one CU-unit per 64 MiB in use (moves with the traffic)
+  if (!getenv("MOCKHIP_KFD_OCC")) return;
+  snprintf(path, sizeof(path), "%s/proc/%d/stats_%d", root, pid, (gid ? atoi(gid) : 1) + dev);
+  mkdir(path, 0755);
+  snprintf(path, sizeof(path), "%s/proc/%d/stats_%d/cu_occupancy", root, pid, (gid ? atoi(gid) : 1) + dev);
+  f = fopen(path, "w");
+  if (!f) return;
+  fprintf(f, "%zu\n", used_bytes[dev] >> 26);
+  fclose(f);
 }
 hipError_t do_alloc(void** p, size_t sz) {
   std::lock_guard<std::mutex> lk(mu);

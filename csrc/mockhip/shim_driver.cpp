@@ -17,7 +17,8 @@
 //                    ROCR_VISIBLE_DEVICES ROCr would read
 //   stress <threads> <iters> <max MiB>
 //                    threads doing random hipMalloc/hipFree and
-//                    hipMemCreate/hipMemRelease (sanitizer + race tests)
+//                    hipMemCreate/hipMemRelease, one kernel launch per
+//                    iteration (sanitizer + race tests)
 #include <hip/hip_runtime_api.h>
 
 #include <dlfcn.h>
@@ -37,7 +38,11 @@ static void stress_thread(int seed, int iters, int max_mib, std::atomic<long>* a
   std::mt19937 rng(seed);
   std::vector<void*> bufs;
   std::vector<hipMemGenericAllocationHandle_t> handles;
+  static char kernel;
   for (int k = 0; k < iters; ++k) {
+    // a launch per iteration: the launch hooks (and the occupancy sampler
+    // they start) run concurrently with the allocation hooks
+    (void)hipLaunchKernel(&kernel, dim3(1), dim3(64), nullptr, 0, nullptr);
     const int op = rng() % 4;
     const size_t mib = 1 + rng() % max_mib;
     if (op == 0 || (op == 1 && bufs.empty())) {

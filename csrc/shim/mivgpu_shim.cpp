@@ -1164,7 +1164,10 @@ struct OccDev {
   uint64_t win_start_ns = 0;   // utilisation window
   double win_start_share = 0;
 };
-OccDev g_occ[MIVGPU_MAX_DEVICES];
+// Heap-allocated and never freed: the sampler thread is detached, and a
+// static array's destructor at exit would free the peer vectors under it.
+OccDev* const g_occ = new OccDev[MIVGPU_MAX_DEVICES];
+std::mutex& g_occ_pass_mu = *new std::mutex;   // held for one sampling pass; exit waits on it (never destroyed)
 std::atomic<bool> g_occ_started{false};
 std::atomic<bool> g_occ_live[MIVGPU_MAX_DEVICES];
 std::atomic<uint64_t> g_last_gate_ns[MIVGPU_MAX_DEVICES];   // coarse clock of the latest gate
@@ -1292,6 +1295,7 @@ void* occ_main(void*) {
     bool fast = false;
     for (int d = 0; d < g_num_devices; ++d) fast |= t - g_last_gate_ns[d].load(std::memory_order_relaxed) < 1000000000ull;
     usleep((useconds_t)((fast ? g_cfg.occ_period_ns : g_cfg.occ_idle_period_ns) / 1000));
+    std::lock_guard<std::mutex> pass(g_occ_pass_mu);
     if (g_exiting.load(std::memory_order_acquire)) return nullptr;
     Guard g;
     const uint64_t now = mono_ns();
@@ -1398,6 +1402,7 @@ bool stream_capturing(hipStream_t stream);
 // Wait out a stamper that is inside an enqueue (it holds G.mu), so no gate
 // launch races the runtime's teardown; later passes see g_exiting and stop.
 void quiesce_background_threads() {
+  { std::lock_guard<std::mutex> pass(g_occ_pass_mu); }   // an occupancy pass in flight ends first
   for (int d = 0; d < MIVGPU_MAX_DEVICES; ++d) {
     DeviceGate& G = g_gates[d];
     if (!G.stamper_started) continue;
