@@ -49,6 +49,12 @@ int main(int argc, char** argv) {
   double t2 = now_ns();
   CHECK(hipGetLastError());
 
+  if (getenv("LAUNCH_BENCH_NO_GRAPH")) {
+    CHECK(hipStreamDestroy(s));
+    printf("{\"launches\": %ld, \"launch_ns\": %.1f, \"launch_drain_ns\": %.1f}\n", n, (t1 - t0) / n,
+           (t2 - t0) / n);
+    return 0;
+  }
   // graph replay: 32 empty kernels per graph
   hipGraph_t g;
   hipGraphExec_t ge;

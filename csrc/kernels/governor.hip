@@ -17,8 +17,8 @@
 //      weighted by the process's share of the GPU while busy.  The share is
 //      measured by the shim's sampler from KFD's per-process wave counts
 //      (SPI_CSQ_WF_ACTIVE_COUNT): own / (own + every other process) averaged
-//      over the samples in which the process was contending, published in
-//      host memory and read here at execution time.  A tenant alone is
+//      over the samples in which the process was contending, passed as a
+//      kernel argument when the gate is enqueued.  A tenant alone is
 //      charged its wall time, N tenants time-sliced or co-resident are each
 //      charged ~1/N, a CU-masked tenant at most its CU fraction -- the
 //      analogue of HAMi-core charging NVML per-process SM utilisation.
@@ -68,8 +68,7 @@ struct mivgpu_gate_host_stats {
   long long last_now_ns;
   long long last_tokens_ns;
   long long last_hold_ns;
-  unsigned long long share_ppm;  // HOST-written: the process's measured GPU share, ppm
-  unsigned long long pad;
+  unsigned long long pad[2];
   mivgpu_gate_trace_entry trace[MIVGPU_GATE_TRACE];  // ring, index = gates % N
   long long hold_end_ns[MIVGPU_GATE_SLOTS];          // device ns at which a slot's hold ends
 };
@@ -93,7 +92,8 @@ __device__ __forceinline__ void astoreu(unsigned long long* p, unsigned long lon
 
 extern "C" __global__ void __launch_bounds__(64)
 mivgpu_gate(mivgpu_gate_state* st, mivgpu_gate_host_stats* hs, long long submit_ns,
-            int slot, unsigned int rate_ppm, long long cap_ns, long long max_hold_ns, int occupancy) {
+            int slot, unsigned int rate_ppm, long long cap_ns, long long max_hold_ns, unsigned int share_ppm,
+            unsigned int flags) {
   if (threadIdx.x != 0) return;
   if (slot < 0 || slot >= MIVGPU_GATE_SLOTS) slot = 0;
   if (rate_ppm == 0) rate_ppm = 1;
@@ -130,12 +130,10 @@ mivgpu_gate(mivgpu_gate_state* st, mivgpu_gate_host_stats* hs, long long submit_
   long long begin = prev_exit > submit_ns ? prev_exit : submit_ns;
   if (submit_ns < 0 || begin <= 0 || begin > now) begin = now;
   long long busy = now - begin;
-  if (occupancy && hs) {
-    // weight by the measured share (ppm; 0 = no sample yet -> wall time)
-    unsigned long long share =
-        __hip_atomic_load(&hs->share_ppm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (share > 0 && share < 1000000ull) busy = (long long)(((__int128)busy * (long long)share) / 1000000);
-  }
+  // weight by the measured share (ppm, passed at enqueue: the sampler's
+  // 20-ms average moves far slower than a queue drains; 0 = no sample yet ->
+  // plain wall time).  No host-memory read on the gate's path.
+  if (share_ppm > 0 && share_ppm < 1000000u) busy = (long long)(((__int128)busy * share_ppm) / 1000000);
   tokens -= busy;
   // Bound the debt to one burst: a single mis-measured interval can never
   // stall a tenant for longer than cap / rate.
@@ -159,24 +157,31 @@ mivgpu_gate(mivgpu_gate_state* st, mivgpu_gate_host_stats* hs, long long submit_
   astoreu(&st->gates, gates);
   if (locked) __hip_atomic_store(&st->lock, 0ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 
-  // Publish stats to host memory (system scope, plain stores are enough: the
-  // host only ever reads them as monotone counters).
+  // Publish to host memory (system scope; the host only reads monotone
+  // counters and hold ends): three counters, the hold end when holding (the
+  // sampler discounts the gate's own resident wave), and -- only with
+  // MIVGPU_GATE_TRACE (flags bit 0) -- the last-state fields and trace ring.
+  // Each system-scope store is a fabric write the gate's completion waits for:
+  // fewer of them = a cheaper gate (measured 6.3 -> see profiles §25).
   if (hs) {
     __hip_atomic_store(&hs->busy_total_ns, busy_tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&hs->held_total_ns, held_tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&hs->gates, gates, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&hs->last_now_ns, now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&hs->last_tokens_ns, tokens, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&hs->last_hold_ns, hold, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    mivgpu_gate_trace_entry* e = &hs->trace[(gates - 1) % MIVGPU_GATE_TRACE];
-    e->now_ns = now;
-    e->submit_ns = submit_ns;
-    e->prev_exit_ns = prev_exit;
-    e->busy_ns = busy;
-    e->hold_ns = hold;
-    e->tokens_ns = tokens;
-    e->slot = slot;
-    __hip_atomic_store(&hs->hold_end_ns[slot], t_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (hold > 0)
+      __hip_atomic_store(&hs->hold_end_ns[slot], t_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (flags & 1u) {
+      __hip_atomic_store(&hs->last_now_ns, now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&hs->last_tokens_ns, tokens, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&hs->last_hold_ns, hold, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      mivgpu_gate_trace_entry* e = &hs->trace[(gates - 1) % MIVGPU_GATE_TRACE];
+      e->now_ns = now;
+      e->submit_ns = submit_ns;
+      e->prev_exit_ns = prev_exit;
+      e->busy_ns = busy;
+      e->hold_ns = hold;
+      e->tokens_ns = tokens;
+      e->slot = slot;
+    }
   }
 
   // Hold the stream on-device.  ~3.4 us per s_sleep(127) at 2.4 GHz; bounded

@@ -256,6 +256,7 @@ struct Config {
   double share_tau_ns = 20e6;              // EWMA time constant of the governor's share
   char kfd_sysfs[256] = "/sys/class/kfd/kfd";
   uint64_t gate_min_interval_ns = 200000;  // >= 200 us of host submission per gate
+  bool gate_trace = false;                 // gates also write their trace ring (mivgpu_gate_trace)
   int64_t gate_cap_ns = 100000000;         // 100 ms burst (absorbs share-measurement noise)
   int64_t gate_max_hold_ns = 100000000;    // 100 ms per gate, bounds every spin
   char cache_path[512] = {0};
@@ -422,6 +423,8 @@ void load_config() {
   if (crm && *crm) g_cfg.context_refresh_ns = (uint64_t)atoll(crm) * 1000000ull;
   const char* kfd = grant_env("MIVGPU_KFD_SYSFS");
   if (kfd && *kfd) snprintf(g_cfg.kfd_sysfs, sizeof(g_cfg.kfd_sysfs), "%s", kfd);
+  const char* gt = getenv("MIVGPU_GATE_TRACE");
+  g_cfg.gate_trace = gt && (!strcmp(gt, "1") || !strcasecmp(gt, "true"));
   const char* gi = grant_env("MIVGPU_GATE_INTERVAL_US");
   if (gi) g_cfg.gate_min_interval_ns = (uint64_t)atoll(gi) * 1000ull;
   const char* cap = grant_env("MIVGPU_GATE_BURST_US");
@@ -1044,9 +1047,8 @@ std::atomic<uint64_t> g_launches_local{0};
 
 // Governor (gate) per device.  Host stats = 8 counters + a 128-entry trace
 // ring of 8 x int64 per gate + 64 per-slot hold ends (layout: governor.hip
-// mivgpu_gate_host_stats; counter 6 is the sampler's measured share).
+// mivgpu_gate_host_stats).
 constexpr size_t kHostStatsBytes = 64 + 128 * 64 + 64 * 8;
-constexpr int kHsSharePpm = 6;          // u64 index of share_ppm (sampler -> gate)
 constexpr int kHsHoldEnd = 8 + 128 * 8; // u64 index of hold_end_ns[0]
 struct GateSlot {
   hipStream_t stream;
@@ -1172,6 +1174,7 @@ std::atomic<bool> g_occ_started{false};
 std::atomic<bool> g_occ_live[MIVGPU_MAX_DEVICES];
 std::atomic<uint64_t> g_last_gate_ns[MIVGPU_MAX_DEVICES];   // coarse clock of the latest gate
 std::atomic<uint64_t> g_last_launch_ns{0};                   // coarse clock of the latest launch
+std::atomic<uint32_t> g_share_ppm[MIVGPU_MAX_DEVICES];       // sampler -> gate argument (0 = none yet)
 
 int read_occ(int fd) {
   char buf[32];
@@ -1270,7 +1273,7 @@ bool occ_sample(int dev, uint64_t now) {
     o.share_avg = o.share_avg < 0 ? share : o.share_avg + a * (share - o.share_avg);
     uint64_t ppm = (uint64_t)(o.share_avg * 1e6 + 0.5);
     if (!ppm) ppm = 1;   // 0 means "no sample yet" to the gate
-    if (hs) __atomic_store_n(const_cast<uint64_t*>(&hs[kHsSharePpm]), ppm, __ATOMIC_RELAXED);
+    g_share_ppm[dev].store((uint32_t)ppm, std::memory_order_relaxed);
     if (g_slot >= 0) __atomic_store_n(&g_region->procs[g_slot].util[dev].share_ppm, ppm, __ATOMIC_RELAXED);
   }
   if (g_slot >= 0) {
@@ -1346,10 +1349,13 @@ void enqueue_gate_locked(int dev, DeviceGate& G, int slot, hipStream_t stream, u
   unsigned int rate_ppm = (unsigned int)(rate < 1000000ull ? rate : 1000000ull);
   long long cap = g_cfg.gate_cap_ns, hold = g_cfg.gate_max_hold_ns;
   int slot_arg = slot;
-  int occupancy = g_occ_live[dev].load(std::memory_order_acquire) ? 1 : 0;
+  unsigned int share_ppm = g_occ_live[dev].load(std::memory_order_acquire)
+                               ? g_share_ppm[dev].load(std::memory_order_relaxed) : 0u;
+  unsigned int flags = g_cfg.gate_trace ? 1u : 0u;
+  const bool occupancy = share_ppm != 0;
   void* state = G.state;
   void* hs = G.host_stats;
-  void* args[] = {&state, &hs, &submit_dev, &slot_arg, &rate_ppm, &cap, &hold, &occupancy};
+  void* args[] = {&state, &hs, &submit_dev, &slot_arg, &rate_ppm, &cap, &hold, &share_ppm, &flags};
   if (real_hipModuleLaunchKernel()(G.gate_fn, 1, 1, 1, 64, 1, 1, 0, stream, args, nullptr) != hipSuccess) {
     static std::atomic<bool> warned{false};
     if (!warned.exchange(true)) mlog(1, "device %d: governor gate launch failed; this batch is not throttled", dev);
@@ -1965,9 +1971,9 @@ MIVGPU_EXPORT int mivgpu_gate_stats(int dev, unsigned long long* busy, unsigned 
 }
 
 // Copy up to `n` most recent gate trace entries (8 x int64 each) into `out`;
-// returns the number copied.
+// returns the number copied (0 unless MIVGPU_GATE_TRACE=1).
 MIVGPU_EXPORT int mivgpu_gate_trace(int dev, long long* out, int n) {
-  if (dev < 0 || dev >= MIVGPU_MAX_DEVICES || !out || n <= 0) return 0;
+  if (dev < 0 || dev >= MIVGPU_MAX_DEVICES || !out || n <= 0 || !g_cfg.gate_trace) return 0;
   DeviceGate& G = g_gates[dev];
   if (!G.ok || !G.host_stats) return 0;
   const volatile long long* h = static_cast<const volatile long long*>(G.host_stats);
