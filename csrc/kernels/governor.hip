@@ -17,8 +17,8 @@
 //      weighted by the process's share of the GPU while busy.  The share is
 //      measured by the shim's sampler from KFD's per-process wave counts
 //      (SPI_CSQ_WF_ACTIVE_COUNT): own / (own + every other process) averaged
-//      over the samples in which the process was contending, passed as a
-//      kernel argument when the gate is enqueued.  A tenant alone is
+//      over the samples in which the process was contending, published in
+//      pinned host memory and read here at execution time.  A tenant alone is
 //      charged its wall time, N tenants time-sliced or co-resident are each
 //      charged ~1/N, a CU-masked tenant at most its CU fraction -- the
 //      analogue of HAMi-core charging NVML per-process SM utilisation.
@@ -68,7 +68,8 @@ struct mivgpu_gate_host_stats {
   long long last_now_ns;
   long long last_tokens_ns;
   long long last_hold_ns;
-  unsigned long long pad[2];
+  unsigned long long share_ppm;  // HOST-written by the sampler: the process's measured GPU share, ppm
+  unsigned long long pad;
   mivgpu_gate_trace_entry trace[MIVGPU_GATE_TRACE];  // ring, index = gates % N
   long long hold_end_ns[MIVGPU_GATE_SLOTS];          // device ns at which a slot's hold ends
 };
@@ -92,7 +93,7 @@ __device__ __forceinline__ void astoreu(unsigned long long* p, unsigned long lon
 
 extern "C" __global__ void __launch_bounds__(64)
 mivgpu_gate(mivgpu_gate_state* st, mivgpu_gate_host_stats* hs, long long submit_ns,
-            int slot, unsigned int rate_ppm, long long cap_ns, long long max_hold_ns, unsigned int share_ppm,
+            int slot, unsigned int rate_ppm, long long cap_ns, long long max_hold_ns, unsigned int use_share,
             unsigned int flags) {
   if (threadIdx.x != 0) return;
   if (slot < 0 || slot >= MIVGPU_GATE_SLOTS) slot = 0;
@@ -130,10 +131,16 @@ mivgpu_gate(mivgpu_gate_state* st, mivgpu_gate_host_stats* hs, long long submit_
   long long begin = prev_exit > submit_ns ? prev_exit : submit_ns;
   if (submit_ns < 0 || begin <= 0 || begin > now) begin = now;
   long long busy = now - begin;
-  // weight by the measured share (ppm, passed at enqueue: the sampler's
-  // 20-ms average moves far slower than a queue drains; 0 = no sample yet ->
-  // plain wall time).  No host-memory read on the gate's path.
-  if (share_ppm > 0 && share_ppm < 1000000u) busy = (long long)(((__int128)busy * share_ppm) / 1000000);
+  // Weight by the measured share (ppm) as of NOW, read from host memory: the
+  // host can run far ahead of a held stream (hundreds of queued graph
+  // launches), so a share captured at enqueue time would be stale (measured:
+  // 2 x 50 % tenants 0.86 of unthrottled, fairness 0.83, vs 1.01 / 0.999).
+  // 0 = no sample yet (or no KFD view) -> plain wall time.
+  if (use_share && hs) {
+    const unsigned long long share =
+        __hip_atomic_load(&hs->share_ppm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (share > 0 && share < 1000000ull) busy = (long long)(((__int128)busy * (long long)share) / 1000000);
+  }
   tokens -= busy;
   // Bound the debt to one burst: a single mis-measured interval can never
   // stall a tenant for longer than cap / rate.

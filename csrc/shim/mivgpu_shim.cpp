@@ -1047,8 +1047,9 @@ std::atomic<uint64_t> g_launches_local{0};
 
 // Governor (gate) per device.  Host stats = 8 counters + a 128-entry trace
 // ring of 8 x int64 per gate + 64 per-slot hold ends (layout: governor.hip
-// mivgpu_gate_host_stats).
+// mivgpu_gate_host_stats; counter 6 is the sampler's measured share).
 constexpr size_t kHostStatsBytes = 64 + 128 * 64 + 64 * 8;
+constexpr int kHsSharePpm = 6;          // u64 index of share_ppm (sampler -> gate)
 constexpr int kHsHoldEnd = 8 + 128 * 8; // u64 index of hold_end_ns[0]
 struct GateSlot {
   hipStream_t stream;
@@ -1174,7 +1175,6 @@ std::atomic<bool> g_occ_started{false};
 std::atomic<bool> g_occ_live[MIVGPU_MAX_DEVICES];
 std::atomic<uint64_t> g_last_gate_ns[MIVGPU_MAX_DEVICES];   // coarse clock of the latest gate
 std::atomic<uint64_t> g_last_launch_ns{0};                   // coarse clock of the latest launch
-std::atomic<uint32_t> g_share_ppm[MIVGPU_MAX_DEVICES];       // sampler -> gate argument (0 = none yet)
 
 int read_occ(int fd) {
   char buf[32];
@@ -1273,7 +1273,7 @@ bool occ_sample(int dev, uint64_t now) {
     o.share_avg = o.share_avg < 0 ? share : o.share_avg + a * (share - o.share_avg);
     uint64_t ppm = (uint64_t)(o.share_avg * 1e6 + 0.5);
     if (!ppm) ppm = 1;   // 0 means "no sample yet" to the gate
-    g_share_ppm[dev].store((uint32_t)ppm, std::memory_order_relaxed);
+    if (hs) __atomic_store_n(const_cast<uint64_t*>(&hs[kHsSharePpm]), ppm, __ATOMIC_RELAXED);
     if (g_slot >= 0) __atomic_store_n(&g_region->procs[g_slot].util[dev].share_ppm, ppm, __ATOMIC_RELAXED);
   }
   if (g_slot >= 0) {
@@ -1349,13 +1349,12 @@ void enqueue_gate_locked(int dev, DeviceGate& G, int slot, hipStream_t stream, u
   unsigned int rate_ppm = (unsigned int)(rate < 1000000ull ? rate : 1000000ull);
   long long cap = g_cfg.gate_cap_ns, hold = g_cfg.gate_max_hold_ns;
   int slot_arg = slot;
-  unsigned int share_ppm = g_occ_live[dev].load(std::memory_order_acquire)
-                               ? g_share_ppm[dev].load(std::memory_order_relaxed) : 0u;
+  unsigned int use_share = g_occ_live[dev].load(std::memory_order_acquire) ? 1u : 0u;
   unsigned int flags = g_cfg.gate_trace ? 1u : 0u;
-  const bool occupancy = share_ppm != 0;
+  const bool occupancy = use_share != 0;
   void* state = G.state;
   void* hs = G.host_stats;
-  void* args[] = {&state, &hs, &submit_dev, &slot_arg, &rate_ppm, &cap, &hold, &share_ppm, &flags};
+  void* args[] = {&state, &hs, &submit_dev, &slot_arg, &rate_ppm, &cap, &hold, &use_share, &flags};
   if (real_hipModuleLaunchKernel()(G.gate_fn, 1, 1, 1, 64, 1, 1, 0, stream, args, nullptr) != hipSuccess) {
     static std::atomic<bool> warned{false};
     if (!warned.exchange(true)) mlog(1, "device %d: governor gate launch failed; this batch is not throttled", dev);

@@ -56,9 +56,13 @@ def busy_share(trace_dir: str, skip_first_s: float = 0.0) -> dict:
         span = max(e for _, e in work) - t0
         busy = _union(work)
         gate = [(max(s, t0), e) for s, e in d["gate"] if e > t0]
+        # gates that did not hold (< 100 us): the governor's per-gate cost
+        quick = sorted((e - s) / 1e3 for s, e in d["gate"] if e - s < 100_000)
         out[pid] = {"kernels": len(work), "span_ms": round(span / 1e6, 2), "busy_ms": round(busy / 1e6, 2),
                     "busy_share": round(busy / span, 4) if span else None, "gates": len(gate),
-                    "gate_hold_ms": round(_union(gate) / 1e6, 2) if gate else 0.0}
+                    "gate_hold_ms": round(_union(gate) / 1e6, 2) if gate else 0.0,
+                    "nonholding_gates": len(quick),
+                    "nonholding_gate_us_p50": round(quick[len(quick) // 2], 2) if quick else None}
     return out
 
 
