@@ -63,7 +63,11 @@ def main():
     ap.add_argument("--gpumem-mib", type=int, default=36864, help="HBM hard limit per slice")
     ap.add_argument("--model", default="qwen3-8b", choices=["qwen3-8b", "qwen3-tiny"])
     ap.add_argument("--mode", default="all", choices=["all", "both", "shim", "native"],
-                    help="all = native (same queues) + native (HIP default queues) + shim rounds")
+                    help="all = shim + masked_noshim + temporal + native (same queues) + native (HIP default "
+                         "queues) rounds; both = shim + native")
+    ap.add_argument("--rounds", default="",
+                    help="explicit comma list of rounds to run, in this order (experiments): shim, masked_noshim, "
+                         "temporal, native, native_hip_default")
     ap.add_argument("--no-spatial", action="store_true", help="no HSA_CU_MASK (temporal governor)")
     ap.add_argument("--active-slices", type=int, default=0,
                     help="run only the first K of the --slices planned slices (same masks/limits; 0 = all)")
@@ -121,14 +125,22 @@ def main():
     # round that oversubscribes the hardware queues (8 slices x HIP's default 4
     # queues) was seen to leave the next round on the GPU unfair (one 8-slice
     # shim round behind it: fairness 0.51, 6.3k tok/s; alone: 0.99, 8.2k).
+    wanted = [r for r in args.rounds.split(",") if r]
+    if not wanted:
+        wanted = {"all": ["shim", "masked_noshim", "temporal", "native", "native_hip_default"],
+                  "both": ["shim", "native"], "shim": ["shim"], "native": ["native"]}[args.mode]
+        if args.slices <= 1 or args.no_spatial:
+            wanted = [r for r in wanted if r not in ("masked_noshim", "temporal")]
+        if args.slices <= 1 or not args.hw_queues:
+            wanted = [r for r in wanted if r != "native_hip_default"]
     rounds = []
-    if args.mode in ("all", "both", "shim"):
+    if "shim" in wanted:
         rounds.append(("shim", spawn_round(
             with_env(plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib,
                                  spatial=not args.no_spatial, policy=args.policy,
                                  hw_queues=args.hw_queues or None)),
             phys, work, log_dir, child_args, "shim")))
-    if args.mode == "all" and args.slices > 1 and not args.no_spatial:
+    if "masked_noshim" in wanted:
         # the same CU masks and queues without libmivgpu.so: what the shim
         # itself costs (the overhead vs native also contains the
         # partitioning's own benefit)
@@ -137,18 +149,21 @@ def main():
             sp.shim = False
         rounds.append(("masked_noshim", spawn_round(with_env(bare), phys, work / "bare", log_dir, child_args,
                                                     "masked_noshim")))
+    if "temporal" in wanted:
         # the same slices time-shared by the governor gate instead of CU masks
         # (BASELINE config 3: "4 pods x 25% gpucores, CU-throttle governor kernel")
         rounds.append(("temporal", spawn_round(
             with_env(plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib, spatial=False,
                                  policy="force", hw_queues=args.hw_queues or None)),
             phys, work / "temporal", log_dir, child_args, "temporal")))
-    if args.mode in ("all", "both", "native"):
+    if "native" in wanted:
         rounds.append(("native", spawn_round(native_specs(args.hw_queues), phys, work, log_dir, child_args,
                                              "native")))
-    if args.mode == "all" and args.slices > 1 and args.hw_queues:
+    if "native_hip_default" in wanted:
         rounds.append(("native_hip_default", spawn_round(native_specs(0), phys, work, log_dir, child_args,
                                                          "native_hip_default")))
+    order = {name: i for i, name in enumerate(wanted)}
+    rounds.sort(key=lambda r: order[r[0]])
 
     import torch
     import torch.distributed as dist
@@ -203,7 +218,7 @@ def main():
         coll = [measure("all_reduce", nb, env, iters=10, warmup=3) for nb in sizes]
 
     if rank == 0:
-        head = results.get("shim") or results["native"]
+        head = results.get("shim") or results.get("native") or next(iter(results.values()))
         per_slice = [round(d["tok_s"], 1) for d in head["done"]]
         out = {
             "metric": METRIC,
@@ -230,7 +245,7 @@ def main():
                 "isolation": ("HSA_CU_MASK + libmivgpu" if not args.no_spatial else f"governor ({args.policy})")
                 + (f" + {args.hw_queues} HW queue/slice" if args.hw_queues and args.slices > 1 else ""),
             },
-            "round": "shim" if "shim" in results else "native",
+            "round": "shim" if "shim" in results else ("native" if "native" in results else next(iter(results))),
             "per_slice_tok_s_rank0": per_slice,
             "slice_fairness_min_over_max": round(min(per_slice) / max(per_slice), 3) if per_slice else None,
             "slice_mem_total_mib": [rd["mem_total_mib"] for rd in head["ready"]],

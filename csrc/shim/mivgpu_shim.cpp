@@ -1073,6 +1073,7 @@ struct DeviceGate {
   int64_t offset_ns = 0;        // device_ns - host_mono_ns
   bool stamper_started = false;
   std::atomic<void*> hs_pub{nullptr};  // host_stats, published for the sampler thread
+  std::atomic<uint64_t> enqueued{0};   // gates enqueued; host_stats[2] counts the ones that ran
   GateSlot slots[64];
 };
 DeviceGate g_gates[MIVGPU_MAX_DEVICES];
@@ -1263,11 +1264,22 @@ bool occ_sample(int dev, uint64_t now) {
   o.last_ns = now;
   o.share_ns += share * (double)dt;
   const uint64_t total = (uint64_t)o.share_ns;
-  const uint64_t last_launch = g_last_launch_ns.load(std::memory_order_relaxed);
-  // (a sample taken while the governor itself holds this process says
-  // nothing about contention: skipped)
-  const bool contending =
-      holding == 0 && (own > 0 || (others > 0 && coarse_ns() - last_launch < 5000000ull));
+  // Contending = waves resident, or work queued behind others: a gate has
+  // been enqueued that has not run yet (every batch is closed by a gate, so
+  // the GPU still owes this process work).  A sample taken while the
+  // governor itself holds the process says nothing about contention and is
+  // skipped.  (A "launched within the last few ms" test instead missed the
+  // queued time of graph replays, biasing the share up by the fraction of
+  // time the process waits: 8 governed slices collapsed into running one at
+  // a time, 3.4-3.8k tok/s.)
+  bool pending = false;
+  if (hs) {
+    const uint64_t done = __atomic_load_n(&hs[2], __ATOMIC_RELAXED);
+    pending = G.enqueued.load(std::memory_order_acquire) > done;
+  } else {
+    pending = coarse_ns() - g_last_launch_ns.load(std::memory_order_relaxed) < 5000000ull;
+  }
+  const bool contending = holding == 0 && (own > 0 || (others > 0 && pending));
   if (contending) {
     const double a = (double)dt / g_cfg.share_tau_ns < 1.0 ? (double)dt / g_cfg.share_tau_ns : 1.0;
     o.share_avg = o.share_avg < 0 ? share : o.share_avg + a * (share - o.share_avg);
@@ -1361,6 +1373,7 @@ void enqueue_gate_locked(int dev, DeviceGate& G, int slot, hipStream_t stream, u
     return;
   }
   g_last_gate_ns[dev].store(coarse_ns(), std::memory_order_relaxed);
+  G.enqueued.fetch_add(1, std::memory_order_release);
   tmark("mivgpu:gate dev=%d slot=%d rate_pct=%u charge=%s", dev, slot, rate_ppm / 10000u,
         occupancy ? "occupancy" : "wall");
   S.last_gate_host_ns = now;
