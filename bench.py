@@ -65,6 +65,9 @@ def main():
     ap.add_argument("--mode", default="all", choices=["all", "both", "shim", "native"],
                     help="all = shim + masked_noshim + temporal + native (same queues) + native (HIP default "
                          "queues) rounds; both = shim + native")
+    ap.add_argument("--round-gap", type=float, default=-1.0,
+                    help="seconds to idle between rounds (default: 5 at >= 8 slices, else 0): at 8 slices the round "
+                         "right after another ran slower and unfair (profiles/README.md §26)")
     ap.add_argument("--rounds", default="",
                     help="explicit comma list of rounds to run, in this order (experiments): shim, masked_noshim, "
                          "temporal, native, native_hip_default")
@@ -168,14 +171,22 @@ def main():
     import torch
     import torch.distributed as dist
 
-    dev = "cpu" if cpu else "cuda"
+    # The bench process itself must hold no hardware queues while the slices
+    # run: a GPU tensor or an RCCL barrier gives it two, and at 8 slices the
+    # ninth queue-owning process on the GPU pushed the round after the first
+    # into hardware-scheduler oversubscription (half the slices at half speed,
+    # fairness 0.49; parent_queues probe, profiles/README.md §27).  So the
+    # harness talks over gloo with CPU tensors; RCCL is only used after the
+    # timed rounds, for the collective check (cuda tensors -> nccl).
     if world > 1:
         if cpu:
             dist.init_process_group("gloo")
         else:
             torch.cuda.set_device(local_rank)
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
-        barrier = dist.barrier
+            dist.init_process_group("cpu:gloo,cuda:nccl")
+
+        def barrier():
+            dist.all_reduce(torch.zeros(1))       # CPU tensor: gloo
     else:
         if not cpu:
             torch.cuda.set_device(0)
@@ -185,8 +196,11 @@ def main():
         if not cpu:
             torch.cuda.synchronize()
 
+    gap = args.round_gap if args.round_gap >= 0 else (5.0 if args.slices >= 8 else 0.0)
     results = {}
-    for name, procs in rounds:
+    for i, (name, procs) in enumerate(rounds):
+        if i and gap > 0 and not cpu:
+            time.sleep(gap)
         mon = None
         if args.monitor > 0 and name in ("shim", "temporal"):
             from k8s_vgpu_scheduler_amd.bench.slices import RoundMonitor
@@ -194,8 +208,8 @@ def main():
         r = run_round(procs, barrier=barrier, sync=sync)
         if mon is not None:
             r["monitor"] = mon.stop()
-        wall = torch.tensor([r["wall_s"]], dtype=torch.float64, device=dev)
-        toks = torch.tensor([float(r["tokens"])], dtype=torch.float64, device=dev)
+        wall = torch.tensor([r["wall_s"]], dtype=torch.float64)        # CPU: no queues in this process
+        toks = torch.tensor([float(r["tokens"])], dtype=torch.float64)
         if world > 1:
             dist.all_reduce(wall, op=dist.ReduceOp.MAX)
             dist.all_reduce(toks, op=dist.ReduceOp.SUM)
@@ -294,7 +308,7 @@ def main():
             Path(args.out).parent.mkdir(parents=True, exist_ok=True)
             Path(args.out).write_text(line + "\n")
     if world > 1:
-        dist.barrier()
+        barrier()
         dist.destroy_process_group()
 
 
