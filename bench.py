@@ -65,9 +65,9 @@ def main():
     ap.add_argument("--mode", default="all", choices=["all", "both", "shim", "native"],
                     help="all = shim + masked_noshim + temporal + native (same queues) + native (HIP default "
                          "queues) rounds; both = shim + native")
-    ap.add_argument("--round-gap", type=float, default=-1.0,
-                    help="seconds to idle between rounds (default: 5 at >= 8 slices, else 0): at 8 slices the round "
-                         "right after another ran slower and unfair (profiles/README.md §26)")
+    ap.add_argument("--round-gap", type=float, default=0.0,
+                    help="seconds to idle between rounds (the 8-slice second-round slowdown this was tried for "
+                         "was the bench process owning GPU queues, profiles/README.md §27)")
     ap.add_argument("--rounds", default="",
                     help="explicit comma list of rounds to run, in this order (experiments): shim, masked_noshim, "
                          "temporal, native, native_hip_default")
@@ -196,7 +196,7 @@ def main():
         if not cpu:
             torch.cuda.synchronize()
 
-    gap = args.round_gap if args.round_gap >= 0 else (5.0 if args.slices >= 8 else 0.0)
+    gap = args.round_gap
     results = {}
     for i, (name, procs) in enumerate(rounds):
         if i and gap > 0 and not cpu:
