@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -167,9 +168,26 @@ EXPORT hipError_t hipLaunchKernel(const void*, dim3, dim3, void**, size_t, hipSt
   launches++;
   return hipSuccess;
 }
-EXPORT hipError_t hipModuleLaunchKernel(hipFunction_t, unsigned, unsigned, unsigned, unsigned,
-                                        unsigned, unsigned, unsigned, hipStream_t, void**, void**) {
+// MOCKHIP_GOVERNOR=1: the governor's code object "loads" and its two kernels
+// run on the host at launch (the clock kernel writes CLOCK_MONOTONIC, the gate
+// counts itself done in the host stats without holding), so the shim's whole
+// gating path -- enqueue, idle stamper, occupancy sampler -- runs on the CPU
+// (race tests under ThreadSanitizer).  Otherwise no code object loads.
+enum MockFn : uintptr_t { kNoFn = 0, kGateFn = 0x6a7e, kClockFn = 0xc10c };
+bool mock_governor() { return getenv("MOCKHIP_GOVERNOR") != nullptr; }
+EXPORT hipError_t hipModuleLaunchKernel(hipFunction_t f, unsigned, unsigned, unsigned, unsigned,
+                                        unsigned, unsigned, unsigned, hipStream_t, void** args, void**) {
   launches++;
+  const uintptr_t fn = reinterpret_cast<uintptr_t>(f);
+  if (fn == kClockFn && args) {
+    long long* out = *static_cast<long long**>(args[0]);
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    __atomic_store_n(out, (long long)ts.tv_sec * 1000000000ll + ts.tv_nsec, __ATOMIC_RELEASE);
+  } else if (fn == kGateFn && args) {
+    unsigned long long* hs = *static_cast<unsigned long long**>(args[1]);
+    if (hs) __atomic_fetch_add(&hs[2], 1ull, __ATOMIC_ACQ_REL);   // gates done
+  }
   return hipSuccess;
 }
 EXPORT hipError_t hipGraphLaunch(hipGraphExec_t, hipStream_t) { launches++; return hipSuccess; }
@@ -178,9 +196,17 @@ EXPORT hipError_t hipStreamIsCapturing(hipStream_t, hipStreamCaptureStatus* s) {
   return hipSuccess;
 }
 EXPORT hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
-// No GPU: the governor code object cannot load, so temporal gating stays off.
-EXPORT hipError_t hipModuleLoadData(hipModule_t*, const void*) { return hipErrorNoBinaryForGpu; }
-EXPORT hipError_t hipModuleGetFunction(hipFunction_t*, hipModule_t, const char*) {
-  return hipErrorNotFound;
+// No GPU: the governor code object loads only in MOCKHIP_GOVERNOR mode.
+EXPORT hipError_t hipModuleLoadData(hipModule_t* m, const void*) {
+  if (!mock_governor()) return hipErrorNoBinaryForGpu;
+  *m = reinterpret_cast<hipModule_t>(0x10001);
+  return hipSuccess;
+}
+EXPORT hipError_t hipModuleGetFunction(hipFunction_t* f, hipModule_t, const char* name) {
+  if (!mock_governor()) return hipErrorNotFound;
+  if (!strcmp(name, "mivgpu_gate")) *f = reinterpret_cast<hipFunction_t>(kGateFn);
+  else if (!strcmp(name, "mivgpu_clock")) *f = reinterpret_cast<hipFunction_t>(kClockFn);
+  else return hipErrorNotFound;
+  return hipSuccess;
 }
 EXPORT unsigned long long mockhip_launch_count(void) { return launches.load(); }

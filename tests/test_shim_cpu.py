@@ -414,3 +414,28 @@ def test_governor_engages_only_where_the_mask_does_not_hold_the_limit(native_bui
     run(native_build, tmp_path, "launch", 3, cache="g.cache", env=env)
     lines = trace.read_text().splitlines() if trace.exists() else []
     assert ("push mivgpu:governor-init" in lines) == gated, lines
+
+
+def test_governor_host_path_on_the_mock(native_build, tmp_path):
+    """With the mock running the gate on the host, a governed launch loop
+    enqueues gates (every 256 launches at most, in front of every graph
+    launch, and the idle stamper closes the last batch) and the counters
+    reach the region."""
+    trace = tmp_path / "roctx.txt"
+    env = {"HIP_DEVICE_CORE_LIMIT": "50", "GPU_CORE_UTILIZATION_POLICY": "force", "MOCKHIP_GOVERNOR": "1",
+           "MIVGPU_ROCTX": "1", "MIVGPU_ROCTX_LIB": str(native_build["roctx"]), "MOCK_ROCTX_OUT": str(trace)}
+    e = dict(os.environ, MOCKHIP_TOTAL_MIB="65536", MIVGPU_SHARED_CACHE=str(tmp_path / "gov.cache"),
+             LD_PRELOAD=str(native_build["shim"]), **env)
+    p = subprocess.Popen([str(native_build["driver"]), "launch", "2000", "sleep", "1500"], env=e,
+                         stdout=subprocess.PIPE, text=True)
+    json.loads(p.stdout.readline())
+    time.sleep(0.8)
+    reg = R.SharedRegion(str(tmp_path / "gov.cache"))
+    gates = reg.active_procs()[0].util[0].gates
+    reg.close()
+    p.wait(timeout=30)
+    lines = trace.read_text().splitlines()
+    assert "push mivgpu:governor-init" in lines
+    n = sum(1 for l in lines if l.startswith("mark mivgpu:gate dev=0"))
+    assert n >= 2000 // 256 and gates >= 1, (n, gates)
+    assert all("charge=wall" in l for l in lines if l.startswith("mark mivgpu:gate"))   # no KFD view

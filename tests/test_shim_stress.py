@@ -79,14 +79,16 @@ def test_stress_with_runtime_vram_accounting(kind, native_build, tmp_path):
     """Concurrent alloc/free and launches with the KFD context accounting and
     the occupancy sampler active (the mock runtime publishes its per-process
     VRAM and wave-count files, the other stress process is a peer on the same
-    GPU), the governor path engaged: no sanitizer reports, no
+    GPU), the governor's whole host path engaged (the mock runs the gate and
+    clock kernels on the host: enqueue, idle stamper, sampler): no sanitizer
+    reports, no
     errors, and the shared region is clean once every process has exited."""
     from tests.test_shim_cpu import _fake_kfd
 
     kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
     env = {"MIVGPU_KFD_SYSFS": str(kfd), "MOCKHIP_KFD_SYSFS": str(kfd), "MOCKHIP_KFD_GPU_ID": "4242",
            "MIVGPU_CONTEXT_REFRESH_MS": "1", "HIP_DEVICE_CORE_LIMIT": "50", "GPU_CORE_UTILIZATION_POLICY": "force",
-           "MOCKHIP_KFD_OCC": "1",
+           "MOCKHIP_KFD_OCC": "1", "MOCKHIP_GOVERNOR": "1",
            "TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1:report_signal_unsafe=0"}
     if kind == "plain":
         driver, shim, extra = native_build["driver"], native_build["shim"], ()
