@@ -96,6 +96,13 @@ class MonitorCollector:
                                    "Time the governor held the container's streams", labels=CTR_LABELS)
         cumask = GaugeMetricFamily("mivgpu_container_cu_mask_cus", "CUs granted through HSA_CU_MASK",
                                    labels=CTR_LABELS)
+        share = GaugeMetricFamily("mivgpu_container_gpu_share_ratio",
+                                  "Governor's measured GPU share of the container while contending (percent of "
+                                  "the resident wavefronts, KFD occupancy), summed over its processes",
+                                  labels=CTR_LABELS)
+        occw = GaugeMetricFamily("mivgpu_container_wave_occupancy",
+                                 "Last KFD cu_occupancy sample of the container's processes (CU units)",
+                                 labels=CTR_LABELS)
         part = GaugeMetricFamily("mivgpu_container_partition_info",
                                  "Compute-partition identity of a container allocation (the MI355X analogue "
                                  "of hami_mig_device_info)",
@@ -147,7 +154,11 @@ class MonitorCollector:
                 busy.add_metric(lab, r.busy_ns(i) / 1e9)
                 held.add_metric(lab, sum(p.util[i].throttled_ns for p in r.active_procs()) / 1e9)
                 cumask.add_metric(lab, float(r.r.cu_mask_count[i]))
-        yield from (used, limit, dmem, dutil, lastk, ctx, mod, buf, busy, held, cumask, part)
+                procs = r.active_procs()
+                if any(p.util[i].share_ppm for p in procs):
+                    share.add_metric(lab, min(100.0, sum(p.util[i].share_ppm for p in procs) / 1e4))
+                occw.add_metric(lab, float(sum(p.util[i].occupancy for p in procs)))
+        yield from (used, limit, dmem, dutil, lastk, ctx, mod, buf, busy, held, cumask, part, share, occw)
         if self.legacy:
             yield from (l_used, l_limit, l_desc, l_cutil, l_lastk)
 

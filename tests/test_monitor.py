@@ -201,6 +201,7 @@ def test_container_utilization_from_shim_or_kfd(tmp_path):
     busy.close()
     rep = make_container(tmp_path, "u2", "main", uuid="GPU-0000")
     rep.r.procs[0].util[0].share_ns, rep.r.procs[0].util[0].util_pct = 5 * 10 ** 9, 40
+    rep.r.procs[0].util[0].share_ppm, rep.r.procs[0].util[0].occupancy = 250_000, 64
     rep.close()
     idle = make_container(tmp_path, "u3", "main", uuid="GPU-0000")
     idle.r.procs[0].hostpid = 999                    # holds the GPU, no waves
@@ -217,6 +218,11 @@ def test_container_utilization_from_shim_or_kfd(tmp_path):
     assert util("busy") == 75.0
     assert util("rep") == 40.0
     assert util("idle") == 0.0
+    # the governor's measured share and last wave sample, as the shim published them
+    lab = 'container="main",device_uuid="GPU-0000",namespace="default",pod="rep",vdevice_index="0"'
+    assert f"mivgpu_container_gpu_share_ratio{{{lab}}} 25.0" in text
+    assert f"mivgpu_container_wave_occupancy{{{lab}}} 64.0" in text
+    assert 'mivgpu_container_gpu_share_ratio{container="main",device_uuid="GPU-0000",namespace="default",pod="idle"' not in text
 
 
 def test_partition_info_and_legacy_series(tmp_path):
