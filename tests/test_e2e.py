@@ -7,6 +7,7 @@ HBM limit, the shared region and the monitor's per-pod metrics are real.
 The GPU variant of this test (tests/test_e2e_gpu.py) runs a PyTorch workload
 on the MI355X instead."""
 
+import json
 import subprocess
 
 import pytest
@@ -81,3 +82,25 @@ def test_pod_lifecycle(cluster, native_build):
     wait_for(lambda: not [1 for l, v in samples(cl.metrics("sched_metrics"), "hami_vgpu_memory_allocated_bytes")
                           if l.get("pod") == "vgpu-a"], 30, "scheduler to release the pod")
     assert all(v is None for v in cl.alive().values()), cl.alive()
+
+
+def test_gputype_and_uuid_selection(cluster):
+    """Type and uuid selectors through the real binaries (webhook, /filter,
+    /bind, Allocate); the same cases run against the amd-smi registered card in
+    tests/test_e2e_gpu.py."""
+    cl = cluster
+    devs = codec.unmarshal_node_devices(
+        cl.api.cluster.get("nodes", "node1")["metadata"]["annotations"]["hami.io/node-amd-register"])
+    cases = [("want-mi355", {"amd.com/use-gputype": "MI355"}, "node1"),
+             ("avoid-mi355", {"amd.com/nouse-gputype": "MI355"}, None),
+             ("want-mi300", {"amd.com/use-gputype": "MI300X"}, None),
+             ("want-uuid", {"amd.com/use-gpu-uuid": devs[1].id}, "node1"),
+             ("avoid-uuid", {"amd.com/nouse-gpu-uuid": ",".join(d.id for d in devs)}, None)]
+    for name, annos, want in cases:
+        cl.submit(amd_pod(name, mem=1024, cores=10, annotations=annos))
+        assert cl.schedule("default", name) == want, (name, annos)
+        if want:
+            alloc = cl.start_containers("default", name)[0]
+            if "use-gpu-uuid" in str(annos):
+                assert devs[1].id in json.dumps(alloc), alloc
+        cl.delete_pod("default", name)

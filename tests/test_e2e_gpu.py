@@ -104,3 +104,27 @@ def test_pod_on_mi355x_end_to_end(cluster):
     assert alloc_m == [36864 * MIB]
     cl.delete_pod("default", "llm-a")
     assert all(v is None for v in cl.alive().values()), cl.alive()
+
+
+def test_gputype_and_uuid_selection_on_the_real_node(cluster):
+    """amd.com/use-gputype / nouse-gputype and use-gpu-uuid against what the
+    amd-smi backend registered for the real card (device.go's type and uuid
+    selectors; VERDICT r1: the registered type must be the MI355X name, never
+    "AMD Radeon Graphics")."""
+    cl = cluster
+    devs = codec.unmarshal_node_devices(
+        cl.api.cluster.get("nodes", "node1")["metadata"]["annotations"]["hami.io/node-amd-register"])
+    assert "MI355" in devs[0].type and "Radeon" not in devs[0].type, devs[0].type
+    assert devs[0].id.startswith("GPU-"), devs[0].id
+    cases = [("want-mi355", {"amd.com/use-gputype": "MI355"}, "node1"),
+             ("avoid-mi355", {"amd.com/nouse-gputype": "MI355"}, None),
+             ("want-mi300", {"amd.com/use-gputype": "MI300X"}, None),
+             ("want-uuid", {"amd.com/use-gpu-uuid": devs[0].id}, "node1"),
+             ("avoid-uuid", {"amd.com/nouse-gpu-uuid": ",".join(d.id for d in devs)}, None)]
+    for name, annos, want in cases:
+        cl.submit(amd_pod(name, mem=1024, cores=10, annotations=annos))
+        assert cl.schedule("default", name) == want, (name, annos)
+        if want:
+            cl.start_containers("default", name)    # Allocate releases the node lock Bind took
+        cl.delete_pod("default", name)
+
