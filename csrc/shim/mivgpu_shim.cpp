@@ -1056,9 +1056,12 @@ struct GateSlot {
   uint64_t last_gate_host_ns;
   uint64_t first_submit_host_ns;   // first launch since the last gate (0 = none pending)
   bool used;
-  uint64_t last_launch_host_ns;    // most recent launch on this stream
+  // most recent launch on this stream, and the host threads inside a launch
+  // call on it: raised under G.mu, lowered lock-free when the call returns
+  // (LaunchScope), so a governed launch takes the mutex once
+  std::atomic<uint64_t> last_launch_host_ns;
   int batch_launches;              // launches since the last gate
-  int in_launch;                   // host threads inside a launch call on this stream
+  std::atomic<int> in_launch;
 };
 struct DeviceGate {
   std::mutex mu;
@@ -1403,7 +1406,13 @@ int find_slot_locked(DeviceGate& G, hipStream_t stream, bool create, uint64_t no
   }
   if (!create) return -1;
   int slot = free_slot >= 0 ? free_slot : (int)(reinterpret_cast<uintptr_t>(stream) % 64);
-  G.slots[slot] = GateSlot{stream, 0, 0, true, 0, 0, 0};
+  GateSlot& S = G.slots[slot];
+  S.stream = stream;
+  S.last_gate_host_ns = S.first_submit_host_ns = 0;
+  S.used = true;
+  S.last_launch_host_ns.store(0, std::memory_order_relaxed);
+  S.batch_launches = 0;
+  S.in_launch.store(0, std::memory_order_relaxed);
   (void)now;
   return slot;
 }
@@ -1449,8 +1458,9 @@ void* stamper_main(void* arg) {
       // idleness: a gate enqueued now could land in front of that launch's
       // packets and close its batch before the work is in it (measured: a
       // 50 % limit ran at 67-86 % of the unthrottled rate under backpressure)
-      if (S.in_launch > 0) continue;
-      if (now - S.last_launch_host_ns < kStampIdleNs) continue;
+      // the idle clock is stored before in_launch drops (release)
+      if (S.in_launch.load(std::memory_order_acquire) > 0) continue;
+      if (now - S.last_launch_host_ns.load(std::memory_order_relaxed) < kStampIdleNs) continue;
       if (stream_capturing(S.stream)) continue;
       enqueue_gate_locked(dev, G, i, S.stream, now);
       S.first_submit_host_ns = 0;
@@ -1491,8 +1501,8 @@ int maybe_gate(hipStream_t stream, bool graph, int dev) {
   uint64_t now = mono_ns();
   int slot = find_slot_locked(G, stream, true, now);
   GateSlot& S = G.slots[slot];
-  S.last_launch_host_ns = now;
-  ++S.in_launch;
+  S.last_launch_host_ns.store(now, std::memory_order_relaxed);
+  S.in_launch.fetch_add(1, std::memory_order_relaxed);
   if (!G.stamper_started) start_stamper_locked(dev, G);
   const bool pending = S.first_submit_host_ns != 0;
   if (!pending || S.last_gate_host_ns == 0 || graph || S.batch_launches >= kMaxBatchLaunches ||
@@ -1519,11 +1529,12 @@ struct LaunchScope {
   explicit LaunchScope(LaunchTicket x) : t(x) {}
   ~LaunchScope() {
     if (t.slot < 0) return;
-    DeviceGate& G = g_gates[t.dev];
-    std::lock_guard<std::mutex> lk(G.mu);
-    GateSlot& S = G.slots[t.slot];
-    if (S.in_launch > 0) --S.in_launch;
-    S.last_launch_host_ns = mono_ns();
+    GateSlot& S = g_gates[t.dev].slots[t.slot];
+    S.last_launch_host_ns.store(mono_ns(), std::memory_order_relaxed);
+    int n = S.in_launch.load(std::memory_order_relaxed);
+    while (n > 0 && !S.in_launch.compare_exchange_weak(n, n - 1, std::memory_order_release,
+                                                       std::memory_order_relaxed)) {
+    }
   }
 };
 
