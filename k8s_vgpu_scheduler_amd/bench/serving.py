@@ -1,0 +1,135 @@
+"""Serving benchmark: TTFT and per-token latency of the OpenAI-compatible
+server natively vs inside vGPU slices (the reference's
+benchmarks/deployments/job-on-hami.yml vs job-on-nvidia-device-plugin.yml,
+run as processes on one MI355X instead of pods).
+
+Each configuration starts ``serve.server`` in its own process with exactly the
+environment a pod would get (libmivgpu.so preloaded, the grant in a limits
+file, HSA_CU_MASK / queue count for CU slices), waits for /health, drives it
+with ``serve.client`` (sequential streaming requests, warmup then timed runs),
+stops it, and ``serve.report`` compares every configuration with the first.
+
+    python -m k8s_vgpu_scheduler_amd.bench.serving --configs native,vgpu50,slice25 \\
+        --warmup 30 --runs 200 --out-dir gpurun_out/serving
+
+Configurations:
+  native    no shim, whole GPU
+  vgpu50    shim, gpumem 50 % of the card (the reference's job-on-hami.yml), all CUs
+  slice25   shim, gpucores 25: 64-CU balanced mask + 2 HW queues, gpumem 36 GiB
+  slice50   shim, gpucores 50: 128-CU mask, gpumem 72 GiB
+  temporal25 shim, gpucores 25 time-sliced by the governor (no mask, policy force)
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+from k8s_vgpu_scheduler_amd.bench.slices import SliceSpec, slice_env
+from k8s_vgpu_scheduler_amd.serve import client, report
+
+CARD_MIB = 288 * 1024     # MI355X HBM3E
+
+CONFIGS = {
+    "native": SliceSpec(index=0, gpumem_mib=None, cu_ranges=None, shim=False),
+    "vgpu50": SliceSpec(index=1, gpumem_mib=CARD_MIB // 2, cu_ranges=None),
+    "slice25": SliceSpec(index=2, gpumem_mib=36864, cu_ranges=[(0, 63)], core_pct=25, hw_queues=2),
+    "slice50": SliceSpec(index=3, gpumem_mib=73728, cu_ranges=[(0, 127)], core_pct=50, hw_queues=2),
+    "temporal25": SliceSpec(index=4, gpumem_mib=36864, cu_ranges=None, core_pct=25, policy="force"),
+}
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _log(msg):
+    print(msg, flush=True)
+
+
+def run_config(name: str, spec: SliceSpec, a, workdir: Path, log=_log) -> list[dict]:
+    env = dict(os.environ)
+    env.update(slice_env(spec, None, workdir))
+    env["PYTHONPATH"] = os.pathsep.join(p for p in (str(Path(__file__).resolve().parents[2]),
+                                                    env.get("PYTHONPATH")) if p)
+    port = free_port()
+    cmd = [sys.executable, "-u", "-m", "k8s_vgpu_scheduler_amd.serve.server", "--model", a.model,
+           "--port", str(port), "--max-model-len", str(a.max_model_len), "--max-tokens", str(a.max_tokens)]
+    if a.device:
+        cmd += ["--device", a.device]
+    if a.no_graph:
+        cmd.append("--no-graph")
+    logf = open(workdir / f"{name}.server.log", "w")
+    proc = subprocess.Popen(cmd, env=env, stdout=logf, stderr=subprocess.STDOUT, start_new_session=True)
+    url = f"http://127.0.0.1:{port}/v1/chat/completions"
+    try:
+        info = client.wait_ready(url, timeout=a.load_timeout, proc=proc)
+        log(f"[serving] {name}: ready in {info.get('load_s')} s, {a.warmup} warmup + {a.runs} runs")
+        rows = client.run(url, a.runs, a.warmup, a.prompt, a.max_tokens, str(workdir / f"{name}.jsonl"),
+                          timeout=a.request_timeout, log=lambda m: log(f"[serving] {name}:{m}"))
+    finally:
+        if proc.poll() is None:
+            os.killpg(proc.pid, signal.SIGTERM)
+            try:
+                proc.wait(timeout=60)
+            except subprocess.TimeoutExpired:
+                os.killpg(proc.pid, signal.SIGKILL)
+                proc.wait()
+        logf.close()
+    if not rows or any(r.get("t_first") is None for r in rows):
+        tail = (workdir / f"{name}.server.log").read_text()[-3000:]
+        raise RuntimeError(f"{name}: {sum(r.get('t_first') is None for r in rows)} of {len(rows)} requests "
+                           f"streamed no token; server log tail:\n{tail}")
+    return rows
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("--configs", default="native,vgpu50,slice25")
+    ap.add_argument("--model", default="qwen3-8b")
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--runs", type=int, default=200)
+    ap.add_argument("--max-tokens", type=int, default=128)
+    ap.add_argument("--max-model-len", type=int, default=4096)
+    ap.add_argument("--prompt", default=client.DEFAULT_PROMPT)
+    ap.add_argument("--device", default=None)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--load-timeout", type=float, default=600.0)
+    ap.add_argument("--request-timeout", type=float, default=60.0)
+    ap.add_argument("--out-dir", default=None)
+    a = ap.parse_args(argv)
+    names = [n.strip() for n in a.configs.split(",") if n.strip()]
+    unknown = [n for n in names if n not in CONFIGS]
+    if unknown:
+        ap.error(f"unknown configs {unknown}; choose from {sorted(CONFIGS)}")
+    workdir = Path(a.out_dir or tempfile.mkdtemp(prefix="mivgpu-serving-"))
+    workdir.mkdir(parents=True, exist_ok=True)
+    results = {}
+    t0 = time.time()
+    for n in names:
+        results[n] = run_config(n, CONFIGS[n], a, workdir)
+        s = report.summarize(results[n])
+        print(json.dumps({"config": n, "ttft_p50_ms": round(s["ttft_p50_s"] * 1e3, 3),
+                          "per_token_clean_mean_ms": round(s["per_token_clean_mean_s"] * 1e3, 4),
+                          "decode_tok_s": round(s["decode_tok_s"], 1)}), flush=True)
+    summary = report.write_report(results, workdir)
+    line = {"metric": "serving TTFT / per-token latency, vGPU slices vs native", "model": a.model,
+            "runs": a.runs, "warmup": a.warmup, "max_tokens": a.max_tokens, "data": "synthetic prompt, random-init "
+            "weights", "wall_s": round(time.time() - t0, 1), "configs": summary, "out_dir": str(workdir)}
+    (workdir / "serving.json").write_text(json.dumps(line, indent=1))
+    print(json.dumps(line))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -311,6 +311,124 @@ class Qwen3Decoder:
         self.seqlens.add_(1)
         return logits
 
+    # ---------------------------------------------------------- prefill --
+    # Prompt processing for serving (serve/engine.py): all prompt positions of
+    # one batch row in one pass.  Projections run on the same weights as the
+    # decode step -- the packed skinny kernel in row chunks of <= 128 where the
+    # decoder packed them, hipBLASLt (F.linear) elsewhere; norms on the HIP
+    # kernels; QK-norm/RoPE and the causal attention in fp32 PyTorch (batched
+    # GEMMs); K/V written into the cache in the decode kernels' layout.  A
+    # short chat prompt costs about one decode step (weight streaming).
+    PREFILL_CHUNK = 128
+
+    def _rows(self, pl, x):
+        if x.shape[0] <= self.PREFILL_CHUNK:
+            return pl(x.contiguous())
+        return torch.cat([pl(x[s:s + self.PREFILL_CHUNK].contiguous())
+                          for s in range(0, x.shape[0], self.PREFILL_CHUNK)])
+
+    def _proj(self, lw, name, x):
+        packed, plain = {"qkv": ("pqkv", "wqkv"), "o": ("po", "wo"), "gu": ("pgu", "wgu"),
+                         "d": ("pd", "wd")}[name]
+        if packed in lw:
+            return self._rows(lw[packed], x)     # gate_up: SiLU*up fused in the epilogue
+        y = F.linear(x, lw[plain])
+        if name == "gu":
+            if self.native:
+                return ops.silu_mul(y)
+            return ref.silu_mul(y)
+        return y
+
+    def _norm(self, x, w):
+        return ops.rmsnorm(x, w, self.cfg.eps) if self.native else ref.rmsnorm(x, w, self.cfg.eps)
+
+    def _add_norm(self, x, res, w):
+        if self.native:
+            return ops.add_rmsnorm(x, res, w, self.cfg.eps)
+        return ref.add_rmsnorm(x, res, w, self.cfg.eps)
+
+    def _write_kv(self, li, b, k, v):
+        """k, v: [L, Hkv, D] fp32 of positions 0..L-1 -> cache row b."""
+        L, Hkv, D = k.shape
+        kc, vc = self.k_cache[li], self.v_cache[li]
+        if not self.kv_native_layout:
+            kc[b, :, :L] = k.transpose(0, 1).to(kc.dtype)
+            vc[b, :, :L] = v.transpose(0, 1).to(vc.dtype)
+            return
+        # the packed layout is per 32-key group: whole groups, zero tail (the
+        # decode kernel writes each later position into its group)
+        Lp = -(-L // 32) * 32
+        for c, t, to_layout in ((kc, k, ops.k_to_cache_layout), (vc, v, ops.v_to_cache_layout)):
+            full = torch.zeros(1, Hkv, Lp, D, dtype=c.dtype, device=c.device)
+            full[0, :, :L] = t.transpose(0, 1).to(c.dtype)
+            c[b:b + 1, :, :Lp // 32] = to_layout(full)
+
+    def _causal_attention(self, q, k, v, chunk: int = 1024):
+        """q [L, Hq, D], k/v [L, Hkv, D] fp32 (K/V rounded to the cache dtype,
+        as decode reads them) -> [L, Hq*D] bf16."""
+        L, Hq, D = q.shape
+        G = Hq // k.shape[1]
+        kh = k.to(torch.bfloat16).float().transpose(0, 1).repeat_interleave(G, dim=0)   # [Hq, L, D]
+        vh = v.to(torch.bfloat16).float().transpose(0, 1).repeat_interleave(G, dim=0)
+        qh = q.transpose(0, 1)
+        out = torch.empty(Hq, L, D, dtype=torch.float32, device=q.device)
+        for s in range(0, L, chunk):
+            e = min(L, s + chunk)
+            sc = torch.matmul(qh[:, s:e], kh[:, :e].transpose(1, 2)) * self.scale       # [Hq, e-s, e]
+            qi = torch.arange(s, e, device=q.device)[:, None]
+            kj = torch.arange(e, device=q.device)[None, :]
+            sc.masked_fill_(kj > qi, float("-inf"))
+            out[:, s:e] = torch.matmul(torch.softmax(sc, dim=-1), vh[:, :e])
+        return out.transpose(0, 1).reshape(L, Hq * D).to(torch.bfloat16)
+
+    @torch.no_grad()
+    def prefill(self, prompt, b: int = 0) -> torch.Tensor:
+        """Process the prompt token ids into batch row ``b`` (KV for positions
+        0..L-1), set that row's next token to the greedy choice and its
+        position to L, and return the last position's logits [vocab]."""
+        if self.norm_fused:
+            raise NotImplementedError("prefill with MIVGPU_NORM_FUSED=1 (norm weights folded into the packed columns)")
+        cfg, w = self.cfg, self.w
+        ids = torch.as_tensor(prompt, dtype=torch.long, device=self.device).view(-1)
+        L = ids.numel()
+        if not 0 < L < self.T:
+            raise ValueError(f"prompt of {L} tokens does not fit a context of {self.T}")
+        Hq, Hkv, D = cfg.heads, cfg.kv_heads, cfg.head_dim
+        pos = torch.arange(L, device=self.device)
+
+        def head_norm(t, wn):
+            return t * torch.rsqrt(t.pow(2).mean(-1, keepdim=True) + cfg.eps) * wn.float()
+
+        res = F.embedding(ids, w.embed).contiguous()
+        h = self._norm(res, w.layers[0]["ln1"])
+        for li, lw in enumerate(w.layers):
+            qkv = self._proj(lw, "qkv", h).float().view(L, Hq + 2 * Hkv, D)
+            q = ref.rope_neox(head_norm(qkv[:, :Hq], lw["q_norm"]), pos, cfg.rope_theta)
+            k = ref.rope_neox(head_norm(qkv[:, Hq:Hq + Hkv], lw["k_norm"]), pos, cfg.rope_theta)
+            v = qkv[:, Hq + Hkv:]
+            self._write_kv(li, b, k, v)
+            o = self._proj(lw, "o", self._causal_attention(q, k, v))
+            h = self._add_norm(o, res, lw["ln2"])
+            d = self._proj(lw, "d", self._proj(lw, "gu", h))
+            nxt = w.layers[li + 1]["ln1"] if li + 1 < len(w.layers) else w.final_norm
+            h = self._add_norm(d, res, nxt)
+        last = h[L - 1:L].contiguous()
+        logits = (self._rows(self.p_lm, last) if self.skinny else F.linear(last, w.lm_head))[0]
+        self.tokens[b] = torch.argmax(logits)
+        self.pos[b] = L
+        self.seqlens[b] = L + 1
+        return logits
+
+    def packed_linears(self) -> list:
+        out = [pl for lw in self.w.layers for pl in lw.values() if isinstance(pl, ops.PackedLinear)]
+        return out + ([self.p_lm] if self.skinny else [])
+
+    def reserve_prefill(self):
+        """Size every packed projection's scratch for prefill row chunks, so a
+        prompt after capture() never reallocates under the graph."""
+        for pl in self.packed_linears():
+            pl.reserve(self.PREFILL_CHUNK)
+
     def capture(self, warmup: int = 2):
         """Capture one decode step into a hipGraph (state advances per replay)."""
         assert self.device.type == "cuda"
@@ -325,6 +443,8 @@ class Qwen3Decoder:
         with torch.cuda.graph(self.graph):
             self._step_impl()
         torch.cuda.synchronize()
+        for pl in self.packed_linears():
+            pl.frozen = True
 
     def step(self):
         if self.graph is not None:

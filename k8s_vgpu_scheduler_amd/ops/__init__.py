@@ -362,12 +362,28 @@ class PackedLinear:
         self.wp = pack_weight(interleave_gate_up(w) if silu_mul else w)
         self.scratch = None
         self.tickets = None
+        # set once a hipGraph holds the slabs' addresses: growing them then
+        # would free memory the graph still writes
+        self.frozen = False
+
+    def reserve(self, max_m: int):
+        """Size the split-K slabs for every row count up to ``max_m`` (before a
+        graph capture, when later calls may use other row counts)."""
+        floats = tickets = 0
+        for m in range(1, max_m + 1):
+            pl = skinny_plan(m, self.K, self.N, self.epi)
+            floats, tickets = max(floats, pl["scratch_floats"]), max(tickets, pl["tickets"])
+        self._ensure_scratch(floats, tickets, self.wp.device)
 
     @property
     def out_features(self) -> int:
         return self.N // 2 if self.silu_mul else self.N
 
     def _ensure_scratch(self, floats: int, tickets: int, device):
+        if self.frozen and ((floats and (self.scratch is None or self.scratch.numel() < floats))
+                            or (tickets and (self.tickets is None or self.tickets.numel() < tickets))):
+            raise RuntimeError("skinny_gemm: split-K scratch would grow under a captured graph; "
+                               "reserve() the row counts before capture")
         if floats and (self.scratch is None or self.scratch.numel() < floats):
             self.scratch = torch.zeros(floats, dtype=torch.float32, device=device)
         if tickets and (self.tickets is None or self.tickets.numel() < tickets):

@@ -1,0 +1,82 @@
+"""Serving path on the MI355X: native prefill (packed skinny GEMMs, packed KV
+layout) against teacher-forced decode on the HIP kernels, and the serving
+benchmark's native-vs-slice comparison on Qwen3-8B (short run)."""
+
+from __future__ import annotations
+
+import json
+import os
+from pathlib import Path
+
+import pytest
+import torch
+
+from k8s_vgpu_scheduler_amd import ops
+from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
+
+pytestmark = pytest.mark.gpu
+
+
+def test_native_prefill_matches_native_decode():
+    ops.require_native()
+    torch.manual_seed(0)
+    prompt = torch.randint(0, QWEN3_TINY.vocab, (150,)).tolist()     # > one 128-row chunk, 5 KV groups
+    a = Qwen3Decoder(QWEN3_TINY, batch=1, max_ctx=256, device="cuda")
+    assert a.skinny and a.kv_native_layout
+    a.reserve_prefill()
+    la = a.prefill(prompt).float()
+    b = Qwen3Decoder(QWEN3_TINY, batch=1, max_ctx=256, device="cuda")
+    for t in prompt:
+        b.tokens[0] = t
+        lb = b.step()[0].float()
+    torch.cuda.synchronize()
+    cos = torch.nn.functional.cosine_similarity(la, lb, dim=0).item()
+    assert cos > 0.999, cos
+    assert int(a.pos[0]) == int(b.pos[0]) == len(prompt)
+    for li in range(QWEN3_TINY.layers):
+        ka = ops.k_from_cache_layout(a.k_cache[li])[0, :, :len(prompt)].float()
+        kb = ops.k_from_cache_layout(b.k_cache[li])[0, :, :len(prompt)].float()
+        va = ops.v_from_cache_layout(a.v_cache[li])[0, :, :len(prompt)].float()
+        vb = ops.v_from_cache_layout(b.v_cache[li])[0, :, :len(prompt)].float()
+        torch.testing.assert_close(ka, kb, atol=6e-2, rtol=3e-2)
+        torch.testing.assert_close(va, vb, atol=6e-2, rtol=3e-2)
+    # the graph captured after prefill continues from the prefilled state
+    a.capture(warmup=0)
+    a.graph.replay()
+    b.step()
+    torch.cuda.synchronize()
+    assert int(a.pos[0]) == int(b.pos[0]) == len(prompt) + 1
+
+
+def test_scratch_never_grows_under_a_graph():
+    ops.require_native()
+    d = Qwen3Decoder(QWEN3_TINY, batch=1, max_ctx=256, device="cuda")
+    d.capture()
+    pl = d.packed_linears()[0]
+    pl.scratch, pl.tickets = None, None        # as if nothing were reserved
+    with pytest.raises(RuntimeError, match="under a captured graph"):
+        pl(torch.zeros(100, pl.K, dtype=torch.bfloat16, device="cuda"))
+
+
+def test_serving_native_vs_slice(tmp_path):
+    """Qwen3-8B behind the OpenAI-compatible server: native vs a 64-CU slice
+    under libmivgpu.so (short run; the full comparison is profiles/serving)."""
+    from k8s_vgpu_scheduler_amd.bench import serving
+    from k8s_vgpu_scheduler_amd.utils import build
+    build.build_all()
+    # kept for a post-mortem when run through gpurun (server logs, JSONL rows)
+    if os.environ.get("GRAFT_REPO_ROOT"):
+        tmp_path = Path(os.environ["GRAFT_REPO_ROOT"]) / "gpurun_out" / "serving_test"
+    rc = serving.main(["--configs", "native,slice25", "--warmup", "3", "--runs", "12", "--max-tokens", "32",
+                       "--out-dir", str(tmp_path)])
+    assert rc == 0
+    out = json.loads((tmp_path / "serving.json").read_text())["configs"]
+    nat, sl = out["native"], out["slice25"]
+    print(json.dumps({k: {m: v for m, v in s.items() if "ms" in m or "_s" in m} for k, s in out.items()}))
+    assert nat["tokens_per_request"] == sl["tokens_per_request"] == 32.0
+    # batch-1 decode streams the 16 GB of weights per token: ~2.5-4 ms whole
+    # GPU; a 64-CU slice reads HBM at about half the chip's rate
+    assert 1.5e-3 < nat["per_token_clean_mean_s"] < 6e-3, nat
+    assert nat["per_token_clean_mean_s"] < sl["per_token_clean_mean_s"] < 4 * nat["per_token_clean_mean_s"], out
+    assert nat["ttft_p50_s"] < 0.1 and sl["ttft_p50_s"] < 0.2, out
+    assert (tmp_path / "slice2.cache").exists()           # the slice server ran under the shim

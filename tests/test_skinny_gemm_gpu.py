@@ -272,3 +272,21 @@ def test_slice_partition_plans(mask, want):
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][0][7:])
     assert {k: out[k] for k in want} == want
+
+
+@pytest.mark.parametrize("M", [33, 92, 128])
+def test_prefill_row_counts_at_qwen3_8b_shapes(M):
+    """The serving prefill runs the packed projections on row chunks of up to
+    128 (models/qwen3.py prefill): gate_up + SiLU (24576 x 4096) and down
+    (4096 x 12288) at Qwen3-8B shapes, row counts the decode path never uses."""
+    torch.manual_seed(M)
+    for N, K, silu in ((24576, 4096, True), (4096, 12288, False)):
+        x = torch.randn(M, K, device="cuda").bfloat16()
+        w = (torch.randn(N, K, device="cuda") * 0.02).bfloat16()
+        pl = ops.PackedLinear(w, silu_mul=silu)
+        pl.reserve(128)
+        got = pl(x).float()
+        torch.cuda.synchronize()
+        gu = _ref(x, w).bfloat16().float()
+        ref = torch.nn.functional.silu(gu[:, :N // 2]) * gu[:, N // 2:] if silu else gu
+        _close(got, ref)
