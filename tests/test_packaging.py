@@ -94,15 +94,16 @@ def test_vgpu_init_installs_atomically(tmp_path):
 
 def _example_pods():
     for f in sorted((ROOT / "examples/amd").glob("*.yaml")):
-        doc = yaml.safe_load(f.read_text())
-        if doc["kind"] == "Job":
-            pod = {"apiVersion": "v1", "kind": "Pod",
-                   "metadata": {"name": doc["metadata"]["name"], "namespace": "default"},
-                   "spec": doc["spec"]["template"]["spec"]}
-        else:
-            pod = doc
-            pod["metadata"].setdefault("namespace", "default")
-        yield f.name, pod
+        docs = [d for d in yaml.safe_load_all(f.read_text()) if d]
+        for i, doc in enumerate(docs):
+            if doc["kind"] == "Job":
+                pod = {"apiVersion": "v1", "kind": "Pod",
+                       "metadata": {"name": doc["metadata"]["name"], "namespace": "default"},
+                       "spec": doc["spec"]["template"]["spec"]}
+            else:
+                pod = doc
+                pod["metadata"].setdefault("namespace", "default")
+            yield (f.name if len(docs) == 1 else f"{f.name}#{i}"), pod
 
 
 @pytest.mark.parametrize("name,pod", list(_example_pods()), ids=lambda v: v if isinstance(v, str) else "")
