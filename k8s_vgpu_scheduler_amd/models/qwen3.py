@@ -243,9 +243,9 @@ class Qwen3Decoder:
         (qkv, attention, combine, o_proj+residual, gate_up+SiLU, down+residual)."""
         cfg, w = self.cfg, self.w
         h, eps = cfg.hidden, cfg.eps
-        self.res.copy_(F.embedding(self.tokens, w.embed))
+        torch.index_select(w.embed, 0, self.tokens, out=self.res)
         # the first norm's sums of squares (one slot), later ones come from the epilogues
-        self.ss_a.view(-1, ops.SS_ROWS)[0, :self.B].copy_(self.res.float().pow(2).sum(-1))
+        torch.sum(self.res.float().pow(2), dim=-1, out=self.ss_a.view(-1, ops.SS_ROWS)[0, :self.B])
         na = 1
         for li, lw in enumerate(w.layers):
             qkv = lw["pqkv"].norm_call(self.res, out=self.qkv_buf, row_scale=(self.ss_a, na, h, eps))
@@ -255,7 +255,7 @@ class Qwen3Decoder:
             lw["pd"].norm_call(self.act, out=self.res, residual=True, ss_out=self.ss_a)
             na = self.slots_d
         logits = self.p_lm.norm_call(self.res, out=self.logits, row_scale=(self.ss_a, na, h, eps))
-        self.tokens.copy_(torch.argmax(logits, dim=-1))
+        torch.argmax(logits, dim=-1, out=self.tokens)
         self.pos.add_(1)
         self.seqlens.add_(1)
         return logits
@@ -264,8 +264,13 @@ class Qwen3Decoder:
         if self.norm_fused:
             return self._step_norm_fused()
         cfg, w = self.cfg, self.w
-        x = F.embedding(self.tokens, w.embed)
-        self.res.copy_(x)
+        # every graph node a kernel: the step's state moves through kernels that
+        # write their outputs in place (index_select / argmax with out=), never
+        # through a device-to-device copy node -- replayed after a prefill, a
+        # captured copy of the argmax result raced the argmax kernel on this
+        # stack and fed the next step a garbage token (AMD_SERIALIZE_KERNEL=3
+        # hid it; scripts/probe/prefill_graph_bisect.py)
+        torch.index_select(w.embed, 0, self.tokens, out=self.res)
         L = cfg.layers
         if self.native:
             ops.rmsnorm(self.res, w.layers[0]["ln1"], cfg.eps, out=self.h)
@@ -306,7 +311,7 @@ class Qwen3Decoder:
             else:
                 self.h.copy_(ref.add_rmsnorm(d, self.res, nxt, cfg.eps))
         logits = self.p_lm(self.h, out=self.logits) if self.skinny else F.linear(self.h, w.lm_head)
-        self.tokens.copy_(torch.argmax(logits, dim=-1))
+        torch.argmax(logits, dim=-1, out=self.tokens)
         self.pos.add_(1)
         self.seqlens.add_(1)
         return logits

@@ -48,6 +48,37 @@ def test_native_prefill_matches_native_decode():
     assert int(a.pos[0]) == int(b.pos[0]) == len(prompt) + 1
 
 
+def test_graph_replay_after_prefill_matches_eager_step():
+    """Qwen3-8B at B=1: the decode graph captured once, replayed after later
+    prefills, gives the eager step's token every time (a captured copy node
+    once raced the argmax here and fed the next replay a garbage token)."""
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_8B
+    ops.require_native()
+    d = Qwen3Decoder(QWEN3_8B, batch=1, max_ctx=4096, device="cuda")
+    d.reserve_prefill()
+    d.prefill(list(range(3, 163)))
+    d.capture()
+    for L in (92, 40, 300):
+        prompt = list(range(5, 5 + L))
+        d.prefill(prompt)
+        with torch.no_grad():
+            d._step_impl()
+        want = [int(d.tokens[0])]
+        for _ in range(7):
+            d._step_impl()
+            want.append(int(d.tokens[0]))
+        d.prefill(prompt)
+        got = []
+        for _ in range(8):
+            d.graph.replay()
+            torch.cuda.synchronize()
+            t = int(d.tokens[0])
+            assert 0 <= t < QWEN3_8B.vocab, (L, got, t)      # never replay on a garbage token
+            got.append(t)
+        assert got == want, (L, got, want)
+        assert int(d.pos[0]) == L + 8
+
+
 def test_scratch_never_grows_under_a_graph():
     ops.require_native()
     d = Qwen3Decoder(QWEN3_TINY, batch=1, max_ctx=256, device="cuda")
