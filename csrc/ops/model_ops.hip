@@ -10,6 +10,7 @@
 //   mivgpu_rmsnorm          out = rmsnorm(x) * w
 //   mivgpu_add_rmsnorm      res += x ; out = rmsnorm(res) * w      (fused)
 //   mivgpu_qk_norm_rope_kv  per-head RMSNorm(q,k) + NeoX RoPE + KV-cache append
+//   mivgpu_prefill_qk_norm_rope_kv  the same over a prompt's tokens into one cache row
 //   mivgpu_decode_attention GQA split-K flash-decoding (partials + combine)
 //   mivgpu_silu_mul         out = silu(gate) * up
 //
@@ -126,17 +127,26 @@ rmsnorm_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ res, const bf1
 // ------------------------------------------- QK-norm + RoPE + KV append ----
 // grid = (B, Hq + 2*Hkv); one wave per (token, head).  D = 128: lane l owns
 // elements l and l+64, which is exactly a NeoX rotate-half pair.
+// Decode: row b is sequence b (cache row b), q out [B][Hq][D].
+// Prefill (cache_b >= 0): the rows are the prompt tokens of ONE sequence, all
+// appended to cache row cache_b at their own positions; q is written
+// head-grouped [Hkv][G][rows][D] (the G query heads sharing a KV head are one
+// contiguous block of rows for the attention GEMMs), and K/V also go to
+// k_plain / v_plain [Hkv][rows][D] when given (the prompt's own attention).
 template <bool PACKED>
 __global__ void __launch_bounds__(64)
 qk_norm_rope_kv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ qw,
                        const bf16_t* __restrict__ kw, const int* __restrict__ pos,
                        bf16_t* __restrict__ q_out, bf16_t* __restrict__ k_cache,
                        bf16_t* __restrict__ v_cache, int Hq, int Hkv, int max_ctx, float eps,
-                       float theta) {
+                       float theta, int cache_b, bf16_t* __restrict__ k_plain,
+                       bf16_t* __restrict__ v_plain) {
   constexpr int D = 128;
   const int b = blockIdx.x;
   const int h = blockIdx.y;
   const int l = threadIdx.x;
+  const int rows = gridDim.x;
+  const int cb = cache_b >= 0 ? cache_b : b;
   const int row_stride = (Hq + 2 * Hkv) * D;
   const bf16_t* src = qkv + (size_t)b * row_stride + (size_t)h * D;
   float x0 = bf2f(src[l]);
@@ -144,15 +154,20 @@ qk_norm_rope_kv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict_
   const int p = pos[b];
   const bool in_range = p >= 0 && p < max_ctx;  // never write past the cache
   if (h >= Hq + Hkv) {  // V head: plain copy into the cache
-    if (!in_range) return;
     const int hv = h - Hq - Hkv;
+    if (v_plain) {
+      bf16_t* dst = v_plain + ((size_t)hv * rows + b) * D;
+      dst[l] = src[l];
+      dst[l + 64] = src[l + 64];
+    }
+    if (!in_range) return;
     if (PACKED) {  // V group [dt 8][q 4][r 16][e 8]: key = 8q + e, dim = 16dt + r
-      bf16_t* grp = v_cache + ((size_t)b * Hkv + hv) * (size_t)max_ctx * D + (size_t)(p >> 5) * (32 * D);
+      bf16_t* grp = v_cache + ((size_t)cb * Hkv + hv) * (size_t)max_ctx * D + (size_t)(p >> 5) * (32 * D);
       const int kq = (p & 31) >> 3, ke = p & 7;
       grp[(((l >> 4) * 4 + kq) * 16 + (l & 15)) * 8 + ke] = f2bf(x0);
       grp[((((l + 64) >> 4) * 4 + kq) * 16 + (l & 15)) * 8 + ke] = f2bf(x1);
     } else {
-      bf16_t* dst = v_cache + (((size_t)b * Hkv + hv) * max_ctx + p) * D;
+      bf16_t* dst = v_cache + (((size_t)cb * Hkv + hv) * max_ctx + p) * D;
       dst[l] = f2bf(x0);
       dst[l + 64] = f2bf(x1);
     }
@@ -172,19 +187,29 @@ qk_norm_rope_kv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict_
   const float o1 = x1 * c + x0 * s;
   bf16_t* dst;
   if (is_q) {
-    dst = q_out + ((size_t)b * Hq + h) * D;
+    if (cache_b >= 0) {
+      const int G = Hq / Hkv;
+      dst = q_out + (((size_t)(h / G) * G + h % G) * rows + b) * D;
+    } else {
+      dst = q_out + ((size_t)b * Hq + h) * D;
+    }
   } else {
-    if (!in_range) return;
     const int hk = h - Hq;
+    if (k_plain) {
+      bf16_t* kp = k_plain + ((size_t)hk * rows + b) * D;
+      kp[l] = f2bf(o0);
+      kp[l + 64] = f2bf(o1);
+    }
+    if (!in_range) return;
     if (PACKED) {  // K group [t 2][s 4][q 4][r 16][e 8]: key = 8(r/4) + 4t + r%4, dim = 32s + 8q + e
-      bf16_t* grp = k_cache + ((size_t)b * Hkv + hk) * (size_t)max_ctx * D + (size_t)(p >> 5) * (32 * D);
+      bf16_t* grp = k_cache + ((size_t)cb * Hkv + hk) * (size_t)max_ctx * D + (size_t)(p >> 5) * (32 * D);
       const int k = p & 31;
       const int kt = (k >> 2) & 1, kr = 4 * (k >> 3) + (k & 3);
       grp[(((kt * 4 + (l >> 5)) * 4 + ((l >> 3) & 3)) * 16 + kr) * 8 + (l & 7)] = f2bf(o0);
       grp[(((kt * 4 + ((l + 64) >> 5)) * 4 + (((l + 64) >> 3) & 3)) * 16 + kr) * 8 + (l & 7)] = f2bf(o1);
       return;
     }
-    dst = k_cache + (((size_t)b * Hkv + hk) * max_ctx + p) * D;
+    dst = k_cache + (((size_t)cb * Hkv + hk) * max_ctx + p) * D;
   }
   dst[l] = f2bf(o0);
   dst[l + 64] = f2bf(o1);
@@ -974,12 +999,35 @@ int mivgpu_qk_norm_rope_kv(const void* qkv, const void* qw, const void* kw, cons
     hipLaunchKernelGGL(qk_norm_rope_kv_kernel<true>, dim3(B, Hq + 2 * Hkv), dim3(64), 0, s,
                        (const bf16_t*)qkv, (const bf16_t*)qw, (const bf16_t*)kw, pos,
                        (bf16_t*)q_out, (bf16_t*)k_cache, (bf16_t*)v_cache, Hq, Hkv, max_ctx, eps,
-                       theta);
+                       theta, -1, (bf16_t*)nullptr, (bf16_t*)nullptr);
   } else {
     hipLaunchKernelGGL(qk_norm_rope_kv_kernel<false>, dim3(B, Hq + 2 * Hkv), dim3(64), 0, s,
                        (const bf16_t*)qkv, (const bf16_t*)qw, (const bf16_t*)kw, pos,
                        (bf16_t*)q_out, (bf16_t*)k_cache, (bf16_t*)v_cache, Hq, Hkv, max_ctx, eps,
-                       theta);
+                       theta, -1, (bf16_t*)nullptr, (bf16_t*)nullptr);
+  }
+  return (int)hipGetLastError();
+}
+
+// Prefill of one sequence: `rows` prompt tokens (positions pos[0..rows)) into
+// cache row cache_b of a [B][Hkv][max_ctx][D] (or packed) cache; q out
+// head-grouped [Hkv][G][rows][D], K/V also plain [Hkv][rows][D] (may be null).
+int mivgpu_prefill_qk_norm_rope_kv(const void* qkv, const void* qw, const void* kw, const int* pos,
+                                   void* q_out, void* k_plain, void* v_plain, void* k_cache, void* v_cache,
+                                   int rows, int cache_b, int Hq, int Hkv, int head_dim, int max_ctx, float eps,
+                                   float theta, hipStream_t s) {
+  if (head_dim != 128 || rows <= 0 || cache_b < 0 || Hkv <= 0 || Hq % Hkv) return -1;
+  if (attn_impl()) {
+    if (max_ctx % ATT_KPW) return -1;
+    hipLaunchKernelGGL(qk_norm_rope_kv_kernel<true>, dim3(rows, Hq + 2 * Hkv), dim3(64), 0, s,
+                       (const bf16_t*)qkv, (const bf16_t*)qw, (const bf16_t*)kw, pos, (bf16_t*)q_out,
+                       (bf16_t*)k_cache, (bf16_t*)v_cache, Hq, Hkv, max_ctx, eps, theta, cache_b,
+                       (bf16_t*)k_plain, (bf16_t*)v_plain);
+  } else {
+    hipLaunchKernelGGL(qk_norm_rope_kv_kernel<false>, dim3(rows, Hq + 2 * Hkv), dim3(64), 0, s,
+                       (const bf16_t*)qkv, (const bf16_t*)qw, (const bf16_t*)kw, pos, (bf16_t*)q_out,
+                       (bf16_t*)k_cache, (bf16_t*)v_cache, Hq, Hkv, max_ctx, eps, theta, cache_b,
+                       (bf16_t*)k_plain, (bf16_t*)v_plain);
   }
   return (int)hipGetLastError();
 }

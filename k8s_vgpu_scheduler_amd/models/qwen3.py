@@ -197,6 +197,7 @@ class Qwen3Decoder:
         self.attn_counters = (torch.zeros(batch * cfg.kv_heads, dtype=torch.int32, device=self.device)
                               if self.attn_fused else None)
         self.graph = None
+        self._pf = {}          # prefill bucket length -> static buffers (+ captured graph)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
 
     # ------------------------------------------------------------- setup --
@@ -318,19 +319,26 @@ class Qwen3Decoder:
 
     # ---------------------------------------------------------- prefill --
     # Prompt processing for serving (serve/engine.py): all prompt positions of
-    # one batch row in one pass.  Projections run on the same weights as the
-    # decode step -- the packed skinny kernel in row chunks of <= 128 where the
-    # decoder packed them, hipBLASLt (F.linear) elsewhere; norms on the HIP
-    # kernels; QK-norm/RoPE and the causal attention in fp32 PyTorch (batched
-    # GEMMs); K/V written into the cache in the decode kernels' layout.  A
-    # short chat prompt costs about one decode step (weight streaming).
+    # one batch row in one pass, padded to a bucket length so each bucket runs
+    # as one captured hipGraph (HIP graphs instead of thousands of eager
+    # launches: the prompt of a chat request is latency-bound, not
+    # FLOP-bound).  Per layer: RMSNorm (HIP), qkv (hipBLASLt or the packed
+    # skinny kernel in <= 128-row chunks), QK-norm + RoPE + KV append to the
+    # cache row + head-grouped q (one HIP kernel), causal GQA attention as two
+    # batched fp32 GEMMs over the G*L rows of each KV head with a per-bucket
+    # additive mask, o_proj, add+RMSNorm, gate_up+SiLU, down, add+RMSNorm.
+    # Pad positions >= L write K/V the decode steps overwrite before reading.
     PREFILL_CHUNK = 128
+    PREFILL_BUCKETS = (32, 64, 128, 256, 512, 1024)
 
-    def _rows(self, pl, x):
-        if x.shape[0] <= self.PREFILL_CHUNK:
-            return pl(x.contiguous())
-        return torch.cat([pl(x[s:s + self.PREFILL_CHUNK].contiguous())
-                          for s in range(0, x.shape[0], self.PREFILL_CHUNK)])
+    def _rows(self, pl, x, out=None):
+        M = x.shape[0]
+        if out is None:
+            out = torch.empty(M, pl.out_features, dtype=torch.bfloat16, device=x.device)
+        for s in range(0, M, self.PREFILL_CHUNK):
+            e = min(M, s + self.PREFILL_CHUNK)
+            pl(x[s:e], out=out[s:e])
+        return out
 
     def _proj(self, lw, name, x):
         packed, plain = {"qkv": ("pqkv", "wqkv"), "o": ("po", "wo"), "gu": ("pgu", "wgu"),
@@ -339,9 +347,7 @@ class Qwen3Decoder:
             return self._rows(lw[packed], x)     # gate_up: SiLU*up fused in the epilogue
         y = F.linear(x, lw[plain])
         if name == "gu":
-            if self.native:
-                return ops.silu_mul(y)
-            return ref.silu_mul(y)
+            return ops.silu_mul(y) if self.native else ref.silu_mul(y)
         return y
 
     def _norm(self, x, w):
@@ -352,39 +358,101 @@ class Qwen3Decoder:
             return ops.add_rmsnorm(x, res, w, self.cfg.eps)
         return ref.add_rmsnorm(x, res, w, self.cfg.eps)
 
-    def _write_kv(self, li, b, k, v):
-        """k, v: [L, Hkv, D] fp32 of positions 0..L-1 -> cache row b."""
-        L, Hkv, D = k.shape
-        kc, vc = self.k_cache[li], self.v_cache[li]
-        if not self.kv_native_layout:
-            kc[b, :, :L] = k.transpose(0, 1).to(kc.dtype)
-            vc[b, :, :L] = v.transpose(0, 1).to(vc.dtype)
-            return
-        # the packed layout is per 32-key group: whole groups, zero tail (the
-        # decode kernel writes each later position into its group)
-        Lp = -(-L // 32) * 32
-        for c, t, to_layout in ((kc, k, ops.k_to_cache_layout), (vc, v, ops.v_to_cache_layout)):
-            full = torch.zeros(1, Hkv, Lp, D, dtype=c.dtype, device=c.device)
-            full[0, :, :L] = t.transpose(0, 1).to(c.dtype)
-            c[b:b + 1, :, :Lp // 32] = to_layout(full)
+    def _prefill_qk(self, li, lw, qkv, pos, b):
+        """-> q [Hkv, G*L, D], k / v [Hkv, L, D] (bf16); K/V appended to cache row b."""
+        cfg = self.cfg
+        L, Hq, Hkv, D = qkv.shape[0], cfg.heads, cfg.kv_heads, cfg.head_dim
+        G = Hq // Hkv
+        if self.native:
+            q = torch.empty(Hkv, G * L, D, dtype=torch.bfloat16, device=qkv.device)
+            k = torch.empty(Hkv, L, D, dtype=torch.bfloat16, device=qkv.device)
+            v = torch.empty_like(k)
+            ops.prefill_qk_norm_rope_kv(qkv, lw["q_norm"], lw["k_norm"], pos, q, k, v, self.k_cache[li],
+                                        self.v_cache[li], b, Hq, Hkv, D, cfg.eps, cfg.rope_theta)
+            return q, k, v
+        x = qkv.float().view(L, Hq + 2 * Hkv, D)
 
-    def _causal_attention(self, q, k, v, chunk: int = 1024):
-        """q [L, Hq, D], k/v [L, Hkv, D] fp32 (K/V rounded to the cache dtype,
-        as decode reads them) -> [L, Hq*D] bf16."""
-        L, Hq, D = q.shape
-        G = Hq // k.shape[1]
-        kh = k.to(torch.bfloat16).float().transpose(0, 1).repeat_interleave(G, dim=0)   # [Hq, L, D]
-        vh = v.to(torch.bfloat16).float().transpose(0, 1).repeat_interleave(G, dim=0)
-        qh = q.transpose(0, 1)
-        out = torch.empty(Hq, L, D, dtype=torch.float32, device=q.device)
-        for s in range(0, L, chunk):
-            e = min(L, s + chunk)
-            sc = torch.matmul(qh[:, s:e], kh[:, :e].transpose(1, 2)) * self.scale       # [Hq, e-s, e]
-            qi = torch.arange(s, e, device=q.device)[:, None]
-            kj = torch.arange(e, device=q.device)[None, :]
-            sc.masked_fill_(kj > qi, float("-inf"))
-            out[:, s:e] = torch.matmul(torch.softmax(sc, dim=-1), vh[:, :e])
-        return out.transpose(0, 1).reshape(L, Hq * D).to(torch.bfloat16)
+        def head_norm(t, wn):
+            return t * torch.rsqrt(t.pow(2).mean(-1, keepdim=True) + cfg.eps) * wn.float()
+
+        qf = ref.rope_neox(head_norm(x[:, :Hq], lw["q_norm"]), pos, cfg.rope_theta)
+        kf = ref.rope_neox(head_norm(x[:, Hq:Hq + Hkv], lw["k_norm"]), pos, cfg.rope_theta)
+        k = kf.transpose(0, 1).to(torch.bfloat16)                         # [Hkv, L, D]
+        v = x[:, Hq + Hkv:].transpose(0, 1).to(torch.bfloat16)
+        n = min(L, self.T)
+        self.k_cache[li][b, :, :n] = k[:, :n]
+        self.v_cache[li][b, :, :n] = v[:, :n]
+        q = qf.view(L, Hkv, G, D).permute(1, 2, 0, 3).reshape(Hkv, G * L, D).to(torch.bfloat16)
+        return q, k, v
+
+    def _prefill_attention(self, q, k, v, mask):
+        """Causal GQA attention: q [Hkv, G*L, D], k/v [Hkv, L, D] -> [L, Hq*D] bf16."""
+        Hkv, GL, D = q.shape
+        L = k.shape[1]
+        sc = torch.baddbmm(mask.expand(Hkv, GL, L), q.float(), k.float().transpose(1, 2), alpha=self.scale)
+        o = torch.bmm(torch.softmax(sc, dim=-1), v.float())                # [Hkv, G*L, D]
+        return o.view(Hkv, GL // L, L, D).permute(2, 0, 1, 3).reshape(L, Hkv * (GL // L) * D).to(torch.bfloat16)
+
+    def _prefill_bufs(self, Lb: int) -> dict:
+        bufs = self._pf.get(Lb)
+        if bufs is None:
+            G = self.cfg.heads // self.cfg.kv_heads
+            i = torch.arange(Lb, device=self.device)
+            causal = torch.zeros(Lb, Lb, device=self.device).masked_fill_(i[None, :] > i[:, None], float("-inf"))
+            bufs = dict(ids=torch.zeros(Lb, dtype=torch.long, device=self.device),
+                        pos=i.to(torch.int32), mask=causal.repeat(G, 1),
+                        last=torch.zeros(1, dtype=torch.long, device=self.device),
+                        plen=torch.zeros(1, dtype=torch.int32, device=self.device), graph=None)
+            self._pf[Lb] = bufs
+        return bufs
+
+    def _prefill_impl(self, bufs: dict, b: int):
+        cfg, w = self.cfg, self.w
+        res = torch.index_select(w.embed, 0, bufs["ids"])
+        h = self._norm(res, w.layers[0]["ln1"])
+        for li, lw in enumerate(w.layers):
+            q, k, v = self._prefill_qk(li, lw, self._proj(lw, "qkv", h), bufs["pos"], b)
+            o = self._proj(lw, "o", self._prefill_attention(q, k, v, bufs["mask"]))
+            h = self._add_norm(o, res, lw["ln2"])
+            d = self._proj(lw, "d", self._proj(lw, "gu", h))
+            nxt = w.layers[li + 1]["ln1"] if li + 1 < len(w.layers) else w.final_norm
+            h = self._add_norm(d, res, nxt)
+        last = torch.index_select(h, 0, bufs["last"])
+        logits = self._rows(self.p_lm, last) if self.skinny else F.linear(last, w.lm_head)
+        # in-place kernels only (no copy nodes in a captured graph)
+        torch.argmax(logits, dim=-1, out=self.tokens[b:b + 1])
+        torch.add(bufs["plen"], 0, out=self.pos[b:b + 1])
+        torch.add(bufs["plen"], 1, out=self.seqlens[b:b + 1])
+        return logits
+
+    def _bucket(self, L: int) -> int | None:
+        for Lb in self.PREFILL_BUCKETS:
+            if L <= Lb <= self.T:
+                return Lb
+        return None
+
+    @torch.no_grad()
+    def capture_prefill(self, buckets=None, b: int = 0):
+        """Capture the prefill of row ``b`` for each bucket length (<= T)."""
+        assert self.device.type == "cuda"
+        if self.norm_fused:
+            raise NotImplementedError("prefill with MIVGPU_NORM_FUSED=1")
+        for Lb in (buckets or self.PREFILL_BUCKETS):
+            if Lb > self.T:
+                continue
+            bufs = self._prefill_bufs(Lb)
+            bufs["plen"].fill_(1)
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self._prefill_impl(bufs, b)                     # warm: library plans, allocator
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                bufs["logits"] = self._prefill_impl(bufs, b)
+            bufs["graph"] = g
+        torch.cuda.synchronize()
 
     @torch.no_grad()
     def prefill(self, prompt, b: int = 0) -> torch.Tensor:
@@ -393,36 +461,20 @@ class Qwen3Decoder:
         position to L, and return the last position's logits [vocab]."""
         if self.norm_fused:
             raise NotImplementedError("prefill with MIVGPU_NORM_FUSED=1 (norm weights folded into the packed columns)")
-        cfg, w = self.cfg, self.w
-        ids = torch.as_tensor(prompt, dtype=torch.long, device=self.device).view(-1)
+        ids = torch.as_tensor(prompt, dtype=torch.long).view(-1)
         L = ids.numel()
         if not 0 < L < self.T:
             raise ValueError(f"prompt of {L} tokens does not fit a context of {self.T}")
-        Hq, Hkv, D = cfg.heads, cfg.kv_heads, cfg.head_dim
-        pos = torch.arange(L, device=self.device)
-
-        def head_norm(t, wn):
-            return t * torch.rsqrt(t.pow(2).mean(-1, keepdim=True) + cfg.eps) * wn.float()
-
-        res = F.embedding(ids, w.embed).contiguous()
-        h = self._norm(res, w.layers[0]["ln1"])
-        for li, lw in enumerate(w.layers):
-            qkv = self._proj(lw, "qkv", h).float().view(L, Hq + 2 * Hkv, D)
-            q = ref.rope_neox(head_norm(qkv[:, :Hq], lw["q_norm"]), pos, cfg.rope_theta)
-            k = ref.rope_neox(head_norm(qkv[:, Hq:Hq + Hkv], lw["k_norm"]), pos, cfg.rope_theta)
-            v = qkv[:, Hq + Hkv:]
-            self._write_kv(li, b, k, v)
-            o = self._proj(lw, "o", self._causal_attention(q, k, v))
-            h = self._add_norm(o, res, lw["ln2"])
-            d = self._proj(lw, "d", self._proj(lw, "gu", h))
-            nxt = w.layers[li + 1]["ln1"] if li + 1 < len(w.layers) else w.final_norm
-            h = self._add_norm(d, res, nxt)
-        last = h[L - 1:L].contiguous()
-        logits = (self._rows(self.p_lm, last) if self.skinny else F.linear(last, w.lm_head))[0]
-        self.tokens[b] = torch.argmax(logits)
-        self.pos[b] = L
-        self.seqlens[b] = L + 1
-        return logits
+        Lb = self._bucket(L) if self.device.type == "cuda" else None
+        bufs = self._prefill_bufs(Lb or L)
+        bufs["ids"].zero_()
+        bufs["ids"][:L].copy_(ids.to(self.device, non_blocking=False))
+        bufs["plen"].fill_(L)
+        bufs["last"].fill_(L - 1)
+        if bufs["graph"] is not None:
+            bufs["graph"].replay()
+            return bufs["logits"][0]
+        return self._prefill_impl(bufs, b)[0]
 
     def packed_linears(self) -> list:
         out = [pl for lw in self.w.layers for pl in lw.values() if isinstance(pl, ops.PackedLinear)]

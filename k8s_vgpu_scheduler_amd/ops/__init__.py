@@ -39,6 +39,8 @@ def lib():
         L.mivgpu_rmsnorm.argtypes = [vp, vp, vp, i, i, f, vp]
         L.mivgpu_add_rmsnorm.argtypes = [vp, vp, vp, vp, i, i, f, vp]
         L.mivgpu_qk_norm_rope_kv.argtypes = [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, f, f, vp]
+        L.mivgpu_prefill_qk_norm_rope_kv.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, f, f,
+                                                     vp]
         L.mivgpu_decode_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, f, vp]
         L.mivgpu_decode_attention_fused.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i,
                                                      i, f, f, f, vp]
@@ -59,7 +61,8 @@ def lib():
                    "mivgpu_hwid_probe", "mivgpu_pack_weight", "mivgpu_skinny_gemm",
                    "mivgpu_skinny_max_m", "mivgpu_skinny_plan", "mivgpu_mfma_burn",
                    "mivgpu_stream_copy", "mivgpu_stream_read", "mivgpu_ops_visible_cus",
-                   "mivgpu_ops_kv_packed", "mivgpu_decode_attention_fused", "mivgpu_skinny_gemm_norm"):
+                   "mivgpu_ops_kv_packed", "mivgpu_decode_attention_fused", "mivgpu_skinny_gemm_norm",
+                   "mivgpu_prefill_qk_norm_rope_kv"):
             getattr(L, fn).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -128,6 +131,34 @@ def qk_norm_rope_kv(qkv, q_norm_w, k_norm_w, pos, q_out, k_cache, v_cache, n_q_h
     _check(lib().mivgpu_qk_norm_rope_kv(_p(qkv), _p(q_norm_w), _p(k_norm_w), _p(pos), _p(q_out),
                                         _p(k_cache), _p(v_cache), B, n_q_heads, n_kv_heads, head_dim,
                                         max_ctx, eps, theta, _stream()), "qk_norm_rope_kv")
+
+
+def prefill_qk_norm_rope_kv(qkv, q_norm_w, k_norm_w, pos, q_out, k_plain, v_plain, k_cache, v_cache, cache_b,
+                            n_q_heads, n_kv_heads, head_dim, eps, theta):
+    """Prompt tokens of one sequence (qkv [L, (Hq+2Hkv)*D], positions pos [L]
+    int32) -> QK-norm + RoPE; K/V appended to cache row ``cache_b`` (positions
+    >= the cache length dropped); q_out [Hkv, G*L, D] head-grouped, k_plain /
+    v_plain [Hkv, L, D] (or None)."""
+    L = qkv.shape[0]
+    B = k_cache.shape[0]
+    max_ctx = _check_kv(k_cache, v_cache, B, n_kv_heads, head_dim)
+    if not 0 <= cache_b < B:
+        raise ValueError(f"cache row {cache_b} outside [0, {B})")
+    if qkv.shape[1] != (n_q_heads + 2 * n_kv_heads) * head_dim or not qkv.is_contiguous():
+        raise ValueError(f"qkv shape {tuple(qkv.shape)} does not match the head counts")
+    if pos.dtype != torch.int32 or pos.numel() < L:
+        raise ValueError("pos must be int32 with one position per row")
+    if q_out.numel() < L * n_q_heads * head_dim or not q_out.is_contiguous():
+        raise ValueError("q_out too small")
+    for t in (k_plain, v_plain):
+        if t is not None and (t.numel() < L * n_kv_heads * head_dim or not t.is_contiguous()):
+            raise ValueError("k_plain / v_plain too small")
+    _check(lib().mivgpu_prefill_qk_norm_rope_kv(_p(qkv), _p(q_norm_w), _p(k_norm_w), _p(pos), _p(q_out),
+                                                _p(k_plain) if k_plain is not None else None,
+                                                _p(v_plain) if v_plain is not None else None,
+                                                _p(k_cache), _p(v_cache), L, cache_b, n_q_heads, n_kv_heads,
+                                                head_dim, max_ctx, eps, theta, _stream()),
+           "prefill_qk_norm_rope_kv")
 
 
 def visible_cus() -> int:

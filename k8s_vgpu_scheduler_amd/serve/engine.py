@@ -8,7 +8,8 @@ benchmarks/deployments/job-on-hami.yml).  This engine is the MI355X-native
 stand-in: the Qwen3 decoder of models/qwen3.py (random-init weights of the
 exact architecture; no network for checkpoints) with
 
-  * prefill of the prompt in one pass (``Qwen3Decoder.prefill``),
+  * prefill of the prompt in one pass (``Qwen3Decoder.prefill``), replayed
+    as one captured hipGraph per prompt-length bucket (32 ... 1024 tokens),
   * decode as replays of one captured hipGraph per token (the hand-written
     gfx950 kernels: skinny MFMA GEMMs, fused decode attention, norms),
   * one request at a time (the reference client is sequential), tokens
@@ -77,7 +78,7 @@ class Engine:
     token while the previous one is being written to the client."""
 
     def __init__(self, model: str | Qwen3Config = "qwen3-8b", max_ctx: int = 4096, device: str | None = None,
-                 graph: bool = True, seed: int = 0):
+                 graph: bool = True, seed: int = 0, max_prefill_graph: int = 1024):
         cfg = MODELS[model] if isinstance(model, str) else model
         self.cfg = cfg
         self.model_name = cfg.name
@@ -88,7 +89,7 @@ class Engine:
         self.dec = None
         self.graph = False
         self.load_s = 0.0
-        self._th = threading.Thread(target=self._loop, args=(cfg, max_ctx, device, graph, seed),
+        self._th = threading.Thread(target=self._loop, args=(cfg, max_ctx, device, graph, seed, max_prefill_graph),
                                     name="mivgpu-engine", daemon=True)
         self._th.start()
         self._ready.wait()
@@ -96,23 +97,26 @@ class Engine:
             raise self._err
 
     # ----------------------------------------------------------- engine thread
-    def _build(self, cfg, max_ctx, device, graph, seed):
+    def _build(self, cfg, max_ctx, device, graph, seed, max_prefill_graph):
         t0 = time.perf_counter()
         dev = device or ("cuda" if torch.cuda.is_available() else "cpu")
         self.dec = Qwen3Decoder(cfg, batch=1, max_ctx=max_ctx, device=dev, seed=seed)
         self.graph = graph and self.dec.device.type == "cuda"
         if self.dec.skinny:
             self.dec.reserve_prefill()
-        # warm the prefill path (library GEMM plans, allocator) before capture
-        self.dec.prefill(self.tok.encode("warm up " * 20))
         if self.graph:
+            # one graph per prompt-length bucket, then the decode step's
+            self.dec.capture_prefill([b for b in self.dec.PREFILL_BUCKETS if b <= max_prefill_graph])
+            self.dec.prefill(self.tok.encode("warm up " * 20))
             self.dec.capture()
+        else:
+            self.dec.prefill(self.tok.encode("warm up " * 20))
         self._sync()
         self.load_s = time.perf_counter() - t0
 
-    def _loop(self, cfg, max_ctx, device, graph, seed):
+    def _loop(self, cfg, max_ctx, device, graph, seed, max_prefill_graph):
         try:
-            self._build(cfg, max_ctx, device, graph, seed)
+            self._build(cfg, max_ctx, device, graph, seed, max_prefill_graph)
         except BaseException as e:  # noqa: BLE001 -- reported to the constructor
             self._err = e
             self._ready.set()

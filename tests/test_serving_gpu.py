@@ -81,6 +81,31 @@ def test_graph_replay_after_prefill_matches_eager_step():
         assert int(d.pos[0]) == L + 8
 
 
+def test_prefill_graph_matches_eager_prefill():
+    """The captured per-bucket prefill graph (padded to 128) against the same
+    prefill run eagerly, and the decode graph continuing from either."""
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_8B
+    ops.require_native()
+    d = Qwen3Decoder(QWEN3_8B, batch=1, max_ctx=4096, device="cuda")
+    d.reserve_prefill()
+    d.capture_prefill([128])
+    d.capture()
+    for L in (92, 17, 128):
+        prompt = list(range(7, 7 + L))
+        lg = d.prefill(prompt).float().clone()
+        tg, pg = int(d.tokens[0]), int(d.pos[0])
+        bufs = d._pf[128]
+        g, bufs["graph"] = bufs["graph"], None
+        le = d.prefill(prompt).float()
+        bufs["graph"] = g
+        torch.cuda.synchronize()
+        cos = torch.nn.functional.cosine_similarity(lg, le, dim=0).item()
+        assert cos > 0.9999 and tg == int(d.tokens[0]) and pg == int(d.pos[0]) == L, (L, cos)
+        d.graph.replay()
+        torch.cuda.synchronize()
+        assert 0 <= int(d.tokens[0]) < QWEN3_8B.vocab and int(d.pos[0]) == L + 1
+
+
 def test_scratch_never_grows_under_a_graph():
     ops.require_native()
     d = Qwen3Decoder(QWEN3_TINY, batch=1, max_ctx=256, device="cuda")
