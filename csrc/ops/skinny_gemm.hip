@@ -946,9 +946,12 @@ int resolve(int M, int K, int N, int epi, int* nt, int* ks, int* S, int variant)
       const char* e = getenv("MIVGPU_SKINNY_WIDE");
       return e && *e ? atoi(e) : -1;
     }();
-    // wide unless forced off; above 64 rows (4 M-tiles) it is not measured
-    // to win (profiles/gemm_wide_plan_full.json), so the classic kernel runs
-    variant = env >= 0 ? (env ? 2 : 1) : (M <= 64 ? 2 : 1);
+    // wide unless forced off.  Prefill row counts (96-128, 4 M-tiles) too
+    // (profiles/round2/gemm_prefill_rows/): at 64 CUs wide vs classic is
+    // gate_up 178 vs 355 us, down 162 vs 226, qkv 60 vs 119, o_proj 59 vs 85;
+    // on the whole chip gate_up 93 vs 126 and down 72 vs 74 (qkv / o_proj,
+    // where classic is ahead, run on hipBLASLt there)
+    variant = env >= 0 ? (env ? 2 : 1) : 2;
   }
   if (variant == 2) {
     int a = *nt, b = *ks, c = *S;
