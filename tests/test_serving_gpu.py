@@ -99,7 +99,8 @@ def test_prefill_graph_matches_eager_prefill():
         cos = torch.nn.functional.cosine_similarity(lg, le, dim=0).item()
         assert cos > 0.998 and pg == int(d.pos[0]) == L, (L, cos)
         top2 = le.topk(2).values
-        if top2[0] - top2[1] > 0.05:             # random weights: near-ties may flip
+        # random weights: near-ties (within a few bf16 ulps of the top logit) may flip
+        if top2[0] - top2[1] > 0.03 * top2[0].abs():
             assert tg == int(d.tokens[0]), L
         d.graph.replay()
         torch.cuda.synchronize()
