@@ -119,7 +119,11 @@ class Qwen3Decoder:
         # 256 CUs, and on o_proj inside a CU partition; qkv stays on hipBLASLt
         # (profiles/gemm_wide_*.json).
         self.skinny_gate_up = skinny
-        self.skinny_o = skinny and ops.visible_cus() <= int(os.environ.get("MIVGPU_SLICE_PLAN_CUS", "96"))
+        # o_proj on the whole chip: the wide kernel up to 8 rows (1 row 10.4 vs
+        # 15.5 us, 8 rows 11.3 vs 15.7), hipBLASLt from 32 (13.3 vs 15.2,
+        # profiles/gemm_wide_plan_full.json) -- batch-1 serving takes the former
+        self.skinny_o = skinny and (ops.visible_cus() <= int(os.environ.get("MIVGPU_SLICE_PLAN_CUS", "96"))
+                                    or batch <= 16)
         # qkv joins them in partitions: hipBLASLt vs wide kernel at 32 CUs
         # 50.7 vs 40.7 us, 64 CUs 27.9 vs 29.6, 128 CUs 20.9 vs 17.5, whole
         # GPU 15.2 vs 17.0 (profiles/cu32/, cu128/, gemm_wide_plan_*.json).
