@@ -12,6 +12,8 @@
 #   kernels     rocprofv3 --kernel-trace --stats of one 64-CU slice decode step
 #   pmc         PMC passes over a 64-CU decode step (one counter group per pass)
 #   membw       partition read ceilings (bench/membw.py)
+#   serving     TTFT / per-token latency, native vs vGPU slices (bench/serving.py)
+#   prefill     prefill microbench + rocprofv3 kernel summary, whole GPU and 64 CUs
 # Results go to gpurun_out/<suite>/ (copy the ones to keep into profiles/).
 set -o pipefail
 suite=${1:-full}; shift || true
@@ -61,5 +63,14 @@ case $suite in
       step 300 "membw8_b$b" python -u -m k8s_vgpu_scheduler_amd.bench.membw --gib 20 --shared-only 8 --shared-bpc "$b" \
         --out "$out/membw8_b$b.json"
     done ;;
+  serving)
+    step 1100 serving python -u -m k8s_vgpu_scheduler_amd.bench.serving --configs "${1:-native,vgpu50,slice25,slice50}" \
+      --warmup 30 --runs 200 --max-tokens 128 --out-dir "$out" ;;
+  prefill)
+    step 120 native python3 -m k8s_vgpu_scheduler_amd.bench.prefill
+    HSA_CU_MASK=0:0-63 step 120 cu64 python3 -m k8s_vgpu_scheduler_amd.bench.prefill
+    cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
+    step 200 prof rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof" -o run -- \
+      python3 -m k8s_vgpu_scheduler_amd.bench.prefill --iters 10 ;;
   *) echo "unknown suite $suite"; exit 2 ;;
 esac
