@@ -57,6 +57,9 @@ def _log(msg):
     print(msg, flush=True)
 
 
+infos: dict = {}     # config -> the server's /health (visible device memory, context length)
+
+
 def run_config(name: str, spec: SliceSpec, a, workdir: Path, log=_log) -> list[dict]:
     env = dict(os.environ)
     env.update(slice_env(spec, None, workdir))
@@ -69,12 +72,16 @@ def run_config(name: str, spec: SliceSpec, a, workdir: Path, log=_log) -> list[d
         cmd += ["--device", a.device]
     if a.no_graph:
         cmd.append("--no-graph")
+    if a.gpu_memory_utilization:
+        cmd += ["--gpu-memory-utilization", str(a.gpu_memory_utilization)]
     logf = open(workdir / f"{name}.server.log", "w")
     proc = subprocess.Popen(cmd, env=env, stdout=logf, stderr=subprocess.STDOUT, start_new_session=True)
     url = f"http://127.0.0.1:{port}/v1/chat/completions"
     try:
         info = client.wait_ready(url, timeout=a.load_timeout, proc=proc)
-        log(f"[serving] {name}: ready in {info.get('load_s')} s, {a.warmup} warmup + {a.runs} runs")
+        log(f"[serving] {name}: ready in {info.get('load_s')} s (device memory {info.get('device_mem_total_mib')} MiB, "
+            f"max_model_len {info.get('max_model_len')}), {a.warmup} warmup + {a.runs} runs")
+        infos[name] = info
         rows = client.run(url, a.runs, a.warmup, a.prompt, a.max_tokens, str(workdir / f"{name}.jsonl"),
                           timeout=a.request_timeout, log=lambda m: log(f"[serving] {name}:{m}"))
     finally:
@@ -104,6 +111,7 @@ def main(argv=None):
     ap.add_argument("--prompt", default=client.DEFAULT_PROMPT)
     ap.add_argument("--device", default=None)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--gpu-memory-utilization", type=float, default=None)
     ap.add_argument("--load-timeout", type=float, default=600.0)
     ap.add_argument("--request-timeout", type=float, default=60.0)
     ap.add_argument("--out-dir", default=None)
@@ -123,6 +131,10 @@ def main(argv=None):
                           "per_token_clean_mean_ms": round(s["per_token_clean_mean_s"] * 1e3, 4),
                           "decode_tok_s": round(s["decode_tok_s"], 1)}), flush=True)
     summary = report.write_report(results, workdir)
+    for n, info in infos.items():
+        if n in summary:
+            summary[n]["device_mem_total_mib"] = info.get("device_mem_total_mib")
+            summary[n]["max_model_len"] = info.get("max_model_len")
     line = {"metric": "serving TTFT / per-token latency, vGPU slices vs native", "model": a.model,
             "runs": a.runs, "warmup": a.warmup, "max_tokens": a.max_tokens, "data": "synthetic prompt, random-init "
             "weights", "wall_s": round(time.time() - t0, 1), "configs": summary, "out_dir": str(workdir)}

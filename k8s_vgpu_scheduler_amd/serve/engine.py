@@ -78,7 +78,8 @@ class Engine:
     token while the previous one is being written to the client."""
 
     def __init__(self, model: str | Qwen3Config = "qwen3-8b", max_ctx: int = 4096, device: str | None = None,
-                 graph: bool = True, seed: int = 0, max_prefill_graph: int = 1024):
+                 graph: bool = True, seed: int = 0, max_prefill_graph: int = 1024,
+                 gpu_memory_utilization: float | None = None):
         cfg = MODELS[model] if isinstance(model, str) else model
         self.cfg = cfg
         self.model_name = cfg.name
@@ -89,6 +90,8 @@ class Engine:
         self.dec = None
         self.graph = False
         self.load_s = 0.0
+        self.mem_total_mib = None
+        self.gpu_memory_utilization = gpu_memory_utilization
         self._th = threading.Thread(target=self._loop, args=(cfg, max_ctx, device, graph, seed, max_prefill_graph),
                                     name="mivgpu-engine", daemon=True)
         self._th.start()
@@ -97,9 +100,31 @@ class Engine:
             raise self._err
 
     # ----------------------------------------------------------- engine thread
+    @staticmethod
+    def kv_bytes_per_token(cfg: Qwen3Config) -> int:
+        return cfg.layers * 2 * cfg.kv_heads * cfg.head_dim * 2          # K and V, bf16
+
+    def size_context(self, cfg, max_ctx, util):
+        """vLLM-style --gpu-memory-utilization: the context (KV tokens) that
+        fits in ``util`` of the device memory the process sees -- inside a
+        slice that is the grant (libmivgpu.so virtualises hipMemGetInfo), not
+        the card -- after the weights and a working margin."""
+        free, total = torch.cuda.mem_get_info()
+        self.mem_total_mib = total >> 20
+        budget = int(total * util) - (total - free) - cfg.param_count() * 2 - (2 << 30)
+        fit = max(0, budget) // self.kv_bytes_per_token(cfg) // 32 * 32
+        if fit < 64:
+            raise RuntimeError(f"{total >> 20} MiB visible: no room for a KV cache after the weights")
+        return min(max_ctx, fit)
+
     def _build(self, cfg, max_ctx, device, graph, seed, max_prefill_graph):
         t0 = time.perf_counter()
         dev = device or ("cuda" if torch.cuda.is_available() else "cpu")
+        if dev != "cpu":
+            free, total = torch.cuda.mem_get_info()
+            self.mem_total_mib = total >> 20
+            if self.gpu_memory_utilization:
+                max_ctx = self.size_context(cfg, max_ctx, self.gpu_memory_utilization)
         self.dec = Qwen3Decoder(cfg, batch=1, max_ctx=max_ctx, device=dev, seed=seed)
         self.graph = graph and self.dec.device.type == "cuda"
         if self.dec.skinny:

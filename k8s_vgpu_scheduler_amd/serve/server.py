@@ -9,7 +9,8 @@ the reference's benchmark pod, benchmarks/ai-benchmark/Dockerfile).
 Streaming responses are server-sent events, one ``data: {chunk}`` line per
 generated token, a final chunk carrying ``finish_reason`` and ``usage``, then
 ``data: [DONE]``; the connection closes after each response.  Requests are
-served one at a time on the GPU (the engine's lock); further clients wait.
+served one at a time, in arrival order, by the engine thread that owns the
+GPU; further clients wait.
 
     python -m k8s_vgpu_scheduler_amd.serve.server --model qwen3-8b --port 8000
 """
@@ -47,7 +48,8 @@ class Handler(BaseHTTPRequestHandler):
     def do_GET(self):
         if self.path == "/health":
             return self._json(200, {"status": "ok", "model": self.engine.model_name,
-                                    "load_s": round(self.engine.load_s, 2)})
+                                    "load_s": round(self.engine.load_s, 2), "max_model_len": self.engine.max_ctx,
+                                    "device_mem_total_mib": self.engine.mem_total_mib})
         if self.path == "/v1/models":
             return self._json(200, {"object": "list", "data": [{"id": self.engine.model_name, "object": "model",
                                                                  "max_model_len": self.engine.max_ctx}]})
@@ -129,11 +131,16 @@ def main(argv=None):
     ap.add_argument("--max-tokens", type=int, default=128, help="default completion length")
     ap.add_argument("--no-graph", action="store_true", help="eager decode steps instead of hipGraph replays")
     ap.add_argument("--device", default=None)
+    ap.add_argument("--gpu-memory-utilization", type=float, default=None,
+                    help="size max_model_len to this fraction of the device memory the process sees "
+                         "(the slice's grant under libmivgpu.so), capped by --max-model-len")
     a = ap.parse_args(argv)
-    eng = Engine(a.model, max_ctx=a.max_model_len, device=a.device, graph=not a.no_graph)
+    eng = Engine(a.model, max_ctx=a.max_model_len, device=a.device, graph=not a.no_graph,
+                 gpu_memory_utilization=a.gpu_memory_utilization)
     srv = make_server(eng, a.host, a.port, a.max_tokens)
     print(json.dumps({"serving": eng.model_name, "url": f"http://{a.host}:{srv.server_address[1]}",
-                      "load_s": round(eng.load_s, 2), "graph": eng.graph}), flush=True)
+                      "load_s": round(eng.load_s, 2), "graph": eng.graph, "max_model_len": eng.max_ctx,
+                      "device_mem_total_mib": eng.mem_total_mib}), flush=True)
     try:
         srv.serve_forever(poll_interval=0.2)
     except KeyboardInterrupt:

@@ -127,7 +127,7 @@ def test_serving_native_vs_slice(tmp_path):
     if os.environ.get("GRAFT_REPO_ROOT"):
         tmp_path = Path(os.environ["GRAFT_REPO_ROOT"]) / "gpurun_out" / "serving_test"
     rc = serving.main(["--configs", "native,slice25", "--warmup", "3", "--runs", "12", "--max-tokens", "32",
-                       "--out-dir", str(tmp_path)])
+                       "--gpu-memory-utilization", "0.6", "--max-model-len", "65536", "--out-dir", str(tmp_path)])
     assert rc == 0
     out = json.loads((tmp_path / "serving.json").read_text())["configs"]
     nat, sl = out["native"], out["slice25"]
@@ -139,3 +139,7 @@ def test_serving_native_vs_slice(tmp_path):
     assert nat["per_token_clean_mean_s"] < sl["per_token_clean_mean_s"] < 4 * nat["per_token_clean_mean_s"], out
     assert nat["ttft_p50_s"] < 0.1 and sl["ttft_p50_s"] < 0.2, out
     assert (tmp_path / "slice2.cache").exists()           # the slice server ran under the shim
+    # the server sizes its KV cache from the memory it sees: the 36 GiB grant
+    # inside the slice (virtualised hipMemGetInfo), the card natively
+    assert sl["device_mem_total_mib"] == 36864 and nat["device_mem_total_mib"] > 280_000, out
+    assert nat["max_model_len"] == 65536 and 4096 < sl["max_model_len"] < 32768, out
