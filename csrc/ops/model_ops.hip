@@ -600,9 +600,10 @@ decode_attn_mfma_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__
 //     published with write-through (sc1) stores; after every storing wave's
 //     vmcnt(0) and a workgroup barrier, one lane bumps the (b, kv-head)
 //     arrival counter (agent-scope atomic); the workgroup whose add returns
-//     nsplit-1 is the last one: it resets the counter and merges all splits
-//     with sc1 loads (MI355X_MICROARCH.md, "Hand-offs measured with sc1
-//     loads", row 1).  Every workgroup arrives, empty splits included.
+//     active-1 is the last one: it resets the counter and merges the active
+//     splits with sc1 loads (MI355X_MICROARCH.md, "Hand-offs measured with sc1
+//     loads", row 1).  Only splits holding keys arrive (active = ceil(L /
+//     SPLIT), the same in every workgroup of the row); empty ones leave.
 // The qkv/weight loads are issued before the K/V loads so the prep math does
 // not wait behind the 16 KB of K/V (vmcnt retires in order).
 template <int G, int WAVES, bool NT, bool COMBINE>
@@ -630,6 +631,10 @@ decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restric
   const int p = pos[b];
   const int j0 = split * SPLIT;
   const int n = min(SPLIT, L - j0);
+  // splits holding keys: only these take part in the combine (a long cache
+  // with a short sequence -- serving -- launches mostly empty splits; they
+  // leave at once instead of arriving on the counter)
+  const int active = L > 0 ? min(nsplit, (L + SPLIT - 1) / SPLIT) : 1;
   const size_t part_base = ((size_t)b * Hq + (size_t)hk * G);
   __shared__ float s_o[WAVES][G][DP];
   __shared__ float s_m[WAVES][G];
@@ -823,7 +828,7 @@ decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restric
         }
       }
     }
-  } else if (t < G) {   // empty split: neutral partial
+  } else if (t < G && (!COMBINE || split < active)) {   // empty split: neutral partial
     float* mp = &ml_part[((part_base + t) * nsplit + split) * 2];
     if constexpr (COMBINE) {
       __hip_atomic_store(mp, -INFINITY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -834,6 +839,7 @@ decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restric
     }
   }
   if constexpr (!COMBINE) return;
+  if (split >= active) return;     // uniform per workgroup: no barrier below is split
 
   // ---- arrival: every storing wave drained, then one add per workgroup
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -841,7 +847,7 @@ decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restric
   int* cnt = counters + (size_t)b * Hkv + hk;
   if (t == 0) {
     const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old == nsplit - 1;
+    s_last = old == active - 1;
   }
   __syncthreads();
   if (!s_last) return;
@@ -854,18 +860,18 @@ decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restric
     const int g = idx / D, d = idx % D;
     const size_t base = part_base + g;
     float M = -INFINITY, num = 0.f, den = 0.f;
-    for (int s0 = 0; s0 < nsplit; s0 += MS) {
+    for (int s0 = 0; s0 < active; s0 += MS) {
       float mv[MS], lv[MS], ov[MS];
 #pragma unroll
       for (int i = 0; i < MS; ++i) {
-        const int sp = s0 + i < nsplit ? s0 + i : s0;
+        const int sp = s0 + i < active ? s0 + i : s0;
         mv[i] = __hip_atomic_load(&ml_part[(base * nsplit + sp) * 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         lv[i] = __hip_atomic_load(&ml_part[(base * nsplit + sp) * 2 + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ov[i] = __hip_atomic_load(&o_part[(base * nsplit + sp) * D + d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
 #pragma unroll
       for (int i = 0; i < MS; ++i) {
-        if (s0 + i >= nsplit || mv[i] == -INFINITY) continue;
+        if (s0 + i >= active || mv[i] == -INFINITY) continue;
         const float nm = fmaxf(M, mv[i]);
         const float a = M == -INFINITY ? 0.f : __expf(M - nm), w = __expf(mv[i] - nm);
         num = num * a + w * ov[i];
