@@ -828,7 +828,7 @@ decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restric
         }
       }
     }
-  } else if (t < G && (!COMBINE || split < active)) {   // empty split: neutral partial
+  } else if (t < G && split < active) {   // empty split below the combine's count: neutral partial
     float* mp = &ml_part[((part_base + t) * nsplit + split) * 2];
     if constexpr (COMBINE) {
       __hip_atomic_store(mp, -INFINITY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -886,13 +886,20 @@ decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restric
 // grid = (Hq, B), 128 threads (one per output dim).
 __global__ void __launch_bounds__(128)
 decode_attn_combine_kernel(const float* __restrict__ o_part, const float* __restrict__ ml_part,
-                           bf16_t* __restrict__ out, int Hq, int nsplit, int count) {
-  // nsplit = workspace stride, count = splits actually written (<= nsplit)
+                           bf16_t* __restrict__ out, int Hq, int nsplit, int count,
+                           const int* __restrict__ seqlens, int split_keys, int max_ctx) {
+  // nsplit = workspace stride, count = splits written (<= nsplit); with
+  // seqlens, only the splits holding keys of row b are merged (a cache sized
+  // for a long context with a short sequence: most partials are empty)
   // Loads batched 8 splits at a time (one memory round trip per batch) with
   // an online merge; a max pass followed by a weighted pass costs a dependent
   // round trip per split.
   const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
   const size_t base = (size_t)b * Hq + h;
+  if (seqlens) {
+    const int L = min(seqlens[b], max_ctx);
+    count = min(count, L > 0 ? (L + split_keys - 1) / split_keys : 0);
+  }
   constexpr int MS = 8;
   float M = -INFINITY, num = 0.f, den = 0.f;
   for (int s0 = 0; s0 < count; s0 += MS) {
@@ -1080,7 +1087,8 @@ int mivgpu_decode_attention(const void* q, const void* k_cache, const void* v_ca
 #undef MIVGPU_ATTN_MFMA_G
 #undef MIVGPU_ATTN_MFMA
     hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(Hq, B), dim3(ATT_D), 0, s,
-                       (const float*)o_part, (const float*)ml_part, (bf16_t*)out, Hq, nsplit, nsplit);
+                       (const float*)o_part, (const float*)ml_part, (bf16_t*)out, Hq, nsplit, nsplit, seqlens,
+                       waves * ATT_KPW, max_ctx);
     return (int)hipGetLastError();
   }
   // Load scheduling variant (see the kernel); MIVGPU_ATTN_PF overrides for experiments.
@@ -1117,7 +1125,8 @@ int mivgpu_decode_attention(const void* q, const void* k_cache, const void* v_ca
 #undef MIVGPU_ATTN_G
 #undef MIVGPU_ATTN_LAUNCH
   hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(Hq, B), dim3(ATT_D), 0, s,
-                     (const float*)o_part, (const float*)ml_part, (bf16_t*)out, Hq, nsplit, nsplit);
+                     (const float*)o_part, (const float*)ml_part, (bf16_t*)out, Hq, nsplit, nsplit, seqlens,
+                     ATT_SPLIT, max_ctx);
   return (int)hipGetLastError();
 }
 
@@ -1177,7 +1186,8 @@ int mivgpu_decode_attention_fused(const void* qkv, const void* q_norm_w, const v
 #undef MIVGPU_ATTN_FUSED2
   if (!comb)
     hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(Hq, B), dim3(ATT_D), 0, s, (const float*)o_part,
-                       (const float*)ml_part, (bf16_t*)out, Hq, nsplit, nsplit);
+                       (const float*)ml_part, (bf16_t*)out, Hq, nsplit, nsplit, seqlens, waves * ATT_KPW,
+                       max_ctx);
   return (int)hipGetLastError();
 }
 
