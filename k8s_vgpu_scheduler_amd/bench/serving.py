@@ -135,6 +135,7 @@ def main(argv=None):
         if n in summary:
             summary[n]["device_mem_total_mib"] = info.get("device_mem_total_mib")
             summary[n]["max_model_len"] = info.get("max_model_len")
+    (workdir / "summary.json").write_text(json.dumps(summary, indent=1))
     line = {"metric": "serving TTFT / per-token latency, vGPU slices vs native", "model": a.model,
             "runs": a.runs, "warmup": a.warmup, "max_tokens": a.max_tokens, "data": "synthetic prompt, random-init "
             "weights", "wall_s": round(time.time() - t0, 1), "configs": summary, "out_dir": str(workdir)}
