@@ -18,6 +18,10 @@ Configurations:
   slice25   shim, gpucores 25: 64-CU balanced mask + 2 HW queues, gpumem 36 GiB
   slice50   shim, gpucores 50: 128-CU mask, gpumem 72 GiB
   temporal25 shim, gpucores 25 time-sliced by the governor (no mask, policy force)
+A ``+K`` suffix (``slice25+3``, ``native+3``) runs K busy Qwen3-8B decode
+tenants (batch 32) next to the server for that configuration: in the other CU
+partitions of a 4-way split for slice configs (shim, 36 GiB grants, as pods),
+unpartitioned without the vGPU layer otherwise (a plain time-shared GPU).
 """
 
 from __future__ import annotations
@@ -33,7 +37,7 @@ import tempfile
 import time
 from pathlib import Path
 
-from k8s_vgpu_scheduler_amd.bench.slices import SliceSpec, slice_env
+from k8s_vgpu_scheduler_amd.bench.slices import SliceProc, SliceSpec, plan_slices, slice_env
 from k8s_vgpu_scheduler_amd.serve import client, report
 
 CARD_MIB = 288 * 1024     # MI355X HBM3E
@@ -45,6 +49,11 @@ CONFIGS = {
     "slice50": SliceSpec(index=3, gpumem_mib=73728, cu_ranges=[(0, 127)], core_pct=50, hw_queues=2),
     "temporal25": SliceSpec(index=4, gpumem_mib=36864, cu_ranges=None, core_pct=25, policy="force"),
 }
+
+
+def _nb_ok(name: str) -> bool:
+    _, _, nb = name.partition("+")
+    return not nb or (nb.isdigit() and int(nb) <= 3)
 
 
 def free_port() -> int:
@@ -60,7 +69,66 @@ def _log(msg):
 infos: dict = {}     # config -> the server's /health (visible device memory, context length)
 
 
+def neighbour_specs(spec: SliceSpec, k: int) -> list[SliceSpec]:
+    """k busy tenants next to the server: in the other CU partitions of a
+    4-way split when the server has one (each with the shim and a 36 GiB
+    grant, as pods), else unpartitioned processes without the shim (plain
+    time-shared GPU, no vGPU layer)."""
+    if spec.cu_ranges:
+        own = spec.cu_ranges[0][0]
+        others = [s for s in plan_slices(4, shim=True, gpumem_mib=36864) if s.cu_ranges[0][0] != own]
+        out = others[:k]
+    else:
+        out = [SliceSpec(index=0, gpumem_mib=None, cu_ranges=None, shim=False) for _ in range(k)]
+    for i, s in enumerate(out):
+        s.index = 20 + i
+    return out
+
+
+def start_neighbours(name, spec, a, workdir: Path, log=_log) -> list:
+    procs = []
+    args = ["--model", a.neighbour_model, "--batch", "32", "--ctx", "1024", "--steps", "64", "--loop"]
+    if a.device == "cpu":
+        args += ["--device", "cpu"]
+    for s in neighbour_specs(spec, a.neighbours):
+        procs.append(SliceProc(s, slice_env(s, None, workdir), args, workdir / f"{name}.neighbour{s.index}.log"))
+    for p in procs:
+        p.send("LOAD")
+    for p in procs:
+        p.expect("READY", a.load_timeout)
+    for p in procs:
+        p.send("GO")
+    log(f"[serving] {name}: {len(procs)} busy neighbours "
+        f"({'CU partitions' if spec.cu_ranges else 'unpartitioned, no shim'})")
+    return procs
+
+
+def stop_neighbours(procs) -> list[dict]:
+    done = []
+    for p in procs:
+        try:
+            p.send("STOP")
+            done.append(p.expect("DONE", 120))
+        except (OSError, RuntimeError, TimeoutError) as e:
+            done.append({"error": str(e)})
+        p.close(timeout=60)
+    return done
+
+
 def run_config(name: str, spec: SliceSpec, a, workdir: Path, log=_log) -> list[dict]:
+    if getattr(a, "neighbours", 0):
+        nb = start_neighbours(name, spec, a, workdir, log)
+        try:
+            return _run_server(name, spec, a, workdir, log)
+        finally:
+            neighbours_done[name] = stop_neighbours(nb)
+    return _run_server(name, spec, a, workdir, log)
+
+
+neighbours_done: dict = {}
+
+
+def _run_server(name: str, spec: SliceSpec, a, workdir: Path, log=_log) -> list[dict]:
     env = dict(os.environ)
     env.update(slice_env(spec, None, workdir))
     env["PYTHONPATH"] = os.pathsep.join(p for p in (str(Path(__file__).resolve().parents[2]),
@@ -112,20 +180,27 @@ def main(argv=None):
     ap.add_argument("--device", default=None)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--gpu-memory-utilization", type=float, default=None)
+    ap.add_argument("--neighbours", type=int, default=0,
+                    help="busy Qwen3 decode tenants next to the server during each configuration: in the other "
+                         "CU partitions for slice configs, unpartitioned (no vGPU layer) otherwise")
+    ap.add_argument("--neighbour-model", default="qwen3-8b")
     ap.add_argument("--load-timeout", type=float, default=600.0)
     ap.add_argument("--request-timeout", type=float, default=60.0)
     ap.add_argument("--out-dir", default=None)
     a = ap.parse_args(argv)
     names = [n.strip() for n in a.configs.split(",") if n.strip()]
-    unknown = [n for n in names if n not in CONFIGS]
+    unknown = [n for n in names if n.split("+")[0] not in CONFIGS or not _nb_ok(n)]
     if unknown:
         ap.error(f"unknown configs {unknown}; choose from {sorted(CONFIGS)}")
+    default_nb = a.neighbours
     workdir = Path(a.out_dir or tempfile.mkdtemp(prefix="mivgpu-serving-"))
     workdir.mkdir(parents=True, exist_ok=True)
     results = {}
     t0 = time.time()
     for n in names:
-        results[n] = run_config(n, CONFIGS[n], a, workdir)
+        base, _, nb = n.partition("+")
+        a.neighbours = int(nb) if nb else default_nb
+        results[n] = run_config(n, CONFIGS[base], a, workdir)
         s = report.summarize(results[n])
         print(json.dumps({"config": n, "ttft_p50_ms": round(s["ttft_p50_s"] * 1e3, 3),
                           "per_token_clean_mean_ms": round(s["per_token_clean_mean_s"] * 1e3, 4),
@@ -135,8 +210,12 @@ def main(argv=None):
         if n in summary:
             summary[n]["device_mem_total_mib"] = info.get("device_mem_total_mib")
             summary[n]["max_model_len"] = info.get("max_model_len")
+    for n, d in neighbours_done.items():
+        if n in summary:
+            summary[n]["neighbours"] = d
     (workdir / "summary.json").write_text(json.dumps(summary, indent=1))
     line = {"metric": "serving TTFT / per-token latency, vGPU slices vs native", "model": a.model,
+            "neighbours_default": default_nb,
             "runs": a.runs, "warmup": a.warmup, "max_tokens": a.max_tokens, "data": "synthetic prompt, random-init "
             "weights", "wall_s": round(time.time() - t0, 1), "configs": summary, "out_dir": str(workdir)}
     (workdir / "serving.json").write_text(json.dumps(line, indent=1))

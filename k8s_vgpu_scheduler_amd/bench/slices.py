@@ -208,6 +208,9 @@ def child_main(argv):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = harness rehearsal (fp32 reference path, no GPU)")
+    ap.add_argument("--loop", action="store_true",
+                    help="after GO, decode until STOP arrives on stdin (a noisy neighbour for the serving "
+                         "bench); the context position wraps every --steps steps")
     a = ap.parse_args(argv)
     cmd = sys.stdin.readline().strip()
     if cmd != "LOAD":
@@ -245,6 +248,8 @@ def child_main(argv):
     print("READY " + json.dumps(ready), flush=True)
     if sys.stdin.readline().strip() != "GO":
         return 0
+    if a.loop:
+        return _loop_until_stop(a, dec, torch.cuda.synchronize)
     # per-step completion events: time per output token (TPOT) of this slice
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
     torch.cuda.synchronize()
@@ -305,6 +310,8 @@ def _child_cpu(a, cfg, Qwen3Decoder):
                                  "cu_mask": os.environ.get("HSA_CU_MASK", "")}), flush=True)
     if sys.stdin.readline().strip() != "GO":
         return 0
+    if a.loop:
+        return _loop_until_stop(a, dec, lambda: None)
     t_start = time.time()
     t0 = time.perf_counter()
     tpot = []
@@ -317,6 +324,28 @@ def _child_cpu(a, cfg, Qwen3Decoder):
     print("DONE " + json.dumps({"seconds": dt, "tokens": a.batch * a.steps, "tok_s": a.batch * a.steps / dt,
                                 "t_start": t_start, "t_end": t_start + dt, "tpot_ms_p50": tpot[len(tpot) // 2],
                                 "tpot_ms_p99": tpot[min(len(tpot) - 1, int(0.99 * len(tpot)))]}), flush=True)
+    return 0
+
+
+def _loop_until_stop(a, dec, sync) -> int:
+    """Decode rounds of a.steps steps (position rewound to the context each
+    round, so the cache never grows) until STOP arrives; DONE carries the
+    tokens/s over the whole loop."""
+    import select as _select
+    t0, steps = time.perf_counter(), 0
+    while True:
+        dec.pos.fill_(a.ctx)
+        dec.seqlens.fill_(a.ctx + 1)
+        for _ in range(a.steps):
+            dec.step()
+        steps += a.steps
+        sync()
+        r, _, _ = _select.select([sys.stdin], [], [], 0)
+        if r and sys.stdin.readline().strip() in ("STOP", ""):
+            break
+    dt = time.perf_counter() - t0
+    print("DONE " + json.dumps({"seconds": dt, "tokens": a.batch * steps, "tok_s": a.batch * steps / dt,
+                                "loop": True}), flush=True)
     return 0
 
 

@@ -145,3 +145,26 @@ def test_serving_orchestrator_cpu(tmp_path):
     out = json.loads((tmp_path / "serving.json").read_text())
     assert out["configs"]["native"]["requests"] == 3 and out["configs"]["native"]["tokens_per_request"] == 4.0
     assert (tmp_path / "report.md").exists() and (tmp_path / "native.jsonl").exists()
+
+
+def test_serving_orchestrator_with_neighbours_cpu(tmp_path):
+    """``native+1``: one busy neighbour (the bench/slices child in --loop
+    mode) runs while the server is measured, then stops and reports."""
+    from k8s_vgpu_scheduler_amd.bench import serving
+    rc = serving.main(["--configs", "native+1", "--model", "qwen3-tiny", "--device", "cpu", "--warmup", "1",
+                       "--runs", "2", "--max-tokens", "3", "--max-model-len", "256", "--neighbour-model",
+                       "qwen3-tiny", "--out-dir", str(tmp_path)])
+    assert rc == 0
+    out = json.loads((tmp_path / "serving.json").read_text())["configs"]["native+1"]
+    assert out["requests"] == 2
+    nb = out["neighbours"]
+    assert len(nb) == 1 and nb[0].get("loop") is True and nb[0]["tokens"] > 0, nb
+
+
+def test_neighbour_layouts():
+    from k8s_vgpu_scheduler_amd.bench import serving
+    sl = serving.neighbour_specs(serving.CONFIGS["slice25"], 3)
+    assert [s.cu_ranges for s in sl] == [[(64, 127)], [(128, 191)], [(192, 255)]]
+    assert all(s.shim and s.gpumem_mib == 36864 for s in sl)
+    nat = serving.neighbour_specs(serving.CONFIGS["native"], 2)
+    assert all(s.cu_ranges is None and not s.shim for s in nat)
