@@ -21,7 +21,8 @@ Configurations:
 A ``+K`` suffix (``slice25+3``, ``native+3``) runs K busy Qwen3-8B decode
 tenants (batch 32) next to the server for that configuration: in the other CU
 partitions of a 4-way split for slice configs (shim, 36 GiB grants, as pods),
-unpartitioned without the vGPU layer otherwise (a plain time-shared GPU).
+governed at the same limit for the temporal config, unpartitioned without the
+vGPU layer otherwise (a plain time-shared GPU).
 """
 
 from __future__ import annotations
@@ -78,6 +79,10 @@ def neighbour_specs(spec: SliceSpec, k: int) -> list[SliceSpec]:
         own = spec.cu_ranges[0][0]
         others = [s for s in plan_slices(4, shim=True, gpumem_mib=36864) if s.cu_ranges[0][0] != own]
         out = others[:k]
+    elif spec.shim and spec.core_pct < 100:
+        # a time-sliced server: the neighbours are governed the same way
+        out = [SliceSpec(index=0, gpumem_mib=36864, cu_ranges=None, core_pct=spec.core_pct, policy=spec.policy,
+                         hw_queues=spec.hw_queues) for _ in range(k)]
     else:
         out = [SliceSpec(index=0, gpumem_mib=None, cu_ranges=None, shim=False) for _ in range(k)]
     for i, s in enumerate(out):
@@ -98,8 +103,9 @@ def start_neighbours(name, spec, a, workdir: Path, log=_log) -> list:
         p.expect("READY", a.load_timeout)
     for p in procs:
         p.send("GO")
-    log(f"[serving] {name}: {len(procs)} busy neighbours "
-        f"({'CU partitions' if spec.cu_ranges else 'unpartitioned, no shim'})")
+    kind = ("CU partitions" if spec.cu_ranges else
+            f"governed at {spec.core_pct} %" if spec.shim and spec.core_pct < 100 else "unpartitioned, no shim")
+    log(f"[serving] {name}: {len(procs)} busy neighbours ({kind})")
     return procs
 
 

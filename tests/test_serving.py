@@ -168,3 +168,5 @@ def test_neighbour_layouts():
     assert all(s.shim and s.gpumem_mib == 36864 for s in sl)
     nat = serving.neighbour_specs(serving.CONFIGS["native"], 2)
     assert all(s.cu_ranges is None and not s.shim for s in nat)
+    tmp = serving.neighbour_specs(serving.CONFIGS["temporal25"], 3)
+    assert all(s.shim and s.cu_ranges is None and s.core_pct == 25 and s.policy == "force" for s in tmp)
