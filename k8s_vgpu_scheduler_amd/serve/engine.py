@@ -132,12 +132,15 @@ class Engine:
         if self.graph:
             # one graph per prompt-length bucket, then the decode step's
             self.dec.capture_prefill([b for b in self.dec.PREFILL_BUCKETS if b <= max_prefill_graph])
-            self.dec.prefill(self.tok.encode("warm up " * 20))
+            self.dec.prefill(self._warm_prompt())
             self.dec.capture()
         else:
-            self.dec.prefill(self.tok.encode("warm up " * 20))
+            self.dec.prefill(self._warm_prompt())
         self._sync()
         self.load_s = time.perf_counter() - t0
+
+    def _warm_prompt(self) -> list[int]:
+        return self.tok.encode("warm up " * 20)[:max(1, self.dec.T // 2)]
 
     def _loop(self, cfg, max_ctx, device, graph, seed, max_prefill_graph):
         try:
@@ -185,12 +188,19 @@ class Engine:
         n = max(0, min(max_tokens, self.dec.T - len(prompt_ids) - 1))
         if n == 0:
             return
+        if not self._th.is_alive():
+            raise RuntimeError("the engine thread is gone")
         out: queue.Queue = queue.Queue()
         cancel = threading.Event()
         self._jobs.put((list(prompt_ids), n, out, cancel))
         try:
             while True:
-                x = out.get()
+                try:
+                    x = out.get(timeout=1.0)
+                except queue.Empty:
+                    if not self._th.is_alive():
+                        raise RuntimeError("the engine thread is gone") from None
+                    continue
                 if x is _END:
                     return
                 if isinstance(x, BaseException):

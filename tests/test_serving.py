@@ -170,3 +170,17 @@ def test_neighbour_layouts():
     assert all(s.cu_ranges is None and not s.shim for s in nat)
     tmp = serving.neighbour_specs(serving.CONFIGS["temporal25"], 3)
     assert all(s.shim and s.cu_ranges is None and s.core_pct == 25 and s.policy == "force" for s in tmp)
+
+
+def test_engine_reports_a_failed_request_and_keeps_serving():
+    """A job that raises on the engine thread (here: a prompt id outside the
+    vocabulary) reaches its request as an exception; the next request works."""
+    eng = Engine("qwen3-tiny", max_ctx=128, device="cpu")
+    try:
+        with pytest.raises(Exception):
+            list(eng.stream([10 ** 9], 3))
+        assert len(eng.generate(eng.tok.encode("ok"), 3).tokens) == 3
+    finally:
+        eng.close()
+    with pytest.raises(RuntimeError, match="engine thread"):
+        list(eng.stream([5, 6], 2))
