@@ -148,7 +148,10 @@ class Qwen3Decoder:
                     lw["pgu"] = ops.PackedLinear(lw.pop("wgu"), silu_mul=True, col_scale=lw["ln2"])
                 else:
                     if self.skinny_gate_up:
-                        lw["pgu"] = ops.PackedLinear(lw.pop("wgu"), silu_mul=True)
+                        # batch-1 serving on the whole chip: the plain copy too, for
+                        # prompts (hipBLASLt + SiLU 58 vs wide 93 us at 128 rows; +201 MB/layer)
+                        keep_gu = batch <= 16 and ops.visible_cus() > int(os.environ.get("MIVGPU_SLICE_PLAN_CUS", "96"))
+                        lw["pgu"] = ops.PackedLinear(lw["wgu"] if keep_gu else lw.pop("wgu"), silu_mul=True)
                     if self.skinny_qkv:
                         lw["pqkv"] = ops.PackedLinear(lw.pop("wqkv"))
                 if self.skinny_o:
