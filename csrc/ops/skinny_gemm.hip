@@ -908,6 +908,21 @@ bool plan_wide(int M, int K, int N, int epi, int* nt, int* wv, int* S) {
   const int vgroups = ntiles / *nt;
   const bool auto_s = *S <= 0;
   if (auto_s) *S = (!slice && vgroups <= 128) ? 4 : 1;
+  if (M > 64) {
+    // Prompt rows (serving prefill chunks of up to 128), swept by
+    // scripts/probe/wide_m128_sweep.py (profiles/round2/gemm_prefill_rows/):
+    //  * gate_up + SiLU: 2 waves, no split -- 64 CUs 158 vs 177 us at 128
+    //    rows, 256 CUs 77.5 vs 91.5;
+    //  * stores split K: inside a partition S = 2 for N <= 4096 (down 105 vs
+    //    162 us, o_proj 54 vs 59), on the chip S = 4 up to 192 wave-groups
+    //    (qkv 49.9 vs 59.2; down / o_proj already split 4).
+    if (auto_s) {
+      if (epi == EPI_SILU_MUL) *S = 1;
+      else if (slice) *S = ntiles <= 128 ? 2 : 1;
+      else *S = vgroups <= 192 ? 4 : 1;
+    }
+    if (*wv <= 0) *wv = epi == EPI_SILU_MUL ? 2 : 4;
+  }
   if (*wv <= 0) {
     // > 32 rows: 4 waves (2-wave workgroups of 2-4 M-tiles spill registers)
     *wv = (M > 32 || (slice && vgroups >= 16 * cus)) ? 4 : 2;
