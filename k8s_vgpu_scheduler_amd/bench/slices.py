@@ -344,8 +344,10 @@ def _loop_until_stop(a, dec, sync) -> int:
         if r and sys.stdin.readline().strip() in ("STOP", ""):
             break
     dt = time.perf_counter() - t0
-    print("DONE " + json.dumps({"seconds": dt, "tokens": a.batch * steps, "tok_s": a.batch * steps / dt,
-                                "loop": True}), flush=True)
+    done = {"seconds": dt, "tokens": a.batch * steps, "tok_s": a.batch * steps / dt, "loop": True}
+    if a.device != "cpu":
+        done.update(_governor_stats())
+    print("DONE " + json.dumps(done), flush=True)
     return 0
 
 
