@@ -148,3 +148,11 @@ def test_serving_native_vs_slice(tmp_path):
     # inside the slice (virtualised hipMemGetInfo), the card natively
     assert sl["device_mem_total_mib"] == 36864 and nat["device_mem_total_mib"] > 280_000, out
     assert nat["max_model_len"] == 65536 and 4096 < sl["max_model_len"] < 32768, out
+
+
+def test_prefill_bench_runs(capsys):
+    """bench/prefill.py: the captured bucket graph on the tiny model."""
+    from k8s_vgpu_scheduler_amd.bench import prefill
+    prefill.main(["--model", "qwen3-tiny", "--len", "40", "--iters", "3", "--ctx", "512"])
+    out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert out["graph"] and out["bucket"] == 64 and out["ms_per_prefill"] > 0
