@@ -919,7 +919,9 @@ bool plan_wide(int M, int K, int N, int epi, int* nt, int* wv, int* S) {
     if (auto_s) {
       if (epi == EPI_SILU_MUL) *S = 1;
       else if (slice) *S = ntiles <= 128 ? 2 : 1;
-      else *S = vgroups <= 192 ? 4 : 1;
+      else if (cus > 160) *S = vgroups <= 192 ? 4 : 1;
+      // 97-160 CUs keep the split chosen above (measured: the chip's rule cost
+      // the 128-CU prefill 0.8 ms)
     }
     if (*wv <= 0) *wv = epi == EPI_SILU_MUL ? 2 : 4;
   }
