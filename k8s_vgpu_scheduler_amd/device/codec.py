@@ -206,7 +206,10 @@ def encode_cu_ranges(pd_single: list) -> str:
 
 
 def decode_cu_ranges(s: str) -> list[dict[str, list]]:
-    """-> per container: {uuid: [(lo, hi), ...]} (empty containers kept)."""
+    """-> per container: {uuid: [(lo, hi), ...]} (empty containers kept; a
+    pod with no containers encodes to "" and decodes back to [])."""
+    if not s:
+        return []
     out = []
     for ctr in s.split(CTR_SEP)[:-1] if s.endswith(CTR_SEP) else s.split(CTR_SEP):
         m = {}
