@@ -132,3 +132,86 @@ def test_admission_matrix(cluster, case):
     if case.check is not None:
         ops = json.loads(base64.b64decode(resp["patch"])) if resp.get("patch") else []
         assert case.check(ops), (case.name, ops)
+
+
+# ------------------------------------------------------------ review edges --
+
+def _review(pod):
+    return {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview", "request": {"uid": "u", "object": pod}}
+
+
+def test_pod_without_containers_denied(cluster):
+    resp = Webhook("hami-scheduler").handle_review(_review({"metadata": {"name": "p"}, "spec": {}}))["response"]
+    assert not resp["allowed"] and resp["status"]["code"] == 403
+
+
+@pytest.mark.parametrize("force,want_changed", [(True, True), (False, False)])
+def test_default_scheduler_overwrite_flag(cluster, force, want_changed):
+    pod = amd_pod("p", mem=1000)
+    pod["spec"]["schedulerName"] = "default-scheduler"
+    resp = Webhook("hami-scheduler", force_overwrite_default_scheduler=force).handle_review(_review(pod))["response"]
+    ops = json.loads(base64.b64decode(resp["patch"])) if resp.get("patch") else []
+    assert resp["allowed"]
+    assert sets(ops, "/schedulerName", "hami-scheduler") == want_changed
+
+
+def test_privileged_pod_without_device_request_allowed(cluster):
+    pod = amd_pod("p", containers=[c(gpu=None)])
+    pod["spec"]["containers"][0]["securityContext"] = {"privileged": True}
+    assert Webhook("hami-scheduler").handle_review(_review(pod))["response"]["allowed"]
+
+
+def test_uid_and_api_version_echoed(cluster):
+    out = Webhook("hami-scheduler").handle_review(_review(amd_pod("p", mem=10)))
+    assert out["response"]["uid"] == "u" and out["apiVersion"] == "admission.k8s.io/v1"
+    assert out["kind"] == "AdmissionReview"
+
+
+# ---------------------------------------------------------------- json_patch --
+
+from hypothesis import given, settings, strategies as st  # noqa: E402
+
+from k8s_vgpu_scheduler_amd.scheduler.webhook import json_patch  # noqa: E402
+
+
+def _unesc(k):
+    return k.replace("~1", "/").replace("~0", "~")
+
+
+def _apply(doc, ops):
+    """Minimal RFC 6902 applier for add/remove/replace (test oracle)."""
+    import copy
+    doc = copy.deepcopy(doc)
+    for op in ops:
+        if op["path"] == "/":
+            doc = copy.deepcopy(op["value"])
+            continue
+        parts = [_unesc(p) for p in op["path"].split("/")[1:]]
+        tgt = doc
+        for p in parts[:-1]:
+            tgt = tgt[int(p)] if isinstance(tgt, list) else tgt[p]
+        last = parts[-1]
+        if isinstance(tgt, list):
+            last = int(last)
+        if op["op"] == "remove":
+            del tgt[last]
+        else:
+            tgt[last] = copy.deepcopy(op["value"])
+    return doc
+
+
+keys = st.sampled_from(["a", "b", "c/d", "e~f", "amd.com/gpu"])
+json_vals = st.recursive(st.one_of(st.none(), st.booleans(), st.integers(-5, 5), st.text(max_size=3)),
+                         lambda ch: st.one_of(st.lists(ch, max_size=3), st.dictionaries(keys, ch, max_size=4)),
+                         max_leaves=12)
+
+
+@settings(max_examples=150, deadline=None)
+@given(st.dictionaries(keys, json_vals, max_size=4), st.dictionaries(keys, json_vals, max_size=4))
+def test_json_patch_transforms_a_into_b(a, b):
+    assert _apply(a, json_patch(a, b)) == b
+
+
+def test_json_patch_escapes_resource_names():
+    ops = json_patch({"r": {}}, {"r": {"amd.com/gpucores": "100"}})
+    assert ops == [{"op": "add", "path": "/r/amd.com~1gpucores", "value": "100"}]
