@@ -1,6 +1,7 @@
 """Numerics of the hand-written gfx950 kernels vs plain PyTorch fp32 references."""
 
 import math
+import os
 
 import pytest
 import torch
@@ -143,14 +144,18 @@ def test_decoder_native_matches_reference():
 
 
 @pytest.mark.parametrize("batch", [1, 5, 32])
-def test_decoder_skinny_path_matches(batch):
+def test_decoder_skinny_path_matches(ops, batch):
     """Skinny MFMA GEMM path (packed gate_up+SiLU / down / lm_head) vs the
     hipBLASLt path and the fp32 reference, same weights, over 3 decode steps."""
     from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
 
     decs = [Qwen3Decoder(QWEN3_TINY, batch=batch, max_ctx=64, device="cuda", native=nat, seed=5, skinny=sk)
             for nat, sk in ((True, True), (True, False), (False, False))]
-    assert decs[0].skinny and decs[0].w.lm_head is None and "wgu" not in decs[0].w.layers[0]
+    assert decs[0].skinny and decs[0].w.lm_head is None
+    # batch <= 16 on the whole chip keeps the plain gate_up copy for prompt rows
+    # (hipBLASLt + SiLU), otherwise only the packed one exists (models/qwen3.py)
+    keep_gu = batch <= 16 and ops.visible_cus() > int(os.environ.get("MIVGPU_SLICE_PLAN_CUS", "96"))
+    assert ("wgu" in decs[0].w.layers[0]) == keep_gu and "pgu" in decs[0].w.layers[0]
     for d in decs:
         d.fill_context(12)
     for _ in range(3):

@@ -116,10 +116,15 @@ def test_scratch_never_grows_under_a_graph():
     ops.require_native()
     d = Qwen3Decoder(QWEN3_TINY, batch=1, max_ctx=256, device="cuda")
     d.capture()
-    pl = d.packed_linears()[0]
+    # a projection and row count whose plan splits K (not every plan does:
+    # wide SiLU plans of prompt rows run unsplit, ops.skinny_plan)
+    pick = [(pl, m) for pl in d.packed_linears() for m in (1, 8, 32, 100, 128)
+            if ops.skinny_plan(m, pl.K, pl.N, pl.epi)["scratch_floats"] > 0]
+    assert pick, "no split-K plan among the tiny decoder's projections"
+    pl, m = pick[0]
     pl.scratch, pl.tickets = None, None        # as if nothing were reserved
     with pytest.raises(RuntimeError, match="under a captured graph"):
-        pl(torch.zeros(100, pl.K, dtype=torch.bfloat16, device="cuda"))
+        pl(torch.zeros(m, pl.K, dtype=torch.bfloat16, device="cuda"))
 
 
 def test_serving_native_vs_slice(tmp_path):
