@@ -45,6 +45,10 @@ def parse(q) -> Decimal:
 
 
 def _num(s: str) -> Decimal:
+    # Decimal() also takes "1_000", " 1" (as in "1 Gi"), "Infinity" and "NaN";
+    # a Quantity takes none of them
+    if "_" in s or any(c.isspace() for c in s):
+        raise QuantityError(f"invalid quantity number {s!r}")
     try:
         d = Decimal(s)
     except InvalidOperation as e:
