@@ -1,0 +1,38 @@
+"""Differential tests: the shim's C++ parsers (libmivgpu.so, exported for
+tests) against the monitor's Python ones (monitor/feedback.py), which must
+agree because the monitor reconciles each region against the same grant the
+shim parsed (``expected_region``)."""
+
+import ctypes
+
+from hypothesis import given, settings, strategies as st
+
+from k8s_vgpu_scheduler_amd.monitor import feedback as F
+
+rng = st.tuples(st.integers(0, 255), st.integers(0, 63)).map(lambda t: f"{t[0]}-{t[0] + t[1]}" if t[1] else str(t[0]))
+dev_mask = st.tuples(st.integers(0, 7), st.lists(rng, min_size=1, max_size=4)).map(
+    lambda t: f"{t[0]}:{','.join(t[1])}")
+mask = st.lists(dev_mask, max_size=4, unique_by=lambda s: s.split(":")[0]).map(";".join)
+
+
+def _lib(native_build):
+    lib = ctypes.CDLL(str(native_build["shim"]))
+    lib.mivgpu_parse_size.restype = ctypes.c_ulonglong
+    lib.mivgpu_parse_size.argtypes = [ctypes.c_char_p]
+    lib.mivgpu_parse_cu_mask_count.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    return lib
+
+
+@settings(max_examples=200, deadline=None)
+@given(mask, st.integers(0, 7))
+def test_cu_mask_count_agrees(native_build, m, idx):
+    lib = _lib(native_build)
+    assert lib.mivgpu_parse_cu_mask_count(m.encode(), idx) == F.mask_count(m, idx), (m, idx)
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.integers(1, 10 ** 6), st.sampled_from(["", "k", "m", "g", "K", "M", "G"]))
+def test_parse_size_agrees(native_build, n, suf):
+    lib = _lib(native_build)
+    s = f"{n}{suf}"
+    assert lib.mivgpu_parse_size(s.encode()) == F.parse_size(s), s
