@@ -36,3 +36,24 @@ def test_parse_size_agrees(native_build, n, suf):
     lib = _lib(native_build)
     s = f"{n}{suf}"
     assert lib.mivgpu_parse_size(s.encode()) == F.parse_size(s), s
+
+
+@settings(max_examples=100, deadline=None)
+@given(st.lists(st.integers(1, 31), min_size=1, max_size=3))
+def test_device_plugin_mask_counted_by_the_shim(native_build, granules):
+    """A grant built by the scheduler's allocator and the device plugin's env
+    writer is counted by the shim as exactly the CUs granted, per device."""
+    from k8s_vgpu_scheduler_amd.device.amd import cu_alloc
+    from k8s_vgpu_scheduler_amd.device.types import ContainerDevice
+    from k8s_vgpu_scheduler_amd.deviceplugin.allocate import PluginConfig, container_env
+
+    lib = _lib(native_build)
+    topo = cu_alloc.CUTopology()
+    devs = []
+    for i, g in enumerate(granules):
+        ranges = cu_alloc.pick(0, g * 8, topo)
+        devs.append(ContainerDevice(uuid=f"GPU-{i}", type="AMD", usedmem=10, usedcores=g * 8,
+                                    custominfo={"cu_ranges": ranges}))
+    env = container_env(devs, {}, PluginConfig(), "/tmp/x.cache")
+    for i, g in enumerate(granules):
+        assert lib.mivgpu_parse_cu_mask_count(env["HSA_CU_MASK"].encode(), i) == g * 8
