@@ -123,6 +123,11 @@ class Scheduler:
         self._usage_cache: dict[str, tuple[tuple, NodeUsage]] = {}
         self._score_memo: OrderedDict = OrderedDict()
         self._cache_mu = threading.Lock()
+        # Filter's read-usage -> fit -> commit-to-cache section: two overlapping
+        # Filters (threaded HTTP server, several scheduler profiles, a retried
+        # request) would otherwise both fit against the same free capacity and
+        # over-commit a GPU (tests/test_filter_concurrency.py)
+        self._decide_mu = threading.Lock()
         self.memo_hits = 0
         self.memo_misses = 0
         self.memo_class_hits = 0
@@ -619,6 +624,10 @@ class Scheduler:
             return {"NodeNames": node_names, "FailedNodes": None, "Error": ""}
         if nodes is not None:
             return self._filter_simulation(pod, nodes, reqs)
+        with self._decide_mu:
+            return self._filter_locked(pod, node_names, reqs)
+
+    def _filter_locked(self, pod: dict, node_names, reqs) -> dict:
         pi = self.pod_manager.take_and_delete_pod(pod)
         if pi:
             self.quota_manager.rm_usage(pod, pi.devices)

@@ -1,0 +1,73 @@
+"""Concurrent Filter calls must not over-commit a GPU.
+
+kube-scheduler calls the extender once per scheduling cycle, but the HTTP
+server is threaded and several scheduler profiles (or a retried request) can
+overlap; the reference serialises through its caches
+(pkg/scheduler/scheduler.go Filter).  Here 16 threads filter 16 pods that
+each want 40 % of a GPU's HBM onto a 1-node, 4-GPU cluster: at most 2 fit per
+GPU, so at most 8 may be placed and no GPU may end above its HBM."""
+
+import sys
+import threading
+import time
+from collections import defaultdict
+
+from k8s_vgpu_scheduler_amd.device.quota import get_local_cache
+from k8s_vgpu_scheduler_amd.k8s.client import init_global_client
+from k8s_vgpu_scheduler_amd.k8s.fake import FakeCluster
+from k8s_vgpu_scheduler_amd.scheduler.config import SchedulerConfig, init_devices_with_config
+from k8s_vgpu_scheduler_amd.scheduler import scheduler as S
+from k8s_vgpu_scheduler_amd.scheduler.scheduler import Scheduler
+from k8s_vgpu_scheduler_amd.testing import MI355X_MEM_MIB, amd_node, amd_pod
+
+from test_score_matrix import devs_of
+
+
+def test_concurrent_filters_never_overcommit(monkeypatch):
+    # widen the read-usage -> commit window so an unserialised Filter races
+    # every time (without the lock this places 16 pods, 1.5 TB on one GPU)
+    orig = S.score_node_safe
+
+    def slow(*a, **k):
+        r = orig(*a, **k)
+        time.sleep(0.002)
+        return r
+    monkeypatch.setattr(S, "score_node_safe", slow)
+    cluster = FakeCluster()
+    init_global_client(cluster)
+    init_devices_with_config()
+    get_local_cache().quotas.clear()
+    cluster.create("nodes", amd_node("n1", n=4))
+    s = Scheduler(cluster, SchedulerConfig())
+    s.start()
+    s.register()
+    mem = MI355X_MEM_MIB * 40 // 100
+    names = [f"p{i}" for i in range(16)]
+    for n in names:
+        cluster.create("pods", amd_pod(n, mem=mem))
+    barrier = threading.Barrier(len(names))
+    old = sys.getswitchinterval()
+    sys.setswitchinterval(1e-6)     # interleave the threads as finely as the GIL allows
+    placed, errors = [], []
+
+    def go(n):
+        try:
+            barrier.wait()
+            r = s.filter({"Pod": cluster.get_pod("default", n), "NodeNames": ["n1"]})
+            if r.get("NodeNames"):
+                placed.append(n)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+    ts = [threading.Thread(target=go, args=(n,)) for n in names]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    sys.setswitchinterval(old)
+    assert not errors, errors
+    per_gpu = defaultdict(int)
+    for n in placed:
+        for d in devs_of(cluster, n)[0]:
+            per_gpu[d.uuid] += d.usedmem
+    assert all(v <= MI355X_MEM_MIB for v in per_gpu.values()), dict(per_gpu)
+    assert len(placed) == 8, placed
