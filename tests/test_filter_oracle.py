@@ -114,3 +114,68 @@ def test_filter_agrees_with_oracle(nodes, pods, gpu_policy):
                 assert bin(bm).count("1") == d.usedcores
                 g["bitmap"] |= bm
             assert g["mem"] <= MEM and g["cu"] <= CUS and g["tasks"] <= SPLIT
+
+
+@settings(max_examples=60, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(st.dictionaries(st.sampled_from(["a", "b"]), st.integers(1, 2), min_size=1, max_size=2),
+       st.lists(st.one_of(st.tuples(st.just("add"), pod_spec),
+                          st.tuples(st.sampled_from(["delete", "succeed"]), st.integers(0, 50))),
+                min_size=1, max_size=14))
+def test_usage_released_by_delete_and_completion(nodes, ops):
+    """Interleave placements with pod deletions and completions: freed capacity
+    must become schedulable again at once (the usage cache and the Filter memo
+    are invalidated by the pod events), and the oracle still agrees."""
+    cluster = FakeCluster()
+    init_global_client(cluster)
+    init_devices_with_config()
+    get_local_cache().quotas.clear()
+    for name, k in nodes.items():
+        cluster.create("nodes", amd_node(name, n=k, split=SPLIT))
+    s = Scheduler(cluster, SchedulerConfig())
+    s.start()
+    s.register()
+    book = Book(nodes)
+    live = {}                       # pod name -> devices
+    for i, (kind, arg) in enumerate(ops):
+        if kind != "add":
+            if not live:
+                continue
+            name = sorted(live)[arg % len(live)]
+            if kind == "delete":
+                cluster.delete("pods", name, "default")
+            else:
+                p = cluster.get_pod("default", name)
+                p["status"] = {"phase": "Succeeded"}
+                cluster.update("pods", p)
+            for d in live.pop(name):
+                g = book.gpus[d.uuid]
+                g["mem"] -= d.usedmem
+                g["cu"] -= d.usedcores
+                g["tasks"] -= 1
+                g["bitmap"] &= ~cu_alloc.bitmap_from_ranges((d.custominfo or {}).get("cu_ranges") or [])
+            continue
+        n_gpu, mem, cores = arg
+        name = f"p{i}"
+        kw = dict(gpu=n_gpu, mem=mem)
+        if cores:
+            kw["cores"] = cores
+        cluster.create("pods", amd_pod(name, **kw))
+        want = book.feasible_nodes(n_gpu, mem, cores)
+        res = s.filter({"Pod": cluster.get_pod("default", name), "NodeNames": sorted(nodes)})
+        got = res.get("NodeNames") or []
+        assert bool(got) == bool(want), (i, ops[: i + 1], want, res)
+        if not got:
+            cluster.delete("pods", name, "default")
+            continue
+        assert got[0] in want
+        devs = devs_of(cluster, name)[0]
+        for d in devs:
+            g = book.gpus[d.uuid]
+            assert book.eligible(d.uuid, mem, cores)
+            g["mem"] += d.usedmem
+            g["cu"] += d.usedcores
+            g["tasks"] += 1
+            bm = cu_alloc.bitmap_from_ranges((d.custominfo or {}).get("cu_ranges") or [])
+            assert bm & g["bitmap"] == 0
+            g["bitmap"] |= bm
+        live[name] = devs
