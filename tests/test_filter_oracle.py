@@ -179,3 +179,51 @@ def test_usage_released_by_delete_and_completion(nodes, ops):
             assert bm & g["bitmap"] == 0
             g["bitmap"] |= bm
         live[name] = devs
+
+
+@settings(max_examples=50, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(st.integers(0, 600000), st.integers(0, 400),
+       st.lists(st.tuples(st.integers(1, 2), st.sampled_from([1000, 50000, 150000]), st.sampled_from([0, 25, 50])),
+                min_size=1, max_size=10))
+def test_namespace_quota_is_never_exceeded(mem_quota, core_quota, pods):
+    """Filter under a namespace ResourceQuota (limits.amd.com/gpumem / gpucores,
+    pkg/device/quota.go): a pod is placed only if the namespace's usage plus its
+    request stays within both limits (cores in % per GPU), on top of fitting."""
+    cluster = FakeCluster()
+    init_global_client(cluster)
+    init_devices_with_config()
+    q = get_local_cache()
+    q.quotas.clear()
+    q.add_quota({"metadata": {"name": "q", "namespace": "default"},
+                 "spec": {"hard": {"limits.amd.com/gpumem": str(mem_quota),
+                                   "limits.amd.com/gpucores": str(core_quota)}}})
+    cluster.create("nodes", amd_node("a", n=4, split=SPLIT))
+    s = Scheduler(cluster, SchedulerConfig())
+    s.start()
+    s.register()
+    book = Book({"a": 4})
+    used_mem = used_core = 0
+    try:
+        for i, (n_gpu, mem, cores) in enumerate(pods):
+            name = f"p{i}"
+            kw = dict(gpu=n_gpu, mem=mem)
+            if cores:
+                kw["cores"] = cores
+            cluster.create("pods", amd_pod(name, **kw))
+            fits_quota = used_mem + mem * n_gpu <= mem_quota and used_core + cores * n_gpu <= core_quota
+            want = fits_quota and bool(book.feasible_nodes(n_gpu, mem, cores))
+            res = s.filter({"Pod": cluster.get_pod("default", name), "NodeNames": ["a"]})
+            got = bool(res.get("NodeNames"))
+            assert got == want, (i, pods[: i + 1], mem_quota, core_quota, used_mem, used_core, res)
+            if not got:
+                cluster.delete("pods", name, "default")
+                continue
+            used_mem += mem * n_gpu
+            used_core += cores * n_gpu
+            for d in devs_of(cluster, name)[0]:
+                g = book.gpus[d.uuid]
+                g["mem"] += d.usedmem
+                g["cu"] += d.usedcores
+                g["tasks"] += 1
+    finally:
+        q.quotas.clear()
