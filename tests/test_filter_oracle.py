@@ -227,3 +227,39 @@ def test_namespace_quota_is_never_exceeded(mem_quota, core_quota, pods):
                 g["tasks"] += 1
     finally:
         q.quotas.clear()
+
+
+@settings(max_examples=40, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(st.dictionaries(st.sampled_from(["a", "b", "c"]), st.integers(1, 3), min_size=1, max_size=3),
+       st.lists(pod_spec, min_size=1, max_size=8))
+def test_simulation_filter_matches_the_real_one_without_side_effects(nodes, pods):
+    """Cluster-Autoscaler simulation (``Nodes`` given): the nodes are
+    transient templates, fitted empty as in the reference
+    (scheduler.go:865-893 getSimulationNodesUsage -> buildNodeUsage without
+    pod usage).  On an empty cluster it picks the node the real Filter picks;
+    it never patches a pod nor caches one, and it ignores the cached usage."""
+    cluster = FakeCluster()
+    init_global_client(cluster)
+    init_devices_with_config()
+    get_local_cache().quotas.clear()
+    for name, k in nodes.items():
+        cluster.create("nodes", amd_node(name, n=k, split=SPLIT))
+    s = Scheduler(cluster, SchedulerConfig())
+    s.start()
+    s.register()
+    node_objs = [cluster.get_node(n) for n in sorted(nodes)]
+    for i, (n_gpu, mem, cores) in enumerate(pods):
+        name = f"p{i}"
+        kw = dict(gpu=n_gpu, mem=mem)
+        if cores:
+            kw["cores"] = cores
+        cluster.create("pods", amd_pod(name, **kw))
+        pod = cluster.get_pod("default", name)
+        cached, patches = len(s.pod_manager), cluster.count("patch", "pods")
+        sim = s.filter({"Pod": pod, "Nodes": {"items": node_objs}})
+        assert len(s.pod_manager) == cached and cluster.count("patch", "pods") == patches
+        sim_node = [n["metadata"]["name"] for n in (sim.get("Nodes") or {}).get("items", [])]
+        real = s.filter({"Pod": pod, "NodeNames": sorted(nodes)})
+        assert sim_node == (real.get("NodeNames") or []), (i, pods[: i + 1], sim, real)
+        cluster.delete("pods", name, "default")      # back to an empty cluster
+        assert len(s.pod_manager) == 0
