@@ -624,10 +624,36 @@ class Scheduler:
             return {"NodeNames": node_names, "FailedNodes": None, "Error": ""}
         if nodes is not None:
             return self._filter_simulation(pod, nodes, reqs)
+        # decide and commit to the caches under the lock; the API writes
+        # (events, the allocation patch) happen outside it
         with self._decide_mu:
-            return self._filter_locked(pod, node_names, reqs)
+            d = self._decide(pod, node_names, reqs)
+        if d["best"] is None:
+            for reason, ns_ in sorted(d["failure"].items()):
+                self.events.filter_result(pod, E.FILTERING_FAILED, "",
+                                          f"{len(ns_)} nodes {reason}({','.join(sorted(ns_))})")
+            self.events.filter_result(pod, E.FILTERING_FAILED, "",
+                                      f"no available node, {len(node_names or [])} nodes do not meet")
+            return {"FailedNodes": d["failed"], "NodeNames": None, "Error": ""}
+        best, scores = d["best"], d["scores"]
+        try:
+            util.patch_pod_annotations(pod, d["annos"])
+        except Exception as e:  # noqa: BLE001
+            self.events.filter_result(pod, E.FILTERING_FAILED, "", e)
+            with self._decide_mu:
+                if d["added"]:
+                    self.quota_manager.rm_usage(pod, d["eff"])
+                self.pod_manager.del_pod(pod)
+            return {"Error": str(e)}
+        msg = (f"find fit node({best.node_id}), {len(node_names or []) - len(scores.node_list)} nodes not fit, "
+               f"{len(scores.node_list)} nodes fit("
+               + ",".join(f"{n.node_id}:{n.score:.2f}" for n in scores.node_list) + ")")
+        self.events.filter_result(pod, E.FILTERING_SUCCEED, msg, None)
+        return {"NodeNames": [best.node_id], "FailedNodes": d["failed"], "Error": ""}
 
-    def _filter_locked(self, pod: dict, node_names, reqs) -> dict:
+    def _decide(self, pod: dict, node_names, reqs) -> dict:
+        """Fit ``pod`` and, when a node fits, commit its allocation to the pod
+        and quota caches (caller holds ``_decide_mu``)."""
         pi = self.pod_manager.take_and_delete_pod(pod)
         if pi:
             self.quota_manager.rm_usage(pod, pi.devices)
@@ -637,12 +663,7 @@ class Scheduler:
             usage, _, failed = self.get_nodes_usage(node_names or [], pod)
             scores, failure = calc_score(usage, reqs, pod, failed, self.cfg.node_scheduler_policy)
         if not scores.node_list:
-            for reason, ns_ in sorted(failure.items()):
-                self.events.filter_result(pod, E.FILTERING_FAILED, "",
-                                          f"{len(ns_)} nodes {reason}({','.join(sorted(ns_))})")
-            self.events.filter_result(pod, E.FILTERING_FAILED, "",
-                                      f"no available node, {len(node_names or [])} nodes do not meet")
-            return {"FailedNodes": failed, "NodeNames": None, "Error": ""}
+            return {"best": None, "failure": failure, "failed": failed}
         scores.sort()
         best = scores.node_list[-1]
         # memo entries are shared: hand the winner's allocation out as a copy
@@ -654,19 +675,7 @@ class Scheduler:
         added = self.pod_manager.add_pod(pod, best.node_id, eff)
         if added:
             self.quota_manager.add_usage(pod, eff)
-        try:
-            util.patch_pod_annotations(pod, annos)
-        except Exception as e:  # noqa: BLE001
-            self.events.filter_result(pod, E.FILTERING_FAILED, "", e)
-            if added:
-                self.quota_manager.rm_usage(pod, eff)
-            self.pod_manager.del_pod(pod)
-            return {"Error": str(e)}
-        msg = (f"find fit node({best.node_id}), {len(node_names or []) - len(scores.node_list)} nodes not fit, "
-               f"{len(scores.node_list)} nodes fit("
-               + ",".join(f"{n.node_id}:{n.score:.2f}" for n in scores.node_list) + ")")
-        self.events.filter_result(pod, E.FILTERING_SUCCEED, msg, None)
-        return {"NodeNames": [best.node_id], "FailedNodes": failed, "Error": ""}
+        return {"best": best, "scores": scores, "failed": failed, "annos": annos, "eff": eff, "added": added}
 
     def _filter_simulation(self, pod: dict, nodes, reqs) -> dict:
         items = nodes.get("items", []) if isinstance(nodes, dict) else list(nodes)
