@@ -8,7 +8,9 @@
 //
 // MI355X-first design: the shim enqueues this one-wave kernel on the SAME
 // stream, in front of a user launch, at most once per `min interval` of host
-// submission.  The gate
+// submission.  With a KFD view of the GPU (the normal case) the bucket lives
+// on the host and the gate only enforces it (host_bucket_gate below).
+// Without one, the gate keeps the bucket itself (device-bucket mode): it
 //   1. reads the 100 MHz constant clock (s_memrealtime -> 10 ns ticks),
 //   2. debits the GPU time the process received since this stream's previous
 //      gate from a bucket shared by all its streams on this device: the
@@ -69,7 +71,7 @@ struct mivgpu_gate_host_stats {
   long long last_tokens_ns;
   long long last_hold_ns;
   unsigned long long share_ppm;  // HOST-written by the sampler: the process's measured GPU share, ppm
-  unsigned long long pad;
+  long long host_tokens_ns;      // HOST-written by the sampler: the bucket balance (host-bucket mode)
   mivgpu_gate_trace_entry trace[MIVGPU_GATE_TRACE];  // ring, index = gates % N
   long long hold_end_ns[MIVGPU_GATE_SLOTS];          // device ns at which a slot's hold ends
 };
@@ -91,6 +93,72 @@ __device__ __forceinline__ void astoreu(unsigned long long* p, unsigned long lon
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Bounded spin lock (acquire).  If it cannot be taken in ~0.5 s something is
+// badly wrong (a gate died holding it); proceed unlocked rather than hang.
+__device__ __forceinline__ bool gate_lock(mivgpu_gate_state* st) {
+  for (unsigned int spins = 0; spins < (1u << 17); ++spins) {
+    unsigned long long expected = 0ull;
+    if (__hip_atomic_compare_exchange_strong(&st->lock, &expected, 1ull, __ATOMIC_ACQUIRE,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      return true;
+    __builtin_amdgcn_s_sleep(8);
+  }
+  return false;
+}
+
+__device__ __forceinline__ long long host_load(long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Host-bucket mode (flags bit 1, used whenever the shim has a KFD view of the
+// GPU): the shim's sampler integrates the share of the GPU this process
+// actually receives -- own resident waves / all resident waves, every ~2 ms --
+// against its entitlement (rate x wall time) and publishes the balance.  The
+// gate only enforces it: in debt, it holds the stream until the balance is
+// back to zero (the sampler refills it while the process has no waves
+// resident), at most max_hold_ns per gate; larger debts are repaid over the
+// following gates.  Time the process spends co-resident with other tenants is
+// charged at the share it got, and time it spends queued or idle is not
+// charged at all -- the sample-time bias of charging a whole batch at one
+// share estimate is gone.
+__device__ void host_bucket_gate(mivgpu_gate_state* st, mivgpu_gate_host_stats* hs, int slot,
+                                 long long max_hold_ns, unsigned int flags) {
+  const long long t0 = rt_ns();
+  long long tokens = host_load(&hs->host_tokens_ns);
+  long long t = t0;
+  if (tokens < 0) {
+    // "holding until at most" marker: the sampler discounts the gate's own
+    // resident wave while it sits here
+    __hip_atomic_store(&hs->hold_end_ns[slot], t0 + max_hold_ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    while (tokens < 0 && t < t0 + max_hold_ns) {
+      for (int k = 0; k < 4; ++k) __builtin_amdgcn_s_sleep(127);   // ~14 us between host reads
+      tokens = host_load(&hs->host_tokens_ns);
+      t = rt_ns();
+    }
+    __hip_atomic_store(&hs->hold_end_ns[slot], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  const long long hold = t - t0;
+  const bool locked = gate_lock(st);
+  astore(&st->slot_exit_ns[slot], t);
+  const unsigned long long held_tot = aloadu(&st->held_total_ns) + (unsigned long long)hold;
+  const unsigned long long gates = aloadu(&st->gates) + 1ull;
+  astoreu(&st->held_total_ns, held_tot);
+  astoreu(&st->gates, gates);
+  if (locked) __hip_atomic_store(&st->lock, 0ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&hs->held_total_ns, held_tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&hs->gates, gates, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (flags & 1u) {
+    mivgpu_gate_trace_entry* e = &hs->trace[(gates - 1) % MIVGPU_GATE_TRACE];
+    e->now_ns = t0;
+    e->submit_ns = -1;
+    e->prev_exit_ns = -1;
+    e->busy_ns = 0;
+    e->hold_ns = hold;
+    e->tokens_ns = tokens;
+    e->slot = slot;
+  }
+}
+
 extern "C" __global__ void __launch_bounds__(64)
 mivgpu_gate(mivgpu_gate_state* st, mivgpu_gate_host_stats* hs, long long submit_ns,
             int slot, unsigned int rate_ppm, long long cap_ns, long long max_hold_ns, unsigned int use_share,
@@ -98,19 +166,13 @@ mivgpu_gate(mivgpu_gate_state* st, mivgpu_gate_host_stats* hs, long long submit_
   if (threadIdx.x != 0) return;
   if (slot < 0 || slot >= MIVGPU_GATE_SLOTS) slot = 0;
   if (rate_ppm == 0) rate_ppm = 1;
-
-  // Bounded spin lock (acquire).  If it cannot be taken in ~0.5 s something is
-  // badly wrong (a gate died holding it); proceed unlocked rather than hang.
-  bool locked = false;
-  for (unsigned int spins = 0; spins < (1u << 17); ++spins) {
-    unsigned long long expected = 0ull;
-    if (__hip_atomic_compare_exchange_strong(&st->lock, &expected, 1ull, __ATOMIC_ACQUIRE,
-                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-      locked = true;
-      break;
-    }
-    __builtin_amdgcn_s_sleep(8);
+  if ((flags & 2u) && hs) {
+    host_bucket_gate(st, hs, slot, max_hold_ns, flags);
+    return;
   }
+
+  // Device-bucket mode (no KFD view: the busy wall time is the charge).
+  const bool locked = gate_lock(st);
 
   const long long now = rt_ns();
   long long last = aload(&st->last_ns);

@@ -40,6 +40,16 @@ int ndev() {
 // = runtime "context" bytes (mockhip_set_kfd_context) + live allocations.
 // MOCKHIP_KFD_PID != getpid() stands for a container's pid namespace.
 size_t kfd_context[16] = {0};
+// Simulated runtime VRAM of loaded code objects (MOCKHIP_MODULES=1):
+// MOCKHIP_MODULE_KIB per module (default 2048, one 2 MiB fragment), part of
+// the KFD per-process total like the runtime's real code-object allocations.
+size_t module_bytes[16] = {0};
+std::unordered_map<void*, size_t> modules;
+size_t module_cost() {
+  const char* k = getenv("MOCKHIP_MODULE_KIB");
+  return (size_t)(k ? strtoull(k, nullptr, 10) : 2048) << 10;
+}
+
 void kfd_publish_locked(int dev) {
   const char* root = getenv("MOCKHIP_KFD_SYSFS");
   if (!root) return;
@@ -54,7 +64,7 @@ void kfd_publish_locked(int dev) {
   snprintf(path, sizeof(path), "%s/proc/%d/vram_%d", root, pid, (gid ? atoi(gid) : 1) + dev);
   FILE* f = fopen(path, "w");
   if (!f) return;
-  fprintf(f, "%zu\n", kfd_context[dev] + used_bytes[dev]);
+  fprintf(f, "%zu\n", kfd_context[dev] + used_bytes[dev] + module_bytes[dev]);
   fclose(f);
   // with MOCKHIP_KFD_OCC=1, also the per-process wave count the occupancy
   // sampler reads: one CU-unit per 64 MiB in use (moves with the traffic)
@@ -196,10 +206,40 @@ EXPORT hipError_t hipStreamIsCapturing(hipStream_t, hipStreamCaptureStatus* s) {
   return hipSuccess;
 }
 EXPORT hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
-// No GPU: the governor code object loads only in MOCKHIP_GOVERNOR mode.
-EXPORT hipError_t hipModuleLoadData(hipModule_t* m, const void*) {
-  if (!mock_governor()) return hipErrorNoBinaryForGpu;
-  *m = reinterpret_cast<hipModule_t>(0x10001);
+// No GPU: the governor code object loads only in MOCKHIP_GOVERNOR mode, any
+// other image only in MOCKHIP_MODULES mode (as a fake module with simulated
+// code-object VRAM).
+hipError_t mock_module_load(hipModule_t* m) {
+  if (mock_governor()) {
+    *m = reinterpret_cast<hipModule_t>(0x10001);
+    return hipSuccess;
+  }
+  if (!getenv("MOCKHIP_MODULES")) return hipErrorNoBinaryForGpu;
+  std::lock_guard<std::mutex> lk(mu);
+  void* h = malloc(64);
+  modules[h] = module_cost();
+  module_bytes[cur_dev] += module_cost();
+  kfd_publish_locked(cur_dev);
+  *m = reinterpret_cast<hipModule_t>(h);
+  return hipSuccess;
+}
+EXPORT hipError_t hipModuleLoadData(hipModule_t* m, const void*) { return mock_module_load(m); }
+EXPORT hipError_t hipModuleLoadDataEx(hipModule_t* m, const void*, unsigned int, hipJitOption*, void**) {
+  return mock_module_load(m);
+}
+EXPORT hipError_t hipModuleLoad(hipModule_t* m, const char* path) {
+  struct stat st;
+  if (!path || stat(path, &st) != 0) return hipErrorFileNotFound;
+  return mock_module_load(m);
+}
+EXPORT hipError_t hipModuleUnload(hipModule_t m) {
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = modules.find(reinterpret_cast<void*>(m));
+  if (it == modules.end()) return hipErrorInvalidResourceHandle;
+  module_bytes[cur_dev] -= it->second;
+  kfd_publish_locked(cur_dev);
+  free(it->first);
+  modules.erase(it);
   return hipSuccess;
 }
 EXPORT hipError_t hipModuleGetFunction(hipFunction_t* f, hipModule_t, const char* name) {
@@ -210,3 +250,83 @@ EXPORT hipError_t hipModuleGetFunction(hipFunction_t* f, hipModule_t, const char
   return hipSuccess;
 }
 EXPORT unsigned long long mockhip_launch_count(void) { return launches.load(); }
+
+// ---- launch entry points beyond the classic ones (hip_6.5, multi-device) ----
+EXPORT hipError_t hipLaunchKernelExC(const hipLaunchConfig_t*, const void*, void**) { launches++; return hipSuccess; }
+EXPORT hipError_t hipDrvLaunchKernelEx(const HIP_LAUNCH_CONFIG*, hipFunction_t, void**, void**) {
+  launches++;
+  return hipSuccess;
+}
+EXPORT hipError_t hipLaunchCooperativeKernelMultiDevice(hipLaunchParams*, int n, unsigned int) {
+  launches += (unsigned long long)n;
+  return hipSuccess;
+}
+EXPORT hipError_t hipExtLaunchMultiKernelMultiDevice(hipLaunchParams*, int n, unsigned int) {
+  launches += (unsigned long long)n;
+  return hipSuccess;
+}
+// Mock streams are the device index + 1 cast to a handle (nullptr: current device).
+EXPORT hipError_t hipStreamGetDevice(hipStream_t s, hipDevice_t* d) {
+  *d = s ? (int)(reinterpret_cast<uintptr_t>(s) - 1) : cur_dev;
+  return hipSuccess;
+}
+
+// ---- arrays: a handle whose "VRAM" is width x height x depth x element ----
+EXPORT hipError_t hipMallocArray(hipArray_t* a, const hipChannelFormatDesc* d, size_t w, size_t h, unsigned int) {
+  const size_t e = d ? (size_t)(d->x + d->y + d->z + d->w) / 8 : 4;
+  return do_alloc(reinterpret_cast<void**>(a), w * (h ? h : 1) * (e ? e : 4));
+}
+EXPORT hipError_t hipMalloc3DArray(hipArray_t* a, const hipChannelFormatDesc* d, hipExtent x, unsigned int) {
+  const size_t e = d ? (size_t)(d->x + d->y + d->z + d->w) / 8 : 4;
+  return do_alloc(reinterpret_cast<void**>(a), x.width * (x.height ? x.height : 1) * (x.depth ? x.depth : 1) * e);
+}
+EXPORT hipError_t hipArrayCreate(hipArray_t* a, const HIP_ARRAY_DESCRIPTOR* d) {
+  return do_alloc(reinterpret_cast<void**>(a), d->Width * (d->Height ? d->Height : 1) * 4 * d->NumChannels);
+}
+EXPORT hipError_t hipArray3DCreate(hipArray_t* a, const HIP_ARRAY3D_DESCRIPTOR* d) {
+  return do_alloc(reinterpret_cast<void**>(a),
+                  d->Width * (d->Height ? d->Height : 1) * (d->Depth ? d->Depth : 1) * 4 * d->NumChannels);
+}
+EXPORT hipError_t hipMallocMipmappedArray(hipMipmappedArray_t* a, const hipChannelFormatDesc*, hipExtent x,
+                                          unsigned int, unsigned int) {
+  return do_alloc(reinterpret_cast<void**>(a), x.width * (x.height ? x.height : 1) * 4);
+}
+EXPORT hipError_t hipMipmappedArrayCreate(hipMipmappedArray_t* a, HIP_ARRAY3D_DESCRIPTOR* d, unsigned int) {
+  return do_alloc(reinterpret_cast<void**>(a), d->Width * (d->Height ? d->Height : 1) * 4);
+}
+EXPORT hipError_t hipMalloc3D(hipPitchedPtr* pp, hipExtent x) {
+  pp->pitch = (x.width + 255) & ~size_t(255);
+  pp->xsize = x.width;
+  pp->ysize = x.height;
+  return do_alloc(&pp->ptr, pp->pitch * (x.height ? x.height : 1) * (x.depth ? x.depth : 1));
+}
+EXPORT hipError_t hipFreeArray(hipArray_t a) { return do_free(a); }
+EXPORT hipError_t hipArrayDestroy(hipArray_t a) { return do_free(a); }
+EXPORT hipError_t hipFreeMipmappedArray(hipMipmappedArray_t a) { return do_free(a); }
+EXPORT hipError_t hipMipmappedArrayDestroy(hipMipmappedArray_t a) { return do_free(a); }
+
+// ---- run-time lookup: the runtime's OWN functions by name, like the real
+// hipGetProcAddress (never the global binding an interposer would provide) ----
+EXPORT hipError_t hipGetProcAddress(const char* sym, void** pfn, int, uint64_t, hipDriverProcAddressQueryResult* st) {
+  static const struct { const char* n; void* f; } kTable[] = {
+      {"hipMalloc", reinterpret_cast<void*>(static_cast<hipError_t (*)(void**, size_t)>(&hipMalloc))},
+      {"hipFree", reinterpret_cast<void*>(&hipFree)},
+      {"hipModuleLaunchKernel", reinterpret_cast<void*>(&hipModuleLaunchKernel)},
+      {"hipLaunchKernel", reinterpret_cast<void*>(&hipLaunchKernel)},
+      {"hipDrvLaunchKernelEx", reinterpret_cast<void*>(&hipDrvLaunchKernelEx)},
+      {"hipModuleLoadDataEx", reinterpret_cast<void*>(&hipModuleLoadDataEx)},
+      {"hipMemGetInfo", reinterpret_cast<void*>(&hipMemGetInfo)},
+      {"hipGetDeviceProperties", reinterpret_cast<void*>(&hipGetDevicePropertiesR0600)},
+      {"hipGetDeviceCount", reinterpret_cast<void*>(&hipGetDeviceCount)},
+  };
+  for (const auto& e : kTable) {
+    if (!strcmp(e.n, sym)) {
+      *pfn = e.f;
+      if (st) *st = HIP_GET_PROC_ADDRESS_SUCCESS;
+      return hipSuccess;
+    }
+  }
+  *pfn = nullptr;
+  if (st) *st = HIP_GET_PROC_ADDRESS_SYMBOL_NOT_FOUND;
+  return hipErrorNotFound;
+}

@@ -15,6 +15,25 @@
 //   device <i>       hipSetDevice
 //   hsainit          hsa_init (interposed by the shim) + the HSA_CU_MASK /
 //                    ROCR_VISIBLE_DEVICES ROCr would read
+//   dlsym_alloc <MiB>  hipMalloc looked up at run time: dlopen + dlsym
+//   dlvsym_alloc <MiB> ... dlopen + dlvsym(hip_4.2)
+//   gpa_alloc <MiB>    ... dlsym("hipGetProcAddress") + hipGetProcAddress
+//                      (Triton's path)
+//   gpa_launch <n>     hipModuleLaunchKernel via hipGetProcAddress, n times
+//   launchex <n>       n x hipLaunchKernelExC + n x hipDrvLaunchKernelEx
+//   multilaunch        hipLaunchCooperativeKernelMultiDevice + hipExt... on
+//                      every device (MOCKHIP_DEVICES)
+//   array <MiB>        hipMallocArray (float4 texels)
+//   array3d <MiB>      hipMalloc3DArray
+//   arraycreate <MiB>  hipArrayCreate (driver API)
+//   malloc3d <MiB>     hipMalloc3D (pitched)
+//   mipmap <MiB>       hipMallocMipmappedArray, 1 level
+//   arrayfree          free every array / mipmap (hipFreeArray, hipArrayDestroy ...)
+//   modload <path>     hipModuleLoad; moddata <path>: hipModuleLoadData of the
+//                      file's bytes; moddataex <path>: hipModuleLoadDataEx
+//   modunload          hipModuleUnload every module
+//   getenv <KEY>       getenv as the runtime would call it
+//   balance            the governor's host-bucket balance on device 0
 //   stress <threads> <iters> <max MiB>
 //                    threads doing random hipMalloc/hipFree and
 //                    hipMemCreate/hipMemRelease, one kernel launch per
@@ -78,6 +97,35 @@ static void stress_thread(int seed, int iters, int max_mib, std::atomic<long>* a
 }
 
 extern "C" hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_tR0600*, int);
+
+static void* hip_handle() {
+  void* h = dlopen("libamdhip64.so", RTLD_NOW | RTLD_NOLOAD);
+  return h;
+}
+
+static unsigned long long shim_seen() {
+  auto f = (unsigned long long (*)(void))dlsym(RTLD_DEFAULT, "mivgpu_launch_count");
+  return f ? f() : 0ull;
+}
+static unsigned long long real_seen() {
+  auto g = (unsigned long long (*)(void))dlsym(RTLD_DEFAULT, "mockhip_launch_count");
+  return g ? g() : 0ull;
+}
+
+static std::vector<void*> g_arrays;          // hipArray_t / hipMipmappedArray_t (tagged below)
+static std::vector<int> g_array_kind;        // 0 FreeArray, 1 ArrayDestroy, 2 FreeMipmappedArray
+static std::vector<hipModule_t> g_modules;
+
+static std::vector<char> read_file(const char* path) {
+  std::vector<char> b;
+  FILE* f = fopen(path, "rb");
+  if (!f) return b;
+  char buf[65536];
+  size_t n;
+  while ((n = fread(buf, 1, sizeof(buf), f)) > 0) b.insert(b.end(), buf, buf + n);
+  fclose(f);
+  return b;
+}
 
 int main(int argc, char** argv) {
   std::vector<void*> bufs;
@@ -160,6 +208,147 @@ int main(int argc, char** argv) {
       auto f = (long long (*)(int))dlsym(RTLD_DEFAULT, "mivgpu_process_usage");
       printf("{\"op\":\"stress\",\"allocs\":%ld,\"ooms\":%ld,\"errors\":%ld,\"usage_after\":%lld}\n",
              allocs.load(), ooms.load(), errors.load(), f ? f(0) : -2ll);
+    } else if (!strcmp(c, "dlsym_alloc") || !strcmp(c, "dlvsym_alloc") || !strcmp(c, "gpa_alloc")) {
+      size_t mib = strtoull(argv[++i], nullptr, 10);
+      using malloc_fn = hipError_t (*)(void**, size_t);
+      malloc_fn f = nullptr;
+      void* h = hip_handle();
+      if (!strcmp(c, "dlsym_alloc")) {
+        f = (malloc_fn)dlsym(h, "hipMalloc");
+      } else if (!strcmp(c, "dlvsym_alloc")) {
+        f = (malloc_fn)dlvsym(h, "hipMalloc", "hip_4.2");
+      } else {
+        using gpa_fn = hipError_t (*)(const char*, void**, int, uint64_t, hipDriverProcAddressQueryResult*);
+        gpa_fn gpa = (gpa_fn)dlsym(h, "hipGetProcAddress");
+        hipDriverProcAddressQueryResult st;
+        if (gpa) (void)gpa("hipMalloc", (void**)&f, 700, 0, &st);
+      }
+      void* p = nullptr;
+      hipError_t rc = f ? f(&p, mib << 20) : hipErrorNotFound;
+      // the lookup must hand out the interposed entry point (the global binding)
+      printf("{\"op\":\"%s\",\"mib\":%zu,\"rc\":%d,\"hooked\":%d}\n", c, mib, (int)rc,
+             f == (malloc_fn)&hipMalloc ? 1 : 0);
+      if (rc == hipSuccess) bufs.push_back(p);
+    } else if (!strcmp(c, "gpa_launch")) {
+      long n = strtol(argv[++i], nullptr, 10);
+      using gpa_fn = hipError_t (*)(const char*, void**, int, uint64_t, hipDriverProcAddressQueryResult*);
+      gpa_fn gpa = (gpa_fn)dlsym(hip_handle(), "hipGetProcAddress");
+      using launch_fn = hipError_t (*)(hipFunction_t, unsigned, unsigned, unsigned, unsigned, unsigned, unsigned,
+                                       unsigned, hipStream_t, void**, void**);
+      launch_fn f = nullptr;
+      hipDriverProcAddressQueryResult st;
+      if (gpa) (void)gpa("hipModuleLaunchKernel", (void**)&f, 700, 0, &st);
+      for (long k = 0; f && k < n; ++k) (void)f(nullptr, 1, 1, 1, 64, 1, 1, 0, nullptr, nullptr, nullptr);
+      printf("{\"op\":\"gpa_launch\",\"n\":%ld,\"found\":%d,\"shim_seen\":%llu,\"real_seen\":%llu}\n", n,
+             f ? 1 : 0, shim_seen(), real_seen());
+    } else if (!strcmp(c, "launchex")) {
+      long n = strtol(argv[++i], nullptr, 10);
+      static char dummy;
+      hipLaunchConfig_t cfg{};
+      cfg.gridDim = dim3(1);
+      cfg.blockDim = dim3(64);
+      HIP_LAUNCH_CONFIG dcfg{};
+      dcfg.gridDimX = dcfg.gridDimY = dcfg.gridDimZ = 1;
+      dcfg.blockDimX = 64;
+      dcfg.blockDimY = dcfg.blockDimZ = 1;
+      for (long k = 0; k < n; ++k) {
+        (void)hipLaunchKernelExC(&cfg, &dummy, nullptr);
+        (void)hipDrvLaunchKernelEx(&dcfg, nullptr, nullptr, nullptr);
+      }
+      printf("{\"op\":\"launchex\",\"n\":%ld,\"shim_seen\":%llu,\"real_seen\":%llu}\n", n, shim_seen(),
+             real_seen());
+    } else if (!strcmp(c, "multilaunch")) {
+      int nd = 0;
+      (void)hipGetDeviceCount(&nd);
+      static char dummy;
+      std::vector<hipLaunchParams> lp(nd);
+      for (int d = 0; d < nd; ++d) {
+        lp[d].func = &dummy;
+        lp[d].gridDim = dim3(1);
+        lp[d].blockDim = dim3(64);
+        lp[d].args = nullptr;
+        lp[d].sharedMem = 0;
+        lp[d].stream = reinterpret_cast<hipStream_t>((uintptr_t)d + 1);   // mock: device d's stream
+      }
+      (void)hipLaunchCooperativeKernelMultiDevice(lp.data(), nd, 0);
+      (void)hipExtLaunchMultiKernelMultiDevice(lp.data(), nd, 0);
+      printf("{\"op\":\"multilaunch\",\"devices\":%d,\"shim_seen\":%llu,\"real_seen\":%llu}\n", nd, shim_seen(),
+             real_seen());
+    } else if (!strcmp(c, "array") || !strcmp(c, "array3d") || !strcmp(c, "arraycreate") || !strcmp(c, "mipmap")) {
+      size_t mib = strtoull(argv[++i], nullptr, 10);
+      hipChannelFormatDesc desc{};
+      desc.x = desc.y = desc.z = desc.w = 32;       // float4 = 16 B per texel
+      desc.f = hipChannelFormatKindFloat;
+      const size_t w = 4096, h = (mib << 20) / (w * 16);
+      void* a = nullptr;
+      hipError_t rc;
+      int kind = 0;
+      if (!strcmp(c, "array")) {
+        rc = hipMallocArray((hipArray_t*)&a, &desc, w, h, 0);
+      } else if (!strcmp(c, "array3d")) {
+        rc = hipMalloc3DArray((hipArray_t*)&a, &desc, make_hipExtent(w, h, 1), 0);
+      } else if (!strcmp(c, "arraycreate")) {
+        HIP_ARRAY_DESCRIPTOR d{};
+        d.Width = w;
+        d.Height = h;
+        d.Format = HIP_AD_FORMAT_FLOAT;
+        d.NumChannels = 4;
+        rc = hipArrayCreate((hipArray_t*)&a, &d);
+        kind = 1;
+      } else {
+        rc = hipMallocMipmappedArray((hipMipmappedArray_t*)&a, &desc, make_hipExtent(w, h, 0), 1, 0);
+        kind = 2;
+      }
+      printf("{\"op\":\"%s\",\"mib\":%zu,\"rc\":%d}\n", c, mib, (int)rc);
+      if (rc == hipSuccess) {
+        g_arrays.push_back(a);
+        g_array_kind.push_back(kind);
+      }
+    } else if (!strcmp(c, "malloc3d")) {
+      size_t mib = strtoull(argv[++i], nullptr, 10);
+      hipPitchedPtr pp{};
+      hipError_t rc = hipMalloc3D(&pp, make_hipExtent(1 << 20, mib, 1));   // mib rows of 1 MiB
+      printf("{\"op\":\"malloc3d\",\"mib\":%zu,\"rc\":%d}\n", mib, (int)rc);
+      if (rc == hipSuccess) bufs.push_back(pp.ptr);
+    } else if (!strcmp(c, "arrayfree")) {
+      int bad = 0;
+      for (size_t k = 0; k < g_arrays.size(); ++k) {
+        hipError_t rc = g_array_kind[k] == 0   ? hipFreeArray((hipArray_t)g_arrays[k])
+                        : g_array_kind[k] == 1 ? hipArrayDestroy((hipArray_t)g_arrays[k])
+                                               : hipFreeMipmappedArray((hipMipmappedArray_t)g_arrays[k]);
+        bad += rc != hipSuccess;
+      }
+      g_arrays.clear();
+      g_array_kind.clear();
+      printf("{\"op\":\"arrayfree\",\"errors\":%d}\n", bad);
+    } else if (!strcmp(c, "modload") || !strcmp(c, "moddata") || !strcmp(c, "moddataex")) {
+      const char* path = argv[++i];
+      hipModule_t m = nullptr;
+      hipError_t rc;
+      if (!strcmp(c, "modload")) {
+        rc = hipModuleLoad(&m, path);
+      } else {
+        std::vector<char> img = read_file(path);
+        rc = !strcmp(c, "moddata") ? hipModuleLoadData(&m, img.data())
+                                   : hipModuleLoadDataEx(&m, img.data(), 0, nullptr, nullptr);
+      }
+      printf("{\"op\":\"%s\",\"rc\":%d}\n", c, (int)rc);
+      if (rc == hipSuccess) g_modules.push_back(m);
+    } else if (!strcmp(c, "modunload")) {
+      int bad = 0;
+      for (hipModule_t m : g_modules) bad += hipModuleUnload(m) != hipSuccess;
+      g_modules.clear();
+      printf("{\"op\":\"modunload\",\"errors\":%d}\n", bad);
+    } else if (!strcmp(c, "balance")) {
+      auto f = (int (*)(int, long long*, unsigned long long*))dlsym(RTLD_DEFAULT, "mivgpu_gate_balance");
+      long long t = 0;
+      unsigned long long r = 0;
+      int rc = f ? f(0, &t, &r) : -2;
+      printf("{\"op\":\"balance\",\"rc\":%d,\"tokens_ns\":%lld,\"received_ns\":%llu}\n", rc, t, r);
+    } else if (!strcmp(c, "getenv")) {
+      const char* k = argv[++i];
+      const char* v = getenv(k);
+      printf("{\"op\":\"getenv\",\"key\":\"%s\",\"set\":%d,\"value\":\"%s\"}\n", k, v ? 1 : 0, v ? v : "");
     } else if (!strcmp(c, "device")) {
       int d = atoi(argv[++i]);
       printf("{\"op\":\"device\",\"rc\":%d}\n", (int)hipSetDevice(d));

@@ -79,6 +79,9 @@ def main(argv=None):
     ap.add_argument("--device-core-scaling", type=float, default=1.0)
     ap.add_argument("--disable-core-limit", action="store_true")
     ap.add_argument("--hw-queues", type=int, default=2, help="GPU_MAX_HW_QUEUES for shared pods (0 = HIP default)")
+    ap.add_argument("--allow-tenant-opt-out", action="store_true",
+                    help="honour MIVGPU_DISABLE_CONTROL / GPU_CORE_UTILIZATION_POLICY=disable in the spec of "
+                         "fractional (shared) containers (default: only whole-GPU containers may opt out)")
     ap.add_argument("--hook-path", default=os.environ.get("HOOK_PATH", "/usr/local/vgpu"))
     ap.add_argument("--kubelet-socket", default=api.KUBELET_SOCKET)
     ap.add_argument("--socket-dir", default=api.DEVICE_PLUGIN_PATH)
@@ -102,7 +105,7 @@ def main(argv=None):
                        device_memory_scaling=a.device_memory_scaling, device_core_scaling=a.device_core_scaling,
                        disable_core_limit=a.disable_core_limit, log_level=a.log_level, hw_queues_shared=a.hw_queues,
                        enable_numa_topology=a.enable_numa_topology, node_name=a.node_name,
-                       device_list_strategy=a.device_list_strategy)
+                       device_list_strategy=a.device_list_strategy, allow_tenant_opt_out=a.allow_tenant_opt_out)
     cfg = apply_node_config(cfg, a.node_config, a.node_name)
     install_shim(a.hook_path)
     backend = detect(a.smi_backend)

@@ -81,6 +81,9 @@ IN_REQUEST_DEVICES: dict[str, str] = {}   # type -> "...-devices-to-allocate" an
 SUPPORT_DEVICES: dict[str, str] = {}      # type -> "...-devices-allocated" annotation
 DEVICES_TO_HANDLE: list[str] = []
 GPU_SCHEDULER_POLICY = [GPU_POLICY_SPREAD]  # mutable cell (config sets it)
+# bumped on every registry rebuild (config reload): caches of Fit results made
+# under the old backends (memory factor, CU topology, policies) key on it
+REGISTRY_GENERATION = [0]
 
 
 def get_devices() -> dict[str, Devices]:
@@ -91,7 +94,12 @@ def gpu_scheduler_policy() -> str:
     return GPU_SCHEDULER_POLICY[0]
 
 
+def registry_generation() -> int:
+    return REGISTRY_GENERATION[0]
+
+
 def reset_registry():
+    REGISTRY_GENERATION[0] += 1
     DEVICES_MAP.clear()
     IN_REQUEST_DEVICES.clear()
     SUPPORT_DEVICES.clear()

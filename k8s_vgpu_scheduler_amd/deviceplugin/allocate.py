@@ -8,11 +8,18 @@ docs/develop/amd-vgpu.md:47-104.  MI355X translation:
                               order (= container-local device index)
        HSA_CU_MASK            ``i:ranges;...`` for devices with a CU partition
        HIP_DEVICE_MEMORY_LIMIT_i  ``<MiB>m`` hard limit per local device
-       HIP_DEVICE_CORE_LIMIT  CU share in % (first device, for the governor)
+       HIP_DEVICE_CORE_LIMIT  CU share in % (first device; the reference's single
+                              CUDA_DEVICE_SM_LIMIT, server.go:837)
+       HIP_DEVICE_CORE_LIMIT_i  CU share in % of local device i (a container
+                              can hold a compute partition next to a whole GPU)
        GPU_MAX_HW_QUEUES      2 for shared (fractional) pods: HIP's default 4
                               queues/process oversubscribes the HW scheduler
                               when tenants share a GPU (measured, see
-                              profiles/README.md §2)
+                              profiles/README.md §2); part of the grant, so a
+                              tenant cannot raise it
+       HIP_TASK_PRIORITY, GPU_CORE_UTILIZATION_POLICY  from the container spec
+                              (the webhook writes them, device/amd/device.py),
+                              carried into the grant
        MIVGPU_SHARED_CACHE    $HOOK_PATH/vgpu/<uuid4>.cache
        MIVGPU_DEVICE_UUIDS, MIVGPU_OVERSUBSCRIBE, MIVGPU_LOG_LEVEL,
        GPU_CORE_UTILIZATION_POLICY=disable (with --disable-core-limit)
@@ -45,7 +52,9 @@ GRANT_KEYS = ("HIP_DEVICE_MEMORY_LIMIT", "HIP_DEVICE_CORE_LIMIT", "HSA_CU_MASK",
               "HIP_TASK_PRIORITY", "MIVGPU_OVERSUBSCRIBE", "MIVGPU_SHARED_CACHE", "MIVGPU_DEVICE_UUIDS",
               "ROCR_VISIBLE_DEVICES", "MIVGPU_ACCOUNT_CONTEXT", "MIVGPU_KFD_SYSFS", "MIVGPU_OCCUPANCY",
               "MIVGPU_OCC_PERIOD_US", "MIVGPU_GATE_INTERVAL_US", "MIVGPU_GATE_BURST_US", "MIVGPU_SHARE_TAU_MS",
-              "MIVGPU_DISABLE_CONTROL")
+              "MIVGPU_DISABLE_CONTROL", "GPU_MAX_HW_QUEUES")
+# per-device forms of grant keys (HIP_DEVICE_MEMORY_LIMIT_<i>, HIP_DEVICE_CORE_LIMIT_<i>)
+GRANT_PREFIXES = ("HIP_DEVICE_MEMORY_LIMIT_", "HIP_DEVICE_CORE_LIMIT_")
 
 
 def limits_host_path(hook_path: str, pod_uid: str, ctr_name: str) -> str:
@@ -54,7 +63,7 @@ def limits_host_path(hook_path: str, pod_uid: str, ctr_name: str) -> str:
 
 
 def grant_text(env: dict) -> str:
-    keys = [k for k in env if k in GRANT_KEYS or k.startswith("HIP_DEVICE_MEMORY_LIMIT_")]
+    keys = [k for k in env if k in GRANT_KEYS or k.startswith(GRANT_PREFIXES)]
     return "".join(f"{k}={env[k]}\n" for k in sorted(keys))
 
 
@@ -77,6 +86,11 @@ class PluginConfig:
     disable_core_limit: bool = False
     log_level: str = ""
     hw_queues_shared: int = 2
+    priority_resource: str = "amd.com/priority"
+    # a fractional (shared) container may opt itself out of enforcement
+    # (MIVGPU_DISABLE_CONTROL, GPU_CORE_UTILIZATION_POLICY=disable) only when
+    # the operator allows it; whole-GPU containers always may
+    allow_tenant_opt_out: bool = False
     pass_device_specs: bool = True
     enable_preferred_allocation: bool = True
     filter_uuids: tuple = ()
@@ -94,12 +108,34 @@ def _truthy(v) -> bool:
     return str(v).strip().lower() in ("1", "t", "true", "yes")
 
 
+def is_fractional(devreq: list, gpus: dict, cfg: PluginConfig) -> bool:
+    """True if the container shares any of its GPUs (a memory slice, a CU
+    share or a CU partition smaller than the device)."""
+    for d in devreq:
+        g = gpus.get(d.uuid)
+        total_cus = g.cus if g else 256
+        ranges = (d.custominfo or {}).get("cu_ranges")
+        if ranges and ranges_count(ranges) < total_cus:
+            return True
+        if g and d.usedmem < int(g.memory_mib * cfg.device_memory_scaling):
+            return True
+        if 0 < d.usedcores < total_cus or d.usedcores == 0:
+            return True
+    return False
+
+
+def _core_pct(d, gpus: dict) -> int:
+    g = gpus.get(d.uuid)
+    total = g.cus if g else 256
+    return 0 if d.usedcores == 0 else max(1, min(100, round(d.usedcores * 100 / total)))
+
+
 def container_env(devreq: list, gpus: dict, cfg: PluginConfig, cache_file: str) -> dict:
     """devreq: ContainerDevices of this container; gpus: uuid -> smi.GPUInfo."""
     env = {}
     rocr = []
     masks = []
-    shared = False
+    shared = is_fractional(devreq, gpus, cfg)
     for i, d in enumerate(devreq):
         g = gpus.get(d.uuid)
         rocr.append(g.rocr_id if g else d.uuid)
@@ -108,19 +144,15 @@ def container_env(devreq: list, gpus: dict, cfg: PluginConfig, cache_file: str) 
         ranges = (d.custominfo or {}).get("cu_ranges")
         if ranges and ranges_count(ranges) < total_cus:
             masks.append(f"{i}:{format_ranges(ranges)}")
-            shared = True
-        if g and d.usedmem < int(g.memory_mib * cfg.device_memory_scaling):
-            shared = True
-        if 0 < d.usedcores < total_cus or d.usedcores == 0:
-            shared = True
     env["ROCR_VISIBLE_DEVICES"] = ",".join(rocr)
     if masks:
         env["HSA_CU_MASK"] = ";".join(masks)
     if devreq:
-        g0 = gpus.get(devreq[0].uuid)
-        total0 = g0.cus if g0 else 256
-        pct = 0 if devreq[0].usedcores == 0 else max(1, min(100, round(devreq[0].usedcores * 100 / total0)))
-        env["HIP_DEVICE_CORE_LIMIT"] = str(pct)
+        pcts = [_core_pct(d, gpus) for d in devreq]
+        env["HIP_DEVICE_CORE_LIMIT"] = str(pcts[0])
+        if any(p != pcts[0] for p in pcts):
+            for i, p in enumerate(pcts):
+                env[f"HIP_DEVICE_CORE_LIMIT_{i}"] = str(p)
     env["MIVGPU_SHARED_CACHE"] = cache_file
     env["MIVGPU_DEVICE_UUIDS"] = ",".join(d.uuid for d in devreq)
     if cfg.device_memory_scaling > 1:
@@ -140,6 +172,9 @@ def allocate_container(pod: dict, ctr: dict, devreq: list, gpus: dict, cfg: Plug
     hook = cfg.hook_path
     cache_file = f"{hook}/vgpu/{_uuid.uuid4()}.cache"
     envs = container_env(devreq, gpus, cfg, cache_file)
+    spec = {e.get("name"): str(e.get("value", "")) for e in ctr.get("env") or [] if e.get("name")}
+    opt_out_ok = cfg.allow_tenant_opt_out or not is_fractional(devreq, gpus, cfg)
+    envs.update(_spec_policy(ctr, spec, cfg, opt_out_ok))
     uid = (pod.get("metadata") or {}).get("uid", "")
     host_dir = f"{hook}/vgpu/containers/{uid}_{ctr.get('name', '')}"
     limits = limits_host_path(hook, uid, ctr.get("name", ""))
@@ -162,8 +197,10 @@ def allocate_container(pod: dict, ctr: dict, devreq: list, gpus: dict, cfg: Plug
         {"container_path": f"{hook}/vgpu", "host_path": host_dir, "read_only": False},
         {"container_path": LIMITS_PATH, "host_path": limits, "read_only": True},
     ]
-    disabled = any(e.get("name") == "MIVGPU_DISABLE_CONTROL" and _truthy(e.get("value", ""))
-                   for e in ctr.get("env") or [])
+    # the pod-spec opt-out drops the preload -- only where opting out is allowed
+    # (a fractional pod would otherwise escape every limit; the webhook also
+    # denies it, scheduler/webhook.py, this covers pods that bypassed it)
+    disabled = opt_out_ok and _truthy(spec.get("MIVGPU_DISABLE_CONTROL", ""))
     if not disabled:
         mounts.append({"container_path": "/etc/ld.so.preload", "host_path": f"{hook}/vgpu/ld.so.preload",
                        "read_only": True})
@@ -190,6 +227,40 @@ def allocate_container(pod: dict, ctr: dict, devreq: list, gpus: dict, cfg: Plug
     elif cfg.device_list_strategy == "cdi-annotations":
         from k8s_vgpu_scheduler_amd.deviceplugin.cdi import annotation_key
         out["annotations"] = {annotation_key(ctr.get("name", "")): ",".join(cdi_names)}
+    return out
+
+
+def _spec_policy(ctr: dict, spec: dict, cfg: PluginConfig, opt_out_ok: bool) -> dict:
+    """Priority and core policy of the container, for the grant.
+
+    The webhook writes both into the container spec (HIP_TASK_PRIORITY from
+    the ``amd.com/priority`` resource, GPU_CORE_UTILIZATION_POLICY from the
+    device config, device/amd/device.py:mutate_admission); the shim takes
+    them from the grant file alone, so they must be carried into it.  The
+    priority resource is the authority (a forged env cannot raise a
+    container's priority); policy ``disable`` only where opting out is
+    allowed; ``--disable-core-limit`` wins."""
+    out = {}
+    lim = ((ctr.get("resources") or {}).get("limits") or {}).get(cfg.priority_resource)
+    prio = None
+    if lim is not None:
+        try:
+            prio = int(str(lim))
+        except ValueError:
+            prio = None
+    if prio is None and "HIP_TASK_PRIORITY" in spec:
+        try:
+            # without the resource a container may lower its priority, never raise it
+            prio = max(1, int(spec["HIP_TASK_PRIORITY"]))
+        except ValueError:
+            prio = None
+    if prio is not None:
+        out["HIP_TASK_PRIORITY"] = str(prio)
+    pol = spec.get("GPU_CORE_UTILIZATION_POLICY", "").strip().lower()
+    if cfg.disable_core_limit:
+        out["GPU_CORE_UTILIZATION_POLICY"] = "disable"
+    elif pol in ("force", "default") or (pol == "disable" and opt_out_ok):
+        out["GPU_CORE_UTILIZATION_POLICY"] = pol
     return out
 
 

@@ -125,9 +125,16 @@ def expected_region(grant: dict) -> dict:
         prio = int(grant.get("HIP_TASK_PRIORITY", "1"))
     except ValueError:
         prio = 1
+    cores = []
+    for i in range(MAX_DEVICES):
+        try:
+            ci = int(grant.get(f"HIP_DEVICE_CORE_LIMIT_{i}", "0"))
+        except ValueError:
+            ci = 0
+        cores.append(ci if 1 <= ci <= 100 else core)
     return {"mem_limit": [parse_size(grant.get(f"HIP_DEVICE_MEMORY_LIMIT_{i}")) or allmem
                           for i in range(MAX_DEVICES)],
-            "cu_limit": core, "cu_mask": [mask_count(grant.get("HSA_CU_MASK"), i) for i in range(MAX_DEVICES)],
+            "cu_limit": cores, "cu_mask": [mask_count(grant.get("HSA_CU_MASK"), i) for i in range(MAX_DEVICES)],
             "core_policy": pol, "priority": prio}
 
 
@@ -150,7 +157,7 @@ def reconcile_limits(lister: ContainerLister) -> int:
         want = expected_region(grant)
         r = c.region.r
         for i in range(c.region.device_num()):
-            for field, val in (("mem_limit", want["mem_limit"][i]), ("cu_limit", want["cu_limit"]),
+            for field, val in (("mem_limit", want["mem_limit"][i]), ("cu_limit", want["cu_limit"][i]),
                                ("cu_mask_count", want["cu_mask"][i])):
                 arr = getattr(r, field)
                 if int(arr[i]) != val:

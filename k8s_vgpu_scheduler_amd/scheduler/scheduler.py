@@ -128,6 +128,12 @@ class Scheduler:
         # request) would otherwise both fit against the same free capacity and
         # over-commit a GPU (tests/test_filter_concurrency.py)
         self._decide_mu = threading.Lock()
+        # Filters of the SAME pod (an extender-timeout retry, two scheduler
+        # profiles) run one at a time from decide through the annotation patch
+        # and its rollback: otherwise a rollback could delete the
+        # other Filter's live reservation, or the patches land out of order
+        self._pod_serial_mu = threading.Lock()
+        self._pod_serial: dict[str, list] = {}   # uid -> [lock, users]
         self.memo_hits = 0
         self.memo_misses = 0
         self.memo_class_hits = 0
@@ -479,7 +485,7 @@ class Scheduler:
         failure: dict[str, list] = {}
         failed: dict[str, str] = {}
         sig = (fit_signature(pod), D.gpu_scheduler_policy(), self.cfg.node_scheduler_policy,
-               tuple(id(d) for d in D.get_devices().values()),   # a config reload re-creates the backends
+               D.registry_generation(),   # a config reload re-creates the backends (ids may be reused)
                self.quota_manager.fit_key((pod.get("metadata") or {}).get("namespace", "default")))
         # UUID selectors name concrete devices: equal-shaped nodes stop being interchangeable
         annos = annotations(pod)
@@ -624,8 +630,24 @@ class Scheduler:
             return {"NodeNames": node_names, "FailedNodes": None, "Error": ""}
         if nodes is not None:
             return self._filter_simulation(pod, nodes, reqs)
+        uid = (pod.get("metadata") or {}).get("uid") or \
+            f"{(pod.get('metadata') or {}).get('namespace', '')}/{(pod.get('metadata') or {}).get('name', '')}"
+        with self._pod_serial_mu:
+            ent = self._pod_serial.setdefault(uid, [threading.Lock(), 0])
+            ent[1] += 1
+        ent[0].acquire()
+        try:
+            return self._filter_one(pod, node_names, reqs)
+        finally:
+            ent[0].release()
+            with self._pod_serial_mu:
+                ent[1] -= 1
+                if ent[1] == 0:
+                    self._pod_serial.pop(uid, None)
+
+    def _filter_one(self, pod: dict, node_names, reqs) -> dict:
         # decide and commit to the caches under the lock; the API writes
-        # (events, the allocation patch) happen outside it
+        # (events, the allocation patch) happen outside it, serialised per pod
         with self._decide_mu:
             d = self._decide(pod, node_names, reqs)
         if d["best"] is None:
@@ -641,9 +663,13 @@ class Scheduler:
         except Exception as e:  # noqa: BLE001
             self.events.filter_result(pod, E.FILTERING_FAILED, "", e)
             with self._decide_mu:
-                if d["added"]:
-                    self.quota_manager.rm_usage(pod, d["eff"])
-                self.pod_manager.del_pod(pod)
+                # roll back only this decision's reservation (an informer event
+                # may have replaced it in the meantime)
+                cur = self.pod_manager.get_pod(pod)
+                if cur is not None and cur.node_id == best.node_id and cur.devices == d["eff"]:
+                    if d["added"]:
+                        self.quota_manager.rm_usage(pod, d["eff"])
+                    self.pod_manager.del_pod(pod)
             return {"Error": str(e)}
         msg = (f"find fit node({best.node_id}), {len(node_names or []) - len(scores.node_list)} nodes not fit, "
                f"{len(scores.node_list)} nodes fit("

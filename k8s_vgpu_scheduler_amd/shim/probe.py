@@ -197,6 +197,243 @@ def child_region(args) -> dict:
     return out
 
 
+def _launch_count() -> int:
+    """Launches the preloaded shim has seen in this process (-1 without it)."""
+    import ctypes
+
+    try:
+        fn = ctypes.CDLL(None).mivgpu_launch_count
+    except AttributeError:
+        return -1
+    fn.restype = ctypes.c_ulonglong
+    return int(fn())
+
+
+def child_triton(args) -> dict:
+    """A @triton.jit matmul loop: Triton resolves every HIP entry point at run
+    time (dlopen + dlsym("hipGetProcAddress") + hipGetProcAddress), the path
+    that bypassed PLT interposition before round 3."""
+    import torch
+    import triton
+    import triton.language as tl
+
+    @triton.jit
+    def mm_kernel(a, b, c, M, N, K, BM: tl.constexpr, BN: tl.constexpr, BK: tl.constexpr):
+        pid_m = tl.program_id(0)
+        pid_n = tl.program_id(1)
+        rm = pid_m * BM + tl.arange(0, BM)
+        rn = pid_n * BN + tl.arange(0, BN)
+        rk = tl.arange(0, BK)
+        acc = tl.zeros((BM, BN), dtype=tl.float32)
+        for k0 in range(0, K, BK):
+            x = tl.load(a + rm[:, None] * K + (k0 + rk)[None, :])
+            y = tl.load(b + (k0 + rk)[:, None] * N + rn[None, :])
+            acc += tl.dot(x, y)
+        tl.store(c + rm[:, None] * N + rn[None, :], acc.to(tl.bfloat16))
+
+    n = args.n
+    a = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
+    c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
+    grid = (n // 128, n // 128)
+
+    def step():
+        mm_kernel[grid](a, b, c, n, n, n, BM=128, BN=128, BK=64, num_warps=4)
+
+    step()
+    torch.cuda.synchronize()
+    ref = (a[:64].float() @ b.float())[:, :64]
+    err = ((c[:64, :64].float() - ref).abs().max() / ref.abs().max()).item()
+    l0 = _launch_count()
+    dt = _timed(step, args.iters)
+    launches = _launch_count() - l0 if l0 >= 0 else -1
+    res = {"mode": "triton", "tflops": 2 * n ** 3 * args.iters / dt / 1e12, "seconds": dt, "rel_err": err,
+           "shim_launches": launches, "iters": args.iters}
+    res.update(gate_stats())
+    return res
+
+
+def child_compile(args) -> dict:
+    """A torch.compile'd MLP whose GEMMs and epilogues are Inductor-generated
+    Triton kernels (max-autotune, Triton GEMM backend only), launched through
+    Triton's run-time-resolved HIP entry points."""
+    import torch
+    import torch._inductor.config as ic
+
+    ic.max_autotune = True
+    ic.max_autotune_gemm_backends = "TRITON"
+    ic.max_autotune_gemm_search_space = "DEFAULT"
+    ic.coordinate_descent_tuning = False
+    d, h, m = 4096, 8192, args.n
+    w1 = torch.randn(d, h, device="cuda", dtype=torch.bfloat16) * d ** -0.5
+    w2 = torch.randn(h, d, device="cuda", dtype=torch.bfloat16) * h ** -0.5
+    x = torch.randn(m, d, device="cuda", dtype=torch.bfloat16)
+
+    def mlp(x):
+        return torch.nn.functional.gelu(x @ w1) @ w2 + x
+
+    f = torch.compile(mlp)
+    y = f(x)
+    torch.cuda.synchronize()
+    ref = mlp(x)
+    err = ((y.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
+    l0 = _launch_count()
+    dt = _timed(lambda: f(x), args.iters)
+    launches = _launch_count() - l0 if l0 >= 0 else -1
+    res = {"mode": "compile", "tflops": 2 * m * d * h * 2 * args.iters / dt / 1e12, "seconds": dt,
+           "rel_err": err, "shim_launches": launches, "iters": args.iters}
+    res.update(gate_stats())
+    return res
+
+
+def _hip_runtime_path() -> str:
+    """Path of the libamdhip64 the process has mapped (PyTorch's copy)."""
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if "libamdhip64.so" in line:
+                return line.split()[-1]
+    raise RuntimeError("libamdhip64 not mapped")
+
+
+def child_lookup(args) -> dict:
+    """HIP allocators reached by run-time lookup from Python -- ctypes dlsym
+    on the runtime's handle, hipGetProcAddress, and the array / 3D allocators
+    -- past the container's grant."""
+    import ctypes
+
+    import torch
+
+    torch.zeros(1, device="cuda")                 # runtime up, context created
+    lib = ctypes.CDLL(_hip_runtime_path(), mode=os.RTLD_NOLOAD | os.RTLD_LAZY)
+    big = args.oom_probe_mib << 20
+    out = {"mode": "lookup"}
+    p = ctypes.c_void_p()
+    malloc = lib.hipMalloc                         # dlsym(handle, "hipMalloc")
+    malloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    out["dlsym_big_rc"] = malloc(ctypes.byref(p), big)
+    out["dlsym_small_rc"] = malloc(ctypes.byref(p), 256 << 20)
+    if out["dlsym_small_rc"] == 0:
+        lib.hipFree(p)
+    gpa = lib.hipGetProcAddress
+    gpa.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p]
+    fp = ctypes.c_void_p()
+    out["gpa_rc"] = gpa(b"hipMalloc", ctypes.byref(fp), 700, 0, None)
+    fmalloc = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t)(fp.value)
+    out["gpa_big_rc"] = fmalloc(ctypes.byref(p), big)
+    out["gpa_is_hook"] = fp.value == ctypes.cast(ctypes.CDLL(None).hipMalloc, ctypes.c_void_p).value
+
+    class Extent(ctypes.Structure):
+        _fields_ = [("width", ctypes.c_size_t), ("height", ctypes.c_size_t), ("depth", ctypes.c_size_t)]
+
+    class PitchedPtr(ctypes.Structure):
+        _fields_ = [("ptr", ctypes.c_void_p), ("pitch", ctypes.c_size_t), ("xsize", ctypes.c_size_t),
+                    ("ysize", ctypes.c_size_t)]
+
+    class ChannelDesc(ctypes.Structure):
+        _fields_ = [("x", ctypes.c_int), ("y", ctypes.c_int), ("z", ctypes.c_int), ("w", ctypes.c_int),
+                    ("f", ctypes.c_int)]
+
+    pp = PitchedPtr()
+    m3 = lib.hipMalloc3D
+    m3.argtypes = [ctypes.POINTER(PitchedPtr), Extent]
+    rows = big // (64 << 10)
+    out["malloc3d_big_rc"] = m3(ctypes.byref(pp), Extent(64 << 10, rows, 1))
+    out["malloc3d_small_rc"] = m3(ctypes.byref(pp), Extent(64 << 10, 4096, 1))       # 256 MiB
+    if out["malloc3d_small_rc"] == 0:
+        lib.hipFree(ctypes.c_void_p(pp.ptr))
+    # a 2D float4 array of 8192 x 8192 x 16 B = 1 GiB while only 0.5 GiB of the slice is free
+    free, total = torch.cuda.mem_get_info()
+    hold = torch.empty(max(free - (512 << 20), 1), dtype=torch.uint8, device="cuda")
+    arr = ctypes.c_void_p()
+    ma = lib.hipMallocArray
+    ma.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ChannelDesc), ctypes.c_size_t, ctypes.c_size_t,
+                   ctypes.c_uint]
+    desc = ChannelDesc(32, 32, 32, 32, 2)          # float4
+    out["array_rc"] = ma(ctypes.byref(arr), ctypes.byref(desc), 8192, 8192, 0)
+    if out["array_rc"] == 0:
+        lib.hipFreeArray(arr)
+    del hold
+    free, total = torch.cuda.mem_get_info()
+    out["mem_total_mib"] = total >> 20
+    return out
+
+
+def child_module(args) -> dict:
+    """hipModuleLoadData of a gfx950 code object (the governor kernel's offload
+    bundle): its load span is charged as `module` bytes, and context + module
+    + buffer + vmm is still KFD's per-process VRAM."""
+    import ctypes
+
+    import torch
+
+    from k8s_vgpu_scheduler_amd.monitor.region import SharedRegion
+    from k8s_vgpu_scheduler_amd.utils import build as b
+
+    x = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
+    lib = ctypes.CDLL(_hip_runtime_path(), mode=os.RTLD_NOLOAD | os.RTLD_LAZY)
+    img = ctypes.create_string_buffer(b.GOV_HSACO.read_bytes())
+    mods = []
+    for _ in range(max(1, args.iters)):
+        m = ctypes.c_void_p()
+        rc = lib.hipModuleLoadData(ctypes.byref(m), img)
+        if rc != 0:
+            return {"mode": "module", "load_rc": rc}
+        mods.append(m)
+    torch.cuda.synchronize()
+    time.sleep(0.05)
+    torch.cuda.mem_get_info()                     # refresh the context charge
+    reg = SharedRegion(os.environ["MIVGPU_SHARED_CACHE"], writable=False)
+    me = [p for p in reg.active_procs() if p.pid == os.getpid()][0]
+    kfd = Path("/sys/class/kfd/kfd/proc") / str(me.hostpid or os.getpid())
+    kfd_vram = sum(int(f.read_text()) for f in kfd.glob("vram_*")) if kfd.is_dir() else -1
+    u = me.used[0]
+    out = {"mode": "module", "load_rc": 0, "modules": len(mods), "module": u.module, "context": u.context,
+           "buffer": u.buffer, "vmm": u.vmm, "total": u.total, "kfd_vram": kfd_vram}
+    reg.close()
+    for m in mods:
+        lib.hipModuleUnload(m)
+    reg = SharedRegion(os.environ["MIVGPU_SHARED_CACHE"], writable=False)
+    out["module_after_unload"] = [p for p in reg.active_procs() if p.pid == os.getpid()][0].used[0].module
+    reg.close()
+    del x
+    return out
+
+
+def child_queues(args) -> dict:
+    """A tenant that raises GPU_MAX_HW_QUEUES before HIP starts, then spreads
+    work over 8 streams: how many KFD hardware queues does it own?"""
+    if not args.keep_env:
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
+    import torch
+
+    streams = [torch.cuda.Stream() for _ in range(8)]
+    x = torch.ones(1 << 20, device="cuda")
+    for s in streams:
+        with torch.cuda.stream(s):
+            for _ in range(4):
+                x.add_(1)
+    torch.cuda.synchronize()
+    pid = os.getpid()
+    try:
+        from k8s_vgpu_scheduler_amd.monitor.region import SharedRegion
+
+        reg = SharedRegion(os.environ["MIVGPU_SHARED_CACHE"], writable=False)
+        me = [p for p in reg.active_procs() if p.pid == pid]
+        if me and me[0].hostpid:
+            pid = me[0].hostpid
+        reg.close()
+    except (KeyError, OSError, IndexError):
+        pass
+    qdir = Path("/sys/class/kfd/kfd/proc") / str(pid) / "queues"
+    out = {"mode": "queues", "kfd_queues": len(os.listdir(qdir)) if qdir.is_dir() else -1,
+           "env_seen_by_python": os.environ.get("GPU_MAX_HW_QUEUES"), "pid": pid}
+    if out["kfd_queues"] < 0:
+        procs = Path("/sys/class/kfd/kfd/proc")
+        out["kfd_procs"] = sorted(os.listdir(procs)) if procs.is_dir() else None
+        out["own_entry"] = sorted(os.listdir(procs / str(pid))) if (procs / str(pid)).is_dir() else None
+    return out
+
+
 def run_child(mode: str, env_extra: dict, shim: bool, extra_args=(), timeout=300) -> dict:
     env = dict(os.environ)
     if shim:
@@ -252,6 +489,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--hwid", action="store_true")
+    ap.add_argument("--keep-env", action="store_true", help="child queues: do not raise GPU_MAX_HW_QUEUES")
     ap.add_argument("--hostile", action="store_true",
                     help="child: rewrite the grant in the environment before the runtime starts "
                          "(all CUs, 200 GiB, control disabled) -- the grant file must still win")
@@ -264,7 +502,8 @@ def main():
     if args.child:
         fn = {"matmul": child_matmul, "stream": child_stream, "hwid": child_hwid,
               "region": child_region, "mfma": child_mfma, "hipstream": child_hipstream,
-              "light": child_light}[args.child]
+              "light": child_light, "triton": child_triton, "compile": child_compile, "lookup": child_lookup,
+              "module": child_module, "queues": child_queues}[args.child]
         print(json.dumps(fn(args)), flush=True)
         return
     tmp = Path(os.environ.get("TMPDIR", "/tmp")) / f"mivgpu-probe-{os.getpid()}"

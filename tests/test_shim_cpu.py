@@ -439,3 +439,33 @@ def test_governor_host_path_on_the_mock(native_build, tmp_path):
     n = sum(1 for l in lines if l.startswith("mark mivgpu:gate dev=0"))
     assert n >= 2000 // 256 and gates >= 1, (n, gates)
     assert all("charge=wall" in l for l in lines if l.startswith("mark mivgpu:gate"))   # no KFD view
+
+
+@pytest.mark.parametrize("own,peer,limit,trend", [
+    (30, 0, 25, "debt"),        # alone: receives the whole GPU at a 25 % limit -> in debt
+    (10, 30, 25, "full"),       # co-resident with a 3x heavier peer: receives 25 % = its limit
+    (10, 90, 25, "full"),       # receives 10 % < 25 %: nothing charged beyond the refill
+    (0, 50, 25, "full"),        # queued, no waves resident: charged nothing
+])
+def test_host_bucket_charges_the_share_received(native_build, tmp_path, own, peer, limit, trend):
+    """Host-bucket mode: the sampler charges the GPU time
+    the process actually receives -- own / (own + others) resident waves,
+    integrated every sample -- against rate x wall time; co-resident or queued
+    time is not charged as exclusive.  The gates (run on the host by the mock)
+    only read the balance."""
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
+    _occ(kfd, 987654, 4242, own)
+    if peer:
+        _occ(kfd, 111, 4242, peer)
+    env = dict(_kfd_env(kfd), HIP_DEVICE_CORE_LIMIT=str(limit), GPU_CORE_UTILIZATION_POLICY="force",
+               MOCKHIP_GOVERNOR="1", MIVGPU_GATE_BURST_US="100000")
+    out = run(native_build, tmp_path, "kfdctx", 0, "alloc", 100, "launch", 300, "sleep", 600, "launch", 10,
+              "balance", env=env, cache=f"hb{own}_{peer}.cache")
+    bal = out[-1]
+    assert bal["rc"] == 0, bal
+    if trend == "debt":
+        assert bal["tokens_ns"] < -50_000_000, bal          # 0.6 s at 75 % over the limit: -100 ms bound
+    else:
+        assert bal["tokens_ns"] >= 95_000_000, bal           # stays at the 100 ms burst
+    # the integral of the received share
+    assert bal["received_ns"] <= 0.75e9 * own / max(1, own + peer) + 1e7, bal

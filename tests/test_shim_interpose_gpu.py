@@ -1,0 +1,116 @@
+"""Run-time-resolved HIP entry points under libmivgpu.so on an MI355X
+(VERDICT r2 "do this" #1, #4c, #6).
+
+Triton (and torch.compile/Inductor, which generates Triton kernels) resolves
+every HIP function through dlopen + dlsym("hipGetProcAddress") +
+hipGetProcAddress; ctypes resolves through dlsym.  Before round 3 those paths
+bypassed every hook: no governor gate, no launch count, no HBM verdict.  The
+bounds are those of test_heavy_tenant_held_to_its_share_next_to_light_neighbours
+(tests/test_shim_gpu.py).
+"""
+
+import json
+import os
+import tempfile
+
+import pytest
+
+from k8s_vgpu_scheduler_amd.shim.probe import run_child
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def tmp():
+    from k8s_vgpu_scheduler_amd.utils import build
+    if not build.SHIM_SO.exists():
+        build.build_all()
+    return tempfile.mkdtemp(prefix="mivgpu-interpose-")
+
+
+GOVERNED_25 = {"HIP_DEVICE_CORE_LIMIT": "25", "GPU_CORE_UTILIZATION_POLICY": "force"}
+
+
+def test_triton_kernel_loop_held_to_its_share(tmp):
+    """(a) a @triton.jit matmul loop at 25 %, policy force: 0.18-0.30 of its
+    unthrottled rate, and every Triton launch counted by the shim."""
+    args = ["--n", "8192", "--iters", "600"]
+    free = run_child("triton", {"MIVGPU_SHARED_CACHE": os.path.join(tmp, "tf.cache")}, True, args, timeout=600)
+    gov = run_child("triton", {"MIVGPU_SHARED_CACHE": os.path.join(tmp, "tg.cache"), **GOVERNED_25}, True, args,
+                    timeout=600)
+    assert free["rc"] == 0 and gov["rc"] == 0, (free.get("stderr"), gov.get("stderr"))
+    ratio = gov["tflops"] / free["tflops"]
+    print(json.dumps({"unthrottled_tflops": round(free["tflops"], 1), "governed_tflops": round(gov["tflops"], 1),
+                      "ratio": round(ratio, 3), "launches": gov["shim_launches"], "gates": gov.get("gates"),
+                      "held_ms": gov.get("gate_held_ms"), "rel_err": gov["rel_err"]}))
+    assert free["rel_err"] < 2e-2
+    assert free["shim_launches"] >= 601 and gov["shim_launches"] >= 601     # warm-up + timed loop
+    assert gov["gates"] > 0 and gov["gate_held_ms"] > 0
+    assert 0.18 <= ratio <= 0.30, ratio
+
+
+def test_torch_compile_mlp_held_to_its_share(tmp):
+    """(b) a torch.compile'd MLP (Inductor Triton GEMMs + epilogues) obeys the
+    same bound."""
+    args = ["--n", "8192", "--iters", "400"]
+    free = run_child("compile", {"MIVGPU_SHARED_CACHE": os.path.join(tmp, "cf.cache")}, True, args, timeout=900)
+    gov = run_child("compile", {"MIVGPU_SHARED_CACHE": os.path.join(tmp, "cg.cache"), **GOVERNED_25}, True, args,
+                    timeout=900)
+    assert free["rc"] == 0 and gov["rc"] == 0, (free.get("stderr"), gov.get("stderr"))
+    ratio = gov["tflops"] / free["tflops"]
+    print(json.dumps({"unthrottled_tflops": round(free["tflops"], 1), "governed_tflops": round(gov["tflops"], 1),
+                      "ratio": round(ratio, 3), "launches": gov["shim_launches"], "gates": gov.get("gates"),
+                      "rel_err": gov["rel_err"]}))
+    assert free["rel_err"] < 5e-2
+    assert gov["shim_launches"] >= 400
+    assert 0.18 <= ratio <= 0.30, ratio
+
+
+def test_run_time_resolved_allocators_held_to_the_grant(tmp):
+    """(c)+(d) a 5000 MiB hipMalloc through ctypes dlsym and through
+    hipGetProcAddress, and a hipMalloc3D of the same size, all past a 4 GiB
+    grant: hipErrorOutOfMemory (2); smaller ones succeed; a 1 GiB
+    hipMallocArray with 0.5 GiB of the slice left: OOM."""
+    r = run_child("lookup", {"MIVGPU_SHARED_CACHE": os.path.join(tmp, "lk.cache"),
+                             "HIP_DEVICE_MEMORY_LIMIT_0": "4096m"}, True, ["--oom-probe-mib", "5000"])
+    assert r["rc"] == 0, r.get("stderr")
+    print(json.dumps(r))
+    assert r["mem_total_mib"] == 4096
+    assert r["dlsym_big_rc"] == 2 and r["dlsym_small_rc"] == 0
+    assert r["gpa_rc"] == 0 and r["gpa_is_hook"] and r["gpa_big_rc"] == 2
+    assert r["malloc3d_big_rc"] == 2 and r["malloc3d_small_rc"] == 0
+    assert r["array_rc"] == 2
+
+
+def test_module_bytes_reported_and_kfd_split_exact(tmp):
+    """Code objects loaded with hipModuleLoadData are charged as module bytes
+    (hami_vgpu_memory_module_bytes > 0); context + module + buffer + vmm is
+    still KFD's per-process VRAM."""
+    cache = os.path.join(tmp, "mod.cache")
+    r = run_child("module", {"MIVGPU_SHARED_CACHE": cache, "HIP_DEVICE_MEMORY_LIMIT_0": "8192m"}, True,
+                  ["--iters", "4"])
+    assert r["rc"] == 0 and r["load_rc"] == 0, r
+    print(json.dumps(r))
+    assert r["module"] > 0 and r["module_after_unload"] == 0
+    assert r["total"] == r["context"] + r["module"] + r["buffer"] + r["vmm"]
+    assert abs(r["total"] - r["kfd_vram"]) <= 64 << 20
+
+
+def test_granted_queue_cap_holds_against_the_tenant(tmp):
+    """(4c) a tenant that exports GPU_MAX_HW_QUEUES=8 before importing torch
+    and spreads work over 8 streams still owns at most the 2 hardware queues
+    of its grant; without a grant file the same tenant gets more."""
+    grant = os.path.join(tmp, "q.conf")
+    with open(grant, "w") as f:
+        f.write(f"GPU_MAX_HW_QUEUES=2\nMIVGPU_SHARED_CACHE={os.path.join(tmp, 'q.cache')}\n")
+    capped = run_child("queues", {"MIVGPU_LIMITS_FILE": grant, "GPU_MAX_HW_QUEUES": "2"}, True, [])
+    free = run_child("queues", {"MIVGPU_SHARED_CACHE": os.path.join(tmp, "qf.cache"), "GPU_MAX_HW_QUEUES": "2"},
+                     True, [])
+    # the same process obeying its cap: the queue count a 2-queue tenant has
+    honest = run_child("queues", {"MIVGPU_SHARED_CACHE": os.path.join(tmp, "qh.cache"), "GPU_MAX_HW_QUEUES": "2"},
+                       True, ["--keep-env"])
+    assert capped["rc"] == 0 and free["rc"] == 0 and honest["rc"] == 0, (capped.get("stderr"), free.get("stderr"))
+    print(json.dumps({"granted": capped, "ungranted": free, "honest": honest}))
+    assert capped["env_seen_by_python"] == "8"
+    assert 1 <= capped["kfd_queues"] <= honest["kfd_queues"], (capped, honest)
+    assert free["kfd_queues"] > honest["kfd_queues"], (free, honest)
