@@ -83,6 +83,11 @@ def main():
                     help="GPU_MAX_HW_QUEUES per slice in the shim round (0 = HIP default)")
     ap.add_argument("--child-env", action="append", default=[], metavar="K=V",
                     help="extra environment for every slice process (experiments)")
+    ap.add_argument("--gov-steps", type=int, default=600,
+                    help="decode steps of the two governor rounds (one unthrottled slice, then the same slice "
+                         "held to --gov-limit %%): >= 2 s of GPU work whatever --steps is, so the 100 ms burst "
+                         "is amortised (0 = skip)")
+    ap.add_argument("--gov-limit", type=int, default=25, help="core limit (%%) of the governed round")
     ap.add_argument("--no-collectives", action="store_true",
                     help="skip the untimed all-reduce check between the bench ranks (N > 1)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
@@ -136,7 +141,24 @@ def main():
             wanted = [r for r in wanted if r not in ("masked_noshim", "temporal")]
         if args.slices <= 1 or not args.hw_queues:
             wanted = [r for r in wanted if r != "native_hip_default"]
+    # The governor must HOLD in the driver-timed bench:
+    # four symmetric 25 % tenants get 25 % each without it, so two extra
+    # rounds time one slice alone on the whole GPU, unthrottled and then held
+    # to --gov-limit % (policy force, no CU mask), over --gov-steps steps.
+    if args.gov_steps > 0 and args.mode == "all" and not args.rounds and not cpu:
+        wanted += ["governed_ref", "governed"]
+    gov_args = list(child_args)
+    gov_args[gov_args.index("--steps") + 1] = str(max(args.gov_steps, args.steps))
     rounds = []
+    if "governed_ref" in wanted:
+        rounds.append(("governed_ref", spawn_round(
+            with_env(plan_slices(1, shim=True, gpumem_mib=args.gpumem_mib, spatial=False)),
+            phys, work / "gref", log_dir, gov_args, "governed_ref")))
+    if "governed" in wanted:
+        gspec = plan_slices(1, shim=True, gpumem_mib=args.gpumem_mib, spatial=False, policy="force")
+        gspec[0].core_pct = args.gov_limit
+        rounds.append(("governed", spawn_round(with_env(gspec), phys, work / "gov", log_dir, gov_args,
+                                               "governed")))
     if "shim" in wanted:
         rounds.append(("shim", spawn_round(
             with_env(plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib,
@@ -294,6 +316,16 @@ def main():
         for nm in ("shim", "temporal"):
             if nm in results and "monitor" in results[nm]:
                 out[f"{nm}_monitor"] = results[nm]["monitor"]
+        if "governed" in results and "governed_ref" in results:
+            g, ref = results["governed"], results["governed_ref"]
+            gd = g["done"][0]
+            out["governor_enforcement"] = {
+                "limit_pct": args.gov_limit, "policy": "force", "steps": max(args.gov_steps, args.steps),
+                "unthrottled_tok_s": round(ref["tok_s"], 1), "governed_tok_s": round(g["tok_s"], 1),
+                "fraction_of_unthrottled": round(g["tok_s"] / ref["tok_s"], 4),
+                "unthrottled_gpu_s": round(ref["max_wall_s"], 3), "governed_wall_s": round(g["max_wall_s"], 3),
+                "held_ms": gd.get("gov_held_ms"), "gates": gd.get("gov_gates"),
+                "busy_share_pct": gd.get("busy_share_pct"), "received_gpu_ms": gd.get("received_gpu_ms")}
         if "native_hip_default" in results:
             nd = results["native_hip_default"]["tok_s"]
             out["native_hip_default_queues_value"] = round(nd, 2)

@@ -253,6 +253,7 @@ def child_main(argv):
     # per-step completion events: time per output token (TPOT) of this slice
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
     torch.cuda.synchronize()
+    rx0 = _received_ns()
     t_start = time.time()
     t0 = time.perf_counter()
     evs[0].record()
@@ -266,9 +267,31 @@ def child_main(argv):
             "t_start": t_start, "t_end": t_start + dt,
             "tpot_ms_p50": tpot[len(tpot) // 2],
             "tpot_ms_p99": tpot[min(len(tpot) - 1, int(0.99 * len(tpot)))]}
+    rx1 = _received_ns()
+    if rx0 is not None and rx1 is not None:
+        # GPU time the slice received over the timed steps (the governor's
+        # share integral), as a share of the wall time
+        done["received_gpu_ms"] = round((rx1 - rx0) / 1e6, 1)
+        done["busy_share_pct"] = round(100.0 * (rx1 - rx0) / 1e9 / dt, 2)
     done.update(_governor_stats())
     print("DONE " + json.dumps(done), flush=True)
     return 0
+
+
+def _received_ns():
+    """The shim's share integral on device 0 (ns of GPU time received), or
+    None without a host bucket."""
+    import ctypes
+    if not os.environ.get("LD_PRELOAD"):
+        return None
+    try:
+        fn = ctypes.CDLL(None).mivgpu_gate_balance
+    except (OSError, AttributeError):
+        return None
+    t, r = ctypes.c_longlong(), ctypes.c_ulonglong()
+    if fn(0, ctypes.byref(t), ctypes.byref(r)) != 0:
+        return None
+    return r.value
 
 
 def _governor_stats() -> dict:

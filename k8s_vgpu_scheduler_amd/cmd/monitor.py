@@ -5,7 +5,9 @@ HOOK_PATH, watches this node's pods only (server-side field selector
 spec.nodeName, pkg/monitor/nvidia/cudevshr.go:308) for the container lister,
 samples KFD wave occupancy, serves Prometheus (``--legacy-metrics`` adds the
 pre-2.x series), and runs the 5 s feedback loop -- paused while the device
-plugin holds the compute-partition apply lock (main.go:79-109).
+plugin holds the compute-partition apply lock (main.go:79-109).  Each pass
+also restores every container's HBM usage from KFD host truth and blocks a
+container over its grant (monitor/hosttruth.py).
 """
 
 from __future__ import annotations
@@ -38,6 +40,8 @@ def main(argv=None):
                     help="also export the pre-2.x metric names (HostGPUMemoryUsage, vGPU_device_memory_*, ...)")
     ap.add_argument("--occupancy-period", type=float, default=0.05,
                     help="seconds between KFD wave-occupancy samples (0 = off)")
+    ap.add_argument("--no-host-truth", action="store_true",
+                    help="do not recompute container HBM usage from KFD each pass (trust the shared regions)")
     ap.add_argument("-v", type=int, default=2)
     a = ap.parse_args(argv)
     setup_logging(a.v)
@@ -55,14 +59,20 @@ def main(argv=None):
         log.warning("no amd-smi backend (%s): host metrics disabled", e)
         backend = None
     occ = OccupancySampler(period_s=a.occupancy_period).start() if a.occupancy_period > 0 else None
+    truth = None
+    if not a.no_host_truth:
+        from k8s_vgpu_scheduler_amd.monitor.hosttruth import HostTruth, kfd_gpu_ids
+        from k8s_vgpu_scheduler_amd.scheduler.events import EventRecorder
+        truth = HostTruth(kfd_gpu_ids(backend), events=EventRecorder(client, component="hami-vgpu-monitor"))
     reg = CollectorRegistry()
-    reg.register(MonitorCollector(lister, backend, a.node_name, occupancy=occ, legacy=a.legacy_metrics))
+    reg.register(MonitorCollector(lister, backend, a.node_name, occupancy=occ, legacy=a.legacy_metrics,
+                                  truth=truth))
     host, _, port = a.metrics_bind_address.rpartition(":")
     start_http_server(int(port), addr=host or "0.0.0.0", registry=reg)
     stop = threading.Event()
     pause = threading.Event()
     threading.Thread(target=watch_partition_lock, args=(pause, stop), name="partition-lock", daemon=True).start()
-    watch_and_feedback(lister, stop, pause=pause)
+    watch_and_feedback(lister, stop, pause=pause, truth=truth)
     return 0
 
 

@@ -47,7 +47,10 @@ def check_priority(ut: dict, p: int, c) -> bool:
     return False
 
 
-def observe(lister: ContainerLister):
+def observe(lister: ContainerLister, over: set | None = None):
+    """``over``: (pod_uid, container) keys the host-truth pass found over
+    their HBM grant (hosttruth.py): they stay blocked whatever the
+    priorities say."""
     ut: dict[str, list[int]] = {}
     cs = lister.list_containers()
     for c in cs:
@@ -67,7 +70,10 @@ def observe(lister: ContainerLister):
         p = c.region.priority()
         rk = c.region.recent_kernel()
         sw = c.region.utilization_switch()
-        if check_blocking(ut, p, c):
+        if over and (c.pod_uid, c.container) in over:
+            if rk >= 0:
+                c.region.set_recent_kernel(-1)
+        elif check_blocking(ut, p, c):
             if rk >= 0:
                 c.region.set_recent_kernel(-1)
         elif rk < 0:
@@ -174,17 +180,30 @@ def reconcile_limits(lister: ContainerLister) -> int:
     return fixed
 
 
+def feedback_pass(lister: ContainerLister, truth=None) -> dict:
+    """One pass: map host pids, restore the limits from the grants, restore
+    the usage from host truth (hosttruth.HostTruth, optional), then the
+    priority feedback."""
+    lister.update()
+    fill_host_pids(lister.list_containers())
+    fixed = reconcile_limits(lister)
+    over = set()
+    if truth is not None:
+        from .hosttruth import grants_from_files
+        truth.enforce(lister, grants_from_files(lister))
+        over = truth.snapshot()[1]
+    ut = observe(lister, over)
+    return {"limits_fixed": fixed, "over": over, "util": ut}
+
+
 def watch_and_feedback(lister: ContainerLister, stop: threading.Event, period: float = 5.0,
-                       pause: threading.Event | None = None):
+                       pause: threading.Event | None = None, truth=None):
     """The 5 s loop; skipped while ``pause`` is set (a compute-partition apply
     is in progress, cmd/vGPUmonitor/main.go:79-109)."""
     while not stop.wait(period):
         if pause is not None and pause.is_set():
             continue
         try:
-            lister.update()
-            fill_host_pids(lister.list_containers())
-            reconcile_limits(lister)
-            observe(lister)
+            feedback_pass(lister, truth)
         except Exception:  # noqa: BLE001
             log.exception("feedback iteration failed")

@@ -27,8 +27,10 @@ LEGACY_HOST_LABELS = ["nodeid", "deviceidx", "deviceuuid", "devicetype"]
 
 
 class MonitorCollector:
-    def __init__(self, lister, backend=None, node_name: str = "", occupancy=None, legacy: bool = False):
+    def __init__(self, lister, backend=None, node_name: str = "", occupancy=None, legacy: bool = False,
+                 truth=None):
         self.lister = lister
+        self.truth = truth        # monitor.hosttruth.HostTruth (host-truth HBM usage) or None
         self.backend = backend
         self.node = node_name
         self.occ = occupancy      # monitor.occupancy.OccupancySampler (hostPID view) or None
@@ -108,6 +110,14 @@ class MonitorCollector:
                                  "of hami_mig_device_info)",
                                  labels=CTR_LABELS + ["compute_partition", "memory_partition", "partition_index",
                                                       "physical_index", "cus"])
+        host_b = GaugeMetricFamily("mivgpu_container_memory_host_bytes",
+                                   "Container device memory from host truth (KFD per-process VRAM of the pod's "
+                                   "processes), independent of the tenant-writable shared region",
+                                   labels=CTR_LABELS)
+        over_g = GaugeMetricFamily("mivgpu_container_memory_over_grant",
+                                   "1 while the container's host-truth HBM exceeds its grant (launches blocked)",
+                                   labels=CTR_LABELS)
+        truth, over = self.truth.snapshot() if self.truth is not None else ({}, set())
         l_used = GaugeMetricFamily("vGPU_device_memory_usage_in_bytes", "vGPU device usage", labels=LEGACY_CTR_LABELS)
         l_limit = GaugeMetricFamily("vGPU_device_memory_limit_in_bytes", "vGPU device limit",
                                     labels=LEGACY_CTR_LABELS)
@@ -158,7 +168,13 @@ class MonitorCollector:
                 if any(p.util[i].share_ppm for p in procs):
                     share.add_metric(lab, min(100.0, sum(p.util[i].share_ppm for p in procs) / 1e4))
                 occw.add_metric(lab, float(sum(p.util[i].occupancy for p in procs)))
+                tb = truth.get((c.pod_uid, c.container, i))
+                if tb is not None:
+                    host_b.add_metric(lab, float(tb))
+                    over_g.add_metric(lab, 1.0 if (c.pod_uid, c.container) in over else 0.0)
         yield from (used, limit, dmem, dutil, lastk, ctx, mod, buf, busy, held, cumask, part, share, occw)
+        if self.truth is not None:
+            yield from (host_b, over_g)
         if self.legacy:
             yield from (l_used, l_limit, l_desc, l_cutil, l_lastk)
 

@@ -434,6 +434,46 @@ def child_queues(args) -> dict:
     return out
 
 
+def child_tamper(args) -> dict:
+    """A hostile tenant: rewrites its own shared region (zeroes dev_used and
+    its slot totals, raises mem_limit to 1 TiB), allocates past its grant,
+    then -- after the parent ran one monitor pass -- tries again."""
+    import torch
+
+    from k8s_vgpu_scheduler_amd.monitor.region import SharedRegion
+
+    x = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    reg = SharedRegion(args.out)
+    reg.r.dev_used[0] = 0
+    reg.r.mem_limit[0] = 1 << 40
+    for p in reg.active_procs():
+        p.used[0].total = 0
+        p.used[0].buffer = 0
+    y = None
+    try:
+        y = torch.empty(args.oom_probe_mib << 20, dtype=torch.uint8, device="cuda")
+        y.fill_(1)
+        torch.cuda.synchronize()
+        first = "allocated"
+    except torch.OutOfMemoryError:
+        first = "oom"
+    print("TAMPERED " + json.dumps({"first": first}), flush=True)
+    sys.stdin.readline()                      # the parent's monitor pass
+    rk = int(reg.r.recent_kernel)
+    try:
+        z = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
+        second = "allocated"
+        del z
+    except torch.OutOfMemoryError:
+        second = "oom"
+    out = {"mode": "tamper", "first": first, "second": second, "recent_kernel": rk,
+           "mem_limit_mib": int(reg.r.mem_limit[0]) >> 20, "dev_used_mib": int(reg.r.dev_used[0]) >> 20}
+    reg.r.recent_kernel = 0                   # let the exit path run
+    reg.close()
+    del x, y
+    return out
+
+
 def run_child(mode: str, env_extra: dict, shim: bool, extra_args=(), timeout=300) -> dict:
     env = dict(os.environ)
     if shim:
@@ -503,7 +543,7 @@ def main():
         fn = {"matmul": child_matmul, "stream": child_stream, "hwid": child_hwid,
               "region": child_region, "mfma": child_mfma, "hipstream": child_hipstream,
               "light": child_light, "triton": child_triton, "compile": child_compile, "lookup": child_lookup,
-              "module": child_module, "queues": child_queues}[args.child]
+              "module": child_module, "queues": child_queues, "tamper": child_tamper}[args.child]
         print(json.dumps(fn(args)), flush=True)
         return
     tmp = Path(os.environ.get("TMPDIR", "/tmp")) / f"mivgpu-probe-{os.getpid()}"
