@@ -17,9 +17,9 @@
 //     many CUs the device plugin gave the container through HSA_CU_MASK (0 = no
 //     spatial mask), which decides whether the temporal governor has to run.
 //
-// Layout is pinned by tests/test_shared_region_abi.py against
-// k8s_vgpu_scheduler_amd/monitor/region.py (ctypes mirror) via the exported
-// mivgpu_abi_offsetof() of libmivgpu.so.
+// Layout is pinned by tests/test_shim_cpu.py::test_abi_offsets_match_c_layout
+// against k8s_vgpu_scheduler_amd/monitor/region.py (ctypes mirror) via the
+// exported mivgpu_abi_offsetof() of libmivgpu.so.
 #ifndef MIVGPU_SHARED_REGION_H
 #define MIVGPU_SHARED_REGION_H
 

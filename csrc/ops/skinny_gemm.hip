@@ -108,13 +108,7 @@ __device__ __forceinline__ void load_kblock(Frag<MT, NT>& f, const u32x4_t* __re
   for (int m = 0; m < MT; ++m) {
     const u32x4_t* src = (const u32x4_t*)(xrow[m] + kb * 64);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-#ifdef MIVGPU_SKINNY_NOX_EXPERIMENT  // throughput experiment only: X from registers, results meaningless
-      f.a[m][j] = (u32x4_t){(unsigned)kb, (unsigned)j, (unsigned)m, (unsigned)(uintptr_t)src};
-#else
-      f.a[m][j] = src[j];
-#endif
-    }
+    for (int j = 0; j < 4; ++j) f.a[m][j] = src[j];
   }
 }
 
@@ -137,13 +131,7 @@ __device__ __forceinline__ void load_x_kblock(Frag<MT, NT>& f, const bf16_t* con
   for (int m = 0; m < MT; ++m) {
     const u32x4_t* src = (const u32x4_t*)(xrow[m] + kb * 64);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-#ifdef MIVGPU_SKINNY_NOX_EXPERIMENT
-      f.a[m][j] = (u32x4_t){(unsigned)kb, (unsigned)j, (unsigned)m, (unsigned)(uintptr_t)src};
-#else
-      f.a[m][j] = src[j];
-#endif
-    }
+    for (int j = 0; j < 4; ++j) f.a[m][j] = src[j];
   }
 }
 
