@@ -34,6 +34,7 @@
 //   modunload          hipModuleUnload every module
 //   getenv <KEY>       getenv as the runtime would call it
 //   balance            the governor's host-bucket balance on device 0
+//   launchfor <ms>     hipLaunchKernel every 100 us for <ms> (a busy tenant)
 //   stress <threads> <iters> <max MiB>
 //                    threads doing random hipMalloc/hipFree and
 //                    hipMemCreate/hipMemRelease, one kernel launch per
@@ -45,6 +46,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -339,6 +341,20 @@ int main(int argc, char** argv) {
       for (hipModule_t m : g_modules) bad += hipModuleUnload(m) != hipSuccess;
       g_modules.clear();
       printf("{\"op\":\"modunload\",\"errors\":%d}\n", bad);
+    } else if (!strcmp(c, "launchfor")) {
+      // launch back to back for <ms> milliseconds (a busy tenant)
+      const long ms = strtol(argv[++i], nullptr, 10);
+      static char dummy;
+      struct timespec t0, t;
+      clock_gettime(CLOCK_MONOTONIC, &t0);
+      long n = 0;
+      do {
+        (void)hipLaunchKernel(&dummy, dim3(1), dim3(64), nullptr, 0, nullptr);
+        ++n;
+        usleep(100);
+        clock_gettime(CLOCK_MONOTONIC, &t);
+      } while ((t.tv_sec - t0.tv_sec) * 1000 + (t.tv_nsec - t0.tv_nsec) / 1000000 < ms);
+      printf("{\"op\":\"launchfor\",\"n\":%ld}\n", n);
     } else if (!strcmp(c, "balance")) {
       auto f = (int (*)(int, long long*, unsigned long long*))dlsym(RTLD_DEFAULT, "mivgpu_gate_balance");
       long long t = 0;

@@ -1497,7 +1497,18 @@ struct OccDev {
   double win_start_share = 0;
   bool bucket = false;         // host bucket started (the device's gate is up)
   double tokens_ns = 0;        // host bucket balance: rate x wall time - GPU time received
+  uint64_t batch_win_ns = 0;   // batch-size estimate window (host mode)
+  uint64_t batch_win_launches = 0;
+  double batch_win_share = 0;
+  double ns_per_launch = 0;    // GPU time received per launch (EWMA)
 };
+// Background stamper idle threshold and the batch bounds (see stamper_main
+// and maybe_gate below).
+constexpr uint64_t kStampIdleNs = 1000000;  // 1 ms
+constexpr int kMaxBatchLaunches = 256;
+// Host mode: launches per batch sized by the sampler to ~2 ms of GPU time.
+std::atomic<int> g_batch_max[MIVGPU_MAX_DEVICES];
+
 // Heap-allocated and never freed: the sampler thread is detached, and a
 // static array's destructor at exit would free the peer vectors under it.
 OccDev* const g_occ = new OccDev[MIVGPU_MAX_DEVICES];
@@ -1583,7 +1594,26 @@ bool occ_sample(int dev, uint64_t now) {
       if ((int64_t)__atomic_load_n(&hs[kHsHoldEnd + i], __ATOMIC_RELAXED) > now_dev) ++holding;
     own = own > holding ? own - holding : 0;
   }
-  double share = own > 0 ? (double)own / (double)(own + others) : 0.0;
+  // Busy: the streams still owe GPU work -- a gate enqueued that has not run
+  // (every batch is closed by the next launch's gate or the idle stamper),
+  // or a launch within the stamper's idle window.
+  bool pending = false;
+  const uint64_t since_launch = coarse_ns() - g_last_launch_ns.load(std::memory_order_relaxed);
+  if (hs) {
+    const uint64_t done = __atomic_load_n(&hs[2], __ATOMIC_RELAXED);
+    pending = G.enqueued.load(std::memory_order_acquire) > done || since_launch < 2 * kStampIdleNs;
+  } else {
+    pending = since_launch < 5000000ull;
+  }
+  // The share of the GPU received at this instant: own / all resident waves;
+  // alone and busy with no wave resident (dispatch gaps, barrier and event
+  // packets between kernels -- a decode step is hundreds of small kernels)
+  // the GPU is still serving this process alone, so that time is its too
+  // (measured: without this a governed decode slice ran at 0.32 of its
+  // unthrottled rate at a 25 % limit).  Held by its own gate: nothing.
+  double share = 0.0;
+  if (own > 0) share = (double)own / (double)(own + others);
+  else if (holding == 0 && others == 0 && pending) share = 1.0;
   const int mask = (int)__atomic_load_n(&g_region->cu_mask_count[dev], __ATOMIC_RELAXED);
   if (mask > 0) {
     const double f = (double)mask / (double)device_cus(dev);
@@ -1613,21 +1643,25 @@ bool occ_sample(int dev, uint64_t now) {
     __atomic_store_n(reinterpret_cast<int64_t*>(const_cast<uint64_t*>(&hs[kHsHostTokens])), (int64_t)o.tokens_ns,
                      __ATOMIC_RELAXED);
   }
-  // Contending = waves resident, or work queued behind others: a gate has
-  // been enqueued that has not run yet (every batch is closed by a gate, so
-  // the GPU still owes this process work).  A sample taken while the
-  // governor itself holds the process says nothing about contention and is
-  // skipped.  (A "launched within the last few ms" test instead missed the
-  // queued time of graph replays, biasing the share up by the fraction of
-  // time the process waits: 8 governed slices collapsed into running one at
-  // a time, 3.4-3.8k tok/s.)
-  bool pending = false;
-  if (hs) {
-    const uint64_t done = __atomic_load_n(&hs[2], __ATOMIC_RELAXED);
-    pending = G.enqueued.load(std::memory_order_acquire) > done;
-  } else {
-    pending = coarse_ns() - g_last_launch_ns.load(std::memory_order_relaxed) < 5000000ull;
+  // Host mode: size the batches between gates to ~2 ms of GPU time from the
+  // GPU time received per launch (a gate is a few us; a batch of 256 long
+  // kernels -- a Triton GEMM loop -- was ~300 ms, far coarser than a 25 ms hold)
+  if (hs && now - o.batch_win_ns >= 20000000ull) {
+    const uint64_t l = g_launches_local.load(std::memory_order_relaxed);
+    if (o.batch_win_ns && l > o.batch_win_launches) {
+      const double per = (o.share_ns - o.batch_win_share) / (double)(l - o.batch_win_launches);
+      o.ns_per_launch = o.ns_per_launch <= 0 ? per : 0.7 * o.ns_per_launch + 0.3 * per;
+      const double n = o.ns_per_launch > 0 ? 2e6 / o.ns_per_launch : (double)kMaxBatchLaunches;
+      g_batch_max[dev].store(n < 1 ? 1 : (n > kMaxBatchLaunches ? kMaxBatchLaunches : (int)n),
+                             std::memory_order_relaxed);
+    }
+    o.batch_win_ns = now;
+    o.batch_win_launches = l;
+    o.batch_win_share = o.share_ns;
   }
+  // Contending (for the reported share): waves resident, or work queued
+  // behind others; a sample taken while the governor holds the process says
+  // nothing about contention and is skipped.
   const bool contending = holding == 0 && (own > 0 || (others > 0 && pending));
   if (contending) {
     const double a = (double)dt / g_cfg.share_tau_ns < 1.0 ? (double)dt / g_cfg.share_tau_ns : 1.0;
@@ -1773,7 +1807,6 @@ int find_slot_locked(DeviceGate& G, hipStream_t stream, bool create, uint64_t no
 // pause (CPU work, library initialisation, data loading) is never charged to
 // the tenant as GPU-busy time.  Runs under G.mu, which hipStreamBeginCapture
 // also takes, so a stamp can never be captured into a user graph.
-constexpr uint64_t kStampIdleNs = 1000000;  // 1 ms
 void enqueue_gate_locked(int dev, DeviceGate& G, int slot, hipStream_t stream, uint64_t now);
 bool stream_capturing(hipStream_t stream);
 
@@ -1801,9 +1834,6 @@ void* stamper_main(void* arg) {
     Guard g;
     std::lock_guard<std::mutex> lk(G.mu);
     if (g_exiting.load(std::memory_order_acquire)) return nullptr;
-    // host-bucket mode charges the share actually received, so an idle gap
-    // costs nothing already: no closing gates needed
-    if (g_occ_live[dev].load(std::memory_order_acquire)) continue;
     const uint64_t now = mono_ns();
     for (int i = 0; i < 64; ++i) {
       GateSlot& S = G.slots[i];
@@ -1839,7 +1869,6 @@ void start_stamper_locked(int dev, DeviceGate& G) {
 // (the host can enqueue 100 ms of graph replays within the 200 us interval:
 // measured 66 % throughput at a 50 % limit).  Gate in front of every graph
 // launch and after at most kMaxBatchLaunches kernels, whatever the host time.
-constexpr int kMaxBatchLaunches = 256;
 
 // Returns the gate slot of `stream` (its in_launch count raised; the caller's
 // LaunchScope lowers it when the real launch call returns), or -1.
@@ -1859,7 +1888,12 @@ int maybe_gate(hipStream_t stream, bool graph, int dev) {
   S.in_launch.fetch_add(1, std::memory_order_relaxed);
   if (!G.stamper_started) start_stamper_locked(dev, G);
   const bool pending = S.first_submit_host_ns != 0;
-  if (!pending || S.last_gate_host_ns == 0 || graph || S.batch_launches >= kMaxBatchLaunches ||
+  int bmax = kMaxBatchLaunches;
+  if (g_occ_live[dev].load(std::memory_order_relaxed)) {
+    const int b = g_batch_max[dev].load(std::memory_order_relaxed);
+    bmax = b > 0 ? b : 16;
+  }
+  if (!pending || S.last_gate_host_ns == 0 || graph || S.batch_launches >= bmax ||
       now - S.last_gate_host_ns >= g_cfg.gate_min_interval_ns) {
     // Gate in front of this launch: settles the batch submitted since the
     // previous gate (if any); this launch starts the next batch.
@@ -1898,7 +1932,7 @@ void stamp_before_sync(hipStream_t stream, bool all_streams) {
   if (g_cfg.disabled || !g_region) return;
   int dev = current_device();
   DeviceGate& G = g_gates[dev];
-  if (!G.ok || g_occ_live[dev].load(std::memory_order_acquire)) return;   // host bucket: nothing to close
+  if (!G.ok) return;
   std::lock_guard<std::mutex> lk(G.mu);
   uint64_t now = mono_ns();
   for (int i = 0; i < 64; ++i) {

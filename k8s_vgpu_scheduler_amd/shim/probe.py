@@ -382,7 +382,7 @@ def child_module(args) -> dict:
     torch.cuda.synchronize()
     time.sleep(0.05)
     torch.cuda.mem_get_info()                     # refresh the context charge
-    reg = SharedRegion(os.environ["MIVGPU_SHARED_CACHE"], writable=False)
+    reg = SharedRegion(_region_path(), writable=False)
     me = [p for p in reg.active_procs() if p.pid == os.getpid()][0]
     kfd = Path("/sys/class/kfd/kfd/proc") / str(me.hostpid or os.getpid())
     kfd_vram = sum(int(f.read_text()) for f in kfd.glob("vram_*")) if kfd.is_dir() else -1
@@ -399,6 +399,35 @@ def child_module(args) -> dict:
     return out
 
 
+def _region_path() -> str | None:
+    """This process's shared region: the environment, else the grant file."""
+    path = os.environ.get("MIVGPU_SHARED_CACHE")
+    if path:
+        return path
+    grant = os.environ.get("MIVGPU_LIMITS_FILE")
+    if grant and os.path.exists(grant):
+        from k8s_vgpu_scheduler_amd.deviceplugin.allocate import parse_grant
+        return parse_grant(Path(grant).read_text()).get("MIVGPU_SHARED_CACHE")
+    return None
+
+
+def _kfd_pid(pid: int | None = None) -> int:
+    """KFD's name for a process (the host pid; the box may run us in a pid
+    namespace): the hostpid the shim found for itself and published in its
+    region slot, else the pid itself."""
+    pid = os.getpid() if pid is None else pid
+    path = _region_path()
+    if not path or not os.path.exists(path):
+        return pid
+    from k8s_vgpu_scheduler_amd.monitor.region import SharedRegion
+    reg = SharedRegion(path, writable=False)
+    try:
+        me = [p for p in reg.active_procs() if p.pid == pid]
+        return me[0].hostpid if me and me[0].hostpid else pid
+    finally:
+        reg.close()
+
+
 def child_queues(args) -> dict:
     """A tenant that raises GPU_MAX_HW_QUEUES before HIP starts, then spreads
     work over 8 streams: how many KFD hardware queues does it own?"""
@@ -413,17 +442,7 @@ def child_queues(args) -> dict:
             for _ in range(4):
                 x.add_(1)
     torch.cuda.synchronize()
-    pid = os.getpid()
-    try:
-        from k8s_vgpu_scheduler_amd.monitor.region import SharedRegion
-
-        reg = SharedRegion(os.environ["MIVGPU_SHARED_CACHE"], writable=False)
-        me = [p for p in reg.active_procs() if p.pid == pid]
-        if me and me[0].hostpid:
-            pid = me[0].hostpid
-        reg.close()
-    except (KeyError, OSError, IndexError):
-        pass
+    pid = _kfd_pid()
     qdir = Path("/sys/class/kfd/kfd/proc") / str(pid) / "queues"
     out = {"mode": "queues", "kfd_queues": len(os.listdir(qdir)) if qdir.is_dir() else -1,
            "env_seen_by_python": os.environ.get("GPU_MAX_HW_QUEUES"), "pid": pid}
@@ -457,7 +476,7 @@ def child_tamper(args) -> dict:
         first = "allocated"
     except torch.OutOfMemoryError:
         first = "oom"
-    print("TAMPERED " + json.dumps({"first": first}), flush=True)
+    print("TAMPERED " + json.dumps({"first": first, "kfd_pid": _kfd_pid()}), flush=True)
     sys.stdin.readline()                      # the parent's monitor pass
     rk = int(reg.r.recent_kernel)
     try:

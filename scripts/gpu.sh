@@ -7,6 +7,7 @@
 #   full        GPU test suite + smoke + default bench (all rounds)
 #   bench [N..] bench.py --slices N for each N (default 1 2 4 8), all rounds
 #   governor    governor GPU tests + bench (spatial, temporal, native rounds)
+#   interpose   run-time lookup / governor / tamper GPU tests + governed bench rounds
 #   busyshare   rocprofv3 busy share of governed tenants (scripts/probe/governor_busyshare.py)
 #   probes      KFD occupancy + topology probes (scripts/probe/*.py)
 #   kernels     rocprofv3 --kernel-trace --stats of one 64-CU slice decode step
@@ -42,6 +43,10 @@ case $suite in
     step 900 tests python -u -m pytest tests/test_shim_gpu.py -v -s --timeout 300 --timeout-method thread \
       -k "governor or temporal or masked or heavy or launch or grant"
     step 400 bench python -u bench.py --out "$out/bench.json" ;;
+  interpose)
+    step 900 tests python -u -m pytest tests/test_shim_interpose_gpu.py tests/test_shim_gpu.py -v -s --timeout 300 \
+      --timeout-method thread -k "interpose or governor or temporal or heavy or triton or compile or tamper or queue"
+    step 400 bench python -u bench.py --rounds governed_ref,governed,temporal --steps 100 --out "$out/bench.json" ;;
   busyshare)
     step 500 busyshare python -u scripts/probe/governor_busyshare.py ;;
   probes)

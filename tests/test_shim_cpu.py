@@ -441,13 +441,15 @@ def test_governor_host_path_on_the_mock(native_build, tmp_path):
     assert all("charge=wall" in l for l in lines if l.startswith("mark mivgpu:gate"))   # no KFD view
 
 
-@pytest.mark.parametrize("own,peer,limit,trend", [
-    (30, 0, 25, "debt"),        # alone: receives the whole GPU at a 25 % limit -> in debt
-    (10, 30, 25, "full"),       # co-resident with a 3x heavier peer: receives 25 % = its limit
-    (10, 90, 25, "full"),       # receives 10 % < 25 %: nothing charged beyond the refill
-    (0, 50, 25, "full"),        # queued, no waves resident: charged nothing
+@pytest.mark.parametrize("own,peer,limit,trend,busy", [
+    (30, 0, 25, "debt", False),   # alone: receives the whole GPU at a 25 % limit -> in debt
+    (10, 30, 25, "full", False),  # co-resident with a 3x heavier peer: receives 25 % = its limit
+    (10, 90, 25, "full", False),  # receives 10 % < 25 %: nothing charged beyond the refill
+    (0, 50, 25, "full", True),    # queued behind a peer, no waves resident: charged nothing
+    (0, 0, 25, "debt", True),     # alone and launching, no wave caught resident: still its GPU time
+    (0, 0, 25, "full", False),    # alone and idle: nothing
 ])
-def test_host_bucket_charges_the_share_received(native_build, tmp_path, own, peer, limit, trend):
+def test_host_bucket_charges_the_share_received(native_build, tmp_path, own, peer, limit, trend, busy):
     """Host-bucket mode: the sampler charges the GPU time
     the process actually receives -- own / (own + others) resident waves,
     integrated every sample -- against rate x wall time; co-resident or queued
@@ -459,8 +461,9 @@ def test_host_bucket_charges_the_share_received(native_build, tmp_path, own, pee
         _occ(kfd, 111, 4242, peer)
     env = dict(_kfd_env(kfd), HIP_DEVICE_CORE_LIMIT=str(limit), GPU_CORE_UTILIZATION_POLICY="force",
                MOCKHIP_GOVERNOR="1", MIVGPU_GATE_BURST_US="100000")
-    out = run(native_build, tmp_path, "kfdctx", 0, "alloc", 100, "launch", 300, "sleep", 600, "launch", 10,
-              "balance", env=env, cache=f"hb{own}_{peer}.cache")
+    work = ["launchfor", 600] if busy else ["sleep", 600]
+    out = run(native_build, tmp_path, "kfdctx", 0, "alloc", 100, "launch", 300, *work, "launch", 10,
+              "balance", env=env, cache=f"hb{own}_{peer}_{busy}.cache")
     bal = out[-1]
     assert bal["rc"] == 0, bal
     if trend == "debt":
@@ -468,4 +471,5 @@ def test_host_bucket_charges_the_share_received(native_build, tmp_path, own, pee
     else:
         assert bal["tokens_ns"] >= 95_000_000, bal           # stays at the 100 ms burst
     # the integral of the received share
-    assert bal["received_ns"] <= 0.75e9 * own / max(1, own + peer) + 1e7, bal
+    frac = own / (own + peer) if own else (1.0 if (busy and not peer) else 0.0)
+    assert bal["received_ns"] <= 0.75e9 * frac + 5e7, bal
