@@ -5,7 +5,10 @@
 // loop alone and for loop + drain.  Run natively, under libmivgpu.so with
 // the governor off, and with it on: the difference is what the shim adds to
 // a launch-bound eager workload.  Also times hipGraphLaunch of a captured
-// graph of 32 empty kernels (replay path).  Prints one JSON line.
+// graph of 32 empty kernels (replay path).  host_launch_ns: the same launches
+// queued behind a held stream in rounds of 512 -- the host's enqueue cost
+// alone (launch_ns is paced by the GPU's empty-kernel dispatch, ~2.9 us).
+// Prints one JSON line.
 //
 //   launch_bench [N=100000] [graph_replays=2000]
 #include <hip/hip_runtime.h>
@@ -25,6 +28,17 @@
 
 __global__ void __launch_bounds__(64) empty_kernel(int* p) {
   if (p && threadIdx.x == 0 && blockIdx.x == 0x7fffffff) *p = 1;  // never taken
+}
+
+// Holds the stream until the host raises *flag (or ~2 s pass: every wave
+// exits on its own), so the launches queued behind it measure the host's
+// enqueue cost alone -- no dispatch of the GPU paces the loop.
+__global__ void __launch_bounds__(64) hold_until(int* flag) {
+  if (threadIdx.x != 0) return;
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0 &&
+         (long long)__builtin_amdgcn_s_memrealtime() - t0 < 200000000ll)
+    __builtin_amdgcn_s_sleep(32);
 }
 
 static double now_ns() {
@@ -49,10 +63,28 @@ int main(int argc, char** argv) {
   double t2 = now_ns();
   CHECK(hipGetLastError());
 
+  // Host-bound: rounds of `chunk` launches queued behind a held stream (far
+  // below the queue's capacity, so no launch waits for a slot).
+  const long chunk = 512, rounds = n / chunk > 0 ? (n / chunk < 200 ? n / chunk : 200) : 1;
+  int* flag = nullptr;
+  CHECK(hipHostMalloc((void**)&flag, sizeof(int), hipHostMallocCoherent | hipHostMallocMapped));
+  double host_ns = 0;
+  for (long r = 0; r < rounds; ++r) {
+    __atomic_store_n(flag, 0, __ATOMIC_RELEASE);
+    hold_until<<<1, 64, 0, s>>>(flag);
+    double h0 = now_ns();
+    for (long i = 0; i < chunk; ++i) empty_kernel<<<1, 64, 0, s>>>(nullptr);
+    host_ns += now_ns() - h0;
+    __atomic_store_n(flag, 1, __ATOMIC_RELEASE);
+    CHECK(hipStreamSynchronize(s));
+  }
+  CHECK(hipHostFree(flag));
+  const double host_launch_ns = host_ns / (double)(rounds * chunk);
+
   if (getenv("LAUNCH_BENCH_NO_GRAPH")) {
     CHECK(hipStreamDestroy(s));
-    printf("{\"launches\": %ld, \"launch_ns\": %.1f, \"launch_drain_ns\": %.1f}\n", n, (t1 - t0) / n,
-           (t2 - t0) / n);
+    printf("{\"launches\": %ld, \"launch_ns\": %.1f, \"launch_drain_ns\": %.1f, \"host_launch_ns\": %.1f}\n", n,
+           (t1 - t0) / n, (t2 - t0) / n, host_launch_ns);
     return 0;
   }
   // graph replay: 32 empty kernels per graph
@@ -72,8 +104,8 @@ int main(int argc, char** argv) {
   CHECK(hipGraphExecDestroy(ge));
   CHECK(hipGraphDestroy(g));
   CHECK(hipStreamDestroy(s));
-  printf("{\"launches\": %ld, \"launch_ns\": %.1f, \"launch_drain_ns\": %.1f, \"graph_replays\": %ld, "
-         "\"graph_launch_ns\": %.1f, \"graph_drain_ns\": %.1f}\n",
-         n, (t1 - t0) / n, (t2 - t0) / n, replays, (g1 - g0) / replays, (g2 - g0) / replays);
+  printf("{\"launches\": %ld, \"launch_ns\": %.1f, \"launch_drain_ns\": %.1f, \"host_launch_ns\": %.1f, "
+         "\"graph_replays\": %ld, \"graph_launch_ns\": %.1f, \"graph_drain_ns\": %.1f}\n",
+         n, (t1 - t0) / n, (t2 - t0) / n, host_launch_ns, replays, (g1 - g0) / replays, (g2 - g0) / replays);
   return 0;
 }

@@ -33,6 +33,8 @@
 //                      file's bytes; moddataex <path>: hipModuleLoadDataEx
 //   modunload          hipModuleUnload every module
 //   getenv <KEY>       getenv as the runtime would call it
+//   envscan <KEY>      the KEY entry of environ, read directly (ROCclr's way)
+//   setenv|putenv <KEY> <VAL>, unsetenv <KEY>   a tenant rewriting its environment
 //   balance            the governor's host-bucket balance on device 0
 //   launchfor <ms>     hipLaunchKernel every 100 us for <ms> (a busy tenant)
 //   stress <threads> <iters> <max MiB>
@@ -50,6 +52,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <string>
 #include <random>
 #include <thread>
 #include <vector>
@@ -99,6 +102,8 @@ static void stress_thread(int seed, int iters, int max_mib, std::atomic<long>* a
 }
 
 extern "C" hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_tR0600*, int);
+
+extern char** environ;
 
 static void* hip_handle() {
   void* h = dlopen("libamdhip64.so", RTLD_NOW | RTLD_NOLOAD);
@@ -361,6 +366,27 @@ int main(int argc, char** argv) {
       unsigned long long r = 0;
       int rc = f ? f(0, &t, &r) : -2;
       printf("{\"op\":\"balance\",\"rc\":%d,\"tokens_ns\":%lld,\"received_ns\":%llu}\n", rc, t, r);
+    } else if (!strcmp(c, "setenv") || !strcmp(c, "putenv") || !strcmp(c, "unsetenv")) {
+      const char* k = argv[++i];
+      int rc;
+      if (!strcmp(c, "setenv")) {
+        rc = setenv(k, argv[++i], 1);
+      } else if (!strcmp(c, "putenv")) {
+        static std::vector<std::string> keep;      // putenv keeps the pointer
+        keep.emplace_back(std::string(k) + "=" + argv[++i]);
+        rc = putenv(const_cast<char*>(keep.back().c_str()));
+      } else {
+        rc = unsetenv(k);
+      }
+      printf("{\"op\":\"%s\",\"rc\":%d}\n", c, rc);
+    } else if (!strcmp(c, "envscan")) {
+      // what ROCclr does for its flags: walk environ itself
+      const char* k = argv[++i];
+      const size_t n = strlen(k);
+      const char* v = nullptr;
+      for (char** e = environ; e && *e; ++e)
+        if (!strncmp(*e, k, n) && (*e)[n] == '=') v = *e + n + 1;
+      printf("{\"op\":\"envscan\",\"key\":\"%s\",\"set\":%d,\"value\":\"%s\"}\n", k, v ? 1 : 0, v ? v : "");
     } else if (!strcmp(c, "getenv")) {
       const char* k = argv[++i];
       const char* v = getenv(k);

@@ -71,6 +71,14 @@ def gate_stats() -> dict:
         return {"gate": "inactive"}
     out = {"gate_busy_ms": b.value / 1e6, "gate_held_ms": h.value / 1e6, "gates": g.value}
     try:
+        bal = ctypes.CDLL(None).mivgpu_gate_balance
+        t, r = ctypes.c_longlong(), ctypes.c_ulonglong()
+        if bal(0, ctypes.byref(t), ctypes.byref(r)) == 0:
+            out["received_ms"] = r.value / 1e6       # the host bucket's share integral
+            out["tokens_ms"] = t.value / 1e6
+    except AttributeError:
+        pass
+    try:
         tr = ctypes.CDLL(None).mivgpu_gate_trace
         buf = (ctypes.c_longlong * (128 * 8))()
         n = tr(0, buf, 128)

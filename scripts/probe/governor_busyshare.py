@@ -70,8 +70,11 @@ def scenario(name, pct, lights, iters):
     res = json.loads(line)
     shares = busy_share(str(out_dir), skip_first_s=0.5)   # skip startup (first GEMMs, bucket's burst)
     heavy = max(shares.values(), key=lambda d: d["kernels"]) if shares else {}
+    if heavy.get("kernels"):
+        heavy["kernel_us_mean"] = round(1e3 * heavy["busy_ms"] / heavy["kernels"], 2)
     print(json.dumps({"scenario": name, "limit_pct": pct, "lights": lights, "rc": r.returncode,
                       "tflops": round(res.get("tflops", 0), 1), "gate_held_ms": res.get("gate_held_ms"),
+                      "received_ms": res.get("received_ms"), "seconds": res.get("seconds"),
                       "trace": heavy}), flush=True)
     if r.returncode != 0:
         print(r.stderr[-2000:], file=sys.stderr)
@@ -79,6 +82,7 @@ def scenario(name, pct, lights, iters):
 
 
 if __name__ == "__main__":
+    scenario("heavy100_alone", 100, 0, 1000)    # unthrottled: the kernel duration to compare against
     scenario("heavy25_light3", 25, 3, 2000)
     scenario("heavy25_alone", 25, 0, 2000)
     scenario("heavy50_alone", 50, 0, 1500)

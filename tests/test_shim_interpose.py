@@ -282,13 +282,34 @@ def test_runtime_reads_the_granted_queue_cap_and_mask(native_build, tmp_path):
     assert out[0]["value"] == "8"
 
 
+def test_granted_values_are_in_environ_and_cannot_be_rewritten(native_build, tmp_path):
+    """ROCclr parses GPU_MAX_HW_QUEUES out of `environ` itself, not through
+    getenv: the shim writes the granted values into the environment when it
+    loads, and setenv / putenv / unsetenv cannot move them afterwards (a
+    tenant's os.environ[...] = before `import torch`); other keys are free."""
+    grant = tmp_path / "limits.conf"
+    grant.write_text("GPU_MAX_HW_QUEUES=2\nHSA_CU_MASK=0:0-63\n")
+    env = {"MIVGPU_LIMITS_FILE": str(grant), "GPU_MAX_HW_QUEUES": "8"}
+    out = run(native_build, tmp_path, "envscan", "GPU_MAX_HW_QUEUES", "setenv", "GPU_MAX_HW_QUEUES", "16",
+              "envscan", "GPU_MAX_HW_QUEUES", "putenv", "HSA_CU_MASK", "0:0-255", "envscan", "HSA_CU_MASK",
+              "unsetenv", "GPU_MAX_HW_QUEUES", "envscan", "GPU_MAX_HW_QUEUES", "setenv", "OTHER_KEY", "x",
+              "envscan", "OTHER_KEY", env=env)
+    scans = [o for o in out if o["op"] == "envscan"]
+    assert [s["value"] for s in scans] == ["2", "2", "0:0-63", "2", "x"], out
+    assert all(o["rc"] == 0 for o in out if o["op"] in ("setenv", "putenv", "unsetenv"))
+    # no grant file: the tenant's own environment
+    out = run(native_build, tmp_path, "setenv", "GPU_MAX_HW_QUEUES", "16", "envscan", "GPU_MAX_HW_QUEUES",
+              env={"GPU_MAX_HW_QUEUES": "8"}, cache="free.cache")
+    assert out[1]["value"] == "16"
+
+
 def test_shim_exports_the_lookup_interposers(native_build):
     """dlsym/dlvsym under both glibc versions callers bind to, getenv, and
     every new HIP hook under the runtime's version node."""
     syms = subprocess.run(["readelf", "--dyn-syms", "-W", str(native_build["shim"])], stdout=subprocess.PIPE,
                           text=True, check=True).stdout
     for s in ("dlsym@@GLIBC_2.34", "dlsym@GLIBC_2.2.5", "dlvsym@@GLIBC_2.34", "dlvsym@GLIBC_2.2.5",
-              "getenv@@GLIBC_2.2.5", "hipGetProcAddress@@hip_6.1", "hipLaunchKernelExC@@hip_6.5",
+              "getenv@@GLIBC_2.2.5", "setenv@@GLIBC_2.2.5", "putenv@@GLIBC_2.2.5", "unsetenv@@GLIBC_2.2.5", "hipGetProcAddress@@hip_6.1", "hipLaunchKernelExC@@hip_6.5",
               "hipDrvLaunchKernelEx@@hip_6.5", "hipLaunchCooperativeKernelMultiDevice@@hip_4.2",
               "hipExtLaunchMultiKernelMultiDevice@@hip_4.2", "hipMallocArray@@hip_4.2", "hipMalloc3D@@hip_4.2",
               "hipMalloc3DArray@@hip_4.2", "hipArrayCreate@@hip_4.2", "hipMipmappedArrayCreate@@hip_4.2",
