@@ -74,6 +74,8 @@ struct mivgpu_gate_host_stats {
   long long host_tokens_ns;      // HOST-written by the sampler: the bucket balance (host-bucket mode)
   mivgpu_gate_trace_entry trace[MIVGPU_GATE_TRACE];  // ring, index = gates % N
   long long hold_end_ns[MIVGPU_GATE_SLOTS];          // device ns at which a slot's hold ends
+  long long hold_start_ns[MIVGPU_GATE_SLOTS];        // device ns at which its latest hold began
+  long long held_cum_ns[MIVGPU_GATE_SLOTS];          // its completed holds, total ns
 };
 
 __device__ __forceinline__ long long rt_ns() {
@@ -120,22 +122,34 @@ __device__ __forceinline__ long long host_load(long long* p) {
 // following gates.  Time the process spends co-resident with other tenants is
 // charged at the share it got, and time it spends queued or idle is not
 // charged at all -- the sample-time bias of charging a whole batch at one
-// share estimate is gone.
+// share estimate is gone.  The gate publishes its holds
+// (start, end, running total per slot) so that the sampler takes the exact
+// held time out of each interval instead of classifying the interval by the
+// state it sees at the sample: releases follow the sampler's refills, so a
+// sample lands in the next hold far more often than in the batch between
+// (measured: 0.31 of the GPU at a 25 % limit before, the batches uncharged).
 __device__ void host_bucket_gate(mivgpu_gate_state* st, mivgpu_gate_host_stats* hs, int slot,
                                  long long max_hold_ns, unsigned int flags) {
   const long long t0 = rt_ns();
   long long tokens = host_load(&hs->host_tokens_ns);
   long long t = t0;
   if (tokens < 0) {
-    // "holding until at most" marker: the sampler discounts the gate's own
-    // resident wave while it sits here
-    __hip_atomic_store(&hs->hold_end_ns[slot], t0 + max_hold_ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // "holding since / until at most" markers: the sampler discounts the
+    // gate's own resident wave while it sits here, and takes the exact held
+    // time out of the interval it charges (start, then end: the sampler reads
+    // end, then start)
+    __hip_atomic_store(&hs->hold_start_ns[slot], t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&hs->hold_end_ns[slot], t0 + max_hold_ns, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     while (tokens < 0 && t < t0 + max_hold_ns) {
       for (int k = 0; k < 4; ++k) __builtin_amdgcn_s_sleep(127);   // ~14 us between host reads
       tokens = host_load(&hs->host_tokens_ns);
       t = rt_ns();
     }
+    // end, then the running total (the sampler reads the total first: a race
+    // can only delay a hold's count to its next sample, never count it twice)
     __hip_atomic_store(&hs->hold_end_ns[slot], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const long long cum = __hip_atomic_load(&hs->held_cum_ns[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&hs->held_cum_ns[slot], cum + (t - t0), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const long long hold = t - t0;
   const bool locked = gate_lock(st);

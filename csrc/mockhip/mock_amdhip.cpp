@@ -184,6 +184,30 @@ EXPORT hipError_t hipLaunchKernel(const void*, dim3, dim3, void**, size_t, hipSt
 // gating path -- enqueue, idle stamper, occupancy sampler -- runs on the CPU
 // (race tests under ThreadSanitizer).  Otherwise no code object loads.
 enum MockFn : uintptr_t { kNoFn = 0, kGateFn = 0x6a7e, kClockFn = 0xc10c };
+long long mono_now() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (long long)ts.tv_sec * 1000000000ll + ts.tv_nsec;
+}
+// MOCKHIP_GATE_HOLD=1: the gate holds like governor.hip host_bucket_gate
+// (the launching thread stands in for the stream): while the host bucket is
+// in debt, up to max_hold, publishing the same hold markers.
+void mock_host_bucket_hold(unsigned long long* hs, int slot, long long max_hold) {
+  long long* h = reinterpret_cast<long long*>(hs);
+  constexpr int kTokens = 7, kEnd = 8 + 128 * 8, kStart = kEnd + 64, kCum = kEnd + 128;
+  if (slot < 0 || slot >= 64 || __atomic_load_n(&h[kTokens], __ATOMIC_RELAXED) >= 0) return;
+  const long long t0 = mono_now();
+  long long t = t0;
+  __atomic_store_n(&h[kStart + slot], t0, __ATOMIC_RELAXED);
+  __atomic_store_n(&h[kEnd + slot], t0 + max_hold, __ATOMIC_RELEASE);
+  while (__atomic_load_n(&h[kTokens], __ATOMIC_RELAXED) < 0 && t < t0 + max_hold) {
+    usleep(20);
+    t = mono_now();
+  }
+  __atomic_store_n(&h[kEnd + slot], t, __ATOMIC_RELAXED);
+  __atomic_store_n(&h[kCum + slot], __atomic_load_n(&h[kCum + slot], __ATOMIC_RELAXED) + (t - t0), __ATOMIC_RELEASE);
+  __atomic_fetch_add(&hs[1], (unsigned long long)(t - t0), __ATOMIC_RELAXED);   // held_total_ns
+}
 bool mock_governor() { return getenv("MOCKHIP_GOVERNOR") != nullptr; }
 EXPORT hipError_t hipModuleLaunchKernel(hipFunction_t f, unsigned, unsigned, unsigned, unsigned,
                                         unsigned, unsigned, unsigned, hipStream_t, void** args, void**) {
@@ -196,6 +220,10 @@ EXPORT hipError_t hipModuleLaunchKernel(hipFunction_t f, unsigned, unsigned, uns
     __atomic_store_n(out, (long long)ts.tv_sec * 1000000000ll + ts.tv_nsec, __ATOMIC_RELEASE);
   } else if (fn == kGateFn && args) {
     unsigned long long* hs = *static_cast<unsigned long long**>(args[1]);
+    const int slot = *static_cast<int*>(args[3]);
+    const long long max_hold = *static_cast<long long*>(args[6]);
+    const unsigned flags = *static_cast<unsigned*>(args[8]);
+    if (hs && (flags & 2u) && getenv("MOCKHIP_GATE_HOLD")) mock_host_bucket_hold(hs, slot, max_hold);
     if (hs) __atomic_fetch_add(&hs[2], 1ull, __ATOMIC_ACQ_REL);   // gates done
   }
   return hipSuccess;

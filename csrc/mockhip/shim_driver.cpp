@@ -365,7 +365,12 @@ int main(int argc, char** argv) {
       long long t = 0;
       unsigned long long r = 0;
       int rc = f ? f(0, &t, &r) : -2;
-      printf("{\"op\":\"balance\",\"rc\":%d,\"tokens_ns\":%lld,\"received_ns\":%llu}\n", rc, t, r);
+      auto st = (int (*)(int, unsigned long long*, unsigned long long*, unsigned long long*))dlsym(
+          RTLD_DEFAULT, "mivgpu_gate_stats");
+      unsigned long long busy = 0, held = 0, gates = 0;
+      if (st) (void)st(0, &busy, &held, &gates);
+      printf("{\"op\":\"balance\",\"rc\":%d,\"tokens_ns\":%lld,\"received_ns\":%llu,\"held_ns\":%llu,"
+             "\"gates\":%llu}\n", rc, t, r, held, gates);
     } else if (!strcmp(c, "setenv") || !strcmp(c, "putenv") || !strcmp(c, "unsetenv")) {
       const char* k = argv[++i];
       int rc;

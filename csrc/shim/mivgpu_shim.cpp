@@ -1353,12 +1353,15 @@ std::atomic<uint64_t> g_last_kernel_write_ns{0};
 std::atomic<uint64_t> g_launches_local{0};
 
 // Governor (gate) per device.  Host stats = 8 counters + a 128-entry trace
-// ring of 8 x int64 per gate + 64 per-slot hold ends (layout: governor.hip
-// mivgpu_gate_host_stats; counter 6 is the sampler's measured share).
-constexpr size_t kHostStatsBytes = 64 + 128 * 64 + 64 * 8;
+// ring of 8 x int64 per gate + 64 per-slot hold ends, hold starts and held
+// totals (layout: governor.hip mivgpu_gate_host_stats; counter 6 is the
+// sampler's measured share).
+constexpr size_t kHostStatsBytes = 64 + 128 * 64 + 3 * 64 * 8;
 constexpr int kHsSharePpm = 6;          // u64 index of share_ppm (sampler -> gate)
 constexpr int kHsHostTokens = 7;        // u64 index of host_tokens_ns (sampler -> gate, host-bucket mode)
 constexpr int kHsHoldEnd = 8 + 128 * 8; // u64 index of hold_end_ns[0]
+constexpr int kHsHoldStart = kHsHoldEnd + 64;
+constexpr int kHsHeldCum = kHsHoldEnd + 128;
 // Written under G.mu; the launch fast path (maybe_gate) reads them lock-free.
 struct GateSlot {
   std::atomic<hipStream_t> stream;
@@ -1503,6 +1506,15 @@ struct OccDev {
   uint64_t batch_win_launches = 0;
   double batch_win_share = 0;
   double ns_per_launch = 0;    // GPU time received per launch (EWMA)
+  // wall time by sampler state (mivgpu_occ_states): own waves resident,
+  // alone + busy with none resident, held by its gate, others only, idle
+  double state_ns[5] = {0, 0, 0, 0, 0};
+  uint64_t samples = 0;
+  // exact held time (host mode): each slot's held total incl. a hold in
+  // progress at the previous sample, and the held time counted late (a hold
+  // published after its interval) carried into the next interval
+  int64_t held_prev[64] = {};
+  double held_carry = 0;
 };
 // Background stamper idle threshold and the batch bounds (see stamper_main
 // and maybe_gate below).
@@ -1590,10 +1602,25 @@ bool occ_sample(int dev, uint64_t now) {
   DeviceGate& G = g_gates[dev];
   const uint64_t* hs = static_cast<const uint64_t*>(G.hs_pub.load(std::memory_order_acquire));
   int holding = 0;
+  int64_t held_dt = 0;   // time the process sat in its gates since the previous sample (longest slot)
   if (hs) {
     const int64_t now_dev = (int64_t)mono_ns() + G.offset_ns;
-    for (int i = 0; i < 64; ++i)
-      if ((int64_t)__atomic_load_n(&hs[kHsHoldEnd + i], __ATOMIC_RELAXED) > now_dev) ++holding;
+    const int64_t* hi = reinterpret_cast<const int64_t*>(hs);
+    for (int i = 0; i < 64; ++i) {
+      // total first, then end, then start (governor.hip host_bucket_gate
+      // writes them in the opposite orders)
+      int64_t f = __atomic_load_n(&hi[kHsHeldCum + i], __ATOMIC_ACQUIRE);
+      const int64_t end = __atomic_load_n(&hi[kHsHoldEnd + i], __ATOMIC_ACQUIRE);
+      if (end > now_dev) {
+        ++holding;
+        const int64_t start = __atomic_load_n(&hi[kHsHoldStart + i], __ATOMIC_RELAXED);
+        if (start > 0 && start < now_dev) f += now_dev - start;
+      }
+      if (f != o.held_prev[i]) {
+        if (o.bucket && f - o.held_prev[i] > held_dt) held_dt = f - o.held_prev[i];
+        o.held_prev[i] = f;
+      }
+    }
     own = own > holding ? own - holding : 0;
   }
   // Busy: the streams still owe GPU work -- a gate enqueued that has not run
@@ -1613,9 +1640,25 @@ bool occ_sample(int dev, uint64_t now) {
   // the GPU is still serving this process alone, so that time is its too
   // (measured: without this a governed decode slice ran at 0.32 of its
   // unthrottled rate at a 25 % limit).  Held by its own gate: nothing.
+  // The time held by its gates is known exactly and charged nothing; the
+  // rest of the interval is charged at the share seen now -- or, if the
+  // process was held in it (the sample shows the hold, not the batch that ran
+  // before it), at the share it gets while running: the whole GPU alone,
+  // else its running average.
   double share = 0.0;
-  if (own > 0) share = (double)own / (double)(own + others);
-  else if (holding == 0 && others == 0 && pending) share = 1.0;
+  int state = 4;
+  if (own > 0) {
+    share = (double)own / (double)(own + others);
+    state = 0;
+  } else if (held_dt > 0 || holding > 0) {
+    share = others == 0 ? 1.0 : (o.share_avg > 0 ? o.share_avg : 0.0);
+    state = others == 0 ? 1 : 3;
+  } else if (others == 0 && pending) {
+    share = 1.0;
+    state = 1;
+  } else if (others > 0) {
+    state = 3;
+  }
   const int mask = (int)__atomic_load_n(&g_region->cu_mask_count[dev], __ATOMIC_RELAXED);
   if (mask > 0) {
     const double f = (double)mask / (double)device_cus(dev);
@@ -1624,7 +1667,14 @@ bool occ_sample(int dev, uint64_t now) {
   uint64_t dt = now - o.last_ns;
   if (dt > 100000000ull) dt = 100000000ull;   // a stalled sampler does not invent history
   o.last_ns = now;
-  o.share_ns += share * (double)dt;
+  double run = (double)dt - (double)held_dt + o.held_carry;
+  o.held_carry = run < 0 ? run : 0;
+  if (run < 0) run = 0;
+  const double held = (double)dt - run;
+  o.share_ns += share * run;
+  o.state_ns[state] += run;
+  o.state_ns[2] += held;
+  ++o.samples;
   const uint64_t total = (uint64_t)o.share_ns;
   // Host bucket (governor.hip host_bucket_gate): entitlement accrues at the
   // core limit, the GPU time actually received (the share integral) is
@@ -1638,7 +1688,7 @@ bool occ_sample(int dev, uint64_t now) {
       o.bucket = true;
       o.tokens_ns = cap;
     } else {
-      o.tokens_ns += (rate - share) * (double)dt;
+      o.tokens_ns += rate * (double)dt - share * run;
       if (o.tokens_ns > cap) o.tokens_ns = cap;
       if (o.tokens_ns < -cap) o.tokens_ns = -cap;
     }
@@ -2865,6 +2915,17 @@ MIVGPU_EXPORT int mivgpu_gate_balance(int dev, long long* tokens, unsigned long 
   if (tokens) *tokens = (long long)__atomic_load_n(&hs[kHsHostTokens], __ATOMIC_RELAXED);
   if (received && g_region && g_slot >= 0)
     *received = __atomic_load_n(&g_region->procs[g_slot].util[dev].share_ns, __ATOMIC_RELAXED);
+  return 0;
+}
+
+// Sampler diagnostics of `dev`: wall ns spent in each sampling state (own
+// waves resident / alone+busy with none resident / held by its own gate /
+// only other tenants' waves / idle) and the number of samples.
+MIVGPU_EXPORT int mivgpu_occ_states(int dev, double* ns5, unsigned long long* samples) {
+  if (dev < 0 || dev >= MIVGPU_MAX_DEVICES || !g_occ_live[dev].load(std::memory_order_acquire)) return -1;
+  std::lock_guard<std::mutex> pass(g_occ_pass_mu);
+  for (int i = 0; i < 5; ++i) ns5[i] = g_occ[dev].state_ns[i];
+  if (samples) *samples = g_occ[dev].samples;
   return 0;
 }
 

@@ -76,6 +76,12 @@ def gate_stats() -> dict:
         if bal(0, ctypes.byref(t), ctypes.byref(r)) == 0:
             out["received_ms"] = r.value / 1e6       # the host bucket's share integral
             out["tokens_ms"] = t.value / 1e6
+        st = ctypes.CDLL(None).mivgpu_occ_states
+        ns5, n = (ctypes.c_double * 5)(), ctypes.c_ulonglong()
+        if st(0, ns5, ctypes.byref(n)) == 0:
+            out["sampler_state_ms"] = dict(zip(("own", "alone_busy", "held", "others", "idle"),
+                                               (round(v / 1e6, 1) for v in ns5)))
+            out["sampler_samples"] = n.value
     except AttributeError:
         pass
     try:

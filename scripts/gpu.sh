@@ -11,6 +11,7 @@
 #   busyshare   rocprofv3 busy share of governed tenants (scripts/probe/governor_busyshare.py)
 #   probes      KFD occupancy + topology probes (scripts/probe/*.py)
 #   kernels     rocprofv3 --kernel-trace --stats of one 64-CU slice decode step
+#   kernels_full  the same on the whole GPU (kernel trace: durations and the gaps between them)
 #   pmc         PMC passes over a 64-CU decode step (one counter group per pass)
 #   membw       partition read ceilings (bench/membw.py)
 #   serving     TTFT / per-token latency, native vs vGPU slices (bench/serving.py)
@@ -56,6 +57,10 @@ case $suite in
   kernels)
     cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
     HSA_CU_MASK=0:0-63 step 240 prof_cu64 rocprofv3 --kernel-trace --stats -d "$out/prof_cu64" -o run -- \
+      python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 20 ;;
+  kernels_full)
+    cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
+    step 240 prof_full rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_full" -o run -- \
       python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 20 ;;
   pmc)
     cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R HSA_CU_MASK=0:0-63

@@ -75,6 +75,7 @@ def scenario(name, pct, lights, iters):
     print(json.dumps({"scenario": name, "limit_pct": pct, "lights": lights, "rc": r.returncode,
                       "tflops": round(res.get("tflops", 0), 1), "gate_held_ms": res.get("gate_held_ms"),
                       "received_ms": res.get("received_ms"), "seconds": res.get("seconds"),
+                      "sampler_state_ms": res.get("sampler_state_ms"), "sampler_samples": res.get("sampler_samples"),
                       "trace": heavy}), flush=True)
     if r.returncode != 0:
         print(r.stderr[-2000:], file=sys.stderr)

@@ -473,3 +473,25 @@ def test_host_bucket_charges_the_share_received(native_build, tmp_path, own, pee
     # the integral of the received share
     frac = own / (own + peer) if own else (1.0 if (busy and not peer) else 0.0)
     assert bal["received_ns"] <= 0.75e9 * frac + 5e7, bal
+
+
+def test_host_bucket_takes_held_time_out_exactly(native_build, tmp_path):
+    """The gates publish their holds (start, end, running total per slot) and
+    the sampler takes that time out of each interval exactly.  Here the
+    process's waves are "resident" at every sample (a static occupancy file),
+    as a real sample lands in the hold that follows a batch more often than in
+    the batch: classified by the sample, every interval would be charged
+    whole.  With the exact held time a 25 % tenant receives ~25 % of the wall
+    time and sits in its gates for the rest (the mock gate holds the
+    launching thread like governor.hip's gate holds the stream)."""
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
+    _occ(kfd, 987654, 4242, 30)
+    env = dict(_kfd_env(kfd), HIP_DEVICE_CORE_LIMIT="25", GPU_CORE_UTILIZATION_POLICY="force",
+               MOCKHIP_GOVERNOR="1", MOCKHIP_GATE_HOLD="1", MIVGPU_GATE_BURST_US="20000")
+    out = run(native_build, tmp_path, "kfdctx", 0, "alloc", 100, "launch", 10, "launchfor", 1500, "balance",
+              env=env, cache="held.cache")
+    bal = out[-1]
+    assert bal["rc"] == 0 and bal["gates"] > 10, bal
+    frac = bal["received_ns"] / (bal["received_ns"] + bal["held_ns"])
+    assert 0.18 <= frac <= 0.32, (frac, bal)
+    assert bal["held_ns"] >= 0.9e9, bal
