@@ -1685,8 +1685,11 @@ bool occ_sample(int dev, uint64_t now) {
     const double rate = (lim > 0 && lim < 100) ? (double)lim / 100.0 : 1.0;
     const double cap = (double)g_cfg.gate_cap_ns;
     if (!o.bucket) {
+      // empty, not full: a burst is earned by idling below the limit, not
+      // granted at start (a 100 ms start burst put a 1.5 s job at 0.32 of its
+      // unthrottled rate under a 25 % limit)
       o.bucket = true;
-      o.tokens_ns = cap;
+      o.tokens_ns = 0;
     } else {
       o.tokens_ns += rate * (double)dt - share * run;
       if (o.tokens_ns > cap) o.tokens_ns = cap;
