@@ -386,7 +386,7 @@ struct Config {
   bool occupancy = true;                   // charge the governor the sampled wave-occupancy share
   uint64_t occ_period_ns = 2000000;        // sampling period while the governor runs (2 ms)
   uint64_t occ_idle_period_ns = 50000000;  // ... and for utilisation reporting only (50 ms)
-  double share_tau_ns = 20e6;              // EWMA time constant of the governor's share
+  double share_tau_ns = 250e6;             // EWMA time constant of the occupancy averages (>> holds, batches)
   char kfd_sysfs[256] = "/sys/class/kfd/kfd";
   uint64_t gate_min_interval_ns = 200000;  // >= 200 us of host submission per gate
   bool gate_trace = false;                 // gates also write their trace ring (mivgpu_gate_trace)
@@ -1487,7 +1487,10 @@ bool gate_init_locked(int dev, DeviceGate& G) {
 struct OccPeer {
   int pid;
   int fd;
+  uint64_t busy_ns;   // last sample that saw it running (more than one CU's worth of waves)
 };
+// A peer is busy for this long after its last sample with waves resident.
+constexpr uint64_t kPeerBusyNs = 200000000ull;   // 200 ms
 struct OccDev {
   bool live = false;           // sampler has this device's KFD view
   int gpu_id = -1;
@@ -1497,7 +1500,9 @@ struct OccDev {
   uint64_t list_ns = 0;        // last peer directory scan
   uint64_t last_ns = 0;        // last sample
   double share_ns = 0;         // integral of the share, GPU-ns
-  double share_avg = -1;       // EWMA of the share while contending (-1 = no sample yet)
+  double share_avg = -1;       // the share while owing work (-1 = no sample yet)
+  double own_avg = 0;          // EWMAs of own / other tenants' resident waves while owing work
+  double others_avg = 0;
   uint64_t win_start_ns = 0;   // utilisation window
   double win_start_share = 0;
   bool bucket = false;         // host bucket started (the device's gate is up)
@@ -1559,10 +1564,11 @@ void occ_rescan(OccDev& o, uint64_t now) {
     long pid = strtol(e->d_name, &end, 10);
     if (end == e->d_name || *end || pid <= 0 || pid == o.own_pid) continue;
     int fd = -1;
+    uint64_t busy = 0;
     for (auto& p : o.peers)
-      if (p.pid == pid && p.fd >= 0) { fd = p.fd; p.fd = -1; break; }
+      if (p.pid == pid && p.fd >= 0) { fd = p.fd; busy = p.busy_ns; p.fd = -1; break; }
     if (fd < 0) fd = open_occ((int)pid, o.gpu_id);   // no stats_<gpu_id>: not on this GPU
-    if (fd >= 0) next.push_back(OccPeer{(int)pid, fd});
+    if (fd >= 0) next.push_back(OccPeer{(int)pid, fd, busy});
   }
   closedir(d);
   for (auto& p : o.peers)
@@ -1592,10 +1598,18 @@ bool occ_sample(int dev, uint64_t now) {
   if (now - o.list_ns > 100000000ull) occ_rescan(o, now);
   int own = read_occ(o.own_fd);
   if (own < 0) own = 0;
+  // Other tenants' waves.  A reading of one CU's worth is not counted: it is
+  // what a peer's gate holding its stream shows (one spinning wave), and
+  // charging less for it would hand the held peer's time to this tenant.
   long others = 0;
+  int busy_peers = 0;
   for (auto& p : o.peers) {
     int v = read_occ(p.fd);
-    if (v > 0) others += v;
+    if (v > 1) {
+      others += v;
+      p.busy_ns = now;
+    }
+    if (p.busy_ns && now - p.busy_ns < kPeerBusyNs) ++busy_peers;
   }
   // The gate's own resident wave is not consumption: discount one unit per
   // gate slot holding right now.
@@ -1634,39 +1648,41 @@ bool occ_sample(int dev, uint64_t now) {
   } else {
     pending = since_launch < 5000000ull;
   }
-  // The share of the GPU received at this instant: own / all resident waves;
-  // alone and busy with no wave resident (dispatch gaps, barrier and event
-  // packets between kernels -- a decode step is hundreds of small kernels)
-  // the GPU is still serving this process alone, so that time is its too
-  // (measured: without this a governed decode slice ran at 0.32 of its
-  // unthrottled rate at a 25 % limit).  Held by its own gate: nothing.
-  // The time held by its gates is known exactly and charged nothing; the
-  // rest of the interval is charged at the share seen now -- or, if the
-  // process was held in it (the sample shows the hold, not the batch that ran
-  // before it), at the share it gets while running: the whole GPU alone,
-  // else its running average.
+  uint64_t dt = now - o.last_ns;
+  if (dt > 100000000ull) dt = 100000000ull;   // a stalled sampler does not invent history
+  o.last_ns = now;
+  // The share of the GPU the process receives while it owes work (waves
+  // resident, a batch queued or running, or held in the interval) is the
+  // ratio of its AVERAGE resident waves to everyone's, both averaged over the
+  // samples in which it owes work and is not held -- not the ratio seen at one
+  // instant.  Instants mislead both ways: a decode step is hundreds of short
+  // kernels and the hardware scheduler time-slices processes' queues, so most
+  // samples catch one tenant or none resident (measured: 4 governed decode
+  // tenants each saw no wave at all in 64 % of their samples, and a running
+  // one usually alone), and charging each instant's ratio billed every
+  // pending tenant the whole GPU for the same time.  The averages charge each
+  // tenant in proportion to what it holds of the GPU, the charges of tenants
+  // owing work at the same time sum to the GPU, and alone the process pays
+  // its whole busy time (dispatch gaps included).  The time held by its gates
+  // is known exactly and charged nothing.
+  const bool owes = own > 0 || pending || holding > 0 || held_dt > 0;
+  if (owes && holding == 0) {
+    const double a = (double)dt / g_cfg.share_tau_ns < 1.0 ? (double)dt / g_cfg.share_tau_ns : 1.0;
+    o.own_avg += a * ((double)own - o.own_avg);
+    o.others_avg += a * ((double)others - o.others_avg);
+  }
   double share = 0.0;
   int state = 4;
-  if (own > 0) {
-    share = (double)own / (double)(own + others);
-    state = 0;
-  } else if (held_dt > 0 || holding > 0) {
-    share = others == 0 ? 1.0 : (o.share_avg > 0 ? o.share_avg : 0.0);
-    state = others == 0 ? 1 : 3;
-  } else if (others == 0 && pending) {
-    share = 1.0;
-    state = 1;
-  } else if (others > 0) {
-    state = 3;
+  if (owes) {
+    const double tot = o.own_avg + o.others_avg;
+    share = tot > 0 ? o.own_avg / tot : 1.0 / (double)(1 + busy_peers);
+    state = own > 0 ? 0 : (others > 0 ? 3 : 1);
   }
   const int mask = (int)__atomic_load_n(&g_region->cu_mask_count[dev], __ATOMIC_RELAXED);
   if (mask > 0) {
     const double f = (double)mask / (double)device_cus(dev);
     if (share > f) share = f;
   }
-  uint64_t dt = now - o.last_ns;
-  if (dt > 100000000ull) dt = 100000000ull;   // a stalled sampler does not invent history
-  o.last_ns = now;
   double run = (double)dt - (double)held_dt + o.held_carry;
   o.held_carry = run < 0 ? run : 0;
   if (run < 0) run = 0;
@@ -1714,13 +1730,10 @@ bool occ_sample(int dev, uint64_t now) {
     o.batch_win_launches = l;
     o.batch_win_share = o.share_ns;
   }
-  // Contending (for the reported share): waves resident, or work queued
-  // behind others; a sample taken while the governor holds the process says
-  // nothing about contention and is skipped.
-  const bool contending = holding == 0 && (own > 0 || (others > 0 && pending));
-  if (contending) {
-    const double a = (double)dt / g_cfg.share_tau_ns < 1.0 ? (double)dt / g_cfg.share_tau_ns : 1.0;
-    o.share_avg = o.share_avg < 0 ? share : o.share_avg + a * (share - o.share_avg);
+  // The reported share (and the device-bucket gate's weight): the share
+  // while owing work, as charged.
+  if (owes && holding == 0) {
+    o.share_avg = share;
     uint64_t ppm = (uint64_t)(o.share_avg * 1e6 + 0.5);
     if (!ppm) ppm = 1;   // 0 means "no sample yet" to the gate
     if (hs) __atomic_store_n(const_cast<uint64_t*>(&hs[kHsSharePpm]), ppm, __ATOMIC_RELAXED);
@@ -1740,6 +1753,8 @@ bool occ_sample(int dev, uint64_t now) {
   return true;
 }
 
+uint64_t g_occ_pass_ns = 0, g_occ_passes = 0, g_occ_pass_max_ns = 0;   // under g_occ_pass_mu
+
 void* occ_main(void*) {
   int tries[MIVGPU_MAX_DEVICES] = {0};
   for (;;) {
@@ -1758,6 +1773,11 @@ void* occ_main(void*) {
       if (!g_occ[d].live && tries[d] >= 40) continue;
       if (!occ_sample(d, now)) ++tries[d];
     }
+    // the cost of a pass (KFD's cu_occupancy reads walk every XCD's waves)
+    const uint64_t took = mono_ns() - now;
+    g_occ_pass_ns += took;
+    ++g_occ_passes;
+    if (took > g_occ_pass_max_ns) g_occ_pass_max_ns = took;
   }
   return nullptr;
 }
@@ -2929,6 +2949,16 @@ MIVGPU_EXPORT int mivgpu_occ_states(int dev, double* ns5, unsigned long long* sa
   std::lock_guard<std::mutex> pass(g_occ_pass_mu);
   for (int i = 0; i < 5; ++i) ns5[i] = g_occ[dev].state_ns[i];
   if (samples) *samples = g_occ[dev].samples;
+  return 0;
+}
+
+// Sampler passes so far, their total and their longest duration (ns).
+MIVGPU_EXPORT int mivgpu_occ_timing(unsigned long long* passes, unsigned long long* total_ns,
+                                    unsigned long long* max_ns) {
+  std::lock_guard<std::mutex> pass(g_occ_pass_mu);
+  if (passes) *passes = g_occ_passes;
+  if (total_ns) *total_ns = g_occ_pass_ns;
+  if (max_ns) *max_ns = g_occ_pass_max_ns;
   return 0;
 }
 

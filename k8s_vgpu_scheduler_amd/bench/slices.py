@@ -308,6 +308,12 @@ def _governor_stats() -> dict:
                         "gov_gates": g.value})
     except (OSError, AttributeError):
         pass
+    from k8s_vgpu_scheduler_amd.shim.probe import gate_stats
+    g = gate_stats()
+    for k in ("received_ms", "tokens_ms", "sampler_state_ms", "sampler_samples", "sampler_pass_us_mean",
+              "sampler_pass_us_max"):
+        if k in g:
+            out["gov_" + k] = g[k]
     cache = os.environ.get("MIVGPU_SHARED_CACHE")
     if cache and os.path.exists(cache):
         from k8s_vgpu_scheduler_amd.monitor.region import SharedRegion

@@ -82,6 +82,11 @@ def gate_stats() -> dict:
             out["sampler_state_ms"] = dict(zip(("own", "alone_busy", "held", "others", "idle"),
                                                (round(v / 1e6, 1) for v in ns5)))
             out["sampler_samples"] = n.value
+        tm = ctypes.CDLL(None).mivgpu_occ_timing
+        passes, tot, mx = ctypes.c_ulonglong(), ctypes.c_ulonglong(), ctypes.c_ulonglong()
+        if tm(ctypes.byref(passes), ctypes.byref(tot), ctypes.byref(mx)) == 0 and passes.value:
+            out["sampler_pass_us_mean"] = round(tot.value / passes.value / 1e3, 1)
+            out["sampler_pass_us_max"] = round(mx.value / 1e3, 1)
     except AttributeError:
         pass
     try:

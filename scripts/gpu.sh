@@ -15,6 +15,7 @@
 #   pmc         PMC passes over a 64-CU decode step (one counter group per pass)
 #   membw       partition read ceilings (bench/membw.py)
 #   serving     TTFT / per-token latency, native vs vGPU slices (bench/serving.py)
+#   mixed       governed server + 3 governed decode tenants; 8 x 12 % temporal over 600 steps
 #   prefill     prefill microbench + rocprofv3 kernel summary, whole GPU and 64 CUs
 # Results go to gpurun_out/<suite>/ (copy the ones to keep into profiles/).
 set -o pipefail
@@ -75,7 +76,13 @@ case $suite in
     done ;;
   serving)
     step 1100 serving python -u -m k8s_vgpu_scheduler_amd.bench.serving --configs "${1:-native,vgpu50,slice25,slice50}" \
-      --warmup 30 --runs 200 --max-tokens 128 --out-dir "$out" ;;
+      --warmup "${WARMUP:-30}" --runs "${RUNS:-200}" --max-tokens 128 --out-dir "$out" ;;
+  mixed)
+    # a governed server next to three governed decode tenants
+    # (all 25 %, force), then 8 x 12 % temporal over 600 steps vs native
+    step 900 serving python -u -m k8s_vgpu_scheduler_amd.bench.serving --configs temporal25,temporal25+3 \
+      --warmup 10 --runs 60 --max-tokens 128 --out-dir "$out/serving"
+    step 500 t8 python -u bench.py --slices 8 --rounds temporal,native --steps 600 --out "$out/t8.json" ;;
   prefill)
     step 120 native python3 -m k8s_vgpu_scheduler_amd.bench.prefill
     HSA_CU_MASK=0:0-63 step 120 cu64 python3 -m k8s_vgpu_scheduler_amd.bench.prefill

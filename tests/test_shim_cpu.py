@@ -497,3 +497,41 @@ def test_host_bucket_takes_held_time_out_exactly(native_build, tmp_path):
     frac = bal["received_ns"] / (bal["received_ns"] + bal["held_ns"])
     assert 0.18 <= frac <= 0.32, (frac, bal)
     assert bal["held_ns"] >= 0.9e9, bal
+
+
+def test_share_is_the_ratio_of_average_occupancies(native_build, tmp_path):
+    """The share charged while owing work is own / (own + others) of the
+    AVERAGE resident waves, not of one instant: a neighbour whose waves come
+    and go (30 half the time, 0 the other half) holds 15 on average, so a
+    tenant steadily holding 10 pays 10 / 25 = 0.4 of its busy time -- the
+    instant ratio would bill 1.0 whenever the neighbour is between kernels
+    (0.625 on average).  Alone with no wave caught (a peer reading one CU's
+    worth is a held gate, not a tenant at work) it pays its whole busy time."""
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
+    _occ(kfd, 987654, 4242, 0)
+    _occ(kfd, 111, 4242, 1)
+    env = dict(_kfd_env(kfd), HIP_DEVICE_CORE_LIMIT="25", GPU_CORE_UTILIZATION_POLICY="force",
+               MOCKHIP_GOVERNOR="1", MIVGPU_GATE_BURST_US="100000")
+    alone = run(native_build, tmp_path, "kfdctx", 0, "alloc", 100, "launch", 10, "launchfor", 900, "balance",
+                env=env, cache="alone.cache")[-1]
+    _occ(kfd, 987654, 4242, 10)
+    stop = threading.Event()
+
+    def toggle():   # the neighbour's waves come and go every 20 ms
+        v = 0
+        while not stop.is_set():
+            v = 30 - v
+            _occ(kfd, 111, 4242, v)
+            time.sleep(0.02)
+
+    th = threading.Thread(target=toggle)
+    th.start()
+    try:
+        shared = run(native_build, tmp_path, "kfdctx", 0, "alloc", 100, "launch", 10, "launchfor", 1500, "balance",
+                     env=dict(env, MIVGPU_SHARE_TAU_MS="100"), cache="shared.cache")[-1]
+    finally:
+        stop.set()
+        th.join()
+    assert alone["rc"] == 0 and shared["rc"] == 0, (alone, shared)
+    assert alone["received_ns"] >= 0.8e9, alone                    # the whole GPU, ~0.9 s
+    assert 0.45e9 <= shared["received_ns"] <= 0.75e9, shared         # ~0.4 x 1.5 s
