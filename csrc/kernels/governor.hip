@@ -191,9 +191,9 @@ mivgpu_gate(mivgpu_gate_state* st, mivgpu_gate_host_stats* hs, long long submit_
   const long long now = rt_ns();
   long long last = aload(&st->last_ns);
   long long tokens = aload(&st->tokens_ns);
-  if (last == 0) {  // first gate of the process on this device: full bucket
+  if (last == 0) {  // first gate of the process on this device: an empty bucket (bursts are earned)
     last = now;
-    tokens = cap_ns;
+    tokens = 0;
   }
   long long elapsed = now - last;
   if (elapsed < 0) elapsed = 0;  // bucket already settled into the future by a hold

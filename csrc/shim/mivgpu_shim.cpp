@@ -387,6 +387,12 @@ struct Config {
   uint64_t occ_period_ns = 2000000;        // sampling period while the governor runs (2 ms)
   uint64_t occ_idle_period_ns = 50000000;  // ... and for utilisation reporting only (50 ms)
   double share_tau_ns = 250e6;             // EWMA time constant of the occupancy averages (>> holds, batches)
+  // A/B switches (not grant keys): MIVGPU_GATE_MODE=device keeps the bucket
+  // in the gate (busy wall time x share) instead of the sampler;
+  // MIVGPU_SHARE_EST=instant averages the per-sample ratio own/(own+others)
+  // instead of taking the ratio of the averaged wave counts.
+  bool gate_device_mode = false;
+  bool share_instant = false;
   char kfd_sysfs[256] = "/sys/class/kfd/kfd";
   uint64_t gate_min_interval_ns = 200000;  // >= 200 us of host submission per gate
   bool gate_trace = false;                 // gates also write their trace ring (mivgpu_gate_trace)
@@ -565,6 +571,10 @@ void load_config() {
   g_cfg.occupancy = !(oc && (!strcmp(oc, "0") || !strcasecmp(oc, "false")));
   const char* op = grant_env("MIVGPU_OCC_PERIOD_US");
   if (op && atoll(op) >= 200) g_cfg.occ_period_ns = (uint64_t)atoll(op) * 1000ull;
+  const char* gm = getenv("MIVGPU_GATE_MODE");
+  g_cfg.gate_device_mode = gm && !strcmp(gm, "device");
+  const char* se = getenv("MIVGPU_SHARE_EST");
+  g_cfg.share_instant = se && !strcmp(se, "instant");
   const char* tau = grant_env("MIVGPU_SHARE_TAU_MS");
   if (tau && atof(tau) > 0) g_cfg.share_tau_ns = atof(tau) * 1e6;
   const char* crm = getenv("MIVGPU_CONTEXT_REFRESH_MS");
@@ -1487,7 +1497,7 @@ bool gate_init_locked(int dev, DeviceGate& G) {
 struct OccPeer {
   int pid;
   int fd;
-  uint64_t busy_ns;   // last sample that saw it running (more than one CU's worth of waves)
+  uint64_t busy_ns;   // last sample that saw waves of it resident
 };
 // A peer is busy for this long after its last sample with waves resident.
 constexpr uint64_t kPeerBusyNs = 200000000ull;   // 200 ms
@@ -1503,6 +1513,7 @@ struct OccDev {
   double share_avg = -1;       // the share while owing work (-1 = no sample yet)
   double own_avg = 0;          // EWMAs of own / other tenants' resident waves while owing work
   double others_avg = 0;
+  double inst_avg = -1;        // MIVGPU_SHARE_EST=instant: EWMA of the per-sample ratio
   uint64_t win_start_ns = 0;   // utilisation window
   double win_start_share = 0;
   bool bucket = false;         // host bucket started (the device's gate is up)
@@ -1598,14 +1609,15 @@ bool occ_sample(int dev, uint64_t now) {
   if (now - o.list_ns > 100000000ull) occ_rescan(o, now);
   int own = read_occ(o.own_fd);
   if (own < 0) own = 0;
-  // Other tenants' waves.  A reading of one CU's worth is not counted: it is
-  // what a peer's gate holding its stream shows (one spinning wave), and
-  // charging less for it would hand the held peer's time to this tenant.
+  // Other tenants' waves, counted like this process's own (a held peer's gate
+  // wave among them: discounting one CU's worth for peers but not for itself
+  // billed every symmetric tenant above 1/N -- measured, 8 x 12 % decode
+  // tenants held 27 % of the time).
   long others = 0;
   int busy_peers = 0;
   for (auto& p : o.peers) {
     int v = read_occ(p.fd);
-    if (v > 1) {
+    if (v > 0) {
       others += v;
       p.busy_ns = now;
     }
@@ -1666,16 +1678,21 @@ bool occ_sample(int dev, uint64_t now) {
   // its whole busy time (dispatch gaps included).  The time held by its gates
   // is known exactly and charged nothing.
   const bool owes = own > 0 || pending || holding > 0 || held_dt > 0;
+  const double a = (double)dt / g_cfg.share_tau_ns < 1.0 ? (double)dt / g_cfg.share_tau_ns : 1.0;
   if (owes && holding == 0) {
-    const double a = (double)dt / g_cfg.share_tau_ns < 1.0 ? (double)dt / g_cfg.share_tau_ns : 1.0;
     o.own_avg += a * ((double)own - o.own_avg);
     o.others_avg += a * ((double)others - o.others_avg);
+  }
+  if (g_cfg.share_instant && holding == 0 && (own > 0 || (others > 0 && pending))) {
+    const double inst = (double)own / (double)(own + others);
+    o.inst_avg = o.inst_avg < 0 ? inst : o.inst_avg + a * (inst - o.inst_avg);
   }
   double share = 0.0;
   int state = 4;
   if (owes) {
     const double tot = o.own_avg + o.others_avg;
     share = tot > 0 ? o.own_avg / tot : 1.0 / (double)(1 + busy_peers);
+    if (g_cfg.share_instant && o.inst_avg >= 0) share = o.inst_avg;
     state = own > 0 ? 0 : (others > 0 ? 3 : 1);
   }
   const int mask = (int)__atomic_load_n(&g_region->cu_mask_count[dev], __ATOMIC_RELAXED);
@@ -1823,7 +1840,7 @@ void enqueue_gate_locked(int dev, DeviceGate& G, int slot, hipStream_t stream, u
   int slot_arg = slot;
   unsigned int use_share = g_occ_live[dev].load(std::memory_order_acquire) ? 1u : 0u;
   // bit 0: trace ring; bit 1: host-bucket mode (the sampler keeps the bucket)
-  unsigned int flags = (g_cfg.gate_trace ? 1u : 0u) | (use_share ? 2u : 0u);
+  unsigned int flags = (g_cfg.gate_trace ? 1u : 0u) | (use_share && !g_cfg.gate_device_mode ? 2u : 0u);
   const bool occupancy = use_share != 0;
   void* state = G.state;
   void* hs = G.host_stats;

@@ -17,7 +17,7 @@ Configurations:
   vgpu50    shim, gpumem 50 % of the card (the reference's job-on-hami.yml), all CUs
   slice25   shim, gpucores 25: 64-CU balanced mask + 2 HW queues, gpumem 36 GiB
   slice50   shim, gpucores 50: 128-CU mask, gpumem 72 GiB
-  temporal25 shim, gpucores 25 time-sliced by the governor (no mask, policy force)
+  temporal25 shim, gpucores 25 time-sliced by the governor (no mask, policy force, 2 HW queues)
 A ``+K`` suffix (``slice25+3``, ``native+3``) runs K busy Qwen3-8B decode
 tenants (batch 32) next to the server for that configuration: in the other CU
 partitions of a 4-way split for slice configs (shim, 36 GiB grants, as pods),
@@ -48,7 +48,8 @@ CONFIGS = {
     "vgpu50": SliceSpec(index=1, gpumem_mib=CARD_MIB // 2, cu_ranges=None),
     "slice25": SliceSpec(index=2, gpumem_mib=36864, cu_ranges=[(0, 63)], core_pct=25, hw_queues=2),
     "slice50": SliceSpec(index=3, gpumem_mib=73728, cu_ranges=[(0, 127)], core_pct=50, hw_queues=2),
-    "temporal25": SliceSpec(index=4, gpumem_mib=36864, cu_ranges=None, core_pct=25, policy="force"),
+    # 2 HW queues: what the device plugin grants a shared pod (--hw-queues)
+    "temporal25": SliceSpec(index=4, gpumem_mib=36864, cu_ranges=None, core_pct=25, policy="force", hw_queues=2),
 }
 
 

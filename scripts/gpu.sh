@@ -14,6 +14,7 @@
 #   kernels_full  the same on the whole GPU (kernel trace: durations and the gaps between them)
 #   pmc         PMC passes over a 64-CU decode step (one counter group per pass)
 #   membw       partition read ceilings (bench/membw.py)
+#   mall        projection GEMMs cold vs with their weights prefetched into the Infinity Cache
 #   serving     TTFT / per-token latency, native vs vGPU slices (bench/serving.py)
 #   mixed       governed server + 3 governed decode tenants; 8 x 12 % temporal over 600 steps
 #   prefill     prefill microbench + rocprofv3 kernel summary, whole GPU and 64 CUs
@@ -69,6 +70,17 @@ case $suite in
     timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$out/a" -o run -- $dec > "$out/a.log" 2>&1 || exit 1
     timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS \
       --kernel-trace --output-format csv -d "$out/b" -o run -- $dec > "$out/b.log" 2>&1 || exit 1 ;;
+  govmodes)
+    # A/B of the governor's bucket (host / device) and share estimator on 8 x 12 %
+    step 400 host_ratio python -u bench.py --slices 8 --rounds temporal --steps 600 --out "$out/host_ratio.json"
+    MIVGPU_GATE_MODE=device step 400 device_ratio python -u bench.py --slices 8 --rounds temporal --steps 600 \
+      --out "$out/device_ratio.json"
+    MIVGPU_GATE_MODE=device MIVGPU_SHARE_EST=instant MIVGPU_SHARE_TAU_MS=20 step 400 device_inst20 \
+      python -u bench.py --slices 8 --rounds temporal --steps 600 --out "$out/device_inst20.json"
+    MIVGPU_SHARE_EST=instant MIVGPU_SHARE_TAU_MS=20 step 400 host_inst20 \
+      python -u bench.py --slices 8 --rounds temporal --steps 600 --out "$out/host_inst20.json" ;;
+  mall)
+    step 300 mall python -u scripts/probe/mall_prefetch.py --out "$out/mall.json" ;;
   membw)
     for b in 2 4 8 16; do
       step 300 "membw8_b$b" python -u -m k8s_vgpu_scheduler_amd.bench.membw --gib 20 --shared-only 8 --shared-bpc "$b" \

@@ -505,11 +505,11 @@ def test_share_is_the_ratio_of_average_occupancies(native_build, tmp_path):
     and go (30 half the time, 0 the other half) holds 15 on average, so a
     tenant steadily holding 10 pays 10 / 25 = 0.4 of its busy time -- the
     instant ratio would bill 1.0 whenever the neighbour is between kernels
-    (0.625 on average).  Alone with no wave caught (a peer reading one CU's
-    worth is a held gate, not a tenant at work) it pays its whole busy time."""
+    (0.625 on average).  Alone with no wave caught it pays its whole busy
+    time."""
     kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
     _occ(kfd, 987654, 4242, 0)
-    _occ(kfd, 111, 4242, 1)
+    _occ(kfd, 111, 4242, 0)
     env = dict(_kfd_env(kfd), HIP_DEVICE_CORE_LIMIT="25", GPU_CORE_UTILIZATION_POLICY="force",
                MOCKHIP_GOVERNOR="1", MIVGPU_GATE_BURST_US="100000")
     alone = run(native_build, tmp_path, "kfdctx", 0, "alloc", 100, "launch", 10, "launchfor", 900, "balance",
