@@ -110,6 +110,13 @@ class MonitorCollector:
                                  "of hami_mig_device_info)",
                                  labels=CTR_LABELS + ["compute_partition", "memory_partition", "partition_index",
                                                       "physical_index", "cus"])
+        # the reference's series name and labels for the same identity, so HAMi
+        # dashboards built on hami_mig_device_info keep working
+        # (cmd/vGPUmonitor/metrics.go:102-106): mig_uuid = the partition
+        # device, profile = <mode>.<CUs>cu, gpu instance = partition index
+        mig = GaugeMetricFamily("hami_mig_device_info", "MIG runtime identity for a container allocation "
+                                "(MI355X: compute-partition identity)",
+                                labels=CTR_LABELS + ["mig_uuid", "profile", "gpu_instance_id", "compute_instance_id"])
         host_b = GaugeMetricFamily("mivgpu_container_memory_host_bytes",
                                    "Container device memory from host truth (KFD per-process VRAM of the pod's "
                                    "processes), independent of the tenant-writable shared region",
@@ -151,6 +158,9 @@ class MonitorCollector:
                 if g is not None:
                     part.add_metric(lab + [g.compute_partition, g.memory_partition, str(g.partition_index),
                                            str(g.physical), str(g.cus)], 1.0)
+                    if str(g.compute_partition).upper() != "SPX":
+                        mig.add_metric(lab + [r.uuid(i), f"{str(g.compute_partition).lower()}.{g.cus}cu",
+                                              str(g.partition_index), "0"], 1.0)
                 if self.legacy:
                     ctx_b, mod_b = r.memory_field(i, "context"), r.memory_field(i, "module")
                     data_b = r.memory_field(i, "buffer") + r.memory_field(i, "vmm")
@@ -172,7 +182,7 @@ class MonitorCollector:
                 if tb is not None:
                     host_b.add_metric(lab, float(tb))
                     over_g.add_metric(lab, 1.0 if (c.pod_uid, c.container) in over else 0.0)
-        yield from (used, limit, dmem, dutil, lastk, ctx, mod, buf, busy, held, cumask, part, share, occw)
+        yield from (used, limit, dmem, dutil, lastk, ctx, mod, buf, busy, held, cumask, part, mig, share, occw)
         if self.truth is not None:
             yield from (host_b, over_g)
         if self.legacy:

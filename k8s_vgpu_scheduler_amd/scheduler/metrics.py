@@ -55,6 +55,13 @@ class SchedulerCollector:
         # compute-partition device (mode dpx/qpx/cpx), value = its CU count
         part = _g("hami_node_gpu_partition_info", "Compute-partition devices (SPX/DPX/QPX/CPX) on a node",
                   ["node", "device_uuid", "device_index", "mode", "device_type"])
+        # the reference's name and labels for the same rows (cmd/scheduler/metrics.go:142-146), so
+        # HAMi dashboards keep working: mig_uuid = the partition device, profile = its mode,
+        # placement = its CU count
+        mig = _g("hami_node_gpu_mig_instance_info", "Realized MIG instance identity and scheduler placement "
+                 "(MI355X: compute-partition devices)",
+                 ["node", "device_uuid", "device_index", "mig_uuid", "profile", "gpu_instance_id",
+                  "compute_instance_id", "placement_start", "placement_size"])
         legacy = []
         if self.legacy:
             ll = ["nodeid", "deviceuuid", "deviceidx", "devicetype"]
@@ -77,11 +84,12 @@ class SchedulerCollector:
                     mem_pct.add_metric([node_id, d.id, idx, d.type, ZONE], d.usedmem / d.totalmem)
                 if d.mode and d.mode != "hami-core":
                     part.add_metric([node_id, d.id, idx, d.mode, d.type, ZONE], float(d.totalcore))
+                    mig.add_metric([node_id, d.id, idx, d.id, d.mode, idx, "0", "0", str(d.totalcore), ZONE], 1.0)
                 if self.legacy:
                     legacy[0].add_metric([node_id, d.id, idx, d.type, ZONE], mib_to_bytes(d.totalmem))
                     legacy[1].add_metric([node_id, d.id, idx, d.type, ZONE], float(d.totalcore))
                     legacy[2].add_metric([node_id, d.id, idx, d.type, ZONE], float(d.used))
-        yield from (mem_limit, core_limit, mem_alloc, shared, core_alloc, overview, mem_pct, part, *legacy)
+        yield from (mem_limit, core_limit, mem_alloc, shared, core_alloc, overview, mem_pct, part, mig, *legacy)
 
         q_used = _g("hami_resource_quota_used", "resource quota used", ["namespace", "quota_name", "limit"])
         q_limit = _g("hami_resource_quota_limit", "resource quota limit", ["namespace", "quota_name"])

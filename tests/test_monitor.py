@@ -239,6 +239,10 @@ def test_partition_info_and_legacy_series(tmp_path):
     assert ('mivgpu_container_partition_info{compute_partition="CPX",container="main",cus="32",'
             'device_uuid="GPU-0001-cpx3",memory_partition="NPS1",namespace="ns1",partition_index="3",'
             'physical_index="1",pod="p1",vdevice_index="0"} 1.0') in text
+    # the reference's series for the same identity (hami_mig_device_info)
+    assert ('hami_mig_device_info{compute_instance_id="0",container="main",device_uuid="GPU-0001-cpx3",'
+            'gpu_instance_id="3",mig_uuid="GPU-0001-cpx3",namespace="ns1",pod="p1",profile="cpx.32cu",'
+            'vdevice_index="0"} 1.0') in text
     assert 'vGPU_device_memory_usage_in_bytes{ctrname="main",deviceuuid="GPU-0001-cpx3",podname="p1",podnamespace="ns1",vdeviceid="0"} 3.145728e+08' in text
     assert 'vGPU_device_memory_limit_in_bytes{' in text
     assert 'Device_memory_desc_of_container{context="0",ctrname="main",data="314572800"' in text

@@ -118,6 +118,11 @@ def test_partition_info_series():
     assert len(m["hami_node_gpu_partition_info"]) == 4
     assert {lab["mode"] for lab, _ in m["hami_node_gpu_partition_info"]} == {"qpx"}
     assert {v for _, v in m["hami_node_gpu_partition_info"]} == {64.0}
+    # the reference's series name for the same rows (HAMi dashboards)
+    mig = m["hami_node_gpu_mig_instance_info"]
+    assert len(mig) == 4 and {lab["profile"] for lab, _ in mig} == {"qpx"}
+    assert {lab["placement_size"] for lab, _ in mig} == {"64"}
+    assert {lab["mig_uuid"] for lab, _ in mig} == {lab["device_uuid"] for lab, _ in mig}
 
 
 def test_build_info(sched):
