@@ -390,9 +390,11 @@ struct Config {
   // A/B switches (not grant keys): MIVGPU_GATE_MODE=device keeps the bucket
   // in the gate (busy wall time x share) instead of the sampler;
   // MIVGPU_SHARE_EST=instant averages the per-sample ratio own/(own+others)
-  // instead of taking the ratio of the averaged wave counts.
+  // (ratio: the ratio of the averaged wave counts) instead of counting the
+  // contending tenants.
   bool gate_device_mode = false;
   bool share_instant = false;
+  bool share_ratio = false;
   char kfd_sysfs[256] = "/sys/class/kfd/kfd";
   uint64_t gate_min_interval_ns = 200000;  // >= 200 us of host submission per gate
   bool gate_trace = false;                 // gates also write their trace ring (mivgpu_gate_trace)
@@ -575,6 +577,7 @@ void load_config() {
   g_cfg.gate_device_mode = gm && !strcmp(gm, "device");
   const char* se = getenv("MIVGPU_SHARE_EST");
   g_cfg.share_instant = se && !strcmp(se, "instant");
+  g_cfg.share_ratio = se && !strcmp(se, "ratio");
   const char* tau = grant_env("MIVGPU_SHARE_TAU_MS");
   if (tau && atof(tau) > 0) g_cfg.share_tau_ns = atof(tau) * 1e6;
   const char* crm = getenv("MIVGPU_CONTEXT_REFRESH_MS");
@@ -1498,7 +1501,13 @@ struct OccPeer {
   int pid;
   int fd;
   uint64_t busy_ns;   // last sample that saw waves of it resident
+  int v;              // its reading this sample
+  double avg;         // EWMA of its readings over this process's owing samples
 };
+// Busy peers whose average resident waves are within this factor of this
+// process's own (either way) contend as equals; a peer this many times
+// lighter is ignored, one this many times heavier is shared with by ratio.
+constexpr double kContendFrac = 0.1;
 // A peer is busy for this long after its last sample with waves resident.
 constexpr uint64_t kPeerBusyNs = 200000000ull;   // 200 ms
 struct OccDev {
@@ -1576,10 +1585,11 @@ void occ_rescan(OccDev& o, uint64_t now) {
     if (end == e->d_name || *end || pid <= 0 || pid == o.own_pid) continue;
     int fd = -1;
     uint64_t busy = 0;
+    double avg = 0;
     for (auto& p : o.peers)
-      if (p.pid == pid && p.fd >= 0) { fd = p.fd; busy = p.busy_ns; p.fd = -1; break; }
+      if (p.pid == pid && p.fd >= 0) { fd = p.fd; busy = p.busy_ns; avg = p.avg; p.fd = -1; break; }
     if (fd < 0) fd = open_occ((int)pid, o.gpu_id);   // no stats_<gpu_id>: not on this GPU
-    if (fd >= 0) next.push_back(OccPeer{(int)pid, fd, busy});
+    if (fd >= 0) next.push_back(OccPeer{(int)pid, fd, busy, 0, avg});
   }
   closedir(d);
   for (auto& p : o.peers)
@@ -1617,6 +1627,7 @@ bool occ_sample(int dev, uint64_t now) {
   int busy_peers = 0;
   for (auto& p : o.peers) {
     int v = read_occ(p.fd);
+    p.v = v > 0 ? v : 0;
     if (v > 0) {
       others += v;
       p.busy_ns = now;
@@ -1663,25 +1674,30 @@ bool occ_sample(int dev, uint64_t now) {
   uint64_t dt = now - o.last_ns;
   if (dt > 100000000ull) dt = 100000000ull;   // a stalled sampler does not invent history
   o.last_ns = now;
-  // The share of the GPU the process receives while it owes work (waves
-  // resident, a batch queued or running, or held in the interval) is the
-  // ratio of its AVERAGE resident waves to everyone's, both averaged over the
-  // samples in which it owes work and is not held -- not the ratio seen at one
-  // instant.  Instants mislead both ways: a decode step is hundreds of short
-  // kernels and the hardware scheduler time-slices processes' queues, so most
-  // samples catch one tenant or none resident (measured: 4 governed decode
-  // tenants each saw no wave at all in 64 % of their samples, and a running
-  // one usually alone), and charging each instant's ratio billed every
-  // pending tenant the whole GPU for the same time.  The averages charge each
-  // tenant in proportion to what it holds of the GPU, the charges of tenants
-  // owing work at the same time sum to the GPU, and alone the process pays
-  // its whole busy time (dispatch gaps included).  The time held by its gates
-  // is known exactly and charged nothing.
+  // While the process owes work (waves resident, a batch queued or running,
+  // or held in the interval) it is charged an equal split of that time with
+  // the other tenants contending for the GPU as equals: busy ones (waves seen
+  // within 200 ms) whose average resident waves -- averaged over the samples
+  // in which this process owes work and is not held -- are within 10x of its
+  // own.  A tenant that occupies the GPU far less (a light neighbour's small
+  // kernels, a peer held behind its gate) does not dilute the charge, so alone
+  // or next to light tenants the process pays its whole busy time (dispatch
+  // gaps included); N symmetric busy tenants pay 1/N each; next to a tenant
+  // 10x heavier it pays its ratio of the waves (queued behind it with none of
+  // its own resident: nothing).  Measured on
+  // MI355X, magnitudes read by each tenant's own sampler are not comparable
+  // across tenants: a decode step is hundreds of short kernels, the hardware
+  // scheduler time-slices processes' queues, and the sampler thread runs when
+  // its process lets it -- the ratio of averaged wave counts put 8 symmetric
+  // 12 % tenants at 3-55 % each (fairness 0.91), per-sample ratios at 2-80 %
+  // (0.81).  The count needs only "is it busy, and not much lighter".  The
+  // time held by its gates is known exactly and charged nothing.
   const bool owes = own > 0 || pending || holding > 0 || held_dt > 0;
   const double a = (double)dt / g_cfg.share_tau_ns < 1.0 ? (double)dt / g_cfg.share_tau_ns : 1.0;
   if (owes && holding == 0) {
     o.own_avg += a * ((double)own - o.own_avg);
     o.others_avg += a * ((double)others - o.others_avg);
+    for (auto& p : o.peers) p.avg += a * ((double)p.v - p.avg);
   }
   if (g_cfg.share_instant && holding == 0 && (own > 0 || (others > 0 && pending))) {
     const double inst = (double)own / (double)(own + others);
@@ -1690,9 +1706,22 @@ bool occ_sample(int dev, uint64_t now) {
   double share = 0.0;
   int state = 4;
   if (owes) {
-    const double tot = o.own_avg + o.others_avg;
-    share = tot > 0 ? o.own_avg / tot : 1.0 / (double)(1 + busy_peers);
-    if (g_cfg.share_instant && o.inst_avg >= 0) share = o.inst_avg;
+    if (g_cfg.share_ratio) {
+      const double tot = o.own_avg + o.others_avg;
+      share = tot > 0 ? o.own_avg / tot : 1.0 / (double)(1 + busy_peers);
+    } else if (g_cfg.share_instant && o.inst_avg >= 0) {
+      share = o.inst_avg;
+    } else {
+      int comparable = 0;
+      double heavier = 0;
+      for (const auto& p : o.peers) {
+        if (!p.busy_ns || now - p.busy_ns >= kPeerBusyNs) continue;
+        if (p.avg * kContendFrac > o.own_avg) heavier += p.avg;
+        else if (p.avg >= kContendFrac * o.own_avg) ++comparable;
+      }
+      const double base = o.own_avg + heavier > 0 ? o.own_avg / (o.own_avg + heavier) : 1.0;
+      share = base / (double)(1 + comparable);
+    }
     state = own > 0 ? 0 : (others > 0 ? 3 : 1);
   }
   const int mask = (int)__atomic_load_n(&g_region->cu_mask_count[dev], __ATOMIC_RELAXED);

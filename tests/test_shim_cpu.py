@@ -309,9 +309,12 @@ def _sample_util(native_build, tmp_path, kfd, cache, extra_env=None, wait_s=1.3)
 
 def test_occupancy_sampler_measures_the_gpu_share(native_build, tmp_path):
     """The shim samples KFD's per-process wave counts (cu_occupancy) of itself
-    and of every other process on its GPU and integrates its share of the
-    resident waves: own 30 vs neighbours 10 -> 75 % of the GPU received,
-    published as util_pct / share_ns for the monitor and the gate kernel."""
+    and of every other process on its GPU and splits its busy time evenly with
+    the busy tenants that contend (average waves within 10x of its own):
+    own 30 vs a neighbour at 10 -> 50 % of the GPU received, published as
+    util_pct / share_ns for the monitor and the gate kernel; a light
+    neighbour (2 < 30 / 10) does not count; MIVGPU_SHARE_EST=ratio charges
+    own / (own + others) of the averages instead (30 vs 10 -> 75 %)."""
     kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0), (5151, 0x85 << 8, 0)])
     _occ(kfd, 987654, 4242, 30)      # this process (the mock's KFD pid)
     _occ(kfd, 111, 4242, 10)         # a neighbour on the same GPU
@@ -319,9 +322,14 @@ def test_occupancy_sampler_measures_the_gpu_share(native_build, tmp_path):
     _occ(kfd, 333, 4242, 0)          # an idle neighbour: costs nothing
     r = _sample_util(native_build, tmp_path, kfd, "occ.cache")
     assert r["occupancy"] == 30
-    assert 70 <= r["util_pct"] <= 76, r
-    # the integral grows at ~0.75 GPU-ns per ns
-    assert 0.5 * 0.75 * r["elapsed_ns"] <= r["share_ns"] <= 0.75 * (r["elapsed_ns"] + 1.5e9), r
+    assert 46 <= r["util_pct"] <= 52, r
+    # the integral grows at ~0.5 GPU-ns per ns
+    assert 0.5 * 0.5 * r["elapsed_ns"] <= r["share_ns"] <= 0.5 * (r["elapsed_ns"] + 1.5e9), r
+    ratio = _sample_util(native_build, tmp_path, kfd, "occr.cache", {"MIVGPU_SHARE_EST": "ratio"})
+    assert 70 <= ratio["util_pct"] <= 76, ratio
+    _occ(kfd, 111, 4242, 2)          # a light neighbour
+    light = _sample_util(native_build, tmp_path, kfd, "occl.cache")
+    assert light["util_pct"] >= 97, light
 
 
 def test_occupancy_share_capped_by_the_cu_mask(native_build, tmp_path):
@@ -441,20 +449,22 @@ def test_governor_host_path_on_the_mock(native_build, tmp_path):
     assert all("charge=wall" in l for l in lines if l.startswith("mark mivgpu:gate"))   # no KFD view
 
 
-@pytest.mark.parametrize("own,peer,limit,trend,busy", [
-    (30, 0, 25, "debt", False),   # alone: receives the whole GPU at a 25 % limit -> in debt
-    (10, 30, 25, "even", False),  # co-resident with a 3x heavier peer: receives 25 % = its limit
-    (10, 90, 25, "full", False),  # receives 10 % < 25 %: nothing charged beyond the refill
-    (0, 50, 25, "full", True),    # queued behind a peer, no waves resident: charged nothing
-    (0, 0, 25, "debt", True),     # alone and launching, no wave caught resident: still its GPU time
-    (0, 0, 25, "full", False),    # alone and idle: nothing
+@pytest.mark.parametrize("own,peer,limit,trend,busy,frac", [
+    (30, 0, 25, "debt", False, 1.0),    # alone: receives the whole GPU at a 25 % limit -> in debt
+    (10, 30, 50, "even", False, 0.5),   # a comparable busy peer (within 10x): half each = its 50 % limit
+    (10, 200, 25, "full", False, 0.05),  # next to a 20x heavier peer: its ratio, 5 % < 25 %
+    (30, 2, 25, "debt", False, 1.0),    # a 15x lighter peer does not dilute the charge
+    (0, 50, 25, "full", True, 0.0),     # queued behind a peer, no waves resident: charged nothing
+    (0, 0, 25, "debt", True, 1.0),      # alone and launching, no wave caught resident: still its GPU time
+    (0, 0, 25, "full", False, 0.0),     # alone and idle: nothing
 ])
-def test_host_bucket_charges_the_share_received(native_build, tmp_path, own, peer, limit, trend, busy):
+def test_host_bucket_charges_the_share_received(native_build, tmp_path, own, peer, limit, trend, busy, frac):
     """Host-bucket mode: the sampler charges the GPU time
-    the process actually receives -- own / (own + others) resident waves,
-    integrated every sample -- against rate x wall time; co-resident or queued
-    time is not charged as exclusive.  The gates (run on the host by the mock)
-    only read the balance."""
+    the process actually receives -- its busy time split evenly with comparable
+    busy tenants, by wave ratio next to much heavier ones, integrated every
+    sample -- against rate x wall time; co-resident or queued time is not
+    charged as exclusive.  The gates (run on the host by the mock) only read
+    the balance."""
     kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
     _occ(kfd, 987654, 4242, own)
     if peer:
@@ -473,7 +483,6 @@ def test_host_bucket_charges_the_share_received(native_build, tmp_path, own, pee
     else:
         assert bal["tokens_ns"] >= 95_000_000, bal           # fills to the 100 ms burst
     # the integral of the received share
-    frac = own / (own + peer) if own else (1.0 if (busy and not peer) else 0.0)
     assert bal["received_ns"] <= 1.05e9 * frac + 5e7, bal
 
 
@@ -500,7 +509,7 @@ def test_host_bucket_takes_held_time_out_exactly(native_build, tmp_path):
 
 
 def test_share_is_the_ratio_of_average_occupancies(native_build, tmp_path):
-    """The share charged while owing work is own / (own + others) of the
+    """MIVGPU_SHARE_EST=ratio: the share charged while owing work is own / (own + others) of the
     AVERAGE resident waves, not of one instant: a neighbour whose waves come
     and go (30 half the time, 0 the other half) holds 15 on average, so a
     tenant steadily holding 10 pays 10 / 25 = 0.4 of its busy time -- the
@@ -528,7 +537,7 @@ def test_share_is_the_ratio_of_average_occupancies(native_build, tmp_path):
     th.start()
     try:
         shared = run(native_build, tmp_path, "kfdctx", 0, "alloc", 100, "launch", 10, "launchfor", 1500, "balance",
-                     env=dict(env, MIVGPU_SHARE_TAU_MS="100"), cache="shared.cache")[-1]
+                     env=dict(env, MIVGPU_SHARE_TAU_MS="100", MIVGPU_SHARE_EST="ratio"), cache="shared.cache")[-1]
     finally:
         stop.set()
         th.join()

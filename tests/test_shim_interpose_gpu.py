@@ -51,8 +51,10 @@ def test_triton_kernel_loop_held_to_its_share(tmp):
 
 def test_torch_compile_mlp_held_to_its_share(tmp):
     """(b) a torch.compile'd MLP (Inductor Triton GEMMs + epilogues) obeys the
-    same bound."""
-    args = ["--n", "8192", "--iters", "400"]
+    same bound.  1000 iterations (~4 s governed): the tokens the bucket earns
+    while Inductor compiles on the CPU (up to its 100 ms burst) are spent at
+    the start of the timed loop, which over 400 iterations read 0.31."""
+    args = ["--n", "8192", "--iters", "1000"]
     free = run_child("compile", {"MIVGPU_SHARED_CACHE": os.path.join(tmp, "cf.cache")}, True, args, timeout=900)
     gov = run_child("compile", {"MIVGPU_SHARED_CACHE": os.path.join(tmp, "cg.cache"), **GOVERNED_25}, True, args,
                     timeout=900)
@@ -60,7 +62,8 @@ def test_torch_compile_mlp_held_to_its_share(tmp):
     ratio = gov["tflops"] / free["tflops"]
     print(json.dumps({"unthrottled_tflops": round(free["tflops"], 1), "governed_tflops": round(gov["tflops"], 1),
                       "ratio": round(ratio, 3), "launches": gov["shim_launches"], "gates": gov.get("gates"),
-                      "rel_err": gov["rel_err"]}))
+                      "held_ms": gov.get("gate_held_ms"), "received_ms": gov.get("received_ms"),
+                      "sampler_state_ms": gov.get("sampler_state_ms"), "rel_err": gov["rel_err"]}))
     assert free["rel_err"] < 5e-2
     assert gov["shim_launches"] >= 400
     assert 0.18 <= ratio <= 0.30, ratio
