@@ -185,6 +185,17 @@ int main(int argc, char** argv) {
       auto g = (unsigned long long (*)(void))dlsym(RTLD_DEFAULT, "mockhip_launch_count");
       printf("{\"op\":\"launch\",\"n\":%ld,\"shim_seen\":%llu,\"real_seen\":%llu}\n", n,
              f ? f() : 0ull, g ? g() : 0ull);
+    } else if (!strcmp(c, "launchtime")) {
+      // host cost per launch: N launches into the mock runtime (which only counts)
+      long n = strtol(argv[++i], nullptr, 10);
+      static char dummy;
+      for (long k = 0; k < 1000; ++k) (void)hipLaunchKernel(&dummy, dim3(1), dim3(64), nullptr, 0, nullptr);
+      struct timespec t0, t1;
+      clock_gettime(CLOCK_MONOTONIC, &t0);
+      for (long k = 0; k < n; ++k) (void)hipLaunchKernel(&dummy, dim3(1), dim3(64), nullptr, 0, nullptr);
+      clock_gettime(CLOCK_MONOTONIC, &t1);
+      const double ns = ((t1.tv_sec - t0.tv_sec) * 1e9 + (t1.tv_nsec - t0.tv_nsec)) / (double)n;
+      printf("{\"op\":\"launchtime\",\"n\":%ld,\"ns_per_launch\":%.1f}\n", n, ns);
     } else if (!strcmp(c, "usage")) {
       auto f = (long long (*)(int))dlsym(RTLD_DEFAULT, "mivgpu_process_usage");
       printf("{\"op\":\"usage\",\"bytes\":%lld}\n", f ? f(0) : -2ll);

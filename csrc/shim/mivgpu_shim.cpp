@@ -825,6 +825,8 @@ inline void ensure_init() {
 }
 
 inline int current_device() {
+  // one visible device (the common pod): no runtime call on the launch path
+  if (g_num_devices == 1) return 0;
   int d = 0;
   if (real_hipGetDevice()) (void)real_hipGetDevice()(&d);  // on failure: device 0
   if (d < 0 || d >= MIVGPU_MAX_DEVICES) d = 0;

@@ -544,3 +544,26 @@ def test_share_is_the_ratio_of_average_occupancies(native_build, tmp_path):
     assert alone["rc"] == 0 and shared["rc"] == 0, (alone, shared)
     assert alone["received_ns"] >= 0.8e9, alone                    # the whole GPU, ~0.9 s
     assert 0.45e9 <= shared["received_ns"] <= 0.75e9, shared         # ~0.4 x 1.5 s
+
+
+def test_launch_hook_host_cost(native_build, tmp_path):
+    """Host cost of the launch hooks on the mock runtime (which only counts
+    launches): measured ~30 ns with the governor off and ~130 ns governed (no
+    mutex on a launch that does not close a batch); generous bounds for a
+    shared CI machine.  profiles/README.md section 32 has the MI355X numbers."""
+    def ns(extra, preload=True, tag=""):
+        e = dict(os.environ, MOCKHIP_TOTAL_MIB="65536", MIVGPU_SHARED_CACHE=str(tmp_path / f"lt{tag}.cache"), **extra)
+        if preload:
+            e["LD_PRELOAD"] = str(native_build["shim"])
+        else:
+            e.pop("LD_PRELOAD", None)
+        out = subprocess.run([str(native_build["driver"]), "launchtime", "300000"], env=e, capture_output=True,
+                             text=True, timeout=120).stdout
+        return [json.loads(line) for line in out.splitlines() if line.startswith("{")][-1]["ns_per_launch"]
+
+    base = min(ns({}, False, "a") for _ in range(2))
+    off = min(ns({}, True, "b") for _ in range(2))
+    gov = min(ns({"HIP_DEVICE_CORE_LIMIT": "99", "GPU_CORE_UTILIZATION_POLICY": "force", "MOCKHIP_GOVERNOR": "1"},
+                 True, "c") for _ in range(2))
+    assert off - base < 250, (base, off)
+    assert gov - base < 900, (base, gov)
