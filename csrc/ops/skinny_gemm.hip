@@ -422,61 +422,6 @@ __device__ __forceinline__ void wide_store_x(bf16_t* xs, const u32x4_t (&xr)[XC]
   }
 }
 
-// Add-norm prologue (PRO): X = bf16(x + x2) chunk by chunk as it is staged
-// (x2 may be null: X = x), each thread's per-row sums of squares of the
-// staged X accumulated in ssr (a chunk's row does not change between groups),
-// and the workgroup that owns block 0 writes X back to xsum (the updated
-// residual stream; a different buffer from x, so no workgroup reads a row
-// another has already updated).
-template <int XC>
-__device__ __forceinline__ void wide_load_x2(u32x4_t (&x2r)[XC], const bf16_t* __restrict__ x2, int M, int ldx,
-                                             int kb, int tid, int nthreads, int u8) {
-#pragma unroll
-  for (int i = 0; i < XC; ++i) {
-    const int c = tid + i * nthreads;
-    const int row = c / u8, c8 = c % u8;
-    x2r[i] = *(const u32x4_t*)(x2 + (size_t)min(row, M - 1) * ldx + kb * 64 + c8 * 8);
-  }
-}
-
-__device__ __forceinline__ u32x4_t add_bf8(u32x4_t a, u32x4_t b, float& ss) {
-  u32x4_t r;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const float lo = __uint_as_float(a[e] << 16) + __uint_as_float(b[e] << 16);
-    const float hi = __uint_as_float(a[e] & 0xffff0000u) + __uint_as_float(b[e] & 0xffff0000u);
-    const uint32_t l = f2bf(lo), h = f2bf(hi);
-    const float lr = __uint_as_float(l << 16), hr = __uint_as_float(h << 16);
-    ss += lr * lr + hr * hr;
-    r[e] = l | (h << 16);
-  }
-  return r;
-}
-
-__device__ __forceinline__ void sq_bf8(u32x4_t a, float& ss) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const float lo = __uint_as_float(a[e] << 16), hi = __uint_as_float(a[e] & 0xffff0000u);
-    ss += lo * lo + hi * hi;
-  }
-}
-
-template <int MT, int U, int XC>
-__device__ __forceinline__ void pro_combine(u32x4_t (&xr)[XC], const u32x4_t (&x2r)[XC], bool has_x2,
-                                            float (&ssr)[XC], bf16_t* __restrict__ xsum, int M, int ldx, int kb,
-                                            int tid, int nthreads) {
-#pragma unroll
-  for (int i = 0; i < XC; ++i) {
-    if (has_x2) xr[i] = add_bf8(xr[i], x2r[i], ssr[i]);
-    else sq_bf8(xr[i], ssr[i]);
-    if (xsum) {
-      const int c = tid + i * nthreads;
-      const int row = c / (U * 8), c8 = c % (U * 8);
-      if (row < M) *(u32x4_t*)(xsum + (size_t)row * ldx + kb * 64 + c8 * 8) = xr[i];
-    }
-  }
-}
-
 template <int MT, int NT, int U, int PITCH>
 __device__ __forceinline__ void wide_mma(const WFrag<NT> (&f)[U], const bf16_t* xs, f32x16_t (&acc)[MT][NT], int r,
                                          int h) {
@@ -499,26 +444,20 @@ __device__ __forceinline__ void wide_mma(const WFrag<NT> (&f)[U], const bf16_t* 
 // `cur` + LDS buffer `xc`, (then stage the prefetched X into `xn` and hand it
 // over with the barrier).  X is issued before W: vmcnt retires in issue
 // order, so staging X never waits for the W prefetch.
-template <int MT, int NT, int U, int XC, int PITCH, bool PREFETCH, bool PRO>
+template <int MT, int NT, int U, int XC, int PITCH, bool PREFETCH>
 __device__ __forceinline__ void wide_step(const WFrag<NT> (&cur)[U], WFrag<NT> (&nxt)[U], const bf16_t* xc,
                                           bf16_t* xn, f32x16_t (&acc)[MT][NT], const u32x4_t* __restrict__ wbase,
                                           WStride ws, const bf16_t* __restrict__ x, int M, int ldx, int kb, int tid,
-                                          int nthreads, int lane, int r, int h, const bf16_t* __restrict__ x2,
-                                          bf16_t* __restrict__ xsum, float (&ssr)[XC]) {
+                                          int nthreads, int lane, int r, int h) {
   u32x4_t xr[XC];
-  u32x4_t x2r[PRO ? XC : 1];
   if constexpr (PREFETCH) {
     wide_load_x<MT, U, XC>(xr, x, M, ldx, kb + U, tid, nthreads);
-    if constexpr (PRO) {
-      if (x2) wide_load_x2<XC>(x2r, x2, M, ldx, kb + U, tid, nthreads, U * 8);
-    }
     wide_load_w<NT, U>(nxt, wbase, ws, kb + U, lane);
   }
   DB_FENCE();
   wide_mma<MT, NT, U, PITCH>(cur, xc, acc, r, h);
   DB_FENCE();
   if constexpr (PREFETCH) {
-    if constexpr (PRO) pro_combine<MT, U, XC>(xr, x2r, x2 != nullptr, ssr, xsum, M, ldx, kb + U, tid, nthreads);
     wide_store_x<MT, U, XC, PITCH>(xn, xr, tid, nthreads);
     __syncthreads();
   }
@@ -625,14 +564,13 @@ __device__ __forceinline__ void rs_finish(const float4 (&v)[RS_LMAX], float inv_
   }
 }
 
-template <int MT, int NT, int WV, int EPI, bool PRO = false>
+template <int MT, int NT, int WV, int EPI>
 __global__ void __launch_bounds__(64 * WV)
 skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int M,
                    int K, int N, int ldx, int ldy, int S, float* __restrict__ scratch, int* __restrict__ tickets,
                    int kmajor, const float* __restrict__ rs_part, int rs_nparts, float rs_inv_dim, float rs_eps,
-                   float* __restrict__ ss_out, const bf16_t* __restrict__ x2, bf16_t* __restrict__ xsum) {
+                   float* __restrict__ ss_out) {
   static_assert(EPI != EPI_SILU_MUL || NT == 2, "SiLU*up pairs a gate tile with an up tile");
-  static_assert(!PRO || EPI != EPI_RESID, "the add-norm prologue feeds a store or SiLU epilogue");
   constexpr int U = unroll_wide(NT);
   constexpr int PITCH = U * 64 + 8;                 // +16 B per row: conflict-free ds_read_b128
   constexpr int XBUF = MT * 32 * PITCH;
@@ -644,7 +582,6 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
   constexpr bool RS = EPI != EPI_RESID;
   __shared__ float s_rs[MT * 32];
   __shared__ float s_rtmp[RS ? WV * MT * 32 : 1];
-  __shared__ float s_ss[PRO ? MT * 32 : 1];   // PRO: per-row sums of squares of the staged X
   // EPI_RESID: each wave's residual tile [m][t][32 rows][32 cols], prefetched by LDS-DMA
   __shared__ __attribute__((aligned(16))) bf16_t s_res[EPI == EPI_RESID ? WV * MT * NT * 32 * 32 : 2];
   const int tid = threadIdx.x;
@@ -671,18 +608,8 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
   // Row-scale slot loads are issued first and reduced after the first X/W
   // loads are in flight (vmcnt retires in order: the reduction waits only for
   // them); the barrier below publishes s_rs.
-  const float* rs = (RS && (rs_part || PRO)) ? s_rs : nullptr;
+  const float* rs = (RS && rs_part) ? s_rs : nullptr;
   bf16_t* res_lds = s_res + (EPI == EPI_RESID ? wave * (MT * NT * 32 * 32) : 0);
-  // PRO: X = x + x2 as staged, its per-row sums of squares, and (block 0) the
-  // write-back of X; S == 1 (the plan guarantees it), so this workgroup sees
-  // every column of its rows
-  float ssr[XC];
-#pragma unroll
-  for (int i = 0; i < XC; ++i) ssr[i] = 0.f;
-  bf16_t* const xs_out = (PRO && blockIdx.x == 0) ? xsum : nullptr;
-  if constexpr (PRO) {
-    for (int i = tid; i < MT * 32; i += NTHREADS) s_ss[i] = 0.f;
-  }
   {
     // row-scale slot loads and the residual tile's LDS-DMA first: older than
     // the X loads, so the X wait below covers them as well
@@ -704,46 +631,30 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
           }
     }
     u32x4_t xr[XC];
-    u32x4_t x2r[PRO ? XC : 1];
     wide_load_x<MT, U, XC>(xr, x, M, ldx, kb0, tid, NTHREADS);
-    if constexpr (PRO) {
-      if (x2) wide_load_x2<XC>(x2r, x2, M, ldx, kb0, tid, NTHREADS, U * 8);
-    }
     wide_load_w<NT, U>(fa, wbase, ws, kb0, lane);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (RS) {
-      if (rs_part && !PRO) rs_finish<MT, NTHREADS>(rsv, rs_inv_dim, rs_eps, s_rs, s_rtmp, tid);
+      if (rs_part) rs_finish<MT, NTHREADS>(rsv, rs_inv_dim, rs_eps, s_rs, s_rtmp, tid);
     }
-    if constexpr (PRO) pro_combine<MT, U, XC>(xr, x2r, x2 != nullptr, ssr, xs_out, M, ldx, kb0, tid, NTHREADS);
     wide_store_x<MT, U, XC, PITCH>(xs, xr, tid, NTHREADS);
     __syncthreads();
   }
   int g = 0, kb = kb0;
   for (; g + 3 <= G; g += 2, kb += 2 * U) {
-    wide_step<MT, NT, U, XC, PITCH, true, PRO>(fa, fb, xs, xs + XBUF, acc, wbase, ws, x, M, ldx, kb, tid, NTHREADS,
-                                               lane, r, h, x2, xs_out, ssr);
-    wide_step<MT, NT, U, XC, PITCH, true, PRO>(fb, fa, xs + XBUF, xs, acc, wbase, ws, x, M, ldx, kb + U, tid,
-                                               NTHREADS, lane, r, h, x2, xs_out, ssr);
+    wide_step<MT, NT, U, XC, PITCH, true>(fa, fb, xs, xs + XBUF, acc, wbase, ws, x, M, ldx, kb, tid, NTHREADS, lane,
+                                          r, h);
+    wide_step<MT, NT, U, XC, PITCH, true>(fb, fa, xs + XBUF, xs, acc, wbase, ws, x, M, ldx, kb + U, tid, NTHREADS,
+                                          lane, r, h);
   }
   if (G - g == 2) {
-    wide_step<MT, NT, U, XC, PITCH, true, PRO>(fa, fb, xs, xs + XBUF, acc, wbase, ws, x, M, ldx, kb, tid, NTHREADS,
-                                               lane, r, h, x2, xs_out, ssr);
-    wide_step<MT, NT, U, XC, PITCH, false, PRO>(fb, fa, xs + XBUF, xs, acc, wbase, ws, x, M, ldx, kb + U, tid,
-                                                NTHREADS, lane, r, h, x2, xs_out, ssr);
+    wide_step<MT, NT, U, XC, PITCH, true>(fa, fb, xs, xs + XBUF, acc, wbase, ws, x, M, ldx, kb, tid, NTHREADS, lane,
+                                          r, h);
+    wide_step<MT, NT, U, XC, PITCH, false>(fb, fa, xs + XBUF, xs, acc, wbase, ws, x, M, ldx, kb + U, tid, NTHREADS,
+                                           lane, r, h);
   } else {
-    wide_step<MT, NT, U, XC, PITCH, false, PRO>(fa, fb, xs, xs + XBUF, acc, wbase, ws, x, M, ldx, kb, tid, NTHREADS,
-                                                lane, r, h, x2, xs_out, ssr);
-  }
-  if constexpr (PRO) {
-    // row scales from the staged X: per-thread partial sums -> LDS -> rsqrt
-#pragma unroll
-    for (int i = 0; i < XC; ++i) {
-      const int row = (tid + i * NTHREADS) / (U * 8);
-      atomicAdd(&s_ss[row], ssr[i]);
-    }
-    __syncthreads();
-    for (int i = tid; i < MT * 32; i += NTHREADS) s_rs[i] = rsqrtf(s_ss[i] * rs_inv_dim + rs_eps);
-    __syncthreads();
+    wide_step<MT, NT, U, XC, PITCH, false>(fa, fb, xs, xs + XBUF, acc, wbase, ws, x, M, ldx, kb, tid, NTHREADS, lane,
+                                           r, h);
   }
 
   if constexpr (EPI == EPI_RESID) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // residual tile landed
@@ -809,8 +720,6 @@ struct Args {
   float rs_inv_dim = 0.f;
   float rs_eps = 0.f;
   float* ss_out = nullptr;
-  const void* x2 = nullptr;         // add-norm prologue (wide kernel, PRO)
-  void* xsum = nullptr;
 };
 
 template <int MT, int NT, int KS, int EPI>
@@ -859,14 +768,13 @@ hipError_t launch_mt(int mt, int ks, const Args& a, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
-template <int MT, int NT, int EPI, bool PRO = false>
+template <int MT, int NT, int EPI>
 hipError_t launch_wide(int wv, const Args& a, hipStream_t s) {
   const int blocks = (a.N / 32) / NT / wv * a.S;
 #define MIVGPU_LAUNCH_WIDE(WV)                                                                                \
-  hipLaunchKernelGGL((skinny_wide_kernel<MT, NT, WV, EPI, PRO>), dim3(blocks), dim3(64 * WV), 0, s,          \
+  hipLaunchKernelGGL((skinny_wide_kernel<MT, NT, WV, EPI>), dim3(blocks), dim3(64 * WV), 0, s,               \
                      (const u32x4_t*)a.wp, (const bf16_t*)a.x, (bf16_t*)a.y, a.M, a.K, a.N, a.ldx, a.ldy, a.S, \
-                     a.scratch, a.tickets, a.kmajor, a.rs_part, a.rs_nparts, a.rs_inv_dim, a.rs_eps, a.ss_out, \
-                     (const bf16_t*)a.x2, (bf16_t*)a.xsum)
+                     a.scratch, a.tickets, a.kmajor, a.rs_part, a.rs_nparts, a.rs_inv_dim, a.rs_eps, a.ss_out)
   switch (wv) {
     case 1: MIVGPU_LAUNCH_WIDE(1); break;
     case 2: MIVGPU_LAUNCH_WIDE(2); break;
@@ -1096,39 +1004,6 @@ int mivgpu_pack_weight(const void* w, void* wp, int N, int K, hipStream_t s) {
 int mivgpu_skinny_gemm_norm(const void* wp, const void* x, void* y, int M, int K, int N, int ldx, int ldy, int epi,
                             int nt, int ks, int S, int variant, float* scratch, int* tickets, const float* rs_part,
                             int rs_nparts, float rs_inv_dim, float rs_eps, float* ss_out, hipStream_t s);
-
-// Add-norm prologue (wide kernel): Y = RMSNorm(x + x2) . W^T with the norm
-// weight folded into W's columns -- X = bf16(x + x2) as it is staged (x2 may
-// be null), its per-row rsqrt(mean(X^2) + eps) applied in the epilogue, X
-// written to xsum (may be null; must not alias x) -- in one launch: the
-// add + RMSNorm kernel between a projection and the next one goes away.
-// M <= 64, epi 0 (store) or 1 (SiLU*up), and the plan must resolve to the
-// wide kernel without an inter-workgroup split (S = 1: every workgroup sees
-// all of K); hipErrorInvalidValue otherwise.
-int mivgpu_skinny_gemm_addnorm(const void* wp, const void* x, const void* x2, void* xsum, void* y, int M, int K,
-                               int N, int ldx, int ldy, int epi, int ks, float eps, hipStream_t s) {
-  if (M <= 0 || M > 64 || K <= 0 || (K & 63) || N <= 0 || (N & 31) || ldx < K || (ldx & 7) || (ldy & 7))
-    return (int)hipErrorInvalidValue;
-  if (epi != EPI_STORE && epi != EPI_SILU_MUL) return (int)hipErrorInvalidValue;
-  if (xsum != nullptr && xsum == x) return (int)hipErrorInvalidValue;
-  int nt = 0, S = 1;
-  if (resolve(M, K, N, epi, &nt, &ks, &S, 2) != 2 || S != 1) return (int)hipErrorInvalidValue;
-  if (epi == EPI_SILU_MUL ? ldy < N / 2 : ldy < N) return (int)hipErrorInvalidValue;
-  Args a{wp, x, y, M, K, N, ldx, ldy, 1, nullptr, nullptr, false, use_kmajor() ? 1 : 0};
-  a.rs_inv_dim = 1.f / (float)K;
-  a.rs_eps = eps;
-  a.x2 = x2;
-  a.xsum = xsum;
-  const int mt = mt_of(M);
-  hipError_t e = hipErrorInvalidValue;
-  if (epi == EPI_SILU_MUL)
-    e = mt == 1 ? launch_wide<1, 2, EPI_SILU_MUL, true>(ks, a, s) : launch_wide<2, 2, EPI_SILU_MUL, true>(ks, a, s);
-  else if (nt == 2)
-    e = mt == 1 ? launch_wide<1, 2, EPI_STORE, true>(ks, a, s) : launch_wide<2, 2, EPI_STORE, true>(ks, a, s);
-  else
-    e = mt == 1 ? launch_wide<1, 1, EPI_STORE, true>(ks, a, s) : launch_wide<2, 1, EPI_STORE, true>(ks, a, s);
-  return (int)e;
-}
 
 // epi: 0 = store Y[M][N] (ldy >= N);  1 = SiLU(gate)*up -> Y[M][N/2] for an
 // interleaved gate/up weight.  variant: 0 auto, 1 classic, 2 wide workgroups

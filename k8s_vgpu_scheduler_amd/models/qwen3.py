@@ -140,19 +140,10 @@ class Qwen3Decoder:
         self.norm_fused = skinny and os.environ.get("MIVGPU_NORM_FUSED", "0") == "1"
         if self.norm_fused:
             self.skinny_o = True
-        # Add-norm prologue (MIVGPU_NORM_PROLOGUE=1): qkv, gate_up and lm_head
-        # on the wide kernel compute RMSNorm(res + delta) of their own input as
-        # they stage it (csrc/ops/skinny_gemm.hip mivgpu_skinny_gemm_addnorm),
-        # the norm weights folded into their columns; the residual stream
-        # ping-pongs between two buffers.  No add+RMSNorm launch remains.
-        self.norm_pro = (skinny and not self.norm_fused and batch <= 64
-                         and os.environ.get("MIVGPU_NORM_PROLOGUE", "0") == "1")
-        if self.norm_pro:
-            self.skinny_qkv = self.skinny_gate_up = True
         if self.skinny:
             # Keep only the packed copies (no duplicate 16 GB of weights).
             for lw in self.w.layers:
-                if self.norm_fused or self.norm_pro:
+                if self.norm_fused:
                     lw["pqkv"] = ops.PackedLinear(lw.pop("wqkv"), col_scale=lw["ln1"])
                     lw["pgu"] = ops.PackedLinear(lw.pop("wgu"), silu_mul=True, col_scale=lw["ln2"])
                 else:
@@ -169,8 +160,7 @@ class Qwen3Decoder:
                     keep = ops.visible_cus() > int(os.environ.get("MIVGPU_SLICE_PLAN_CUS", "96"))
                     lw["po"] = ops.PackedLinear(lw["wo"] if keep else lw.pop("wo"))
                 lw["pd"] = ops.PackedLinear(lw.pop("wd"))
-            self.p_lm = ops.PackedLinear(self.w.lm_head, col_scale=self.w.final_norm
-                                         if (self.norm_fused or self.norm_pro) else None)
+            self.p_lm = ops.PackedLinear(self.w.lm_head, col_scale=self.w.final_norm if self.norm_fused else None)
             if not cfg.tie_embeddings:
                 self.w.lm_head = None
             torch.cuda.empty_cache()
@@ -199,9 +189,6 @@ class Qwen3Decoder:
         self.logits = torch.zeros(batch, cfg.vocab, dtype=dt, device=self.device)
         if self.norm_fused or self.skinny_qkv:
             self.qkv_buf = torch.zeros(batch, cfg.qkv_dim, dtype=dt, device=self.device)
-        if self.norm_pro:
-            self.res_b = torch.zeros(batch, h, dtype=dt, device=self.device)   # the residual's other buffer
-            self._unit_norm = torch.ones(h, dtype=dt, device=self.device)     # prefill: weights already folded
         if self.norm_fused:
             l0 = self.w.layers[0]
             self.slots_o, self.slots_d = l0["po"].slots(batch), l0["pd"].slots(batch)
@@ -284,38 +271,9 @@ class Qwen3Decoder:
         self.seqlens.add_(1)
         return logits
 
-    def _step_norm_prologue(self):
-        """Decode step with the add-norm prologue: six launches per layer (qkv,
-        attention, combine, o_proj, gate_up+SiLU, down); each projection that
-        follows a residual add computes RMSNorm(res + delta) itself and writes
-        res + delta to the residual's other buffer."""
-        cfg, w = self.cfg, self.w
-        eps = cfg.eps
-        torch.index_select(w.embed, 0, self.tokens, out=self.res)
-        cur, other = self.res, self.res_b
-        delta = None                      # the previous layer's MLP output, not yet added
-        for li, lw in enumerate(w.layers):
-            if delta is None:
-                qkv = lw["pqkv"].addnorm_call(cur, out=self.qkv_buf, eps=eps)
-            else:
-                qkv = lw["pqkv"].addnorm_call(cur, out=self.qkv_buf, eps=eps, x2=delta, xsum=other)
-                cur, other = other, cur
-            self._attention(li, lw, qkv)
-            o = lw["po"](self.attn, out=self.o_out) if self.skinny_o else F.linear(self.attn, lw["wo"])
-            lw["pgu"].addnorm_call(cur, out=self.act, eps=eps, x2=o, xsum=other)
-            cur, other = other, cur
-            delta = lw["pd"](self.act, out=self.mlp_out)
-        logits = self.p_lm.addnorm_call(cur, out=self.logits, eps=eps, x2=delta)
-        torch.argmax(logits, dim=-1, out=self.tokens)
-        self.pos.add_(1)
-        self.seqlens.add_(1)
-        return logits
-
     def _step_impl(self):
         if self.norm_fused:
             return self._step_norm_fused()
-        if self.norm_pro:
-            return self._step_norm_prologue()
         cfg, w = self.cfg, self.w
         # every graph node a kernel: the step's state moves through kernels that
         # write their outputs in place (index_select / argmax with out=), never
@@ -458,26 +416,17 @@ class Qwen3Decoder:
             self._pf[Lb] = bufs
         return bufs
 
-    def _nw(self, wn):
-        """A norm weight as the prefill applies it: with the add-norm prologue
-        it is already folded into the next projection's packed columns."""
-        if not self.norm_pro:
-            return wn
-        if getattr(self, "_unit_norm", None) is None:
-            self._unit_norm = torch.ones_like(wn)
-        return self._unit_norm
-
     def _prefill_impl(self, bufs: dict, b: int):
         cfg, w = self.cfg, self.w
         res = torch.index_select(w.embed, 0, bufs["ids"])
-        h = self._norm(res, self._nw(w.layers[0]["ln1"]))
+        h = self._norm(res, w.layers[0]["ln1"])
         for li, lw in enumerate(w.layers):
             q, k, v = self._prefill_qk(li, lw, self._proj(lw, "qkv", h), bufs["pos"], b)
             o = self._proj(lw, "o", self._prefill_attention(q, k, v, bufs["mask"]))
-            h = self._add_norm(o, res, self._nw(lw["ln2"]))
+            h = self._add_norm(o, res, lw["ln2"])
             d = self._proj(lw, "d", self._proj(lw, "gu", h))
             nxt = w.layers[li + 1]["ln1"] if li + 1 < len(w.layers) else w.final_norm
-            h = self._add_norm(d, res, self._nw(nxt))
+            h = self._add_norm(d, res, nxt)
         last = torch.index_select(h, 0, bufs["last"])
         logits = self._rows(self.p_lm, last) if self.skinny else F.linear(last, w.lm_head)
         # in-place kernels only (no copy nodes in a captured graph)

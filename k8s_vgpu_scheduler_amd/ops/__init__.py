@@ -49,7 +49,6 @@ def lib():
         L.mivgpu_pack_weight.argtypes = [vp, vp, i, i, vp]
         L.mivgpu_skinny_gemm.argtypes = [vp, vp, vp, i, i, i, i, i, i, i, i, i, i, vp, vp, vp]
         L.mivgpu_skinny_gemm_norm.argtypes = [vp, vp, vp, i, i, i, i, i, i, i, i, i, i, vp, vp, vp, i, f, f, vp, vp]
-        L.mivgpu_skinny_gemm_addnorm.argtypes = [vp, vp, vp, vp, vp, i, i, i, i, i, i, i, f, vp]
         ip, lp = ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_longlong)
         L.mivgpu_mfma_burn.argtypes = [vp, i, i, ctypes.c_uint, vp]
         L.mivgpu_mfma_burn_flops.argtypes = [i, i]
@@ -63,7 +62,6 @@ def lib():
                    "mivgpu_skinny_max_m", "mivgpu_skinny_plan", "mivgpu_mfma_burn",
                    "mivgpu_stream_copy", "mivgpu_stream_read", "mivgpu_ops_visible_cus",
                    "mivgpu_ops_kv_packed", "mivgpu_decode_attention_fused", "mivgpu_skinny_gemm_norm",
-                   "mivgpu_skinny_gemm_addnorm",
                    "mivgpu_prefill_qk_norm_rope_kv"):
             getattr(L, fn).restype = ctypes.c_int
         _lib = L
@@ -443,27 +441,6 @@ class PackedLinear:
         """Sum-of-squares slots a residual call (``norm_call(residual=True)``)
         writes: one per wave-group of the wide plan."""
         return (self.N // 32) // skinny_plan(M, self.K, self.N, EPI_RESID, variant=VARIANT_WIDE)["nt"]
-
-    def addnorm_call(self, x: torch.Tensor, out: torch.Tensor, eps: float, x2: torch.Tensor | None = None,
-                     xsum: torch.Tensor | None = None, ks: int = 0):
-        """``out = RMSNorm(x + x2) . W^T`` in one launch (csrc/ops/skinny_gemm.hip
-        mivgpu_skinny_gemm_addnorm): the RMSNorm weight must have been folded
-        into W (``col_scale``); ``x + x2`` (rounded to bf16) is written to
-        ``xsum`` when given (the updated residual stream; not ``x`` itself).
-        M <= 64, wide kernel without inter-workgroup split."""
-        M = x.shape[0]
-        for t in (x, x2, xsum):
-            if t is not None and (t.dim() != 2 or tuple(t.shape) != (M, self.K) or not t.is_contiguous()):
-                raise ValueError(f"addnorm: operands must be contiguous [M, {self.K}], got {tuple(t.shape)}")
-        if not 0 < M <= 64:
-            raise ValueError(f"addnorm: M must be 1..64, got {M}")
-        if xsum is not None and xsum.data_ptr() == x.data_ptr():
-            raise ValueError("addnorm: xsum must not alias x")
-        _check(lib().mivgpu_skinny_gemm_addnorm(_p(self.wp), _p(x), _p(x2) if x2 is not None else None,
-                                                _p(xsum) if xsum is not None else None, _p(out), M, self.K, self.N,
-                                                x.stride(0), out.stride(0), self.epi, ks, float(eps), _stream()),
-               "skinny_gemm_addnorm")
-        return out
 
     def norm_call(self, x: torch.Tensor, out: torch.Tensor, row_scale: tuple | None = None,
                   residual: bool = False, ss_out: torch.Tensor | None = None, ks: int = 0, S: int = 0):

@@ -14,7 +14,6 @@
 #   kernels_full  the same on the whole GPU (kernel trace: durations and the gaps between them)
 #   pmc         PMC passes over a 64-CU decode step (one counter group per pass)
 #   membw       partition read ceilings (bench/membw.py)
-#   normpro     add-norm prologue: numerics + decode A/B (whole GPU, 64 CUs) + kernel trace
 #   mall        projection GEMMs cold vs with their weights prefetched into the Infinity Cache
 #   serving     TTFT / per-token latency, native vs vGPU slices (bench/serving.py)
 #   mixed       governed server + 3 governed decode tenants; 8 x 12 % temporal over 600 steps
@@ -82,18 +81,6 @@ case $suite in
       python -u bench.py --slices 8 --rounds temporal --steps 600 --out "$out/device_inst20.json"
     MIVGPU_SHARE_EST=instant MIVGPU_SHARE_TAU_MS=20 step 400 host_inst20 \
       python -u bench.py --slices 8 --rounds temporal --steps 600 --out "$out/host_inst20.json" ;;
-  normpro)
-    # add-norm prologue: numerics, then decode A/B on the whole GPU and a 64-CU slice
-    step 600 tests python -u -m pytest tests/test_ops_gpu.py -v --timeout 300 --timeout-method thread \
-      -k "addnorm or norm_prologue or norm_fused or qkv_on_wide"
-    for pro in 0 1; do
-      MIVGPU_NORM_PROLOGUE=$pro step 300 "full_pro$pro" python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 200
-      HSA_CU_MASK=0:0-63 MIVGPU_NORM_PROLOGUE=$pro step 300 "cu64_pro$pro" \
-        python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 100
-    done
-    cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
-    MIVGPU_NORM_PROLOGUE=1 step 240 prof_pro rocprofv3 --kernel-trace --stats --output-format csv \
-      -d "$out/prof_pro" -o run -- python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 20 ;;
   mall)
     step 300 mall python -u scripts/probe/mall_prefetch.py --out "$out/mall.json" ;;
   membw)

@@ -392,71 +392,6 @@ def test_decoder_norm_fused_matches_reference(monkeypatch):
         b.tokens.copy_(a.tokens)
 
 
-@pytest.mark.parametrize("M,N,K,silu,has_x2", [(1, 6144, 4096, False, True), (32, 6144, 4096, False, True),
-                                               (40, 2048, 1024, False, True), (7, 4096, 2048, True, True),
-                                               (32, 24576, 4096, True, True), (5, 2048, 1024, False, False)])
-def test_skinny_addnorm_prologue(ops, M, N, K, silu, has_x2):
-    """Y = RMSNorm(x + x2) . W^T in one launch (norm weight folded into W's
-    columns), against the fp32 reference add + RMSNorm + GEMM; the written
-    residual is exactly bf16(x + x2)."""
-    g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
-    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
-    x2 = torch.randn(M, K, device="cuda", generator=g).bfloat16() if has_x2 else None
-    wn = (1 + 0.1 * torch.randn(K, device="cuda", generator=g)).bfloat16()
-    w = (torch.randn(N, K, device="cuda", generator=g) * 0.02).bfloat16()
-    lin = ops.PackedLinear(w, silu_mul=silu, col_scale=wn)
-    out = torch.empty(M, N // 2 if silu else N, device="cuda", dtype=torch.bfloat16)
-    xsum = torch.empty(M, K, device="cuda", dtype=torch.bfloat16) if has_x2 else None
-    lin.addnorm_call(x, out=out, eps=1e-6, x2=x2, xsum=xsum)
-    torch.cuda.synchronize()
-    s = (x.float() + x2.float()).bfloat16() if has_x2 else x
-    if has_x2:
-        assert torch.equal(xsum, s)
-    h = ref.rmsnorm(s, wn, 1e-6)
-    y = h.float() @ w.float().t()
-    if silu:
-        exp = ref.silu_mul(y.bfloat16())
-    else:
-        exp = y
-    _close(out, exp, 2e-2)
-
-
-def test_decoder_norm_prologue_matches_reference(monkeypatch):
-    """Add-norm prologue (MIVGPU_NORM_PROLOGUE=1): qkv / gate_up / lm_head
-    compute RMSNorm(res + delta) themselves; 3 eager steps and 2 graph replays
-    against the fp32 reference decoder, batch 5 (one M-tile) and 40 (two)."""
-    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
-
-    monkeypatch.setenv("MIVGPU_NORM_PROLOGUE", "1")
-    for B in (5, 40):
-        a = Qwen3Decoder(QWEN3_TINY, batch=B, max_ctx=64, device="cuda", native=True, seed=9)
-        assert a.norm_pro and "pqkv" in a.w.layers[0] and "wqkv" not in a.w.layers[0]
-        b = Qwen3Decoder(QWEN3_TINY, batch=B, max_ctx=64, device="cuda", native=False, seed=9)
-        a.fill_context(12)
-        b.fill_context(12)
-        for i in range(5):
-            if i == 3:
-                a.capture()
-            la, lb = a.step(), b.step()
-            _close(la, lb, 5e-2)
-            b.tokens.copy_(a.tokens)
-
-
-def test_prefill_with_norm_prologue_matches_reference(monkeypatch):
-    """Prompt processing when the norm weights live in the packed columns:
-    the same logits as the fp32 reference decoder's prefill."""
-    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
-
-    monkeypatch.setenv("MIVGPU_NORM_PROLOGUE", "1")
-    prompt = list(range(5, 45))
-    a = Qwen3Decoder(QWEN3_TINY, batch=1, max_ctx=96, device="cuda", native=True, seed=10)
-    b = Qwen3Decoder(QWEN3_TINY, batch=1, max_ctx=96, device="cuda", native=False, seed=10)
-    assert a.norm_pro
-    la, lb = a.prefill(prompt).float(), b.prefill(prompt).float()
-    cos = torch.nn.functional.cosine_similarity(la, lb, dim=0).item()
-    assert cos > 0.999, cos
-
-
 def test_decoder_qkv_on_wide_kernel_matches_reference(monkeypatch):
     """Small-partition plan (qkv on the wide skinny kernel, forced here on the
     whole GPU with MIVGPU_QKV_WIDE_CUS): 3 steps against the fp32 reference."""
