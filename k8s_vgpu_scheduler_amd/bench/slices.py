@@ -215,6 +215,11 @@ def child_main(argv):
     cmd = sys.stdin.readline().strip()
     if cmd != "LOAD":
         return 0
+    tq = os.environ.get("MIVGPU_BENCH_TENANT_QUEUES")
+    if tq:
+        # a tenant raising its own hardware queue count before the runtime
+        # starts (tests: the grant's cap must hold against it)
+        os.environ["GPU_MAX_HW_QUEUES"] = tq
     import torch
 
     from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_8B, QWEN3_TINY, Qwen3Decoder

@@ -12,7 +12,7 @@
 #   probes      KFD occupancy + topology probes (scripts/probe/*.py)
 #   kernels     rocprofv3 --kernel-trace --stats of one 64-CU slice decode step
 #   kernels_full  the same on the whole GPU (kernel trace: durations and the gaps between them)
-#   pmc         PMC passes over a 64-CU decode step (one counter group per pass)
+#   pmc [cfg..] PMC passes over a decode step: whole GPU, 64 CUs, 32 CUs (one counter group per pass)
 #   membw       partition read ceilings (bench/membw.py)
 #   mall        projection GEMMs cold vs with their weights prefetched into the Infinity Cache
 #   serving     TTFT / per-token latency, native vs vGPU slices (bench/serving.py)
@@ -67,11 +67,22 @@ case $suite in
     MIVGPU_NORM_FUSED=1 step 240 prof_fused rocprofv3 --kernel-trace --stats --output-format csv \
       -d "$out/prof_fused" -o run -- python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 20 ;;
   pmc)
-    cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R HSA_CU_MASK=0:0-63
+    # per-kernel counters of one decode step for each partition size: the whole
+    # GPU (1 slice), 64 CUs (4 slices) and 32 CUs (8 slices); one counter group
+    # per pass.  pmc [full|cu64|cu32 ...]
+    cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
     dec="python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 3 --warmup 1 --no-graph"
-    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$out/a" -o run -- $dec > "$out/a.log" 2>&1 || exit 1
-    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS \
-      --kernel-trace --output-format csv -d "$out/b" -o run -- $dec > "$out/b.log" 2>&1 || exit 1 ;;
+    for cfg in ${@:-full cu64 cu32}; do
+      case $cfg in full) unset HSA_CU_MASK ;; cu64) export HSA_CU_MASK=0:0-63 ;; cu32) export HSA_CU_MASK=0:0-31 ;;
+        *) echo "unknown $cfg"; exit 2 ;; esac
+      timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv \
+        -d "$out/$cfg/a" -o run -- $dec > "$out/$cfg.a.log" 2>&1 || exit 1
+      timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_BF16 \
+        SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS --kernel-trace --output-format csv -d "$out/$cfg/b" -o run -- $dec \
+        > "$out/$cfg.b.log" 2>&1 || exit 1
+      # per-kernel summary; the raw CSVs are tens of MB per configuration
+      python3 "$R/scripts/probe/pmc_summary.py" "$out/$cfg" > "$out/$cfg.json" && rm -rf "$out/$cfg"
+    done ;;
   govmodes)
     # A/B of the governor's bucket (host / device) and share estimator on 8 x 12 %
     step 400 host_ratio python -u bench.py --slices 8 --rounds temporal --steps 600 --out "$out/host_ratio.json"

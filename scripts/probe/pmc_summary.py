@@ -1,0 +1,49 @@
+"""Summarise rocprofv3 --pmc passes (scripts/gpu.sh pmc) into per-kernel JSON.
+
+``python scripts/probe/pmc_summary.py <dir>`` reads every
+``*counter_collection.csv`` under ``<dir>`` (one counter group per pass
+subdirectory) and prints, per kernel name (first 90 characters), the number of
+dispatches, the mean duration and the mean of each counter per dispatch, plus
+FETCH_SIZE / duration as the achieved fetch bandwidth (FETCH_SIZE is in KiB).
+The raw CSVs (tens of MB, mostly the random-init kernels' template names) are
+not kept.
+"""
+
+from __future__ import annotations
+
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def summarise(root: str) -> dict:
+    per = defaultdict(lambda: {"dispatches": set(), "dur_ns": {}, "counters": defaultdict(float)})
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                name = r["Kernel_Name"][:90]
+                d = per[name]
+                key = (f, r["Dispatch_Id"])
+                d["dispatches"].add(key)
+                d["dur_ns"][key] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                d["counters"][r["Counter_Name"]] += float(r["Counter_Value"])
+    out = {}
+    for name, d in per.items():
+        # every pass runs the same dispatches: per-dispatch means over the pass that holds the counter
+        passes = {k[0] for k in d["dispatches"]}
+        n = max(1, len(d["dispatches"]) // max(1, len(passes)))
+        dur = sum(d["dur_ns"].values()) / max(1, len(d["dur_ns"]))
+        row = {"dispatches": n, "mean_us": round(dur / 1e3, 2)}
+        for c, v in d["counters"].items():
+            row[c] = round(v / n, 1)
+        if "FETCH_SIZE" in row and dur > 0:
+            row["fetch_TBps"] = round(row["FETCH_SIZE"] * 1024 / dur / 1e3, 2)
+        out[name] = row
+    return dict(sorted(out.items(), key=lambda kv: -kv[1]["mean_us"] * kv[1]["dispatches"]))
+
+
+if __name__ == "__main__":
+    print(json.dumps(summarise(sys.argv[1]), indent=1))
