@@ -690,6 +690,129 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
   if (lane == 0) tickets[vgroup] = 0;
 }
 
+// ============================================================================
+// K-split wide workgroups ("widek", variant 3) for the small projections of a
+// decode step on the whole chip (qkv 50 MB, o_proj 34 MB, down 101 MB: 128-192
+// n-tiles for 256 CUs).  The wide kernel above gives each wave its own n-tile
+// over the workgroup's whole k-range, so these shapes ran 96-256 workgroups of
+// 1-2 waves -- few bytes in flight per CU -- or split K across workgroups with
+// device-scope atomics and a last-arriver epilogue on the critical path.
+// Here KW waves share ONE n-tile and interleave its k-blocks (wave kw takes
+// k-blocks kw*U.. of every group of KW*U), all fed from one LDS X tile of the
+// group's KW*U k-blocks; the KW partial accumulators are summed through LDS at
+// the end, so K is split KW ways inside the workgroup with no global traffic.
+// An inter-workgroup split S (as above) can still be added to fill the chip.
+template <int MT, int KW>
+__global__ void __launch_bounds__(64 * KW)
+skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int M,
+                    int K, int N, int ldx, int ldy, int S, float* __restrict__ scratch, int* __restrict__ tickets,
+                    int kmajor) {
+  constexpr int NT = 1;
+  constexpr int U = 2;                               // k-blocks per wave per group
+  constexpr int GK = KW * U;                         // k-blocks per group (the X tile)
+  constexpr int PITCH = GK * 64 + 8;                 // +16 B per row: conflict-free ds_read_b128
+  constexpr int XBUF = MT * 32 * PITCH;
+  constexpr int NTHREADS = 64 * KW;
+  constexpr int XC = MT * GK * 256 / NTHREADS;       // X chunks per thread per group
+  static_assert(XC * NTHREADS == MT * GK * 256, "X tile must split evenly over the workgroup");
+  static_assert(KW * MT * 16 * 64 * 4 <= 2 * XBUF * 2, "the k-wave reduction reuses the X buffers");
+  __shared__ __attribute__((aligned(16))) bf16_t xs[2 * XBUF];
+  const int tid = threadIdx.x;
+  const int kw = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int KB = K >> 6;
+  const int tile0 = blockIdx.x / S, split = blockIdx.x % S;
+  const WStride ws = kmajor ? WStride{256, (size_t)(N >> 5) * 256} : WStride{(size_t)KB * 256, 256};
+  const u32x4_t* wbase = wp + (size_t)tile0 * ws.tile;
+  const int kb0 = (int)((long long)KB * split / S), kb1 = (int)((long long)KB * (split + 1) / S);
+  const int G = (kb1 - kb0) / GK;                    // the plan makes (kb1 - kb0) a multiple of GK, >= GK
+
+  f32x16_t acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[m][0][e] = 0.f;
+
+  WFrag<NT> fa[U], fb[U];
+  {
+    u32x4_t xr[XC];
+    wide_load_x<MT, GK, XC>(xr, x, M, ldx, kb0, tid, NTHREADS);
+    wide_load_w<NT, U>(fa, wbase, ws, kb0 + kw * U, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    wide_store_x<MT, GK, XC, PITCH>(xs, xr, tid, NTHREADS);
+    __syncthreads();
+  }
+  // one group: prefetch the next group's X then this wave's W, MFMAs of this
+  // group from registers + this wave's columns of the LDS tile, stage X
+  auto step = [&](const WFrag<NT>(&cur)[U], WFrag<NT>(&nxt)[U], const bf16_t* xc, bf16_t* xn, int kb,
+                  bool prefetch) {
+    u32x4_t xr[XC];
+    if (prefetch) {
+      wide_load_x<MT, GK, XC>(xr, x, M, ldx, kb + GK, tid, NTHREADS);
+      wide_load_w<NT, U>(nxt, wbase, ws, kb + GK + kw * U, lane);
+    }
+    DB_FENCE();
+    wide_mma<MT, NT, U, PITCH>(cur, xc + kw * U * 64, acc, r, h);
+    DB_FENCE();
+    if (prefetch) {
+      wide_store_x<MT, GK, XC, PITCH>(xn, xr, tid, NTHREADS);
+      __syncthreads();
+    }
+  };
+  int g = 0, kb = kb0;
+  for (; g + 3 <= G; g += 2, kb += 2 * GK) {
+    step(fa, fb, xs, xs + XBUF, kb, true);
+    step(fb, fa, xs + XBUF, xs, kb + GK, true);
+  }
+  if (G - g == 2) {
+    step(fa, fb, xs, xs + XBUF, kb, true);
+    step(fb, fa, xs + XBUF, xs, kb + GK, false);
+  } else {
+    step(fa, fb, xs, xs + XBUF, kb, false);
+  }
+  // sum the KW waves' partial tiles through LDS (the X buffers are free now)
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(xs);
+  if (kw > 0) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) red[(((kw - 1) * MT + m) * 16 + e) * 64 + lane] = acc[m][0][e];
+  }
+  __syncthreads();
+  if (kw > 0) return;
+#pragma unroll
+  for (int w = 1; w < KW; ++w)
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[m][0][e] += red[(((w - 1) * MT + m) * 16 + e) * 64 + lane];
+  if (S == 1) {
+    wide_epilogue<MT, NT, EPI_STORE>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, tile0, r,
+                                     h, nullptr, nullptr, nullptr);
+    return;
+  }
+  constexpr int SLAB = MT * NT * 16 * 64;
+  float* sc = scratch + (size_t)tile0 * SLAB;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) atomicAdd(sc + (m * 16 + e) * 64 + lane, acc[m][0][e]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int ticket = 0;
+  if (lane == 0) ticket = atomicAdd(tickets + tile0, 1);
+  ticket = __shfl(ticket, 0, 64);
+  if (ticket != S - 1) return;
+  wide_epilogue<MT, NT, EPI_STORE>(
+      [&](int m, int t, int e) {
+        return __hip_atomic_load(sc + ((m * NT + t) * 16 + e) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      },
+      y, M, ldy, tile0, tile0, r, h, nullptr, nullptr, nullptr);
+#pragma unroll
+  for (int i = 0; i < SLAB / 64; ++i) sc[i * 64 + lane] = 0.f;
+  if (lane == 0) tickets[tile0] = 0;
+}
+
 // Pack W[N][K] (row-major bf16) into the fragment order above.
 __global__ void pack_weight_kernel(const bf16_t* __restrict__ w, u32x4_t* __restrict__ wp, int N, int K,
                                    int kmajor) {
@@ -802,6 +925,22 @@ hipError_t launch_wide_resid(int mt, int wv, const Args& a, hipStream_t s) {
     case 2: return launch_wide<2, NT, EPI_RESID>(wv, a, s);
   }
   return hipErrorInvalidValue;
+}
+
+template <int MT>
+hipError_t launch_widek(int kw, const Args& a, hipStream_t s) {
+  const int blocks = (a.N / 32) * a.S;
+#define MIVGPU_LAUNCH_WIDEK(KW)                                                                              \
+  hipLaunchKernelGGL((skinny_widek_kernel<MT, KW>), dim3(blocks), dim3(64 * KW), 0, s, (const u32x4_t*)a.wp,  \
+                     (const bf16_t*)a.x, (bf16_t*)a.y, a.M, a.K, a.N, a.ldx, a.ldy, a.S, a.scratch, a.tickets, \
+                     a.kmajor)
+  switch (kw) {
+    case 2: MIVGPU_LAUNCH_WIDEK(2); break;
+    case 4: MIVGPU_LAUNCH_WIDEK(4); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef MIVGPU_LAUNCH_WIDEK
+  return hipGetLastError();
 }
 
 int mt_of(int M) { return M <= 32 ? 1 : (M <= 64 ? 2 : 4); }
@@ -942,6 +1081,25 @@ bool plan_wide(int M, int K, int N, int epi, int* nt, int* wv, int* S) {
   return *S >= 1 && KB % (*S * U) == 0 && KB / *S >= U;
 }
 
+// K-split wide plan (variant 3): nt = 1, ks = k-waves per workgroup (2 or 4,
+// default 4), S = inter-workgroup split (default 1).  Stores only, M <= 64.
+// False when it cannot run these values.
+bool plan_widek(int M, int K, int N, int epi, int* nt, int* kw, int* S) {
+  static const int cus = mivgpu_ops_visible_cus();
+  if (epi != EPI_STORE || M > 64) return false;
+  if (*nt > 1) return false;
+  *nt = 1;
+  if (*kw <= 0) *kw = 4;
+  if (*kw != 2 && *kw != 4) return false;
+  const int KB = K / 64, GK = *kw * 2;
+  // no inter-workgroup split by default: measured on the whole chip (bench/gemm.py,
+  // profiles/round3/widek_gemm.json) S = 2 costs qkv 13.6 -> 19.1 us and o_proj
+  // 12.2 -> 15.6 us at 32 rows (the atomics + last-arriver tail)
+  (void)cus;
+  if (*S <= 0) *S = 1;
+  return *S >= 1 && KB % (*S * GK) == 0 && KB / *S >= GK;
+}
+
 // Kernel choice: 1 = classic, 2 = wide; 0 = auto = wide where it can run
 // (MIVGPU_SKINNY_WIDE=0/1 forces one for A/B runs).  An infeasible wide request
 // falls back to classic.  Resolves nt/ks/S for the kernel chosen.
@@ -957,6 +1115,14 @@ int resolve(int M, int K, int N, int epi, int* nt, int* ks, int* S, int variant)
     // on the whole chip gate_up 93 vs 126 and down 72 vs 74 (qkv / o_proj,
     // where classic is ahead, run on hipBLASLt there)
     variant = env >= 0 ? (env ? 2 : 1) : 2;
+  }
+  if (variant == 3) {
+    int a = *nt, b = *ks, c = *S;
+    if (plan_widek(M, K, N, epi, &a, &b, &c)) {
+      *nt = a, *ks = b, *S = c;
+      return 3;
+    }
+    variant = 2;   // infeasible: the wide kernel's plan
   }
   if (variant == 2) {
     int a = *nt, b = *ks, c = *S;
@@ -1033,7 +1199,13 @@ int mivgpu_skinny_gemm_norm(const void* wp, const void* x, void* y, int M, int K
   const bool fused = rs_part != nullptr || epi == EPI_RESID;
   if (epi == EPI_RESID && ss_out == nullptr) return (int)hipErrorInvalidValue;
   if (rs_part != nullptr && rs_nparts <= 0) return (int)hipErrorInvalidValue;
-  if (resolve(M, K, N, epi == EPI_RESID ? EPI_STORE : epi, &nt, &ks, &S, fused ? 2 : variant) == 2) {
+  const int v = resolve(M, K, N, epi == EPI_RESID ? EPI_STORE : epi, &nt, &ks, &S, fused ? 2 : variant);
+  if (v == 3) {
+    if (ldy < N || (S > 1 && (scratch == nullptr || tickets == nullptr))) return (int)hipErrorInvalidValue;
+    const Args a{wp, x, y, M, K, N, ldx, ldy, S, scratch, tickets, false, use_kmajor() ? 1 : 0};
+    return (int)(mt_of(M) == 1 ? launch_widek<1>(ks, a, s) : launch_widek<2>(ks, a, s));
+  }
+  if (v == 2) {
     if (epi == EPI_SILU_MUL && ldy < N / 2) return (int)hipErrorInvalidValue;
     if (epi != EPI_SILU_MUL && ldy < N) return (int)hipErrorInvalidValue;
     if (S > 1 && (scratch == nullptr || tickets == nullptr)) return (int)hipErrorInvalidValue;

@@ -85,12 +85,20 @@ def main():
             t_lib = _time(lib_fn, a.reps)
             t_sk = _time(lambda i: lins[i % ncopy](x, out=out), a.reps)
             t_wide = _time(lambda i: lins[i % ncopy](x, out=out, variant=ops.VARIANT_WIDE), a.reps)
+            widek = {}
+            if not silu and M <= 64:
+                for kw in (2, 4):
+                    for S in (0, 1, 2, 4):
+                        if ops.skinny_plan(M, K, N, lin.epi, 1, kw, S, ops.VARIANT_WIDEK)["variant"] != ops.VARIANT_WIDEK:
+                            continue
+                        widek[f"kw{kw}_S{S or 'auto'}"] = round(_time(
+                            lambda i: lins[i % ncopy](x, out=out, ks=kw, S=S, variant=ops.VARIANT_WIDEK), a.reps), 2)
             row = {"plan": ops.skinny_plan(M, K, N, lin.epi), "shape": name, "M": M, "N": N, "K": K, "fused_silu": silu,
                    "wide_plan": ops.skinny_plan(M, K, N, lin.epi, variant=ops.VARIANT_WIDE),
                    "wide_us": round(t_wide, 2), "wide_TBps": round(wbytes / t_wide / 1e6, 3),
                    "hipblaslt_us": round(t_lib, 2), "skinny_us": round(t_sk, 2),
                    "hipblaslt_TBps": round(wbytes / t_lib / 1e6, 3), "skinny_TBps": round(wbytes / t_sk / 1e6, 3),
-                   "speedup": round(t_lib / t_sk, 3), "weight_copies": ncopy}
+                   "speedup": round(t_lib / t_sk, 3), "weight_copies": ncopy, "widek_us": widek}
             if a.sweep and M == 32:
                 sw = {}
                 for variant, tag, kss in ((ops.VARIANT_CLASSIC, "", (1, 2, 4, 8)), (ops.VARIANT_WIDE, "wide_", (1, 2, 4))):

@@ -140,6 +140,20 @@ class Qwen3Decoder:
         self.norm_fused = skinny and os.environ.get("MIVGPU_NORM_FUSED", "0") == "1"
         if self.norm_fused:
             self.skinny_o = True
+        # K-split wide kernel (csrc/ops/skinny_gemm.hip skinny_widek_kernel) for
+        # the small projections on the whole chip, where the wide kernel leaves
+        # CUs idle and hipBLASLt is slower: qkv 13.6 vs 15.1 us, o_proj 12.2 vs
+        # 13.3 at 32 rows; 11.6 vs 14.3 / 10.0 vs 10.6 at 1 row
+        # (profiles/round3/widek_gemm.json).  Inside a CU partition the tuned
+        # wide plans stay.  MIVGPU_WIDEK=qkv,o,down picks the set, "off" none.
+        wk_env = os.environ.get("MIVGPU_WIDEK")
+        if wk_env is None:
+            wk_env = "qkv,o" if (self.native and ops.visible_cus() > 160) else ""
+        widek = {p for p in wk_env.split(",") if p and p != "off"} if skinny else set()
+        if "qkv" in widek:
+            self.skinny_qkv = True
+        if "o" in widek:
+            self.skinny_o = True
         if self.skinny:
             # Keep only the packed copies (no duplicate 16 GB of weights).
             for lw in self.w.layers:
@@ -153,13 +167,19 @@ class Qwen3Decoder:
                         keep_gu = batch <= 16 and ops.visible_cus() > int(os.environ.get("MIVGPU_SLICE_PLAN_CUS", "96"))
                         lw["pgu"] = ops.PackedLinear(lw["wgu"] if keep_gu else lw.pop("wgu"), silu_mul=True)
                     if self.skinny_qkv:
-                        lw["pqkv"] = ops.PackedLinear(lw.pop("wqkv"))
+                        # on the whole chip the plain copy stays for prompt-sized GEMMs
+                        # (hipBLASLt 25 vs wide 50 us at 128 rows; +50 MB/layer)
+                        keep_qkv = "qkv" in widek and ops.visible_cus() > 160
+                        lw["pqkv"] = ops.PackedLinear(lw["wqkv"] if keep_qkv else lw.pop("wqkv"))
                 if self.skinny_o:
                     # on the whole chip the plain copy stays for prompt-sized
                     # GEMMs (hipBLASLt 24.6 vs wide 46 us at 128 rows; +34 MB/layer)
                     keep = ops.visible_cus() > int(os.environ.get("MIVGPU_SLICE_PLAN_CUS", "96"))
                     lw["po"] = ops.PackedLinear(lw["wo"] if keep else lw.pop("wo"))
                 lw["pd"] = ops.PackedLinear(lw.pop("wd"))
+                for key, name in (("pqkv", "qkv"), ("po", "o"), ("pd", "down")):
+                    if name in widek and key in lw:
+                        lw[key].variant = ops.VARIANT_WIDEK
             self.p_lm = ops.PackedLinear(self.w.lm_head, col_scale=self.w.final_norm if self.norm_fused else None)
             if not cfg.tie_embeddings:
                 self.w.lm_head = None

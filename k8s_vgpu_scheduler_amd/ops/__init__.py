@@ -349,7 +349,7 @@ def interleave_gate_up(w_gu: torch.Tensor) -> torch.Tensor:
     return w_gu.view(2, inter // 32, 32, K).transpose(0, 1).reshape(two_i, K)
 
 
-VARIANT_AUTO, VARIANT_CLASSIC, VARIANT_WIDE = 0, 1, 2
+VARIANT_AUTO, VARIANT_CLASSIC, VARIANT_WIDE, VARIANT_WIDEK = 0, 1, 2, 3
 
 
 def skinny_plan(M: int, K: int, N: int, epi: int, nt: int = 0, ks: int = 0, S: int = 0, variant: int = 0) -> dict:
@@ -391,6 +391,7 @@ class PackedLinear:
                 raise ValueError(f"col_scale must be [{self.K}], got {tuple(col_scale.shape)}")
             w = (w.float() * col_scale.float()[None, :]).to(w.dtype)
         self.wp = pack_weight(interleave_gate_up(w) if silu_mul else w)
+        self.variant = VARIANT_AUTO   # kernel used when a call does not ask for one (VARIANT_WIDEK: K-split waves)
         self.scratch = None
         self.tickets = None
         # set once a hipGraph holds the slabs' addresses: growing them then
@@ -402,8 +403,9 @@ class PackedLinear:
         graph capture, when later calls may use other row counts)."""
         floats = tickets = 0
         for m in range(1, max_m + 1):
-            pl = skinny_plan(m, self.K, self.N, self.epi)
-            floats, tickets = max(floats, pl["scratch_floats"]), max(tickets, pl["tickets"])
+            for v in {VARIANT_AUTO, self.variant}:
+                pl = skinny_plan(m, self.K, self.N, self.epi, variant=v)
+                floats, tickets = max(floats, pl["scratch_floats"]), max(tickets, pl["tickets"])
         self._ensure_scratch(floats, tickets, self.wp.device)
 
     @property
@@ -427,6 +429,7 @@ class PackedLinear:
             raise ValueError(f"skinny_gemm: x must be [M, {self.K}] row-major, got {tuple(x.shape)}")
         if out is None:
             out = torch.empty(M, self.out_features, dtype=torch.bfloat16, device=x.device)
+        variant = variant or self.variant
         if 0 < M <= 128:
             pl = skinny_plan(M, self.K, self.N, self.epi, nt, ks, S, variant)
             self._ensure_scratch(pl["scratch_floats"], pl["tickets"], x.device)

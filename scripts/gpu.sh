@@ -14,6 +14,7 @@
 #   kernels_full  the same on the whole GPU (kernel trace: durations and the gaps between them)
 #   pmc [cfg..] PMC passes over a decode step: whole GPU, 64 CUs, 32 CUs (one counter group per pass)
 #   membw       partition read ceilings (bench/membw.py)
+#   widek       K-split wide GEMM kernel: numerics, GEMM sweep, decode A/B
 #   mall        projection GEMMs cold vs with their weights prefetched into the Infinity Cache
 #   serving     TTFT / per-token latency, native vs vGPU slices (bench/serving.py)
 #   mixed       governed server + 3 governed decode tenants; 8 x 12 % temporal over 600 steps
@@ -92,6 +93,19 @@ case $suite in
       python -u bench.py --slices 8 --rounds temporal --steps 600 --out "$out/device_inst20.json"
     MIVGPU_SHARE_EST=instant MIVGPU_SHARE_TAU_MS=20 step 400 host_inst20 \
       python -u bench.py --slices 8 --rounds temporal --steps 600 --out "$out/host_inst20.json" ;;
+  widek)
+    # K-split wide kernel: numerics, GEMM sweep, decode A/B (whole GPU and 64 CUs)
+    step 600 tests python -u -m pytest tests/test_ops_gpu.py -v --timeout 300 --timeout-method thread -k "widek"
+    step 300 gemm python -u -m k8s_vgpu_scheduler_amd.bench.gemm --shapes qkv,o_proj,down --batches 1,32 \
+      --out "$out/gemm.json"
+    for wk in off qkv,o qkv,o,down; do
+      tag=${wk//,/_}
+      MIVGPU_WIDEK=$wk step 300 "full_$tag" python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 200
+    done
+    HSA_CU_MASK=0:0-63 MIVGPU_WIDEK=qkv,o step 300 cu64_qkv_o python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 100
+    HSA_CU_MASK=0:0-63 MIVGPU_WIDEK=off step 300 cu64_off python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 100
+    step 300 serve_b1 python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 1 --steps 200
+    MIVGPU_WIDEK=off step 300 serve_b1_off python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 1 --steps 200 ;;
   mall)
     step 300 mall python -u scripts/probe/mall_prefetch.py --out "$out/mall.json" ;;
   membw)

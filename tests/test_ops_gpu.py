@@ -392,12 +392,53 @@ def test_decoder_norm_fused_matches_reference(monkeypatch):
         b.tokens.copy_(a.tokens)
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 6144, 4096), (32, 6144, 4096), (8, 4096, 4096), (32, 4096, 12288),
+                                   (48, 4096, 4096)])
+@pytest.mark.parametrize("kw,S", [(4, 0), (2, 1), (4, 2)])
+def test_skinny_widek_matches_reference(ops, M, N, K, kw, S):
+    """K-split wide kernel (variant 3): KW waves interleave one n-tile's
+    k-blocks and reduce through LDS, optionally split S ways across
+    workgroups; vs the fp32 reference, twice (slabs and tickets left clean)."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + kw)
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) * 0.02).bfloat16()
+    lin = ops.PackedLinear(w)
+    pl = ops.skinny_plan(M, K, N, lin.epi, 1, kw, S, ops.VARIANT_WIDEK)
+    if pl["variant"] != ops.VARIANT_WIDEK:
+        pytest.skip(f"plan {pl}")
+    exp = x.float() @ w.float().t()
+    for _ in range(2):
+        out = lin(x, ks=kw, S=S, variant=ops.VARIANT_WIDEK)
+        torch.cuda.synchronize()
+        _close(out, exp, 2e-2)
+    if lin.tickets is not None:
+        assert int(lin.tickets.abs().sum()) == 0 and float(lin.scratch.abs().sum()) == 0.0
+
+
+def test_decoder_widek_matches_reference(monkeypatch):
+    """qkv, o_proj and down on the K-split wide kernel (MIVGPU_WIDEK): 3 steps
+    against the fp32 reference decoder."""
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
+
+    monkeypatch.setenv("MIVGPU_WIDEK", "qkv,o,down")
+    a = Qwen3Decoder(QWEN3_TINY, batch=6, max_ctx=64, device="cuda", native=True, seed=11)
+    assert a.w.layers[0]["pd"].variant == 3 and a.skinny_qkv and a.skinny_o
+    b = Qwen3Decoder(QWEN3_TINY, batch=6, max_ctx=64, device="cuda", native=False, seed=11)
+    a.fill_context(12)
+    b.fill_context(12)
+    for _ in range(3):
+        la, lb = a.step(), b.step()
+        _close(la, lb, 5e-2)
+        b.tokens.copy_(a.tokens)
+
+
 def test_decoder_qkv_on_wide_kernel_matches_reference(monkeypatch):
     """Small-partition plan (qkv on the wide skinny kernel, forced here on the
     whole GPU with MIVGPU_QKV_WIDE_CUS): 3 steps against the fp32 reference."""
     from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
 
     monkeypatch.setenv("MIVGPU_QKV_WIDE_CUS", "100000")
+    monkeypatch.setenv("MIVGPU_WIDEK", "off")       # the wide kernel's plan, not the K-split one
     a = Qwen3Decoder(QWEN3_TINY, batch=7, max_ctx=64, device="cuda", native=True, seed=8)
     assert a.skinny_qkv and "pqkv" in a.w.layers[0] and "wqkv" not in a.w.layers[0]
     b = Qwen3Decoder(QWEN3_TINY, batch=7, max_ctx=64, device="cuda", native=False, seed=8)
