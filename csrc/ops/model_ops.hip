@@ -13,6 +13,8 @@
 //   mivgpu_prefill_qk_norm_rope_kv  the same over a prompt's tokens into one cache row
 //   mivgpu_decode_attention GQA split-K flash-decoding (partials + combine)
 //   mivgpu_silu_mul         out = silu(gate) * up
+//   mivgpu_embed_rmsnorm    decode head: res = embed[tokens], out = rmsnorm(res) * w
+//   mivgpu_decode_tail      decode tail: tokens = argmax(logits), pos += 1, seqlens += 1
 //
 // All tensors bf16 (raw uint16 bits) unless noted; fp32 accumulation.
 #include <hip/hip_runtime.h>
@@ -122,6 +124,137 @@ rmsnorm_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ res, const bf1
       orow[vi] = pack8(o);
     }
   }
+}
+
+// ------------------------------------------ decode step head and tail ----
+// Head: res[b] = embed[tokens[b]], h[b] = rmsnorm(res[b]) * w in one launch
+// (was index_select + rmsnorm).  One 256-thread workgroup per row, the
+// embedding row loaded up front as in rmsnorm_kernel.
+__global__ void __launch_bounds__(256)
+embed_rmsnorm_kernel(const bf16_t* __restrict__ embed, const int64_t* __restrict__ tokens,
+                     const bf16_t* __restrict__ w, bf16_t* __restrict__ res, bf16_t* __restrict__ out, int dim,
+                     long long vocab, float eps) {
+  const int row = blockIdx.x;
+  const int t = threadIdx.x;
+  long long tok = tokens[row];
+  tok = tok < 0 ? 0 : (tok >= vocab ? vocab - 1 : tok);   // a bad id reads a valid row, never out of bounds
+  const uint4* xr = reinterpret_cast<const uint4*>(embed + (size_t)tok * dim);
+  uint4* rr = reinterpret_cast<uint4*>(res + (size_t)row * dim);
+  uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * dim);
+  const uint4* wv = reinterpret_cast<const uint4*>(w);
+  __shared__ float red[4];
+  constexpr int MAXV = 4;
+  const int nvec = dim / 8;
+  uint4 xa[MAXV], wa[MAXV];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = min(t + k * 256, nvec - 1);
+    xa[k] = xr[vi];
+    wa[k] = wv[vi];
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = t + k * 256;
+    if (vi < nvec) {
+      rr[vi] = xa[k];
+      float a[8];
+      unpack8(xa[k], a);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += a[e] * a[e];
+    }
+  }
+  ss = wave_sum(ss);
+  if ((t & 63) == 0) red[t >> 6] = ss;
+  __syncthreads();
+  const float inv = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)dim + eps);
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = t + k * 256;
+    if (vi < nvec) {
+      float a[8], wf[8], o[8];
+      unpack8(xa[k], a);
+      unpack8(wa[k], wf);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = a[e] * inv * wf[e];
+      orow[vi] = pack8(o);
+    }
+  }
+}
+
+// Tail: tokens[b] = argmax(logits[b]) (first index of the maximum, NaN
+// counts as the maximum, as torch.argmax), pos[b] += 1, seqlens[b] += 1 in
+// one launch (was argmax + two adds: 48 + 9 us of a 4.9 ms step on the whole
+// GPU).  TAIL_SPLIT workgroups per row, each over a contiguous slice with
+// every 16-byte load issued before the compare (one memory round trip); each
+// publishes its best as one 64-bit key (order-preserving value bits above the
+// complemented index, so the larger key is the larger value, then the smaller
+// index) with a device-scope atomicMax into the row's slot, then takes a
+// ticket; the last arriver writes the token, advances pos / seqlens and
+// resets slot and ticket for the next launch.
+constexpr int TAIL_THREADS = 256;
+constexpr int TAIL_SPLIT = 8;
+constexpr int TAIL_MAXV = 10;   // 16-byte vectors per thread: vocab <= 10 * 8 * 256 * 8 = 163840
+
+__device__ __forceinline__ unsigned long long argmax_key(float v, int i) {
+  uint32_t u = __float_as_uint(v);
+  u = (v != v) ? 0xffffffffu : ((u & 0x80000000u) ? ~u : (u | 0x80000000u));
+  return ((unsigned long long)u << 32) | (uint32_t)(~(uint32_t)i);
+}
+
+__global__ void __launch_bounds__(TAIL_THREADS)
+decode_tail_kernel(const bf16_t* __restrict__ logits, int ld, int vocab, int64_t* __restrict__ tokens,
+                   int* __restrict__ pos, int* __restrict__ seqlens, unsigned long long* __restrict__ slots,
+                   int* __restrict__ tickets) {
+  const int row = blockIdx.y, part = blockIdx.x;
+  const int t = threadIdx.x;
+  const int nvec = vocab / 8;
+  const int v0 = (int)((long long)nvec * part / TAIL_SPLIT), v1 = (int)((long long)nvec * (part + 1) / TAIL_SPLIT);
+  const uint4* lr = reinterpret_cast<const uint4*>(logits + (size_t)row * ld);
+  uint4 va[TAIL_MAXV];
+#pragma unroll
+  for (int k = 0; k < TAIL_MAXV; ++k) va[k] = lr[min(v0 + t + k * TAIL_THREADS, nvec - 1)];
+  unsigned long long best = 0;
+#pragma unroll
+  for (int k = 0; k < TAIL_MAXV; ++k) {
+    const int vi = v0 + t + k * TAIL_THREADS;
+    if (vi < v1) {
+      float a[8];
+      unpack8(va[k], a);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const unsigned long long key = argmax_key(a[e], vi * 8 + e);
+        best = key > best ? key : best;
+      }
+    }
+  }
+  if (part == TAIL_SPLIT - 1)
+    for (int i = nvec * 8 + t; i < vocab; i += TAIL_THREADS) {   // vocab % 8 tail
+      const unsigned long long key = argmax_key(bf2f(logits[(size_t)row * ld + i]), i);
+      best = key > best ? key : best;
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long other = __shfl_xor(best, o, 64);
+    best = other > best ? other : best;
+  }
+  __shared__ unsigned long long s_b[TAIL_THREADS / 64];
+  if ((t & 63) == 0) s_b[t >> 6] = best;
+  __syncthreads();
+  if (t != 0) return;
+#pragma unroll
+  for (int w = 1; w < TAIL_THREADS / 64; ++w) best = s_b[w] > best ? s_b[w] : best;
+  // device-scope atomics only (no cache-flushing fences): the max is drained
+  // (vmcnt) before the ticket is taken, as the split-K GEMM's slab adds
+  __hip_atomic_fetch_max(slots + row, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int ticket = __hip_atomic_fetch_add(tickets + row, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (ticket != TAIL_SPLIT - 1) return;
+  const unsigned long long key = __hip_atomic_exchange(slots + row, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(tickets + row, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  tokens[row] = (int64_t)(~(uint32_t)(key & 0xffffffffu));
+  pos[row] += 1;
+  seqlens[row] += 1;
 }
 
 // ------------------------------------------- QK-norm + RoPE + KV append ----
@@ -606,7 +739,7 @@ decode_attn_mfma_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__
 //     SPLIT), the same in every workgroup of the row); empty ones leave.
 // The qkv/weight loads are issued before the K/V loads so the prep math does
 // not wait behind the 16 KB of K/V (vmcnt retires in order).
-template <int G, int WAVES, bool NT, bool COMBINE>
+template <int G, int WAVES, bool NT, bool COMBINE, bool MULTI>
 __global__ void __launch_bounds__(WAVES * 64)
 decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ qnw,
                          const bf16_t* __restrict__ knw, const int* __restrict__ pos,
@@ -614,12 +747,15 @@ decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restric
                          bf16_t* __restrict__ v_pack, bf16_t* __restrict__ out,
                          float* __restrict__ o_part, float* __restrict__ ml_part,
                          int* __restrict__ counters, int Hq, int Hkv, int max_ctx, int nsplit,
-                         float scale_log2, float eps, float log2_theta) {
+                         int iters, float scale_log2, float eps, float log2_theta) {
   typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
   typedef __attribute__((ext_vector_type(4))) float f32x4_t;
   typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
   constexpr int D = ATT_D;
-  constexpr int SPLIT = WAVES * ATT_KPW;
+  // keys per split: `iters` 32-key groups per wave (MULTI; 1 otherwise), group
+  // i of wave w at position (i * WAVES + w) in the split (the waves read
+  // adjacent groups at each step)
+  const int SPLIT = WAVES * ATT_KPW * (MULTI ? iters : 1);
   constexpr int DP = D + 4;
   const int split = blockIdx.x;
   const int hk = blockIdx.y;
@@ -656,22 +792,26 @@ decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restric
     const bf16_t raw_x0 = src[lane], raw_x1 = src[lane + 64];
     const bf16_t raw_w0 = nw[lane], raw_w1 = nw[lane + 64];
     __builtin_amdgcn_sched_barrier(0);
-    // ---- K/V loads of this wave's 32-key group (as decode_attn_mfma_kernel)
-    const int wj0 = j0 + wave * ATT_KPW;
-    const int wn = min(ATT_KPW, L - wj0);
-    const int grp = (wn > 0 ? wj0 : j0) / ATT_KPW;
+    // ---- K/V loads of one 32-key group of this wave (as decode_attn_mfma_kernel);
+    // a group past the keys re-reads the split's first group (valid address,
+    // every score masked)
     const size_t head = ((size_t)b * Hkv + hk) * (size_t)max_ctx * D;
-    const u32x4_t* kp = reinterpret_cast<const u32x4_t*>(k_pack + head + (size_t)grp * ATT_GROUP) + lane;
-    const u32x4_t* vp = reinterpret_cast<const u32x4_t*>(v_pack + head + (size_t)grp * ATT_GROUP) + lane;
-    u32x4_t kr[2][4];
-    u32x4_t vr[8];
+    // (always_inline: an outlined lambda keeps the fragment arrays in scratch)
+    auto load_kv = [&](u32x4_t (&kr)[2][4], u32x4_t (&vr)[8], int it) __attribute__((always_inline)) {
+      const int wj0 = j0 + (it * WAVES + wave) * ATT_KPW;
+      const int grp = (wj0 < L ? wj0 : j0) / ATT_KPW;
+      const u32x4_t* kp = reinterpret_cast<const u32x4_t*>(k_pack + head + (size_t)grp * ATT_GROUP) + lane;
+      const u32x4_t* vp = reinterpret_cast<const u32x4_t*>(v_pack + head + (size_t)grp * ATT_GROUP) + lane;
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
+      for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        kr[tt][s] = NT ? __builtin_nontemporal_load(kp + 64 * (4 * tt + s)) : kp[64 * (4 * tt + s)];
+        for (int s = 0; s < 4; ++s)
+          kr[tt][s] = NT ? __builtin_nontemporal_load(kp + 64 * (4 * tt + s)) : kp[64 * (4 * tt + s)];
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt) vr[dt] = NT ? __builtin_nontemporal_load(vp + 64 * dt) : vp[64 * dt];
+      for (int dt = 0; dt < 8; ++dt) vr[dt] = NT ? __builtin_nontemporal_load(vp + 64 * dt) : vp[64 * dt];
+    };
+    u32x4_t kra[2][4], vra[8], krb[2][4], vrb[8];
+    load_kv(kra, vra, 0);
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- prep math: RMSNorm + NeoX RoPE (q, k), copy (v).  Computed by every
@@ -715,75 +855,112 @@ decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restric
     }
     __syncthreads();
 
-    // ---- Q operand from LDS; the wave owning the new key patches its fragments
+    // ---- Q operand from LDS
     u32x4_t qr[4];
     {
       const int g = r16 < G ? r16 : 0;
 #pragma unroll
       for (int s = 0; s < 4; ++s) qr[s] = *reinterpret_cast<const u32x4_t*>(&s_q[g][32 * s + 8 * q4]);
     }
-    if (owner && p >= wj0 && p < wj0 + ATT_KPW) {
-      const int k = p & 31;
-      const int kt = (k >> 2) & 1, kr_ = 4 * (k >> 3) + (k & 3);
-      if (r16 == kr_) {
+
+    // ---- per group: the wave owning the new key patches its fragments (its
+    // loads may predate the append), scores, online softmax, P.V accumulated
+    // into o[] with the running max and sum rescaled
+    f32x4_t o[8];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, lsum = 0.f;
+    auto group = [&](u32x4_t (&kr)[2][4], u32x4_t (&vr)[8], int it) __attribute__((always_inline)) {
+      const int wj0 = j0 + (it * WAVES + wave) * ATT_KPW;
+      const int wn = min(ATT_KPW, L - wj0);
+      if (owner && p >= wj0 && p < wj0 + ATT_KPW) {   // uniform per wave
+        // selects, not stores under a lane-dependent branch: those kept the
+        // fragment arrays in scratch (112 bytes per lane)
+        const bool patch = true;
+        const int k = p & 31;
+        const int kt = (k >> 2) & 1, kr_ = 4 * (k >> 3) + (k & 3);
+        const bool pk = patch && r16 == kr_;
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
-          if (tt == kt) {
 #pragma unroll
-            for (int s = 0; s < 4; ++s) kr[tt][s] = *reinterpret_cast<const u32x4_t*>(&s_kv[0][32 * s + 8 * q4]);
+          for (int s = 0; s < 4; ++s) {
+            const u32x4_t nk = *reinterpret_cast<const u32x4_t*>(&s_kv[0][32 * s + 8 * q4]);
+            kr[tt][s] = (pk && tt == kt) ? nk : kr[tt][s];
           }
-      }
-      if (q4 == (k >> 3)) {
+        const bool pv = patch && q4 == (k >> 3);
         const int ke = k & 7;
         const unsigned sh = (ke & 1) * 16, keep = 0xffff0000u >> sh;
 #pragma unroll
         for (int dt = 0; dt < 8; ++dt) {
           const unsigned nv = (unsigned)s_kv[1][16 * dt + r16] << sh;
 #pragma unroll
-          for (int c = 0; c < 4; ++c)
-            if (c == (ke >> 1)) vr[dt][c] = (vr[dt][c] & keep) | nv;
+          for (int c = 0; c < 4; ++c) vr[dt][c] = (pv && c == (ke >> 1)) ? ((vr[dt][c] & keep) | nv) : vr[dt][c];
         }
       }
-    }
-
-    // ---- scores, local softmax, P.V (as decode_attn_mfma_kernel)
-    f32x4_t sc[2];
+      f32x4_t sc[2];
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      sc[tt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int tt = 0; tt < 2; ++tt) {
+        sc[tt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        sc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, kr[tt][s]),
-                                                        __builtin_bit_cast(bf16x8_t, qr[s]), sc[tt], 0, 0, 0);
-    }
-    float pr[8];
-    float m = -INFINITY;
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool ok = (8 * q4 + 4 * tt + i) < wn;
-        pr[4 * tt + i] = ok ? sc[tt][i] : -INFINITY;
-        m = fmaxf(m, pr[4 * tt + i]);
+        for (int s = 0; s < 4; ++s)
+          sc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, kr[tt][s]),
+                                                          __builtin_bit_cast(bf16x8_t, qr[s]), sc[tt], 0, 0, 0);
       }
-    m = fmaxf(m, __shfl_xor(m, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
-    float lsum = 0.f;
+      float pr[8];
+      float mg = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      pr[j] = m == -INFINITY ? 0.f : exp2f((pr[j] - m) * scale_log2);
-      lsum += pr[j];
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool ok = (8 * q4 + 4 * tt + i) < wn;
+          pr[4 * tt + i] = ok ? sc[tt][i] : -INFINITY;
+          mg = fmaxf(mg, pr[4 * tt + i]);
+        }
+      mg = fmaxf(mg, __shfl_xor(mg, 16, 64));
+      mg = fmaxf(mg, __shfl_xor(mg, 32, 64));
+      const float mn = fmaxf(m, mg);
+      const float a = m == -INFINITY ? 0.f : exp2f((m - mn) * scale_log2);
+      float ls = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pr[j] = mn == -INFINITY ? 0.f : exp2f((pr[j] - mn) * scale_log2);
+        ls += pr[j];
+      }
+      ls += __shfl_xor(ls, 16, 64);
+      ls += __shfl_xor(ls, 32, 64);
+      lsum = lsum * a + ls;
+      m = mn;
+      bf16x8_t pb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pb[j] = (__bf16)pr[j];
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, vr[dt]), pb, o[dt] * a, 0, 0,
+                                                        0);
+    };
+    // groups of this wave holding keys: it < nit (later groups are past L)
+    const int first = j0 + wave * ATT_KPW;
+    const int nit = first < L ? min(iters, (L - first + WAVES * ATT_KPW - 1) / (WAVES * ATT_KPW)) : 0;
+    // The first group is processed unconditionally (a wave past the keys sees
+    // every score masked: a neutral partial): its loads were issued before the
+    // prep math, and a use inside a branch lets LLVM sink them behind the
+    // barrier (measured 42 vs 26 us per layer).
+    if constexpr (MULTI) {
+      // two register buffers: the next group's loads go out before this group's math
+      int it = 0;
+      while (true) {
+        if (it + 1 < nit) load_kv(krb, vrb, it + 1);
+        group(kra, vra, it);
+        if (++it >= nit) break;
+        if (it + 1 < nit) load_kv(kra, vra, it + 1);
+        group(krb, vrb, it);
+        if (++it >= nit) break;
+      }
+    } else {
+      // one group per wave (iters == 1): one register buffer, ~100 fewer VGPRs,
+      // so several workgroups share a CU and hide each other's load latency
+      group(kra, vra, 0);
     }
-    lsum += __shfl_xor(lsum, 16, 64);
-    lsum += __shfl_xor(lsum, 32, 64);
-    bf16x8_t pb;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) pb[j] = (__bf16)pr[j];
-    f32x4_t o[8];
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt)
-      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, vr[dt]), pb,
-                                                      f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     if (r16 < G) {
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt)
@@ -810,6 +987,10 @@ decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restric
           num += f * s_o[w][g][d];
           den += f * s_l[w][g];
         }
+      }
+      if (!COMBINE && nsplit == 1) {   // one split holds every key: the merged output, no combine
+        out[(part_base + g) * D + d] = f2bf(den > 0.f ? num / den : 0.f);
+        continue;
       }
       const float mn = M == -INFINITY ? -INFINITY : M * scale_log2 * 0.69314718f;
       float* op = &o_part[((part_base + g) * nsplit + split) * D + d];
@@ -948,6 +1129,27 @@ int mivgpu_rmsnorm(const void* x, const void* w, void* out, int rows, int dim, f
   if (dim % 8 || dim > 8192 || rows <= 0) return -1;
   hipLaunchKernelGGL(rmsnorm_kernel<false>, dim3(rows), dim3(256), 0, s, (const bf16_t*)x,
                      (bf16_t*)nullptr, (const bf16_t*)w, (bf16_t*)out, dim, eps);
+  return (int)hipGetLastError();
+}
+
+int mivgpu_embed_rmsnorm(const void* embed, const int64_t* tokens, const void* w, void* res, void* out, int rows,
+                         int dim, long long vocab, float eps, hipStream_t s) {
+  if (dim % 8 || dim > 8192 || rows <= 0 || vocab <= 0) return -1;
+  hipLaunchKernelGGL(embed_rmsnorm_kernel, dim3(rows), dim3(256), 0, s, (const bf16_t*)embed, tokens,
+                     (const bf16_t*)w, (bf16_t*)res, (bf16_t*)out, dim, vocab, eps);
+  return (int)hipGetLastError();
+}
+
+// work: rows * 2 int64-sized words (slots, then tickets as ints), zeroed once;
+// every launch leaves it zero.
+int mivgpu_decode_tail(const void* logits, int ld, int vocab, int rows, int64_t* tokens, int* pos, int* seqlens,
+                       void* work, hipStream_t s) {
+  if (rows <= 0 || vocab < 8 * TAIL_SPLIT || ld < vocab || ld % 8 || vocab > TAIL_MAXV * 8 * TAIL_THREADS * TAIL_SPLIT ||
+      work == nullptr)
+    return -1;
+  unsigned long long* slots = (unsigned long long*)work;
+  hipLaunchKernelGGL(decode_tail_kernel, dim3(TAIL_SPLIT, rows), dim3(TAIL_THREADS), 0, s, (const bf16_t*)logits, ld,
+                     vocab, tokens, pos, seqlens, slots, (int*)(slots + rows));
   return (int)hipGetLastError();
 }
 
@@ -1143,17 +1345,27 @@ int mivgpu_decode_attention_fused(const void* qkv, const void* q_norm_w, const v
   if (!attn_impl() || head_dim != ATT_D || Hq % Hkv || nsplit <= 0 || B <= 0) return -1;
   const int G = Hq / Hkv;
   const int waves = attn_impl();
-  if (max_ctx % ATT_KPW || (long long)nsplit * waves * ATT_KPW < max_ctx || G + 2 > waves) return -1;
+  if (max_ctx % ATT_KPW || G + 2 > waves) return -1;
+  // 32-key groups per wave so that nsplit splits cover max_ctx; nsplit = 1
+  // (one workgroup per (b, kv-head), each wave looping over its groups) writes
+  // the output itself and needs no combine
+  const int per = waves * ATT_KPW;
+  const int iters = (int)((max_ctx + (long long)nsplit * per - 1) / ((long long)nsplit * per));
   const bool nt = attn_nt() != 0;
   const float scale_log2 = scale * 1.44269504f;
   const float log2_theta = log2f(theta);
   dim3 grid(nsplit, Hkv, B);
-  const bool comb = attn_fused_mode() >= 2;
-#define MIVGPU_ATTN_FUSED2(GG, WW, NN, CC)                                                                     \
-  hipLaunchKernelGGL((decode_attn_fused_kernel<GG, WW, NN, CC>), grid, dim3(WW * 64), 0, s,                  \
+  const bool comb = attn_fused_mode() >= 2 && nsplit > 1;
+#define MIVGPU_ATTN_FUSED3(GG, WW, NN, CC, MM)                                                                 \
+  hipLaunchKernelGGL((decode_attn_fused_kernel<GG, WW, NN, CC, MM>), grid, dim3(WW * 64), 0, s,              \
                      (const bf16_t*)qkv, (const bf16_t*)q_norm_w, (const bf16_t*)k_norm_w, pos, seqlens,     \
                      (bf16_t*)k_cache, (bf16_t*)v_cache, (bf16_t*)out, (float*)o_part, (float*)ml_part,      \
-                     counters, Hq, Hkv, max_ctx, nsplit, scale_log2, eps, log2_theta)
+                     counters, Hq, Hkv, max_ctx, nsplit, iters, scale_log2, eps, log2_theta)
+#define MIVGPU_ATTN_FUSED2(GG, WW, NN, CC)                  \
+  do {                                                      \
+    if (iters > 1) MIVGPU_ATTN_FUSED3(GG, WW, NN, CC, true); \
+    else MIVGPU_ATTN_FUSED3(GG, WW, NN, CC, false);         \
+  } while (0)
 #define MIVGPU_ATTN_FUSED(GG, WW, NN)                      \
   do {                                                     \
     if (comb) MIVGPU_ATTN_FUSED2(GG, WW, NN, true);        \
@@ -1184,10 +1396,10 @@ int mivgpu_decode_attention_fused(const void* qkv, const void* q_norm_w, const v
 #undef MIVGPU_ATTN_FUSED_G
 #undef MIVGPU_ATTN_FUSED
 #undef MIVGPU_ATTN_FUSED2
-  if (!comb)
+#undef MIVGPU_ATTN_FUSED3
+  if (!comb && nsplit > 1)
     hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(Hq, B), dim3(ATT_D), 0, s, (const float*)o_part,
-                       (const float*)ml_part, (bf16_t*)out, Hq, nsplit, nsplit, seqlens, waves * ATT_KPW,
-                       max_ctx);
+                       (const float*)ml_part, (bf16_t*)out, Hq, nsplit, nsplit, seqlens, iters * per, max_ctx);
   return (int)hipGetLastError();
 }
 

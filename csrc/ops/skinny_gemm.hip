@@ -702,11 +702,18 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
 // group's KW*U k-blocks; the KW partial accumulators are summed through LDS at
 // the end, so K is split KW ways inside the workgroup with no global traffic.
 // An inter-workgroup split S (as above) can still be added to fill the chip.
-template <int MT, int KW>
+//
+// Row-norm fusion as in the wide kernel: EPI_RESID updates the residual Y in
+// place and writes one sum-of-squares slot per n-tile (the old residual tile
+// is fetched by LDS-DMA at the start, off the critical path); rs_part != null
+// scales the rows of a store by the producer's slots (rs_issue / rs_finish).
+template <int MT, int KW, int EPI>
 __global__ void __launch_bounds__(64 * KW)
 skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int M,
                     int K, int N, int ldx, int ldy, int S, float* __restrict__ scratch, int* __restrict__ tickets,
-                    int kmajor) {
+                    int kmajor, const float* __restrict__ rs_part, int rs_nparts, float rs_inv_dim, float rs_eps,
+                    float* __restrict__ ss_out) {
+  static_assert(EPI == EPI_STORE || EPI == EPI_RESID, "widek: stores or the residual update");
   constexpr int NT = 1;
   constexpr int U = 2;                               // k-blocks per wave per group
   constexpr int GK = KW * U;                         // k-blocks per group (the X tile)
@@ -717,11 +724,17 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
   static_assert(XC * NTHREADS == MT * GK * 256, "X tile must split evenly over the workgroup");
   static_assert(KW * MT * 16 * 64 * 4 <= 2 * XBUF * 2, "the k-wave reduction reuses the X buffers");
   __shared__ __attribute__((aligned(16))) bf16_t xs[2 * XBUF];
+  constexpr bool RS = EPI != EPI_RESID;
+  __shared__ float s_rs[MT * 32];
+  __shared__ float s_rtmp[RS ? KW * MT * 32 : 1];
+  // EPI_RESID: the old residual tile [m][32 rows][32 cols], prefetched by wave 0
+  __shared__ __attribute__((aligned(16))) bf16_t s_res[EPI == EPI_RESID ? MT * 32 * 32 : 2];
   const int tid = threadIdx.x;
   const int kw = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
   const int KB = K >> 6;
   const int tile0 = blockIdx.x / S, split = blockIdx.x % S;
+  const float* rs = (RS && rs_part) ? s_rs : nullptr;
   const WStride ws = kmajor ? WStride{256, (size_t)(N >> 5) * 256} : WStride{(size_t)KB * 256, 256};
   const u32x4_t* wbase = wp + (size_t)tile0 * ws.tile;
   const int kb0 = (int)((long long)KB * split / S), kb1 = (int)((long long)KB * (split + 1) / S);
@@ -735,10 +748,31 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
 
   WFrag<NT> fa[U], fb[U];
   {
+    // row-scale slot loads and the residual tile's LDS-DMA first: older than
+    // the X loads, so the X wait below covers them as well
+    float4 rsv[RS ? RS_LMAX : 1];
+    if constexpr (RS) {
+      if (rs_part) rs_issue<MT, NTHREADS>(rsv, rs_part, rs_nparts, tid);
+    }
+    if constexpr (EPI == EPI_RESID) {
+      if (kw == 0) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int row = m * 32 + 4 * i + (lane >> 4);
+            const bf16_t* g = y + (size_t)min(row, M - 1) * ldy + (size_t)tile0 * 32 + 2 * (lane & 15);
+            __builtin_amdgcn_global_load_lds(g, s_res + (m * 32 + 4 * i) * 32, 4, 0, 0);
+          }
+      }
+    }
     u32x4_t xr[XC];
     wide_load_x<MT, GK, XC>(xr, x, M, ldx, kb0, tid, NTHREADS);
     wide_load_w<NT, U>(fa, wbase, ws, kb0 + kw * U, lane);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (RS) {
+      if (rs_part) rs_finish<MT, NTHREADS>(rsv, rs_inv_dim, rs_eps, s_rs, s_rtmp, tid);
+    }
     wide_store_x<MT, GK, XC, PITCH>(xs, xr, tid, NTHREADS);
     __syncthreads();
   }
@@ -787,9 +821,10 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[m][0][e] += red[(((w - 1) * MT + m) * 16 + e) * 64 + lane];
+  if constexpr (EPI == EPI_RESID) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // residual tile landed
   if (S == 1) {
-    wide_epilogue<MT, NT, EPI_STORE>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, tile0, r,
-                                     h, nullptr, nullptr, nullptr);
+    wide_epilogue<MT, NT, EPI>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, tile0, r, h, rs,
+                               ss_out, s_res);
     return;
   }
   constexpr int SLAB = MT * NT * 16 * 64;
@@ -803,11 +838,11 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
   if (lane == 0) ticket = atomicAdd(tickets + tile0, 1);
   ticket = __shfl(ticket, 0, 64);
   if (ticket != S - 1) return;
-  wide_epilogue<MT, NT, EPI_STORE>(
+  wide_epilogue<MT, NT, EPI>(
       [&](int m, int t, int e) {
         return __hip_atomic_load(sc + ((m * NT + t) * 16 + e) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       },
-      y, M, ldy, tile0, tile0, r, h, nullptr, nullptr, nullptr);
+      y, M, ldy, tile0, tile0, r, h, rs, ss_out, s_res);
 #pragma unroll
   for (int i = 0; i < SLAB / 64; ++i) sc[i * 64 + lane] = 0.f;
   if (lane == 0) tickets[tile0] = 0;
@@ -927,13 +962,13 @@ hipError_t launch_wide_resid(int mt, int wv, const Args& a, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
-template <int MT>
+template <int MT, int EPI>
 hipError_t launch_widek(int kw, const Args& a, hipStream_t s) {
   const int blocks = (a.N / 32) * a.S;
-#define MIVGPU_LAUNCH_WIDEK(KW)                                                                              \
-  hipLaunchKernelGGL((skinny_widek_kernel<MT, KW>), dim3(blocks), dim3(64 * KW), 0, s, (const u32x4_t*)a.wp,  \
-                     (const bf16_t*)a.x, (bf16_t*)a.y, a.M, a.K, a.N, a.ldx, a.ldy, a.S, a.scratch, a.tickets, \
-                     a.kmajor)
+#define MIVGPU_LAUNCH_WIDEK(KW)                                                                                   \
+  hipLaunchKernelGGL((skinny_widek_kernel<MT, KW, EPI>), dim3(blocks), dim3(64 * KW), 0, s, (const u32x4_t*)a.wp, \
+                     (const bf16_t*)a.x, (bf16_t*)a.y, a.M, a.K, a.N, a.ldx, a.ldy, a.S, a.scratch, a.tickets,      \
+                     a.kmajor, a.rs_part, a.rs_nparts, a.rs_inv_dim, a.rs_eps, a.ss_out)
   switch (kw) {
     case 2: MIVGPU_LAUNCH_WIDEK(2); break;
     case 4: MIVGPU_LAUNCH_WIDEK(4); break;
@@ -1082,7 +1117,8 @@ bool plan_wide(int M, int K, int N, int epi, int* nt, int* wv, int* S) {
 }
 
 // K-split wide plan (variant 3): nt = 1, ks = k-waves per workgroup (2 or 4,
-// default 4), S = inter-workgroup split (default 1).  Stores only, M <= 64.
+// default 4), S = inter-workgroup split (default 1).  Stores (optionally row
+// scaled) or the residual update (planned as stores), M <= 64.
 // False when it cannot run these values.
 bool plan_widek(int M, int K, int N, int epi, int* nt, int* kw, int* S) {
   static const int cus = mivgpu_ops_visible_cus();
@@ -1199,11 +1235,22 @@ int mivgpu_skinny_gemm_norm(const void* wp, const void* x, void* y, int M, int K
   const bool fused = rs_part != nullptr || epi == EPI_RESID;
   if (epi == EPI_RESID && ss_out == nullptr) return (int)hipErrorInvalidValue;
   if (rs_part != nullptr && rs_nparts <= 0) return (int)hipErrorInvalidValue;
-  const int v = resolve(M, K, N, epi == EPI_RESID ? EPI_STORE : epi, &nt, &ks, &S, fused ? 2 : variant);
+  // the row-norm fusion runs on the wide kernel or, when asked for, the K-split one
+  const int v = resolve(M, K, N, epi == EPI_RESID ? EPI_STORE : epi, &nt, &ks, &S,
+                        fused ? (variant == 3 ? 3 : 2) : variant);
   if (v == 3) {
     if (ldy < N || (S > 1 && (scratch == nullptr || tickets == nullptr))) return (int)hipErrorInvalidValue;
-    const Args a{wp, x, y, M, K, N, ldx, ldy, S, scratch, tickets, false, use_kmajor() ? 1 : 0};
-    return (int)(mt_of(M) == 1 ? launch_widek<1>(ks, a, s) : launch_widek<2>(ks, a, s));
+    Args a{wp, x, y, M, K, N, ldx, ldy, S, scratch, tickets, false, use_kmajor() ? 1 : 0};
+    a.rs_part = rs_part;
+    a.rs_nparts = rs_nparts;
+    a.rs_inv_dim = rs_inv_dim;
+    a.rs_eps = rs_eps;
+    a.ss_out = ss_out;
+    const int mt = mt_of(M);
+    if (rs_part != nullptr && (epi == EPI_RESID || rs_nparts > 64 * ks * RS_LMAX / (mt * 8)))
+      return (int)hipErrorInvalidValue;
+    if (epi == EPI_RESID) return (int)(mt == 1 ? launch_widek<1, EPI_RESID>(ks, a, s) : launch_widek<2, EPI_RESID>(ks, a, s));
+    return (int)(mt == 1 ? launch_widek<1, EPI_STORE>(ks, a, s) : launch_widek<2, EPI_STORE>(ks, a, s));
   }
   if (v == 2) {
     if (epi == EPI_SILU_MUL && ldy < N / 2) return (int)hipErrorInvalidValue;

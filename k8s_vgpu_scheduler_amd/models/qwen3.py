@@ -134,10 +134,15 @@ class Qwen3Decoder:
         # residual stream in their epilogue and write per-row sums of squares,
         # and the next projection applies rsqrt(mean + eps) per row in its
         # epilogue -- no add+RMSNorm launches (csrc/ops/skinny_gemm.hip).
-        # Measured: 64-CU slice 8.85 vs 8.87 ms/step, whole GPU 4.97 vs 4.92
-        # (qkv and o_proj are slower on the wide kernel than on hipBLASLt
-        # there), profiles/README.md section 14.
-        self.norm_fused = skinny and os.environ.get("MIVGPU_NORM_FUSED", "0") == "1"
+        # Round 2, with qkv / o_proj on the wide kernel: 64-CU slice 8.85 vs
+        # 8.87 ms/step, whole GPU 4.97 vs 4.92 (profiles/README.md section 14).
+        # Default on the whole chip, where qkv / o_proj run on the K-split
+        # kernel with the row-scale / residual epilogues: decode 4.84 vs 4.89
+        # ms at batch 32, 3.57 vs 3.62 at batch 1; inside a CU partition the
+        # two norm launches are cheaper than the epilogues (64 CUs: 8.98 vs
+        # 8.92 ms), profiles/README.md section 35.
+        nf_default = "1" if (skinny and ops.visible_cus() > 160) else "0"
+        self.norm_fused = skinny and os.environ.get("MIVGPU_NORM_FUSED", nf_default) == "1"
         if self.norm_fused:
             self.skinny_o = True
         # K-split wide kernel (csrc/ops/skinny_gemm.hip skinny_widek_kernel) for
@@ -196,7 +201,6 @@ class Qwen3Decoder:
         self.tokens = torch.zeros(batch, dtype=torch.long, device=self.device)
         self.pos = torch.zeros(batch, dtype=torch.int32, device=self.device)
         self.seqlens = torch.ones(batch, dtype=torch.int32, device=self.device)
-        self.nsplit = max(1, math.ceil(self.T / (ops.attn_split() if self.native else 256)))
         h = cfg.hidden
         # Static activation buffers (graph-capture friendly).
         self.res = torch.zeros(batch, h, dtype=dt, device=self.device)
@@ -215,18 +219,26 @@ class Qwen3Decoder:
             n = max(self.slots_o, self.slots_d, 1) * ops.SS_ROWS
             self.ss_a = torch.zeros(n, dtype=torch.float32, device=self.device)   # before qkv / lm_head
             self.ss_b = torch.zeros(n, dtype=torch.float32, device=self.device)   # before gate_up
-        self.o_part = torch.zeros(batch * cfg.heads * self.nsplit * cfg.head_dim, dtype=torch.float32,
-                                  device=self.device)
-        self.ml_part = torch.zeros(batch * cfg.heads * self.nsplit * 2, dtype=torch.float32,
-                                   device=self.device)
+            self.ss_pf = torch.zeros(ops.SS_ROWS, dtype=torch.float32, device=self.device)   # prefill chunks
         # One launch per layer for QK-norm + RoPE + KV append + attention +
         # split combine (csrc/ops/model_ops.hip decode_attn_fused_kernel);
         # MIVGPU_ATTN_FUSED=0 runs the three separate kernels.
         self.attn_fused = (self.native and os.environ.get("MIVGPU_ATTN_FUSED", "1") != "0"
                            and ops.attn_fused_ok(cfg.heads, cfg.kv_heads, cfg.head_dim))
+        # key splits: the fused kernel covers the context with any count
+        # (ops.attn_fused_splits); the unfused one needs attn_split() keys each
+        if self.attn_fused:
+            self.nsplit = ops.attn_fused_splits(batch, cfg.kv_heads, self.T)
+        else:
+            self.nsplit = max(1, math.ceil(self.T / (ops.attn_split() if self.native else 256)))
+        self.o_part = torch.zeros(batch * cfg.heads * self.nsplit * cfg.head_dim, dtype=torch.float32,
+                                  device=self.device)
+        self.ml_part = torch.zeros(batch * cfg.heads * self.nsplit * 2, dtype=torch.float32,
+                                   device=self.device)
         self.attn_counters = (torch.zeros(batch * cfg.kv_heads, dtype=torch.int32, device=self.device)
                               if self.attn_fused else None)
         self.graph = None
+        self._tail_work = ops.decode_tail_workspace(batch, self.device) if self.native else None
         self._pf = {}          # prefill bucket length -> static buffers (+ captured graph)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
 
@@ -286,9 +298,7 @@ class Qwen3Decoder:
             lw["pd"].norm_call(self.act, out=self.res, residual=True, ss_out=self.ss_a)
             na = self.slots_d
         logits = self.p_lm.norm_call(self.res, out=self.logits, row_scale=(self.ss_a, na, h, eps))
-        torch.argmax(logits, dim=-1, out=self.tokens)
-        self.pos.add_(1)
-        self.seqlens.add_(1)
+        self._tail(logits)
         return logits
 
     def _step_impl(self):
@@ -301,11 +311,12 @@ class Qwen3Decoder:
         # captured copy of the argmax result raced the argmax kernel on this
         # stack and fed the next step a garbage token (AMD_SERIALIZE_KERNEL=3
         # hid it; scripts/probe/prefill_graph_bisect.py)
-        torch.index_select(w.embed, 0, self.tokens, out=self.res)
         L = cfg.layers
         if self.native:
-            ops.rmsnorm(self.res, w.layers[0]["ln1"], cfg.eps, out=self.h)
+            # gather + first RMSNorm in one launch (csrc/ops/model_ops.hip embed_rmsnorm_kernel)
+            ops.embed_rmsnorm(w.embed, self.tokens, w.layers[0]["ln1"], cfg.eps, res=self.res, out=self.h)
         else:
+            torch.index_select(w.embed, 0, self.tokens, out=self.res)
             self.h.copy_(ref.rmsnorm(self.res, w.layers[0]["ln1"], cfg.eps))
         for li, lw in enumerate(w.layers):
             qkv = lw["pqkv"](self.h, out=self.qkv_buf) if self.skinny_qkv else F.linear(self.h, lw["wqkv"])
@@ -342,10 +353,19 @@ class Qwen3Decoder:
             else:
                 self.h.copy_(ref.add_rmsnorm(d, self.res, nxt, cfg.eps))
         logits = self.p_lm(self.h, out=self.logits) if self.skinny else F.linear(self.h, w.lm_head)
+        self._tail(logits)
+        return logits
+
+    def _tail(self, logits):
+        if self.native and logits.dtype == torch.bfloat16:
+            # argmax + pos / seqlens advance in one launch (decode_tail_kernel)
+            if self._tail_work is None:
+                self._tail_work = ops.decode_tail_workspace(self.B, self.device)
+            ops.decode_tail(logits, self.tokens, self.pos, self.seqlens, self._tail_work)
+            return
         torch.argmax(logits, dim=-1, out=self.tokens)
         self.pos.add_(1)
         self.seqlens.add_(1)
-        return logits
 
     # ---------------------------------------------------------- prefill --
     # Prompt processing for serving (serve/engine.py): all prompt positions of
@@ -369,6 +389,33 @@ class Qwen3Decoder:
             e = min(M, s + self.PREFILL_CHUNK)
             pl(x[s:e], out=out[s:e])
         return out
+
+    def _rows_normed(self, pl, x, out=None):
+        """RMSNorm(x) . W^T for a packed weight with the norm folded into its
+        columns (norm-fused decoder): per <= 128-row chunk, the rows' sums of
+        squares in one slot, applied as row scales by the kernel."""
+        M = x.shape[0]
+        if out is None:
+            out = torch.empty(M, pl.out_features, dtype=torch.bfloat16, device=x.device)
+        for s in range(0, M, self.PREFILL_CHUNK):
+            e = min(M, s + self.PREFILL_CHUNK)
+            torch.sum(x[s:e].float().pow(2), dim=-1, out=self.ss_pf[:e - s])
+            pl.norm_call(x[s:e], out=out[s:e], row_scale=(self.ss_pf, 1, self.cfg.hidden, self.cfg.eps))
+        return out
+
+    def _prefill_impl_norm_fused(self, bufs: dict, b: int):
+        cfg, w = self.cfg, self.w
+        res = torch.index_select(w.embed, 0, bufs["ids"])
+        for li, lw in enumerate(w.layers):
+            q, k, v = self._prefill_qk(li, lw, self._rows_normed(lw["pqkv"], res), bufs["pos"], b)
+            res = res + self._proj(lw, "o", self._prefill_attention(q, k, v, bufs["mask"]))
+            res = res + self._proj(lw, "d", self._rows_normed(lw["pgu"], res))   # SiLU*up in the epilogue
+        last = torch.index_select(res, 0, bufs["last"])
+        logits = self._rows_normed(self.p_lm, last)
+        torch.argmax(logits, dim=-1, out=self.tokens[b:b + 1])
+        torch.add(bufs["plen"], 0, out=self.pos[b:b + 1])
+        torch.add(bufs["plen"], 1, out=self.seqlens[b:b + 1])
+        return logits
 
     def _proj(self, lw, name, x):
         packed, plain = {"qkv": ("pqkv", "wqkv"), "o": ("po", "wo"), "gu": ("pgu", "wgu"),
@@ -437,6 +484,8 @@ class Qwen3Decoder:
         return bufs
 
     def _prefill_impl(self, bufs: dict, b: int):
+        if self.norm_fused:
+            return self._prefill_impl_norm_fused(bufs, b)
         cfg, w = self.cfg, self.w
         res = torch.index_select(w.embed, 0, bufs["ids"])
         h = self._norm(res, w.layers[0]["ln1"])
@@ -465,8 +514,6 @@ class Qwen3Decoder:
     def capture_prefill(self, buckets=None, b: int = 0):
         """Capture the prefill of row ``b`` for each bucket length (<= T)."""
         assert self.device.type == "cuda"
-        if self.norm_fused:
-            raise NotImplementedError("prefill with MIVGPU_NORM_FUSED=1")
         for Lb in (buckets or self.PREFILL_BUCKETS):
             if Lb > self.T:
                 continue
@@ -489,8 +536,6 @@ class Qwen3Decoder:
         """Process the prompt token ids into batch row ``b`` (KV for positions
         0..L-1), set that row's next token to the greedy choice and its
         position to L, and return the last position's logits [vocab]."""
-        if self.norm_fused:
-            raise NotImplementedError("prefill with MIVGPU_NORM_FUSED=1 (norm weights folded into the packed columns)")
         ids = torch.as_tensor(prompt, dtype=torch.long).view(-1)
         L = ids.numel()
         if not 0 < L < self.T:

@@ -38,6 +38,8 @@ def lib():
         vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
         L.mivgpu_rmsnorm.argtypes = [vp, vp, vp, i, i, f, vp]
         L.mivgpu_add_rmsnorm.argtypes = [vp, vp, vp, vp, i, i, f, vp]
+        L.mivgpu_embed_rmsnorm.argtypes = [vp, vp, vp, vp, vp, i, i, ctypes.c_longlong, f, vp]
+        L.mivgpu_decode_tail.argtypes = [vp, i, i, i, vp, vp, vp, vp, vp]
         L.mivgpu_qk_norm_rope_kv.argtypes = [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, f, f, vp]
         L.mivgpu_prefill_qk_norm_rope_kv.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, f, f,
                                                      vp]
@@ -111,6 +113,41 @@ def add_rmsnorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: float,
     _check(lib().mivgpu_add_rmsnorm(_p(x), _p(res), _p(w), _p(out), rows, dim, eps, _stream()),
            "add_rmsnorm")
     return out
+
+
+def embed_rmsnorm(embed: torch.Tensor, tokens: torch.Tensor, w: torch.Tensor, eps: float, res: torch.Tensor,
+                  out: torch.Tensor):
+    """Decode-step head in one launch: res = embed[tokens] (ids clamped to
+    the table), out = rmsnorm(res) * w."""
+    rows, dim = res.shape
+    if (tokens.dtype != torch.int64 or tokens.numel() != rows or embed.shape[1] != dim or out.shape != res.shape
+            or not (embed.is_contiguous() and res.is_contiguous() and out.is_contiguous())):
+        raise ValueError("embed_rmsnorm: embed [V, D], tokens int64 [B], res / out [B, D] contiguous")
+    _check(lib().mivgpu_embed_rmsnorm(_p(embed), _p(tokens), _p(w), _p(res), _p(out), rows, dim, embed.shape[0],
+                                      eps, _stream()), "embed_rmsnorm")
+    return out
+
+
+def decode_tail_workspace(rows: int, device) -> torch.Tensor:
+    """Zeroed workspace of decode_tail (per-row 64-bit argmax slot + ticket);
+    every launch leaves it zero."""
+    return torch.zeros(2 * rows, dtype=torch.int64, device=device)
+
+
+def decode_tail(logits: torch.Tensor, tokens: torch.Tensor, pos: torch.Tensor, seqlens: torch.Tensor,
+                work: torch.Tensor):
+    """Decode-step tail in one launch: tokens = argmax(logits, -1) (first
+    maximum, NaN as the maximum, as torch.argmax), pos += 1, seqlens += 1.
+    ``work`` from decode_tail_workspace(rows) (not shared by concurrent calls)."""
+    rows, vocab = logits.shape
+    if (logits.dtype != torch.bfloat16 or logits.stride(1) != 1 or tokens.dtype != torch.int64
+            or pos.dtype != torch.int32 or seqlens.dtype != torch.int32
+            or min(tokens.numel(), pos.numel(), seqlens.numel()) < rows
+            or work.dtype != torch.int64 or work.numel() < 2 * rows):
+        raise ValueError("decode_tail: bf16 logits [B, V], int64 tokens, int32 pos / seqlens, int64 work [2B]")
+    _check(lib().mivgpu_decode_tail(_p(logits), logits.stride(0), vocab, rows, _p(tokens), _p(pos), _p(seqlens),
+                                    _p(work), _stream()), "decode_tail")
+    return tokens
 
 
 def _check_kv(k_cache, v_cache, B, n_kv_heads, head_dim):
@@ -258,6 +295,29 @@ def attn_fused_ok(n_q_heads: int, n_kv_heads: int, head_dim: int = 128) -> bool:
             and attn_split() // 32 >= G + 2)
 
 
+ATTN_MAX_SPLITS = 16
+
+
+def attn_fused_splits(B: int, n_kv_heads: int, max_ctx: int) -> int:
+    """Key splits for decode_attention_fused.  One split per attn_split()
+    keys (one 32-key group per wave: several workgroups share a CU and hide
+    each other's load latency) up to ATTN_MAX_SPLITS; a longer context keeps
+    ATTN_MAX_SPLITS splits (or enough to give every CU two workgroups) whose
+    waves loop over several groups, so the workspace and the combine stay
+    bounded.  One split per (b, kv-head) writes the output itself (no combine
+    launch) but at batch 32 ran slower than 5 splits + combine (43 vs 31 us,
+    profiles/README.md section 35).  MIVGPU_ATTN_SPLITS=n forces n (0 = one
+    split per attn_split() keys)."""
+    full = max(1, -(-max_ctx // attn_split()))
+    env = os.environ.get("MIVGPU_ATTN_SPLITS")
+    if env is not None and env.strip():
+        n = int(env)
+        return full if n <= 0 else n
+    if full <= ATTN_MAX_SPLITS:
+        return full
+    return min(full, max(ATTN_MAX_SPLITS, -(-2 * visible_cus() // max(1, B * n_kv_heads))))
+
+
 def decode_attention_fused(qkv, q_norm_w, k_norm_w, pos, seqlens, k_cache, v_cache, out, o_part, ml_part,
                            counters, n_q_heads, n_kv_heads, head_dim, nsplit, scale, eps, theta):
     """One launch per layer: QK-norm + RoPE (q heads, new key), KV append at
@@ -266,7 +326,8 @@ def decode_attention_fused(qkv, q_norm_w, k_norm_w, pos, seqlens, k_cache, v_cac
     B = qkv.shape[0]
     max_ctx = _check_kv(k_cache, v_cache, B, n_kv_heads, head_dim)
     need = B * n_q_heads * nsplit
-    if nsplit * attn_split() < max_ctx or o_part.numel() < need * head_dim or ml_part.numel() < need * 2:
+    # any nsplit >= 1 covers max_ctx (each wave loops over its key groups)
+    if nsplit < 1 or o_part.numel() < need * head_dim or ml_part.numel() < need * 2:
         raise ValueError(f"attention workspace too small for nsplit={nsplit}, max_ctx={max_ctx}")
     if counters.dtype != torch.int32 or counters.numel() < B * n_kv_heads:
         raise ValueError("counters must be int32 with B * n_kv_heads entries")
@@ -443,7 +504,12 @@ class PackedLinear:
     def slots(self, M: int) -> int:
         """Sum-of-squares slots a residual call (``norm_call(residual=True)``)
         writes: one per wave-group of the wide plan."""
-        return (self.N // 32) // skinny_plan(M, self.K, self.N, EPI_RESID, variant=VARIANT_WIDE)["nt"]
+        return (self.N // 32) // skinny_plan(M, self.K, self.N, EPI_RESID, variant=self._norm_variant())["nt"]
+
+    def _norm_variant(self) -> int:
+        # the row-norm fusion runs on the wide kernel, or the K-split one when
+        # this projection is set to it
+        return VARIANT_WIDEK if self.variant == VARIANT_WIDEK else VARIANT_WIDE
 
     def norm_call(self, x: torch.Tensor, out: torch.Tensor, row_scale: tuple | None = None,
                   residual: bool = False, ss_out: torch.Tensor | None = None, ks: int = 0, S: int = 0):
@@ -460,9 +526,10 @@ class PackedLinear:
         if residual and (self.silu_mul or ss_out is None or ss_out.numel() < self.slots(M) * SS_ROWS
                          or tuple(out.shape) != (M, self.N)):
             raise ValueError("residual call needs out [M, N], ss_out of slots(M) * SS_ROWS floats, no SiLU")
-        pl = skinny_plan(M, self.K, self.N, epi, 0, ks, S, variant=VARIANT_WIDE)
-        if pl["variant"] != VARIANT_WIDE:
-            raise ValueError(f"row-norm fusion needs the wide kernel; plan {pl}")
+        variant = self._norm_variant()
+        pl = skinny_plan(M, self.K, self.N, EPI_STORE if residual else epi, 0, ks, S, variant=variant)
+        if pl["variant"] not in (VARIANT_WIDE, VARIANT_WIDEK):
+            raise ValueError(f"row-norm fusion needs the wide or K-split kernel; plan {pl}")
         self._ensure_scratch(pl["scratch_floats"], pl["tickets"], x.device)
         sp = _p(self.scratch) if self.scratch is not None else None
         tp = _p(self.tickets) if self.tickets is not None else None
@@ -473,7 +540,7 @@ class PackedLinear:
                 raise ValueError("row_scale slots must be fp32 [nparts * SS_ROWS]")
             rs, inv_dim = _p(part), 1.0 / dim
         _check(lib().mivgpu_skinny_gemm_norm(_p(self.wp), _p(x), _p(out), M, self.K, self.N, x.stride(0),
-                                             out.stride(0), epi, 0, ks, S, VARIANT_WIDE, sp, tp, rs, nparts,
+                                             out.stride(0), epi, 0, ks, S, variant, sp, tp, rs, nparts,
                                              inv_dim, eps, _p(ss_out) if residual else None, _stream()),
                "skinny_gemm_norm")
         return out

@@ -15,6 +15,9 @@
 #   pmc [cfg..] PMC passes over a decode step: whole GPU, 64 CUs, 32 CUs (one counter group per pass)
 #   membw       partition read ceilings (bench/membw.py)
 #   widek       K-split wide GEMM kernel: numerics, GEMM sweep, decode A/B
+#   decode      ops + GEMM GPU tests, decode per partition size and batch 1, whole-GPU kernel trace
+#   normfused   row-norm fusion on the wide / K-split kernels: tests, decode A/B, profile
+#   attnsplit   fused attention, one split per (b, kv-head) vs per 256 keys: tests, decode A/B, profile
 #   mall        projection GEMMs cold vs with their weights prefetched into the Infinity Cache
 #   serving     TTFT / per-token latency, native vs vGPU slices (bench/serving.py)
 #   mixed       governed server + 3 governed decode tenants; 8 x 12 % temporal over 600 steps
@@ -106,6 +109,44 @@ case $suite in
     HSA_CU_MASK=0:0-63 MIVGPU_WIDEK=off step 300 cu64_off python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 100
     step 300 serve_b1 python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 1 --steps 200
     MIVGPU_WIDEK=off step 300 serve_b1_off python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 1 --steps 200 ;;
+  attnsplit)
+    # fused attention with one split per (b, kv-head) (waves loop over the
+    # context, no combine launch) vs one split per 256 keys: numerics, decode A/B
+    step 600 tests python -u -m pytest tests/test_ops_gpu.py -v --timeout 300 --timeout-method thread -k "fused"
+    for sp in "" 0; do
+      tag=split${sp:-auto}
+      MIVGPU_ATTN_SPLITS=$sp step 300 "full_$tag" python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 200
+      HSA_CU_MASK=0:0-63 MIVGPU_ATTN_SPLITS=$sp step 300 "cu64_$tag" python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 100
+      HSA_CU_MASK=0:0-31 MIVGPU_ATTN_SPLITS=$sp step 300 "cu32_$tag" python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 60
+      MIVGPU_ATTN_SPLITS=$sp step 300 "b1_$tag" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 1 --steps 200
+    done
+    cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
+    step 240 prof_full rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_full" -o run -- \
+      python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 20 ;;
+  normfused)
+    # row-norm fusion with qkv / o_proj on the K-split kernel: numerics, decode A/B per partition size
+    step 900 tests python -u -m pytest tests/test_ops_gpu.py tests/test_skinny_gemm_gpu.py -v --timeout 300 \
+      --timeout-method thread -k "norm or fused or widek or row_scale"
+    for nf in 0 1; do
+      MIVGPU_NORM_FUSED=$nf step 300 "full_nf$nf" python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 200
+      HSA_CU_MASK=0:0-63 MIVGPU_NORM_FUSED=$nf step 300 "cu64_nf$nf" python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 100
+      HSA_CU_MASK=0:0-31 MIVGPU_NORM_FUSED=$nf step 300 "cu32_nf$nf" python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 60
+      MIVGPU_NORM_FUSED=$nf step 300 "b1_nf$nf" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 1 --steps 200
+    done
+    cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
+    MIVGPU_NORM_FUSED=1 step 240 prof_nf rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_nf" -o run -- \
+      python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 20 ;;
+  decode)
+    # the ops / GEMM GPU tests, then decode per partition size and batch 1, then a kernel trace of the whole GPU
+    step 900 tests python -u -m pytest tests/test_ops_gpu.py tests/test_skinny_gemm_gpu.py -v --timeout 300 \
+      --timeout-method thread
+    step 300 full python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 200
+    HSA_CU_MASK=0:0-63 step 300 cu64 python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 100
+    HSA_CU_MASK=0:0-31 step 300 cu32 python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 60
+    step 300 b1 python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 1 --steps 200
+    cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
+    step 240 prof rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof" -o run -- \
+      python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 20 ;;
   mall)
     step 300 mall python -u scripts/probe/mall_prefetch.py --out "$out/mall.json" ;;
   membw)

@@ -246,15 +246,19 @@ def _fused_case(ops, B, Hq, Hkv, T, pos_list, seed=0):
     (2, 8, 4, 320, [100, 7]),                    # G = 2
     (2, 16, 16, 96, [50, 95]),                   # G = 1 (MHA)
 ])
-def test_decode_attention_fused(ops, B, Hq, Hkv, T, pos_list):
+@pytest.mark.parametrize("splits", ["full", 1, 2])
+def test_decode_attention_fused(ops, B, Hq, Hkv, T, pos_list, splits):
     """QK-norm + RoPE + KV append + attention + combine in one launch vs the
-    fp32 reference chain (ref.qk_norm_rope_kv -> ref.decode_attention)."""
+    fp32 reference chain (ref.qk_norm_rope_kv -> ref.decode_attention).
+    splits: one split per attn_split() keys (one 32-key group per wave), or
+    fewer splits whose waves loop over several groups (online softmax); one
+    split writes the output itself (no combine)."""
     if not ops.attn_fused_ok(Hq, Hkv):
         pytest.skip("fused attention needs the packed MFMA kernel")
     D = 128
     qkv, qw, kw, k, v, pos, seqlens = _fused_case(ops, B, Hq, Hkv, T, pos_list)
     kc, vc = ops.k_to_cache_layout(k), ops.v_to_cache_layout(v)
-    nsplit = math.ceil(T / ops.attn_split())
+    nsplit = math.ceil(T / ops.attn_split()) if splits == "full" else splits
     out = torch.empty(B, Hq * D, device="cuda", dtype=torch.bfloat16)
     o_part = torch.empty(B * Hq * nsplit * D, device="cuda")
     ml = torch.empty(B * Hq * nsplit * 2, device="cuda")
@@ -329,7 +333,8 @@ def test_decode_attention_fused_modes(mode, mask):
     assert float(err) < 2e-2 and int(cnt) == 0
 
 
-def test_decode_attention_fused_repeated_launches(ops):
+@pytest.mark.parametrize("splits", ["full", 1])
+def test_decode_attention_fused_repeated_launches(ops, splits):
     """Back-to-back launches (the decoder's 36 layers x N steps) reuse one
     counter array: each launch's last workgroup resets it."""
     B, Hq, Hkv, T, D = 3, 32, 8, 608, 128
@@ -338,7 +343,7 @@ def test_decode_attention_fused_repeated_launches(ops):
     qkv, qw, kw, k, v, pos, seqlens = _fused_case(ops, B, Hq, Hkv, T, [300, 511, 17], seed=3)
     kc, vc = ops.k_to_cache_layout(k), ops.v_to_cache_layout(v)
     k_ref, v_ref = k.clone(), v.clone()
-    nsplit = math.ceil(T / ops.attn_split())
+    nsplit = math.ceil(T / ops.attn_split()) if splits == "full" else splits
     out = torch.empty(B, Hq * D, device="cuda", dtype=torch.bfloat16)
     o_part = torch.empty(B * Hq * nsplit * D, device="cuda")
     ml = torch.empty(B * Hq * nsplit * 2, device="cuda")
@@ -357,16 +362,20 @@ def test_decode_attention_fused_repeated_launches(ops):
     assert int(cnt.abs().sum()) == 0
 
 
-def test_decoder_fused_matches_unfused():
+@pytest.mark.parametrize("splits", ["", "1"])
+def test_decoder_fused_matches_unfused(monkeypatch, splits):
     """Whole tiny decoder, 4 steps: the one-launch attention vs the three
-    separate kernels, same weights and context."""
+    separate kernels, same weights and context (default splits and one split
+    per (b, kv-head))."""
     from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
 
+    monkeypatch.setenv("MIVGPU_ATTN_SPLITS", splits)
     a = Qwen3Decoder(QWEN3_TINY, batch=3, max_ctx=96, device="cuda", native=True, seed=4)
-    b = Qwen3Decoder(QWEN3_TINY, batch=3, max_ctx=96, device="cuda", native=True, seed=4)
     if not a.attn_fused:
         pytest.skip("fused attention not selected")
-    b.attn_fused = False
+    monkeypatch.setenv("MIVGPU_ATTN_FUSED", "0")
+    b = Qwen3Decoder(QWEN3_TINY, batch=3, max_ctx=96, device="cuda", native=True, seed=4)
+    assert not b.attn_fused and (splits != "1" or a.nsplit == 1)
     a.fill_context(30)
     b.fill_context(30)
     for _ in range(4):
@@ -389,6 +398,66 @@ def test_decoder_norm_fused_matches_reference(monkeypatch):
     for _ in range(3):
         la, lb = a.step(), b.step()
         _close(la, lb, 5e-2)
+        b.tokens.copy_(a.tokens)
+
+
+@pytest.mark.parametrize("rows,vocab", [(32, 151936), (1, 151936), (3, 4096), (2, 1000)])
+def test_decode_tail_matches_torch(ops, rows, vocab):
+    """argmax (first maximum, ties and NaN as torch.argmax) + pos / seqlens advance."""
+    g = torch.Generator(device="cuda").manual_seed(rows + vocab)
+    logits = torch.randn(rows, vocab, device="cuda", generator=g).bfloat16()
+    logits[0, vocab // 3] = 50.0
+    logits[0, vocab - 1] = 50.0          # tie: the first index wins
+    if rows > 1:
+        logits[1, 7] = float("nan")      # NaN is the maximum
+    tokens = torch.full((rows,), -1, dtype=torch.int64, device="cuda")
+    pos = torch.arange(rows, dtype=torch.int32, device="cuda")
+    seqlens = pos + 1
+    work = ops.decode_tail_workspace(rows, "cuda")
+    for it in range(2):   # the workspace comes back zeroed for the next launch
+        ops.decode_tail(logits, tokens, pos, seqlens, work)
+        assert torch.equal(tokens, torch.argmax(logits, dim=-1))
+        assert torch.equal(pos.cpu(), torch.arange(rows, dtype=torch.int32) + 1 + it)
+        assert torch.equal(seqlens.cpu(), torch.arange(rows, dtype=torch.int32) + 2 + it)
+        assert int(work.abs().sum()) == 0
+        logits = -logits      # a different maximum on the second launch
+
+
+@pytest.mark.parametrize("rows,dim", [(32, 4096), (1, 4096), (5, 512)])
+def test_embed_rmsnorm_matches_reference(ops, rows, dim):
+    g = torch.Generator(device="cuda").manual_seed(rows * dim)
+    embed = torch.randn(1000, dim, device="cuda", generator=g).bfloat16()
+    w = (1 + 0.1 * torch.randn(dim, device="cuda", generator=g)).bfloat16()
+    tokens = torch.randint(0, 1000, (rows,), device="cuda", generator=g)
+    res = torch.empty(rows, dim, device="cuda", dtype=torch.bfloat16)
+    out = torch.empty_like(res)
+    ops.embed_rmsnorm(embed, tokens, w, 1e-6, res=res, out=out)
+    assert torch.equal(res, embed[tokens])
+    _close(out, ref.rmsnorm(embed[tokens], w, 1e-6), 1e-2)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_decoder_norm_fused_prefill_matches_reference(monkeypatch, graph):
+    """Prompt processing of the norm-fused decoder (RMSNorm folded into the
+    packed columns, row scales from per-chunk sums of squares) vs the fp32
+    reference decoder, eager and replayed from a captured bucket graph, then
+    two decode steps from the prompt's state."""
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
+
+    monkeypatch.setenv("MIVGPU_NORM_FUSED", "1")
+    a = Qwen3Decoder(QWEN3_TINY, batch=2, max_ctx=256, device="cuda", native=True, seed=8)
+    assert a.norm_fused
+    b = Qwen3Decoder(QWEN3_TINY, batch=2, max_ctx=256, device="cuda", native=False, seed=8)
+    prompt = torch.randint(0, QWEN3_TINY.vocab, (150,), generator=torch.Generator().manual_seed(2))
+    if graph:
+        a.reserve_prefill()
+        a.capture_prefill(buckets=(256,), b=1)
+    la, lb = a.prefill(prompt, b=1), b.prefill(prompt, b=1)
+    _close(la, lb, 5e-2)
+    assert int(a.pos[1]) == int(b.pos[1]) == 150
+    b.tokens.copy_(a.tokens)
+    for _ in range(2):
+        _close(a.step()[1], b.step()[1], 5e-2)
         b.tokens.copy_(a.tokens)
 
 

@@ -141,12 +141,14 @@ def _rms_ref(x, w, eps=1e-6):
     return xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
 
 
+@pytest.mark.parametrize("variant", ["wide", "widek"])
 @pytest.mark.parametrize("S", [0, 1, 4])
 @pytest.mark.parametrize("M", [1, 5, 32, 48])
-def test_row_norm_fusion_chain(M, S):
+def test_row_norm_fusion_chain(M, S, variant):
     """o_proj-like residual call (res += X.W^T, per-slot sums of squares) then
     a gate_up-like call that applies RMSNorm through folded column weights and
-    row scales from those slots, vs. add + RMSNorm + GEMM in fp32."""
+    row scales from those slots, vs. add + RMSNorm + GEMM in fp32; on the wide
+    kernel and on the K-split one (variant 3)."""
     g = torch.Generator(device="cuda").manual_seed(M * 13 + S)
     K, N1, N2 = 4096, 4096, 2048
     res = torch.randn(M, K, device="cuda", generator=g).bfloat16()
@@ -156,6 +158,9 @@ def test_row_norm_fusion_chain(M, S):
     wg = (torch.randn(N2, K, device="cuda", generator=g) * 0.02).bfloat16()
     po = ops.PackedLinear(wo)
     pg = ops.PackedLinear(wg, col_scale=wn)
+    if variant == "widek":
+        po.variant = pg.variant = ops.VARIANT_WIDEK
+        assert ops.skinny_plan(M, K, N1, ops.EPI_STORE, 0, 0, S, ops.VARIANT_WIDEK)["variant"] == ops.VARIANT_WIDEK
     slots = po.slots(M)
     ss = torch.full((slots * ops.SS_ROWS,), float("nan"), device="cuda")   # every used slot must be written
     r1 = res.clone()
