@@ -133,7 +133,7 @@ rmsnorm_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ res, const bf1
 __global__ void __launch_bounds__(256)
 embed_rmsnorm_kernel(const bf16_t* __restrict__ embed, const int64_t* __restrict__ tokens,
                      const bf16_t* __restrict__ w, bf16_t* __restrict__ res, bf16_t* __restrict__ out, int dim,
-                     long long vocab, float eps) {
+                     long long vocab, float eps, float* __restrict__ ss_out) {
   const int row = blockIdx.x;
   const int t = threadIdx.x;
   long long tok = tokens[row];
@@ -141,7 +141,9 @@ embed_rmsnorm_kernel(const bf16_t* __restrict__ embed, const int64_t* __restrict
   const uint4* xr = reinterpret_cast<const uint4*>(embed + (size_t)tok * dim);
   uint4* rr = reinterpret_cast<uint4*>(res + (size_t)row * dim);
   uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * dim);
-  const uint4* wv = reinterpret_cast<const uint4*>(w);
+  // w may be null when only the sums of squares are wanted (out == nullptr):
+  // then the norm weight is never read
+  const uint4* wv = reinterpret_cast<const uint4*>(out != nullptr ? w : embed);
   __shared__ float red[4];
   constexpr int MAXV = 4;
   const int nvec = dim / 8;
@@ -167,7 +169,10 @@ embed_rmsnorm_kernel(const bf16_t* __restrict__ embed, const int64_t* __restrict
   ss = wave_sum(ss);
   if ((t & 63) == 0) red[t >> 6] = ss;
   __syncthreads();
-  const float inv = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)dim + eps);
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  if (ss_out != nullptr && t == 0) ss_out[row] = tot;   // the norm-fused decoder's first row-scale slot
+  if (out == nullptr) return;
+  const float inv = rsqrtf(tot / (float)dim + eps);
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) {
     const int vi = t + k * 256;
@@ -1132,11 +1137,13 @@ int mivgpu_rmsnorm(const void* x, const void* w, void* out, int rows, int dim, f
   return (int)hipGetLastError();
 }
 
+// out == nullptr: only res and the rows' sums of squares (ss_out[row]).
 int mivgpu_embed_rmsnorm(const void* embed, const int64_t* tokens, const void* w, void* res, void* out, int rows,
-                         int dim, long long vocab, float eps, hipStream_t s) {
-  if (dim % 8 || dim > 8192 || rows <= 0 || vocab <= 0) return -1;
+                         int dim, long long vocab, float eps, float* ss_out, hipStream_t s) {
+  if (dim % 8 || dim > 8192 || rows <= 0 || vocab <= 0 || (out == nullptr && ss_out == nullptr)) return -1;
+  if (out != nullptr && w == nullptr) return -1;
   hipLaunchKernelGGL(embed_rmsnorm_kernel, dim3(rows), dim3(256), 0, s, (const bf16_t*)embed, tokens,
-                     (const bf16_t*)w, (bf16_t*)res, (bf16_t*)out, dim, vocab, eps);
+                     (const bf16_t*)w, (bf16_t*)res, (bf16_t*)out, dim, vocab, eps, ss_out);
   return (int)hipGetLastError();
 }
 

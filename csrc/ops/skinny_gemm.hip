@@ -707,14 +707,15 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
 // place and writes one sum-of-squares slot per n-tile (the old residual tile
 // is fetched by LDS-DMA at the start, off the critical path); rs_part != null
 // scales the rows of a store by the producer's slots (rs_issue / rs_finish).
-template <int MT, int KW, int EPI>
+// NT = 2 with EPI_SILU_MUL: a gate tile and its up tile (gate_up), both
+// carried by every k-wave, SiLU(gate)*up by the reducing wave.
+template <int MT, int NT, int KW, int EPI>
 __global__ void __launch_bounds__(64 * KW)
 skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int M,
                     int K, int N, int ldx, int ldy, int S, float* __restrict__ scratch, int* __restrict__ tickets,
                     int kmajor, const float* __restrict__ rs_part, int rs_nparts, float rs_inv_dim, float rs_eps,
                     float* __restrict__ ss_out) {
-  static_assert(EPI == EPI_STORE || EPI == EPI_RESID, "widek: stores or the residual update");
-  constexpr int NT = 1;
+  static_assert((EPI == EPI_SILU_MUL) == (NT == 2) && NT <= 2, "widek: one tile, or a gate/up pair for SiLU*up");
   constexpr int U = 2;                               // k-blocks per wave per group
   constexpr int GK = KW * U;                         // k-blocks per group (the X tile)
   constexpr int PITCH = GK * 64 + 8;                 // +16 B per row: conflict-free ds_read_b128
@@ -722,7 +723,7 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
   constexpr int NTHREADS = 64 * KW;
   constexpr int XC = MT * GK * 256 / NTHREADS;       // X chunks per thread per group
   static_assert(XC * NTHREADS == MT * GK * 256, "X tile must split evenly over the workgroup");
-  static_assert(KW * MT * 16 * 64 * 4 <= 2 * XBUF * 2, "the k-wave reduction reuses the X buffers");
+  static_assert(KW * MT * NT * 16 * 64 * 4 <= 2 * XBUF * 2, "the k-wave reduction reuses the X buffers");
   __shared__ __attribute__((aligned(16))) bf16_t xs[2 * XBUF];
   constexpr bool RS = EPI != EPI_RESID;
   __shared__ float s_rs[MT * 32];
@@ -733,7 +734,8 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
   const int kw = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
   const int KB = K >> 6;
-  const int tile0 = blockIdx.x / S, split = blockIdx.x % S;
+  const int vgroup = blockIdx.x / S, split = blockIdx.x % S;
+  const int tile0 = vgroup * NT;
   const float* rs = (RS && rs_part) ? s_rs : nullptr;
   const WStride ws = kmajor ? WStride{256, (size_t)(N >> 5) * 256} : WStride{(size_t)KB * 256, 256};
   const u32x4_t* wbase = wp + (size_t)tile0 * ws.tile;
@@ -744,7 +746,9 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[m][0][e] = 0.f;
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[m][t][e] = 0.f;
 
   WFrag<NT> fa[U], fb[U];
   {
@@ -811,7 +815,9 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) red[(((kw - 1) * MT + m) * 16 + e) * 64 + lane] = acc[m][0][e];
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) red[((((kw - 1) * MT + m) * NT + t) * 16 + e) * 64 + lane] = acc[m][t][e];
   }
   __syncthreads();
   if (kw > 0) return;
@@ -820,32 +826,36 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[m][0][e] += red[(((w - 1) * MT + m) * 16 + e) * 64 + lane];
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[m][t][e] += red[((((w - 1) * MT + m) * NT + t) * 16 + e) * 64 + lane];
   if constexpr (EPI == EPI_RESID) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // residual tile landed
   if (S == 1) {
-    wide_epilogue<MT, NT, EPI>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, tile0, r, h, rs,
-                               ss_out, s_res);
+    wide_epilogue<MT, NT, EPI>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, vgroup, r, h,
+                               rs, ss_out, s_res);
     return;
   }
   constexpr int SLAB = MT * NT * 16 * 64;
-  float* sc = scratch + (size_t)tile0 * SLAB;
+  float* sc = scratch + (size_t)vgroup * SLAB;
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) atomicAdd(sc + (m * 16 + e) * 64 + lane, acc[m][0][e]);
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) atomicAdd(sc + ((m * NT + t) * 16 + e) * 64 + lane, acc[m][t][e]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   int ticket = 0;
-  if (lane == 0) ticket = atomicAdd(tickets + tile0, 1);
+  if (lane == 0) ticket = atomicAdd(tickets + vgroup, 1);
   ticket = __shfl(ticket, 0, 64);
   if (ticket != S - 1) return;
   wide_epilogue<MT, NT, EPI>(
       [&](int m, int t, int e) {
         return __hip_atomic_load(sc + ((m * NT + t) * 16 + e) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       },
-      y, M, ldy, tile0, tile0, r, h, rs, ss_out, s_res);
+      y, M, ldy, tile0, vgroup, r, h, rs, ss_out, s_res);
 #pragma unroll
   for (int i = 0; i < SLAB / 64; ++i) sc[i * 64 + lane] = 0.f;
-  if (lane == 0) tickets[tile0] = 0;
+  if (lane == 0) tickets[vgroup] = 0;
 }
 
 // Pack W[N][K] (row-major bf16) into the fragment order above.
@@ -962,11 +972,11 @@ hipError_t launch_wide_resid(int mt, int wv, const Args& a, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
-template <int MT, int EPI>
+template <int MT, int NT, int EPI>
 hipError_t launch_widek(int kw, const Args& a, hipStream_t s) {
-  const int blocks = (a.N / 32) * a.S;
+  const int blocks = (a.N / 32) / NT * a.S;
 #define MIVGPU_LAUNCH_WIDEK(KW)                                                                                   \
-  hipLaunchKernelGGL((skinny_widek_kernel<MT, KW, EPI>), dim3(blocks), dim3(64 * KW), 0, s, (const u32x4_t*)a.wp, \
+  hipLaunchKernelGGL((skinny_widek_kernel<MT, NT, KW, EPI>), dim3(blocks), dim3(64 * KW), 0, s, (const u32x4_t*)a.wp, \
                      (const bf16_t*)a.x, (bf16_t*)a.y, a.M, a.K, a.N, a.ldx, a.ldy, a.S, a.scratch, a.tickets,      \
                      a.kmajor, a.rs_part, a.rs_nparts, a.rs_inv_dim, a.rs_eps, a.ss_out)
   switch (kw) {
@@ -1116,15 +1126,18 @@ bool plan_wide(int M, int K, int N, int epi, int* nt, int* wv, int* S) {
   return *S >= 1 && KB % (*S * U) == 0 && KB / *S >= U;
 }
 
-// K-split wide plan (variant 3): nt = 1, ks = k-waves per workgroup (2 or 4,
-// default 4), S = inter-workgroup split (default 1).  Stores (optionally row
-// scaled) or the residual update (planned as stores), M <= 64.
+// K-split wide plan (variant 3): nt = 1 (nt = 2 for SiLU*up: a gate/up tile
+// pair), ks = k-waves per workgroup (2 or 4, default 4), S = inter-workgroup
+// split (default 1).  Stores (optionally row scaled), SiLU*up, or the residual
+// update (planned as stores), M <= 64.
 // False when it cannot run these values.
 bool plan_widek(int M, int K, int N, int epi, int* nt, int* kw, int* S) {
   static const int cus = mivgpu_ops_visible_cus();
-  if (epi != EPI_STORE || M > 64) return false;
-  if (*nt > 1) return false;
-  *nt = 1;
+  if ((epi != EPI_STORE && epi != EPI_SILU_MUL) || M > 64) return false;
+  const int want = epi == EPI_SILU_MUL ? 2 : 1;   // SiLU*up: a gate/up tile pair per workgroup
+  if (*nt > 0 && *nt != want) return false;
+  *nt = want;
+  if ((N / 32) % want) return false;
   if (*kw <= 0) *kw = 4;
   if (*kw != 2 && *kw != 4) return false;
   const int KB = K / 64, GK = *kw * 2;
@@ -1239,7 +1252,8 @@ int mivgpu_skinny_gemm_norm(const void* wp, const void* x, void* y, int M, int K
   const int v = resolve(M, K, N, epi == EPI_RESID ? EPI_STORE : epi, &nt, &ks, &S,
                         fused ? (variant == 3 ? 3 : 2) : variant);
   if (v == 3) {
-    if (ldy < N || (S > 1 && (scratch == nullptr || tickets == nullptr))) return (int)hipErrorInvalidValue;
+    if ((epi == EPI_SILU_MUL ? ldy < N / 2 : ldy < N) || (S > 1 && (scratch == nullptr || tickets == nullptr)))
+      return (int)hipErrorInvalidValue;
     Args a{wp, x, y, M, K, N, ldx, ldy, S, scratch, tickets, false, use_kmajor() ? 1 : 0};
     a.rs_part = rs_part;
     a.rs_nparts = rs_nparts;
@@ -1249,8 +1263,11 @@ int mivgpu_skinny_gemm_norm(const void* wp, const void* x, void* y, int M, int K
     const int mt = mt_of(M);
     if (rs_part != nullptr && (epi == EPI_RESID || rs_nparts > 64 * ks * RS_LMAX / (mt * 8)))
       return (int)hipErrorInvalidValue;
-    if (epi == EPI_RESID) return (int)(mt == 1 ? launch_widek<1, EPI_RESID>(ks, a, s) : launch_widek<2, EPI_RESID>(ks, a, s));
-    return (int)(mt == 1 ? launch_widek<1, EPI_STORE>(ks, a, s) : launch_widek<2, EPI_STORE>(ks, a, s));
+    if (epi == EPI_RESID)
+      return (int)(mt == 1 ? launch_widek<1, 1, EPI_RESID>(ks, a, s) : launch_widek<2, 1, EPI_RESID>(ks, a, s));
+    if (epi == EPI_SILU_MUL)
+      return (int)(mt == 1 ? launch_widek<1, 2, EPI_SILU_MUL>(ks, a, s) : launch_widek<2, 2, EPI_SILU_MUL>(ks, a, s));
+    return (int)(mt == 1 ? launch_widek<1, 1, EPI_STORE>(ks, a, s) : launch_widek<2, 1, EPI_STORE>(ks, a, s));
   }
   if (v == 2) {
     if (epi == EPI_SILU_MUL && ldy < N / 2) return (int)hipErrorInvalidValue;

@@ -148,7 +148,9 @@ struct TRange {
 };
 
 // ------------------------------------------------------ re-entrancy guard --
-thread_local int t_depth = 0;
+// initial-exec TLS: a direct thread-pointer access on every hook instead of a
+// __tls_get_addr call (the shim is preloaded, so it has static TLS space)
+__attribute__((tls_model("initial-exec"))) thread_local int t_depth = 0;
 struct Guard {
   bool outer;
   Guard() : outer(t_depth == 0) { ++t_depth; }
@@ -2797,7 +2799,7 @@ MIVGPU_EXPORT hipError_t hipGetProcAddress(const char* symbol, void** pfn, int h
 extern char** environ;
 
 namespace {
-thread_local bool t_in_getenv = false;
+__attribute__((tls_model("initial-exec"))) thread_local bool t_in_getenv = false;
 bool enforced_env_key(const char* name) {
   return !strcmp(name, "GPU_MAX_HW_QUEUES") || !strcmp(name, "HSA_CU_MASK") || !strcmp(name, "ROCR_VISIBLE_DEVICES");
 }

@@ -86,10 +86,10 @@ def main():
             t_sk = _time(lambda i: lins[i % ncopy](x, out=out), a.reps)
             t_wide = _time(lambda i: lins[i % ncopy](x, out=out, variant=ops.VARIANT_WIDE), a.reps)
             widek = {}
-            if not silu and M <= 64:
+            if M <= 64:
                 for kw in (2, 4):
                     for S in (0, 1, 2, 4):
-                        if ops.skinny_plan(M, K, N, lin.epi, 1, kw, S, ops.VARIANT_WIDEK)["variant"] != ops.VARIANT_WIDEK:
+                        if ops.skinny_plan(M, K, N, lin.epi, 0, kw, S, ops.VARIANT_WIDEK)["variant"] != ops.VARIANT_WIDEK:
                             continue
                         widek[f"kw{kw}_S{S or 'auto'}"] = round(_time(
                             lambda i: lins[i % ncopy](x, out=out, ks=kw, S=S, variant=ops.VARIANT_WIDEK), a.reps), 2)

@@ -150,7 +150,7 @@ class Qwen3Decoder:
         # CUs idle and hipBLASLt is slower: qkv 13.6 vs 15.1 us, o_proj 12.2 vs
         # 13.3 at 32 rows; 11.6 vs 14.3 / 10.0 vs 10.6 at 1 row
         # (profiles/round3/widek_gemm.json).  Inside a CU partition the tuned
-        # wide plans stay.  MIVGPU_WIDEK=qkv,o,down picks the set, "off" none.
+        # wide plans stay.  MIVGPU_WIDEK=qkv,o,down,gu picks the set, "off" none.
         wk_env = os.environ.get("MIVGPU_WIDEK")
         if wk_env is None:
             wk_env = "qkv,o" if (self.native and ops.visible_cus() > 160) else ""
@@ -161,20 +161,23 @@ class Qwen3Decoder:
             self.skinny_o = True
         if self.skinny:
             # Keep only the packed copies (no duplicate 16 GB of weights).
+            # batch-1 serving on the whole chip keeps the plain gate_up too, for
+            # prompts (hipBLASLt + SiLU 58 vs wide 93 us at 128 rows; +201
+            # MB/layer); qkv keeps it wherever it runs on the K-split kernel
+            # (hipBLASLt 25 vs wide 50 us at 128 rows; +50 MB/layer).  With the
+            # norm fusion the packed copies carry the RMSNorm weight in their
+            # columns and the plain ones stay unscaled (prefill normalises first).
+            keep_gu = batch <= 16 and ops.visible_cus() > int(os.environ.get("MIVGPU_SLICE_PLAN_CUS", "96"))
+            keep_qkv = "qkv" in widek and ops.visible_cus() > 160
             for lw in self.w.layers:
                 if self.norm_fused:
-                    lw["pqkv"] = ops.PackedLinear(lw.pop("wqkv"), col_scale=lw["ln1"])
-                    lw["pgu"] = ops.PackedLinear(lw.pop("wgu"), silu_mul=True, col_scale=lw["ln2"])
+                    lw["pqkv"] = ops.PackedLinear(lw["wqkv"] if keep_qkv else lw.pop("wqkv"), col_scale=lw["ln1"])
+                    lw["pgu"] = ops.PackedLinear(lw["wgu"] if keep_gu else lw.pop("wgu"), silu_mul=True,
+                                                 col_scale=lw["ln2"])
                 else:
                     if self.skinny_gate_up:
-                        # batch-1 serving on the whole chip: the plain copy too, for
-                        # prompts (hipBLASLt + SiLU 58 vs wide 93 us at 128 rows; +201 MB/layer)
-                        keep_gu = batch <= 16 and ops.visible_cus() > int(os.environ.get("MIVGPU_SLICE_PLAN_CUS", "96"))
                         lw["pgu"] = ops.PackedLinear(lw["wgu"] if keep_gu else lw.pop("wgu"), silu_mul=True)
                     if self.skinny_qkv:
-                        # on the whole chip the plain copy stays for prompt-sized GEMMs
-                        # (hipBLASLt 25 vs wide 50 us at 128 rows; +50 MB/layer)
-                        keep_qkv = "qkv" in widek and ops.visible_cus() > 160
                         lw["pqkv"] = ops.PackedLinear(lw["wqkv"] if keep_qkv else lw.pop("wqkv"))
                 if self.skinny_o:
                     # on the whole chip the plain copy stays for prompt-sized
@@ -182,7 +185,7 @@ class Qwen3Decoder:
                     keep = ops.visible_cus() > int(os.environ.get("MIVGPU_SLICE_PLAN_CUS", "96"))
                     lw["po"] = ops.PackedLinear(lw["wo"] if keep else lw.pop("wo"))
                 lw["pd"] = ops.PackedLinear(lw.pop("wd"))
-                for key, name in (("pqkv", "qkv"), ("po", "o"), ("pd", "down")):
+                for key, name in (("pqkv", "qkv"), ("po", "o"), ("pd", "down"), ("pgu", "gu")):
                     if name in widek and key in lw:
                         lw[key].variant = ops.VARIANT_WIDEK
             self.p_lm = ops.PackedLinear(self.w.lm_head, col_scale=self.w.final_norm if self.norm_fused else None)
@@ -286,9 +289,9 @@ class Qwen3Decoder:
         (qkv, attention, combine, o_proj+residual, gate_up+SiLU, down+residual)."""
         cfg, w = self.cfg, self.w
         h, eps = cfg.hidden, cfg.eps
-        torch.index_select(w.embed, 0, self.tokens, out=self.res)
-        # the first norm's sums of squares (one slot), later ones come from the epilogues
-        torch.sum(self.res.float().pow(2), dim=-1, out=self.ss_a.view(-1, ops.SS_ROWS)[0, :self.B])
+        # gather + the first norm's sums of squares (one slot) in one launch;
+        # later slots come from the epilogues
+        ops.embed_rmsnorm(w.embed, self.tokens, None, cfg.eps, res=self.res, out=None, ss_out=self.ss_a)
         na = 1
         for li, lw in enumerate(w.layers):
             qkv = lw["pqkv"].norm_call(self.res, out=self.qkv_buf, row_scale=(self.ss_a, na, h, eps))
@@ -403,13 +406,23 @@ class Qwen3Decoder:
             pl.norm_call(x[s:e], out=out[s:e], row_scale=(self.ss_pf, 1, self.cfg.hidden, self.cfg.eps))
         return out
 
+    def _normed_proj(self, lw, name, x, ln):
+        """Norm-fused decoder, prefill: RMSNorm(x) . W^T (SiLU*up for gate_up)
+        on the plain weight after a separate norm where one is kept and the
+        rows are prompt-sized, else on the packed copy with the folded norm."""
+        packed, plain = {"qkv": ("pqkv", "wqkv"), "gu": ("pgu", "wgu")}[name]
+        if plain in lw and x.shape[0] > 64:
+            y = F.linear(self._norm(x, ln), lw[plain])
+            return ops.silu_mul(y) if name == "gu" else y
+        return self._rows_normed(lw[packed], x)     # gate_up: SiLU*up fused in the epilogue
+
     def _prefill_impl_norm_fused(self, bufs: dict, b: int):
         cfg, w = self.cfg, self.w
         res = torch.index_select(w.embed, 0, bufs["ids"])
         for li, lw in enumerate(w.layers):
-            q, k, v = self._prefill_qk(li, lw, self._rows_normed(lw["pqkv"], res), bufs["pos"], b)
+            q, k, v = self._prefill_qk(li, lw, self._normed_proj(lw, "qkv", res, lw["ln1"]), bufs["pos"], b)
             res = res + self._proj(lw, "o", self._prefill_attention(q, k, v, bufs["mask"]))
-            res = res + self._proj(lw, "d", self._rows_normed(lw["pgu"], res))   # SiLU*up in the epilogue
+            res = res + self._proj(lw, "d", self._normed_proj(lw, "gu", res, lw["ln2"]))
         last = torch.index_select(res, 0, bufs["last"])
         logits = self._rows_normed(self.p_lm, last)
         torch.argmax(logits, dim=-1, out=self.tokens[b:b + 1])

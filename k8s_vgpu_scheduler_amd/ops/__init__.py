@@ -38,7 +38,7 @@ def lib():
         vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
         L.mivgpu_rmsnorm.argtypes = [vp, vp, vp, i, i, f, vp]
         L.mivgpu_add_rmsnorm.argtypes = [vp, vp, vp, vp, i, i, f, vp]
-        L.mivgpu_embed_rmsnorm.argtypes = [vp, vp, vp, vp, vp, i, i, ctypes.c_longlong, f, vp]
+        L.mivgpu_embed_rmsnorm.argtypes = [vp, vp, vp, vp, vp, i, i, ctypes.c_longlong, f, vp, vp]
         L.mivgpu_decode_tail.argtypes = [vp, i, i, i, vp, vp, vp, vp, vp]
         L.mivgpu_qk_norm_rope_kv.argtypes = [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, f, f, vp]
         L.mivgpu_prefill_qk_norm_rope_kv.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, f, f,
@@ -115,16 +115,20 @@ def add_rmsnorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: float,
     return out
 
 
-def embed_rmsnorm(embed: torch.Tensor, tokens: torch.Tensor, w: torch.Tensor, eps: float, res: torch.Tensor,
-                  out: torch.Tensor):
+def embed_rmsnorm(embed: torch.Tensor, tokens: torch.Tensor, w: torch.Tensor | None, eps: float, res: torch.Tensor,
+                  out: torch.Tensor | None, ss_out: torch.Tensor | None = None):
     """Decode-step head in one launch: res = embed[tokens] (ids clamped to
-    the table), out = rmsnorm(res) * w."""
+    the table), out = rmsnorm(res) * w; ss_out (fp32, >= B) receives the
+    rows' sums of squares (out may then be None: the norm-fused decoder)."""
     rows, dim = res.shape
-    if (tokens.dtype != torch.int64 or tokens.numel() != rows or embed.shape[1] != dim or out.shape != res.shape
-            or not (embed.is_contiguous() and res.is_contiguous() and out.is_contiguous())):
-        raise ValueError("embed_rmsnorm: embed [V, D], tokens int64 [B], res / out [B, D] contiguous")
-    _check(lib().mivgpu_embed_rmsnorm(_p(embed), _p(tokens), _p(w), _p(res), _p(out), rows, dim, embed.shape[0],
-                                      eps, _stream()), "embed_rmsnorm")
+    if (tokens.dtype != torch.int64 or tokens.numel() != rows or embed.shape[1] != dim
+            or (out is not None and (out.shape != res.shape or not out.is_contiguous() or w is None))
+            or (ss_out is not None and (ss_out.dtype != torch.float32 or ss_out.numel() < rows))
+            or (out is None and ss_out is None) or not (embed.is_contiguous() and res.is_contiguous())):
+        raise ValueError("embed_rmsnorm: embed [V, D], tokens int64 [B], res / out [B, D] contiguous, ss_out fp32 [B]")
+    _check(lib().mivgpu_embed_rmsnorm(_p(embed), _p(tokens), _p(w) if w is not None else None, _p(res),
+                                      _p(out) if out is not None else None, rows, dim, embed.shape[0], eps,
+                                      _p(ss_out) if ss_out is not None else None, _stream()), "embed_rmsnorm")
     return out
 
 

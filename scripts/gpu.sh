@@ -138,6 +138,8 @@ case $suite in
       python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 20 ;;
   decode)
     # the ops / GEMM GPU tests, then decode per partition size and batch 1, then a kernel trace of the whole GPU
+    # (extra env for an A/B: e.g. DEC_ENV="MIVGPU_WIDEK=qkv,o,gu")
+    [ -n "$DEC_ENV" ] && export $DEC_ENV
     step 900 tests python -u -m pytest tests/test_ops_gpu.py tests/test_skinny_gemm_gpu.py -v --timeout 300 \
       --timeout-method thread
     step 300 full python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 200

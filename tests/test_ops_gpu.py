@@ -431,13 +431,18 @@ def test_embed_rmsnorm_matches_reference(ops, rows, dim):
     tokens = torch.randint(0, 1000, (rows,), device="cuda", generator=g)
     res = torch.empty(rows, dim, device="cuda", dtype=torch.bfloat16)
     out = torch.empty_like(res)
-    ops.embed_rmsnorm(embed, tokens, w, 1e-6, res=res, out=out)
+    ss = torch.full((rows,), float("nan"), device="cuda")
+    ops.embed_rmsnorm(embed, tokens, w, 1e-6, res=res, out=out, ss_out=ss)
     assert torch.equal(res, embed[tokens])
     _close(out, ref.rmsnorm(embed[tokens], w, 1e-6), 1e-2)
+    _close(ss, embed[tokens].float().pow(2).sum(-1), 1e-4)
+    res.zero_()
+    ops.embed_rmsnorm(embed, tokens, None, 1e-6, res=res, out=None, ss_out=ss)   # the norm-fused head
+    assert torch.equal(res, embed[tokens])
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_decoder_norm_fused_prefill_matches_reference(monkeypatch, graph):
+@pytest.mark.parametrize("graph,plen", [(False, 150), (True, 150), (False, 40), (True, 40)])
+def test_decoder_norm_fused_prefill_matches_reference(monkeypatch, graph, plen):
     """Prompt processing of the norm-fused decoder (RMSNorm folded into the
     packed columns, row scales from per-chunk sums of squares) vs the fp32
     reference decoder, eager and replayed from a captured bucket graph, then
@@ -448,13 +453,15 @@ def test_decoder_norm_fused_prefill_matches_reference(monkeypatch, graph):
     a = Qwen3Decoder(QWEN3_TINY, batch=2, max_ctx=256, device="cuda", native=True, seed=8)
     assert a.norm_fused
     b = Qwen3Decoder(QWEN3_TINY, batch=2, max_ctx=256, device="cuda", native=False, seed=8)
-    prompt = torch.randint(0, QWEN3_TINY.vocab, (150,), generator=torch.Generator().manual_seed(2))
+    # 150 rows: the plain weights after a separate norm (hipBLASLt); 40 rows:
+    # the packed copies with the folded norm and row scales
+    prompt = torch.randint(0, QWEN3_TINY.vocab, (plen,), generator=torch.Generator().manual_seed(2))
     if graph:
         a.reserve_prefill()
-        a.capture_prefill(buckets=(256,), b=1)
+        a.capture_prefill(buckets=(64, 256), b=1)
     la, lb = a.prefill(prompt, b=1), b.prefill(prompt, b=1)
     _close(la, lb, 5e-2)
-    assert int(a.pos[1]) == int(b.pos[1]) == 150
+    assert int(a.pos[1]) == int(b.pos[1]) == plen
     b.tokens.copy_(a.tokens)
     for _ in range(2):
         _close(a.step()[1], b.step()[1], 5e-2)
@@ -484,14 +491,40 @@ def test_skinny_widek_matches_reference(ops, M, N, K, kw, S):
         assert int(lin.tickets.abs().sum()) == 0 and float(lin.scratch.abs().sum()) == 0.0
 
 
-def test_decoder_widek_matches_reference(monkeypatch):
-    """qkv, o_proj and down on the K-split wide kernel (MIVGPU_WIDEK): 3 steps
-    against the fp32 reference decoder."""
+@pytest.mark.parametrize("M,K,inter", [(1, 4096, 12288), (32, 4096, 12288), (48, 1024, 2048), (5, 512, 1024)])
+@pytest.mark.parametrize("kw,S", [(4, 0), (2, 1), (4, 2)])
+def test_skinny_widek_silu_matches_reference(ops, M, K, inter, kw, S):
+    """K-split kernel on gate/up tile pairs with the SiLU(gate)*up epilogue
+    (Qwen3-8B gate_up and small shapes) vs fp32, twice (slabs left clean)."""
+    g = torch.Generator(device="cuda").manual_seed(M + K + inter + kw)
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(2 * inter, K, device="cuda", generator=g) * 0.02).bfloat16()
+    lin = ops.PackedLinear(w, silu_mul=True)
+    pl = ops.skinny_plan(M, K, 2 * inter, lin.epi, 0, kw, S, ops.VARIANT_WIDEK)
+    if pl["variant"] != ops.VARIANT_WIDEK:
+        pytest.skip(f"plan {pl}")
+    assert pl["nt"] == 2
+    gu = (x.float() @ w.float().t()).bfloat16().float()
+    exp = torch.nn.functional.silu(gu[:, :inter]) * gu[:, inter:]
+    for _ in range(2):
+        out = lin(x, ks=kw, S=S, variant=ops.VARIANT_WIDEK)
+        torch.cuda.synchronize()
+        _close(out, exp, 3e-2)
+    if lin.tickets is not None:
+        assert int(lin.tickets.abs().sum()) == 0 and float(lin.scratch.abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("nf", ["0", "1"])
+def test_decoder_widek_matches_reference(monkeypatch, nf):
+    """qkv, o_proj, down and gate_up on the K-split wide kernel (MIVGPU_WIDEK),
+    with and without the row-norm fusion: 3 steps against the fp32 reference
+    decoder."""
     from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
 
-    monkeypatch.setenv("MIVGPU_WIDEK", "qkv,o,down")
+    monkeypatch.setenv("MIVGPU_WIDEK", "qkv,o,down,gu")
+    monkeypatch.setenv("MIVGPU_NORM_FUSED", nf)
     a = Qwen3Decoder(QWEN3_TINY, batch=6, max_ctx=64, device="cuda", native=True, seed=11)
-    assert a.w.layers[0]["pd"].variant == 3 and a.skinny_qkv and a.skinny_o
+    assert a.w.layers[0]["pd"].variant == 3 and a.w.layers[0]["pgu"].variant == 3 and a.skinny_qkv and a.skinny_o
     b = Qwen3Decoder(QWEN3_TINY, batch=6, max_ctx=64, device="cuda", native=False, seed=11)
     a.fill_context(12)
     b.fill_context(12)
