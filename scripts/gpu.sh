@@ -148,7 +148,9 @@ case $suite in
     step 300 b1 python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 1 --steps 200
     cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
     step 240 prof rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof" -o run -- \
-      python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 20 ;;
+      python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 20
+    step 240 prof_b1 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_b1" -o run -- \
+      python3 -m k8s_vgpu_scheduler_amd.bench.decode --batch 1 --steps 20 ;;
   mall)
     step 300 mall python -u scripts/probe/mall_prefetch.py --out "$out/mall.json" ;;
   membw)
