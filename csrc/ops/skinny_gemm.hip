@@ -466,18 +466,22 @@ __device__ __forceinline__ void wide_step(const WFrag<NT> (&cur)[U], WFrag<NT> (
 // 32x32x16 accumulator element e of lane (r, h): row (e&3) + 8*(e>>2) + 4h, column r.
 __device__ __forceinline__ int acc_row(int e, int h) { return (e & 3) + 8 * (e >> 2) + 4 * h; }
 
+// Per-wave LDS tile of the residual epilogue's squares: [MT*32 rows][SQ_PITCH].
+constexpr int SQ_PITCH = 36;   // 16-byte aligned rows, writes of the two halves on different banks
+
 template <int MT, int NT, int EPI, class Get>
 __device__ __forceinline__ void wide_epilogue(Get get, bf16_t* __restrict__ y, int M, int ldy, int tile0,
                                               int vgroup, int r, int h, const float* rs, float* __restrict__ ss_out,
-                                              const bf16_t* res_lds) {
+                                              const bf16_t* res_lds, float* sq_lds = nullptr) {
+  if constexpr (EPI == EPI_RESID) {
+    // update; each lane's squares (one column r of 16 rows) go to the wave's
+    // LDS tile, then lane l sums half of row l/2 with four 16-byte reads
+    // (was 5 dependent cross-lane shuffles per row: 80 per lane, ~3 us)
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+    for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int row = m * 32 + acc_row(e, h);
-      if constexpr (EPI == EPI_RESID) {
-        // per row: update, then sum the squares over the 32 columns (lanes r)
-        // of this half right away (one live value, not 16 per lane)
+      for (int e = 0; e < 16; ++e) {
+        const int row = m * 32 + acc_row(e, h);
         float sq = 0.f;
         if (row < M) {
           const float sc = rs ? rs[row] : 1.f;
@@ -490,11 +494,29 @@ __device__ __forceinline__ void wide_epilogue(Get get, bf16_t* __restrict__ y, i
             sq += v * v;
           }
         }
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) sq += __shfl_xor(sq, o, 64);
-        if (r == 0) ss_out[(size_t)vgroup * SS_ROWS + row] = sq;
-        continue;
+        sq_lds[row * SQ_PITCH + r] = sq;
       }
+    const int lane = r + 32 * h, half = lane & 1;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int row = m * 32 + (lane >> 1);
+      const float4* p = reinterpret_cast<const float4*>(sq_lds + row * SQ_PITCH + 16 * half);
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 q = p[j];
+        sum += (q.x + q.y) + (q.z + q.w);
+      }
+      sum += __shfl_xor(sum, 1, 64);
+      if (half == 0) ss_out[(size_t)vgroup * SS_ROWS + row] = sum;
+    }
+    return;
+  }
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = m * 32 + acc_row(e, h);
       if (row >= M) continue;
       const float sc = rs ? rs[row] : 1.f;
       if constexpr (EPI == EPI_STORE) {
@@ -584,6 +606,8 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
   __shared__ float s_rtmp[RS ? WV * MT * 32 : 1];
   // EPI_RESID: each wave's residual tile [m][t][32 rows][32 cols], prefetched by LDS-DMA
   __shared__ __attribute__((aligned(16))) bf16_t s_res[EPI == EPI_RESID ? WV * MT * NT * 32 * 32 : 2];
+  // EPI_RESID: each wave's squares tile for the row sums (wide_epilogue)
+  __shared__ __attribute__((aligned(16))) float s_sq[EPI == EPI_RESID ? WV * MT * 32 * SQ_PITCH : 4];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
@@ -660,7 +684,7 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
   if constexpr (EPI == EPI_RESID) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // residual tile landed
   if (S == 1) {
     wide_epilogue<MT, NT, EPI>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, vgroup, r, h,
-                               rs, ss_out, res_lds);
+                               rs, ss_out, res_lds, s_sq + wave * (EPI == EPI_RESID ? MT * 32 * SQ_PITCH : 0));
     return;
   }
   // Inter-workgroup split, per wave: add the tile into this wave-group's fp32
@@ -684,7 +708,7 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
         return __hip_atomic_load(sc + ((m * NT + t) * 16 + e) * 64 + lane, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
       },
-      y, M, ldy, tile0, vgroup, r, h, rs, ss_out, res_lds);
+      y, M, ldy, tile0, vgroup, r, h, rs, ss_out, res_lds, s_sq + wave * (EPI == EPI_RESID ? MT * 32 * SQ_PITCH : 0));
 #pragma unroll
   for (int i = 0; i < SLAB / 64; ++i) sc[i * 64 + lane] = 0.f;
   if (lane == 0) tickets[vgroup] = 0;
@@ -724,6 +748,8 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
   constexpr int XC = MT * GK * 256 / NTHREADS;       // X chunks per thread per group
   static_assert(XC * NTHREADS == MT * GK * 256, "X tile must split evenly over the workgroup");
   static_assert(KW * MT * NT * 16 * 64 * 4 <= 2 * XBUF * 2, "the k-wave reduction reuses the X buffers");
+  static_assert((KW * MT * NT * 16 * 64 + MT * 32 * SQ_PITCH) * 4 <= 2 * XBUF * 2,
+                "the residual epilogue's squares tile follows the reduction in the X buffers");
   __shared__ __attribute__((aligned(16))) bf16_t xs[2 * XBUF];
   constexpr bool RS = EPI != EPI_RESID;
   __shared__ float s_rs[MT * 32];
@@ -832,7 +858,7 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
   if constexpr (EPI == EPI_RESID) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // residual tile landed
   if (S == 1) {
     wide_epilogue<MT, NT, EPI>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, vgroup, r, h,
-                               rs, ss_out, s_res);
+                               rs, ss_out, s_res, red + KW * MT * NT * 16 * 64);
     return;
   }
   constexpr int SLAB = MT * NT * 16 * 64;
@@ -852,7 +878,7 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
       [&](int m, int t, int e) {
         return __hip_atomic_load(sc + ((m * NT + t) * 16 + e) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       },
-      y, M, ldy, tile0, vgroup, r, h, rs, ss_out, s_res);
+      y, M, ldy, tile0, vgroup, r, h, rs, ss_out, s_res, red + KW * MT * NT * 16 * 64);
 #pragma unroll
   for (int i = 0; i < SLAB / 64; ++i) sc[i * 64 + lane] = 0.f;
   if (lane == 0) tickets[vgroup] = 0;

@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--sweep", action="store_true", help="also sweep nt/ks for M=32")
+    ap.add_argument("--norm", action="store_true",
+                    help="also time the row-norm fusion epilogues (residual update, row scales) per kernel")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     ops.require_native()
@@ -99,6 +101,30 @@ def main():
                    "hipblaslt_us": round(t_lib, 2), "skinny_us": round(t_sk, 2),
                    "hipblaslt_TBps": round(wbytes / t_lib / 1e6, 3), "skinny_TBps": round(wbytes / t_sk / 1e6, 3),
                    "speedup": round(t_lib / t_sk, 3), "weight_copies": ncopy, "widek_us": widek}
+            if a.norm and M <= 64:
+                # row-norm fusion: the residual update (+ sum-of-squares slots)
+                # and a store with row scales from 128 slots, on the wide and the
+                # K-split kernel, vs the plain store of the same kernel
+                ss = torch.rand(128 * ops.SS_ROWS, device="cuda") + 1.0
+                res_buf = torch.randn(M, N, device="cuda").bfloat16()
+                nrm = {}
+                for tag, v in (("wide", ops.VARIANT_WIDE), ("widek", ops.VARIANT_WIDEK)):
+                    if ops.skinny_plan(M, K, N, lin.epi, variant=v)["variant"] != v:
+                        continue
+                    for L in lins:
+                        L.variant = v
+                    cases = {"store": lambda i: lins[i % ncopy](x, out=out),
+                             "rowscale": lambda i: lins[i % ncopy].norm_call(x, out=out, row_scale=(ss, 128, K, 1e-6))}
+                    if not silu:
+                        cases["resid"] = lambda i: lins[i % ncopy].norm_call(x, out=res_buf, residual=True, ss_out=ss)
+                    for cname, fn in cases.items():
+                        try:
+                            nrm[f"{tag}_{cname}"] = round(_time(fn, a.reps), 2)
+                        except (RuntimeError, ValueError) as e:
+                            nrm[f"{tag}_{cname}"] = str(e)[:60]
+                    for L in lins:
+                        L.variant = ops.VARIANT_AUTO
+                row["norm_us"] = nrm
             if a.sweep and M == 32:
                 sw = {}
                 for variant, tag, kss in ((ops.VARIANT_CLASSIC, "", (1, 2, 4, 8)), (ops.VARIANT_WIDE, "wide_", (1, 2, 4))):

@@ -136,13 +136,11 @@ class Qwen3Decoder:
         # epilogue -- no add+RMSNorm launches (csrc/ops/skinny_gemm.hip).
         # Round 2, with qkv / o_proj on the wide kernel: 64-CU slice 8.85 vs
         # 8.87 ms/step, whole GPU 4.97 vs 4.92 (profiles/README.md section 14).
-        # Default on the whole chip, where qkv / o_proj run on the K-split
-        # kernel with the row-scale / residual epilogues: decode 4.84 vs 4.89
-        # ms at batch 32, 3.57 vs 3.62 at batch 1; inside a CU partition the
-        # two norm launches are cheaper than the epilogues (64 CUs: 8.98 vs
-        # 8.92 ms), profiles/README.md section 35.
-        nf_default = "1" if (skinny and ops.visible_cus() > 160) else "0"
-        self.norm_fused = skinny and os.environ.get("MIVGPU_NORM_FUSED", nf_default) == "1"
+        # Default on since the residual epilogue sums its squares through LDS
+        # (was 80 cross-lane shuffles per lane: +3 us per call): whole GPU
+        # 4.62 vs 4.80 ms at batch 32, 3.36 vs 3.52 at batch 1, 64 CUs 8.63 vs
+        # 8.75, 32 CUs 14.45 vs 14.59 (profiles/README.md section 36).
+        self.norm_fused = skinny and os.environ.get("MIVGPU_NORM_FUSED", "1") == "1"
         if self.norm_fused:
             self.skinny_o = True
         # K-split wide kernel (csrc/ops/skinny_gemm.hip skinny_widek_kernel) for
