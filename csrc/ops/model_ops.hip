@@ -1348,7 +1348,7 @@ int mivgpu_decode_attention_fused(const void* qkv, const void* q_norm_w, const v
                                   const int* pos, const int* seqlens, void* k_cache, void* v_cache,
                                   void* out, void* o_part, void* ml_part, int* counters, int B, int Hq,
                                   int Hkv, int head_dim, int max_ctx, int nsplit, float scale, float eps,
-                                  float theta, hipStream_t s) {
+                                  float theta, int defer_combine, hipStream_t s) {
   if (!attn_impl() || head_dim != ATT_D || Hq % Hkv || nsplit <= 0 || B <= 0) return -1;
   const int G = Hq / Hkv;
   const int waves = attn_impl();
@@ -1362,7 +1362,9 @@ int mivgpu_decode_attention_fused(const void* qkv, const void* q_norm_w, const v
   const float scale_log2 = scale * 1.44269504f;
   const float log2_theta = log2f(theta);
   dim3 grid(nsplit, Hkv, B);
-  const bool comb = attn_fused_mode() >= 2 && nsplit > 1;
+  // defer_combine: leave the partials for a consumer that combines them
+  // itself (the o_proj GEMM's X staging, mivgpu_skinny_gemm_norm_xcomb)
+  const bool comb = attn_fused_mode() >= 2 && nsplit > 1 && !defer_combine;
 #define MIVGPU_ATTN_FUSED3(GG, WW, NN, CC, MM)                                                                 \
   hipLaunchKernelGGL((decode_attn_fused_kernel<GG, WW, NN, CC, MM>), grid, dim3(WW * 64), 0, s,              \
                      (const bf16_t*)qkv, (const bf16_t*)q_norm_w, (const bf16_t*)k_norm_w, pos, seqlens,     \
@@ -1404,7 +1406,7 @@ int mivgpu_decode_attention_fused(const void* qkv, const void* q_norm_w, const v
 #undef MIVGPU_ATTN_FUSED
 #undef MIVGPU_ATTN_FUSED2
 #undef MIVGPU_ATTN_FUSED3
-  if (!comb && nsplit > 1)
+  if (!comb && nsplit > 1 && !defer_combine)
     hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(Hq, B), dim3(ATT_D), 0, s, (const float*)o_part,
                        (const float*)ml_part, (bf16_t*)out, Hq, nsplit, nsplit, seqlens, iters * per, max_ctx);
   return (int)hipGetLastError();

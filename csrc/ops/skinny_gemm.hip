@@ -422,6 +422,64 @@ __device__ __forceinline__ void wide_store_x(bf16_t* xs, const u32x4_t (&xr)[XC]
   }
 }
 
+// X staged from decode-attention split partials instead of a bf16 matrix
+// (small batches): chunk values are the split combine of
+// decode_attn_combine_kernel (csrc/ops/model_ops.hip), computed the same way
+// (online merge in split order, fp32, one bf16 rounding), so the GEMM sees
+// bit-identical X and the combine launch goes.  Only rows < XC_MAXM: they
+// are the first chunk of every thread (GK * 8 chunks per row <= NTHREADS);
+// every other chunk is zero (rows >= M are never stored).
+struct XComb {
+  const float* o;        // [B][Hq][nsplit][128]
+  const float* ml;       // [B][Hq][nsplit][2]: max (natural-log units) and sum
+  const int* seqlens;    // [B]
+  int nsplit, split_keys, max_ctx, hq;
+};
+constexpr int XC_MAXM = 4;
+constexpr int XC_MAXS = 16;
+
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+
+template <int MT, int U, int XC>
+__device__ __forceinline__ void wide_load_x_comb(u32x4_t (&xr)[XC], const XComb& xc, int M, int kb, int tid) {
+#pragma unroll
+  for (int i = 0; i < XC; ++i) xr[i] = u32x4_t{0u, 0u, 0u, 0u};
+  const int row = tid / (U * 8), c8 = tid % (U * 8);
+  if (row >= M) return;
+  const int col = kb * 64 + c8 * 8, h = col >> 7, d = col & 127;
+  const int L = min(xc.seqlens[row], xc.max_ctx);
+  const int active = min(xc.nsplit, L > 0 ? (L + xc.split_keys - 1) / xc.split_keys : 0);
+  const size_t base = ((size_t)row * xc.hq + h) * xc.nsplit;
+  float mv[XC_MAXS], lv[XC_MAXS];
+  float4 oa[XC_MAXS], ob[XC_MAXS];
+#pragma unroll
+  for (int sp = 0; sp < XC_MAXS; ++sp) {
+    const int q = sp < active ? sp : 0;
+    mv[sp] = xc.ml[(base + q) * 2];
+    lv[sp] = xc.ml[(base + q) * 2 + 1];
+    oa[sp] = *reinterpret_cast<const float4*>(xc.o + (base + q) * 128 + d);
+    ob[sp] = *reinterpret_cast<const float4*>(xc.o + (base + q) * 128 + d + 4);
+  }
+  float Mx = -INFINITY, den = 0.f, num[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) num[e] = 0.f;
+#pragma unroll
+  for (int sp = 0; sp < XC_MAXS; ++sp) {
+    if (sp >= active || mv[sp] == -INFINITY) continue;
+    const float nm = fmaxf(Mx, mv[sp]);
+    const float a = Mx == -INFINITY ? 0.f : __expf(Mx - nm), w = __expf(mv[sp] - nm);
+    const float ov[8] = {oa[sp].x, oa[sp].y, oa[sp].z, oa[sp].w, ob[sp].x, ob[sp].y, ob[sp].z, ob[sp].w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) num[e] = num[e] * a + w * ov[e];
+    den = den * a + w * lv[sp];
+    Mx = nm;
+  }
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = den > 0.f ? num[e] / den : 0.f;
+  xr[0] = u32x4_t{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
+}
+
 template <int MT, int NT, int U, int PITCH>
 __device__ __forceinline__ void wide_mma(const WFrag<NT> (&f)[U], const bf16_t* xs, f32x16_t (&acc)[MT][NT], int r,
                                          int h) {
@@ -733,12 +791,12 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
 // scales the rows of a store by the producer's slots (rs_issue / rs_finish).
 // NT = 2 with EPI_SILU_MUL: a gate tile and its up tile (gate_up), both
 // carried by every k-wave, SiLU(gate)*up by the reducing wave.
-template <int MT, int NT, int KW, int EPI>
+template <int MT, int NT, int KW, int EPI, bool COMB = false>
 __global__ void __launch_bounds__(64 * KW)
 skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int M,
                     int K, int N, int ldx, int ldy, int S, float* __restrict__ scratch, int* __restrict__ tickets,
                     int kmajor, const float* __restrict__ rs_part, int rs_nparts, float rs_inv_dim, float rs_eps,
-                    float* __restrict__ ss_out) {
+                    float* __restrict__ ss_out, XComb xcomb) {
   static_assert((EPI == EPI_SILU_MUL) == (NT == 2) && NT <= 2, "widek: one tile, or a gate/up pair for SiLU*up");
   constexpr int U = 2;                               // k-blocks per wave per group
   constexpr int GK = KW * U;                         // k-blocks per group (the X tile)
@@ -797,7 +855,8 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
       }
     }
     u32x4_t xr[XC];
-    wide_load_x<MT, GK, XC>(xr, x, M, ldx, kb0, tid, NTHREADS);
+    if constexpr (COMB) wide_load_x_comb<MT, GK, XC>(xr, xcomb, M, kb0, tid);
+    else wide_load_x<MT, GK, XC>(xr, x, M, ldx, kb0, tid, NTHREADS);
     wide_load_w<NT, U>(fa, wbase, ws, kb0 + kw * U, lane);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (RS) {
@@ -812,7 +871,8 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
                   bool prefetch) {
     u32x4_t xr[XC];
     if (prefetch) {
-      wide_load_x<MT, GK, XC>(xr, x, M, ldx, kb + GK, tid, NTHREADS);
+      if constexpr (COMB) wide_load_x_comb<MT, GK, XC>(xr, xcomb, M, kb + GK, tid);
+      else wide_load_x<MT, GK, XC>(xr, x, M, ldx, kb + GK, tid, NTHREADS);
       wide_load_w<NT, U>(nxt, wbase, ws, kb + GK + kw * U, lane);
     }
     DB_FENCE();
@@ -914,6 +974,7 @@ struct Args {
   float rs_inv_dim = 0.f;
   float rs_eps = 0.f;
   float* ss_out = nullptr;
+  XComb xcomb{};                    // K-split kernel: X from attention split partials (xcomb.o != null)
 };
 
 template <int MT, int NT, int KS, int EPI>
@@ -1001,13 +1062,26 @@ hipError_t launch_wide_resid(int mt, int wv, const Args& a, hipStream_t s) {
 template <int MT, int NT, int EPI>
 hipError_t launch_widek(int kw, const Args& a, hipStream_t s) {
   const int blocks = (a.N / 32) / NT * a.S;
-#define MIVGPU_LAUNCH_WIDEK(KW)                                                                                   \
-  hipLaunchKernelGGL((skinny_widek_kernel<MT, NT, KW, EPI>), dim3(blocks), dim3(64 * KW), 0, s, (const u32x4_t*)a.wp, \
-                     (const bf16_t*)a.x, (bf16_t*)a.y, a.M, a.K, a.N, a.ldx, a.ldy, a.S, a.scratch, a.tickets,      \
-                     a.kmajor, a.rs_part, a.rs_nparts, a.rs_inv_dim, a.rs_eps, a.ss_out)
+#define MIVGPU_LAUNCH_WIDEK(KW, CC)                                                                                \
+  hipLaunchKernelGGL((skinny_widek_kernel<MT, NT, KW, EPI, CC>), dim3(blocks), dim3(64 * KW), 0, s,               \
+                     (const u32x4_t*)a.wp, (const bf16_t*)a.x, (bf16_t*)a.y, a.M, a.K, a.N, a.ldx, a.ldy, a.S,      \
+                     a.scratch, a.tickets, a.kmajor, a.rs_part, a.rs_nparts, a.rs_inv_dim, a.rs_eps, a.ss_out, a.xcomb)
+  const bool comb = a.xcomb.o != nullptr;
+  if constexpr (MT == 1 && NT == 1) {
+    if (comb) {
+      switch (kw) {
+        case 2: MIVGPU_LAUNCH_WIDEK(2, true); break;
+        case 4: MIVGPU_LAUNCH_WIDEK(4, true); break;
+        default: return hipErrorInvalidValue;
+      }
+      return hipGetLastError();
+    }
+  } else if (comb) {
+    return hipErrorInvalidValue;
+  }
   switch (kw) {
-    case 2: MIVGPU_LAUNCH_WIDEK(2); break;
-    case 4: MIVGPU_LAUNCH_WIDEK(4); break;
+    case 2: MIVGPU_LAUNCH_WIDEK(2, false); break;
+    case 4: MIVGPU_LAUNCH_WIDEK(4, false); break;
     default: return hipErrorInvalidValue;
   }
 #undef MIVGPU_LAUNCH_WIDEK
@@ -1265,9 +1339,44 @@ int mivgpu_skinny_gemm(const void* wp, const void* x, void* y, int M, int K, int
 // slots ss_out[(N/32/nt) * 128]; rs_part != nullptr = row scales from rs_nparts
 // such slots (rs_inv_dim = 1/normalised dim).  Either requires the wide kernel
 // (hipErrorInvalidValue when the plan resolves to the classic one).
+static int skinny_gemm_norm_impl(const void* wp, const void* x, void* y, int M, int K, int N, int ldx, int ldy,
+                                 int epi, int nt, int ks, int S, int variant, float* scratch, int* tickets,
+                                 const float* rs_part, int rs_nparts, float rs_inv_dim, float rs_eps, float* ss_out,
+                                 const XComb& xcomb, hipStream_t s);
+
 int mivgpu_skinny_gemm_norm(const void* wp, const void* x, void* y, int M, int K, int N, int ldx, int ldy, int epi,
                             int nt, int ks, int S, int variant, float* scratch, int* tickets, const float* rs_part,
                             int rs_nparts, float rs_inv_dim, float rs_eps, float* ss_out, hipStream_t s) {
+  return skinny_gemm_norm_impl(wp, x, y, M, K, N, ldx, ldy, epi, nt, ks, S, variant, scratch, tickets, rs_part,
+                               rs_nparts, rs_inv_dim, rs_eps, ss_out, XComb{}, s);
+}
+
+// mivgpu_skinny_gemm_norm on the K-split kernel with X taken from decode
+// attention split partials (o_part [B][Hq][nsplit][128], ml_part
+// [B][Hq][nsplit][2], as mivgpu_decode_attention_fused leaves them with
+// defer_combine): X[b][h*128 + d] is the split combine.  K = Hq * 128,
+// M <= 4, nsplit <= 16; hipErrorInvalidValue when the plan is not the K-split
+// kernel with one M-tile.
+int mivgpu_skinny_gemm_norm_xcomb(const void* wp, const float* o_part, const float* ml_part, const int* seqlens,
+                                  int nsplit, int split_keys, int max_ctx, int hq, void* y, int M, int K, int N,
+                                  int ldy, int epi, int ks, int S, float* scratch, int* tickets,
+                                  const float* rs_part, int rs_nparts, float rs_inv_dim, float rs_eps, float* ss_out,
+                                  hipStream_t s) {
+  if (!o_part || !ml_part || !seqlens || nsplit < 1 || nsplit > XC_MAXS || split_keys <= 0 || max_ctx <= 0 ||
+      hq <= 0 || K != hq * 128 || M < 1 || M > XC_MAXM)
+    return (int)hipErrorInvalidValue;
+  int a = 0, b = ks, c = S;
+  if (!plan_widek(M, K, N, epi == EPI_RESID ? EPI_STORE : epi, &a, &b, &c) || a != 1) return (int)hipErrorInvalidValue;
+  // rows < M <= 4 are the first chunk of every thread: 4 rows x GK * 8 chunks = 64 * KW threads
+  const XComb xc{o_part, ml_part, seqlens, nsplit, split_keys, max_ctx, hq};
+  return skinny_gemm_norm_impl(wp, o_part, y, M, K, N, K, ldy, epi, 1, b, c, 3, scratch, tickets, rs_part, rs_nparts,
+                               rs_inv_dim, rs_eps, ss_out, xc, s);
+}
+
+static int skinny_gemm_norm_impl(const void* wp, const void* x, void* y, int M, int K, int N, int ldx, int ldy,
+                                 int epi, int nt, int ks, int S, int variant, float* scratch, int* tickets,
+                                 const float* rs_part, int rs_nparts, float rs_inv_dim, float rs_eps, float* ss_out,
+                                 const XComb& xcomb, hipStream_t s) {
   if (M <= 0 || M > 128 || K <= 0 || (K & 63) || N <= 0 || (N & 31) || ldx < K || (ldx & 7) || (ldy & 7))
     return (int)hipErrorInvalidValue;
   if (epi != EPI_STORE && epi != EPI_SILU_MUL && epi != EPI_RESID) return (int)hipErrorInvalidValue;
@@ -1286,15 +1395,18 @@ int mivgpu_skinny_gemm_norm(const void* wp, const void* x, void* y, int M, int K
     a.rs_inv_dim = rs_inv_dim;
     a.rs_eps = rs_eps;
     a.ss_out = ss_out;
+    a.xcomb = xcomb;
     const int mt = mt_of(M);
     if (rs_part != nullptr && (epi == EPI_RESID || rs_nparts > 64 * ks * RS_LMAX / (mt * 8)))
       return (int)hipErrorInvalidValue;
+    if (xcomb.o != nullptr && (mt != 1 || nt != 1)) return (int)hipErrorInvalidValue;
     if (epi == EPI_RESID)
       return (int)(mt == 1 ? launch_widek<1, 1, EPI_RESID>(ks, a, s) : launch_widek<2, 1, EPI_RESID>(ks, a, s));
     if (epi == EPI_SILU_MUL)
       return (int)(mt == 1 ? launch_widek<1, 2, EPI_SILU_MUL>(ks, a, s) : launch_widek<2, 2, EPI_SILU_MUL>(ks, a, s));
     return (int)(mt == 1 ? launch_widek<1, 1, EPI_STORE>(ks, a, s) : launch_widek<2, 1, EPI_STORE>(ks, a, s));
   }
+  if (xcomb.o != nullptr) return (int)hipErrorInvalidValue;   // X from partials: the K-split kernel only
   if (v == 2) {
     if (epi == EPI_SILU_MUL && ldy < N / 2) return (int)hipErrorInvalidValue;
     if (epi != EPI_SILU_MUL && ldy < N) return (int)hipErrorInvalidValue;
@@ -1306,8 +1418,13 @@ int mivgpu_skinny_gemm_norm(const void* wp, const void* x, void* y, int M, int K
     a.rs_eps = rs_eps;
     a.ss_out = ss_out;
     const int mt = mt_of(M);
-    // rs_issue reads RS_LMAX slots per thread in one batch
-    // rs_issue reads RS_LMAX slots per thread in one batch; the residual epilogue takes no row scale
+    // rs_issue reads RS_LMAX slots per thread in one batch: a plan with too few
+    // waves for the producer's slot count (the 97-160-CU gate_up plan has one
+    // wave, 64 slots, after a 128-slot down projection) gets more waves
+    while (rs_part != nullptr && rs_nparts > 64 * ks * RS_LMAX / (mt * 8) && ks < 4 &&
+           (N / 32) % (nt * ks * 2) == 0)
+      ks *= 2;
+    // the residual epilogue takes no row scale
     if (rs_part != nullptr && (epi == EPI_RESID || rs_nparts > 64 * ks * RS_LMAX / (mt * 8)))
       return (int)hipErrorInvalidValue;
     if (epi == EPI_RESID && mt > 2) return (int)hipErrorInvalidValue;   // LDS: residual tiles of <= 64 rows

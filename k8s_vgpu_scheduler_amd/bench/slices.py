@@ -180,8 +180,17 @@ class SliceProc:
                 continue
             line = self.p.stdout.readline()
             if not line:
+                try:
+                    self.p.wait(timeout=10)
+                except subprocess.TimeoutExpired:
+                    pass
+                self.log.flush()
+                try:   # the slice's own error output, so a remote run shows it
+                    tail = Path(self.log.name).read_text(errors="replace")[-3000:]
+                except OSError:
+                    tail = ""
                 raise RuntimeError(f"slice {self.spec.index} exited (rc={self.p.poll()}) before {tag}; "
-                                   f"see {self.log.name}")
+                                   f"see {self.log.name}; its log ends:\n{tail}")
             if line.startswith(tag + " "):
                 return json.loads(line[len(tag) + 1:])
 

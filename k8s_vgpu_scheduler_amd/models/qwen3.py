@@ -241,6 +241,19 @@ class Qwen3Decoder:
                                    device=self.device)
         self.attn_counters = (torch.zeros(batch * cfg.kv_heads, dtype=torch.int32, device=self.device)
                               if self.attn_fused else None)
+        # Batch <= 4 under the norm fusion with o_proj on the K-split kernel:
+        # the attention can leave its split partials for o_proj's X staging to
+        # combine (csrc/ops/skinny_gemm.hip wide_load_x_comb), one launch fewer
+        # per layer.  Off by default (MIVGPU_ATTN_XCOMB=1 turns it on):
+        # measured at batch 1 o_proj 25.7 us vs 11.4 + 4.9 (combine launch),
+        # the per-group combine sits in front of every X hand-over
+        # (profiles/README.md section 36).
+        self.xcomb = None
+        if (self.norm_fused and self.attn_fused and 1 < self.nsplit <= 16
+                and self.nsplit == math.ceil(self.T / ops.attn_split())
+                and os.environ.get("MIVGPU_ATTN_XCOMB", "0") == "1"
+                and self.w.layers[0]["po"].xcomb_ok(batch)):
+            self.xcomb = (self.o_part, self.ml_part, self.seqlens, self.nsplit, ops.attn_split(), self.T, cfg.heads)
         self.graph = None
         self._tail_work = ops.decode_tail_workspace(batch, self.device) if self.native else None
         self._pf = {}          # prefill bucket length -> static buffers (+ captured graph)
@@ -270,13 +283,14 @@ class Qwen3Decoder:
         self.tokens.copy_(torch.randint(0, self.cfg.vocab, (self.B,), generator=g, device=self.device))
 
     # -------------------------------------------------------------- step --
-    def _attention(self, li, lw, qkv):
+    def _attention(self, li, lw, qkv, defer_combine: bool = False):
         cfg = self.cfg
         if self.attn_fused:
             ops.decode_attention_fused(qkv, lw["q_norm"], lw["k_norm"], self.pos, self.seqlens,
                                        self.k_cache[li], self.v_cache[li], self.attn, self.o_part,
                                        self.ml_part, self.attn_counters, cfg.heads, cfg.kv_heads,
-                                       cfg.head_dim, self.nsplit, self.scale, cfg.eps, cfg.rope_theta)
+                                       cfg.head_dim, self.nsplit, self.scale, cfg.eps, cfg.rope_theta,
+                                       defer_combine=defer_combine)
         else:
             ops.qk_norm_rope_kv(qkv, lw["q_norm"], lw["k_norm"], self.pos, self.q,
                                 self.k_cache[li], self.v_cache[li], cfg.heads, cfg.kv_heads,
@@ -296,8 +310,14 @@ class Qwen3Decoder:
         na = 1
         for li, lw in enumerate(w.layers):
             qkv = lw["pqkv"].norm_call(self.res, out=self.qkv_buf, row_scale=(self.ss_a, na, h, eps))
-            self._attention(li, lw, qkv)
-            lw["po"].norm_call(self.attn, out=self.res, residual=True, ss_out=self.ss_b)
+            if self.xcomb:
+                # small batch: o_proj combines the attention splits in its X
+                # staging (no combine launch)
+                self._attention(li, lw, qkv, defer_combine=True)
+                lw["po"].norm_call_xcomb(self.xcomb, self.B, out=self.res, residual=True, ss_out=self.ss_b)
+            else:
+                self._attention(li, lw, qkv)
+                lw["po"].norm_call(self.attn, out=self.res, residual=True, ss_out=self.ss_b)
             lw["pgu"].norm_call(self.res, out=self.act, row_scale=(self.ss_b, self.slots_o, h, eps))
             lw["pd"].norm_call(self.act, out=self.res, residual=True, ss_out=self.ss_a)
             na = self.slots_d

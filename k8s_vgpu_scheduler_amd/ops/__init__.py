@@ -45,7 +45,9 @@ def lib():
                                                      vp]
         L.mivgpu_decode_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, f, vp]
         L.mivgpu_decode_attention_fused.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i,
-                                                     i, f, f, f, vp]
+                                                     i, f, f, f, i, vp]
+        L.mivgpu_skinny_gemm_norm_xcomb.argtypes = [vp, vp, vp, vp, i, i, i, i, vp, i, i, i, i, i, i, i, vp, vp,
+                                                    vp, i, f, f, vp, vp]
         L.mivgpu_silu_mul.argtypes = [vp, vp, i, i, vp]
         L.mivgpu_hwid_probe.argtypes = [vp, i, vp]
         L.mivgpu_pack_weight.argtypes = [vp, vp, i, i, vp]
@@ -323,10 +325,13 @@ def attn_fused_splits(B: int, n_kv_heads: int, max_ctx: int) -> int:
 
 
 def decode_attention_fused(qkv, q_norm_w, k_norm_w, pos, seqlens, k_cache, v_cache, out, o_part, ml_part,
-                           counters, n_q_heads, n_kv_heads, head_dim, nsplit, scale, eps, theta):
+                           counters, n_q_heads, n_kv_heads, head_dim, nsplit, scale, eps, theta,
+                           defer_combine: bool = False):
     """One launch per layer: QK-norm + RoPE (q heads, new key), KV append at
     pos[b], attention over seqlens[b] keys, split combine -> out [B, Hq*D].
-    counters: B*Hkv int32, zero before the first call (left zero after)."""
+    counters: B*Hkv int32, zero before the first call (left zero after).
+    defer_combine: leave only the split partials (o_part / ml_part) for
+    PackedLinear.norm_call_xcomb; ``out`` is not written."""
     B = qkv.shape[0]
     max_ctx = _check_kv(k_cache, v_cache, B, n_kv_heads, head_dim)
     need = B * n_q_heads * nsplit
@@ -340,7 +345,8 @@ def decode_attention_fused(qkv, q_norm_w, k_norm_w, pos, seqlens, k_cache, v_cac
     _check(lib().mivgpu_decode_attention_fused(_p(qkv), _p(q_norm_w), _p(k_norm_w), _p(pos), _p(seqlens),
                                                _p(k_cache), _p(v_cache), _p(out), _p(o_part), _p(ml_part),
                                                _p(counters), B, n_q_heads, n_kv_heads, head_dim, max_ctx,
-                                               nsplit, scale, eps, theta, _stream()), "decode_attention_fused")
+                                               nsplit, scale, eps, theta, int(bool(defer_combine)), _stream()),
+           "decode_attention_fused")
     return out
 
 
@@ -514,6 +520,34 @@ class PackedLinear:
         # the row-norm fusion runs on the wide kernel, or the K-split one when
         # this projection is set to it
         return VARIANT_WIDEK if self.variant == VARIANT_WIDEK else VARIANT_WIDE
+
+    def xcomb_ok(self, M: int) -> bool:
+        """norm_call_xcomb can run: the K-split kernel with one M-tile, M <= 4."""
+        return (self.variant == VARIANT_WIDEK and 0 < M <= 4 and not self.silu_mul and self.K % 128 == 0
+                and skinny_plan(M, self.K, self.N, EPI_STORE, variant=VARIANT_WIDEK)["variant"] == VARIANT_WIDEK)
+
+    def norm_call_xcomb(self, parts: tuple, M: int, out: torch.Tensor, residual: bool = False,
+                        ss_out: torch.Tensor | None = None):
+        """norm_call with X = the split combine of decode-attention partials
+        (``decode_attention_fused(..., defer_combine=True)``), done in the
+        kernel's X staging: ``parts = (o_part, ml_part, seqlens, nsplit,
+        split_keys, max_ctx, n_q_heads)``; K must be n_q_heads * 128."""
+        o_part, ml_part, seqlens, nsplit, split_keys, max_ctx, hq = parts
+        if not self.xcomb_ok(M) or self.K != hq * 128 or o_part.dtype != torch.float32 or ml_part.dtype != torch.float32:
+            raise ValueError("norm_call_xcomb needs the K-split kernel, M <= 4, K = Hq * 128, fp32 partials")
+        epi = EPI_RESID if residual else self.epi
+        if residual and (ss_out is None or ss_out.numel() < self.slots(M) * SS_ROWS or tuple(out.shape) != (M, self.N)):
+            raise ValueError("residual call needs out [M, N], ss_out of slots(M) * SS_ROWS floats")
+        pl = skinny_plan(M, self.K, self.N, EPI_STORE, variant=VARIANT_WIDEK)
+        self._ensure_scratch(pl["scratch_floats"], pl["tickets"], out.device)
+        sp = _p(self.scratch) if self.scratch is not None else None
+        tp = _p(self.tickets) if self.tickets is not None else None
+        _check(lib().mivgpu_skinny_gemm_norm_xcomb(_p(self.wp), _p(o_part), _p(ml_part), _p(seqlens), nsplit,
+                                                   split_keys, max_ctx, hq, _p(out), M, self.K, self.N,
+                                                   out.stride(0), epi, 0, 0, sp, tp, None, 0, 0.0, 0.0,
+                                                   _p(ss_out) if residual else None, _stream()),
+               "skinny_gemm_norm_xcomb")
+        return out
 
     def norm_call(self, x: torch.Tensor, out: torch.Tensor, row_scale: tuple | None = None,
                   residual: bool = False, ss_out: torch.Tensor | None = None, ks: int = 0, S: int = 0):

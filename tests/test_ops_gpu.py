@@ -441,6 +441,35 @@ def test_embed_rmsnorm_matches_reference(ops, rows, dim):
     assert torch.equal(res, embed[tokens])
 
 
+@pytest.mark.parametrize("B,xcomb", [(1, "1"), (3, "1"), (3, "0"), (4, "1")])
+def test_decoder_attention_combine_in_o_proj(monkeypatch, B, xcomb):
+    """Small batches under the norm fusion: the attention leaves its split
+    partials and o_proj's X staging combines them (no combine launch); 3
+    steps vs the fp32 reference decoder and vs the combine-kernel path, with
+    a context long enough for several splits and rows of different lengths."""
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
+
+    monkeypatch.setenv("MIVGPU_NORM_FUSED", "1")
+    monkeypatch.setenv("MIVGPU_WIDEK", "qkv,o")
+    monkeypatch.setenv("MIVGPU_ATTN_XCOMB", xcomb)
+    a = Qwen3Decoder(QWEN3_TINY, batch=B, max_ctx=700, device="cuda", native=True, seed=12)
+    if xcomb == "1":
+        assert a.xcomb is not None and a.nsplit > 1, (a.nsplit, a.xcomb)
+    else:
+        assert a.xcomb is None
+    b = Qwen3Decoder(QWEN3_TINY, batch=B, max_ctx=700, device="cuda", native=False, seed=12)
+    a.fill_context(600)
+    b.fill_context(600)
+    lens = torch.tensor([600 - 170 * i for i in range(B)], dtype=torch.int32, device="cuda")
+    for d in (a, b):   # rows of different lengths: some splits of the short rows hold no keys
+        d.pos.copy_(lens)
+        d.seqlens.copy_(lens + 1)
+    for _ in range(3):
+        la, lb = a.step(), b.step()
+        _close(la, lb, 5e-2)
+        b.tokens.copy_(a.tokens)
+
+
 @pytest.mark.parametrize("graph,plen", [(False, 150), (True, 150), (False, 40), (True, 40)])
 def test_decoder_norm_fused_prefill_matches_reference(monkeypatch, graph, plen):
     """Prompt processing of the norm-fused decoder (RMSNorm folded into the

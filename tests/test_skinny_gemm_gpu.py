@@ -220,6 +220,18 @@ for name, N, K, silu in (("gate_up", 24576, 4096, True), ("down", 4096, 12288, F
         r = ref.silu_mul(r.bfloat16()).float()
     out[name] = {"plan": [pl["variant"], pl["nt"], pl["ks"], pl["S"]],
                  "err": ((y - r).abs().max() / r.abs().max()).item()}
+# row-norm fusion: the down projection's 128 sum-of-squares slots into gate_up,
+# whose one-wave plan here reads only 64 (the kernel takes more waves)
+wn = (1 + 0.1 * torch.randn(4096, device="cuda")).bfloat16()
+wg = (torch.randn(24576, 4096, device="cuda") * 0.02).bfloat16()
+pg = ops.PackedLinear(wg, silu_mul=True, col_scale=wn)
+ss = torch.zeros(128 * ops.SS_ROWS, device="cuda")
+ss.view(128, ops.SS_ROWS)[:, :32] = (x.float().pow(2).sum(-1) / 128)[None, :]
+y = torch.empty(32, 12288, device="cuda", dtype=torch.bfloat16)
+pg.norm_call(x, out=y, row_scale=(ss, 128, 4096, 1e-6))
+h = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-6) * wn.float()
+r = ref.silu_mul((h.bfloat16().float() @ wg.float().t()).bfloat16()).float()
+out["rowscale128_err"] = ((y.float() - r).abs().max() / r.abs().max()).item()
 print("RESULT " + json.dumps(out))
 """
 
@@ -243,6 +255,7 @@ def test_half_gpu_partition_plans(mid):
     for k, plan in want.items():
         assert out[k]["plan"] == plan, (k, out[k])
         assert out[k]["err"] < 2e-2, (k, out[k])
+    assert out["rowscale128_err"] < 3e-2, out
 
 
 _SLICE_PLANS_CHILD = r"""
