@@ -422,62 +422,84 @@ __device__ __forceinline__ void wide_store_x(bf16_t* xs, const u32x4_t (&xr)[XC]
   }
 }
 
-// X staged from decode-attention split partials instead of a bf16 matrix
-// (small batches): chunk values are the split combine of
-// decode_attn_combine_kernel (csrc/ops/model_ops.hip), computed the same way
-// (online merge in split order, fp32, one bf16 rounding), so the GEMM sees
-// bit-identical X and the combine launch goes.  Only rows < XC_MAXM: they
-// are the first chunk of every thread (GK * 8 chunks per row <= NTHREADS);
-// every other chunk is zero (rows >= M are never stored).
+// X from decode-attention split partials instead of a bf16 matrix (batch 1):
+// the K-split kernel builds the whole combined row in LDS once, before its W
+// loop, computed as decode_attn_combine_kernel does (csrc/ops/model_ops.hip:
+// online merge in split order, fp32, one bf16 rounding), so the GEMM sees
+// bit-identical X and the combine launch goes.
 struct XComb {
   const float* o;        // [B][Hq][nsplit][128]
   const float* ml;       // [B][Hq][nsplit][2]: max (natural-log units) and sum
   const int* seqlens;    // [B]
   int nsplit, split_keys, max_ctx, hq;
 };
-constexpr int XC_MAXM = 4;
-constexpr int XC_MAXS = 16;
+constexpr int XC_MAXS = 8;   // splits (<= 2048 keys of context)
+constexpr int XC_NCH = 2;    // 8-column chunks per thread: K <= 16 * threads
 
 __device__ __forceinline__ uint32_t pack_bf2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
 
-template <int MT, int U, int XC>
-__device__ __forceinline__ void wide_load_x_comb(u32x4_t (&xr)[XC], const XComb& xc, int M, int kb, int tid) {
-#pragma unroll
-  for (int i = 0; i < XC; ++i) xr[i] = u32x4_t{0u, 0u, 0u, 0u};
-  const int row = tid / (U * 8), c8 = tid % (U * 8);
-  if (row >= M) return;
-  const int col = kb * 64 + c8 * 8, h = col >> 7, d = col & 127;
-  const int L = min(xc.seqlens[row], xc.max_ctx);
+// Row 0's combined X into xrow[0..K) (every load of the thread's chunks issued
+// before the merge: one memory round trip).
+__device__ __forceinline__ void xcomb_row(bf16_t* xrow, const XComb& xc, int K, int tid, int nthreads) {
+  const int L = min(xc.seqlens[0], xc.max_ctx);
   const int active = min(xc.nsplit, L > 0 ? (L + xc.split_keys - 1) / xc.split_keys : 0);
-  const size_t base = ((size_t)row * xc.hq + h) * xc.nsplit;
-  float mv[XC_MAXS], lv[XC_MAXS];
-  float4 oa[XC_MAXS], ob[XC_MAXS];
+  float mv[XC_NCH][XC_MAXS], lv[XC_NCH][XC_MAXS];
+  float4 oa[XC_NCH][XC_MAXS], ob[XC_NCH][XC_MAXS];
 #pragma unroll
-  for (int sp = 0; sp < XC_MAXS; ++sp) {
-    const int q = sp < active ? sp : 0;
-    mv[sp] = xc.ml[(base + q) * 2];
-    lv[sp] = xc.ml[(base + q) * 2 + 1];
-    oa[sp] = *reinterpret_cast<const float4*>(xc.o + (base + q) * 128 + d);
-    ob[sp] = *reinterpret_cast<const float4*>(xc.o + (base + q) * 128 + d + 4);
+  for (int c = 0; c < XC_NCH; ++c) {
+    const int col = min((tid + c * nthreads) * 8, K - 8), h = col >> 7, d = col & 127;
+    const size_t base = (size_t)h * xc.nsplit;
+#pragma unroll
+    for (int sp = 0; sp < XC_MAXS; ++sp) {
+      const int q = sp < active ? sp : 0;
+      mv[c][sp] = xc.ml[(base + q) * 2];
+      lv[c][sp] = xc.ml[(base + q) * 2 + 1];
+      oa[c][sp] = *reinterpret_cast<const float4*>(xc.o + (base + q) * 128 + d);
+      ob[c][sp] = *reinterpret_cast<const float4*>(xc.o + (base + q) * 128 + d + 4);
+    }
   }
-  float Mx = -INFINITY, den = 0.f, num[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) num[e] = 0.f;
+  for (int c = 0; c < XC_NCH; ++c) {
+    const int col = (tid + c * nthreads) * 8;
+    float Mx = -INFINITY, den = 0.f, num[8];
 #pragma unroll
-  for (int sp = 0; sp < XC_MAXS; ++sp) {
-    if (sp >= active || mv[sp] == -INFINITY) continue;
-    const float nm = fmaxf(Mx, mv[sp]);
-    const float a = Mx == -INFINITY ? 0.f : __expf(Mx - nm), w = __expf(mv[sp] - nm);
-    const float ov[8] = {oa[sp].x, oa[sp].y, oa[sp].z, oa[sp].w, ob[sp].x, ob[sp].y, ob[sp].z, ob[sp].w};
+    for (int e = 0; e < 8; ++e) num[e] = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) num[e] = num[e] * a + w * ov[e];
-    den = den * a + w * lv[sp];
-    Mx = nm;
+    for (int sp = 0; sp < XC_MAXS; ++sp) {
+      if (sp >= active || mv[c][sp] == -INFINITY) continue;
+      const float nm = fmaxf(Mx, mv[c][sp]);
+      const float a = Mx == -INFINITY ? 0.f : __expf(Mx - nm), w = __expf(mv[c][sp] - nm);
+      const float ov[8] = {oa[c][sp].x, oa[c][sp].y, oa[c][sp].z, oa[c][sp].w,
+                           ob[c][sp].x, ob[c][sp].y, ob[c][sp].z, ob[c][sp].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) num[e] = num[e] * a + w * ov[e];
+      den = den * a + w * lv[c][sp];
+      Mx = nm;
+    }
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = den > 0.f ? num[e] / den : 0.f;
+    if (col < K)
+      *reinterpret_cast<u32x4_t*>(xrow + col) =
+          u32x4_t{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
   }
-  float v[8];
+}
+
+// MFMAs of one group with the A operand from ONE LDS row (batch 1: rows >= 1
+// of the 32x32 product are never stored, so every lane reads row 0 -- an LDS
+// broadcast).
+template <int NT, int U>
+__device__ __forceinline__ void wide_mma_row(const WFrag<NT> (&f)[U], const bf16_t* xr, f32x16_t (&acc)[1][NT], int h) {
 #pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = den > 0.f ? num[e] / den : 0.f;
-  xr[0] = u32x4_t{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u32x4_t a = *(const u32x4_t*)(xr + u * 64 + 32 * h + 8 * j);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                            __builtin_bit_cast(bf16x8_t, f[u].b[t][j]), acc[0][t], 0, 0, 0);
+    }
 }
 
 template <int MT, int NT, int U, int PITCH>
@@ -854,25 +876,54 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
           }
       }
     }
-    u32x4_t xr[XC];
-    if constexpr (COMB) wide_load_x_comb<MT, GK, XC>(xr, xcomb, M, kb0, tid);
-    else wide_load_x<MT, GK, XC>(xr, x, M, ldx, kb0, tid, NTHREADS);
-    wide_load_w<NT, U>(fa, wbase, ws, kb0 + kw * U, lane);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (RS) {
-      if (rs_part) rs_finish<MT, NTHREADS>(rsv, rs_inv_dim, rs_eps, s_rs, s_rtmp, tid);
+    if constexpr (COMB) {
+      // batch 1, X from attention partials: the whole combined row into LDS
+      // once (W loads of the first group already in flight), then a W loop
+      // with no X hand-overs
+      wide_load_w<NT, U>(fa, wbase, ws, kb0 + kw * U, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      xcomb_row(xs, xcomb, K, tid, NTHREADS);
+      if constexpr (RS) {
+        if (rs_part) rs_finish<MT, NTHREADS>(rsv, rs_inv_dim, rs_eps, s_rs, s_rtmp, tid);
+      }
+      __syncthreads();
+      auto stepc = [&](const WFrag<NT>(&cur)[U], WFrag<NT>(&nxt)[U], int kb, bool prefetch) {
+        if (prefetch) wide_load_w<NT, U>(nxt, wbase, ws, kb + GK + kw * U, lane);
+        DB_FENCE();
+        wide_mma_row<NT, U>(cur, xs + (kb + kw * U) * 64, acc, h);
+        DB_FENCE();
+      };
+      int g = 0, kb = kb0;
+      for (; g + 3 <= G; g += 2, kb += 2 * GK) {
+        stepc(fa, fb, kb, true);
+        stepc(fb, fa, kb + GK, true);
+      }
+      if (G - g == 2) {
+        stepc(fa, fb, kb, true);
+        stepc(fb, fa, kb + GK, false);
+      } else {
+        stepc(fa, fb, kb, false);
+      }
+    } else {
+      u32x4_t xr[XC];
+      wide_load_x<MT, GK, XC>(xr, x, M, ldx, kb0, tid, NTHREADS);
+      wide_load_w<NT, U>(fa, wbase, ws, kb0 + kw * U, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (RS) {
+        if (rs_part) rs_finish<MT, NTHREADS>(rsv, rs_inv_dim, rs_eps, s_rs, s_rtmp, tid);
+      }
+      wide_store_x<MT, GK, XC, PITCH>(xs, xr, tid, NTHREADS);
+      __syncthreads();
     }
-    wide_store_x<MT, GK, XC, PITCH>(xs, xr, tid, NTHREADS);
-    __syncthreads();
   }
+  if constexpr (!COMB) {
   // one group: prefetch the next group's X then this wave's W, MFMAs of this
   // group from registers + this wave's columns of the LDS tile, stage X
   auto step = [&](const WFrag<NT>(&cur)[U], WFrag<NT>(&nxt)[U], const bf16_t* xc, bf16_t* xn, int kb,
                   bool prefetch) {
     u32x4_t xr[XC];
     if (prefetch) {
-      if constexpr (COMB) wide_load_x_comb<MT, GK, XC>(xr, xcomb, M, kb + GK, tid);
-      else wide_load_x<MT, GK, XC>(xr, x, M, ldx, kb + GK, tid, NTHREADS);
+      wide_load_x<MT, GK, XC>(xr, x, M, ldx, kb + GK, tid, NTHREADS);
       wide_load_w<NT, U>(nxt, wbase, ws, kb + GK + kw * U, lane);
     }
     DB_FENCE();
@@ -894,6 +945,7 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
   } else {
     step(fa, fb, xs, xs + XBUF, kb, false);
   }
+  }   // !COMB
   // sum the KW waves' partial tiles through LDS (the X buffers are free now)
   __syncthreads();
   float* red = reinterpret_cast<float*>(xs);
@@ -1354,20 +1406,21 @@ int mivgpu_skinny_gemm_norm(const void* wp, const void* x, void* y, int M, int K
 // mivgpu_skinny_gemm_norm on the K-split kernel with X taken from decode
 // attention split partials (o_part [B][Hq][nsplit][128], ml_part
 // [B][Hq][nsplit][2], as mivgpu_decode_attention_fused leaves them with
-// defer_combine): X[b][h*128 + d] is the split combine.  K = Hq * 128,
-// M <= 4, nsplit <= 16; hipErrorInvalidValue when the plan is not the K-split
-// kernel with one M-tile.
+// defer_combine): X[0][h*128 + d] is the split combine.  K = Hq * 128, M = 1,
+// nsplit <= 8; hipErrorInvalidValue when the plan is not the K-split kernel.
 int mivgpu_skinny_gemm_norm_xcomb(const void* wp, const float* o_part, const float* ml_part, const int* seqlens,
                                   int nsplit, int split_keys, int max_ctx, int hq, void* y, int M, int K, int N,
                                   int ldy, int epi, int ks, int S, float* scratch, int* tickets,
                                   const float* rs_part, int rs_nparts, float rs_inv_dim, float rs_eps, float* ss_out,
                                   hipStream_t s) {
   if (!o_part || !ml_part || !seqlens || nsplit < 1 || nsplit > XC_MAXS || split_keys <= 0 || max_ctx <= 0 ||
-      hq <= 0 || K != hq * 128 || M < 1 || M > XC_MAXM)
+      hq <= 0 || K != hq * 128 || M != 1)
     return (int)hipErrorInvalidValue;
   int a = 0, b = ks, c = S;
   if (!plan_widek(M, K, N, epi == EPI_RESID ? EPI_STORE : epi, &a, &b, &c) || a != 1) return (int)hipErrorInvalidValue;
-  // rows < M <= 4 are the first chunk of every thread: 4 rows x GK * 8 chunks = 64 * KW threads
+  // the combined row: XC_NCH 8-column chunks per thread, in the X buffers
+  // (2 * 32 * (GK * 64 + 8) bf16 >= K + 8)
+  if (K > XC_NCH * 8 * 64 * b || K + 8 > 2 * 32 * (b * 2 * 64 + 8)) return (int)hipErrorInvalidValue;
   const XComb xc{o_part, ml_part, seqlens, nsplit, split_keys, max_ctx, hq};
   return skinny_gemm_norm_impl(wp, o_part, y, M, K, N, K, ldy, epi, 1, b, c, 3, scratch, tickets, rs_part, rs_nparts,
                                rs_inv_dim, rs_eps, ss_out, xc, s);

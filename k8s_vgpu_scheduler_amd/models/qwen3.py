@@ -241,17 +241,16 @@ class Qwen3Decoder:
                                    device=self.device)
         self.attn_counters = (torch.zeros(batch * cfg.kv_heads, dtype=torch.int32, device=self.device)
                               if self.attn_fused else None)
-        # Batch <= 4 under the norm fusion with o_proj on the K-split kernel:
-        # the attention can leave its split partials for o_proj's X staging to
-        # combine (csrc/ops/skinny_gemm.hip wide_load_x_comb), one launch fewer
-        # per layer.  Off by default (MIVGPU_ATTN_XCOMB=1 turns it on):
-        # measured at batch 1 o_proj 25.7 us vs 11.4 + 4.9 (combine launch),
-        # the per-group combine sits in front of every X hand-over
-        # (profiles/README.md section 36).
+        # Batch 1 under the norm fusion with o_proj on the K-split kernel: the
+        # attention leaves its split partials and o_proj builds the combined
+        # row in LDS before its W loop (csrc/ops/skinny_gemm.hip xcomb_row),
+        # one launch fewer per layer: o_proj 13.2 us vs 11.4 + 4.9 for the
+        # combine launch (profiles/README.md section 36).  MIVGPU_ATTN_XCOMB=0
+        # keeps the combine kernel.
         self.xcomb = None
-        if (self.norm_fused and self.attn_fused and 1 < self.nsplit <= 16
+        if (self.norm_fused and self.attn_fused and 1 < self.nsplit <= 8
                 and self.nsplit == math.ceil(self.T / ops.attn_split())
-                and os.environ.get("MIVGPU_ATTN_XCOMB", "0") == "1"
+                and os.environ.get("MIVGPU_ATTN_XCOMB", "1") != "0"
                 and self.w.layers[0]["po"].xcomb_ok(batch)):
             self.xcomb = (self.o_part, self.ml_part, self.seqlens, self.nsplit, ops.attn_split(), self.T, cfg.heads)
         self.graph = None

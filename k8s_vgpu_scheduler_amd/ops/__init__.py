@@ -522,8 +522,8 @@ class PackedLinear:
         return VARIANT_WIDEK if self.variant == VARIANT_WIDEK else VARIANT_WIDE
 
     def xcomb_ok(self, M: int) -> bool:
-        """norm_call_xcomb can run: the K-split kernel with one M-tile, M <= 4."""
-        return (self.variant == VARIANT_WIDEK and 0 < M <= 4 and not self.silu_mul and self.K % 128 == 0
+        """norm_call_xcomb can run: the K-split kernel, one row (batch 1)."""
+        return (self.variant == VARIANT_WIDEK and M == 1 and not self.silu_mul and self.K % 128 == 0
                 and skinny_plan(M, self.K, self.N, EPI_STORE, variant=VARIANT_WIDEK)["variant"] == VARIANT_WIDEK)
 
     def norm_call_xcomb(self, parts: tuple, M: int, out: torch.Tensor, residual: bool = False,

@@ -441,7 +441,7 @@ def test_embed_rmsnorm_matches_reference(ops, rows, dim):
     assert torch.equal(res, embed[tokens])
 
 
-@pytest.mark.parametrize("B,xcomb", [(1, "1"), (3, "1"), (3, "0"), (4, "1")])
+@pytest.mark.parametrize("B,xcomb", [(1, "1"), (1, "0"), (3, "1")])
 def test_decoder_attention_combine_in_o_proj(monkeypatch, B, xcomb):
     """Small batches under the norm fusion: the attention leaves its split
     partials and o_proj's X staging combines them (no combine launch); 3
@@ -453,10 +453,10 @@ def test_decoder_attention_combine_in_o_proj(monkeypatch, B, xcomb):
     monkeypatch.setenv("MIVGPU_WIDEK", "qkv,o")
     monkeypatch.setenv("MIVGPU_ATTN_XCOMB", xcomb)
     a = Qwen3Decoder(QWEN3_TINY, batch=B, max_ctx=700, device="cuda", native=True, seed=12)
-    if xcomb == "1":
+    if xcomb == "1" and B == 1:
         assert a.xcomb is not None and a.nsplit > 1, (a.nsplit, a.xcomb)
     else:
-        assert a.xcomb is None
+        assert a.xcomb is None      # batch 1 only
     b = Qwen3Decoder(QWEN3_TINY, batch=B, max_ctx=700, device="cuda", native=False, seed=12)
     a.fill_context(600)
     b.fill_context(600)
