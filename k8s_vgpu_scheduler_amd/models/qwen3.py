@@ -149,9 +149,13 @@ class Qwen3Decoder:
         # 13.3 at 32 rows; 11.6 vs 14.3 / 10.0 vs 10.6 at 1 row
         # (profiles/round3/widek_gemm.json).  Inside a CU partition the tuned
         # wide plans stay.  MIVGPU_WIDEK=qkv,o,down,gu picks the set, "off" none.
+        # A half-GPU partition (97-160 CUs) takes o_proj only: 128 CUs decode
+        # 5.80 ms vs 6.00 with the wide kernel, qkv there loses (6.09,
+        # profiles/README.md section 36).
         wk_env = os.environ.get("MIVGPU_WIDEK")
         if wk_env is None:
-            wk_env = "qkv,o" if (self.native and ops.visible_cus() > 160) else ""
+            cus = ops.visible_cus() if self.native else 0
+            wk_env = "qkv,o" if cus > 160 else ("o" if cus > 96 else "")
         widek = {p for p in wk_env.split(",") if p and p != "off"} if skinny else set()
         if "qkv" in widek:
             self.skinny_qkv = True
