@@ -53,7 +53,8 @@ def main():
     ap.add_argument("--batches", default="1,8,32,64,128")
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--reps", type=int, default=50)
-    ap.add_argument("--sweep", action="store_true", help="also sweep nt/ks for M=32")
+    ap.add_argument("--sweep", action="store_true", help="also sweep nt/ks/S (at --sweep-rows)")
+    ap.add_argument("--sweep-rows", default="32", help="row counts the sweep runs at (comma list)")
     ap.add_argument("--norm", action="store_true",
                     help="also time the row-norm fusion epilogues (residual update, row scales) per kernel")
     ap.add_argument("--out", default=None)
@@ -125,9 +126,10 @@ def main():
                     for L in lins:
                         L.variant = ops.VARIANT_AUTO
                 row["norm_us"] = nrm
-            if a.sweep and M == 32:
+            if a.sweep and M in {int(v) for v in a.sweep_rows.split(",")}:
                 sw = {}
-                for variant, tag, kss in ((ops.VARIANT_CLASSIC, "", (1, 2, 4, 8)), (ops.VARIANT_WIDE, "wide_", (1, 2, 4))):
+                for variant, tag, kss in ((ops.VARIANT_CLASSIC, "", (1, 2, 4, 8)), (ops.VARIANT_WIDE, "wide_", (1, 2, 4)),
+                                          (ops.VARIANT_WIDEK, "widek_", (2, 4))):
                     for nt in (1, 2):
                         for ks in kss:
                             for S in (1, 2, 4, 8, 16):
