@@ -547,7 +547,7 @@ __device__ __forceinline__ void wide_step(const WFrag<NT> (&cur)[U], WFrag<NT> (
 __device__ __forceinline__ int acc_row(int e, int h) { return (e & 3) + 8 * (e >> 2) + 4 * h; }
 
 // Per-wave LDS tile of the residual epilogue's squares: [MT*32 rows][SQ_PITCH].
-constexpr int SQ_PITCH = 36;   // 16-byte aligned rows, writes of the two halves on different banks
+constexpr int SQ_PITCH = 40;   // 16-byte aligned rows; rows r and r+4 (the two lane halves) 32 banks apart
 
 template <int MT, int NT, int EPI, class Get>
 __device__ __forceinline__ void wide_epilogue(Get get, bf16_t* __restrict__ y, int M, int ldy, int tile0,
