@@ -13,6 +13,7 @@
 //   kfdctx <MiB>     runtime VRAM outside the hooks in the mock's simulated
 //                    KFD per-process file (MOCKHIP_KFD_SYSFS), for context accounting
 //   device <i>       hipSetDevice
+//   cfginfo          mivgpu_config_info: charging modes, grant/control loaded
 //   hsainit          hsa_init (interposed by the shim) + the HSA_CU_MASK /
 //                    ROCR_VISIBLE_DEVICES ROCr would read
 //   dlsym_alloc <MiB>  hipMalloc looked up at run time: dlopen + dlsym
@@ -407,6 +408,11 @@ int main(int argc, char** argv) {
       const char* k = argv[++i];
       const char* v = getenv(k);
       printf("{\"op\":\"getenv\",\"key\":\"%s\",\"set\":%d,\"value\":\"%s\"}\n", k, v ? 1 : 0, v ? v : "");
+    } else if (!strcmp(c, "cfginfo")) {
+      auto f = (int (*)(unsigned long long*))dlsym(RTLD_DEFAULT, "mivgpu_config_info");
+      unsigned long long crn = 0;
+      const int flags = f ? f(&crn) : -1;
+      printf("{\"op\":\"cfginfo\",\"flags\":%d,\"ctx_refresh_ns\":%llu}\n", flags, crn);
     } else if (!strcmp(c, "device")) {
       int d = atoi(argv[++i]);
       printf("{\"op\":\"device\",\"rc\":%d}\n", (int)hipSetDevice(d));

@@ -27,7 +27,11 @@
 //    host blocking.
 //  * Priority blocking: recent_kernel == -1 in the shared region (set by the
 //    node monitor's feedback loop, cmd/vGPUmonitor/feedback.go:74-134 in the
-//    reference) parks launches of the low-priority task.
+//    reference) parks launches of the low-priority task.  Under a grant file
+//    the monitor's verdicts come from a host-owned control file mapped
+//    read-only (block, utilization switch, over-grant, KFD-measured excess
+//    VRAM), and the limits from the read-only grant: nothing the tenant can
+//    write into its shared region loosens either.
 //  * hipIpc* is deliberately NOT wrapped: RCCL and custom all-reduce keep
 //    working (the reference breaks CUDA IPC, examples/nvidia/vllm_cross_vgpu.yaml:99-102).
 #include <hip/hip_runtime_api.h>
@@ -61,6 +65,22 @@
 #include "mivgpu/shared_region.h"
 
 #define MIVGPU_EXPORT extern "C" __attribute__((visibility("default")))
+
+// libstdc++ (linked statically, see glibc_floor.h) reads glibc's
+// __libc_single_threaded (GLIBC_2.32) to skip atomics in single-threaded
+// processes.  Our own copy, always 0: "assume threads", which is always safe.
+extern "C" {
+__attribute__((visibility("hidden"))) char __libc_single_threaded = 0;
+}
+#if defined(__x86_64__) && defined(MIVGPU_GLIBC_FLOOR)
+// (glibc_floor.h) the gthr weak references of the static libstdc++ bind here
+extern "C" __attribute__((visibility("hidden"))) int pthread_once(pthread_once_t* o, void (*f)(void)) noexcept {
+  return mivgpu_glibc_pthread_once(o, f);
+}
+extern "C" __attribute__((visibility("hidden"))) int __pthread_key_create(pthread_key_t* k, void (*d)(void*)) noexcept {
+  return mivgpu_glibc_pthread_key_create(k, d);
+}
+#endif
 
 namespace {
 
@@ -203,18 +223,45 @@ MIVGPU_NO_SANITIZE void* elf_lookup_in(ElfW(Addr) base, const ElfW(Dyn)* dyn, co
   return nullptr;
 }
 
+MIVGPU_NO_SANITIZE bool soname_is(const char* path, const char* want) {
+  const char* base = path;
+  for (const char* c = path; *c; ++c)
+    if (*c == '/') base = c + 1;
+  while (*want && *base == *want) ++base, ++want;
+  return *want == 0 && base[0] == '.' && base[1] == 's' && base[2] == 'o';
+}
+
+// libc's definition of `name`; dlsym/dlvsym/dladdr live in libdl.so.2 before
+// glibc 2.34 (the shim names libdl.so.2 as NEEDED, so it is in the link map).
 MIVGPU_NO_SANITIZE void* libc_sym(const char* name) {
-  for (const struct link_map* m = _r_debug.r_map; m; m = m->l_next) {
-    const char* n = m->l_name ? m->l_name : "";
-    const char* base = n;
-    for (const char* c = n; *c; ++c)
-      if (*c == '/') base = c + 1;
-    if (base[0] == 'l' && base[1] == 'i' && base[2] == 'b' && base[3] == 'c' && base[4] == '.' && base[5] == 's' &&
-        base[6] == 'o') {
+  // (plain indexing: no std::initializer_list helpers, which a sanitizer
+  // build instruments, before its runtime is up)
+  static const char* const kLibs[2] = {"libc", "libdl"};
+  for (int li = 0; li < 2; ++li) {
+    const char* lib = kLibs[li];
+    for (const struct link_map* m = _r_debug.r_map; m; m = m->l_next) {
+      if (!soname_is(m->l_name ? m->l_name : "", lib)) continue;
       if (void* p = elf_lookup_in(m->l_addr, m->l_ld, name)) return p;
     }
   }
   return nullptr;
+}
+
+// Last resort when no libc/libdl dlsym is found (never on a glibc system):
+// look `name` up in the loaded objects ourselves -- every object for the
+// pseudo-handles, the handle's own map otherwise (a glibc handle IS its
+// link_map) -- so lookups keep working, unversioned, instead of aborting.
+MIVGPU_NO_SANITIZE void* fallback_dlsym(void* handle, const char* name) {
+  if (handle && handle != RTLD_DEFAULT && handle != RTLD_NEXT) {
+    const struct link_map* m = static_cast<const struct link_map*>(handle);
+    return elf_lookup_in(m->l_addr, m->l_ld, name);
+  }
+  for (const struct link_map* m = _r_debug.r_map; m; m = m->l_next)
+    if (void* p = elf_lookup_in(m->l_addr, m->l_ld, name)) return p;
+  return nullptr;
+}
+MIVGPU_NO_SANITIZE void* fallback_dlvsym(void* handle, const char* name, const char*) {
+  return fallback_dlsym(handle, name);
 }
 
 using dlsym_fn = void* (*)(void*, const char*);
@@ -224,21 +271,23 @@ using dlvsym_fn = void* (*)(void*, const char*, const char*);
 dlsym_fn g_real_dlsym = nullptr;
 dlvsym_fn g_real_dlvsym = nullptr;
 
-MIVGPU_NO_SANITIZE void die_no_libc(const char* what) {
-  static const char msg[] = "[mivgpu ERROR] libc symbol not found: ";
+MIVGPU_NO_SANITIZE void warn_no_libc(const char* what) {
+  static const char msg[] = "[mivgpu WARN] libc/libdl symbol not found, using the shim's own lookup: ";
   (void)!write(2, msg, sizeof(msg) - 1);
   size_t n = 0;
   while (what[n]) ++n;
   (void)!write(2, what, n);
   (void)!write(2, "\n", 1);
-  abort();
 }
 
 MIVGPU_NO_SANITIZE dlsym_fn libc_dlsym() {
   dlsym_fn f = *const_cast<volatile dlsym_fn*>(&g_real_dlsym);
   if (__builtin_expect(!f, 0)) {
     f = reinterpret_cast<dlsym_fn>(libc_sym("dlsym"));
-    if (!f) die_no_libc("dlsym");
+    if (!f) {
+      warn_no_libc("dlsym");
+      f = &fallback_dlsym;
+    }
     *const_cast<volatile dlsym_fn*>(&g_real_dlsym) = f;
   }
   return f;
@@ -248,7 +297,10 @@ MIVGPU_NO_SANITIZE dlvsym_fn libc_dlvsym() {
   dlvsym_fn f = *const_cast<volatile dlvsym_fn*>(&g_real_dlvsym);
   if (__builtin_expect(!f, 0)) {
     f = reinterpret_cast<dlvsym_fn>(libc_sym("dlvsym"));
-    if (!f) die_no_libc("dlvsym");
+    if (!f) {
+      warn_no_libc("dlvsym");
+      f = &fallback_dlvsym;
+    }
     *const_cast<volatile dlvsym_fn*>(&g_real_dlvsym) = f;
   }
   return f;
@@ -389,7 +441,8 @@ struct Config {
   uint64_t occ_period_ns = 2000000;        // sampling period while the governor runs (2 ms)
   uint64_t occ_idle_period_ns = 50000000;  // ... and for utilisation reporting only (50 ms)
   double share_tau_ns = 250e6;             // EWMA time constant of the occupancy averages (>> holds, batches)
-  // A/B switches (not grant keys): MIVGPU_GATE_MODE=device keeps the bucket
+  // A/B switches (not grant keys, ignored under a grant file, see
+  // unguarded_env): MIVGPU_GATE_MODE=device keeps the bucket
   // in the gate (busy wall time x share) instead of the sampler;
   // MIVGPU_SHARE_EST=instant averages the per-sample ratio own/(own+others)
   // (ratio: the ratio of the averaged wave counts) instead of counting the
@@ -479,9 +532,9 @@ std::once_flag g_limits_once;
 void read_limits_file() {
   const char* path = kLimitsPath;
   struct stat st;
-  if (stat(path, &st) != 0) {
+  if (mivgpu_stat(path, &st) != 0) {
     const char* alt = getenv("MIVGPU_LIMITS_FILE");
-    if (!alt || !*alt || stat(alt, &st) != 0) return;
+    if (!alt || !*alt || mivgpu_stat(alt, &st) != 0) return;
     path = alt;
   }
   FILE* f = fopen(path, "re");
@@ -513,7 +566,7 @@ bool is_grant_key(const char* key) {
                                       "MIVGPU_ACCOUNT_CONTEXT", "ROCR_VISIBLE_DEVICES", "MIVGPU_KFD_SYSFS",
                                       "MIVGPU_OCCUPANCY", "MIVGPU_OCC_PERIOD_US", "MIVGPU_GATE_INTERVAL_US",
                                       "MIVGPU_GATE_BURST_US", "MIVGPU_SHARE_TAU_MS", "GPU_MAX_HW_QUEUES",
-                                      "MIVGPU_GATE_MAX_HOLD_US"};
+                                      "MIVGPU_GATE_MAX_HOLD_US", "MIVGPU_CONTROL_FILE"};
   for (const char* k : kKeys)
     if (!strcmp(key, k)) return true;
   return !strncmp(key, "HIP_DEVICE_MEMORY_LIMIT_", 24) || !strncmp(key, "HIP_DEVICE_CORE_LIMIT_", 22);
@@ -525,6 +578,15 @@ const char* grant_env(const char* key) {
   for (int i = 0; i < g_limits.n; ++i)
     if (!strcmp(g_limits.keys[i], key)) return g_limits.vals[i];
   return nullptr;
+}
+
+// Measurement switches (A/B gate and share-estimator modes, the context
+// refresh period): they change how a tenant is charged, so a container that
+// runs under a grant file cannot set them -- honoured only for hand-run
+// slices without one.
+const char* unguarded_env(const char* key) {
+  ensure_limits();
+  return g_limits.loaded ? nullptr : getenv(key);
 }
 
 void load_config() {
@@ -575,14 +637,14 @@ void load_config() {
   g_cfg.occupancy = !(oc && (!strcmp(oc, "0") || !strcasecmp(oc, "false")));
   const char* op = grant_env("MIVGPU_OCC_PERIOD_US");
   if (op && atoll(op) >= 200) g_cfg.occ_period_ns = (uint64_t)atoll(op) * 1000ull;
-  const char* gm = getenv("MIVGPU_GATE_MODE");
+  const char* gm = unguarded_env("MIVGPU_GATE_MODE");
   g_cfg.gate_device_mode = gm && !strcmp(gm, "device");
-  const char* se = getenv("MIVGPU_SHARE_EST");
+  const char* se = unguarded_env("MIVGPU_SHARE_EST");
   g_cfg.share_instant = se && !strcmp(se, "instant");
   g_cfg.share_ratio = se && !strcmp(se, "ratio");
   const char* tau = grant_env("MIVGPU_SHARE_TAU_MS");
   if (tau && atof(tau) > 0) g_cfg.share_tau_ns = atof(tau) * 1e6;
-  const char* crm = getenv("MIVGPU_CONTEXT_REFRESH_MS");
+  const char* crm = unguarded_env("MIVGPU_CONTEXT_REFRESH_MS");
   if (crm && *crm) g_cfg.context_refresh_ns = (uint64_t)atoll(crm) * 1000000ull;
   const char* kfd = grant_env("MIVGPU_KFD_SYSFS");
   if (kfd && *kfd) snprintf(g_cfg.kfd_sysfs, sizeof(g_cfg.kfd_sysfs), "%s", kfd);
@@ -691,7 +753,7 @@ bool open_region() {
   } else {
     flock(fd, LOCK_EX);
     struct stat st;
-    fstat(fd, &st);
+    mivgpu_fstat(fd, &st);
     if ((size_t)st.st_size < sizeof(mivgpu_shared_region_t)) {
       if (ftruncate(fd, sizeof(mivgpu_shared_region_t)) != 0) {
         mlog(0, "ftruncate(%s) failed: %s", g_cfg.cache_path, strerror(errno));
@@ -777,14 +839,67 @@ bool open_region() {
 std::atomic<bool> g_exiting{false};
 void quiesce_background_threads();
 
+void housekeeping_final();
+
 void on_exit_release() {
   g_exiting.store(true, std::memory_order_release);
   quiesce_background_threads();
+  if (g_region) housekeeping_final();
   if (!g_region || g_slot < 0) return;
   lock_region();
   reclaim_slot_locked(g_slot);
   unlock_region();
   g_slot = -1;
+}
+
+// ----------------------------------------------------------- control file --
+// The monitor's verdicts (shared_region.h mivgpu_control_t): mapped read-only,
+// so neither a block nor the host-measured excess can be cleared from inside
+// the container.  Named by the grant (MIVGPU_CONTROL_FILE, a grant key: with
+// a grant file only the device plugin can point it anywhere).
+const mivgpu_control_t* g_ctl = nullptr;
+// Under a grant file the core limits are fixed: whether any device has one is
+// computed once at bootstrap (-1: no grant file, read the region per launch).
+int g_any_limit_static = -1;
+
+void open_control() {
+  const char* path = grant_env("MIVGPU_CONTROL_FILE");
+  if (!path || !*path) return;
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
+    mlog(1, "control file %s: %s (monitor verdicts only through the shared region)", path, strerror(errno));
+    return;
+  }
+  struct stat st;
+  if (mivgpu_fstat(fd, &st) == 0 && (size_t)st.st_size >= sizeof(mivgpu_control_t)) {
+    void* p = mmap(nullptr, sizeof(mivgpu_control_t), PROT_READ, MAP_SHARED, fd, 0);
+    if (p != MAP_FAILED) g_ctl = static_cast<const mivgpu_control_t*>(p);
+  } else {
+    mlog(1, "control file %s is too short; ignored", path);
+  }
+  close(fd);
+}
+
+inline int64_t realtime_ns() {
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME_COARSE, &ts);
+  return (int64_t)ts.tv_sec * 1000000000ll + (int64_t)ts.tv_nsec;
+}
+
+// The verdicts hold while the monitor's lease is live.
+inline bool ctl_live() {
+  return g_ctl && __atomic_load_n(&g_ctl->magic, __ATOMIC_ACQUIRE) == MIVGPU_CTL_MAGIC &&
+         realtime_ns() < __atomic_load_n(&g_ctl->lease_until_ns, __ATOMIC_RELAXED);
+}
+inline bool ctl_block() {
+  return g_ctl && __atomic_load_n(&g_ctl->block, __ATOMIC_RELAXED) != 0 && ctl_live();
+}
+inline bool ctl_over() {
+  return g_ctl && __atomic_load_n(&g_ctl->over_grant, __ATOMIC_RELAXED) != 0 && ctl_live();
+}
+inline uint64_t ctl_excess(int dev) {
+  if (!g_ctl || !__atomic_load_n(&g_ctl->host_excess[dev], __ATOMIC_RELAXED) || !ctl_live()) return 0;
+  return __atomic_load_n(&g_ctl->host_excess[dev], __ATOMIC_RELAXED);
 }
 
 // --------------------------------------------------------- lazy bootstrap --
@@ -809,6 +924,12 @@ void bootstrap() {
   if (g_num_devices > MIVGPU_MAX_DEVICES) g_num_devices = MIVGPU_MAX_DEVICES;
   if (!open_region()) {
     mlog(0, "shared region unavailable; memory limits enforced per process only");
+  }
+  open_control();
+  if (g_limits.loaded) {
+    g_any_limit_static = 0;
+    for (int d = 0; d < (g_num_devices > 0 ? g_num_devices : 1); ++d)
+      if (g_cfg.cu_limit[d] > 0 && g_cfg.cu_limit[d] < 100) g_any_limit_static = 1;
   }
   atexit(on_exit_release);
   for (int d = 0; d < g_num_devices; ++d) {
@@ -835,9 +956,32 @@ inline int current_device() {
   return d;
 }
 
+// The enforced grant.  Under a grant file it is the file's (host-owned,
+// read-only): the region's copies sit in tenant-writable memory and are only
+// mirrors for the monitor.  Without one (hand-run slices) the region's values
+// rule, so a region-level limit change reaches every process of the container.
 inline uint64_t limit_of(int dev) {
   if (g_cfg.disabled) return 0;
-  return g_region ? __atomic_load_n(&g_region->mem_limit[dev], __ATOMIC_RELAXED) : g_cfg.mem_limit[dev];
+  if (g_limits.loaded || !g_region) return g_cfg.mem_limit[dev];
+  return __atomic_load_n(&g_region->mem_limit[dev], __ATOMIC_RELAXED);
+}
+inline uint64_t cu_limit_of(int dev) {
+  if (g_limits.loaded || !g_region) return (uint64_t)g_cfg.cu_limit[dev];
+  return __atomic_load_n(&g_region->cu_limit[dev], __ATOMIC_RELAXED);
+}
+inline uint64_t cu_mask_of(int dev) {
+  if (g_limits.loaded || !g_region) return (uint64_t)g_cfg.cu_mask_count[dev];
+  return __atomic_load_n(&g_region->cu_mask_count[dev], __ATOMIC_RELAXED);
+}
+inline int core_policy() {
+  if (g_limits.loaded || !g_region) return g_cfg.policy;
+  return __atomic_load_n(&g_region->core_policy, __ATOMIC_RELAXED);
+}
+// The monitor's contention switch (feedback.go:74-134): from the control file
+// when there is one, else from the region.
+inline int util_switch() {
+  if (g_ctl) return ctl_live() ? __atomic_load_n(&g_ctl->utilization_switch, __ATOMIC_RELAXED) : 0;
+  return g_region ? __atomic_load_n(&g_region->utilization_switch, __ATOMIC_RELAXED) : 0;
 }
 
 // ------------------------------------------------------ allocation tracker --
@@ -1119,9 +1263,21 @@ bool reserve(int dev, uint64_t bytes, AllocKind kind) {
     account_add(dev, bytes, kind);
     return true;
   }
+  // Over its grant by host truth (the monitor's verdict, control file): no
+  // allocation at all until a pass finds it back under, whatever the counters
+  // in the (tenant-writable) region say.
+  if (ctl_over()) {
+    tmark("mivgpu:oom-over-grant dev=%d req_mib=%llu", dev, (unsigned long long)(bytes >> 20));
+    mlog(1, "device %d: allocation of %llu MiB refused: the container is over its HBM grant (host truth)", dev,
+         (unsigned long long)(bytes >> 20));
+    return false;
+  }
+  // VRAM the host sees the container hold beyond this counter (the monitor's
+  // KFD truth, control file): a zeroed or stale counter cannot buy headroom
+  const uint64_t excess = ctl_excess(dev);
   for (int attempt = 0; attempt < 2; ++attempt) {
     uint64_t cur = __atomic_load_n(&g_region->dev_used[dev], __ATOMIC_RELAXED);
-    while (cur + bytes <= lim) {
+    while (cur + excess + bytes <= lim) {
       if (__atomic_compare_exchange_n(&g_region->dev_used[dev], &cur, cur + bytes, true,
                                       __ATOMIC_ACQ_REL, __ATOMIC_RELAXED)) {
         // dev_used already bumped by the CAS; mirror into the process slot.
@@ -1337,7 +1493,7 @@ uint64_t code_object_file_bytes(const char* path) {
   if (fd < 0) return 0;
   struct stat st;
   uint64_t n = 0;
-  if (fstat(fd, &st) == 0 && st.st_size > 0) {
+  if (mivgpu_fstat(fd, &st) == 0 && st.st_size > 0) {
     void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
     if (m != MAP_FAILED) {
       n = code_object_bytes(m, (uint64_t)st.st_size);
@@ -1366,8 +1522,10 @@ hipError_t guarded_module_load(hipModule_t* module, uint64_t bytes, Call&& call)
 }
 
 // ------------------------------------------------------- launch-side state --
-std::atomic<uint64_t> g_last_kernel_write_ns{0};
 std::atomic<uint64_t> g_launches_local{0};
+// Launches per device (device 0 for the common one-device container: no
+// runtime call on the launch path), published by the housekeeping thread.
+std::atomic<uint64_t> g_dev_launches[MIVGPU_MAX_DEVICES];
 
 // Governor (gate) per device.  Host stats = 8 counters + a 128-entry trace
 // ring of 8 x int64 per gate + 64 per-slot hold ends, hold starts and held
@@ -1728,7 +1886,7 @@ bool occ_sample(int dev, uint64_t now) {
     }
     state = own > 0 ? 0 : (others > 0 ? 3 : 1);
   }
-  const int mask = (int)__atomic_load_n(&g_region->cu_mask_count[dev], __ATOMIC_RELAXED);
+  const int mask = (int)cu_mask_of(dev);
   if (mask > 0) {
     const double f = (double)mask / (double)device_cus(dev);
     if (share > f) share = f;
@@ -1747,7 +1905,7 @@ bool occ_sample(int dev, uint64_t now) {
   // charged, the balance is bounded by one burst either way.  The gates read
   // it at execution time and hold while it is negative.
   if (hs) {
-    const uint64_t lim = __atomic_load_n(&g_region->cu_limit[dev], __ATOMIC_RELAXED);
+    const uint64_t lim = cu_limit_of(dev);
     const double rate = (lim > 0 && lim < 100) ? (double)lim / 100.0 : 1.0;
     const double cap = (double)g_cfg.gate_cap_ns;
     if (!o.bucket) {
@@ -1805,8 +1963,41 @@ bool occ_sample(int dev, uint64_t now) {
 
 uint64_t g_occ_pass_ns = 0, g_occ_passes = 0, g_occ_pass_max_ns = 0;   // under g_occ_pass_mu
 
+uint64_t g_hk_launches = 0;   // launches seen by the previous pass (under g_occ_pass_mu)
+
+// The launch hooks' publishing, off the launch path: when the process launched
+// since the previous pass -- the heartbeat and last-kernel time, the launch
+// counts, the monitor's activity flag (recent_kernel = 2, feedback.go:74-134),
+// and the latest-launch clock the sampler's "owes work" test reads.
+void housekeeping(uint64_t now) {
+  const uint64_t l = g_launches_local.load(std::memory_order_relaxed);
+  if (l == g_hk_launches) return;
+  g_hk_launches = l;
+  const uint64_t c = coarse_ns();
+  if (c > g_last_launch_ns.load(std::memory_order_relaxed)) g_last_launch_ns.store(c, std::memory_order_relaxed);
+  __atomic_store_n(&g_region->last_kernel_time, (int64_t)time(nullptr), __ATOMIC_RELAXED);
+  const int rk = __atomic_load_n(&g_region->recent_kernel, __ATOMIC_RELAXED);
+  if (rk >= 0 && rk < 2) __atomic_store_n(&g_region->recent_kernel, 2, __ATOMIC_RELAXED);
+  if (g_slot >= 0) {
+    mivgpu_proc_slot_t* s = &g_region->procs[g_slot];
+    __atomic_store_n(&s->heartbeat_ns, now, __ATOMIC_RELAXED);
+    for (int d = 0; d < g_num_devices && d < MIVGPU_MAX_DEVICES; ++d)
+      __atomic_store_n(&s->util[d].launches, g_dev_launches[d].load(std::memory_order_relaxed), __ATOMIC_RELAXED);
+  }
+}
+
+void housekeeping_final() {
+  std::lock_guard<std::mutex> pass(g_occ_pass_mu);
+  housekeeping(mono_ns());
+}
+
 void* occ_main(void*) {
   int tries[MIVGPU_MAX_DEVICES] = {0};
+  {   // the first launch is published at once
+    std::lock_guard<std::mutex> pass(g_occ_pass_mu);
+    Guard g;
+    if (!g_exiting.load(std::memory_order_acquire)) housekeeping(mono_ns());
+  }
   for (;;) {
     // fast while a gate ran within the last second, slow for reporting only
     const uint64_t t = coarse_ns();
@@ -1817,6 +2008,8 @@ void* occ_main(void*) {
     if (g_exiting.load(std::memory_order_acquire)) return nullptr;
     Guard g;
     const uint64_t now = mono_ns();
+    housekeeping(now);
+    if (!g_cfg.occupancy) continue;
     for (int d = 0; d < g_num_devices; ++d) {
       // a device without a KFD view is retried a few times (its identity
       // resolves at the first allocation), then left to wall-time charging
@@ -1832,8 +2025,11 @@ void* occ_main(void*) {
   return nullptr;
 }
 
+// The sampler thread doubles as the housekeeping thread (heartbeat, activity
+// flag, launch counts): started at the first launch, with or without the
+// occupancy sampling.
 void start_occ_sampler() {
-  if (!g_cfg.occupancy || g_cfg.disabled || !g_region || g_occ_started.exchange(true)) return;
+  if (g_cfg.disabled || !g_region || g_occ_started.exchange(true)) return;
   pthread_t th;
   pthread_attr_t a;
   pthread_attr_init(&a);
@@ -1844,17 +2040,17 @@ void start_occ_sampler() {
 
 inline bool gate_wanted(int dev) {
   if (g_cfg.disabled || !g_region) return false;
-  int policy = __atomic_load_n(&g_region->core_policy, __ATOMIC_RELAXED);
+  int policy = core_policy();
   if (policy == 2) return false;
-  uint64_t lim = __atomic_load_n(&g_region->cu_limit[dev], __ATOMIC_RELAXED);
-  int sw = __atomic_load_n(&g_region->utilization_switch, __ATOMIC_RELAXED);
+  uint64_t lim = cu_limit_of(dev);
+  int sw = util_switch();
   if (lim == 0 || lim >= 100) return false;
   // A CU mask no wider than the limit (within one granule of one CU per XCD:
   // the device plugin rounds grants to whole granules) already enforces it in
   // hardware; time-slicing on top would charge the tenant for a GPU it cannot
   // reach (VERDICT r1 "double throttle").  This holds under policy force too:
   // force asks for the limit to be enforced, and the mask enforces it.
-  const uint64_t mask = __atomic_load_n(&g_region->cu_mask_count[dev], __ATOMIC_RELAXED);
+  const uint64_t mask = cu_mask_of(dev);
   if (mask > 0 && mask * 100 <= lim * (uint64_t)device_cus(dev) + 100ull * (uint64_t)device_xcds(dev)) return false;
   if (policy == 1) return true;
   // default: time-slice when there is no mask or the monitor asks for
@@ -1867,7 +2063,7 @@ void enqueue_gate_locked(int dev, DeviceGate& G, int slot, hipStream_t stream, u
   GateSlot& S = G.slots[slot];
   const uint64_t first = S.first_submit_host_ns.load(std::memory_order_relaxed);
   long long submit_dev = first ? (long long)first + G.offset_ns : -1;
-  const uint64_t rate = __atomic_load_n(&g_region->cu_limit[dev], __ATOMIC_RELAXED) * 10000ull;
+  const uint64_t rate = cu_limit_of(dev) * 10000ull;
   unsigned int rate_ppm = (unsigned int)(rate < 1000000ull ? rate : 1000000ull);
   long long cap = g_cfg.gate_cap_ns, hold = g_cfg.gate_max_hold_ns;
   int slot_arg = slot;
@@ -2106,50 +2302,48 @@ void stamp_before_sync(hipStream_t stream, bool all_streams) {
 // Any device of the process under a core limit (each device has its own,
 // HIP_DEVICE_CORE_LIMIT_<i>; the gate decision itself is per device).
 inline bool any_core_limit() {
+  if (g_any_limit_static >= 0) return g_any_limit_static != 0;
   const int n = g_num_devices > 0 ? g_num_devices : 1;
   for (int d = 0; d < n; ++d) {
-    const uint64_t cl = __atomic_load_n(&g_region->cu_limit[d], __ATOMIC_RELAXED);
+    const uint64_t cl = cu_limit_of(d);
     if (cl > 0 && cl < 100) return true;
   }
   return false;
 }
 
-// Per-launch bookkeeping.  Hot path when nothing throttles: a few relaxed
-// loads, one thread-local branch, one coarse clock read at most once per ms.
-// `dev` < 0: the calling thread's current device (the launch's device).
+// Parks the calling launch while a block is in force: the monitor's verdict
+// in the read-only control file (over grant, or a higher-priority task; held
+// while its lease is live), or the legacy region flag (recent_kernel == -1).
+void park_while_blocked() {
+  TRange r("mivgpu:priority-block");
+  const uint64_t t0 = coarse_ns();
+  for (;;) {
+    const bool ctl = ctl_block();
+    const bool reg = __atomic_load_n(&g_region->recent_kernel, __ATOMIC_RELAXED) < 0;
+    if (!ctl && !reg) return;
+    // the region flag is tenant-writable and has no lease: never wedge on it
+    if (!ctl && coarse_ns() - t0 > 60ull * 1000000000ull) return;
+    usleep(1000);
+  }
+}
+
+// Per-launch bookkeeping.  Hot path when nothing throttles: the TLS guard, a
+// few relaxed loads and one counter increment -- no clock read, no region
+// store (the housekeeping thread publishes the heartbeat, the activity flag
+// and the launch counts, see housekeeping()).  `dev` < 0: the calling
+// thread's current device (the launch's device).
 inline LaunchTicket on_launch(hipStream_t stream, bool graph = false, int dev = -1) {
   ensure_init();
   if (g_cfg.disabled || !g_region) return LaunchTicket{};
-  g_launches_local.fetch_add(1, std::memory_order_relaxed);
-  int rk = __atomic_load_n(&g_region->recent_kernel, __ATOMIC_RELAXED);
-  if (__builtin_expect(rk < 0, 0)) {
-    // Priority blocking requested by the node monitor: park until released.
-    TRange r("mivgpu:priority-block");
-    uint64_t t0 = coarse_ns();
-    while (__atomic_load_n(&g_region->recent_kernel, __ATOMIC_RELAXED) < 0) {
-      usleep(1000);
-      if (coarse_ns() - t0 > 60ull * 1000000000ull) break;  // never wedge forever
-    }
-  } else if (rk < 2) {
-    __atomic_store_n(&g_region->recent_kernel, 2, __ATOMIC_RELAXED);
-  }
-  uint64_t now = coarse_ns();
-  g_last_launch_ns.store(now, std::memory_order_relaxed);
-  uint64_t last = g_last_kernel_write_ns.load(std::memory_order_relaxed);
-  if (now - last > 1000000ull && g_last_kernel_write_ns.compare_exchange_strong(last, now)) {
-    __atomic_store_n(&g_region->last_kernel_time, (int64_t)time(nullptr), __ATOMIC_RELAXED);
-    const int hd = dev >= 0 ? dev : current_device();
-    start_occ_sampler();
-    if (g_slot >= 0) {
-      mivgpu_proc_slot_t* s = &g_region->procs[g_slot];
-      __atomic_store_n(&s->heartbeat_ns, now, __ATOMIC_RELAXED);
-      __atomic_store_n(&s->util[hd].launches, g_launches_local.load(std::memory_order_relaxed),
-                       __ATOMIC_RELAXED);
-    }
-  }
-  if (__builtin_expect(any_core_limit() || __atomic_load_n(&g_region->utilization_switch, __ATOMIC_RELAXED), 0)) {
-    if (dev < 0) dev = current_device();
-    return LaunchTicket{dev, maybe_gate(stream, graph, dev)};
+  const int hd = dev >= 0 ? dev : (g_num_devices == 1 ? 0 : current_device());
+  if (__builtin_expect(g_launches_local.fetch_add(1, std::memory_order_relaxed) == 0, 0)) start_occ_sampler();
+  g_dev_launches[hd].fetch_add(1, std::memory_order_relaxed);
+  if (__builtin_expect(__atomic_load_n(&g_region->recent_kernel, __ATOMIC_RELAXED) < 0 ||
+                       (g_ctl && __atomic_load_n(&g_ctl->block, __ATOMIC_RELAXED)), 0))
+    park_while_blocked();
+  if (__builtin_expect(any_core_limit() || util_switch(), 0)) {
+    g_last_launch_ns.store(coarse_ns(), std::memory_order_relaxed);
+    return LaunchTicket{hd, maybe_gate(stream, graph, hd)};
   }
   return LaunchTicket{};
 }
@@ -2359,7 +2553,7 @@ MIVGPU_EXPORT hipError_t hipMemGetInfo(size_t* free_b, size_t* total_b) {
   uint64_t lim = limit_of(dev);
   if (lim && g_region) {
     refresh_context(dev, false);
-    uint64_t used = __atomic_load_n(&g_region->dev_used[dev], __ATOMIC_RELAXED);
+    uint64_t used = __atomic_load_n(&g_region->dev_used[dev], __ATOMIC_RELAXED) + ctl_excess(dev);
     uint64_t vfree = used >= lim ? 0 : lim - used;
     if (free_b) *free_b = vfree < *free_b ? vfree : *free_b;
     if (total_b) *total_b = lim;
@@ -2943,6 +3137,13 @@ MIVGPU_EXPORT long mivgpu_abi_offsetof(int field) {
     case MIVGPU_F_SIZEOF_SLOT: return sizeof(mivgpu_proc_slot_t);
     case MIVGPU_F_SLOT_USED: return offsetof(mivgpu_proc_slot_t, used);
     case MIVGPU_F_SLOT_UTIL: return offsetof(mivgpu_proc_slot_t, util);
+    case MIVGPU_F_CTL_SEQ: return offsetof(mivgpu_control_t, seq);
+    case MIVGPU_F_CTL_LEASE: return offsetof(mivgpu_control_t, lease_until_ns);
+    case MIVGPU_F_CTL_BLOCK: return offsetof(mivgpu_control_t, block);
+    case MIVGPU_F_CTL_SWITCH: return offsetof(mivgpu_control_t, utilization_switch);
+    case MIVGPU_F_CTL_OVER: return offsetof(mivgpu_control_t, over_grant);
+    case MIVGPU_F_CTL_EXCESS: return offsetof(mivgpu_control_t, host_excess);
+    case MIVGPU_F_SIZEOF_CTL: return sizeof(mivgpu_control_t);
     default: return -1;
   }
 }
@@ -3028,6 +3229,16 @@ MIVGPU_EXPORT int mivgpu_gate_trace(int dev, long long* out, int n) {
     for (int k = 0; k < 8; ++k) out[i * 8 + k] = e[k];
   }
   return cnt;
+}
+
+// How the process is charged: bit 0 device-bucket gate mode, bit 1 instant
+// share estimator, bit 2 ratio estimator, bit 3 a grant file is loaded, bit 4
+// a control file is mapped; *ctx_refresh_ns the context-VRAM refresh period.
+MIVGPU_EXPORT int mivgpu_config_info(unsigned long long* ctx_refresh_ns) {
+  ensure_init();
+  if (ctx_refresh_ns) *ctx_refresh_ns = g_cfg.context_refresh_ns;
+  return (g_cfg.gate_device_mode ? 1 : 0) | (g_cfg.share_instant ? 2 : 0) | (g_cfg.share_ratio ? 4 : 0) |
+         (g_limits.loaded ? 8 : 0) | (g_ctl ? 16 : 0);
 }
 
 MIVGPU_EXPORT int mivgpu_active(void) {

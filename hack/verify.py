@@ -229,6 +229,8 @@ def check_static(verbose=False) -> list[str]:
             cmd = [cxx, "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-Wno-unused-parameter",
                    "-Wno-deprecated-declarations", "-D__HIP_PLATFORM_AMD__", f"-isystem{rocm}",
                    f"-I{ROOT / 'csrc/include'}", f"-I{gen}", str(s)]
+            if s.name == "mivgpu_shim.cpp":    # built with its glibc floor (utils/build.py)
+                cmd[-1:-1] = ["-DMIVGPU_GLIBC_FLOOR", "-include", str(ROOT / "csrc/shim/glibc_floor.h")]
             r = subprocess.run(cmd, capture_output=True, text=True)
             if r.returncode:
                 errs.append(f"{s.relative_to(ROOT)}: g++ -Wall -Wextra -Werror:\n{r.stderr[-1500:]}")

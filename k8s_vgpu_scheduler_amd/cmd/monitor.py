@@ -6,8 +6,11 @@ spec.nodeName, pkg/monitor/nvidia/cudevshr.go:308) for the container lister,
 samples KFD wave occupancy, serves Prometheus (``--legacy-metrics`` adds the
 pre-2.x series), and runs the 5 s feedback loop -- paused while the device
 plugin holds the compute-partition apply lock (main.go:79-109).  Each pass
-also restores every container's HBM usage from KFD host truth and blocks a
-container over its grant (monitor/hosttruth.py).
+also enforces every granted container's HBM from KFD host truth, driven by
+the host-owned grant files (monitor/hosttruth.py: over grant, shim not
+loaded, excess), writes the verdicts into the read-only control files
+(monitor/control.py), and escalates a container that stays over its grant
+(``--over-grant-action``, monitor/escalate.py).
 """
 
 from __future__ import annotations
@@ -42,6 +45,12 @@ def main(argv=None):
                     help="seconds between KFD wave-occupancy samples (0 = off)")
     ap.add_argument("--no-host-truth", action="store_true",
                     help="do not recompute container HBM usage from KFD each pass (trust the shared regions)")
+    ap.add_argument("--over-grant-action", choices=("block", "evict", "kill"), default="block",
+                    help="what happens to a container over its HBM grant (host truth) for --over-grant-passes "
+                         "passes: block its launches (control file), evict its pod (Eviction API), or SIGKILL "
+                         "its host processes holding VRAM")
+    ap.add_argument("--over-grant-passes", type=int, default=3,
+                    help="consecutive over-grant passes before --over-grant-action evict/kill")
     ap.add_argument("-v", type=int, default=2)
     a = ap.parse_args(argv)
     setup_logging(a.v)
@@ -59,20 +68,23 @@ def main(argv=None):
         log.warning("no amd-smi backend (%s): host metrics disabled", e)
         backend = None
     occ = OccupancySampler(period_s=a.occupancy_period).start() if a.occupancy_period > 0 else None
-    truth = None
+    truth = escalation = None
     if not a.no_host_truth:
+        from k8s_vgpu_scheduler_amd.monitor.escalate import OverGrantPolicy
         from k8s_vgpu_scheduler_amd.monitor.hosttruth import HostTruth, kfd_gpu_ids
         from k8s_vgpu_scheduler_amd.scheduler.events import EventRecorder
-        truth = HostTruth(kfd_gpu_ids(backend), events=EventRecorder(client, component="hami-vgpu-monitor"))
+        events = EventRecorder(client, component="hami-vgpu-monitor")
+        truth = HostTruth(kfd_gpu_ids(backend), events=events)
+        escalation = OverGrantPolicy(a.over_grant_action, a.over_grant_passes, client=client, events=events)
     reg = CollectorRegistry()
     reg.register(MonitorCollector(lister, backend, a.node_name, occupancy=occ, legacy=a.legacy_metrics,
-                                  truth=truth))
+                                  truth=truth, escalation=escalation))
     host, _, port = a.metrics_bind_address.rpartition(":")
     start_http_server(int(port), addr=host or "0.0.0.0", registry=reg)
     stop = threading.Event()
     pause = threading.Event()
     threading.Thread(target=watch_partition_lock, args=(pause, stop), name="partition-lock", daemon=True).start()
-    watch_and_feedback(lister, stop, pause=pause, truth=truth)
+    watch_and_feedback(lister, stop, pause=pause, truth=truth, escalation=escalation)
     return 0
 
 

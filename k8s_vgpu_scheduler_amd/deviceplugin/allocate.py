@@ -23,9 +23,12 @@ docs/develop/amd-vgpu.md:47-104.  MI355X translation:
        MIVGPU_SHARED_CACHE    $HOOK_PATH/vgpu/<uuid4>.cache
        MIVGPU_DEVICE_UUIDS, MIVGPU_OVERSUBSCRIBE, MIVGPU_LOG_LEVEL,
        GPU_CORE_UTILIZATION_POLICY=disable (with --disable-core-limit)
+       MIVGPU_CONTROL_FILE    /etc/mivgpu/control: the monitor's verdicts (grant key)
   mounts libmivgpu.so (ro), the per-container cache dir (rw), the grant file
-       (ro, LIMITS_PATH), /etc/ld.so.preload (ro) unless the container sets
-       MIVGPU_DISABLE_CONTROL=true
+       (ro, LIMITS_PATH), the control file (ro, monitor/control.py: block,
+       utilization switch and host-measured excess VRAM, written in place by
+       the monitor on the host), /etc/ld.so.preload (ro) unless the container
+       sets MIVGPU_DISABLE_CONTROL=true
 
 The grant file repeats the policy settings of ``env`` (limits, CU mask, core
 limit/policy, visible devices, region path).  It is written on the host and
@@ -44,6 +47,8 @@ import uuid as _uuid
 from dataclasses import dataclass, field
 
 from k8s_vgpu_scheduler_amd.device.codec import format_ranges, ranges_count
+from k8s_vgpu_scheduler_amd.monitor.control import CONTAINER_CONTROL_PATH, control_host_path
+from k8s_vgpu_scheduler_amd.monitor.control import create as create_control
 
 CONTAINER_LIB = "/usr/local/vgpu/libmivgpu.so"
 LIMITS_PATH = "/etc/mivgpu/limits.conf"     # fixed in the shim (kLimitsPath)
@@ -52,7 +57,7 @@ GRANT_KEYS = ("HIP_DEVICE_MEMORY_LIMIT", "HIP_DEVICE_CORE_LIMIT", "HSA_CU_MASK",
               "HIP_TASK_PRIORITY", "MIVGPU_OVERSUBSCRIBE", "MIVGPU_SHARED_CACHE", "MIVGPU_DEVICE_UUIDS",
               "ROCR_VISIBLE_DEVICES", "MIVGPU_ACCOUNT_CONTEXT", "MIVGPU_KFD_SYSFS", "MIVGPU_OCCUPANCY",
               "MIVGPU_OCC_PERIOD_US", "MIVGPU_GATE_INTERVAL_US", "MIVGPU_GATE_BURST_US", "MIVGPU_SHARE_TAU_MS",
-              "MIVGPU_DISABLE_CONTROL", "GPU_MAX_HW_QUEUES", "MIVGPU_GATE_MAX_HOLD_US")
+              "MIVGPU_DISABLE_CONTROL", "GPU_MAX_HW_QUEUES", "MIVGPU_GATE_MAX_HOLD_US", "MIVGPU_CONTROL_FILE")
 # per-device forms of grant keys (HIP_DEVICE_MEMORY_LIMIT_<i>, HIP_DEVICE_CORE_LIMIT_<i>)
 GRANT_PREFIXES = ("HIP_DEVICE_MEMORY_LIMIT_", "HIP_DEVICE_CORE_LIMIT_")
 
@@ -154,6 +159,7 @@ def container_env(devreq: list, gpus: dict, cfg: PluginConfig, cache_file: str) 
             for i, p in enumerate(pcts):
                 env[f"HIP_DEVICE_CORE_LIMIT_{i}"] = str(p)
     env["MIVGPU_SHARED_CACHE"] = cache_file
+    env["MIVGPU_CONTROL_FILE"] = CONTAINER_CONTROL_PATH
     env["MIVGPU_DEVICE_UUIDS"] = ",".join(d.uuid for d in devreq)
     if cfg.device_memory_scaling > 1:
         env["MIVGPU_OVERSUBSCRIBE"] = "true"
@@ -178,6 +184,7 @@ def allocate_container(pod: dict, ctr: dict, devreq: list, gpus: dict, cfg: Plug
     uid = (pod.get("metadata") or {}).get("uid", "")
     host_dir = f"{hook}/vgpu/containers/{uid}_{ctr.get('name', '')}"
     limits = limits_host_path(hook, uid, ctr.get("name", ""))
+    control = control_host_path(hook, uid, ctr.get("name", ""))
     if make_dirs:
         import shutil
         shutil.rmtree(host_dir, ignore_errors=True)
@@ -192,10 +199,12 @@ def allocate_container(pod: dict, ctr: dict, devreq: list, gpus: dict, cfg: Plug
             f.write(grant_text(envs))
         os.chmod(tmp, 0o444)
         os.replace(tmp, limits)
+        create_control(control)
     mounts = [
         {"container_path": CONTAINER_LIB, "host_path": f"{hook}/vgpu/libmivgpu.so", "read_only": True},
         {"container_path": f"{hook}/vgpu", "host_path": host_dir, "read_only": False},
         {"container_path": LIMITS_PATH, "host_path": limits, "read_only": True},
+        {"container_path": CONTAINER_CONTROL_PATH, "host_path": control, "read_only": True},
     ]
     # the pod-spec opt-out drops the preload -- only where opting out is allowed
     # (a fractional pod would otherwise escape every limit; the webhook also

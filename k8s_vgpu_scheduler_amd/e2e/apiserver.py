@@ -275,6 +275,11 @@ class _Handler(BaseHTTPRequestHandler):
             target = (body.get("target") or {}).get("name")
             c.bind(ns or "default", name, target, (body.get("metadata") or {}).get("uid"))
             return self._send(201, {"kind": "Status", "apiVersion": "v1", "status": "Success", "code": 201})
+        if kind == "pods" and name and sub == "eviction":
+            if body.get("kind") != "Eviction":
+                return self._status(400, "BadRequest", "eviction body must be an Eviction")
+            c.evict(ns or "default", name)
+            return self._send(201, {"kind": "Status", "apiVersion": "v1", "status": "Success", "code": 201})
         if name:
             return self._status(405, "MethodNotAllowed", "POST to a named resource")
         self._send(201, c.create(kind, body, ns))

@@ -191,16 +191,18 @@ def container_env(alloc: dict, base: dict | None = None) -> dict:
     env = dict(base if base is not None else os.environ)
     env.update(alloc["envs"])
     mounts = alloc["mounts"]
-    if "MIVGPU_SHARED_CACHE" in env:
-        env["MIVGPU_SHARED_CACHE"] = host_path(env["MIVGPU_SHARED_CACHE"], mounts)
+    for k in ("MIVGPU_SHARED_CACHE", "MIVGPU_CONTROL_FILE"):
+        if k in env:
+            env[k] = host_path(env[k], mounts)
     from k8s_vgpu_scheduler_amd.deviceplugin.allocate import LIMITS_PATH, grant_text, parse_grant
     grant = next((m for m in mounts if m["container_path"] == LIMITS_PATH), None)
     if grant is not None:
         # the shim reads the grant from the read-only mount; on the host the
         # same file (with its region path mapped) is named by MIVGPU_LIMITS_FILE
         g = parse_grant(Path(grant["host_path"]).read_text())
-        if "MIVGPU_SHARED_CACHE" in g:
-            g["MIVGPU_SHARED_CACHE"] = host_path(g["MIVGPU_SHARED_CACHE"], mounts)
+        for k in ("MIVGPU_SHARED_CACHE", "MIVGPU_CONTROL_FILE"):
+            if k in g:
+                g[k] = host_path(g[k], mounts)
         hp = Path(grant["host_path"] + ".host")
         hp.write_text(grant_text(g))
         env["MIVGPU_LIMITS_FILE"] = str(hp)

@@ -81,6 +81,11 @@ class KubeClient:
     def bind(self, namespace: str, pod_name: str, node: str, uid: str | None = None) -> None:
         raise NotImplementedError
 
+    def evict(self, namespace: str, pod_name: str) -> None:
+        """Eviction API (POST pods/<name>/eviction, policy/v1): the API server
+        deletes the pod unless a PodDisruptionBudget refuses (429)."""
+        raise NotImplementedError
+
     def watch(self, kind: str, handler: Callable[[str, dict, Optional[dict]], None],
               namespace: str | None = None, field_selector: dict | None = None) -> Callable[[], None]:
         """Subscribe to ADDED/MODIFIED/DELETED events; returns an unsubscribe fn.

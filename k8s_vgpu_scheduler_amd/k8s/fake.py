@@ -42,6 +42,7 @@ class FakeCluster(KubeClient):
         self._watchers: dict[str, list] = {}
         self.reactors: list[Reactor] = []
         self.actions: list[tuple] = []  # (verb, kind, ns, name)
+        self.evictions: list[tuple] = []  # (ns, name) of Eviction API calls
 
     # ------------------------------------------------------------ internals
     def _store(self, kind):
@@ -197,6 +198,13 @@ class FakeCluster(KubeClient):
             if (cur.get("spec") or {}).get("nodeName"):
                 raise Conflict(f"pod {pod_name} is already assigned to a node")
         self.patch("pods", pod_name, {"spec": {"nodeName": node}}, namespace)
+
+    def evict(self, namespace, pod_name):
+        with self._lock:
+            self.actions.append(("evict", "pods", namespace, pod_name))
+            self._react("evict", "pods", pod_name, namespace, None)
+            self.evictions.append((namespace or "default", pod_name))
+        self.delete("pods", pod_name, namespace)
 
     def watch(self, kind, handler, namespace=None, field_selector=None):
         with self._lock:

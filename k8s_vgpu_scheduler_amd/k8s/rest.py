@@ -181,6 +181,11 @@ class RestClient(KubeClient):
             body["metadata"]["uid"] = uid
         self._req("POST", self._url("pods", pod_name, namespace, "binding"), json=body)
 
+    def evict(self, namespace, pod_name):
+        body = {"apiVersion": "policy/v1", "kind": "Eviction",
+                "metadata": {"name": pod_name, "namespace": namespace}}
+        self._req("POST", self._url("pods", pod_name, namespace, "eviction"), json=body)
+
     def watch(self, kind, handler, namespace=None, field_selector=None):
         stop = threading.Event()
         sel = {"fieldSelector": self._selector(field_selector)} if field_selector else {}

@@ -1,13 +1,17 @@
 """Priority feedback loop over the shared regions (cmd/vGPUmonitor/feedback.go:40-165).
 
 Every 5 s: decay each container's ``recent_kernel`` activity counter (the shim
-sets it to 2 on every launch); count, per GPU uuid and priority level, how
+sets it to 2 while it launches); count, per GPU uuid and priority level, how
 many containers launched recently.  Then per container:
   * blocking  -- a HIGHER-priority (numerically lower) task is active on one of
     its GPUs -> ``recent_kernel = -1`` (the shim parks launches), else 0;
   * util switch -- a higher-priority task, or another task of the SAME priority,
     is active -> ``utilization_switch = 1`` (enforce the core limit with the
     governor even when a CU mask exists), else 0.
+
+Both verdicts go into the shared region (the reference's channel) AND into the
+container's host-owned, read-only control file (control.py), which is what the
+shim obeys when it has one: a tenant rewriting its region cannot clear them.
 """
 
 from __future__ import annotations
@@ -15,6 +19,7 @@ from __future__ import annotations
 import logging
 import threading
 
+from .control import DEFAULT_LEASE_S
 from .hostpid import fill_host_pids
 from .lister import ContainerLister
 from .region import MAX_DEVICES
@@ -47,10 +52,11 @@ def check_priority(ut: dict, p: int, c) -> bool:
     return False
 
 
-def observe(lister: ContainerLister, over: set | None = None):
+def observe(lister: ContainerLister, over: set | None = None, decisions: dict | None = None):
     """``over``: (pod_uid, container) keys the host-truth pass found over
     their HBM grant (hosttruth.py): they stay blocked whatever the
-    priorities say."""
+    priorities say.  ``decisions``: filled with ``{(pod_uid, container):
+    (block, switch)}`` for the control files."""
     ut: dict[str, list[int]] = {}
     cs = lister.list_containers()
     for c in cs:
@@ -70,19 +76,20 @@ def observe(lister: ContainerLister, over: set | None = None):
         p = c.region.priority()
         rk = c.region.recent_kernel()
         sw = c.region.utilization_switch()
-        if over and (c.pod_uid, c.container) in over:
-            if rk >= 0:
-                c.region.set_recent_kernel(-1)
-        elif check_blocking(ut, p, c):
+        block = bool(over and (c.pod_uid, c.container) in over) or check_blocking(ut, p, c)
+        switch = check_priority(ut, p, c)
+        if block:
             if rk >= 0:
                 c.region.set_recent_kernel(-1)
         elif rk < 0:
             c.region.set_recent_kernel(0)
-        if check_priority(ut, p, c):
+        if switch:
             if sw != 1:
                 c.region.set_utilization_switch(1)
         elif sw != 0:
             c.region.set_utilization_switch(0)
+        if decisions is not None:
+            decisions[(c.pod_uid, c.container)] = (block, switch)
     return ut
 
 
@@ -180,30 +187,58 @@ def reconcile_limits(lister: ContainerLister) -> int:
     return fixed
 
 
-def feedback_pass(lister: ContainerLister, truth=None) -> dict:
-    """One pass: map host pids, restore the limits from the grants, restore
-    the usage from host truth (hosttruth.HostTruth, optional), then the
-    priority feedback."""
+def publish_controls(lister: ContainerLister, grants: dict, decisions: dict, verdicts: dict,
+                     lease_s: float = DEFAULT_LEASE_S) -> int:
+    """Write every granted container's verdicts into its host-owned control
+    file (monitor/control.py) and renew the lease.  Returns files written."""
+    n = 0
+    for key, g in grants.items():
+        cf = lister.controls.get(key)
+        if cf is None:
+            continue
+        v = verdicts.get((g.pod_uid, g.container))
+        over = bool(v is not None and v.over)
+        block, switch = decisions.get((g.pod_uid, g.container), (over, False))
+        cf.publish(block=block or over, switch=switch, over=over,
+                   excess=v.excess if v is not None else None, lease_s=lease_s)
+        n += 1
+    lister.controls.retain(set(grants))
+    return n
+
+
+def feedback_pass(lister: ContainerLister, truth=None, escalation=None, lease_s: float = DEFAULT_LEASE_S) -> dict:
+    """One pass: map host pids, restore the region mirrors of the limits from
+    the grants, enforce HBM from host truth (hosttruth.HostTruth, optional:
+    over grant, shim not loaded, excess), the priority feedback, the
+    verdicts into the read-only control files, then the over-grant
+    escalation (escalate.OverGrantPolicy, optional)."""
+    from .hosttruth import load_grants
+
     lister.update()
     fill_host_pids(lister.list_containers())
     fixed = reconcile_limits(lister)
-    over = set()
+    grants = load_grants(lister.base.parent / "limits")
+    verdicts: dict = {}
     if truth is not None:
-        from .hosttruth import grants_from_files
-        truth.enforce(lister, grants_from_files(lister))
-        over = truth.snapshot()[1]
-    ut = observe(lister, over)
-    return {"limits_fixed": fixed, "over": over, "util": ut}
+        verdicts = truth.enforce(lister, grants, lister.pod)
+    over = {k for k, v in verdicts.items() if v.over}
+    decisions: dict = {}
+    ut = observe(lister, over, decisions)
+    published = publish_controls(lister, grants, decisions, verdicts, lease_s)
+    taken = escalation.step(verdicts, lister.pod) if escalation is not None else []
+    return {"limits_fixed": fixed, "over": over, "util": ut, "controls": published, "actions": taken,
+            "no_shim": {k for k, v in verdicts.items() if not v.shim_loaded}}
 
 
 def watch_and_feedback(lister: ContainerLister, stop: threading.Event, period: float = 5.0,
-                       pause: threading.Event | None = None, truth=None):
+                       pause: threading.Event | None = None, truth=None, escalation=None):
     """The 5 s loop; skipped while ``pause`` is set (a compute-partition apply
-    is in progress, cmd/vGPUmonitor/main.go:79-109)."""
+    is in progress, cmd/vGPUmonitor/main.go:79-109).  The control-file lease
+    covers four periods, so a paused or dead monitor releases its verdicts."""
     while not stop.wait(period):
         if pause is not None and pause.is_set():
             continue
         try:
-            feedback_pass(lister, truth)
+            feedback_pass(lister, truth, escalation, lease_s=max(DEFAULT_LEASE_S, 4 * period))
         except Exception:  # noqa: BLE001
             log.exception("feedback iteration failed")

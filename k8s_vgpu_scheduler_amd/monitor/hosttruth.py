@@ -1,39 +1,48 @@
-"""Host-truth HBM accounting for the shared regions (VERDICT r2 weak #3a).
+"""Host-truth HBM enforcement, driven by host-owned state.
 
-The shared region sits in a directory the container mounts read-write.  The
-shim's O(1) quota counter (``dev_used``) and the per-process slot totals live
-there, so a tenant that zeroes them -- or raises ``mem_limit`` -- allocates
-past its grant: the shim's verdict is only as good as the counter.
-``reconcile_limits`` (feedback.py) already restores the limits from the
-read-only grant file; this pass restores the USAGE from host truth.
+The shared region sits in a directory the container mounts read-write, and it
+only exists once the shim in the container creates it.  So this pass starts
+from what the HOST owns, not from the regions:
 
-Every monitor pass (the reference's 5 s feedback period,
-cmd/vGPUmonitor/feedback.go:136-165) recomputes each container's VRAM from
-what the kernel driver itself counts: KFD's ``vram_<gpu_id>`` of every host
-process of the container's pod (the cgroup names the pod UID -- the same
-``/proc`` scan that maps slot pids to host pids, hostpid.py), which a tenant
-cannot write.  Then, per container and device:
+* the grant files the device plugin's Allocate wrote under
+  ``$HOOK_PATH/vgpu/limits/<pod uid>_<container>.conf`` (read-only to the
+  container): which containers hold which GPUs, and their HBM grants;
+* KFD's per-process VRAM ``vram_<gpu_id>`` of every host process of the pod
+  (the cgroup names the pod UID, hostpid.py), which a tenant cannot write.
 
-  * ``dev_used`` is raised to the truth (never below it); slot totals whose
-    host pid is known are raised to that process's KFD total (the excess is
-    runtime memory, charged as context), so the metrics stay honest;
-  * a container whose truth exceeds its GRANT (the grant file, not the
-    region) by more than ``slack`` is blocked -- ``recent_kernel = -1``, the
-    shim parks its launches -- gets a ``VGPUMemoryOverGrant`` Warning event
-    and ``mivgpu_container_memory_over_grant 1``, until it is back under;
-    the raised ``dev_used`` makes its next allocation fail in the shim.
+Every pass (the reference's 5 s feedback period, cmd/vGPUmonitor/feedback.go:
+136-165), per granted container and device:
 
-Multi-container pods: a device used by one container of the pod gets the
-pod's total; otherwise each container is charged the KFD totals of its own
-slots' (validated) host pids, and VRAM held by pod processes outside every
-slot is charged to the pod as a whole: over the sum of the grants, every
-container of the pod on that device is blocked.
+* **truth** = the pod's KFD VRAM on that GPU (a container alone on the GPU in
+  its pod), or the VRAM of its own slots' host pids (several containers of
+  one pod share the GPU; VRAM of pod processes outside every slot is charged
+  to the pod as a whole);
+* **over grant** (truth > grant + slack): a ``VGPUMemoryOverGrant`` Warning
+  event, ``mivgpu_container_memory_over_grant 1``, and a block verdict the
+  feedback pass writes into the container's read-only control file
+  (monitor/control.py) -- the tenant cannot clear it by rewriting its region;
+* **shim not loaded** (the pod holds VRAM on the granted GPU but the
+  container has no shared region with a live process: its image ignored the
+  preload, or it deleted its region file): a ``VGPUShimNotLoaded`` Warning
+  event and ``mivgpu_container_shim_loaded 0``; such a container is enforced
+  from KFD alone (over grant -> the escalation of monitor/escalate.py);
+* **excess** (truth beyond the region's own counter -- all of the truth for a
+  container with no live region -- read before and after
+  the KFD reads so that an allocation in flight never counts, and published
+  only when two consecutive passes agree): written to the control file,
+  where the shim's quota check adds it -- a zeroed or stale counter cannot
+  buy headroom.
+
+The monitor never writes the counters the shim owns (``dev_used``, slot
+totals): the shim changes them with atomics, and a read-modify-write from
+another process could lose a concurrent reservation.
 """
 
 from __future__ import annotations
 
 import logging
 import threading
+from dataclasses import dataclass, field
 from pathlib import Path
 from typing import Callable
 
@@ -43,10 +52,64 @@ from .occupancy import KFD_ROOT
 log = logging.getLogger(__name__)
 
 OVER_GRANT_REASON = "VGPUMemoryOverGrant"
+SHIM_NOT_LOADED_REASON = "VGPUShimNotLoaded"
 
 
 def _uid_forms(pod_uid: str) -> tuple[str, str]:
     return pod_uid, pod_uid.replace("-", "_")
+
+
+@dataclass
+class Grant:
+    """One container's grant file (deviceplugin/allocate.py grant_text)."""
+    pod_uid: str
+    container: str
+    uuids: list[str]
+    mem: list[int]                  # bytes per container-local device (0 = unlimited)
+    path: str = ""
+    mtime: float = 0.0
+
+    @property
+    def key(self) -> str:
+        return f"{self.pod_uid}_{self.container}"
+
+
+def load_grants(limits_dir: Path | str) -> dict[str, Grant]:
+    """``{"<uid>_<ctr>": Grant}`` of every grant file under ``limits_dir``."""
+    from k8s_vgpu_scheduler_amd.deviceplugin.allocate import parse_grant
+
+    from .feedback import expected_region
+
+    out: dict[str, Grant] = {}
+    d = Path(limits_dir)
+    try:
+        files = sorted(d.glob("*.conf"))
+    except OSError:
+        return out
+    for f in files:
+        uid, sep, ctr = f.stem.partition("_")
+        if not sep or not uid or not ctr:
+            continue
+        try:
+            text = f.read_text()
+            mtime = f.stat().st_mtime
+        except OSError:
+            continue
+        g = parse_grant(text)
+        uuids = [u for u in (g.get("MIVGPU_DEVICE_UUIDS") or "").split(",") if u]
+        mem = expected_region(g)["mem_limit"][:max(1, len(uuids))]
+        out[f.stem] = Grant(uid, ctr, uuids, mem, str(f), mtime)
+    return out
+
+
+@dataclass
+class Verdict:
+    """What one pass found for one granted container."""
+    truth: dict[int, int] = field(default_factory=dict)      # device index -> bytes (KFD)
+    over: bool = False
+    shim_loaded: bool = True
+    excess: list[int] = field(default_factory=list)         # per device, published to the control file
+    pids: dict[int, list[int]] = field(default_factory=dict)  # device index -> host pids holding VRAM
 
 
 class HostTruth:
@@ -66,7 +129,12 @@ class HostTruth:
         self._mu = threading.Lock()
         self.truth: dict[tuple, int] = {}      # (pod_uid, container, dev index) -> bytes
         self.over: set[tuple] = set()          # (pod_uid, container) currently over their grant
-        self.corrections = 0
+        self.no_shim: set[tuple] = set()       # (pod_uid, container) holding VRAM with no live shim
+        self.verdicts: dict[tuple, Verdict] = {}
+        self.grants: dict[str, Grant] = {}
+        self._excess_prev: dict[tuple, int] = {}
+        self._suspect: set[tuple] = set()      # no live shim in the previous pass
+        self._reported: set[tuple] = set()     # (reason, pod_uid, container) with an event out
 
     # ------------------------------------------------------------ sources
     def vram(self, host_pid: int, gpu_id: int) -> int:
@@ -88,129 +156,152 @@ class HostTruth:
         return out
 
     # ------------------------------------------------------------- a pass
-    def enforce(self, lister, grants: dict | None = None) -> dict:
-        """One pass over every container of ``lister``.  ``grants``: optional
-        ``{(pod_uid, container): [limit bytes per device]}`` (the grant
-        files); absent -> the region's mem_limit.  Returns the truth map."""
-        containers = lister.list_containers()
-        if not containers:
-            with self._mu:
-                self.truth, self.over = {}, set()
-            return {}
+    def enforce(self, lister, grants: dict[str, Grant] | None = None, pod_info: Callable | None = None) -> dict:
+        """One pass.  ``grants``: the grant files (``load_grants``; default:
+        the ``limits`` directory next to the lister's containers directory).
+        ``pod_info``: ``pod_uid -> pod dict`` for event targets.  Returns
+        ``{(pod_uid, container): Verdict}``."""
+        if grants is None:
+            grants = load_grants(lister.base.parent / "limits")
+        regions = {f"{c.pod_uid}_{c.container}": c for c in lister.list_containers()}
         ids = self.gpu_ids() or {}
-        pods = self._pids_by_pod({c.pod_uid for c in containers})
-        # (pod, uuid) -> [(container, device index)]
+        pods = self._pids_by_pod({g.pod_uid for g in grants.values()})
+        # (pod, uuid) -> [(grant, device index)]
         users: dict[tuple, list] = {}
-        for c in containers:
-            r = c.region
-            for i in range(r.device_num()):
-                if r.is_valid_uuid(i) and r.uuid(i) in ids:
-                    users.setdefault((c.pod_uid, r.uuid(i)), []).append((c, i))
-        truth: dict[tuple, int] = {}
-        over: set[tuple] = set()
+        for g in grants.values():
+            for i, u in enumerate(g.uuids):
+                if u in ids:
+                    users.setdefault((g.pod_uid, u), []).append((g, i))
+        verdicts: dict[tuple, Verdict] = {}
+
+        def verdict(g: Grant) -> Verdict:
+            v = verdicts.get((g.pod_uid, g.container))
+            if v is None:
+                v = verdicts[(g.pod_uid, g.container)] = Verdict(excess=[0] * len(g.uuids))
+            return v
+
         for (uid, dev_uuid), lst in users.items():
             gid = ids[dev_uuid]
+            # the region's counters before the KFD reads (allocations in flight
+            # are reserved in the counter before the runtime allocates)
+            before = {g.key: self._dev_used(regions.get(g.key), i) for g, i in lst}
             pids = set(pods.get(uid, []))
             per_pid = {hp: self.vram(hp, gid) for hp in pids}
             pod_total = sum(per_pid.values())
+            after = {g.key: self._dev_used(regions.get(g.key), i) for g, i in lst}
             attributed = 0
             charged = []
-            for c, i in lst:
+            for g, i in lst:
+                c = regions.get(g.key)
+                live = c is not None and bool(c.region.active_procs())
                 if len(lst) == 1:
-                    t = pod_total
+                    own = {p: v for p, v in per_pid.items() if v > 0}
                 else:
-                    t = sum(per_pid.get(p.hostpid, 0) for p in c.region.active_procs() if p.hostpid in pids)
+                    mine = {s.hostpid for s in c.region.active_procs()} if live else set()
+                    own = {p: per_pid[p] for p in mine if per_pid.get(p, 0) > 0}
+                t = sum(own.values())
                 attributed += t
-                charged.append((c, i, t))
+                charged.append((g, i, c, live, t, own))
             grant_sum = 0
-            for c, i, t in charged:
-                key = (c.pod_uid, c.container)
-                g = self._grant(c, i, grants)
-                grant_sum += g
-                truth[(c.pod_uid, c.container, i)] = t
-                self._correct(c, i, t, per_pid if len(lst) == 1 else
-                              {p: v for p, v in per_pid.items()
-                               if p in {s.hostpid for s in c.region.active_procs()}})
-                if g and t > g + self.slack:
-                    over.add(key)
-                    self._report(c, i, t, g)
+            for g, i, c, live, t, own in charged:
+                v = verdict(g)
+                v.truth[i] = t
+                v.pids[i] = sorted(own)
+                gm = g.mem[i] if i < len(g.mem) else 0
+                grant_sum += gm
+                if gm and t > gm + self.slack:
+                    v.over = True
+                    self._report(OVER_GRANT_REASON, g, pod_info,
+                                 f"container {g.container} holds {t >> 20} MiB of HBM on device {i} (KFD), over "
+                                 f"its grant of {gm >> 20} MiB: launches blocked until it is back under")
+                holds = t > 0 if len(lst) == 1 else (pod_total - attributed > self.slack)
+                if not live and holds:
+                    v.shim_loaded = False
+                if live:
+                    counted = max(before.get(g.key, 0), after.get(g.key, 0))
+                    ex = max(0, t - counted)
+                    prev = self._excess_prev.get((g.key, i), 0)
+                    self._excess_prev[(g.key, i)] = ex
+                    pub = min(ex, prev)
+                    if pub > self.slack:
+                        v.excess[i] = pub
+                        log.warning("%s/%s dev %d: KFD %d MiB, region counts %d MiB: %d MiB charged to its quota "
+                                    "from host truth", g.pod_uid, g.container, i, t >> 20, counted >> 20, pub >> 20)
+                else:
+                    self._excess_prev.pop((g.key, i), None)
             # pod processes outside every slot (a hidden tenant process)
             if len(lst) > 1 and grant_sum and pod_total - attributed > self.slack and pod_total > grant_sum + self.slack:
-                for c, i, _ in charged:
-                    over.add((c.pod_uid, c.container))
-                    self._report(c, i, pod_total, grant_sum)
+                for g, i, *_ in charged:
+                    verdict(g).over = True
+                    self._report(OVER_GRANT_REASON, g, pod_info,
+                                 f"pod holds {pod_total >> 20} MiB of HBM on device {i} (KFD), over the "
+                                 f"{grant_sum >> 20} MiB granted to its containers: launches blocked")
+        # a container's shim creates its region at its first HIP call, a moment
+        # after the runtime took its first VRAM: no live shim is a verdict when
+        # two passes in a row saw it (or the container is over its grant)
+        suspect = {k for k, v in verdicts.items() if not v.shim_loaded}
+        for k in suspect:
+            if k not in self._suspect and not verdicts[k].over:
+                verdicts[k].shim_loaded = True
+        self._suspect = suspect
+        for (uid, ctr), v in verdicts.items():
+            if not v.shim_loaded:
+                # no region to compare with: a shim that is loaded after all
+                # (its region file unlinked) is charged everything KFD sees
+                for i, t in v.truth.items():
+                    if i < len(v.excess) and t > self.slack:
+                        v.excess[i] = t
+                g = grants[f"{uid}_{ctr}"]
+                self._report(SHIM_NOT_LOADED_REASON, g, pod_info,
+                             f"container {ctr} holds HBM on its granted GPU but no process of it runs under "
+                             f"libmivgpu.so (the image ignored the preload, or its region file was removed): "
+                             f"enforced from host truth only")
         with self._mu:
-            newly_clear = self.over - over
-            self.truth, self.over = truth, over
-        for c in containers:
-            key = (c.pod_uid, c.container)
-            if key in over:
-                c.region.set_recent_kernel(-1)
-            elif key in newly_clear:
-                log.info("%s/%s: back under its grant; unblocked", c.pod_uid, c.container)
-                if c.region.recent_kernel() < 0:
-                    c.region.set_recent_kernel(0)
-        return truth
+            self.grants = dict(grants)
+            self.verdicts = verdicts
+            self.truth = {(u, c, i): t for (u, c), v in verdicts.items() for i, t in v.truth.items()}
+            self.over = {k for k, v in verdicts.items() if v.over}
+            self.no_shim = {k for k, v in verdicts.items() if not v.shim_loaded}
+            # an event again once the condition cleared and came back
+            self._reported = {r for r in self._reported
+                              if (r[0] == OVER_GRANT_REASON and (r[1], r[2]) in self.over)
+                              or (r[0] == SHIM_NOT_LOADED_REASON and (r[1], r[2]) in self.no_shim)}
+            live_keys = {g.key for g in grants.values()}
+            self._excess_prev = {k: x for k, x in self._excess_prev.items() if k[0] in live_keys}
+        return verdicts
 
-    def _grant(self, c, i: int, grants: dict | None) -> int:
-        if grants is not None:
-            g = grants.get((c.pod_uid, c.container))
-            if g is not None and i < len(g):
-                return int(g[i])
-        return int(c.region.r.mem_limit[i])
+    @staticmethod
+    def _dev_used(c, i: int) -> int:
+        if c is None:
+            return 0
+        try:
+            return int(c.region.r.dev_used[i])
+        except (AttributeError, IndexError, ValueError):
+            return 0
 
-    def _correct(self, c, i: int, t: int, per_pid: dict):
-        r = c.region.r
-        if int(r.dev_used[i]) < t:
-            log.warning("%s/%s dev %d: region counts %d B in use, KFD %d B; corrected", c.pod_uid, c.container, i,
-                        int(r.dev_used[i]), t)
-            r.dev_used[i] = t
-            self.corrections += 1
-        for s in c.region.active_procs():
-            v = per_pid.get(s.hostpid) if s.hostpid > 0 else None
-            if v is None:
-                continue
-            m = s.used[i]
-            if int(m.total) < v:
-                m.context = int(m.context) + (v - int(m.total))
-                m.total = v
-                self.corrections += 1
-
-    def _report(self, c, i: int, t: int, g: int):
-        key = (c.pod_uid, c.container)
+    def _report(self, reason: str, g: Grant, pod_info, msg: str):
+        key = (reason, g.pod_uid, g.container)
         with self._mu:
-            was = key in self.over
-        msg = (f"container {c.container} holds {t >> 20} MiB of HBM on device {i} (KFD), over its grant of "
-               f"{g >> 20} MiB: launches blocked until it is back under")
-        if not was:
-            log.warning("%s/%s: %s", c.pod_uid, c.container, msg)
-            if self.events is not None:
-                self.events.event({"kind": "Pod", "metadata": {"name": c.pod_name or c.pod_uid,
-                                                               "namespace": c.namespace or "default",
-                                                               "uid": c.pod_uid}},
-                                  "Warning", OVER_GRANT_REASON, msg)
+            if key in self._reported:
+                return
+            self._reported.add(key)
+        log.warning("%s/%s: %s", g.pod_uid, g.container, msg)
+        if self.events is not None:
+            pod = pod_info(g.pod_uid) if pod_info is not None else None
+            md = (pod or {}).get("metadata") or {}
+            self.events.event({"kind": "Pod", "metadata": {"name": md.get("name") or g.pod_uid,
+                                                           "namespace": md.get("namespace") or "default",
+                                                           "uid": g.pod_uid}},
+                              "Warning", reason, msg)
 
     def snapshot(self) -> tuple[dict, set]:
         with self._mu:
             return dict(self.truth), set(self.over)
 
-
-def grants_from_files(lister) -> dict:
-    """``{(pod_uid, container): [limit bytes per device]}`` from the grant
-    files next to the containers directory (deviceplugin/allocate.py)."""
-    from k8s_vgpu_scheduler_amd.deviceplugin.allocate import parse_grant
-
-    from .feedback import expected_region
-
-    out = {}
-    limits_dir = lister.base.parent / "limits"
-    for c in lister.list_containers():
-        try:
-            grant = parse_grant((limits_dir / f"{c.pod_uid}_{c.container}.conf").read_text())
-        except OSError:
-            continue
-        out[(c.pod_uid, c.container)] = expected_region(grant)["mem_limit"]
-    return out
+    def state(self) -> dict:
+        with self._mu:
+            return {"truth": dict(self.truth), "over": set(self.over), "no_shim": set(self.no_shim),
+                    "verdicts": dict(self.verdicts), "grants": dict(self.grants)}
 
 
 def kfd_gpu_ids(backend, kfd_root: Path | str = KFD_ROOT) -> Callable[[], dict]:
@@ -243,4 +334,5 @@ def single_gpu_ids(uuid: str, kfd_root: Path | str = KFD_ROOT) -> dict:
     return {}
 
 
-__all__ = ["HostTruth", "grants_from_files", "kfd_gpu_ids", "single_gpu_ids", "OVER_GRANT_REASON"]
+__all__ = ["HostTruth", "Grant", "Verdict", "load_grants", "kfd_gpu_ids", "single_gpu_ids", "OVER_GRANT_REASON",
+           "SHIM_NOT_LOADED_REASON"]

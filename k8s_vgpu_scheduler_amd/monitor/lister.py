@@ -20,6 +20,7 @@ from typing import Callable
 
 from k8s_vgpu_scheduler_amd.utils.nodelock import parse_go_duration
 
+from .control import ControlSet
 from .region import SharedRegion
 
 log = logging.getLogger(__name__)
@@ -56,6 +57,14 @@ class ContainerLister:
         self.containers: dict[str, ContainerUsage] = {}
         self._mu = threading.Lock()
         self._last_gc = 0.0
+        self._pods: dict[str, dict] = {}
+        # the host-owned control files next to the regions (monitor/control.py)
+        self.controls = ControlSet(str(self.base.parent / "control"))
+
+    def pod(self, uid: str) -> dict | None:
+        """The pod with ``uid`` as of the last ``update()`` (None if unknown)."""
+        with self._mu:
+            return self._pods.get(uid)
 
     def _pod_index(self) -> dict[str, dict] | None:
         if self.pods is None:
@@ -67,9 +76,12 @@ class ContainerLister:
             return None
 
     def update(self):
+        pods = self._pod_index()
+        if pods is not None:
+            with self._mu:
+                self._pods = pods
         if not self.base.exists():
             return
-        pods = self._pod_index()
         now = time.time()
         seen = set()
         for d in self.base.iterdir():
@@ -91,10 +103,13 @@ class ContainerLister:
                 if age > self.resync:
                     log.info("removing stale container dir %s", d)
                     shutil.rmtree(d, ignore_errors=True)
-                    try:   # the container's grant file (deviceplugin/allocate.py)
-                        (self.base.parent / "limits" / f"{d.name}.conf").unlink()
-                    except OSError:
-                        pass
+                    # the container's grant and control files (deviceplugin/allocate.py)
+                    for f in (self.base.parent / "limits" / f"{d.name}.conf",
+                              self.base.parent / "control" / f"{d.name}.ctl"):
+                        try:
+                            f.unlink()
+                        except OSError:
+                            pass
                 continue
             with self._mu:
                 known = d.name in self.containers

@@ -28,9 +28,10 @@ LEGACY_HOST_LABELS = ["nodeid", "deviceidx", "deviceuuid", "devicetype"]
 
 class MonitorCollector:
     def __init__(self, lister, backend=None, node_name: str = "", occupancy=None, legacy: bool = False,
-                 truth=None):
+                 truth=None, escalation=None):
         self.lister = lister
         self.truth = truth        # monitor.hosttruth.HostTruth (host-truth HBM usage) or None
+        self.escalation = escalation   # monitor.escalate.OverGrantPolicy or None
         self.backend = backend
         self.node = node_name
         self.occ = occupancy      # monitor.occupancy.OccupancySampler (hostPID view) or None
@@ -124,7 +125,12 @@ class MonitorCollector:
         over_g = GaugeMetricFamily("mivgpu_container_memory_over_grant",
                                    "1 while the container's host-truth HBM exceeds its grant (launches blocked)",
                                    labels=CTR_LABELS)
-        truth, over = self.truth.snapshot() if self.truth is not None else ({}, set())
+        shim = GaugeMetricFamily("mivgpu_container_shim_loaded",
+                                 "0 while a granted container holds HBM on its GPU with no process under "
+                                 "libmivgpu.so (host truth; enforced from KFD alone), else 1", labels=CTR_LABELS)
+        st = self.truth.state() if self.truth is not None else {"truth": {}, "over": set(), "no_shim": set(),
+                                                                  "grants": {}}
+        truth, over, no_shim = st["truth"], st["over"], st["no_shim"]
         l_used = GaugeMetricFamily("vGPU_device_memory_usage_in_bytes", "vGPU device usage", labels=LEGACY_CTR_LABELS)
         l_limit = GaugeMetricFamily("vGPU_device_memory_limit_in_bytes", "vGPU device limit",
                                     labels=LEGACY_CTR_LABELS)
@@ -135,7 +141,9 @@ class MonitorCollector:
         l_lastk = GaugeMetricFamily("Device_last_kernel_of_container", "Container device last kernel description",
                                     labels=LEGACY_CTR_LABELS)
         now = time.time()
+        seen = set()
         for c in self.lister.list_containers():
+            seen.add((c.pod_uid, c.container))
             r = c.region
             r.refresh()
             for i in range(r.device_num()):
@@ -182,9 +190,32 @@ class MonitorCollector:
                 if tb is not None:
                     host_b.add_metric(lab, float(tb))
                     over_g.add_metric(lab, 1.0 if (c.pod_uid, c.container) in over else 0.0)
+                    shim.add_metric(lab, 0.0 if (c.pod_uid, c.container) in no_shim else 1.0)
+        # granted containers without a shared region (no shim ever started in
+        # them, or the region was removed): the host-truth rows alone
+        for g in st["grants"].values():
+            if (g.pod_uid, g.container) in seen:
+                continue
+            md = (self.lister.pod(g.pod_uid) or {}).get("metadata") or {}
+            for i, u in enumerate(g.uuids):
+                tb = truth.get((g.pod_uid, g.container, i))
+                if tb is None:
+                    continue
+                lab = [md.get("namespace", ""), md.get("name", ""), g.container, str(i), u]
+                host_b.add_metric(lab, float(tb))
+                limit.add_metric(lab, float(g.mem[i] if i < len(g.mem) else 0))
+                over_g.add_metric(lab, 1.0 if (g.pod_uid, g.container) in over else 0.0)
+                shim.add_metric(lab, 0.0 if (g.pod_uid, g.container) in no_shim else 1.0)
         yield from (used, limit, dmem, dutil, lastk, ctx, mod, buf, busy, held, cumask, part, mig, share, occw)
         if self.truth is not None:
-            yield from (host_b, over_g)
+            yield from (host_b, over_g, shim)
+        if self.escalation is not None:
+            acts = CounterMetricFamily("mivgpu_over_grant_actions", "Over-grant escalations taken (evict / kill)",
+                                       labels=["node", "action"])
+            for a, n in self.escalation.actions.items():
+                if a != "block":
+                    acts.add_metric([self.node, a], float(n))
+            yield acts
         if self.legacy:
             yield from (l_used, l_limit, l_desc, l_cutil, l_lastk)
 

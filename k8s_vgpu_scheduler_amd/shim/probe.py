@@ -473,15 +473,26 @@ def child_queues(args) -> dict:
 
 
 def child_tamper(args) -> dict:
-    """A hostile tenant: rewrites its own shared region (zeroes dev_used and
-    its slot totals, raises mem_limit to 1 TiB), allocates past its grant,
-    then -- after the parent ran one monitor pass -- tries again."""
+    """A hostile tenant under a 4 GiB grant.  It maps its
+    own shared region, optionally deletes the region file (``--unlink``: the
+    monitor then sees no region at all), zeroes the usage counters and
+    allocates past its grant.  After the parent's monitor pass(es) it keeps
+    rewriting the region (clearing the block flag, zeroing the counters) from
+    a thread while it allocates again and launches a kernel: the verdicts in
+    the read-only control file must hold anyway."""
+    import threading
+
     import torch
 
     from k8s_vgpu_scheduler_amd.monitor.region import SharedRegion
 
     x = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    x.fill_(1)
+    torch.cuda.synchronize()
+    kfd_pid = _kfd_pid()
     reg = SharedRegion(args.out)
+    if args.unlink:
+        os.unlink(args.out)
     reg.r.dev_used[0] = 0
     reg.r.mem_limit[0] = 1 << 40
     for p in reg.active_procs():
@@ -495,18 +506,32 @@ def child_tamper(args) -> dict:
         first = "allocated"
     except torch.OutOfMemoryError:
         first = "oom"
-    print("TAMPERED " + json.dumps({"first": first, "kfd_pid": _kfd_pid()}), flush=True)
-    sys.stdin.readline()                      # the parent's monitor pass
-    rk = int(reg.r.recent_kernel)
+    print("TAMPERED " + json.dumps({"first": first, "kfd_pid": kfd_pid}), flush=True)
+    sys.stdin.readline()                      # the parent's monitor pass(es)
+    stop = threading.Event()
+
+    def rewrite():                            # "I am not blocked, I use nothing"
+        while not stop.is_set():
+            reg.r.recent_kernel = 0
+            reg.r.dev_used[0] = 0
+            time.sleep(0.002)
+    th = threading.Thread(target=rewrite, daemon=True)
+    th.start()
+    time.sleep(0.05)
     try:
         z = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
         second = "allocated"
         del z
     except torch.OutOfMemoryError:
         second = "oom"
-    out = {"mode": "tamper", "first": first, "second": second, "recent_kernel": rk,
-           "mem_limit_mib": int(reg.r.mem_limit[0]) >> 20, "dev_used_mib": int(reg.r.dev_used[0]) >> 20}
-    reg.r.recent_kernel = 0                   # let the exit path run
+    t0 = time.time()
+    w = torch.ones(1 << 16, device="cuda") + 1         # parked while the control block holds
+    total = float(w.sum().item())
+    parked_s = time.time() - t0
+    stop.set()
+    th.join()
+    out = {"mode": "tamper", "first": first, "second": second, "parked_s": round(parked_s, 3),
+           "sum": total, "unlinked": bool(args.unlink)}
     reg.close()
     del x, y
     return out
@@ -567,6 +592,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--hwid", action="store_true")
+    ap.add_argument("--unlink", action="store_true", help="child tamper: delete the region file first")
     ap.add_argument("--keep-env", action="store_true", help="child queues: do not raise GPU_MAX_HW_QUEUES")
     ap.add_argument("--hostile", action="store_true",
                     help="child: rewrite the grant in the environment before the runtime starts "

@@ -125,7 +125,12 @@ def test_region_contents_visible_to_monitor(native_build, tmp_path):
     assert reg.memory_limit(0) == 2 << 30
     assert reg.r.cu_limit[0] == 25 and reg.r.cu_mask_count[0] == 64
     assert reg.priority() == 1
-    assert reg.recent_kernel() == 2       # set by the launch hook
+    # set off the launch path by the housekeeping thread, at once for the first launch
+    t0 = time.time()
+    while reg.recent_kernel() != 2 and time.time() - t0 < 2.0:
+        time.sleep(0.01)
+    assert reg.recent_kernel() == 2
+    assert reg.r.procs[0].util[0].launches == 5 and reg.last_kernel_time() > 0
     assert reg.pids() == [p.pid]
     reg.close()
     p.wait(timeout=30)

@@ -145,56 +145,104 @@ def test_queue_cap_protects_masked_neighbours(tmp):
         assert b >= 0.97 * a, (honest, hostile)
 
 
-def test_region_tampering_caught_by_host_truth_within_one_pass(tmp):
-    """VERDICT r2 weak #3a: a tenant zeroes dev_used and its slot totals,
-    raises mem_limit, and allocates past its 4 GiB grant.  One monitor pass
-    (limits from the grant file, usage from KFD) blocks it, and its next
-    allocation fails."""
+def _tamper_round(tmp, unlink: bool, passes: int):
+    """A hostile tenant under a 4 GiB grant (probe child ``tamper``) against
+    ``passes`` monitor passes with the evict escalation and a fake API server.
+    Returns (pass results, control snapshot, evictions, child result)."""
     import subprocess
     import sys
+    import time
 
+    from k8s_vgpu_scheduler_amd.e2e.apiserver import FakeApiServer
+    from k8s_vgpu_scheduler_amd.k8s.fake import make_pod
+    from k8s_vgpu_scheduler_amd.k8s.rest import RestClient
     from k8s_vgpu_scheduler_amd.monitor import feedback
+    from k8s_vgpu_scheduler_amd.monitor.control import ControlFile, control_host_path, create
+    from k8s_vgpu_scheduler_amd.monitor.escalate import OverGrantPolicy
     from k8s_vgpu_scheduler_amd.monitor.hosttruth import HostTruth, single_gpu_ids
     from k8s_vgpu_scheduler_amd.monitor.lister import ContainerLister
     from k8s_vgpu_scheduler_amd.shim import shim_env
 
-    hook = os.path.join(tmp, "hook")
+    hook = os.path.join(tmp, f"hook-{int(unlink)}")
     cdir = os.path.join(hook, "vgpu", "containers", "uid-t_main")
     ldir = os.path.join(hook, "vgpu", "limits")
     os.makedirs(cdir)
     os.makedirs(ldir)
     cache = os.path.join(cdir, "r.cache")
+    ctl = control_host_path(hook, "uid-t", "main")
+    create(ctl)
     grant = os.path.join(ldir, "uid-t_main.conf")
     with open(grant, "w") as f:
-        f.write(f"HIP_DEVICE_MEMORY_LIMIT_0=4096m\nMIVGPU_SHARED_CACHE={cache}\nMIVGPU_DEVICE_UUIDS=GPU-tamper\n")
+        f.write(f"HIP_DEVICE_MEMORY_LIMIT_0=4096m\nMIVGPU_SHARED_CACHE={cache}\nMIVGPU_DEVICE_UUIDS=GPU-tamper\n"
+                f"MIVGPU_CONTROL_FILE={ctl}\n")
     env = dict(os.environ)
     env.update(shim_env())
     env["MIVGPU_LIMITS_FILE"] = grant
-    p = subprocess.Popen([sys.executable, "-m", "k8s_vgpu_scheduler_amd.shim.probe", "--child", "tamper",
-                          "--out", cache, "--oom-probe-mib", "5000"], env=env, stdin=subprocess.PIPE,
-                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    api = FakeApiServer().start()
+    pod = make_pod("t", "default")
+    pod["metadata"]["uid"] = "uid-t"
+    api.cluster.create("pods", pod)
+    args = [sys.executable, "-m", "k8s_vgpu_scheduler_amd.shim.probe", "--child", "tamper", "--out", cache,
+            "--oom-probe-mib", "3500"] + (["--unlink"] if unlink else [])
+    p = subprocess.Popen(args, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True)
+    outs = []
+    se = ""
     try:
         line = p.stdout.readline()
         assert line.startswith("TAMPERED "), (line, p.stderr.read()[-2000:] if p.poll() is not None else "")
         first = json.loads(line[9:])
-        assert first["first"] == "allocated"        # the rewrite let it past the grant
-        lister = ContainerLister(hook, lambda: [{"metadata": {"uid": "uid-t", "name": "t", "namespace": "d"}}],
-                                 resync_interval=3600)
+        lister = ContainerLister(hook, lambda: api.cluster.list("pods"), resync_interval=3600)
         # the pod's processes as a hostPID monitor's cgroup scan finds them: the
         # box may run this test in a pid namespace, so KFD's (host) pid of the
         # child -- the one its shim found for itself -- stands in
         truth = HostTruth(lambda: single_gpu_ids("GPU-tamper"), pod_pids=lambda uid: [first["kfd_pid"]])
-        out = feedback.feedback_pass(lister, truth)
-        snap = truth.snapshot()
+        pol = OverGrantPolicy("evict", passes=passes, client=RestClient(api.url))
+        for _ in range(passes):
+            outs.append(feedback.feedback_pass(lister, truth, pol))
+        snap = ControlFile(ctl).snapshot()
         p.stdin.write("go\n")
         p.stdin.flush()
+        time.sleep(3.0)                       # the tenant rewrites its region meanwhile
+        ControlFile(ctl).publish(block=False, switch=False, over=False)   # the verdict lifted
         so, se = p.communicate(timeout=120)
     finally:
         if p.poll() is None:
             p.kill()
+        api.stop()
+    assert p.returncode == 0, se[-3000:]
     res = json.loads([x for x in so.splitlines() if x.startswith("{")][-1])
-    print(json.dumps({"pass": {"limits_fixed": out["limits_fixed"], "over": sorted(out["over"])},
-                      "truth_mib": {str(k): v >> 20 for k, v in snap[0].items()}, "child": res}))
-    assert ("uid-t", "main") in out["over"]
-    assert res["recent_kernel"] == -1 and res["mem_limit_mib"] == 4096
-    assert res["dev_used_mib"] > 4096 and res["second"] == "oom"
+    res["first_alloc"] = first["first"]
+    return outs, snap, list(api.cluster.evictions), res
+
+
+def test_tenant_without_a_region_reported_within_one_pass(tmp):
+    """a tenant that deletes its region file before the
+    first pass, zeroes its counters and allocates past its 4 GiB grant is
+    reported (over grant + shim not loaded) by ONE pass, evicted through the
+    API server, and -- rewriting its region all along -- cannot allocate
+    again or launch while the control-file verdict holds."""
+    outs, snap, evictions, res = _tamper_round(tmp, unlink=True, passes=1)
+    print(json.dumps({"over": sorted(outs[0]["over"]), "no_shim": sorted(outs[0]["no_shim"]),
+                      "control": {k: snap[k] for k in ("block", "over_grant")},
+                      "excess_mib": snap["host_excess"][0] >> 20, "evictions": evictions, "child": res}))
+    assert res["first_alloc"] == "allocated"          # the counter rewrite let it past the grant
+    assert ("uid-t", "main") in outs[0]["over"] and ("uid-t", "main") in outs[0]["no_shim"]
+    assert evictions == [("default", "t")]
+    assert snap["block"] == 1 and snap["host_excess"][0] > 4 << 30
+    assert res["second"] == "oom" and res["parked_s"] >= 2.5
+
+
+def test_tenant_rewriting_its_region_cannot_unblock_itself(tmp):
+    """The region kept: two passes (the excess needs two that agree) block
+    it and charge the KFD excess; the tenant keeps clearing its region's
+    block flag and usage counter, and stays blocked and out of headroom."""
+    outs, snap, evictions, res = _tamper_round(tmp, unlink=False, passes=2)
+    print(json.dumps({"over": sorted(outs[-1]["over"]), "control": {k: snap[k] for k in ("block", "over_grant")},
+                      "excess_mib": snap["host_excess"][0] >> 20, "evictions": evictions, "child": res}))
+    assert res["first_alloc"] == "allocated"
+    assert ("uid-t", "main") in outs[-1]["over"] and not outs[-1]["no_shim"]
+    # the excess: the 1 GiB its counter rewrite hid before the passes
+    assert snap["block"] == 1 and snap["over_grant"] == 1 and snap["host_excess"][0] >= 768 << 20
+    assert evictions == [("default", "t")]
+    assert res["second"] == "oom" and res["parked_s"] >= 2.5
