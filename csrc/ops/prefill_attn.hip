@@ -1,0 +1,237 @@
+// Causal GQA flash attention for prompt prefill (gfx950, MFMA 32x32x16 bf16).
+//
+// The reference's benchmark serves Qwen3-8B with --max-model-len 8192
+// (benchmarks/ai-benchmark/Dockerfile:7-9); a prompt of that length through
+// two batched fp32 GEMMs materialised 8192 x 8192 scores per head group (8.6 GB
+// per layer).  This kernel never materialises them: per 32-row query block it
+// walks the 32-key tiles up to the diagonal with an online softmax.
+//
+//   q   [Hkv][G][L][128]  (head-grouped: row g*L + l of kv head hk = q head hk*G+g)
+//   k,v [Hkv][L][128]
+//   out [L][Hq*128]       (o_proj's input layout)
+//
+// grid = (ceil(L/32) query blocks, heaviest first; Hkv), G waves per workgroup:
+// wave g takes q head hk*G + g over the block's 32 positions, so the G waves
+// share every K/V tile the workgroup stages in LDS.  Per 32-key tile a wave
+// runs 16 MFMAs:
+//   S^T (32 keys x 32 q) = K . Q^T       8 k-steps over D; the scores of query
+//       column r sit on lanes r and r+32 (16 keys each): the row max and the
+//       exponentials stay lane-local (one cross-half exchange for the max);
+//   O^T (128 x 32 q) += V^T . P^T        4 d-blocks x 2 k-steps; P^T is the
+//       score accumulator converted to bf16 in place (its rows are the
+//       reduction index: no lane movement, cdna_hip_programming.md section 3),
+//       V^T comes from the row-major V tile through ds_read_b64_tr_b16.
+// LDS (32 KB, double-buffered; the next tile's loads are in flight during
+// the current tile's MFMAs): K rows with the 16-byte chunk XOR (row & 15) --
+// conflict-free row reads for 16 distinct rows per 16-lane group; V rows with
+// chunk ^ ((row & 3) << 2) -- the 4 rows of a transposed read land in 4
+// different 64-byte slots, conflict-free.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef uint16_t bf16_t;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) short i16x4_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+constexpr int FA_D = 128;
+constexpr int FA_BQ = 32;    // query rows per wave
+constexpr int FA_BK = 32;    // keys per tile
+constexpr int FA_TILE = FA_BK * FA_D;     // elements per K (or V) tile
+constexpr int FA_CHUNKS = FA_TILE / 8;    // 16-byte chunks per tile
+
+__device__ __forceinline__ int k_off(int row, int ch) { return row * FA_D + ((ch ^ (row & 15)) << 3); }
+__device__ __forceinline__ int v_off(int row, int ch) { return row * FA_D + ((ch ^ ((row & 3) << 2)) << 3); }
+
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even (finite inputs)
+  return (bf16_t)(u >> 16);
+}
+
+template <int G>
+__global__ void __launch_bounds__(G * 64)
+prefill_flash_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                     bf16_t* __restrict__ out, int L, int Hq, float scale_log2) {
+  constexpr int NT = G * 64;
+  constexpr int PER = FA_CHUNKS / NT;      // 16-byte chunks per thread per tile (K and V each)
+  static_assert(PER * NT == FA_CHUNKS, "G must divide 8");
+  __shared__ __attribute__((aligned(16))) bf16_t ks[2][FA_TILE];
+  __shared__ __attribute__((aligned(16))) bf16_t vs[2][FA_TILE];
+
+  const int nqb = (L + FA_BQ - 1) / FA_BQ;
+  const int qb = nqb - 1 - (int)blockIdx.x;       // heaviest (longest) blocks first
+  const int hk = blockIdx.y;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int l0 = qb * FA_BQ;
+  const int ntiles = qb + 1;                      // keys 0 .. l0+31 (the last tile is the diagonal)
+
+  const bf16_t* kb = k + (size_t)hk * L * FA_D;
+  const bf16_t* vb = v + (size_t)hk * L * FA_D;
+
+  // Q^T fragments (B operand of S^T = K.Q^T): lane holds Q[l0+r][16s + 8h .. +8]
+  bf16x8_t qf[8];
+  {
+    const int qrow = min(l0 + r, L - 1);
+    const bf16_t* qp = q + (((size_t)hk * G + w) * L + qrow) * FA_D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8_t*>(qp + 16 * s);
+  }
+
+  // tile staging: chunk c = t + i*NT -> row c >> 4, 16-byte chunk c & 15
+  // (16 consecutive threads read one 256-byte key row: coalesced)
+  uint4 kreg[PER], vreg[PER];
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = t + i * NT;
+      const int row = min(kt * FA_BK + (c >> 4), L - 1);   // rows past L: masked (causal)
+      kreg[i] = *reinterpret_cast<const uint4*>(kb + (size_t)row * FA_D + (c & 15) * 8);
+      vreg[i] = *reinterpret_cast<const uint4*>(vb + (size_t)row * FA_D + (c & 15) * 8);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = t + i * NT;
+      *reinterpret_cast<uint4*>(&ks[buf][k_off(c >> 4, c & 15)]) = kreg[i];
+      *reinterpret_cast<uint4*>(&vs[buf][v_off(c >> 4, c & 15)]) = vreg[i];
+    }
+  };
+
+  f32x16_t o[4];
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[dc][i] = 0.f;
+  float m = -INFINITY, lsum = 0.f;
+  const int qpos = l0 + r;
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < ntiles) load_tile(kt + 1);     // in flight during this tile's MFMAs
+
+    // ---- S^T = K . Q^T (32 keys x 32 queries)
+    f32x16_t s;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[i] = 0.f;
+    const bf16_t* kt_lds = ks[buf];
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&kt_lds[k_off(r, 2 * st + h)]);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[st], s, 0, 0, 0);
+    }
+
+    // ---- online softmax (query column r: lanes r and r+32 hold 16 keys each)
+    const int key0 = kt * FA_BK + 4 * h;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = key0 + (i & 3) + 8 * (i >> 2);
+      const float x = key <= qpos ? s[i] * scale_log2 : -INFINITY;
+      s[i] = x;
+      mx = fmaxf(mx, x);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx);
+    const float alpha = exp2f(m - mnew);          // 0 on the first tile (m = -inf)
+    m = mnew;
+    float psum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = exp2f(s[i] - mnew);
+      s[i] = p;
+      psum += p;
+    }
+    lsum = lsum * alpha + psum;
+#pragma unroll
+    for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[dc][i] *= alpha;
+
+    // P^T as the B operand: registers 8u .. 8u+7 are the fragment of k-step u
+    bf16x8_t pf[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pf[u][j] = (__bf16)s[8 * u + j];
+
+    // ---- O^T += V^T . P^T; the A operand (V^T[d][key]) through transposed reads:
+    // lane 4q'+p' of its 16-lane group gives the address of key row q' of the
+    // group's 4-key block, columns 4p' .. 4p'+3 of its 16-column block
+    const bf16_t* vt_lds = vs[buf];
+    const int gi = lane & 15, qq = gi >> 2, pp = gi & 3;
+    const int colblk = 16 * ((lane >> 4) & 1);
+#pragma unroll
+    for (int dc = 0; dc < 4; ++dc) {
+      const int col = 32 * dc + colblk + 4 * pp;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int row_lo = 16 * u + 4 * h + qq, row_hi = row_lo + 8;
+        const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) i16x4_t*)(&vt_lds[v_off(row_lo, col >> 3) + (col & 7)]));
+        const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) i16x4_t*)(&vt_lds[v_off(row_hi, col >> 3) + (col & 7)]));
+        bf16x8_t a;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] = __builtin_bit_cast(__bf16, lo[j]);
+          a[4 + j] = __builtin_bit_cast(__bf16, hi[j]);
+        }
+        o[dc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pf[u], o[dc], 0, 0, 0);
+      }
+    }
+
+    if (kt + 1 < ntiles) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- normalise and store: O^T reg i of block dc is d = 32dc + (i&3) + 8(i>>2) + 4h
+  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  const float inv = 1.f / ltot;
+  if (qpos < L) {
+    bf16_t* op = out + (size_t)qpos * Hq * FA_D + (size_t)(hk * G + w) * FA_D;
+#pragma unroll
+    for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+      for (int i4 = 0; i4 < 4; ++i4) {
+        const int d = 32 * dc + 8 * i4 + 4 * h;
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(o[dc][4 * i4 + 0] * inv) | ((uint32_t)f2bf(o[dc][4 * i4 + 1] * inv) << 16);
+        pk.y = (uint32_t)f2bf(o[dc][4 * i4 + 2] * inv) | ((uint32_t)f2bf(o[dc][4 * i4 + 3] * inv) << 16);
+        *reinterpret_cast<uint2*>(op + d) = pk;
+      }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Causal prefill attention of one sequence of L positions (q head-grouped, see
+// above).  scale: the softmax scale (1/sqrt(D)).  G = Hq / Hkv in {1, 2, 4, 8}.
+int mivgpu_prefill_attention(const void* q, const void* k, const void* v, void* out, int L, int Hq, int Hkv,
+                             int head_dim, float scale, hipStream_t s) {
+  if (head_dim != FA_D || L <= 0 || Hkv <= 0 || Hq % Hkv) return -1;
+  const int G = Hq / Hkv;
+  const dim3 grid((L + FA_BQ - 1) / FA_BQ, Hkv);
+  const float sl2 = scale * 1.4426950408889634f;
+  const bf16_t *qq = (const bf16_t*)q, *kk = (const bf16_t*)k, *vv = (const bf16_t*)v;
+  bf16_t* oo = (bf16_t*)out;
+  switch (G) {
+    case 1: hipLaunchKernelGGL(prefill_flash_kernel<1>, grid, dim3(64), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
+    case 2: hipLaunchKernelGGL(prefill_flash_kernel<2>, grid, dim3(128), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
+    case 4: hipLaunchKernelGGL(prefill_flash_kernel<4>, grid, dim3(256), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
+    case 8: hipLaunchKernelGGL(prefill_flash_kernel<8>, grid, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -44,6 +44,7 @@ def lib():
         L.mivgpu_prefill_qk_norm_rope_kv.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, f, f,
                                                      vp]
         L.mivgpu_decode_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, f, vp]
+        L.mivgpu_prefill_attention.argtypes = [vp, vp, vp, vp, i, i, i, i, f, vp]
         L.mivgpu_decode_attention_fused.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i,
                                                      i, f, f, f, i, vp]
         L.mivgpu_skinny_gemm_norm_xcomb.argtypes = [vp, vp, vp, vp, i, i, i, i, vp, i, i, i, i, i, i, i, vp, vp,
@@ -66,7 +67,7 @@ def lib():
                    "mivgpu_skinny_max_m", "mivgpu_skinny_plan", "mivgpu_mfma_burn",
                    "mivgpu_stream_copy", "mivgpu_stream_read", "mivgpu_ops_visible_cus",
                    "mivgpu_ops_kv_packed", "mivgpu_decode_attention_fused", "mivgpu_skinny_gemm_norm",
-                   "mivgpu_prefill_qk_norm_rope_kv"):
+                   "mivgpu_prefill_qk_norm_rope_kv", "mivgpu_prefill_attention"):
             getattr(L, fn).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -174,6 +175,29 @@ def qk_norm_rope_kv(qkv, q_norm_w, k_norm_w, pos, q_out, k_cache, v_cache, n_q_h
     _check(lib().mivgpu_qk_norm_rope_kv(_p(qkv), _p(q_norm_w), _p(k_norm_w), _p(pos), _p(q_out),
                                         _p(k_cache), _p(v_cache), B, n_q_heads, n_kv_heads, head_dim,
                                         max_ctx, eps, theta, _stream()), "qk_norm_rope_kv")
+
+
+def prefill_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, n_q_heads: int, scale: float,
+                      out: torch.Tensor | None = None) -> torch.Tensor:
+    """Causal GQA flash attention over one prompt (csrc/ops/prefill_attn.hip):
+    q [Hkv, G*L, D] head-grouped, k / v [Hkv, L, D] bf16 -> [L, Hq*D] bf16.
+    Never materialises the L x L scores."""
+    Hkv, GL, D = q.shape
+    L = k.shape[1]
+    if D != 128 or GL != (n_q_heads // Hkv) * L or tuple(k.shape) != (Hkv, L, D) or k.shape != v.shape:
+        raise ValueError(f"prefill_attention shapes q {tuple(q.shape)} k {tuple(k.shape)} v {tuple(v.shape)}")
+    if n_q_heads % Hkv or (n_q_heads // Hkv) not in (1, 2, 4, 8):
+        raise ValueError(f"GQA group {n_q_heads}/{Hkv} unsupported")
+    for t in (q, k, v):
+        if t.dtype != torch.bfloat16 or not t.is_contiguous():
+            raise ValueError("q, k, v must be contiguous bf16")
+    if out is None:
+        out = torch.empty(L, n_q_heads * D, dtype=torch.bfloat16, device=q.device)
+    if out.numel() < L * n_q_heads * D or not out.is_contiguous():
+        raise ValueError("out too small")
+    _check(lib().mivgpu_prefill_attention(_p(q), _p(k), _p(v), _p(out), L, n_q_heads, Hkv, D, scale, _stream()),
+           "prefill_attention")
+    return out
 
 
 def prefill_qk_norm_rope_kv(qkv, q_norm_w, k_norm_w, pos, q_out, k_plain, v_plain, k_cache, v_cache, cache_b,

@@ -68,3 +68,17 @@ def silu_mul(gate_up):
     i = gate_up.shape[-1] // 2
     g, u = gate_up[..., :i].float(), gate_up[..., i:].float()
     return (torch.nn.functional.silu(g) * u).to(gate_up.dtype)
+
+
+def prefill_attention(q, k, v, n_q_heads, scale):
+    """fp32 causal GQA attention: q [Hkv, G*L, D] head-grouped, k / v [Hkv, L, D]
+    -> [L, Hq*D] (the numerics reference of ops.prefill_attention)."""
+    Hkv, GL, D = q.shape
+    L = k.shape[1]
+    G = GL // L
+    qf = q.float().view(Hkv, G, L, D)
+    sc = torch.einsum("hgld,hkd->hglk", qf, k.float()) * scale
+    causal = torch.ones(L, L, dtype=torch.bool, device=q.device).triu(1)
+    sc = sc.masked_fill(causal, float("-inf"))
+    o = torch.einsum("hglk,hkd->hgld", torch.softmax(sc, dim=-1), v.float())
+    return o.permute(2, 0, 1, 3).reshape(L, Hkv * G * D)

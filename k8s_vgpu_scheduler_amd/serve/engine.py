@@ -9,7 +9,8 @@ stand-in: the Qwen3 decoder of models/qwen3.py (random-init weights of the
 exact architecture; no network for checkpoints) with
 
   * prefill of the prompt in one pass (``Qwen3Decoder.prefill``), replayed
-    as one captured hipGraph per prompt-length bucket (32 ... 1024 tokens),
+    as one captured hipGraph per prompt-length bucket (32 ... 8192 tokens;
+    causal flash attention, csrc/ops/prefill_attn.hip),
   * decode as replays of one captured hipGraph per token (the hand-written
     gfx950 kernels: skinny MFMA GEMMs, fused decode attention, norms),
   * one request at a time (the reference client is sequential), tokens
@@ -78,7 +79,7 @@ class Engine:
     token while the previous one is being written to the client."""
 
     def __init__(self, model: str | Qwen3Config = "qwen3-8b", max_ctx: int = 4096, device: str | None = None,
-                 graph: bool = True, seed: int = 0, max_prefill_graph: int = 1024,
+                 graph: bool = True, seed: int = 0, max_prefill_graph: int = 8192,
                  gpu_memory_utilization: float | None = None):
         cfg = MODELS[model] if isinstance(model, str) else model
         self.cfg = cfg

@@ -66,3 +66,24 @@ def test_lane_fragments_are_mfma_operands(packed):
         for lane in (0, 9, 16, 47, 63):
             q, r = lane // 16, lane % 16
             assert torch.equal(pv[dt, lane], x[0, 0, 8 * q:8 * q + 8, 16 * dt + r])
+
+
+def test_prefill_attention_reference_matches_the_masked_path():
+    """ops.reference.prefill_attention (the flash kernel's numerics reference)
+    agrees with the decoder's fp32 masked-GEMM prefill attention."""
+    import math
+
+    import torch
+
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
+    from k8s_vgpu_scheduler_amd.ops import reference as ref
+
+    d = Qwen3Decoder(QWEN3_TINY, batch=1, max_ctx=128, device="cpu", native=False)
+    L, G, Hkv, D = 48, 4, 2, 128
+    q = torch.randn(Hkv, G * L, D).to(torch.bfloat16)
+    k = torch.randn(Hkv, L, D).to(torch.bfloat16)
+    v = torch.randn(Hkv, L, D).to(torch.bfloat16)
+    bufs = d._prefill_bufs(L)
+    a = d._prefill_attention(q, k, v, bufs["mask"]).float()
+    b = ref.prefill_attention(q, k, v, G * Hkv, 1.0 / math.sqrt(D))
+    assert (a - b).abs().max().item() < 2e-2 * b.abs().max().item()

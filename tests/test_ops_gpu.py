@@ -620,3 +620,49 @@ def test_prefill_qk_norm_rope_kv(ops, L, T, cb):
     for o in range(B):
         if o != cb:
             assert torch.equal(k_new[o], k_log[o]) and torch.equal(v_new[o], v_log[o])
+
+
+@pytest.mark.parametrize("L,Hq,Hkv", [(32, 32, 8), (100, 32, 8), (512, 32, 8), (2048, 32, 8), (8192, 8, 2),
+                                      (200, 8, 8), (96, 16, 8), (160, 64, 8)])
+def test_prefill_flash_attention(ops, L, Hq, Hkv):
+    """Causal GQA flash attention (csrc/ops/prefill_attn.hip) vs the fp32
+    reference, at the reference benchmark's 8192 context too (VERDICT r3
+    item 6); ragged L (not a multiple of 32) and every GQA group size."""
+    g = torch.Generator(device="cuda").manual_seed(L + Hq)
+    G, D = Hq // Hkv, 128
+    q = torch.randn(Hkv, G * L, D, generator=g, device="cuda").to(torch.bfloat16)
+    k = torch.randn(Hkv, L, D, generator=g, device="cuda").to(torch.bfloat16)
+    v = torch.randn(Hkv, L, D, generator=g, device="cuda").to(torch.bfloat16)
+    scale = 1.0 / math.sqrt(D)
+    out = ops.prefill_attention(q, k, v, Hq, scale)
+    want = ref.prefill_attention(q, k, v, Hq, scale)
+    assert torch.isfinite(out.float()).all()
+    _close(out, want, 2e-2)
+    # the first positions see one or two keys: exact-ish there
+    _close(out[:4], want[:4], 1e-2)
+
+
+def test_prefill_flash_attention_does_not_write_past_l(ops):
+    L, Hq, Hkv, D = 70, 32, 8, 128
+    q = torch.randn(Hkv, 4 * L, D, device="cuda").to(torch.bfloat16)
+    k = torch.randn(Hkv, L, D, device="cuda").to(torch.bfloat16)
+    v = torch.randn(Hkv, L, D, device="cuda").to(torch.bfloat16)
+    buf = torch.full((L + 26, Hq * D), 7.0, device="cuda", dtype=torch.bfloat16)
+    ops.prefill_attention(q, k, v, Hq, 0.088, out=buf)
+    assert (buf[L:] == 7.0).all()
+
+
+def test_decoder_long_prefill_matches_reference(monkeypatch):
+    """A 3000-token prompt (the 4096 bucket, flash attention) through the
+    native decoder vs the fp32 reference decoder."""
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
+
+    a = Qwen3Decoder(QWEN3_TINY, batch=1, max_ctx=4096, device="cuda", native=True, seed=9)
+    b = Qwen3Decoder(QWEN3_TINY, batch=1, max_ctx=4096, device="cuda", native=False, seed=9)
+    prompt = torch.randint(0, QWEN3_TINY.vocab, (3000,), generator=torch.Generator().manual_seed(4))
+    if a.skinny:
+        a.reserve_prefill()
+    a.capture_prefill(buckets=(4096,))
+    _close(a.prefill(prompt), b.prefill(prompt), 5e-2)
+    b.tokens.copy_(a.tokens)
+    _close(a.step()[0], b.step()[0], 5e-2)
