@@ -72,6 +72,9 @@ def main():
                     help="explicit comma list of rounds to run, in this order (experiments): shim, masked_noshim, "
                          "temporal, native, native_hip_default")
     ap.add_argument("--no-spatial", action="store_true", help="no HSA_CU_MASK (temporal governor)")
+    ap.add_argument("--layout", default="auto", choices=["auto", "hybrid", "disjoint"],
+                    help="CU ranges of slices below a quarter GPU: shared quarters split by the governor "
+                         "(hybrid = auto, the allocator's default) or disjoint ranges")
     ap.add_argument("--active-slices", type=int, default=0,
                     help="run only the first K of the --slices planned slices (same masks/limits; 0 = all)")
     ap.add_argument("--monitor", type=float, default=0.0, metavar="SECONDS",
@@ -163,13 +166,14 @@ def main():
         rounds.append(("shim", spawn_round(
             with_env(plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib,
                                  spatial=not args.no_spatial, policy=args.policy,
-                                 hw_queues=args.hw_queues or None)),
+                                 hw_queues=args.hw_queues or None, layout=args.layout)),
             phys, work, log_dir, child_args, "shim")))
     if "masked_noshim" in wanted:
         # the same CU masks and queues without libmivgpu.so: what the shim
         # itself costs (the overhead vs native also contains the
         # partitioning's own benefit)
-        bare = plan_slices(args.slices, shim=True, gpumem_mib=None, hw_queues=args.hw_queues or None)
+        bare = plan_slices(args.slices, shim=True, gpumem_mib=None, hw_queues=args.hw_queues or None,
+                           layout=args.layout)
         for sp in bare:
             sp.shim = False
         rounds.append(("masked_noshim", spawn_round(with_env(bare), phys, work / "bare", log_dir, child_args,
@@ -278,7 +282,8 @@ def main():
                 "batch_per_slice": args.batch,
                 "gpumem_mib_per_slice": args.gpumem_mib,
                 "gpucores_per_slice": 100 // args.slices if args.slices > 1 else 100,
-                "isolation": ("HSA_CU_MASK + libmivgpu" if not args.no_spatial else f"governor ({args.policy})")
+                "isolation": (f"HSA_CU_MASK ({args.layout} layout) + libmivgpu" if not args.no_spatial
+                              else f"governor ({args.policy})")
                 + (f" + {args.hw_queues} HW queue/slice" if args.hw_queues and args.slices > 1 else ""),
             },
             "round": "shim" if "shim" in results else ("native" if "native" in results else next(iter(results))),

@@ -3165,14 +3165,21 @@ MIVGPU_EXPORT unsigned long long mivgpu_launch_count(void) {
   return g_launches_local.load(std::memory_order_relaxed);
 }
 
-// Governor counters for `dev`: busy, held, gates (ns, ns, count).
+// Governor counters for `dev`: GPU time charged, held, gates (ns, ns, count).
+// Charged = what the bucket was debited: the sampler's share integral in the
+// default host-bucket mode (the gate kernel keeps no busy clock there), the
+// gates' measured busy wall time x share in device-bucket mode.
 MIVGPU_EXPORT int mivgpu_gate_stats(int dev, unsigned long long* busy, unsigned long long* held,
                                     unsigned long long* gates) {
   if (dev < 0 || dev >= MIVGPU_MAX_DEVICES) return -1;
   DeviceGate& G = g_gates[dev];
   if (!G.ok_pub.load(std::memory_order_acquire) || !G.host_stats) return -1;
   const volatile unsigned long long* h = static_cast<const volatile unsigned long long*>(G.host_stats);
-  if (busy) *busy = h[0];
+  const bool host_bucket = g_occ_live[dev].load(std::memory_order_acquire) && !g_cfg.gate_device_mode;
+  if (busy)
+    *busy = host_bucket && g_region && g_slot >= 0
+                ? __atomic_load_n(&g_region->procs[g_slot].util[dev].share_ns, __ATOMIC_RELAXED)
+                : h[0];
   if (held) *held = h[1];
   if (gates) *gates = h[2];
   return 0;

@@ -56,12 +56,24 @@ def cu_mask_string(ranges) -> str:
 
 
 def plan_slices(n: int, shim: bool, gpumem_mib: int | None, spatial: bool = True,
-                policy: str = "default", hw_queues: int | None = 2) -> list[SliceSpec]:
-    """Equal split of one GPU into n slices (CUs in contiguous, XCD-sized runs)."""
+                policy: str = "default", hw_queues: int | None = 2, layout: str = "auto") -> list[SliceSpec]:
+    """Equal split of one GPU into n slices (CUs in contiguous, XCD-sized runs).
+
+    ``layout`` = what the scheduler's CU allocator hands out
+    (device/amd/cu_alloc.py): ``disjoint`` = a range of its own per slice;
+    ``hybrid`` = slices below a quarter of the GPU share quarter-sized
+    ranges (as many as fit), split among them by the governor; ``auto`` =
+    hybrid, the allocator's default (``cuShareSmall``)."""
     specs = []
     per = (MI355X_CUS // n) // MI355X_XCDS * MI355X_XCDS   # whole 8-CU granules: XCD-balanced
+    unit = MI355X_CUS // 4
+    share = unit // per if (layout in ("auto", "hybrid") and 0 < per < unit) else 1
     for i in range(n):
-        ranges = [(i * per, (i + 1) * per - 1)] if (shim and spatial and n > 1) else None
+        if share > 1:
+            q = i // share
+            ranges = [(q * unit, (q + 1) * unit - 1)] if (shim and spatial and n > 1) else None
+        else:
+            ranges = [(i * per, (i + 1) * per - 1)] if (shim and spatial and n > 1) else None
         specs.append(SliceSpec(index=i, gpumem_mib=gpumem_mib if shim else None, cu_ranges=ranges,
                                core_pct=max(1, 100 // n) if n > 1 else 100, shim=shim,
                                policy=policy, hw_queues=hw_queues if (shim and n > 1) else None))

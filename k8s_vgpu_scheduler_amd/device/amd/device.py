@@ -82,6 +82,10 @@ class AMDConfig:
     # MI355X CU topology used by the CU-range allocator (measured, cu_alloc.py)
     xcds_per_device: int = 8
     cu_layout: str = "interleaved"
+    # requests below a quarter of the GPU share a quarter-sized CU range,
+    # time-sliced by the governor (cu_alloc.pick_shared); False = disjoint
+    # ranges of their own
+    cu_share_small: bool = True
     # Node-side (device plugin) knobs, shared through the same config
     device_split_count: int = 8
     device_memory_scaling: float = 1.0
@@ -103,7 +107,8 @@ class AMDConfig:
              "runtimeClassName": "runtime_class_name", "overwriteEnv": "overwrite_env",
              "xcdsPerDevice": "xcds_per_device", "cuLayout": "cu_layout",
              "deviceSplitCount": "device_split_count", "deviceMemoryScaling": "device_memory_scaling",
-             "deviceCoreScaling": "device_core_scaling", "allowTenantOptOut": "allow_tenant_opt_out"}
+             "deviceCoreScaling": "device_core_scaling", "allowTenantOptOut": "allow_tenant_opt_out",
+             "cuShareSmall": "cu_share_small"}
         kw = {}
         for k, v in (d or {}).items():
             if k in m:
@@ -412,7 +417,7 @@ class AMDDevices(D.Devices):
         dev.usedmem += ctr.usedmem
         ranges = (ctr.custominfo or {}).get("cu_ranges")
         if ranges:
-            dev.custominfo["cu_used"] = dev.custominfo.get("cu_used", 0) | cu_alloc.bitmap_from_ranges(ranges)
+            cu_alloc.charge(dev.custominfo, ranges, ctr.usedcores)
 
     def quota_cores(self, d: ContainerDevice) -> int:
         """CU count -> % for ResourceQuota accounting (limits are written in %)."""
@@ -507,7 +512,11 @@ class AMDDevices(D.Devices):
                 continue
             info = {}
             if 0 < cu < dev.totalcore:
-                ranges = cu_alloc.pick(dev.custominfo.get("cu_used", 0), cu, topo)
+                if self.cfg.cu_share_small and cu < cu_alloc.share_unit(topo) and topo.xcds > 1:
+                    ranges = cu_alloc.pick_shared(dev.custominfo.get("cu_used", 0),
+                                                  dev.custominfo.get("cu_shared", {}), cu, topo)
+                else:
+                    ranges = cu_alloc.pick(dev.custominfo.get("cu_used", 0), cu, topo)
                 if ranges is None:
                     bump(R.CARD_CU_FRAGMENTED)
                     continue

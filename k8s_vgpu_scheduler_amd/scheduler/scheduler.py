@@ -392,8 +392,8 @@ class Scheduler:
                         d.pod_infos.append((p.namespace, p.name, p.uid))
                         r = (cd.custominfo or {}).get("cu_ranges")
                         if r:
-                            from k8s_vgpu_scheduler_amd.device.amd.cu_alloc import bitmap_from_ranges
-                            d.custominfo["cu_used"] = d.custominfo.get("cu_used", 0) | bitmap_from_ranges(r)
+                            from k8s_vgpu_scheduler_amd.device.amd.cu_alloc import charge
+                            charge(d.custominfo, r, cd.usedcores)
 
     @staticmethod
     def _shape(usage: NodeUsage) -> tuple[tuple, tuple]:
@@ -406,7 +406,8 @@ class Scheduler:
         from k8s_vgpu_scheduler_amd.device.amd.device import cordoned_devices
         cordon = cordoned_devices(usage.node_info)
         shape = tuple((d.index, d.type, d.count, d.totalmem, d.totalcore, d.mode, d.numa, d.health, d.used,
-                       d.usedmem, d.usedcores, d.custominfo.get("cu_used", 0), d.id in cordon,
+                       d.usedmem, d.usedcores, d.custominfo.get("cu_used", 0),
+                       tuple(sorted((d.custominfo.get("cu_shared") or {}).items())), d.id in cordon,
                        tuple(sorted((pos.get(k, -1), v) for k, v in (d.custominfo.get("pair_scores") or {}).items())))
                       for d in devs)
         return shape, tuple(d.id for d in devs)

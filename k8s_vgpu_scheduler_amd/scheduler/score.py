@@ -67,32 +67,39 @@ def fit_in_devices(node: NodeUsage, requests: dict, pod: dict, node_info: NodeIn
 
 def _snapshot_peak(devices: DeviceUsageList) -> dict:
     return {dl.device.id: (dl.device.used, dl.device.usedcores, dl.device.usedmem,
-                           dl.device.custominfo.get("cu_used", 0)) for dl in devices.device_lists}
+                           dl.device.custominfo.get("cu_used", 0), dl.device.custominfo.get("cu_shared") or {})
+            for dl in devices.device_lists}
 
 
 def _update_peak(peak: dict, copy: NodeUsage):
+    from k8s_vgpu_scheduler_amd.device.amd.cu_alloc import merge_shared
     for dl in copy.devices.device_lists:
         d = dl.device
         p = peak.get(d.id)
         if p is None:
-            peak[d.id] = (d.used, d.usedcores, d.usedmem, d.custominfo.get("cu_used", 0))
+            peak[d.id] = (d.used, d.usedcores, d.usedmem, d.custominfo.get("cu_used", 0),
+                          d.custominfo.get("cu_shared") or {})
         else:
             peak[d.id] = (max(p[0], d.used), max(p[1], d.usedcores), max(p[2], d.usedmem),
-                          p[3] | d.custominfo.get("cu_used", 0))
+                          p[3] | d.custominfo.get("cu_used", 0), merge_shared(p[4], d.custominfo.get("cu_shared")))
 
 
 def _apply_peak(node: NodeUsage, app_copy: NodeUsage, peak: dict):
+    from k8s_vgpu_scheduler_amd.device.amd.cu_alloc import merge_shared
     app = {dl.device.id: dl.device for dl in app_copy.devices.device_lists}
     for dl in node.devices.device_lists:
         d = dl.device
         a = app.get(d.id)
-        u, c, m, cu = (a.used, a.usedcores, a.usedmem, a.custominfo.get("cu_used", 0)) if a else (0, 0, 0, 0)
+        u, c, m, cu, sh = ((a.used, a.usedcores, a.usedmem, a.custominfo.get("cu_used", 0),
+                            a.custominfo.get("cu_shared") or {}) if a else (0, 0, 0, 0, {}))
         p = peak.get(d.id)
         if p:
-            u, c, m, cu = max(u, p[0]), max(c, p[1]), max(m, p[2]), cu | p[3]
+            u, c, m, cu, sh = max(u, p[0]), max(c, p[1]), max(m, p[2]), cu | p[3], merge_shared(sh, p[4])
         d.used, d.usedcores, d.usedmem = u, c, m
         if cu:
             d.custominfo["cu_used"] = cu
+        if sh:
+            d.custominfo["cu_shared"] = sh
 
 
 def _base_types(devices: DeviceUsageList) -> set:

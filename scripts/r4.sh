@@ -1,0 +1,34 @@
+#!/usr/bin/env bash
+# Round-4 GPU runs: each step under its own time limit; a crash, timeout or
+# abort (rc >= 2 and not a plain pytest failure) ends the run there.
+#   bash scripts/r4.sh <outdir> <step>...   steps: flash, attnbench, shim, other, ttft, slices8, governor
+set -o pipefail
+out=${1:?outdir}; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+mkdir -p "$R/gpurun_out/$out"; cd "$R"
+run() {  # run <seconds> <log> <cmd...>; pytest rc 1 (failures) keeps going
+  local t=$1 log=$2; shift 2
+  echo "[r4] $log: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$out/$log.log" 2>&1
+  local rc=$?
+  echo "[r4] $log rc=$rc"
+  if [ $rc -ge 2 ]; then echo "[r4] stopping after $log (rc=$rc)"; exit $rc; fi
+}
+T="--timeout 300 --timeout-method thread"
+for s in "$@"; do
+  case $s in
+    flash) run 400 flash_tests python -u -m pytest tests/test_ops_gpu.py -v -k "prefill_flash or long_prefill" $T ;;
+    attnbench) run 300 prefill_attn python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention \
+                 --out "gpurun_out/$out/prefill_attn.json" ;;
+    shim) run 700 shim_tests python -u -m pytest tests/test_shim_gpu.py tests/test_shim_interpose_gpu.py -v -s $T ;;
+    other) run 700 other_tests python -u -m pytest tests -m gpu -v $T --deselect tests/test_shim_gpu.py \
+             --deselect tests/test_shim_interpose_gpu.py ;;
+    allgpu) run 1000 gpu_tests python -u -m pytest tests -m gpu -v $T ;;
+    ttft) for n in 512 2048 8000; do
+            run 400 "ttft_$n" python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len $n --ctx 8192 --iters 5
+          done ;;
+    bench) run 400 bench python -u bench.py --out "gpurun_out/$out/bench.json" ;;
+    smoke) run 200 smoke python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done

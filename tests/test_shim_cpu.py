@@ -127,7 +127,7 @@ def test_region_contents_visible_to_monitor(native_build, tmp_path):
     assert reg.priority() == 1
     # set off the launch path by the housekeeping thread, at once for the first launch
     t0 = time.time()
-    while reg.recent_kernel() != 2 and time.time() - t0 < 2.0:
+    while (reg.recent_kernel() != 2 or reg.r.procs[0].util[0].launches != 5) and time.time() - t0 < 2.0:
         time.sleep(0.01)
     assert reg.recent_kernel() == 2
     assert reg.r.procs[0].util[0].launches == 5 and reg.last_kernel_time() > 0
