@@ -81,6 +81,9 @@ def main():
                     help="run the node monitor's feedback pass (priority + utilization_switch) over the shim "
                          "rounds' regions every SECONDS while they run (0 = off)")
     ap.add_argument("--policy", default="default", choices=["default", "force", "disable"])
+    ap.add_argument("--slice-limits", default="",
+                    help="comma list of per-slice core limits (%%) for the shim and temporal rounds, e.g. 75,25 "
+                         "(unequal tenants; default 100/N each)")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     ap.add_argument("--hw-queues", type=int, default=2,
                     help="GPU_MAX_HW_QUEUES per slice in the shim round (0 = HIP default)")
@@ -91,6 +94,10 @@ def main():
                          "held to --gov-limit %%): >= 2 s of GPU work whatever --steps is, so the 100 ms burst "
                          "is amortised (0 = skip)")
     ap.add_argument("--gov-limit", type=int, default=25, help="core limit (%%) of the governed round")
+    ap.add_argument("--eager-steps", type=int, default=60,
+                    help="decode steps of the two eager rounds (one batch-1 slice, every kernel launched from the "
+                         "host, under libmivgpu.so and without it: the launch hook's cost on a launch-bound "
+                         "tenant); 0 = skip")
     ap.add_argument("--no-collectives", action="store_true",
                     help="skip the untimed all-reduce check between the bench ranks (N > 1)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
@@ -116,10 +123,20 @@ def main():
 
     extra_env = dict(kv.split("=", 1) for kv in args.child_env)
 
+    limits = [int(x) for x in args.slice_limits.split(",") if x.strip()]
+    if limits and len(limits) != args.slices:
+        ap.error(f"--slice-limits has {len(limits)} entries for {args.slices} slices")
+
     def with_env(specs):
         for sp in specs:
             sp.env.update(extra_env)
         return specs[:args.active_slices] if args.active_slices > 0 else specs
+
+    def with_limits(specs):
+        if limits and len(specs) == len(limits):
+            for sp, lim in zip(specs, limits):
+                sp.core_pct = lim
+        return specs
 
     def native_specs(queues):
         specs = plan_slices(args.slices, shim=False, gpumem_mib=None)
@@ -150,6 +167,8 @@ def main():
     # to --gov-limit % (policy force, no CU mask), over --gov-steps steps.
     if args.gov_steps > 0 and args.mode == "all" and not args.rounds and not cpu:
         wanted += ["governed_ref", "governed"]
+    if args.eager_steps > 0 and args.mode == "all" and not args.rounds and not cpu:
+        wanted += ["eager_shim", "eager_noshim"]
     gov_args = list(child_args)
     gov_args[gov_args.index("--steps") + 1] = str(max(args.gov_steps, args.steps))
     rounds = []
@@ -164,9 +183,9 @@ def main():
                                                "governed")))
     if "shim" in wanted:
         rounds.append(("shim", spawn_round(
-            with_env(plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib,
-                                 spatial=not args.no_spatial, policy=args.policy,
-                                 hw_queues=args.hw_queues or None, layout=args.layout)),
+            with_env(with_limits(plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib,
+                                             spatial=not args.no_spatial, policy=args.policy,
+                                             hw_queues=args.hw_queues or None, layout=args.layout))),
             phys, work, log_dir, child_args, "shim")))
     if "masked_noshim" in wanted:
         # the same CU masks and queues without libmivgpu.so: what the shim
@@ -182,8 +201,8 @@ def main():
         # the same slices time-shared by the governor gate instead of CU masks
         # (BASELINE config 3: "4 pods x 25% gpucores, CU-throttle governor kernel")
         rounds.append(("temporal", spawn_round(
-            with_env(plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib, spatial=False,
-                                 policy="force", hw_queues=args.hw_queues or None)),
+            with_env(with_limits(plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib, spatial=False,
+                                             policy="force", hw_queues=args.hw_queues or None))),
             phys, work / "temporal", log_dir, child_args, "temporal")))
     if "native" in wanted:
         rounds.append(("native", spawn_round(native_specs(args.hw_queues), phys, work, log_dir, child_args,
@@ -191,6 +210,16 @@ def main():
     if "native_hip_default" in wanted:
         rounds.append(("native_hip_default", spawn_round(native_specs(0), phys, work, log_dir, child_args,
                                                          "native_hip_default")))
+    eager_args = list(child_args)
+    eager_args[eager_args.index("--steps") + 1] = str(args.eager_steps)
+    eager_args[eager_args.index("--batch") + 1] = "1"
+    eager_args.append("--eager")
+    for nm, with_shim in (("eager_shim", True), ("eager_noshim", False)):
+        if nm in wanted:
+            sp = plan_slices(1, shim=True, gpumem_mib=args.gpumem_mib, spatial=False)
+            sp[0].shim = with_shim
+            sp[0].gpumem_mib = args.gpumem_mib if with_shim else None
+            rounds.append((nm, spawn_round(with_env(sp), phys, work / nm, log_dir, eager_args, nm)))
     order = {name: i for i, name in enumerate(wanted)}
     rounds.sort(key=lambda r: order[r[0]])
 
@@ -281,7 +310,7 @@ def main():
                 "slices_per_gpu": args.slices,
                 "batch_per_slice": args.batch,
                 "gpumem_mib_per_slice": args.gpumem_mib,
-                "gpucores_per_slice": 100 // args.slices if args.slices > 1 else 100,
+                "gpucores_per_slice": limits or (100 // args.slices if args.slices > 1 else 100),
                 "isolation": (f"HSA_CU_MASK ({args.layout} layout) + libmivgpu" if not args.no_spatial
                               else f"governor ({args.policy})")
                 + (f" + {args.hw_queues} HW queue/slice" if args.hw_queues and args.slices > 1 else ""),
@@ -296,7 +325,8 @@ def main():
         }
         if any("gov_gates" in d or "share_pct" in d for d in head["done"]):
             out["governor_rank0"] = [{k: d.get(k) for k in ("gov_charged_ms", "gov_held_ms", "gov_gates",
-                                                            "share_pct", "util_pct")} for d in head["done"]]
+                                                            "share_pct", "util_pct", "busy_share_pct",
+                                                            "seconds")} for d in head["done"]]
         if "native" in results and "shim" in results:
             nat = results["native"]["tok_s"]
             out["native_value"] = round(nat, 2)
@@ -318,6 +348,15 @@ def main():
                                                                      "share_pct", "util_pct")} for d in tr["done"]]
             if "native" in results:
                 out["temporal_overhead_pct"] = round((1.0 - tr["tok_s"] / results["native"]["tok_s"]) * 100.0, 2)
+        if "eager_shim" in results and "eager_noshim" in results:
+            es, en = results["eager_shim"], results["eager_noshim"]
+            out["eager_launch_bound"] = {
+                "what": "1 slice, batch 1, no hipGraph (every kernel launched from the host)",
+                "steps": args.eager_steps, "shim_tok_s": round(es["tok_s"], 2),
+                "noshim_tok_s": round(en["tok_s"], 2),
+                "shim_overhead_pct": round((1.0 - es["tok_s"] / en["tok_s"]) * 100.0, 2),
+                "ms_per_step_shim": round(es["max_wall_s"] / args.eager_steps * 1e3, 3),
+                "ms_per_step_noshim": round(en["max_wall_s"] / args.eager_steps * 1e3, 3)}
         for nm in ("shim", "temporal"):
             if nm in results and "monitor" in results[nm]:
                 out[f"{nm}_monitor"] = results[nm]["monitor"]

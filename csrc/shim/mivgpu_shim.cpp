@@ -2595,9 +2595,31 @@ MIVGPU_EXPORT hipError_t hipGetDevicePropertiesR0000(void* prop, int device) {
   return rc;
 }
 
+// Cost-attribution builds of the launch path (utils/build.py build_hook_diag;
+// separate files under build/diag, never the shipped library): level 1
+// forwards the launch untouched (the interposition alone), 2 adds the
+// re-entrancy guard and the lazy-init check, 3 adds the launch counters.
+// The shipped build compiles the full prologue below.
+#if defined(MIVGPU_HOOK_DIAG) && MIVGPU_HOOK_DIAG == 1
+#define LAUNCH_PROLOGUE(stream) (void)(stream);
+#elif defined(MIVGPU_HOOK_DIAG) && MIVGPU_HOOK_DIAG == 2
+#define LAUNCH_PROLOGUE(stream) \
+  Guard g_guard;                \
+  ensure_init();                \
+  (void)(stream);
+#elif defined(MIVGPU_HOOK_DIAG) && MIVGPU_HOOK_DIAG == 3
+#define LAUNCH_PROLOGUE(stream)                                                        \
+  Guard g_guard;                                                                       \
+  ensure_init();                                                                       \
+  if (g_guard.outer && g_launches_local.fetch_add(1, std::memory_order_relaxed) == 0) \
+    start_occ_sampler();                                                               \
+  g_dev_launches[0].fetch_add(1, std::memory_order_relaxed);                           \
+  (void)(stream);
+#else
 #define LAUNCH_PROLOGUE(stream)   \
   Guard g_guard;                  \
   LaunchScope g_scope(g_guard.outer ? on_launch(stream) : LaunchTicket{});
+#endif
 #define GRAPH_LAUNCH_PROLOGUE(stream) \
   Guard g_guard;                      \
   LaunchScope g_scope(g_guard.outer ? on_launch(stream, true) : LaunchTicket{});

@@ -229,6 +229,8 @@ def child_main(argv):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = harness rehearsal (fp32 reference path, no GPU)")
+    ap.add_argument("--eager", action="store_true",
+                    help="no hipGraph: every kernel of every step launched from the host (launch-bound)")
     ap.add_argument("--loop", action="store_true",
                     help="after GO, decode until STOP arrives on stdin (a noisy neighbour for the serving "
                          "bench); the context position wraps every --steps steps")
@@ -252,7 +254,8 @@ def child_main(argv):
     max_ctx = a.ctx + a.warmup + a.steps + 16
     dec = Qwen3Decoder(cfg, batch=a.batch, max_ctx=max_ctx, device="cuda")
     dec.fill_context(a.ctx)
-    dec.capture(warmup=1)
+    if not a.eager:
+        dec.capture(warmup=1)
     for _ in range(a.warmup):
         dec.step()
     torch.cuda.synchronize()
