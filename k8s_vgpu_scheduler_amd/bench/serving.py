@@ -133,6 +133,7 @@ def run_config(name: str, spec: SliceSpec, a, workdir: Path, log=_log) -> list[d
 
 
 neighbours_done: dict = {}
+long_ttft: dict = {}      # config -> TTFT of the long prompt (--long-prompt-tokens)
 
 
 def _run_server(name: str, spec: SliceSpec, a, workdir: Path, log=_log) -> list[dict]:
@@ -159,6 +160,19 @@ def _run_server(name: str, spec: SliceSpec, a, workdir: Path, log=_log) -> list[
         infos[name] = info
         rows = client.run(url, a.runs, a.warmup, a.prompt, a.max_tokens, str(workdir / f"{name}.jsonl"),
                           timeout=a.request_timeout, log=lambda m: log(f"[serving] {name}:{m}"))
+        n_long = getattr(a, "long_prompt_tokens", 0)
+        if n_long:
+            # a long prompt through the flash prefill: TTFT at the reference's
+            # context length (the chat template adds ~20 tokens)
+            words = ("lorem ipsum dolor sit amet " * (n_long // 27 + 2))[:max(1, n_long - 32)]
+            long_rows = client.run(url, a.long_runs, 1, words, 4, str(workdir / f"{name}.long.jsonl"),
+                                   timeout=max(a.request_timeout, 120.0), log=None)
+            ttfts = sorted((r["t_first"] - r["t0"]) * 1e3 for r in long_rows if r.get("t_first"))
+            long_ttft[name] = {"prompt_chars": len(words), "runs": len(ttfts),
+                               "ttft_ms_p50": round(ttfts[len(ttfts) // 2], 2) if ttfts else None,
+                               "ttft_ms_min": round(ttfts[0], 2) if ttfts else None,
+                               "ttft_ms_max": round(ttfts[-1], 2) if ttfts else None}
+            log(f"[serving] {name}: long prompt TTFT {long_ttft[name]}")
     finally:
         if proc.poll() is None:
             os.killpg(proc.pid, signal.SIGTERM)
@@ -182,7 +196,12 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--runs", type=int, default=200)
     ap.add_argument("--max-tokens", type=int, default=128)
-    ap.add_argument("--max-model-len", type=int, default=4096)
+    ap.add_argument("--max-model-len", type=int, default=8192,
+                    help="the reference's vLLM --max-model-len (benchmarks/ai-benchmark/Dockerfile:7-9)")
+    ap.add_argument("--long-prompt-tokens", type=int, default=0,
+                    help="after the timed runs, TTFT of a prompt of about this many tokens (e.g. 8000; the "
+                         "byte tokenizer: one token per prompt character), --long-runs times")
+    ap.add_argument("--long-runs", type=int, default=5)
     ap.add_argument("--prompt", default=client.DEFAULT_PROMPT)
     ap.add_argument("--device", default=None)
     ap.add_argument("--no-graph", action="store_true")
@@ -220,6 +239,9 @@ def main(argv=None):
     for n, d in neighbours_done.items():
         if n in summary:
             summary[n]["neighbours"] = d
+    for n, d in long_ttft.items():
+        if n in summary:
+            summary[n]["long_prompt"] = d
     (workdir / "summary.json").write_text(json.dumps(summary, indent=1))
     line = {"metric": "serving TTFT / per-token latency, vGPU slices vs native", "model": a.model,
             "neighbours_default": default_nb,

@@ -127,7 +127,8 @@ def main(argv=None):
     ap.add_argument("--model", default="qwen3-8b", choices=sorted(MODELS))
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8000)
-    ap.add_argument("--max-model-len", type=int, default=4096)
+    ap.add_argument("--max-model-len", type=int, default=8192,
+                    help="context length (the reference benchmark's vLLM --max-model-len 8192)")
     ap.add_argument("--max-tokens", type=int, default=128, help="default completion length")
     ap.add_argument("--no-graph", action="store_true", help="eager decode steps instead of hipGraph replays")
     ap.add_argument("--device", default=None)

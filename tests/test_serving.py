@@ -147,6 +147,17 @@ def test_serving_orchestrator_cpu(tmp_path):
     assert (tmp_path / "report.md").exists() and (tmp_path / "native.jsonl").exists()
 
 
+def test_serving_long_prompt_ttft_cpu(tmp_path):
+    """--long-prompt-tokens: TTFT of a long prompt per configuration."""
+    from k8s_vgpu_scheduler_amd.bench import serving
+    rc = serving.main(["--configs", "native", "--model", "qwen3-tiny", "--device", "cpu", "--warmup", "0",
+                       "--runs", "1", "--max-tokens", "2", "--max-model-len", "512", "--long-prompt-tokens", "300",
+                       "--long-runs", "2", "--out-dir", str(tmp_path)])
+    assert rc == 0
+    lp = json.loads((tmp_path / "serving.json").read_text())["configs"]["native"]["long_prompt"]
+    assert lp["runs"] == 2 and lp["ttft_ms_p50"] > 0 and 200 < lp["prompt_chars"] <= 300
+
+
 def test_serving_orchestrator_with_neighbours_cpu(tmp_path):
     """``native+1``: one busy neighbour (the bench/slices child in --loop
     mode) runs while the server is measured, then stops and reports."""
