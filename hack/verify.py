@@ -45,7 +45,7 @@ VERBS = {"get", "list", "create", "update", "patch", "delete", "watch"}
 # typed helpers of k8s/client.py:KubeClient -> (resource, verb)
 HELPERS = {"get_node": ("nodes", "get"), "list_nodes": ("nodes", "list"), "get_pod": ("pods", "get"),
            "list_pods": ("pods", "list"), "patch_node": ("nodes", "patch"), "patch_pod": ("pods", "patch"),
-           "bind": ("pods/binding", "create")}
+           "bind": ("pods/binding", "create"), "evict": ("pods/eviction", "create")}
 
 
 # ----------------------------------------------------------------- helpers
