@@ -1012,6 +1012,31 @@ __global__ void pack_weight_kernel(const bf16_t* __restrict__ w, u32x4_t* __rest
   }
 }
 
+// The inverse: packed -> W[N][K] row-major, for prompt-sized GEMMs on the
+// library path (a slice keeps only the packed copy; re-streaming it once per
+// 128-row chunk of an 8k prompt read the weights 64 times).  deinterleave:
+// the packed rows are gate/up interleaved per 32-row block (interleave_gate_up
+// in ops/__init__.py); write them back as [gate rows; up rows].
+__global__ void unpack_weight_kernel(const u32x4_t* __restrict__ wp, bf16_t* __restrict__ w, int N, int K,
+                                     int kmajor, int deinterleave) {
+  const size_t KB = K >> 6, NTL = N >> 5;
+  const size_t total = NTL * KB * 256;
+  const size_t half = (size_t)N >> 1;
+  for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (size_t)gridDim.x * blockDim.x) {
+    const int l = q & 63;
+    const int j = (q >> 6) & 3;
+    const size_t tk = q >> 8;
+    const size_t t = kmajor ? tk % NTL : tk / KB, kb = kmajor ? tk / NTL : tk % KB;
+    size_t row = t * 32 + (l & 31);
+    if (deinterleave) {
+      const size_t c = row >> 6, within = row & 63;
+      row = within < 32 ? c * 32 + within : half + c * 32 + (within - 32);
+    }
+    const size_t col = kb * 64 + 32 * (l >> 5) + 8 * j;
+    *(u32x4_t*)(w + row * K + col) = __builtin_nontemporal_load(wp + q);
+  }
+}
+
 struct Args {
   const void* wp;
   const void* x;
@@ -1365,6 +1390,15 @@ int mivgpu_pack_weight(const void* w, void* wp, int N, int K, hipStream_t s) {
   const int blocks = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
   hipLaunchKernelGGL(pack_weight_kernel, dim3(blocks), dim3(256), 0, s, (const bf16_t*)w, (u32x4_t*)wp, N, K,
                      use_kmajor() ? 1 : 0);
+  return (int)hipGetLastError();
+}
+
+int mivgpu_unpack_weight(const void* wp, void* w, int N, int K, int deinterleave, hipStream_t s) {
+  if (N <= 0 || K <= 0 || (N & 31) || (K & 63) || (deinterleave && (N & 63))) return (int)hipErrorInvalidValue;
+  const size_t total = (size_t)(N >> 5) * (K >> 6) * 256;
+  const int blocks = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
+  hipLaunchKernelGGL(unpack_weight_kernel, dim3(blocks), dim3(256), 0, s, (const u32x4_t*)wp, (bf16_t*)w, N, K,
+                     use_kmajor() ? 1 : 0, deinterleave);
   return (int)hipGetLastError();
 }
 

@@ -261,6 +261,8 @@ class Qwen3Decoder:
         self._tail_work = ops.decode_tail_workspace(batch, self.device) if self.native else None
         self._pf = {}          # prefill bucket length -> static buffers (+ captured graph)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        # RMSNorm without a weight (the packed copies carry it folded in)
+        self._ones = torch.ones(cfg.hidden, dtype=torch.bfloat16, device=self.device)
 
     # ------------------------------------------------------------- setup --
     def fill_context(self, ctx_len: int, seed: int = 1):
@@ -411,6 +413,9 @@ class Qwen3Decoder:
     # (benchmarks/ai-benchmark/Dockerfile:7-9).
     PREFILL_CHUNK = 128
     PREFILL_BUCKETS = (32, 64, 128, 256, 512, 1024, 2048, 4096, 8192)
+    # prompts of at least this many rows run packed-only projections as
+    # unpack-once + library GEMM (PackedLinear.prompt) instead of 128-row chunks
+    PROMPT_UNPACK_ROWS = int(os.environ.get("MIVGPU_PROMPT_UNPACK_ROWS", "1024"))
 
     def _rows(self, pl, x, out=None):
         M = x.shape[0]
@@ -437,11 +442,15 @@ class Qwen3Decoder:
     def _normed_proj(self, lw, name, x, ln):
         """Norm-fused decoder, prefill: RMSNorm(x) . W^T (SiLU*up for gate_up)
         on the plain weight after a separate norm where one is kept and the
-        rows are prompt-sized, else on the packed copy with the folded norm."""
+        rows are prompt-sized, on the packed copy unpacked for the library GEMM
+        for long prompts (its folded norm weight: X normalised without one),
+        else on the packed copy with the folded norm and row scales."""
         packed, plain = {"qkv": ("pqkv", "wqkv"), "gu": ("pgu", "wgu")}[name]
         if plain in lw and x.shape[0] > 64:
             y = F.linear(self._norm(x, ln), lw[plain])
             return ops.silu_mul(y) if name == "gu" else y
+        if x.shape[0] >= self.PROMPT_UNPACK_ROWS:
+            return lw[packed].prompt(self._norm(x, self._ones))
         return self._rows_normed(lw[packed], x)     # gate_up: SiLU*up fused in the epilogue
 
     def _prefill_impl_norm_fused(self, bufs: dict, b: int):
@@ -462,6 +471,8 @@ class Qwen3Decoder:
         packed, plain = {"qkv": ("pqkv", "wqkv"), "o": ("po", "wo"), "gu": ("pgu", "wgu"),
                          "d": ("pd", "wd")}[name]
         if packed in lw and not (plain in lw and x.shape[0] > 64):
+            if x.shape[0] >= self.PROMPT_UNPACK_ROWS:
+                return lw[packed].prompt(x)      # long prompt: unpack once, library GEMM
             return self._rows(lw[packed], x)     # gate_up: SiLU*up fused in the epilogue
         y = F.linear(x, lw[plain])
         if name == "gu":

@@ -52,6 +52,7 @@ def lib():
         L.mivgpu_silu_mul.argtypes = [vp, vp, i, i, vp]
         L.mivgpu_hwid_probe.argtypes = [vp, i, vp]
         L.mivgpu_pack_weight.argtypes = [vp, vp, i, i, vp]
+        L.mivgpu_unpack_weight.argtypes = [vp, vp, i, i, i, vp]
         L.mivgpu_skinny_gemm.argtypes = [vp, vp, vp, i, i, i, i, i, i, i, i, i, i, vp, vp, vp]
         L.mivgpu_skinny_gemm_norm.argtypes = [vp, vp, vp, i, i, i, i, i, i, i, i, i, i, vp, vp, vp, i, f, f, vp, vp]
         ip, lp = ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_longlong)
@@ -67,7 +68,7 @@ def lib():
                    "mivgpu_skinny_max_m", "mivgpu_skinny_plan", "mivgpu_mfma_burn",
                    "mivgpu_stream_copy", "mivgpu_stream_read", "mivgpu_ops_visible_cus",
                    "mivgpu_ops_kv_packed", "mivgpu_decode_attention_fused", "mivgpu_skinny_gemm_norm",
-                   "mivgpu_prefill_qk_norm_rope_kv", "mivgpu_prefill_attention"):
+                   "mivgpu_prefill_qk_norm_rope_kv", "mivgpu_prefill_attention", "mivgpu_unpack_weight"):
             getattr(L, fn).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -436,6 +437,32 @@ def pack_weight(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
+# One shared row-major scratch per device for prompt-sized GEMMs on packed
+# weights (PackedLinear.prompt): the largest projection's bytes, not a second
+# copy of every weight (16 GB for Qwen3-8B).
+_UNPACK: dict = {}
+
+
+def unpack_scratch(numel: int, device) -> torch.Tensor:
+    key = str(device)
+    buf = _UNPACK.get(key)
+    if buf is None or buf.numel() < numel:
+        buf = _UNPACK[key] = torch.empty(numel, dtype=torch.bfloat16, device=device)
+    return buf[:numel]
+
+
+def unpack_weight(wp: torch.Tensor, N: int, K: int, out: torch.Tensor | None = None,
+                  deinterleave: bool = False) -> torch.Tensor:
+    """Packed W -> row-major [N, K] (the inverse of pack_weight; with
+    ``deinterleave`` the gate/up blocks of interleave_gate_up are put back as
+    [gate rows; up rows])."""
+    if out is None:
+        out = torch.empty(N, K, dtype=torch.bfloat16, device=wp.device)
+    _check(lib().mivgpu_unpack_weight(_p(wp), _p(out), N, K, 1 if deinterleave else 0, _stream()),
+           "unpack_weight")
+    return out.view(N, K)
+
+
 def interleave_gate_up(w_gu: torch.Tensor) -> torch.Tensor:
     """[2I, K] (gate rows then up rows) -> rows ordered gate[0:32], up[0:32], gate[32:64], ...
     so n-tile pair (2c, 2c+1) of the packed weight is (gate, up) of channel block c."""
@@ -534,6 +561,17 @@ class PackedLinear:
                                         out.stride(0), self.epi, nt, ks, S, variant, sp, tp, _stream()),
                "skinny_gemm")
         return out
+
+    def prompt(self, x: torch.Tensor) -> torch.Tensor:
+        """X . W^T for prompt-sized X (hundreds to thousands of rows): the packed
+        weight unpacked once into the shared scratch, then the library GEMM
+        (hipBLASLt) -- instead of re-streaming the packed weight once per
+        128-row chunk.  SiLU*up for a gate/up weight.  (A folded col_scale
+        stays folded: the caller normalises X without a weight.)"""
+        w = unpack_weight(self.wp, self.N, self.K, unpack_scratch(self.N * self.K, self.wp.device),
+                          deinterleave=self.silu_mul)
+        y = torch.nn.functional.linear(x, w)
+        return silu_mul(y) if self.silu_mul else y
 
     def slots(self, M: int) -> int:
         """Sum-of-squares slots a residual call (``norm_call(residual=True)``)

@@ -666,3 +666,38 @@ def test_decoder_long_prefill_matches_reference(monkeypatch):
     _close(a.prefill(prompt), b.prefill(prompt), 5e-2)
     b.tokens.copy_(a.tokens)
     _close(a.step()[0], b.step()[0], 5e-2)
+
+
+@pytest.mark.parametrize("N,K,gu", [(4096, 4096, False), (6144, 4096, False), (24576, 4096, True), (4096, 12288, False)])
+def test_unpack_weight_inverts_pack(ops, N, K, gu):
+    w = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+    src = ops.interleave_gate_up(w) if gu else w
+    back = ops.unpack_weight(ops.pack_weight(src), N, K, deinterleave=gu)
+    assert torch.equal(back, w)
+
+
+def test_packed_prompt_gemm_matches_reference(ops):
+    """PackedLinear.prompt (unpack once + library GEMM) vs fp32, plain and SiLU*up."""
+    x = torch.randn(700, 4096, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(2048, 4096, device="cuda") * 0.02).to(torch.bfloat16)
+    _close(ops.PackedLinear(w).prompt(x), x.float() @ w.float().t(), 2e-2)
+    pg = ops.PackedLinear(w, silu_mul=True)
+    _close(pg.prompt(x), ref.silu_mul(x.float() @ w.float().t()), 3e-2)
+
+
+def test_decoder_packed_only_long_prefill(monkeypatch):
+    """A slice-style decoder that keeps only the packed weights runs a prompt
+    above MIVGPU_PROMPT_UNPACK_ROWS through unpack + library GEMM, matching
+    the fp32 reference decoder."""
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
+
+    monkeypatch.setenv("MIVGPU_SLICE_PLAN_CUS", "100000")
+    monkeypatch.setenv("MIVGPU_QKV_WIDE_CUS", "100000")
+    monkeypatch.setenv("MIVGPU_WIDEK", "off")
+    monkeypatch.setattr(Qwen3Decoder, "PROMPT_UNPACK_ROWS", 256)
+    a = Qwen3Decoder(QWEN3_TINY, batch=1, max_ctx=1024, device="cuda", native=True, seed=5)
+    assert all(k not in lw for lw in a.w.layers for k in ("wgu", "wd", "wo", "wqkv"))
+    b = Qwen3Decoder(QWEN3_TINY, batch=1, max_ctx=1024, device="cuda", native=False, seed=5)
+    prompt = torch.randint(0, QWEN3_TINY.vocab, (300,), generator=torch.Generator().manual_seed(6))
+    a.reserve_prefill()
+    _close(a.prefill(prompt), b.prefill(prompt), 5e-2)
