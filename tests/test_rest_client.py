@@ -113,3 +113,16 @@ def test_informer_over_http(srv):
         assert _until(lambda: not inf.list())
     finally:
         inf.stop()
+
+
+def test_eviction_api(srv):
+    """POST pods/<name>/eviction (policy/v1): the monitor's --over-grant-action=evict."""
+    s, c = srv
+    c.create("pods", make_pod("victim", "ns1"))
+    c.evict("ns1", "victim")
+    assert s.cluster.evictions == [("ns1", "victim")]
+    with pytest.raises(NotFound):
+        c.get_pod("ns1", "victim")
+    assert ("POST", "/api/v1/namespaces/ns1/pods/victim/eviction") in s.requests
+    with pytest.raises(NotFound):
+        c.evict("ns1", "victim")
