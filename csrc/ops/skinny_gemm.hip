@@ -30,6 +30,7 @@
 //    weight (n-tile 2c = gate rows, 2c+1 = up rows of channel block c), which
 //    removes the separate activation kernel and the [M, 2I] round trip.
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -666,36 +667,74 @@ __device__ __forceinline__ void rs_finish(const float4 (&v)[RS_LMAX], float inv_
   }
 }
 
+// Arguments of one projection (the wide and K-split bodies below).
+struct GemmP {
+  const u32x4_t* wp;
+  const bf16_t* x;
+  bf16_t* y;
+  int M, K, N, ldx, ldy, S;
+  float* scratch;
+  int* tickets;
+  int kmajor;
+  const float* rs_part;
+  int rs_nparts;
+  float rs_inv_dim, rs_eps;
+  float* ss_out;
+};
+
+// Dependency hook of a projection body.  The standalone kernels take NoDeps
+// (every input is complete at launch).  In the chained decode launch
+// (decode_chain_kernel below) a body waits for its producers after the
+// workgroup's first W group is in flight -- the weights do not depend on the
+// previous projection, only X does -- and publishes every finished
+// wave-group's output to its consumers.
+struct NoDeps {
+  static constexpr bool chained = false;
+  __device__ void wait(int, int) const {}
+  __device__ void publish(int) const {}
+};
+
+// LDS of the wide body (one struct: the chained launch overlays the bodies of
+// several projections in one buffer).
 template <int MT, int NT, int WV, int EPI>
-__global__ void __launch_bounds__(64 * WV)
-skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int M,
-                   int K, int N, int ldx, int ldy, int S, float* __restrict__ scratch, int* __restrict__ tickets,
-                   int kmajor, const float* __restrict__ rs_part, int rs_nparts, float rs_inv_dim, float rs_eps,
-                   float* __restrict__ ss_out) {
+struct WideLds {
+  static constexpr int U = unroll_wide(NT);
+  static constexpr int PITCH = U * 64 + 8;   // +16 B per row: conflict-free ds_read_b128
+  static constexpr int XBUF = MT * 32 * PITCH;
+  static constexpr bool RS = EPI != EPI_RESID;   // row scales (the residual epilogue produces the sums)
+  alignas(16) bf16_t xs[2 * XBUF];
+  alignas(16) float s_rs[MT * 32];
+  alignas(16) float s_rtmp[RS ? WV * MT * 32 : 4];
+  // EPI_RESID: each wave's residual tile [m][t][32 rows][32 cols], prefetched by LDS-DMA
+  alignas(16) bf16_t s_res[EPI == EPI_RESID ? WV * MT * NT * 32 * 32 : 8];
+  // EPI_RESID: each wave's squares tile for the row sums (wide_epilogue)
+  alignas(16) float s_sq[EPI == EPI_RESID ? WV * MT * 32 * SQ_PITCH : 4];
+};
+
+template <int MT, int NT, int WV, int EPI, class Deps>
+__device__ __forceinline__ void wide_body(const GemmP& p, int block, WideLds<MT, NT, WV, EPI>& L, const Deps& deps) {
   static_assert(EPI != EPI_SILU_MUL || NT == 2, "SiLU*up pairs a gate tile with an up tile");
-  constexpr int U = unroll_wide(NT);
-  constexpr int PITCH = U * 64 + 8;                 // +16 B per row: conflict-free ds_read_b128
-  constexpr int XBUF = MT * 32 * PITCH;
+  using LD = WideLds<MT, NT, WV, EPI>;
+  constexpr int U = LD::U;
+  constexpr int PITCH = LD::PITCH;
+  constexpr int XBUF = LD::XBUF;
   constexpr int NTHREADS = 64 * WV;
   constexpr int XC = MT * U * 256 / NTHREADS;       // X chunks per thread per group
   static_assert(XC * NTHREADS == MT * U * 256, "X tile must split evenly over the workgroup");
-  __shared__ __attribute__((aligned(16))) bf16_t xs[2 * XBUF];
-  // row scales (not for EPI_RESID: that epilogue is the producer of the sums)
-  constexpr bool RS = EPI != EPI_RESID;
-  __shared__ float s_rs[MT * 32];
-  __shared__ float s_rtmp[RS ? WV * MT * 32 : 1];
-  // EPI_RESID: each wave's residual tile [m][t][32 rows][32 cols], prefetched by LDS-DMA
-  __shared__ __attribute__((aligned(16))) bf16_t s_res[EPI == EPI_RESID ? WV * MT * NT * 32 * 32 : 2];
-  // EPI_RESID: each wave's squares tile for the row sums (wide_epilogue)
-  __shared__ __attribute__((aligned(16))) float s_sq[EPI == EPI_RESID ? WV * MT * 32 * SQ_PITCH : 4];
+  constexpr bool RS = LD::RS;
+  const u32x4_t* __restrict__ wp = p.wp;
+  const bf16_t* __restrict__ x = p.x;
+  bf16_t* __restrict__ y = p.y;
+  const int M = p.M, ldx = p.ldx, ldy = p.ldy, S = p.S;
+  bf16_t* xs = L.xs;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
-  const int KB = K >> 6;
-  const int wg = blockIdx.x / S, split = blockIdx.x % S;
+  const int KB = p.K >> 6;
+  const int wg = block / S, split = block % S;
   const int vgroup = wg * WV + wave;
   const int tile0 = vgroup * NT;
-  const WStride ws = kmajor ? WStride{256, (size_t)(N >> 5) * 256} : WStride{(size_t)KB * 256, 256};
+  const WStride ws = p.kmajor ? WStride{256, (size_t)(p.N >> 5) * 256} : WStride{(size_t)KB * 256, 256};
   const u32x4_t* wbase = wp + (size_t)tile0 * ws.tile;
   const int kb0 = (int)((long long)KB * split / S), kb1 = (int)((long long)KB * (split + 1) / S);
   const int G = (kb1 - kb0) / U;                    // the plan makes (kb1 - kb0) a multiple of U, >= U
@@ -712,14 +751,22 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
   // Row-scale slot loads are issued first and reduced after the first X/W
   // loads are in flight (vmcnt retires in order: the reduction waits only for
   // them); the barrier below publishes s_rs.
-  const float* rs = (RS && rs_part) ? s_rs : nullptr;
-  bf16_t* res_lds = s_res + (EPI == EPI_RESID ? wave * (MT * NT * 32 * 32) : 0);
+  const float* rs = (RS && p.rs_part) ? L.s_rs : nullptr;
+  bf16_t* res_lds = L.s_res + (EPI == EPI_RESID ? wave * (MT * NT * 32 * 32) : 0);
+  if constexpr (Deps::chained) {
+    // chained: this wave-group's first W group goes out before the wait on
+    // the producers (the polling wave issues its own after the wait: the
+    // acquire drains its loads)
+    if (wave != WV - 1) wide_load_w<NT, U>(fa, wbase, ws, kb0, lane);
+    deps.wait(WV - 1, split);
+    if (wave == WV - 1) wide_load_w<NT, U>(fa, wbase, ws, kb0, lane);
+  }
   {
     // row-scale slot loads and the residual tile's LDS-DMA first: older than
     // the X loads, so the X wait below covers them as well
     float4 rsv[RS ? RS_LMAX : 1];
     if constexpr (RS) {
-      if (rs_part) rs_issue<MT, NTHREADS>(rsv, rs_part, rs_nparts, tid);
+      if (p.rs_part) rs_issue<MT, NTHREADS>(rsv, p.rs_part, p.rs_nparts, tid);
     }
     if constexpr (EPI == EPI_RESID) {
       // tile (m, t): 32 rows x 64 B, 4 rows per instruction, lane = (row, 4-byte column pair)
@@ -736,10 +783,10 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
     }
     u32x4_t xr[XC];
     wide_load_x<MT, U, XC>(xr, x, M, ldx, kb0, tid, NTHREADS);
-    wide_load_w<NT, U>(fa, wbase, ws, kb0, lane);
+    if constexpr (!Deps::chained) wide_load_w<NT, U>(fa, wbase, ws, kb0, lane);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (RS) {
-      if (rs_part) rs_finish<MT, NTHREADS>(rsv, rs_inv_dim, rs_eps, s_rs, s_rtmp, tid);
+      if (p.rs_part) rs_finish<MT, NTHREADS>(rsv, p.rs_inv_dim, p.rs_eps, L.s_rs, L.s_rtmp, tid);
     }
     wide_store_x<MT, U, XC, PITCH>(xs, xr, tid, NTHREADS);
     __syncthreads();
@@ -761,17 +808,19 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
                                            r, h);
   }
 
+  float* sq = L.s_sq + wave * (EPI == EPI_RESID ? MT * 32 * SQ_PITCH : 0);
   if constexpr (EPI == EPI_RESID) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // residual tile landed
   if (S == 1) {
     wide_epilogue<MT, NT, EPI>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, vgroup, r, h,
-                               rs, ss_out, res_lds, s_sq + wave * (EPI == EPI_RESID ? MT * 32 * SQ_PITCH : 0));
+                               rs, p.ss_out, res_lds, sq);
+    deps.publish(vgroup);
     return;
   }
   // Inter-workgroup split, per wave: add the tile into this wave-group's fp32
   // slab (lane-major, so the adds and the final reads are coalesced), drain,
   // take a ticket; the last of the S arrivals finishes and re-zeroes.
   constexpr int SLAB = MT * NT * 16 * 64;
-  float* sc = scratch + (size_t)vgroup * SLAB;
+  float* sc = p.scratch + (size_t)vgroup * SLAB;
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -780,7 +829,7 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
       for (int e = 0; e < 16; ++e) atomicAdd(sc + ((m * NT + t) * 16 + e) * 64 + lane, acc[m][t][e]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   int ticket = 0;
-  if (lane == 0) ticket = atomicAdd(tickets + vgroup, 1);
+  if (lane == 0) ticket = atomicAdd(p.tickets + vgroup, 1);
   ticket = __shfl(ticket, 0, 64);
   if (ticket != S - 1) return;
   wide_epilogue<MT, NT, EPI>(
@@ -788,10 +837,17 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
         return __hip_atomic_load(sc + ((m * NT + t) * 16 + e) * 64 + lane, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
       },
-      y, M, ldy, tile0, vgroup, r, h, rs, ss_out, res_lds, s_sq + wave * (EPI == EPI_RESID ? MT * 32 * SQ_PITCH : 0));
+      y, M, ldy, tile0, vgroup, r, h, rs, p.ss_out, res_lds, sq);
 #pragma unroll
   for (int i = 0; i < SLAB / 64; ++i) sc[i * 64 + lane] = 0.f;
-  if (lane == 0) tickets[vgroup] = 0;
+  if (lane == 0) p.tickets[vgroup] = 0;
+  deps.publish(vgroup);
+}
+
+template <int MT, int NT, int WV, int EPI>
+__global__ void __launch_bounds__(64 * WV) skinny_wide_kernel(GemmP p) {
+  __shared__ WideLds<MT, NT, WV, EPI> lds;
+  wide_body<MT, NT, WV, EPI>(p, blockIdx.x, lds, NoDeps{});
 }
 
 // ============================================================================
@@ -813,37 +869,50 @@ skinny_wide_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x,
 // scales the rows of a store by the producer's slots (rs_issue / rs_finish).
 // NT = 2 with EPI_SILU_MUL: a gate tile and its up tile (gate_up), both
 // carried by every k-wave, SiLU(gate)*up by the reducing wave.
-template <int MT, int NT, int KW, int EPI, bool COMB = false>
-__global__ void __launch_bounds__(64 * KW)
-skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int M,
-                    int K, int N, int ldx, int ldy, int S, float* __restrict__ scratch, int* __restrict__ tickets,
-                    int kmajor, const float* __restrict__ rs_part, int rs_nparts, float rs_inv_dim, float rs_eps,
-                    float* __restrict__ ss_out, XComb xcomb) {
+template <int MT, int NT, int KW, int EPI>
+struct WidekLds {
+  static constexpr int U = 2;                        // k-blocks per wave per group
+  static constexpr int GK = KW * U;                  // k-blocks per group (the X tile)
+  static constexpr int PITCH = GK * 64 + 8;          // +16 B per row: conflict-free ds_read_b128
+  static constexpr int XBUF = MT * 32 * PITCH;
+  static constexpr bool RS = EPI != EPI_RESID;
+  alignas(16) bf16_t xs[2 * XBUF];
+  alignas(16) float s_rs[MT * 32];
+  alignas(16) float s_rtmp[RS ? KW * MT * 32 : 4];
+  // EPI_RESID: the old residual tile [m][32 rows][32 cols], prefetched by wave 0
+  alignas(16) bf16_t s_res[EPI == EPI_RESID ? MT * 32 * 32 : 8];
+};
+
+template <int MT, int NT, int KW, int EPI, bool COMB, class Deps>
+__device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<MT, NT, KW, EPI>& L,
+                                           const XComb& xcomb, const Deps& deps) {
   static_assert((EPI == EPI_SILU_MUL) == (NT == 2) && NT <= 2, "widek: one tile, or a gate/up pair for SiLU*up");
-  constexpr int U = 2;                               // k-blocks per wave per group
-  constexpr int GK = KW * U;                         // k-blocks per group (the X tile)
-  constexpr int PITCH = GK * 64 + 8;                 // +16 B per row: conflict-free ds_read_b128
-  constexpr int XBUF = MT * 32 * PITCH;
+  static_assert(!(COMB && Deps::chained), "the X-combine variant runs standalone");
+  using LD = WidekLds<MT, NT, KW, EPI>;
+  constexpr int U = LD::U;
+  constexpr int GK = LD::GK;
+  constexpr int PITCH = LD::PITCH;
+  constexpr int XBUF = LD::XBUF;
   constexpr int NTHREADS = 64 * KW;
   constexpr int XC = MT * GK * 256 / NTHREADS;       // X chunks per thread per group
   static_assert(XC * NTHREADS == MT * GK * 256, "X tile must split evenly over the workgroup");
   static_assert(KW * MT * NT * 16 * 64 * 4 <= 2 * XBUF * 2, "the k-wave reduction reuses the X buffers");
   static_assert((KW * MT * NT * 16 * 64 + MT * 32 * SQ_PITCH) * 4 <= 2 * XBUF * 2,
                 "the residual epilogue's squares tile follows the reduction in the X buffers");
-  __shared__ __attribute__((aligned(16))) bf16_t xs[2 * XBUF];
-  constexpr bool RS = EPI != EPI_RESID;
-  __shared__ float s_rs[MT * 32];
-  __shared__ float s_rtmp[RS ? KW * MT * 32 : 1];
-  // EPI_RESID: the old residual tile [m][32 rows][32 cols], prefetched by wave 0
-  __shared__ __attribute__((aligned(16))) bf16_t s_res[EPI == EPI_RESID ? MT * 32 * 32 : 2];
+  constexpr bool RS = LD::RS;
+  const u32x4_t* __restrict__ wp = p.wp;
+  const bf16_t* __restrict__ x = p.x;
+  bf16_t* __restrict__ y = p.y;
+  const int M = p.M, ldx = p.ldx, ldy = p.ldy, S = p.S;
+  bf16_t* xs = L.xs;
   const int tid = threadIdx.x;
   const int kw = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
-  const int KB = K >> 6;
-  const int vgroup = blockIdx.x / S, split = blockIdx.x % S;
+  const int KB = p.K >> 6;
+  const int vgroup = block / S, split = block % S;
   const int tile0 = vgroup * NT;
-  const float* rs = (RS && rs_part) ? s_rs : nullptr;
-  const WStride ws = kmajor ? WStride{256, (size_t)(N >> 5) * 256} : WStride{(size_t)KB * 256, 256};
+  const float* rs = (RS && p.rs_part) ? L.s_rs : nullptr;
+  const WStride ws = p.kmajor ? WStride{256, (size_t)(p.N >> 5) * 256} : WStride{(size_t)KB * 256, 256};
   const u32x4_t* wbase = wp + (size_t)tile0 * ws.tile;
   const int kb0 = (int)((long long)KB * split / S), kb1 = (int)((long long)KB * (split + 1) / S);
   const int G = (kb1 - kb0) / GK;                    // the plan makes (kb1 - kb0) a multiple of GK, >= GK
@@ -857,12 +926,19 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
       for (int e = 0; e < 16; ++e) acc[m][t][e] = 0.f;
 
   WFrag<NT> fa[U], fb[U];
+  if constexpr (Deps::chained) {
+    // chained: the first W group before the wait on the producers (the
+    // polling wave issues its own after it)
+    if (kw != KW - 1) wide_load_w<NT, U>(fa, wbase, ws, kb0 + kw * U, lane);
+    deps.wait(KW - 1, split);
+    if (kw == KW - 1) wide_load_w<NT, U>(fa, wbase, ws, kb0 + kw * U, lane);
+  }
   {
     // row-scale slot loads and the residual tile's LDS-DMA first: older than
     // the X loads, so the X wait below covers them as well
     float4 rsv[RS ? RS_LMAX : 1];
     if constexpr (RS) {
-      if (rs_part) rs_issue<MT, NTHREADS>(rsv, rs_part, rs_nparts, tid);
+      if (p.rs_part) rs_issue<MT, NTHREADS>(rsv, p.rs_part, p.rs_nparts, tid);
     }
     if constexpr (EPI == EPI_RESID) {
       if (kw == 0) {
@@ -872,7 +948,7 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
           for (int i = 0; i < 8; ++i) {
             const int row = m * 32 + 4 * i + (lane >> 4);
             const bf16_t* g = y + (size_t)min(row, M - 1) * ldy + (size_t)tile0 * 32 + 2 * (lane & 15);
-            __builtin_amdgcn_global_load_lds(g, s_res + (m * 32 + 4 * i) * 32, 4, 0, 0);
+            __builtin_amdgcn_global_load_lds(g, L.s_res + (m * 32 + 4 * i) * 32, 4, 0, 0);
           }
       }
     }
@@ -882,9 +958,9 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
       // with no X hand-overs
       wide_load_w<NT, U>(fa, wbase, ws, kb0 + kw * U, lane);
       __builtin_amdgcn_sched_barrier(0);
-      xcomb_row(xs, xcomb, K, tid, NTHREADS);
+      xcomb_row(xs, xcomb, p.K, tid, NTHREADS);
       if constexpr (RS) {
-        if (rs_part) rs_finish<MT, NTHREADS>(rsv, rs_inv_dim, rs_eps, s_rs, s_rtmp, tid);
+        if (p.rs_part) rs_finish<MT, NTHREADS>(rsv, p.rs_inv_dim, p.rs_eps, L.s_rs, L.s_rtmp, tid);
       }
       __syncthreads();
       auto stepc = [&](const WFrag<NT>(&cur)[U], WFrag<NT>(&nxt)[U], int kb, bool prefetch) {
@@ -907,10 +983,10 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
     } else {
       u32x4_t xr[XC];
       wide_load_x<MT, GK, XC>(xr, x, M, ldx, kb0, tid, NTHREADS);
-      wide_load_w<NT, U>(fa, wbase, ws, kb0 + kw * U, lane);
+      if constexpr (!Deps::chained) wide_load_w<NT, U>(fa, wbase, ws, kb0 + kw * U, lane);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (RS) {
-        if (rs_part) rs_finish<MT, NTHREADS>(rsv, rs_inv_dim, rs_eps, s_rs, s_rtmp, tid);
+        if (p.rs_part) rs_finish<MT, NTHREADS>(rsv, p.rs_inv_dim, p.rs_eps, L.s_rs, L.s_rtmp, tid);
       }
       wide_store_x<MT, GK, XC, PITCH>(xs, xr, tid, NTHREADS);
       __syncthreads();
@@ -970,11 +1046,12 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
   if constexpr (EPI == EPI_RESID) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // residual tile landed
   if (S == 1) {
     wide_epilogue<MT, NT, EPI>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, vgroup, r, h,
-                               rs, ss_out, s_res, red + KW * MT * NT * 16 * 64);
+                               rs, p.ss_out, L.s_res, red + KW * MT * NT * 16 * 64);
+    deps.publish(vgroup);
     return;
   }
   constexpr int SLAB = MT * NT * 16 * 64;
-  float* sc = scratch + (size_t)vgroup * SLAB;
+  float* sc = p.scratch + (size_t)vgroup * SLAB;
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -983,17 +1060,142 @@ skinny_widek_kernel(const u32x4_t* __restrict__ wp, const bf16_t* __restrict__ x
       for (int e = 0; e < 16; ++e) atomicAdd(sc + ((m * NT + t) * 16 + e) * 64 + lane, acc[m][t][e]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   int ticket = 0;
-  if (lane == 0) ticket = atomicAdd(tickets + vgroup, 1);
+  if (lane == 0) ticket = atomicAdd(p.tickets + vgroup, 1);
   ticket = __shfl(ticket, 0, 64);
   if (ticket != S - 1) return;
   wide_epilogue<MT, NT, EPI>(
       [&](int m, int t, int e) {
         return __hip_atomic_load(sc + ((m * NT + t) * 16 + e) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       },
-      y, M, ldy, tile0, vgroup, r, h, rs, ss_out, s_res, red + KW * MT * NT * 16 * 64);
+      y, M, ldy, tile0, vgroup, r, h, rs, p.ss_out, L.s_res, red + KW * MT * NT * 16 * 64);
 #pragma unroll
   for (int i = 0; i < SLAB / 64; ++i) sc[i * 64 + lane] = 0.f;
-  if (lane == 0) tickets[vgroup] = 0;
+  if (lane == 0) p.tickets[vgroup] = 0;
+  deps.publish(vgroup);
+}
+
+template <int MT, int NT, int KW, int EPI, bool COMB = false>
+__global__ void __launch_bounds__(64 * KW) skinny_widek_kernel(GemmP p, XComb xcomb) {
+  __shared__ WidekLds<MT, NT, KW, EPI> lds;
+  widek_body<MT, NT, KW, EPI, COMB>(p, blockIdx.x, lds, xcomb, NoDeps{});
+}
+
+// ============================================================================
+// Chained decode projections: o_proj (+ residual) -> gate_up (+ SiLU*up) ->
+// down (+ residual) -> the next layer's qkv in ONE launch.  Separately, each of
+// these kernels pays its own ramp and drain: the first W bytes arrive ~2 us
+// after the launch and the last workgroups finish alone, ~4-5 us per launch
+// (profiles/README.md section 35).  Here the four bodies run as consecutive
+// block ranges of one grid.  A workgroup of a later projection is dispatched
+// as soon as a CU frees up in the previous one's tail, issues its first W
+// group (the weights do not depend on the previous projection), and only then
+// waits for the inputs it reads:
+//   * gate_up waits for every o_proj tile (its X is the whole residual row and
+//     its row scales are o_proj's sum-of-squares slots);
+//   * down split s waits only for the gate_up channel blocks of its k-range;
+//   * qkv waits for every down tile.
+// Hand-off (MI355X_MICROARCH.md, persistent kernels): the producing wave
+// releases at agent scope (L2 write-back), drains, then bumps a device-scope
+// counter; one lane of the consumer polls it with relaxed loads and s_sleep,
+// then acquires at agent scope (L2 invalidate) before the workgroup barrier.
+// Deadlock freedom: a workgroup only waits on lower block ranges, and each
+// XCD dispatches its workgroups in block order, so every producer a resident
+// consumer waits for has been dispatched ahead of it.  Spins are bounded
+// (CHAIN_SPIN_TICKS of the 100 MHz real-time counter): a give-up sets the
+// error word and the launch completes (wrong output, reported, never a hang).
+// The last workgroup to finish re-zeroes the counters for the next launch.
+constexpr int CHAIN_PROJ = 4;
+constexpr int CHAIN_MAX_SPLITS = 8;
+enum { CTR_O = 0, CTR_D = 1, CTR_FIN = 2, CTR_ERR = 3, CTR_GU = 4, CTR_WORDS = CTR_GU + CHAIN_MAX_SPLITS };
+constexpr unsigned long long CHAIN_SPIN_TICKS = 5000000ull;   // 50 ms
+
+struct ChainDeps {
+  static constexpr bool chained = true;
+  int* wait_ctr;     // counter(s) to wait on (nullptr: none)
+  int wait_target;   // units published per counter
+  int wait_split;    // one counter per split of this projection's k-range
+  int* pub_ctr;      // counter(s) this projection publishes to (nullptr: none)
+  int pub_div;       // units per counter (0: all units to one counter)
+  int* err;
+
+  __device__ void wait(int poll_wave, int split) const {
+    if (wait_ctr == nullptr) return;
+    if ((int)(threadIdx.x >> 6) == poll_wave) {
+      if ((threadIdx.x & 63) == 0) {
+        const int* c = wait_ctr + (wait_split ? split : 0);
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wait_target) {
+          __builtin_amdgcn_s_sleep(2);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > CHAIN_SPIN_TICKS) {
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  }
+
+  __device__ void publish(int unit) const {
+    if (pub_ctr == nullptr) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // inline asm: the compiler drops the wait after the write-back when it
+    // believes the wave's counter is already empty (MI355X_MICROARCH.md)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if ((threadIdx.x & 63) == 0)
+      __hip_atomic_fetch_add(pub_ctr + (pub_div ? unit / pub_div : 0), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+};
+
+struct ChainArgs {
+  GemmP g[CHAIN_PROJ];          // o_proj, gate_up, down, qkv
+  int nblk[CHAIN_PROJ];         // workgroups of each (0: absent)
+  int wait_target[CHAIN_PROJ];  // producer units each one waits for (0: no wait)
+  int gu_div;                   // gate_up units per down split
+  int* ctr;                     // CTR_WORDS ints, zero before the first launch (left zero)
+};
+
+template <int a, int b>
+constexpr int cmax() { return a > b ? a : b; }
+
+template <int W>
+__global__ void __launch_bounds__(64 * W) decode_chain_kernel(ChainArgs a) {
+  using L0 = WidekLds<1, 1, W, EPI_RESID>;
+  using L1 = WideLds<1, 2, W, EPI_SILU_MUL>;
+  using L2 = WideLds<1, 1, W, EPI_RESID>;
+  using L3 = WidekLds<1, 1, W, EPI_STORE>;
+  constexpr int LB = cmax<cmax<(int)sizeof(L0), (int)sizeof(L1)>(), cmax<(int)sizeof(L2), (int)sizeof(L3)>()>();
+  __shared__ __attribute__((aligned(16))) char lds[LB];
+  int* c = a.ctr;
+  int b = blockIdx.x;
+  if (b < a.nblk[0]) {
+    widek_body<1, 1, W, EPI_RESID, false>(a.g[0], b, *reinterpret_cast<L0*>(lds), XComb{},
+                                         ChainDeps{nullptr, 0, 0, c + CTR_O, 0, c + CTR_ERR});
+  } else if ((b -= a.nblk[0]) < a.nblk[1]) {
+    wide_body<1, 2, W, EPI_SILU_MUL>(a.g[1], b, *reinterpret_cast<L1*>(lds),
+                                     ChainDeps{a.wait_target[1] ? c + CTR_O : nullptr, a.wait_target[1], 0,
+                                               a.nblk[2] ? c + CTR_GU : nullptr, a.gu_div, c + CTR_ERR});
+  } else if ((b -= a.nblk[1]) < a.nblk[2]) {
+    wide_body<1, 1, W, EPI_RESID>(a.g[2], b, *reinterpret_cast<L2*>(lds),
+                                  ChainDeps{a.wait_target[2] ? c + CTR_GU : nullptr, a.wait_target[2], 1,
+                                            a.nblk[3] ? c + CTR_D : nullptr, 0, c + CTR_ERR});
+  } else {
+    b -= a.nblk[2];
+    widek_body<1, 1, W, EPI_STORE, false>(a.g[3], b, *reinterpret_cast<L3*>(lds), XComb{},
+                                         ChainDeps{a.wait_target[3] ? c + CTR_D : nullptr, a.wait_target[3], 0,
+                                                   nullptr, 0, c + CTR_ERR});
+  }
+  // the last workgroup out re-zeroes the counters (every wait is behind it)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int total = a.nblk[0] + a.nblk[1] + a.nblk[2] + a.nblk[3];
+    if (__hip_atomic_fetch_add(c + CTR_FIN, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
+      for (int i = 0; i < CTR_WORDS; ++i)
+        if (i != CTR_ERR) __hip_atomic_store(c + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // Pack W[N][K] (row-major bf16) into the fragment order above.
@@ -1054,6 +1256,11 @@ struct Args {
   XComb xcomb{};                    // K-split kernel: X from attention split partials (xcomb.o != null)
 };
 
+GemmP gemm_p(const Args& a) {
+  return GemmP{(const u32x4_t*)a.wp, (const bf16_t*)a.x, (bf16_t*)a.y, a.M, a.K, a.N, a.ldx, a.ldy, a.S, a.scratch,
+               a.tickets, a.kmajor, a.rs_part, a.rs_nparts, a.rs_inv_dim, a.rs_eps, a.ss_out};
+}
+
 template <int MT, int NT, int KS, int EPI>
 hipError_t launch(const Args& a, hipStream_t s) {
   const int groups = (a.N / 32) / NT;
@@ -1104,9 +1311,7 @@ template <int MT, int NT, int EPI>
 hipError_t launch_wide(int wv, const Args& a, hipStream_t s) {
   const int blocks = (a.N / 32) / NT / wv * a.S;
 #define MIVGPU_LAUNCH_WIDE(WV)                                                                                \
-  hipLaunchKernelGGL((skinny_wide_kernel<MT, NT, WV, EPI>), dim3(blocks), dim3(64 * WV), 0, s,               \
-                     (const u32x4_t*)a.wp, (const bf16_t*)a.x, (bf16_t*)a.y, a.M, a.K, a.N, a.ldx, a.ldy, a.S, \
-                     a.scratch, a.tickets, a.kmajor, a.rs_part, a.rs_nparts, a.rs_inv_dim, a.rs_eps, a.ss_out)
+  hipLaunchKernelGGL((skinny_wide_kernel<MT, NT, WV, EPI>), dim3(blocks), dim3(64 * WV), 0, s, gemm_p(a))
   switch (wv) {
     case 1: MIVGPU_LAUNCH_WIDE(1); break;
     case 2: MIVGPU_LAUNCH_WIDE(2); break;
@@ -1140,9 +1345,7 @@ template <int MT, int NT, int EPI>
 hipError_t launch_widek(int kw, const Args& a, hipStream_t s) {
   const int blocks = (a.N / 32) / NT * a.S;
 #define MIVGPU_LAUNCH_WIDEK(KW, CC)                                                                                \
-  hipLaunchKernelGGL((skinny_widek_kernel<MT, NT, KW, EPI, CC>), dim3(blocks), dim3(64 * KW), 0, s,               \
-                     (const u32x4_t*)a.wp, (const bf16_t*)a.x, (bf16_t*)a.y, a.M, a.K, a.N, a.ldx, a.ldy, a.S,      \
-                     a.scratch, a.tickets, a.kmajor, a.rs_part, a.rs_nparts, a.rs_inv_dim, a.rs_eps, a.ss_out, a.xcomb)
+  hipLaunchKernelGGL((skinny_widek_kernel<MT, NT, KW, EPI, CC>), dim3(blocks), dim3(64 * KW), 0, s, gemm_p(a), a.xcomb)
   const bool comb = a.xcomb.o != nullptr;
   if constexpr (MT == 1 && NT == 1) {
     if (comb) {
@@ -1542,6 +1745,106 @@ static int skinny_gemm_norm_impl(const void* wp, const void* x, void* y, int M, 
   else
     e = launch_mt<1, EPI_STORE>(mt, ks, a, s);
   return (int)e;
+}
+
+
+// ---------------------------------------------------------------- chain --
+// One projection of mivgpu_decode_chain (layout shared with ops/__init__.py).
+struct MivgpuChainGemm {
+  const void* wp;
+  const void* x;
+  void* y;
+  int M, K, N, ldx, ldy, S;
+  float* scratch;
+  int* tickets;
+  const float* rs_part;
+  int rs_nparts;
+  float rs_inv_dim, rs_eps;
+  float* ss_out;
+};
+
+int mivgpu_chain_counter_words() { return CTR_WORDS; }
+
+// sizeof and field offsets of MivgpuChainGemm (the ctypes mirror is checked
+// against them): size, wp, x, y, M, S, scratch, tickets, rs_part, rs_nparts,
+// rs_eps, ss_out.
+void mivgpu_chain_gemm_layout(long long* out) {
+  const long long v[] = {(long long)sizeof(MivgpuChainGemm), (long long)offsetof(MivgpuChainGemm, wp),
+                         (long long)offsetof(MivgpuChainGemm, x), (long long)offsetof(MivgpuChainGemm, y),
+                         (long long)offsetof(MivgpuChainGemm, M), (long long)offsetof(MivgpuChainGemm, S),
+                         (long long)offsetof(MivgpuChainGemm, scratch), (long long)offsetof(MivgpuChainGemm, tickets),
+                         (long long)offsetof(MivgpuChainGemm, rs_part), (long long)offsetof(MivgpuChainGemm, rs_nparts),
+                         (long long)offsetof(MivgpuChainGemm, rs_eps), (long long)offsetof(MivgpuChainGemm, ss_out)};
+  for (int i = 0; i < (int)(sizeof(v) / sizeof(v[0])); ++i) out[i] = v[i];
+}
+
+// Plan check of one chained projection; blocks of its range, or -1.
+static int chain_blocks(int role, int W, const MivgpuChainGemm& g) {
+  if (g.wp == nullptr) return 0;
+  if (g.M <= 0 || g.M > 32 || g.K <= 0 || (g.K & 63) || g.N <= 0 || (g.N & 31) || g.ldx < g.K || (g.ldx & 7) ||
+      (g.ldy & 7) || g.x == nullptr || g.y == nullptr)
+    return -1;
+  const int rs_max = 64 * W * RS_LMAX / 8;   // rs_issue's slots per batch at MT = 1
+  int nt = 0, w = W, S = g.S;
+  switch (role) {
+    case 0:   // o_proj: K-split kernel, residual update + slots
+      if (g.ss_out == nullptr || g.rs_part != nullptr || g.ldy < g.N || S != 1) return -1;
+      return plan_widek(g.M, g.K, g.N, EPI_STORE, &nt, &w, &S) && w == W ? g.N / 32 : -1;
+    case 1:   // gate_up: wide kernel, SiLU*up, row scales
+      if (g.ss_out != nullptr || S != 1 || g.ldy < g.N / 2 || (g.rs_part && g.rs_nparts > rs_max)) return -1;
+      nt = 2;
+      return plan_wide(g.M, g.K, g.N, EPI_SILU_MUL, &nt, &w, &S) && w == W && nt == 2 ? g.N / 32 / 2 / W : -1;
+    case 2:   // down: wide kernel, residual update + slots, split S
+      if (g.ss_out == nullptr || g.rs_part != nullptr || g.ldy < g.N || S < 1 || S > CHAIN_MAX_SPLITS) return -1;
+      if (S > 1 && (g.scratch == nullptr || g.tickets == nullptr)) return -1;
+      nt = 1;
+      return plan_wide(g.M, g.K, g.N, EPI_STORE, &nt, &w, &S) && w == W && nt == 1 ? g.N / 32 / W * S : -1;
+    case 3:   // qkv: K-split kernel, stores, row scales
+      if (g.ss_out != nullptr || S != 1 || g.ldy < g.N || (g.rs_part && g.rs_nparts > rs_max)) return -1;
+      return plan_widek(g.M, g.K, g.N, EPI_STORE, &nt, &w, &S) && w == W ? g.N / 32 : -1;
+  }
+  return -1;
+}
+
+// One launch of up to four decode projections (o_proj, gate_up, down, qkv;
+// wp == nullptr: absent) on W-wave workgroups (2 or 4).  ctr:
+// mivgpu_chain_counter_words() ints, zero before the first launch and left
+// zero by every launch except word 3, the give-up flag (nonzero: a wait timed
+// out and the output is wrong).  Consecutive projections must chain: gate_up
+// reads o_proj's output and slots, down gate_up's, qkv down's.
+int mivgpu_decode_chain(const MivgpuChainGemm* g, int W, int* ctr, hipStream_t s) {
+  if (g == nullptr || ctr == nullptr || (W != 2 && W != 4)) return (int)hipErrorInvalidValue;
+  ChainArgs a{};
+  for (int r = 0; r < CHAIN_PROJ; ++r) {
+    const int nb = chain_blocks(r, W, g[r]);
+    if (nb < 0) return (int)hipErrorInvalidValue;
+    a.nblk[r] = nb;
+    const MivgpuChainGemm& q = g[r];
+    a.g[r] = GemmP{(const u32x4_t*)q.wp, (const bf16_t*)q.x, (bf16_t*)q.y, q.M, q.K, q.N, q.ldx, q.ldy,
+                   q.S > 0 ? q.S : 1, q.scratch, q.tickets, use_kmajor() ? 1 : 0, q.rs_part, q.rs_nparts,
+                   q.rs_inv_dim, q.rs_eps, q.ss_out};
+  }
+  // producer -> consumer: each must read what the previous one wrote
+  if (a.nblk[0] && a.nblk[1] && (g[1].x != g[0].y || g[1].rs_part != g[0].ss_out || g[1].K != g[0].N)) return (int)hipErrorInvalidValue;
+  if (a.nblk[1] && a.nblk[2] && (g[2].x != g[1].y || g[2].K != g[1].N / 2)) return (int)hipErrorInvalidValue;
+  if (a.nblk[2] && a.nblk[3] && (g[3].x != g[2].y || g[3].rs_part != g[2].ss_out || g[3].K != g[2].N)) return (int)hipErrorInvalidValue;
+  if (a.nblk[1] && !a.nblk[0] && a.nblk[2] + a.nblk[3] == 0) return (int)hipErrorInvalidValue;   // use the plain launch
+  a.wait_target[1] = a.nblk[0] && a.nblk[1] ? g[0].N / 32 : 0;
+  if (a.nblk[1] && a.nblk[2]) {
+    // gate_up vgroup v writes act channels [32v, 32v + 32) = down k-block v / 2
+    const int kb_per_split = (g[2].K / 64) / a.g[2].S;
+    a.gu_div = 2 * kb_per_split;
+    a.wait_target[2] = a.gu_div;
+  }
+  a.wait_target[3] = a.nblk[2] && a.nblk[3] ? g[2].N / 32 : 0;
+  a.ctr = ctr;
+  const int blocks = a.nblk[0] + a.nblk[1] + a.nblk[2] + a.nblk[3];
+  if (blocks == 0) return 0;
+  if (W == 2)
+    hipLaunchKernelGGL(decode_chain_kernel<2>, dim3(blocks), dim3(128), 0, s, a);
+  else
+    hipLaunchKernelGGL(decode_chain_kernel<4>, dim3(blocks), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
 }
 
 }  // extern "C"

@@ -41,7 +41,10 @@ def main():
     dt = time.perf_counter() - t0
     weight_bytes = cfg.param_count() * 2
     kv_bytes = 2 * cfg.layers * a.batch * cfg.kv_heads * (a.ctx + a.warmup + a.steps // 2) * cfg.head_dim * 2
-    print(json.dumps({"batch": a.batch, "ctx": a.ctx, "skinny_gemm": dec.skinny, "ms_per_step": dt / a.steps * 1e3,
+    gave_up = bool(dec._chains and dec._chains[0].gave_up())
+    print(json.dumps({"batch": a.batch, "ctx": a.ctx, "skinny_gemm": dec.skinny, "chain": dec.chain,
+                      "chain_w": dec.chain_w if dec.chain else None, "chain_gave_up": gave_up,
+                      "ms_per_step": dt / a.steps * 1e3,
                       "tok_s": a.batch * a.steps / dt,
                       "hbm_gbps_lower_bound": (weight_bytes + kv_bytes) * a.steps / dt / 1e9}))
 

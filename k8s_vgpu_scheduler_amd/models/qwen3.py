@@ -221,10 +221,24 @@ class Qwen3Decoder:
         self.logits = torch.zeros(batch, cfg.vocab, dtype=dt, device=self.device)
         if self.norm_fused or self.skinny_qkv:
             self.qkv_buf = torch.zeros(batch, cfg.qkv_dim, dtype=dt, device=self.device)
+        # Chained projections (MIVGPU_CHAIN=1, norm fusion, batch <= 32):
+        # o_proj -> gate_up -> down -> the next layer's qkv as one launch whose
+        # workgroups wait in-kernel for their inputs (ops.DecodeChain), two
+        # launches per layer with the attention.  MIVGPU_CHAIN_W: waves per
+        # workgroup (2: gate_up / down at their tuned wide plans, o_proj / qkv
+        # on 2-wave K-split workgroups); MIVGPU_CHAIN_DOWN_S: down's k-split.
+        self.chain = (self.norm_fused and batch <= 32 and os.environ.get("MIVGPU_CHAIN", "0") == "1")
+        self.chain_w = int(os.environ.get("MIVGPU_CHAIN_W", "2"))
+        self.chain_down_s = int(os.environ.get("MIVGPU_CHAIN_DOWN_S", "4"))
         if self.norm_fused:
             l0 = self.w.layers[0]
             self.slots_o, self.slots_d = l0["po"].slots(batch), l0["pd"].slots(batch)
             n = max(self.slots_o, self.slots_d, 1) * ops.SS_ROWS
+            if self.chain:
+                # the chain's o_proj (K-split) and down (wide, one tile per
+                # wave) write one slot per 32-column tile
+                self.chain_slots_o, self.chain_slots_d = l0["po"].N // 32, l0["pd"].N // 32
+                n = max(n, self.chain_slots_o * ops.SS_ROWS, self.chain_slots_d * ops.SS_ROWS)
             self.ss_a = torch.zeros(n, dtype=torch.float32, device=self.device)   # before qkv / lm_head
             self.ss_b = torch.zeros(n, dtype=torch.float32, device=self.device)   # before gate_up
             self.ss_pf = torch.zeros(ops.SS_ROWS, dtype=torch.float32, device=self.device)   # prefill chunks
@@ -252,11 +266,12 @@ class Qwen3Decoder:
         # combine launch (profiles/README.md section 36).  MIVGPU_ATTN_XCOMB=0
         # keeps the combine kernel.
         self.xcomb = None
-        if (self.norm_fused and self.attn_fused and 1 < self.nsplit <= 8
+        if (self.norm_fused and self.attn_fused and 1 < self.nsplit <= 8 and not self.chain
                 and self.nsplit == math.ceil(self.T / ops.attn_split())
                 and os.environ.get("MIVGPU_ATTN_XCOMB", "1") != "0"
                 and self.w.layers[0]["po"].xcomb_ok(batch)):
             self.xcomb = (self.o_part, self.ml_part, self.seqlens, self.nsplit, ops.attn_split(), self.T, cfg.heads)
+        self._chains = self._build_chains() if self.chain else None
         self.graph = None
         self._tail_work = ops.decode_tail_workspace(batch, self.device) if self.native else None
         self._pf = {}          # prefill bucket length -> static buffers (+ captured graph)
@@ -331,7 +346,41 @@ class Qwen3Decoder:
         self._tail(logits)
         return logits
 
+    def _build_chains(self) -> list:
+        """One ops.DecodeChain per layer: [o_proj, gate_up, down] of layer li
+        and the qkv of layer li + 1 (the last layer's chain ends at down)."""
+        cfg, h, eps = self.cfg, self.cfg.hidden, self.cfg.eps
+        ctr = ops.chain_counters(self.device)
+        chains = []
+        for li, lw in enumerate(self.w.layers):
+            nxt = self.w.layers[li + 1] if li + 1 < cfg.layers else None
+            chains.append(ops.DecodeChain(
+                o=dict(pl=lw["po"], x=self.attn, y=self.res, ss=self.ss_b),
+                gu=dict(pl=lw["pgu"], x=self.res, y=self.act, rs=(self.ss_b, self.chain_slots_o, h, eps)),
+                d=dict(pl=lw["pd"], x=self.act, y=self.res, ss=self.ss_a),
+                qkv=(dict(pl=nxt["pqkv"], x=self.res, y=self.qkv_buf, rs=(self.ss_a, self.chain_slots_d, h, eps))
+                     if nxt is not None else None),
+                W=self.chain_w, down_splits=self.chain_down_s, ctr=ctr))
+        return chains
+
+    def _step_chained(self):
+        """Norm-fused decode step with chained projections: per layer the
+        attention launch and one chain launch (o_proj, gate_up, down, next qkv)."""
+        cfg, w = self.cfg, self.w
+        h, eps = cfg.hidden, cfg.eps
+        ops.embed_rmsnorm(w.embed, self.tokens, None, cfg.eps, res=self.res, out=None, ss_out=self.ss_a)
+        w.layers[0]["pqkv"].norm_call(self.res, out=self.qkv_buf, row_scale=(self.ss_a, 1, h, eps))
+        for li, lw in enumerate(w.layers):
+            self._attention(li, lw, self.qkv_buf)
+            self._chains[li]()
+        ops.rmsnorm(self.res, w.final_norm, eps, out=self.h)
+        logits = self.p_lm(self.h, out=self.logits)
+        self._tail(logits)
+        return logits
+
     def _step_impl(self):
+        if self.chain:
+            return self._step_chained()
         if self.norm_fused:
             return self._step_norm_fused()
         cfg, w = self.cfg, self.w

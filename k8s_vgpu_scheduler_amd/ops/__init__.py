@@ -62,16 +62,27 @@ def lib():
         L.mivgpu_stream_copy.argtypes = [vp, vp, ctypes.c_longlong, i, vp]
         L.mivgpu_stream_read.argtypes = [vp, ctypes.c_longlong, vp, i, vp]
         L.mivgpu_skinny_plan.argtypes = [i, i, i, i, ip, ip, ip, lp, ip, ip]
+        L.mivgpu_decode_chain.argtypes = [ctypes.POINTER(ChainGemm), i, vp, vp]
         for fn in ("mivgpu_rmsnorm", "mivgpu_add_rmsnorm", "mivgpu_qk_norm_rope_kv",
                    "mivgpu_decode_attention", "mivgpu_silu_mul", "mivgpu_ops_attn_split",
                    "mivgpu_hwid_probe", "mivgpu_pack_weight", "mivgpu_skinny_gemm",
                    "mivgpu_skinny_max_m", "mivgpu_skinny_plan", "mivgpu_mfma_burn",
                    "mivgpu_stream_copy", "mivgpu_stream_read", "mivgpu_ops_visible_cus",
                    "mivgpu_ops_kv_packed", "mivgpu_decode_attention_fused", "mivgpu_skinny_gemm_norm",
-                   "mivgpu_prefill_qk_norm_rope_kv", "mivgpu_prefill_attention", "mivgpu_unpack_weight"):
+                   "mivgpu_prefill_qk_norm_rope_kv", "mivgpu_prefill_attention", "mivgpu_unpack_weight",
+                   "mivgpu_decode_chain", "mivgpu_chain_counter_words"):
             getattr(L, fn).restype = ctypes.c_int
         _lib = L
     return _lib
+
+
+class ChainGemm(ctypes.Structure):
+    """One projection of mivgpu_decode_chain (csrc/ops/skinny_gemm.hip MivgpuChainGemm)."""
+    _fields_ = [("wp", ctypes.c_void_p), ("x", ctypes.c_void_p), ("y", ctypes.c_void_p),
+                ("M", ctypes.c_int), ("K", ctypes.c_int), ("N", ctypes.c_int), ("ldx", ctypes.c_int),
+                ("ldy", ctypes.c_int), ("S", ctypes.c_int), ("scratch", ctypes.c_void_p),
+                ("tickets", ctypes.c_void_p), ("rs_part", ctypes.c_void_p), ("rs_nparts", ctypes.c_int),
+                ("rs_inv_dim", ctypes.c_float), ("rs_eps", ctypes.c_float), ("ss_out", ctypes.c_void_p)]
 
 
 def available() -> bool:
@@ -644,3 +655,70 @@ class PackedLinear:
                                              inv_dim, eps, _p(ss_out) if residual else None, _stream()),
                "skinny_gemm_norm")
         return out
+
+
+# ------------------------------------------------------ chained launch --
+def chain_counter_words() -> int:
+    return int(lib().mivgpu_chain_counter_words())
+
+
+def chain_counters(device) -> torch.Tensor:
+    """Zeroed counters of one chained launch sequence (left zero by every
+    launch except word 3, the give-up flag: nonzero = a wait timed out)."""
+    return torch.zeros(chain_counter_words(), dtype=torch.int32, device=device)
+
+
+CHAIN_ERR_WORD = 3
+
+
+class DecodeChain:
+    """o_proj (+ residual) -> gate_up (+ SiLU*up) -> down (+ residual) -> the
+    next layer's qkv as ONE launch (csrc/ops/skinny_gemm.hip
+    decode_chain_kernel): each projection's workgroups are dispatched in the
+    previous one's tail, issue their first weight loads, and wait in-kernel
+    for the producers of their inputs -- one ramp and drain instead of four.
+    Every buffer is bound at construction (static decode buffers), so a call
+    is one C call (and one node of a captured graph).
+
+    Each projection is ``(pl, x, y)`` plus ``rs=(slots, nparts, dim, eps)``
+    (row scales, gate_up / qkv) or ``ss=slots`` (residual update, o_proj /
+    down); ``None`` leaves it out.  ``W``: waves per workgroup (2 or 4);
+    ``down_splits``: the down projection's inter-workgroup k-split."""
+
+    def __init__(self, o=None, gu=None, d=None, qkv=None, W: int = 2, down_splits: int = 4, ctr=None):
+        self.W = W
+        arr = (ChainGemm * 4)()
+        self._keep = []
+        for i, spec in enumerate((o, gu, d, qkv)):
+            if spec is None:
+                continue
+            pl, x, y = spec["pl"], spec["x"], spec["y"]
+            M = x.shape[0]
+            S = down_splits if i == 2 else 1
+            if S > 1:
+                plan = skinny_plan(M, pl.K, pl.N, EPI_STORE, nt=1, ks=W, S=S, variant=VARIANT_WIDE)
+                pl._ensure_scratch(plan["scratch_floats"], plan["tickets"], x.device)
+            g = arr[i]
+            g.wp, g.x, g.y = self._ptr(pl.wp), self._ptr(x), self._ptr(y)
+            g.M, g.K, g.N, g.ldx, g.ldy, g.S = M, pl.K, pl.N, x.stride(0), y.stride(0), S
+            g.scratch = self._ptr(pl.scratch) if S > 1 else None
+            g.tickets = self._ptr(pl.tickets) if S > 1 else None
+            if spec.get("rs") is not None:
+                part, nparts, dim, eps = spec["rs"]
+                g.rs_part, g.rs_nparts, g.rs_inv_dim, g.rs_eps = self._ptr(part), nparts, 1.0 / dim, eps
+            if spec.get("ss") is not None:
+                g.ss_out = self._ptr(spec["ss"])
+            self._keep.append(spec)
+        self.arr = arr
+        dev = (o or gu or d or qkv)["x"].device
+        self.ctr = chain_counters(dev) if ctr is None else ctr
+
+    def _ptr(self, t):
+        self._keep.append(t)
+        return t.data_ptr()
+
+    def __call__(self):
+        _check(lib().mivgpu_decode_chain(self.arr, self.W, _p(self.ctr), _stream()), "decode_chain")
+
+    def gave_up(self) -> bool:
+        return int(self.ctr[CHAIN_ERR_WORD].item()) != 0

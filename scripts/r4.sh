@@ -27,6 +27,13 @@ for s in "$@"; do
     ttft) for n in 512 2048 8000; do
             run 400 "ttft_$n" python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len $n --ctx 8192 --iters 5
           done ;;
+    chain) run 400 chain_tests python -u -m pytest tests/test_ops_gpu.py -v -k chain $T
+           for b in 32 1; do
+             for c in 0 1; do
+               MIVGPU_CHAIN=$c run 200 "chain_b${b}_c$c" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch $b
+             done
+             MIVGPU_CHAIN=1 MIVGPU_CHAIN_W=4 run 200 "chain_b${b}_w4" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch $b
+           done ;;
     bench) run 400 bench python -u bench.py --out "gpurun_out/$out/bench.json" ;;
     smoke) run 200 smoke python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $s"; exit 2 ;;
