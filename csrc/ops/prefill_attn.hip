@@ -28,6 +28,7 @@
 // different 64-byte slots, conflict-free.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace {
 
@@ -51,7 +52,13 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return (bf16_t)(u >> 16);
 }
 
-template <int G>
+// V^T for the P.V MFMAs: TR = the row-major V tile through the hardware
+// transposed read (ds_read_b64_tr_b16); !TR = V staged transposed in LDS
+// ([128 dims][32 keys + 8 pad], one 2-byte write per element) and read with
+// plain 8-byte reads (MIVGPU_FA_TR=0; the correctness fallback).
+constexpr int FA_VT_PITCH = FA_BK + 8;
+
+template <int G, bool TR>
 __global__ void __launch_bounds__(G * 64)
 prefill_flash_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                      bf16_t* __restrict__ out, int L, int Hq, float scale_log2) {
@@ -59,7 +66,7 @@ prefill_flash_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
   constexpr int PER = FA_CHUNKS / NT;      // 16-byte chunks per thread per tile (K and V each)
   static_assert(PER * NT == FA_CHUNKS, "G must divide 8");
   __shared__ __attribute__((aligned(16))) bf16_t ks[2][FA_TILE];
-  __shared__ __attribute__((aligned(16))) bf16_t vs[2][FA_TILE];
+  __shared__ __attribute__((aligned(16))) bf16_t vs[2][TR ? FA_TILE : FA_D * FA_VT_PITCH];
 
   const int nqb = (L + FA_BQ - 1) / FA_BQ;
   const int qb = nqb - 1 - (int)blockIdx.x;       // heaviest (longest) blocks first
@@ -98,7 +105,14 @@ prefill_flash_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
     for (int i = 0; i < PER; ++i) {
       const int c = t + i * NT;
       *reinterpret_cast<uint4*>(&ks[buf][k_off(c >> 4, c & 15)]) = kreg[i];
-      *reinterpret_cast<uint4*>(&vs[buf][v_off(c >> 4, c & 15)]) = vreg[i];
+      if constexpr (TR) {
+        *reinterpret_cast<uint4*>(&vs[buf][v_off(c >> 4, c & 15)]) = vreg[i];
+      } else {   // transposed: vs[d][key]
+        const int key = c >> 4, d0 = (c & 15) * 8;
+        const bf16_t* e = reinterpret_cast<const bf16_t*>(&vreg[i]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vs[buf][(d0 + j) * FA_VT_PITCH + key] = e[j];
+      }
     }
   };
 
@@ -174,6 +188,15 @@ prefill_flash_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int row_lo = 16 * u + 4 * h + qq, row_hi = row_lo + 8;
+        if constexpr (!TR) {
+          // lane (r, h): V^T[32dc + r][keys 16u + 4h .. +4 and 16u + 4h + 8 .. +4]
+          const bf16_t* vrow = vt_lds + (32 * dc + r) * FA_VT_PITCH + 16 * u + 4 * h;
+          const uint2 lo2 = *reinterpret_cast<const uint2*>(vrow);
+          const uint2 hi2 = *reinterpret_cast<const uint2*>(vrow + 8);
+          const uint4 a4 = make_uint4(lo2.x, lo2.y, hi2.x, hi2.y);
+          o[dc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a4), pf[u], o[dc], 0, 0, 0);
+          continue;
+        }
         const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (__attribute__((address_space(3))) i16x4_t*)(&vt_lds[v_off(row_lo, col >> 3) + (col & 7)]));
         const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -210,9 +233,32 @@ prefill_flash_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
   }
 }
 
+// ds_read_b64_tr_b16 semantics probe: LDS holds element e = e; lane l reads
+// at element offset addr[l]; out[4l + i] = element i it received.
+__global__ void __launch_bounds__(64) tr_read_probe_kernel(const int* __restrict__ addr, int* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[4096];
+  for (int i = threadIdx.x; i < 4096; i += 64) lds[i] = (bf16_t)i;
+  __syncthreads();
+  const i16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) i16x4_t*)(&lds[addr[threadIdx.x]]));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) out[4 * threadIdx.x + i] = (int)(uint16_t)v[i];
+}
+
+// read per launch (prompt-sized launches; tests switch it in one process)
+bool fa_tr() {
+  const char* e = getenv("MIVGPU_FA_TR");
+  return !(e && *e && atoi(e) == 0);
+}
+
 }  // namespace
 
 extern "C" {
+
+int mivgpu_tr_read_probe(const int* addr, int* out, hipStream_t s) {
+  hipLaunchKernelGGL(tr_read_probe_kernel, dim3(1), dim3(64), 0, s, addr, out);
+  return (int)hipGetLastError();
+}
 
 // Causal prefill attention of one sequence of L positions (q head-grouped, see
 // above).  scale: the softmax scale (1/sqrt(D)).  G = Hq / Hkv in {1, 2, 4, 8}.
@@ -224,13 +270,17 @@ int mivgpu_prefill_attention(const void* q, const void* k, const void* v, void* 
   const float sl2 = scale * 1.4426950408889634f;
   const bf16_t *qq = (const bf16_t*)q, *kk = (const bf16_t*)k, *vv = (const bf16_t*)v;
   bf16_t* oo = (bf16_t*)out;
+#define MIVGPU_FA(GG, TRV) \
+  hipLaunchKernelGGL((prefill_flash_kernel<GG, TRV>), grid, dim3(64 * GG), 0, s, qq, kk, vv, oo, L, Hq, sl2)
+  const bool tr = fa_tr();
   switch (G) {
-    case 1: hipLaunchKernelGGL(prefill_flash_kernel<1>, grid, dim3(64), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
-    case 2: hipLaunchKernelGGL(prefill_flash_kernel<2>, grid, dim3(128), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
-    case 4: hipLaunchKernelGGL(prefill_flash_kernel<4>, grid, dim3(256), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
-    case 8: hipLaunchKernelGGL(prefill_flash_kernel<8>, grid, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
+    case 1: if (tr) MIVGPU_FA(1, true); else MIVGPU_FA(1, false); break;
+    case 2: if (tr) MIVGPU_FA(2, true); else MIVGPU_FA(2, false); break;
+    case 4: if (tr) MIVGPU_FA(4, true); else MIVGPU_FA(4, false); break;
+    case 8: if (tr) MIVGPU_FA(8, true); else MIVGPU_FA(8, false); break;
     default: return -1;
   }
+#undef MIVGPU_FA
   return (int)hipGetLastError();
 }
 

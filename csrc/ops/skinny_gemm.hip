@@ -400,16 +400,39 @@ __device__ __forceinline__ void wide_load_w(WFrag<NT> (&f)[U], const u32x4_t* __
     }
 }
 
+// Hand-offs inside one launch (decode_chain_kernel): bytes a workgroup of the
+// same grid produced are stored write-through (sc1, 4 or 16 bytes) and loaded
+// with sc1 buffer loads -- coherent across the XCDs' L2s with no L2
+// write-back or invalidate (MI355X_MICROARCH.md, hand-offs with sc1 loads).
+constexpr int AUX_SC1 = 16;   // cache-policy bit sc1
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)0xffffffff, 0x00020000);
+}
+
+__device__ __forceinline__ u32x4_t load16_sc1(const void* base, size_t byte_off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(base), (int)byte_off, 0, AUX_SC1);
+}
+
+__device__ __forceinline__ void store4_sc1(void* p, uint32_t v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // X[MT*32 rows][U*64 k] of k-blocks kb.. as MT*U*256 16-byte chunks, row-major,
-// XC per thread (rows >= M re-read row M-1: never stored, no masks).
-template <int MT, int U, int XC>
+// XC per thread (rows >= M re-read row M-1: never stored, no masks).  SC1: X
+// was produced earlier in the same launch.
+template <int MT, int U, int XC, bool SC1 = false>
 __device__ __forceinline__ void wide_load_x(u32x4_t (&xr)[XC], const bf16_t* __restrict__ x, int M, int ldx, int kb,
                                             int tid, int nthreads) {
 #pragma unroll
   for (int i = 0; i < XC; ++i) {
     const int c = tid + i * nthreads;
     const int row = c / (U * 8), c8 = c % (U * 8);
-    xr[i] = *(const u32x4_t*)(x + (size_t)min(row, M - 1) * ldx + kb * 64 + c8 * 8);
+    const size_t off = (size_t)min(row, M - 1) * ldx + kb * 64 + c8 * 8;
+    if constexpr (SC1)
+      xr[i] = load16_sc1(x, off * 2);
+    else
+      xr[i] = *(const u32x4_t*)(x + off);
   }
 }
 
@@ -525,14 +548,14 @@ __device__ __forceinline__ void wide_mma(const WFrag<NT> (&f)[U], const bf16_t* 
 // `cur` + LDS buffer `xc`, (then stage the prefetched X into `xn` and hand it
 // over with the barrier).  X is issued before W: vmcnt retires in issue
 // order, so staging X never waits for the W prefetch.
-template <int MT, int NT, int U, int XC, int PITCH, bool PREFETCH>
+template <int MT, int NT, int U, int XC, int PITCH, bool PREFETCH, bool SC1 = false>
 __device__ __forceinline__ void wide_step(const WFrag<NT> (&cur)[U], WFrag<NT> (&nxt)[U], const bf16_t* xc,
                                           bf16_t* xn, f32x16_t (&acc)[MT][NT], const u32x4_t* __restrict__ wbase,
                                           WStride ws, const bf16_t* __restrict__ x, int M, int ldx, int kb, int tid,
                                           int nthreads, int lane, int r, int h) {
   u32x4_t xr[XC];
   if constexpr (PREFETCH) {
-    wide_load_x<MT, U, XC>(xr, x, M, ldx, kb + U, tid, nthreads);
+    wide_load_x<MT, U, XC, SC1>(xr, x, M, ldx, kb + U, tid, nthreads);
     wide_load_w<NT, U>(nxt, wbase, ws, kb + U, lane);
   }
   DB_FENCE();
@@ -550,10 +573,85 @@ __device__ __forceinline__ int acc_row(int e, int h) { return (e & 3) + 8 * (e >
 // Per-wave LDS tile of the residual epilogue's squares: [MT*32 rows][SQ_PITCH].
 constexpr int SQ_PITCH = 40;   // 16-byte aligned rows; rows r and r+4 (the two lane halves) 32 banks apart
 
-template <int MT, int NT, int EPI, class Get>
+// SC1 (the output is handed to a later projection of the same launch): the
+// bf16 results go out as 4-byte write-through stores of column pairs -- lanes
+// r and r^1 hold columns r, r^1 of the same rows; one shuffle per row pair
+// gives the even lane (col r, r+1) of row e and the odd lane (col r-1, r) of
+// row e+1.
+__device__ __forceinline__ void store_pair_sc1(bf16_t* __restrict__ y, int M, int ldy, int col0, int row0, int r,
+                                               float v0, float v1) {
+  // v0, v1: this lane's values of rows row0 (e even) and row0 + 1 (e odd), column col0 + r
+  const bool odd = r & 1;
+  const float recv = __shfl_xor(odd ? v0 : v1, 1, 64);
+  const int row = odd ? row0 + 1 : row0;
+  const uint32_t pk = odd ? pack_bf2(recv, v1) : pack_bf2(v0, recv);
+  if (row < M) store4_sc1(y + (size_t)row * ldy + col0 + (r & ~1), pk);
+}
+
+template <int MT, int NT, int EPI, bool SC1 = false, class Get>
 __device__ __forceinline__ void wide_epilogue(Get get, bf16_t* __restrict__ y, int M, int ldy, int tile0,
                                               int vgroup, int r, int h, const float* rs, float* __restrict__ ss_out,
                                               const bf16_t* res_lds, float* sq_lds = nullptr) {
+  if constexpr (SC1 && EPI == EPI_RESID) {
+    // as below, the new values kept for the paired write-through stores
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      float vv[NT][16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = m * 32 + acc_row(e, h);
+        float sq = 0.f;
+        const float sc = (row < M && rs) ? rs[row] : 1.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const bf16_t old = res_lds[((m * NT + t) * 32 + (row - m * 32)) * 32 + r];
+          const float v = round_bf(__uint_as_float((uint32_t)old << 16) + get(m, t, e) * sc);
+          vv[t][e] = v;
+          sq += row < M ? v * v : 0.f;
+        }
+        sq_lds[row * SQ_PITCH + r] = sq;
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          store_pair_sc1(y, M, ldy, (tile0 + t) * 32, m * 32 + acc_row(2 * i, h), r, vv[t][2 * i], vv[t][2 * i + 1]);
+    }
+    const int lane = r + 32 * h, half = lane & 1;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int row = m * 32 + (lane >> 1);
+      const float4* p = reinterpret_cast<const float4*>(sq_lds + row * SQ_PITCH + 16 * half);
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 q = p[j];
+        sum += (q.x + q.y) + (q.z + q.w);
+      }
+      sum += __shfl_xor(sum, 1, 64);
+      if (half == 0) __hip_atomic_store(&ss_out[(size_t)vgroup * SS_ROWS + row], sum, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  if constexpr (SC1 && EPI == EPI_SILU_MUL) {
+    static_assert(NT == 2, "SiLU*up: a gate/up tile pair");
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float v[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int e = 2 * i + k, row = m * 32 + acc_row(e, h);
+          const float sc = (row < M && rs) ? rs[row] : 1.f;
+          const float g = round_bf(get(m, 0, e) * sc), u = round_bf(get(m, 1, e) * sc);
+          v[k] = g / (1.f + __expf(-g)) * u;
+        }
+        store_pair_sc1(y, M, ldy, vgroup * 32, m * 32 + acc_row(2 * i, h), r, v[0], v[1]);
+      }
+    return;
+  }
   if constexpr (EPI == EPI_RESID) {
     // update; each lane's squares (one column r of 16 rows) go to the wave's
     // LDS tile, then lane l sums half of row l/2 with four 16-byte reads
@@ -619,7 +717,7 @@ __device__ __forceinline__ void wide_epilogue(Get get, bf16_t* __restrict__ y, i
 // the slot loads only.
 constexpr int RS_LMAX = 8;
 
-template <int MT, int NTHREADS>
+template <int MT, int NTHREADS, bool SC1 = false>
 __device__ __forceinline__ void rs_issue(float4 (&v)[RS_LMAX], const float* __restrict__ part, int nparts, int tid) {
   constexpr int RC = MT * 8;                 // float4 chunks per slot (MT*32 rows)
   constexpr int PER = NTHREADS / RC;         // slots read in parallel
@@ -628,7 +726,13 @@ __device__ __forceinline__ void rs_issue(float4 (&v)[RS_LMAX], const float* __re
 #pragma unroll
   for (int i = 0; i < RS_LMAX; ++i) {
     const int pp = p0 + i * PER;
-    v[i] = pp < nparts ? *(const float4*)(part + (size_t)pp * SS_ROWS + 4 * rc) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (SC1) {
+      // a clamped slot address (always loaded: no branch around the load), zeroed when unused
+      const u32x4_t q = load16_sc1(part, ((size_t)min(pp, nparts - 1) * SS_ROWS + 4 * rc) * 4);
+      v[i] = pp < nparts ? __builtin_bit_cast(float4, q) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      v[i] = pp < nparts ? *(const float4*)(part + (size_t)pp * SS_ROWS + 4 * rc) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   }
 }
 
@@ -722,6 +826,7 @@ __device__ __forceinline__ void wide_body(const GemmP& p, int block, WideLds<MT,
   constexpr int XC = MT * U * 256 / NTHREADS;       // X chunks per thread per group
   static_assert(XC * NTHREADS == MT * U * 256, "X tile must split evenly over the workgroup");
   constexpr bool RS = LD::RS;
+  constexpr bool SC1 = Deps::chained;               // X, slots and the residual tile come from this launch
   const u32x4_t* __restrict__ wp = p.wp;
   const bf16_t* __restrict__ x = p.x;
   bf16_t* __restrict__ y = p.y;
@@ -761,14 +866,26 @@ __device__ __forceinline__ void wide_body(const GemmP& p, int block, WideLds<MT,
     deps.wait(WV - 1, split);
     if (wave == WV - 1) wide_load_w<NT, U>(fa, wbase, ws, kb0, lane);
   }
+  // chained residual update: the old residual tile was written earlier in the
+  // same launch, so it comes in by sc1 loads to registers (written to the
+  // wave's LDS tile before the epilogue) instead of LDS-DMA
+  constexpr int RCH = (EPI == EPI_RESID && SC1) ? MT * NT * 2 : 1;
+  u32x4_t resr[RCH];
   {
     // row-scale slot loads and the residual tile's LDS-DMA first: older than
     // the X loads, so the X wait below covers them as well
     float4 rsv[RS ? RS_LMAX : 1];
     if constexpr (RS) {
-      if (p.rs_part) rs_issue<MT, NTHREADS>(rsv, p.rs_part, p.rs_nparts, tid);
+      if (p.rs_part) rs_issue<MT, NTHREADS, SC1>(rsv, p.rs_part, p.rs_nparts, tid);
     }
-    if constexpr (EPI == EPI_RESID) {
+    if constexpr (EPI == EPI_RESID && SC1) {
+      // tile (m, t): 32 rows x 32 columns = 128 16-byte chunks, 2 per lane
+#pragma unroll
+      for (int q = 0; q < RCH; ++q) {
+        const int mt = q >> 1, c = lane + 64 * (q & 1), row = (mt / NT) * 32 + (c >> 2);
+        resr[q] = load16_sc1(y, ((size_t)min(row, M - 1) * ldy + (size_t)(tile0 + mt % NT) * 32 + (c & 3) * 8) * 2);
+      }
+    } else if constexpr (EPI == EPI_RESID) {
       // tile (m, t): 32 rows x 64 B, 4 rows per instruction, lane = (row, 4-byte column pair)
 #pragma unroll
       for (int m = 0; m < MT; ++m)
@@ -782,7 +899,7 @@ __device__ __forceinline__ void wide_body(const GemmP& p, int block, WideLds<MT,
           }
     }
     u32x4_t xr[XC];
-    wide_load_x<MT, U, XC>(xr, x, M, ldx, kb0, tid, NTHREADS);
+    wide_load_x<MT, U, XC, SC1>(xr, x, M, ldx, kb0, tid, NTHREADS);
     if constexpr (!Deps::chained) wide_load_w<NT, U>(fa, wbase, ws, kb0, lane);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (RS) {
@@ -793,25 +910,34 @@ __device__ __forceinline__ void wide_body(const GemmP& p, int block, WideLds<MT,
   }
   int g = 0, kb = kb0;
   for (; g + 3 <= G; g += 2, kb += 2 * U) {
-    wide_step<MT, NT, U, XC, PITCH, true>(fa, fb, xs, xs + XBUF, acc, wbase, ws, x, M, ldx, kb, tid, NTHREADS, lane,
+    wide_step<MT, NT, U, XC, PITCH, true, SC1>(fa, fb, xs, xs + XBUF, acc, wbase, ws, x, M, ldx, kb, tid, NTHREADS, lane,
                                           r, h);
-    wide_step<MT, NT, U, XC, PITCH, true>(fb, fa, xs + XBUF, xs, acc, wbase, ws, x, M, ldx, kb + U, tid, NTHREADS,
+    wide_step<MT, NT, U, XC, PITCH, true, SC1>(fb, fa, xs + XBUF, xs, acc, wbase, ws, x, M, ldx, kb + U, tid, NTHREADS,
                                           lane, r, h);
   }
   if (G - g == 2) {
-    wide_step<MT, NT, U, XC, PITCH, true>(fa, fb, xs, xs + XBUF, acc, wbase, ws, x, M, ldx, kb, tid, NTHREADS, lane,
+    wide_step<MT, NT, U, XC, PITCH, true, SC1>(fa, fb, xs, xs + XBUF, acc, wbase, ws, x, M, ldx, kb, tid, NTHREADS, lane,
                                           r, h);
-    wide_step<MT, NT, U, XC, PITCH, false>(fb, fa, xs + XBUF, xs, acc, wbase, ws, x, M, ldx, kb + U, tid, NTHREADS,
+    wide_step<MT, NT, U, XC, PITCH, false, SC1>(fb, fa, xs + XBUF, xs, acc, wbase, ws, x, M, ldx, kb + U, tid, NTHREADS,
                                            lane, r, h);
   } else {
-    wide_step<MT, NT, U, XC, PITCH, false>(fa, fb, xs, xs + XBUF, acc, wbase, ws, x, M, ldx, kb, tid, NTHREADS, lane,
+    wide_step<MT, NT, U, XC, PITCH, false, SC1>(fa, fb, xs, xs + XBUF, acc, wbase, ws, x, M, ldx, kb, tid, NTHREADS, lane,
                                            r, h);
   }
 
   float* sq = L.s_sq + wave * (EPI == EPI_RESID ? MT * 32 * SQ_PITCH : 0);
-  if constexpr (EPI == EPI_RESID) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // residual tile landed
+  if constexpr (EPI == EPI_RESID && SC1) {
+    // this wave's own LDS tile (read back by this wave only: no barrier)
+#pragma unroll
+    for (int q = 0; q < RCH; ++q) {
+      const int mt = q >> 1, c = lane + 64 * (q & 1);
+      *reinterpret_cast<u32x4_t*>(res_lds + (mt * 32 + (c >> 2)) * 32 + (c & 3) * 8) = resr[q];
+    }
+  } else if constexpr (EPI == EPI_RESID) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // residual tile landed
+  }
   if (S == 1) {
-    wide_epilogue<MT, NT, EPI>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, vgroup, r, h,
+    wide_epilogue<MT, NT, EPI, SC1>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, vgroup, r, h,
                                rs, p.ss_out, res_lds, sq);
     deps.publish(vgroup);
     return;
@@ -832,7 +958,7 @@ __device__ __forceinline__ void wide_body(const GemmP& p, int block, WideLds<MT,
   if (lane == 0) ticket = atomicAdd(p.tickets + vgroup, 1);
   ticket = __shfl(ticket, 0, 64);
   if (ticket != S - 1) return;
-  wide_epilogue<MT, NT, EPI>(
+  wide_epilogue<MT, NT, EPI, SC1>(
       [&](int m, int t, int e) {
         return __hip_atomic_load(sc + ((m * NT + t) * 16 + e) * 64 + lane, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
@@ -900,6 +1026,10 @@ __device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<M
   static_assert((KW * MT * NT * 16 * 64 + MT * 32 * SQ_PITCH) * 4 <= 2 * XBUF * 2,
                 "the residual epilogue's squares tile follows the reduction in the X buffers");
   constexpr bool RS = LD::RS;
+  // X and slots produced earlier in the same launch (the chained qkv); the
+  // residual tile of a chained residual update (o_proj, the chain's first
+  // projection) comes from the previous launch: LDS-DMA as standalone
+  constexpr bool SC1 = Deps::chained;
   const u32x4_t* __restrict__ wp = p.wp;
   const bf16_t* __restrict__ x = p.x;
   bf16_t* __restrict__ y = p.y;
@@ -938,7 +1068,7 @@ __device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<M
     // the X loads, so the X wait below covers them as well
     float4 rsv[RS ? RS_LMAX : 1];
     if constexpr (RS) {
-      if (p.rs_part) rs_issue<MT, NTHREADS>(rsv, p.rs_part, p.rs_nparts, tid);
+      if (p.rs_part) rs_issue<MT, NTHREADS, SC1>(rsv, p.rs_part, p.rs_nparts, tid);
     }
     if constexpr (EPI == EPI_RESID) {
       if (kw == 0) {
@@ -982,7 +1112,7 @@ __device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<M
       }
     } else {
       u32x4_t xr[XC];
-      wide_load_x<MT, GK, XC>(xr, x, M, ldx, kb0, tid, NTHREADS);
+      wide_load_x<MT, GK, XC, SC1>(xr, x, M, ldx, kb0, tid, NTHREADS);
       if constexpr (!Deps::chained) wide_load_w<NT, U>(fa, wbase, ws, kb0 + kw * U, lane);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (RS) {
@@ -999,7 +1129,7 @@ __device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<M
                   bool prefetch) {
     u32x4_t xr[XC];
     if (prefetch) {
-      wide_load_x<MT, GK, XC>(xr, x, M, ldx, kb + GK, tid, NTHREADS);
+      wide_load_x<MT, GK, XC, SC1>(xr, x, M, ldx, kb + GK, tid, NTHREADS);
       wide_load_w<NT, U>(nxt, wbase, ws, kb + GK + kw * U, lane);
     }
     DB_FENCE();
@@ -1045,7 +1175,7 @@ __device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<M
         for (int e = 0; e < 16; ++e) acc[m][t][e] += red[((((w - 1) * MT + m) * NT + t) * 16 + e) * 64 + lane];
   if constexpr (EPI == EPI_RESID) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // residual tile landed
   if (S == 1) {
-    wide_epilogue<MT, NT, EPI>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, vgroup, r, h,
+    wide_epilogue<MT, NT, EPI, SC1>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, vgroup, r, h,
                                rs, p.ss_out, L.s_res, red + KW * MT * NT * 16 * 64);
     deps.publish(vgroup);
     return;
@@ -1063,7 +1193,7 @@ __device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<M
   if (lane == 0) ticket = atomicAdd(p.tickets + vgroup, 1);
   ticket = __shfl(ticket, 0, 64);
   if (ticket != S - 1) return;
-  wide_epilogue<MT, NT, EPI>(
+  wide_epilogue<MT, NT, EPI, SC1>(
       [&](int m, int t, int e) {
         return __hip_atomic_load(sc + ((m * NT + t) * 16 + e) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       },
@@ -1094,10 +1224,15 @@ __global__ void __launch_bounds__(64 * KW) skinny_widek_kernel(GemmP p, XComb xc
 //     its row scales are o_proj's sum-of-squares slots);
 //   * down split s waits only for the gate_up channel blocks of its k-range;
 //   * qkv waits for every down tile.
-// Hand-off (MI355X_MICROARCH.md, persistent kernels): the producing wave
-// releases at agent scope (L2 write-back), drains, then bumps a device-scope
-// counter; one lane of the consumer polls it with relaxed loads and s_sleep,
-// then acquires at agent scope (L2 invalidate) before the workgroup barrier.
+// Hand-off (MI355X_MICROARCH.md, hand-offs with sc1 loads, row 1): handed-off
+// bytes (residual stream, SiLU output, sum-of-squares slots) are stored
+// write-through (sc1, 4-byte column pairs) and read with sc1 loads; each
+// storing wave drains its stores, and after the workgroup's last barrier one
+// lane per counter adds the workgroup's published units (agent-scope atomic).
+// One lane of a consumer polls with sc1 loads and s_sleep; its workgroup's
+// barrier releases the rest.  No L2 write-back or invalidate anywhere: the
+// first version released and acquired at agent scope in every wave and ran
+// the decode step 1.65x slower (profiles/README.md section 37).
 // Deadlock freedom: a workgroup only waits on lower block ranges, and each
 // XCD dispatches its workgroups in block order, so every producer a resident
 // consumer waits for has been dispatched ahead of it.  Spins are bounded
@@ -1114,38 +1249,35 @@ struct ChainDeps {
   int* wait_ctr;     // counter(s) to wait on (nullptr: none)
   int wait_target;   // units published per counter
   int wait_split;    // one counter per split of this projection's k-range
-  int* pub_ctr;      // counter(s) this projection publishes to (nullptr: none)
+  int* pub_lds;      // this workgroup's published units per counter (LDS; nullptr: publishes nothing)
   int pub_div;       // units per counter (0: all units to one counter)
   int* err;
 
+  // One lane of the polling wave spins on an sc1 load of the counter; the
+  // other waves join it at the barrier (their loads of the handed-off bytes,
+  // all sc1, come after it).
   __device__ void wait(int poll_wave, int split) const {
     if (wait_ctr == nullptr) return;
-    if ((int)(threadIdx.x >> 6) == poll_wave) {
-      if ((threadIdx.x & 63) == 0) {
-        const int* c = wait_ctr + (wait_split ? split : 0);
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wait_target) {
-          __builtin_amdgcn_s_sleep(2);
-          if (__builtin_amdgcn_s_memrealtime() - t0 > CHAIN_SPIN_TICKS) {
-            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
+    if ((int)(threadIdx.x >> 6) == poll_wave && (threadIdx.x & 63) == 0) {
+      const int* c = wait_ctr + (wait_split ? split : 0);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wait_target) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > CHAIN_SPIN_TICKS) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
   }
 
+  // A wave's write-through stores of `unit` are drained; the workgroup's
+  // count goes out after the kernel's final barrier (one add per counter).
   __device__ void publish(int unit) const {
-    if (pub_ctr == nullptr) return;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    // inline asm: the compiler drops the wait after the write-back when it
-    // believes the wave's counter is already empty (MI355X_MICROARCH.md)
+    if (pub_lds == nullptr) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if ((threadIdx.x & 63) == 0)
-      __hip_atomic_fetch_add(pub_ctr + (pub_div ? unit / pub_div : 0), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((threadIdx.x & 63) == 0) atomicAdd(pub_lds + (pub_div ? unit / pub_div : 0), 1);
   }
 };
 
@@ -1168,27 +1300,37 @@ __global__ void __launch_bounds__(64 * W) decode_chain_kernel(ChainArgs a) {
   using L3 = WidekLds<1, 1, W, EPI_STORE>;
   constexpr int LB = cmax<cmax<(int)sizeof(L0), (int)sizeof(L1)>(), cmax<(int)sizeof(L2), (int)sizeof(L3)>()>();
   __shared__ __attribute__((aligned(16))) char lds[LB];
+  __shared__ int pub[CHAIN_MAX_SPLITS];
+  if (threadIdx.x < CHAIN_MAX_SPLITS) pub[threadIdx.x] = 0;   // published before any body's first barrier
   int* c = a.ctr;
+  int* pub_ctr = nullptr;
   int b = blockIdx.x;
   if (b < a.nblk[0]) {
+    pub_ctr = a.nblk[1] ? c + CTR_O : nullptr;
     widek_body<1, 1, W, EPI_RESID, false>(a.g[0], b, *reinterpret_cast<L0*>(lds), XComb{},
-                                         ChainDeps{nullptr, 0, 0, c + CTR_O, 0, c + CTR_ERR});
+                                         ChainDeps{nullptr, 0, 0, pub_ctr ? pub : nullptr, 0, c + CTR_ERR});
   } else if ((b -= a.nblk[0]) < a.nblk[1]) {
+    pub_ctr = a.nblk[2] ? c + CTR_GU : nullptr;
     wide_body<1, 2, W, EPI_SILU_MUL>(a.g[1], b, *reinterpret_cast<L1*>(lds),
                                      ChainDeps{a.wait_target[1] ? c + CTR_O : nullptr, a.wait_target[1], 0,
-                                               a.nblk[2] ? c + CTR_GU : nullptr, a.gu_div, c + CTR_ERR});
+                                               pub_ctr ? pub : nullptr, a.gu_div, c + CTR_ERR});
   } else if ((b -= a.nblk[1]) < a.nblk[2]) {
+    pub_ctr = a.nblk[3] ? c + CTR_D : nullptr;
     wide_body<1, 1, W, EPI_RESID>(a.g[2], b, *reinterpret_cast<L2*>(lds),
                                   ChainDeps{a.wait_target[2] ? c + CTR_GU : nullptr, a.wait_target[2], 1,
-                                            a.nblk[3] ? c + CTR_D : nullptr, 0, c + CTR_ERR});
+                                            pub_ctr ? pub : nullptr, 0, c + CTR_ERR});
   } else {
     b -= a.nblk[2];
     widek_body<1, 1, W, EPI_STORE, false>(a.g[3], b, *reinterpret_cast<L3*>(lds), XComb{},
                                          ChainDeps{a.wait_target[3] ? c + CTR_D : nullptr, a.wait_target[3], 0,
                                                    nullptr, 0, c + CTR_ERR});
   }
-  // the last workgroup out re-zeroes the counters (every wait is behind it)
+  // every storing wave drained its write-through stores before counting
+  // itself in pub[]: one lane per counter signals for the workgroup
   __syncthreads();
+  if (pub_ctr != nullptr && threadIdx.x < CHAIN_MAX_SPLITS && pub[threadIdx.x] > 0)
+    __hip_atomic_fetch_add(pub_ctr + threadIdx.x, pub[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the last workgroup out re-zeroes the counters (every wait is behind it)
   if (threadIdx.x == 0) {
     const int total = a.nblk[0] + a.nblk[1] + a.nblk[2] + a.nblk[3];
     if (__hip_atomic_fetch_add(c + CTR_FIN, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {

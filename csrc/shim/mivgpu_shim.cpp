@@ -1662,8 +1662,9 @@ bool gate_init_locked(int dev, DeviceGate& G) {
 struct OccPeer {
   int pid;
   int fd;
-  uint64_t busy_ns;   // last sample that saw waves of it resident
+  uint64_t busy_ns;   // last sample that saw waves of it resident (beyond a gate wave)
   int v;              // its reading this sample
+  bool held;          // this sample saw only its gate wave: held, not contending
   double avg;         // EWMA of its readings over this process's owing samples
 };
 // Busy peers whose average resident waves are within this factor of this
@@ -1672,6 +1673,9 @@ struct OccPeer {
 constexpr double kContendFrac = 0.1;
 // A peer is busy for this long after its last sample with waves resident.
 constexpr uint64_t kPeerBusyNs = 200000000ull;   // 200 ms
+// A governed peer held behind its gate has exactly its gate kernel's wave
+// resident (governor.hip host_bucket_gate: one 64-lane wave).
+constexpr int kGateWaves = 1;
 struct OccDev {
   bool live = false;           // sampler has this device's KFD view
   int gpu_id = -1;
@@ -1751,7 +1755,7 @@ void occ_rescan(OccDev& o, uint64_t now) {
     for (auto& p : o.peers)
       if (p.pid == pid && p.fd >= 0) { fd = p.fd; busy = p.busy_ns; avg = p.avg; p.fd = -1; break; }
     if (fd < 0) fd = open_occ((int)pid, o.gpu_id);   // no stats_<gpu_id>: not on this GPU
-    if (fd >= 0) next.push_back(OccPeer{(int)pid, fd, busy, 0, avg});
+    if (fd >= 0) next.push_back(OccPeer{(int)pid, fd, busy, 0, false, avg});
   }
   closedir(d);
   for (auto& p : o.peers)
@@ -1785,16 +1789,19 @@ bool occ_sample(int dev, uint64_t now) {
   // wave among them: discounting one CU's worth for peers but not for itself
   // billed every symmetric tenant above 1/N -- measured, 8 x 12 % decode
   // tenants held 27 % of the time).
+  // A peer showing only its gate wave is held, not contending: it does not
+  // dilute this process's charge while it holds (measured: a 75 % tenant
+  // next to a 25 % one was charged half of its solo time while the 25 % one
+  // sat in its gate, and settled at 50 % instead of 75 %).
   long others = 0;
   int busy_peers = 0;
   for (auto& p : o.peers) {
     int v = read_occ(p.fd);
     p.v = v > 0 ? v : 0;
-    if (v > 0) {
-      others += v;
-      p.busy_ns = now;
-    }
-    if (p.busy_ns && now - p.busy_ns < kPeerBusyNs) ++busy_peers;
+    p.held = v == kGateWaves;
+    if (v > 0) others += v;
+    if (v > kGateWaves) p.busy_ns = now;
+    if (p.busy_ns && now - p.busy_ns < kPeerBusyNs && !p.held) ++busy_peers;
   }
   // The gate's own resident wave is not consumption: discount one unit per
   // gate slot holding right now.
@@ -1877,7 +1884,7 @@ bool occ_sample(int dev, uint64_t now) {
       int comparable = 0;
       double heavier = 0;
       for (const auto& p : o.peers) {
-        if (!p.busy_ns || now - p.busy_ns >= kPeerBusyNs) continue;
+        if (!p.busy_ns || now - p.busy_ns >= kPeerBusyNs || p.held) continue;
         if (p.avg * kContendFrac > o.own_avg) heavier += p.avg;
         else if (p.avg >= kContendFrac * o.own_avg) ++comparable;
       }

@@ -45,6 +45,7 @@ def lib():
                                                      vp]
         L.mivgpu_decode_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, f, vp]
         L.mivgpu_prefill_attention.argtypes = [vp, vp, vp, vp, i, i, i, i, f, vp]
+        L.mivgpu_tr_read_probe.argtypes = [vp, vp, vp]
         L.mivgpu_decode_attention_fused.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i,
                                                      i, f, f, f, i, vp]
         L.mivgpu_skinny_gemm_norm_xcomb.argtypes = [vp, vp, vp, vp, i, i, i, i, vp, i, i, i, i, i, i, i, vp, vp,

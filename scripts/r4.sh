@@ -17,7 +17,9 @@ run() {  # run <seconds> <log> <cmd...>; pytest rc 1 (failures) keeps going
 T="--timeout 300 --timeout-method thread"
 for s in "$@"; do
   case $s in
-    flash) run 400 flash_tests python -u -m pytest tests/test_ops_gpu.py -v -k "prefill_flash or long_prefill" $T ;;
+    flash) run 400 flash_tests python -u -m pytest tests/test_ops_gpu.py -v -k "prefill_flash or long_prefill or tr_read" $T ;;
+    shim2) run 700 shim2_tests python -u -m pytest tests/test_shim_gpu.py tests/test_shim_interpose_gpu.py -v -s $T \
+             -k "unequal or tenant_without or tenant_rewriting" ;;
     attnbench) run 300 prefill_attn python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention \
                  --out "gpurun_out/$out/prefill_attn.json" ;;
     shim) run 700 shim_tests python -u -m pytest tests/test_shim_gpu.py tests/test_shim_interpose_gpu.py -v -s $T ;;

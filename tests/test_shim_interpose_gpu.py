@@ -10,6 +10,7 @@ bounds are those of test_heavy_tenant_held_to_its_share_next_to_light_neighbours
 """
 
 import json
+import time
 import os
 import tempfile
 
@@ -145,25 +146,12 @@ def test_queue_cap_protects_masked_neighbours(tmp):
         assert b >= 0.97 * a, (honest, hostile)
 
 
-def _tamper_round(tmp, unlink: bool, passes: int):
-    """A hostile tenant under a 4 GiB grant (probe child ``tamper``) against
-    ``passes`` monitor passes with the evict escalation and a fake API server.
-    Returns (pass results, control snapshot, evictions, child result)."""
-    import subprocess
-    import sys
-    import time
+def _container(tmp, name):
+    """A container's host-side state: grant file (4 GiB), control file, the
+    directory its region would live in; returns (hook, grant, cache, ctl)."""
+    from k8s_vgpu_scheduler_amd.monitor.control import control_host_path, create
 
-    from k8s_vgpu_scheduler_amd.e2e.apiserver import FakeApiServer
-    from k8s_vgpu_scheduler_amd.k8s.fake import make_pod
-    from k8s_vgpu_scheduler_amd.k8s.rest import RestClient
-    from k8s_vgpu_scheduler_amd.monitor import feedback
-    from k8s_vgpu_scheduler_amd.monitor.control import ControlFile, control_host_path, create
-    from k8s_vgpu_scheduler_amd.monitor.escalate import OverGrantPolicy
-    from k8s_vgpu_scheduler_amd.monitor.hosttruth import HostTruth, single_gpu_ids
-    from k8s_vgpu_scheduler_amd.monitor.lister import ContainerLister
-    from k8s_vgpu_scheduler_amd.shim import shim_env
-
-    hook = os.path.join(tmp, f"hook-{int(unlink)}")
+    hook = os.path.join(tmp, f"hook-{name}")
     cdir = os.path.join(hook, "vgpu", "containers", "uid-t_main")
     ldir = os.path.join(hook, "vgpu", "limits")
     os.makedirs(cdir)
@@ -175,74 +163,118 @@ def _tamper_round(tmp, unlink: bool, passes: int):
     with open(grant, "w") as f:
         f.write(f"HIP_DEVICE_MEMORY_LIMIT_0=4096m\nMIVGPU_SHARED_CACHE={cache}\nMIVGPU_DEVICE_UUIDS=GPU-tamper\n"
                 f"MIVGPU_CONTROL_FILE={ctl}\n")
-    env = dict(os.environ)
-    env.update(shim_env())
-    env["MIVGPU_LIMITS_FILE"] = grant
+    return hook, grant, cache, ctl
+
+
+def _spawn(args, env, tag):
+    import subprocess
+    import sys
+
+    p = subprocess.Popen([sys.executable, "-m", "k8s_vgpu_scheduler_amd.shim.probe"] + args, env=env,
+                         stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    line = p.stdout.readline()
+    assert line.startswith(tag + " "), (line, p.stderr.read()[-2000:] if p.poll() is not None else "")
+    return p, json.loads(line[len(tag) + 1:])
+
+
+def _monitor(hook, api, pids, passes):
+    from k8s_vgpu_scheduler_amd.k8s.rest import RestClient
+    from k8s_vgpu_scheduler_amd.monitor import feedback
+    from k8s_vgpu_scheduler_amd.monitor.escalate import OverGrantPolicy
+    from k8s_vgpu_scheduler_amd.monitor.hosttruth import HostTruth, single_gpu_ids
+    from k8s_vgpu_scheduler_amd.monitor.lister import ContainerLister
+
+    lister = ContainerLister(hook, lambda: api.cluster.list("pods"), resync_interval=3600)
+    # the pod's processes as a hostPID monitor's cgroup scan finds them: KFD's
+    # (host) pids of the children stand in (the box may run us in a pid namespace)
+    truth = HostTruth(lambda: single_gpu_ids("GPU-tamper"), pod_pids=lambda uid: pids)
+    pol = OverGrantPolicy("evict", passes=passes, client=RestClient(api.url))
+    return [feedback.feedback_pass(lister, truth, pol) for _ in range(passes)]
+
+
+def _api():
+    from k8s_vgpu_scheduler_amd.e2e.apiserver import FakeApiServer
+    from k8s_vgpu_scheduler_amd.k8s.fake import make_pod
+
     api = FakeApiServer().start()
     pod = make_pod("t", "default")
     pod["metadata"]["uid"] = "uid-t"
     api.cluster.create("pods", pod)
-    args = [sys.executable, "-m", "k8s_vgpu_scheduler_amd.shim.probe", "--child", "tamper", "--out", cache,
-            "--oom-probe-mib", "3500"] + (["--unlink"] if unlink else [])
-    p = subprocess.Popen(args, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                         text=True)
-    outs = []
-    se = ""
+    return api
+
+
+def test_tenant_without_the_shim_reported_within_one_pass(tmp):
+    """a container process the shim is not loaded into
+    (no region file ever exists: an image whose loader ignored the preload)
+    allocates past its 4 GiB grant.  ONE monitor pass, driven by the grant
+    file and KFD, reports it over its grant and shim-less, and the evict
+    escalation reaches the API server's Eviction endpoint."""
+    hook, grant, cache, ctl = _container(tmp, "noshim")
+    from k8s_vgpu_scheduler_amd.monitor.control import ControlFile
+
+    api = _api()
+    hog = None
     try:
-        line = p.stdout.readline()
-        assert line.startswith("TAMPERED "), (line, p.stderr.read()[-2000:] if p.poll() is not None else "")
-        first = json.loads(line[9:])
-        lister = ContainerLister(hook, lambda: api.cluster.list("pods"), resync_interval=3600)
-        # the pod's processes as a hostPID monitor's cgroup scan finds them: the
-        # box may run this test in a pid namespace, so KFD's (host) pid of the
-        # child -- the one its shim found for itself -- stands in
-        truth = HostTruth(lambda: single_gpu_ids("GPU-tamper"), pod_pids=lambda uid: [first["kfd_pid"]])
-        pol = OverGrantPolicy("evict", passes=passes, client=RestClient(api.url))
-        for _ in range(passes):
-            outs.append(feedback.feedback_pass(lister, truth, pol))
+        hog, info = _spawn(["--child", "hog", "--oom-probe-mib", "4608"], dict(os.environ), "HOG")
+        outs = _monitor(hook, api, [info["kfd_pid"]], passes=1)
         snap = ControlFile(ctl).snapshot()
-        p.stdin.write("go\n")
-        p.stdin.flush()
-        time.sleep(3.0)                       # the tenant rewrites its region meanwhile
-        ControlFile(ctl).publish(block=False, switch=False, over=False)   # the verdict lifted
-        so, se = p.communicate(timeout=120)
+        evictions = list(api.cluster.evictions)
     finally:
-        if p.poll() is None:
-            p.kill()
+        if hog is not None:
+            hog.communicate("go\n", timeout=60)
         api.stop()
-    assert p.returncode == 0, se[-3000:]
-    res = json.loads([x for x in so.splitlines() if x.startswith("{")][-1])
-    res["first_alloc"] = first["first"]
-    return outs, snap, list(api.cluster.evictions), res
-
-
-def test_tenant_without_a_region_reported_within_one_pass(tmp):
-    """a tenant that deletes its region file before the
-    first pass, zeroes its counters and allocates past its 4 GiB grant is
-    reported (over grant + shim not loaded) by ONE pass, evicted through the
-    API server, and -- rewriting its region all along -- cannot allocate
-    again or launch while the control-file verdict holds."""
-    outs, snap, evictions, res = _tamper_round(tmp, unlink=True, passes=1)
     print(json.dumps({"over": sorted(outs[0]["over"]), "no_shim": sorted(outs[0]["no_shim"]),
                       "control": {k: snap[k] for k in ("block", "over_grant")},
-                      "excess_mib": snap["host_excess"][0] >> 20, "evictions": evictions, "child": res}))
-    assert res["first_alloc"] == "allocated"          # the counter rewrite let it past the grant
+                      "excess_mib": snap["host_excess"][0] >> 20, "evictions": evictions}))
+    assert not os.path.exists(cache)
     assert ("uid-t", "main") in outs[0]["over"] and ("uid-t", "main") in outs[0]["no_shim"]
     assert evictions == [("default", "t")]
-    assert snap["block"] == 1 and snap["host_excess"][0] > 4 << 30
-    assert res["second"] == "oom" and res["parked_s"] >= 2.5
+    assert snap["block"] == 1 and snap["over_grant"] == 1 and snap["host_excess"][0] > 4 << 30
 
 
 def test_tenant_rewriting_its_region_cannot_unblock_itself(tmp):
-    """The region kept: two passes (the excess needs two that agree) block
-    it and charge the KFD excess; the tenant keeps clearing its region's
-    block flag and usage counter, and stays blocked and out of headroom."""
-    outs, snap, evictions, res = _tamper_round(tmp, unlink=False, passes=2)
+    """A shim-loaded tenant zeroes its region's usage counters and tries to
+    allocate past its grant: refused (the shim charges the VRAM KFD shows
+    for it).  A sibling process without the shim then takes the container
+    over its grant; two monitor passes block the container through the
+    read-only control file and evict it.  The tenant keeps clearing its
+    region's block flag and counters from a thread: its allocations are
+    still refused and its launches stay parked until the verdict is lifted."""
+    hook, grant, cache, ctl = _container(tmp, "rewrite")
+    from k8s_vgpu_scheduler_amd.monitor.control import ControlFile
+    from k8s_vgpu_scheduler_amd.shim import shim_env
+
+    env = dict(os.environ)
+    env.update(shim_env())
+    env["MIVGPU_LIMITS_FILE"] = grant
+    api = _api()
+    tam = hog = None
+    se = ""
+    try:
+        tam, first = _spawn(["--child", "tamper", "--out", cache, "--oom-probe-mib", "3500"], env, "TAMPERED")
+        hog, info = _spawn(["--child", "hog", "--oom-probe-mib", "4096"], dict(os.environ), "HOG")
+        outs = _monitor(hook, api, [first["kfd_pid"], info["kfd_pid"]], passes=2)
+        snap = ControlFile(ctl).snapshot()
+        tam.stdin.write("go\n")
+        tam.stdin.flush()
+        time.sleep(3.0)                       # the tenant rewrites its region meanwhile
+        ControlFile(ctl).publish(block=False, switch=False, over=False)   # the verdict lifted
+        so, se = tam.communicate(timeout=120)
+        evictions = list(api.cluster.evictions)
+    finally:
+        for p in (tam, hog):
+            if p is not None and p.poll() is None:
+                try:
+                    p.communicate("go\n", timeout=60)
+                except Exception:
+                    p.kill()
+        api.stop()
+    assert tam.returncode == 0, se[-3000:]
+    res = json.loads([x for x in so.splitlines() if x.startswith("{")][-1])
     print(json.dumps({"over": sorted(outs[-1]["over"]), "control": {k: snap[k] for k in ("block", "over_grant")},
                       "excess_mib": snap["host_excess"][0] >> 20, "evictions": evictions, "child": res}))
-    assert res["first_alloc"] == "allocated"
+    assert first["first"] == "oom"            # the counter rewrite bought no headroom
     assert ("uid-t", "main") in outs[-1]["over"] and not outs[-1]["no_shim"]
-    # the excess: the 1 GiB its counter rewrite hid before the passes
-    assert snap["block"] == 1 and snap["over_grant"] == 1 and snap["host_excess"][0] >= 768 << 20
+    assert snap["block"] == 1 and snap["over_grant"] == 1
     assert evictions == [("default", "t")]
     assert res["second"] == "oom" and res["parked_s"] >= 2.5
