@@ -594,7 +594,11 @@ decode_attn_mfma_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__
   typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
   typedef __attribute__((ext_vector_type(4))) float f32x4_t;
   constexpr int SPLIT = WAVES * ATT_KPW;
-  constexpr int DP = ATT_D + 4;   // padded LDS row
+  // padded LDS row: the P.V partial writes (lane (r16, q4) -> row r16,
+  // column 16dt + 4q4 + i) fall on bank r16 * DP + 4q4: a pitch of 1 (mod 32)
+  // spreads the G x 4 lanes of a write over distinct banks (D + 4 put them
+  // 4-way on 4 banks: 491k conflict cycles per call, profiles/round3/pmc_final)
+  constexpr int DP = ATT_D + 1;
   const int split = blockIdx.x;
   const int hk = blockIdx.y;
   const int b = blockIdx.z;
@@ -761,7 +765,7 @@ decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restric
   // i of wave w at position (i * WAVES + w) in the split (the waves read
   // adjacent groups at each step)
   const int SPLIT = WAVES * ATT_KPW * (MULTI ? iters : 1);
-  constexpr int DP = D + 4;
+  constexpr int DP = D + 1;   // conflict-free partial writes (decode_attn_mfma_kernel)
   const int split = blockIdx.x;
   const int hk = blockIdx.y;
   const int b = blockIdx.z;

@@ -41,6 +41,12 @@ def summarise(root: str) -> dict:
             row[c] = round(v / n, 1)
         if "FETCH_SIZE" in row and dur > 0:
             row["fetch_TBps"] = round(row["FETCH_SIZE"] * 1024 / dur / 1e3, 2)
+        # EA read requests summed over every TCC instance: 32-byte ones and
+        # the rest at 64 bytes (the memory-side read bytes, all channels)
+        rq, rq32 = row.get("TCC_EA0_RDREQ_sum"), row.get("TCC_EA0_RDREQ_32B_sum")
+        if rq is not None and rq32 is not None and dur > 0:
+            row["ea_read_MB"] = round((64 * (rq - rq32) + 32 * rq32) / 1e6, 2)
+            row["ea_read_TBps"] = round((64 * (rq - rq32) + 32 * rq32) / dur / 1e3, 2)
         out[name] = row
     return dict(sorted(out.items(), key=lambda kv: -kv[1]["mean_us"] * kv[1]["dispatches"]))
 

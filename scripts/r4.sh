@@ -36,6 +36,19 @@ for s in "$@"; do
              done
              MIVGPU_CHAIN=1 MIVGPU_CHAIN_W=4 run 200 "chain_b${b}_w4" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch $b
            done ;;
+    hbm) # HBM read bytes over ALL TCC channels (FETCH_SIZE covered half of them):
+         # the counter list, then one decode pass with the EA read-request counters summed over instances
+         export TMPDIR=/tmp PYTHONPATH=$R
+         timeout -s KILL 60 rocprofv3 -L > "$R/gpurun_out/$out/counters.txt" 2>&1
+         for cfg in full cu64; do
+           if [ $cfg = cu64 ]; then export HSA_CU_MASK=0:0-63; else unset HSA_CU_MASK; fi
+           run 150 "hbm_$cfg" rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --kernel-trace \
+             --output-format csv -d "$R/gpurun_out/$out/hbm_$cfg" -o run -- \
+             python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 3 --warmup 1 --no-graph
+           python3 "$R/scripts/probe/pmc_summary.py" "$R/gpurun_out/$out/hbm_$cfg" > "$R/gpurun_out/$out/hbm_$cfg.json" \
+             && rm -rf "$R/gpurun_out/$out/hbm_$cfg"
+         done
+         unset HSA_CU_MASK ;;
     bench) run 400 bench python -u bench.py --out "gpurun_out/$out/bench.json" ;;
     smoke) run 200 smoke python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -297,9 +297,14 @@ def test_grant_file_confines_a_hostile_tenant(tmp):
 
 
 def test_launch_overhead_of_the_shim(tmp):
-    """per-launch host cost of the hooks on a launch-bound
-    loop (100k empty kernels through hipLaunchKernel): < 1 us per launch with
-    the governor off; governor-on and graph-replay costs reported."""
+    """the hook's own host cost per launch,
+    measured in-process (csrc/bench/launch_bench.hip hook_ns: the same
+    launches through the interposed symbol and through the runtime's own
+    entry, alternating rounds behind a held stream): <= 80 ns with the
+    governor off, <= 250 ns governed (at 99 %: the gating path with next to
+    no held time); 0 natively.  Attributed to its parts by the diagnostic
+    builds of the launch path (build/diag, never shipped)."""
+    import statistics
     import subprocess
 
     from k8s_vgpu_scheduler_amd.shim import shim_env
@@ -307,54 +312,45 @@ def test_launch_overhead_of_the_shim(tmp):
 
     exe = str(build.build_launch_bench())
 
-    def run(extra, shim):
+    def run(extra, shim, preload=None):
         e = dict(os.environ)
         if shim:
             e.update(shim_env())
+        if preload:
+            e["LD_PRELOAD"] = preload
         e.update(extra)
-        r = subprocess.run([exe, "100000", "2000"], env=e, capture_output=True, text=True, timeout=120)
+        r = subprocess.run([exe, "51200", "2000"], env=e, capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr[-2000:]
         return json.loads(r.stdout.strip().splitlines()[-1])
 
-    native = min((run({}, False) for _ in range(3)), key=lambda x: x["host_launch_ns"])
-    off = min((run({"MIVGPU_SHARED_CACHE": os.path.join(tmp, f"lo{i}.cache")}, True) for i in range(3)),
-              key=lambda x: x["host_launch_ns"])
+    def med(runs):
+        out = dict(runs[0])
+        for k in ("hook_ns", "host_launch_ns", "launch_ns", "graph_launch_ns", "symbol_launch_ns", "direct_launch_ns"):
+            out[k] = round(statistics.median(r[k] for r in runs), 1)
+        return out
+
+    native = med([run({}, False) for _ in range(3)])
+    off = med([run({"MIVGPU_SHARED_CACHE": os.path.join(tmp, f"lo{i}.cache")}, True) for i in range(3)])
     on = run({"MIVGPU_SHARED_CACHE": os.path.join(tmp, "lg.cache"), "HIP_DEVICE_CORE_LIMIT": "50",
               "GPU_CORE_UTILIZATION_POLICY": "force"}, True)
-    # governed at 99 %: the gating path itself (slot lookup, batch gates, the
-    # gate kernels in the queue) with next to no held time
-    path = min((run({"MIVGPU_SHARED_CACHE": os.path.join(tmp, f"lp{i}.cache"), "HIP_DEVICE_CORE_LIMIT": "99",
-                     "GPU_CORE_UTILIZATION_POLICY": "force"}, True) for i in range(3)),
-               key=lambda x: x["host_launch_ns"])
-    # attribution: the same launch loop under the
-    # cost-attribution builds of the launch path (build/diag, never shipped)
-    def run_diag(level):
-        e = dict(os.environ)
-        e["LD_PRELOAD"] = str(build.build_hook_diag(level))
-        e["MIVGPU_SHARED_CACHE"] = os.path.join(tmp, f"ld{level}.cache")
-        r = subprocess.run([exe, "100000", "2000"], env=e, capture_output=True, text=True, timeout=120)
-        assert r.returncode == 0, r.stderr[-2000:]
-        return json.loads(r.stdout.strip().splitlines()[-1])
-    diag = {lv: min((run_diag(lv) for _ in range(3)), key=lambda x: x["host_launch_ns"]) for lv in (1, 2, 3)}
-    attribution = {"interposition_ns": round(diag[1]["host_launch_ns"] - native["host_launch_ns"], 1),
-                   "guard_init_ns": round(diag[2]["host_launch_ns"] - diag[1]["host_launch_ns"], 1),
-                   "counters_ns": round(diag[3]["host_launch_ns"] - diag[2]["host_launch_ns"], 1),
-                   "region_and_gate_checks_ns": round(off["host_launch_ns"] - diag[3]["host_launch_ns"], 1)}
+    path = med([run({"MIVGPU_SHARED_CACHE": os.path.join(tmp, f"lp{i}.cache"), "HIP_DEVICE_CORE_LIMIT": "99",
+                     "GPU_CORE_UTILIZATION_POLICY": "force"}, True) for i in range(3)])
+    diag = {lv: med([run({"MIVGPU_SHARED_CACHE": os.path.join(tmp, f"ld{lv}_{i}.cache")}, True,
+                         preload=str(build.build_hook_diag(lv))) for i in range(3)]) for lv in (1, 2, 3)}
+    attribution = {"interposition_ns": diag[1]["hook_ns"],
+                   "guard_init_ns": round(diag[2]["hook_ns"] - diag[1]["hook_ns"], 1),
+                   "counters_ns": round(diag[3]["hook_ns"] - diag[2]["hook_ns"], 1),
+                   "region_and_gate_checks_ns": round(off["hook_ns"] - diag[3]["hook_ns"], 1)}
     res = {"native": native, "shim_governor_off": off, "shim_governor_on": on, "shim_governed_99": path,
-           "attribution_host_ns": attribution,
-           "overhead_off_ns": round(off["launch_ns"] - native["launch_ns"], 1),
-           "overhead_on_ns": round(on["launch_ns"] - native["launch_ns"], 1),
-           "overhead_gating_path_ns": round(path["launch_ns"] - native["launch_ns"], 1),
-           # the enqueue cost alone (launches queued behind a
-           # held stream, not paced by the GPU's empty-kernel dispatch)
+           "diag": diag, "attribution_hook_ns": attribution,
+           "hook_off_ns": off["hook_ns"], "hook_governed_99_ns": path["hook_ns"], "hook_governed_50_ns": on["hook_ns"],
+           # separate processes (+-200 ns of the runtime's own enqueue): context only
            "host_overhead_off_ns": round(off["host_launch_ns"] - native["host_launch_ns"], 1),
-           "host_overhead_gated_99_ns": round(path["host_launch_ns"] - native["host_launch_ns"], 1)}
+           "overhead_off_ns": round(off["launch_ns"] - native["launch_ns"], 1)}
     print(json.dumps(res))
-    assert off["launch_ns"] - native["launch_ns"] < 1000.0, res
-    assert path["launch_ns"] - native["launch_ns"] < 1000.0, res
-    # measured 289-310 ns on MI355X boxes (profiles/README.md section 32)
-    assert res["host_overhead_off_ns"] < 450.0, res
-    assert res["host_overhead_gated_99_ns"] < 1000.0, res
+    assert abs(native["hook_ns"]) < 40.0, res          # the A/B itself: no hook, no difference
+    assert off["hook_ns"] <= 80.0, res
+    assert path["hook_ns"] <= 250.0, res
 
 
 def test_governor_holds_graph_decode_to_its_limit(tmp):
