@@ -53,12 +53,14 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 }
 
 // V^T for the P.V MFMAs: TR = the row-major V tile through the hardware
-// transposed read (ds_read_b64_tr_b16); !TR = V staged transposed in LDS
-// ([128 dims][32 keys + 8 pad], one 2-byte write per element) and read with
-// plain 8-byte reads (MIVGPU_FA_TR=0; the correctness fallback).
+// transposed read (ds_read_b64_tr_b16; MIVGPU_FA_TR=1, OPAQUE: =2); !TR = V
+// staged transposed in LDS ([128 dims][32 keys + 8 pad], one 2-byte write per
+// element) and read with plain 8-byte reads (the default: the transposed-read
+// build returned wrong sums on MI355X although a probe of the instruction's
+// semantics passes -- profiles/README.md section 37).
 constexpr int FA_VT_PITCH = FA_BK + 8;
 
-template <int G, bool TR>
+template <int G, bool TR, bool OPAQUE = false>
 __global__ void __launch_bounds__(G * 64)
 prefill_flash_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                      bf16_t* __restrict__ out, int L, int Hq, float scale_log2) {
@@ -197,10 +199,15 @@ prefill_flash_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
           o[dc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a4), pf[u], o[dc], 0, 0, 0);
           continue;
         }
+        int olo = v_off(row_lo, col >> 3) + (col & 7), ohi = v_off(row_hi, col >> 3) + (col & 7);
+        if constexpr (OPAQUE) {   // no constant part the compiler could fold into the offset field
+          asm volatile("" : "+v"(olo));
+          asm volatile("" : "+v"(ohi));
+        }
         const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) i16x4_t*)(&vt_lds[v_off(row_lo, col >> 3) + (col & 7)]));
+            (__attribute__((address_space(3))) i16x4_t*)(&vt_lds[olo]));
         const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) i16x4_t*)(&vt_lds[v_off(row_hi, col >> 3) + (col & 7)]));
+            (__attribute__((address_space(3))) i16x4_t*)(&vt_lds[ohi]));
         bf16x8_t a;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -235,28 +242,39 @@ prefill_flash_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
 
 // ds_read_b64_tr_b16 semantics probe: LDS holds element e = e; lane l reads
 // at element offset addr[l]; out[4l + i] = element i it received.
+// OFF: a constant element offset the compiler folds into the instruction's
+// offset field (the probe's addresses otherwise come from memory: none).
+template <int OFF>
 __global__ void __launch_bounds__(64) tr_read_probe_kernel(const int* __restrict__ addr, int* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) bf16_t lds[4096];
-  for (int i = threadIdx.x; i < 4096; i += 64) lds[i] = (bf16_t)i;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[8192];
+  for (int i = threadIdx.x; i < 8192; i += 64) lds[i] = (bf16_t)i;
   __syncthreads();
   const i16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) i16x4_t*)(&lds[addr[threadIdx.x]]));
+      (__attribute__((address_space(3))) i16x4_t*)(&lds[addr[threadIdx.x] + OFF]));
 #pragma unroll
   for (int i = 0; i < 4; ++i) out[4 * threadIdx.x + i] = (int)(uint16_t)v[i];
 }
 
-// read per launch (prompt-sized launches; tests switch it in one process)
-bool fa_tr() {
+// V^T path, read per launch (prompt-sized launches; tests switch it in one
+// process): 0 = V staged transposed, plain reads (default); 1 = transposed
+// reads; 2 = transposed reads from opaque addresses (no folded offsets).
+int fa_tr() {
   const char* e = getenv("MIVGPU_FA_TR");
-  return !(e && *e && atoi(e) == 0);
+  return e && *e ? atoi(e) : 0;
 }
 
 }  // namespace
 
 extern "C" {
 
-int mivgpu_tr_read_probe(const int* addr, int* out, hipStream_t s) {
-  hipLaunchKernelGGL(tr_read_probe_kernel, dim3(1), dim3(64), 0, s, addr, out);
+// offset_elems: 0 or 1024 (folded into the instruction's offset field)
+int mivgpu_tr_read_probe(const int* addr, int* out, int offset_elems, hipStream_t s) {
+  if (offset_elems == 0)
+    hipLaunchKernelGGL(tr_read_probe_kernel<0>, dim3(1), dim3(64), 0, s, addr, out);
+  else if (offset_elems == 1024)
+    hipLaunchKernelGGL(tr_read_probe_kernel<1024>, dim3(1), dim3(64), 0, s, addr, out);
+  else
+    return -1;
   return (int)hipGetLastError();
 }
 
@@ -270,16 +288,23 @@ int mivgpu_prefill_attention(const void* q, const void* k, const void* v, void* 
   const float sl2 = scale * 1.4426950408889634f;
   const bf16_t *qq = (const bf16_t*)q, *kk = (const bf16_t*)k, *vv = (const bf16_t*)v;
   bf16_t* oo = (bf16_t*)out;
-#define MIVGPU_FA(GG, TRV) \
-  hipLaunchKernelGGL((prefill_flash_kernel<GG, TRV>), grid, dim3(64 * GG), 0, s, qq, kk, vv, oo, L, Hq, sl2)
-  const bool tr = fa_tr();
+#define MIVGPU_FA(GG, TRV, OPQ) \
+  hipLaunchKernelGGL((prefill_flash_kernel<GG, TRV, OPQ>), grid, dim3(64 * GG), 0, s, qq, kk, vv, oo, L, Hq, sl2)
+#define MIVGPU_FA_G(GG)                                  \
+  case GG:                                               \
+    if (tr == 1) MIVGPU_FA(GG, true, false);             \
+    else if (tr == 2) MIVGPU_FA(GG, true, true);         \
+    else MIVGPU_FA(GG, false, false);                    \
+    break;
+  const int tr = fa_tr();
   switch (G) {
-    case 1: if (tr) MIVGPU_FA(1, true); else MIVGPU_FA(1, false); break;
-    case 2: if (tr) MIVGPU_FA(2, true); else MIVGPU_FA(2, false); break;
-    case 4: if (tr) MIVGPU_FA(4, true); else MIVGPU_FA(4, false); break;
-    case 8: if (tr) MIVGPU_FA(8, true); else MIVGPU_FA(8, false); break;
+    MIVGPU_FA_G(1)
+    MIVGPU_FA_G(2)
+    MIVGPU_FA_G(4)
+    MIVGPU_FA_G(8)
     default: return -1;
   }
+#undef MIVGPU_FA_G
 #undef MIVGPU_FA
   return (int)hipGetLastError();
 }

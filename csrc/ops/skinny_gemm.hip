@@ -1233,15 +1233,22 @@ __global__ void __launch_bounds__(64 * KW) skinny_widek_kernel(GemmP p, XComb xc
 // barrier releases the rest.  No L2 write-back or invalidate anywhere: the
 // first version released and acquired at agent scope in every wave and ran
 // the decode step 1.65x slower (profiles/README.md section 37).
-// Deadlock freedom: a workgroup only waits on lower block ranges, and each
-// XCD dispatches its workgroups in block order, so every producer a resident
-// consumer waits for has been dispatched ahead of it.  Spins are bounded
+// Deadlock freedom: the grid is one workgroup per CU (the kernel fits two),
+// so every worker is resident -- or becomes so as other tenants' workgroups
+// drain -- and each one's tiles of a projection only wait on tiles of earlier
+// projections.  (A first version ran each projection as its own block range
+// of the grid: consumers dispatched into whatever slots the producer left,
+// two to a CU on half the chip.)  Spins are bounded
 // (CHAIN_SPIN_TICKS of the 100 MHz real-time counter): a give-up sets the
 // error word and the launch completes (wrong output, reported, never a hang).
 // The last workgroup to finish re-zeroes the counters for the next launch.
 constexpr int CHAIN_PROJ = 4;
 constexpr int CHAIN_MAX_SPLITS = 8;
-enum { CTR_O = 0, CTR_D = 1, CTR_FIN = 2, CTR_ERR = 3, CTR_GU = 4, CTR_WORDS = CTR_GU + CHAIN_MAX_SPLITS };
+// counters, each on a 128-byte line of its own (a polled line next to
+// another counter's adds would bounce between them)
+constexpr int CTR_STRIDE = 32;
+enum { CTR_O = 0, CTR_D = 1, CTR_FIN = 2, CTR_ERR = 3, CTR_GU = 4, CTR_N = CTR_GU + CHAIN_MAX_SPLITS };
+constexpr int CTR_WORDS = CTR_N * CTR_STRIDE;
 constexpr unsigned long long CHAIN_SPIN_TICKS = 5000000ull;   // 50 ms
 
 struct ChainDeps {
@@ -1259,7 +1266,7 @@ struct ChainDeps {
   __device__ void wait(int poll_wave, int split) const {
     if (wait_ctr == nullptr) return;
     if ((int)(threadIdx.x >> 6) == poll_wave && (threadIdx.x & 63) == 0) {
-      const int* c = wait_ctr + (wait_split ? split : 0);
+      const int* c = wait_ctr + (wait_split ? split * CTR_STRIDE : 0);
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wait_target) {
         __builtin_amdgcn_s_sleep(2);
@@ -1301,41 +1308,52 @@ __global__ void __launch_bounds__(64 * W) decode_chain_kernel(ChainArgs a) {
   constexpr int LB = cmax<cmax<(int)sizeof(L0), (int)sizeof(L1)>(), cmax<(int)sizeof(L2), (int)sizeof(L3)>()>();
   __shared__ __attribute__((aligned(16))) char lds[LB];
   __shared__ int pub[CHAIN_MAX_SPLITS];
-  if (threadIdx.x < CHAIN_MAX_SPLITS) pub[threadIdx.x] = 0;   // published before any body's first barrier
   int* c = a.ctr;
-  int* pub_ctr = nullptr;
-  int b = blockIdx.x;
-  if (b < a.nblk[0]) {
-    pub_ctr = a.nblk[1] ? c + CTR_O : nullptr;
-    widek_body<1, 1, W, EPI_RESID, false>(a.g[0], b, *reinterpret_cast<L0*>(lds), XComb{},
-                                         ChainDeps{nullptr, 0, 0, pub_ctr ? pub : nullptr, 0, c + CTR_ERR});
-  } else if ((b -= a.nblk[0]) < a.nblk[1]) {
-    pub_ctr = a.nblk[2] ? c + CTR_GU : nullptr;
-    wide_body<1, 2, W, EPI_SILU_MUL>(a.g[1], b, *reinterpret_cast<L1*>(lds),
-                                     ChainDeps{a.wait_target[1] ? c + CTR_O : nullptr, a.wait_target[1], 0,
-                                               pub_ctr ? pub : nullptr, a.gu_div, c + CTR_ERR});
-  } else if ((b -= a.nblk[1]) < a.nblk[2]) {
-    pub_ctr = a.nblk[3] ? c + CTR_D : nullptr;
-    wide_body<1, 1, W, EPI_RESID>(a.g[2], b, *reinterpret_cast<L2*>(lds),
-                                  ChainDeps{a.wait_target[2] ? c + CTR_GU : nullptr, a.wait_target[2], 1,
-                                            pub_ctr ? pub : nullptr, 0, c + CTR_ERR});
-  } else {
-    b -= a.nblk[2];
-    widek_body<1, 1, W, EPI_STORE, false>(a.g[3], b, *reinterpret_cast<L3*>(lds), XComb{},
-                                         ChainDeps{a.wait_target[3] ? c + CTR_D : nullptr, a.wait_target[3], 0,
-                                                   nullptr, 0, c + CTR_ERR});
-  }
-  // every storing wave drained its write-through stores before counting
-  // itself in pub[]: one lane per counter signals for the workgroup
-  __syncthreads();
-  if (pub_ctr != nullptr && threadIdx.x < CHAIN_MAX_SPLITS && pub[threadIdx.x] > 0)
-    __hip_atomic_fetch_add(pub_ctr + threadIdx.x, pub[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // the last workgroup out re-zeroes the counters (every wait is behind it)
+  int* err = c + CTR_ERR * CTR_STRIDE;
+  const int G = gridDim.x, me = blockIdx.x;
+  // one item of projection `role`: its body, then (behind the workgroup
+  // barrier every storing wave's drained stores precede) one add per counter
+  auto item = [&](int role, int it, auto&& body) {
+    if (threadIdx.x < CHAIN_MAX_SPLITS) pub[threadIdx.x] = 0;
+    __syncthreads();   // the previous item's LDS reads are done; pub zeroed
+    body(it);
+    __syncthreads();
+    int* pc = nullptr;
+    if (role == 0 && a.nblk[1]) pc = c + CTR_O * CTR_STRIDE;
+    if (role == 1 && a.nblk[2]) pc = c + CTR_GU * CTR_STRIDE;
+    if (role == 2 && a.nblk[3]) pc = c + CTR_D * CTR_STRIDE;
+    if (pc != nullptr && threadIdx.x < CHAIN_MAX_SPLITS && pub[threadIdx.x] > 0)
+      __hip_atomic_fetch_add(pc + threadIdx.x * CTR_STRIDE, pub[threadIdx.x], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  };
+  for (int it = me; it < a.nblk[0]; it += G)
+    item(0, it, [&](int i) {
+      widek_body<1, 1, W, EPI_RESID, false>(a.g[0], i, *reinterpret_cast<L0*>(lds), XComb{},
+                                           ChainDeps{nullptr, 0, 0, a.nblk[1] ? pub : nullptr, 0, err});
+    });
+  for (int it = me; it < a.nblk[1]; it += G)
+    item(1, it, [&](int i) {
+      wide_body<1, 2, W, EPI_SILU_MUL>(a.g[1], i, *reinterpret_cast<L1*>(lds),
+                                       ChainDeps{a.wait_target[1] ? c + CTR_O * CTR_STRIDE : nullptr,
+                                                 a.wait_target[1], 0, a.nblk[2] ? pub : nullptr, a.gu_div, err});
+    });
+  for (int it = me; it < a.nblk[2]; it += G)
+    item(2, it, [&](int i) {
+      wide_body<1, 1, W, EPI_RESID>(a.g[2], i, *reinterpret_cast<L2*>(lds),
+                                    ChainDeps{a.wait_target[2] ? c + CTR_GU * CTR_STRIDE : nullptr, a.wait_target[2],
+                                              1, a.nblk[3] ? pub : nullptr, 0, err});
+    });
+  for (int it = me; it < a.nblk[3]; it += G)
+    item(3, it, [&](int i) {
+      widek_body<1, 1, W, EPI_STORE, false>(a.g[3], i, *reinterpret_cast<L3*>(lds), XComb{},
+                                           ChainDeps{a.wait_target[3] ? c + CTR_D * CTR_STRIDE : nullptr,
+                                                     a.wait_target[3], 0, nullptr, 0, err});
+    });
+  // the last worker out re-zeroes the counters (every wait is behind it)
   if (threadIdx.x == 0) {
-    const int total = a.nblk[0] + a.nblk[1] + a.nblk[2] + a.nblk[3];
-    if (__hip_atomic_fetch_add(c + CTR_FIN, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
-      for (int i = 0; i < CTR_WORDS; ++i)
-        if (i != CTR_ERR) __hip_atomic_store(c + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__hip_atomic_fetch_add(c + CTR_FIN * CTR_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
+      for (int i = 0; i < CTR_N; ++i)
+        if (i != CTR_ERR) __hip_atomic_store(c + i * CTR_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -1906,6 +1924,7 @@ struct MivgpuChainGemm {
 };
 
 int mivgpu_chain_counter_words() { return CTR_WORDS; }
+int mivgpu_chain_err_word() { return CTR_ERR * CTR_STRIDE; }
 
 // sizeof and field offsets of MivgpuChainGemm (the ctypes mirror is checked
 // against them): size, wp, x, y, M, S, scratch, tickets, rs_part, rs_nparts,
@@ -1951,8 +1970,8 @@ static int chain_blocks(int role, int W, const MivgpuChainGemm& g) {
 // One launch of up to four decode projections (o_proj, gate_up, down, qkv;
 // wp == nullptr: absent) on W-wave workgroups (2 or 4).  ctr:
 // mivgpu_chain_counter_words() ints, zero before the first launch and left
-// zero by every launch except word 3, the give-up flag (nonzero: a wait timed
-// out and the output is wrong).  Consecutive projections must chain: gate_up
+// zero by every launch except word mivgpu_chain_err_word(), the give-up flag
+// (nonzero: a wait timed out and the output is wrong).  Consecutive projections must chain: gate_up
 // reads o_proj's output and slots, down gate_up's, qkv down's.
 int mivgpu_decode_chain(const MivgpuChainGemm* g, int W, int* ctr, hipStream_t s) {
   if (g == nullptr || ctr == nullptr || (W != 2 && W != 4)) return (int)hipErrorInvalidValue;
@@ -1980,12 +1999,15 @@ int mivgpu_decode_chain(const MivgpuChainGemm* g, int W, int* ctr, hipStream_t s
   }
   a.wait_target[3] = a.nblk[2] && a.nblk[3] ? g[2].N / 32 : 0;
   a.ctr = ctr;
-  const int blocks = a.nblk[0] + a.nblk[1] + a.nblk[2] + a.nblk[3];
-  if (blocks == 0) return 0;
+  if (a.nblk[0] + a.nblk[1] + a.nblk[2] + a.nblk[3] == 0) return 0;
+  // one worker per visible CU (each CU fits two of these workgroups: every
+  // worker is resident at once, which the in-kernel waits need)
+  const int workers = mivgpu_ops_visible_cus();
+  if (workers <= 0) return (int)hipErrorInvalidValue;
   if (W == 2)
-    hipLaunchKernelGGL(decode_chain_kernel<2>, dim3(blocks), dim3(128), 0, s, a);
+    hipLaunchKernelGGL(decode_chain_kernel<2>, dim3(workers), dim3(128), 0, s, a);
   else
-    hipLaunchKernelGGL(decode_chain_kernel<4>, dim3(blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(decode_chain_kernel<4>, dim3(workers), dim3(256), 0, s, a);
   return (int)hipGetLastError();
 }
 

@@ -45,7 +45,7 @@ def lib():
                                                      vp]
         L.mivgpu_decode_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, f, vp]
         L.mivgpu_prefill_attention.argtypes = [vp, vp, vp, vp, i, i, i, i, f, vp]
-        L.mivgpu_tr_read_probe.argtypes = [vp, vp, vp]
+        L.mivgpu_tr_read_probe.argtypes = [vp, vp, i, vp]
         L.mivgpu_decode_attention_fused.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i,
                                                      i, f, f, f, i, vp]
         L.mivgpu_skinny_gemm_norm_xcomb.argtypes = [vp, vp, vp, vp, i, i, i, i, vp, i, i, i, i, i, i, i, vp, vp,
@@ -71,7 +71,7 @@ def lib():
                    "mivgpu_stream_copy", "mivgpu_stream_read", "mivgpu_ops_visible_cus",
                    "mivgpu_ops_kv_packed", "mivgpu_decode_attention_fused", "mivgpu_skinny_gemm_norm",
                    "mivgpu_prefill_qk_norm_rope_kv", "mivgpu_prefill_attention", "mivgpu_unpack_weight",
-                   "mivgpu_decode_chain", "mivgpu_chain_counter_words"):
+                   "mivgpu_decode_chain", "mivgpu_chain_counter_words", "mivgpu_chain_err_word"):
             getattr(L, fn).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -665,11 +665,13 @@ def chain_counter_words() -> int:
 
 def chain_counters(device) -> torch.Tensor:
     """Zeroed counters of one chained launch sequence (left zero by every
-    launch except word 3, the give-up flag: nonzero = a wait timed out)."""
+    launch except the give-up flag, chain_err_word(): nonzero = a wait timed
+    out)."""
     return torch.zeros(chain_counter_words(), dtype=torch.int32, device=device)
 
 
-CHAIN_ERR_WORD = 3
+def chain_err_word() -> int:
+    return int(lib().mivgpu_chain_err_word())
 
 
 class DecodeChain:
@@ -722,4 +724,4 @@ class DecodeChain:
         _check(lib().mivgpu_decode_chain(self.arr, self.W, _p(self.ctr), _stream()), "decode_chain")
 
     def gave_up(self) -> bool:
-        return int(self.ctr[CHAIN_ERR_WORD].item()) != 0
+        return int(self.ctr[chain_err_word()].item()) != 0

@@ -11,6 +11,7 @@ and by ``bench.py``/tests marked ``gpu``.
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import subprocess
@@ -552,9 +553,21 @@ def child_hog(args) -> dict:
     x = torch.empty(args.oom_probe_mib << 20, dtype=torch.uint8, device="cuda")
     x.fill_(1)
     torch.cuda.synchronize()
-    new = (set(os.listdir(kfd)) if os.path.isdir(kfd) else set()) - before
-    kfd_pid = int(new.pop()) if len(new) == 1 else os.getpid()
-    print("HOG " + json.dumps({"kfd_pid": kfd_pid, "mib": args.oom_probe_mib}), flush=True)
+    new = sorted((set(os.listdir(kfd)) if os.path.isdir(kfd) else set()) - before)
+
+    def vram(pid):   # this process's VRAM on any GPU, as KFD counts it
+        tot = 0
+        for f in glob.glob(os.path.join(kfd, pid, "vram_*")):
+            try:
+                tot += int(open(f).read().strip() or 0)
+            except (OSError, ValueError):
+                pass
+        return tot
+    # the new entry holding at least what this process allocated (several
+    # may appear at once when other processes start meanwhile)
+    mine = [p for p in new if vram(p) >= args.oom_probe_mib << 20]
+    kfd_pid = int(mine[0]) if len(mine) == 1 else (int(new[0]) if len(new) == 1 else os.getpid())
+    print("HOG " + json.dumps({"kfd_pid": kfd_pid, "mib": args.oom_probe_mib, "new_entries": len(new)}), flush=True)
     sys.stdin.readline()
     del x
     return {"mode": "hog", "kfd_pid": kfd_pid}

@@ -49,6 +49,15 @@ for s in "$@"; do
              && rm -rf "$R/gpurun_out/$out/hbm_$cfg"
          done
          unset HSA_CU_MASK ;;
+    chainprof) export TMPDIR=/tmp PYTHONPATH=$R
+         for c in 0 1; do
+           MIVGPU_CHAIN=$c run 200 "chainprof_c$c" rocprofv3 --kernel-trace --output-format csv \
+             -d "$R/gpurun_out/$out/chainprof_c$c" -o run -- \
+             python3 -m k8s_vgpu_scheduler_amd.bench.decode --batch 32 --steps 12 --warmup 2
+           python3 scripts/probe/trace_step.py "$R/gpurun_out/$out/chainprof_c$c" --steps 8 --json \
+             > "$R/gpurun_out/$out/chainprof_c$c.json" && rm -rf "$R/gpurun_out/$out/chainprof_c$c"
+         done ;;
+    launch) run 400 launch_test python -u -m pytest tests/test_shim_gpu.py -v -s $T -k launch_overhead ;;
     bench) run 400 bench python -u bench.py --out "gpurun_out/$out/bench.json" ;;
     smoke) run 200 smoke python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $s"; exit 2 ;;

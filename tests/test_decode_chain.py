@@ -30,8 +30,9 @@ def test_chain_struct_layout_matches_c(L):
 
 
 def test_counter_words(L):
-    assert ops.chain_counter_words() == 12
-    assert ops.CHAIN_ERR_WORD == 3
+    # 12 counters, each on its own 128-byte line; the give-up flag is the 4th
+    assert ops.chain_counter_words() == 12 * 32
+    assert ops.chain_err_word() == 3 * 32
 
 
 def _gemm(wp, x, y, M, K, N, S=1, rs=0, ss=0):
@@ -47,7 +48,7 @@ def _gemm(wp, x, y, M, K, N, S=1, rs=0, ss=0):
 
 def _call(L, gemms, W=2):
     arr = (ops.ChainGemm * 4)(*gemms)
-    ctr = (ctypes.c_int * 12)()
+    ctr = (ctypes.c_int * (12 * 32))()
     return L.mivgpu_decode_chain(arr, W, ctypes.cast(ctr, ctypes.c_void_p), None)
 
 

