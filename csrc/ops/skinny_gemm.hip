@@ -794,6 +794,7 @@ struct GemmP {
 // wave-group's output to its consumers.
 struct NoDeps {
   static constexpr bool chained = false;
+  static constexpr bool sc1_loads = false;
   __device__ void wait(int, int) const {}
   __device__ void publish(int) const {}
 };
@@ -826,7 +827,10 @@ __device__ __forceinline__ void wide_body(const GemmP& p, int block, WideLds<MT,
   constexpr int XC = MT * U * 256 / NTHREADS;       // X chunks per thread per group
   static_assert(XC * NTHREADS == MT * U * 256, "X tile must split evenly over the workgroup");
   constexpr bool RS = LD::RS;
-  constexpr bool SC1 = Deps::chained;               // X, slots and the residual tile come from this launch
+  // chained: X, slots and the residual tile come from this launch -- sc1
+  // loads, or plain ones after the waiting wave's acquire (ChainDeps ACQ)
+  constexpr bool SC1 = Deps::sc1_loads;
+  constexpr bool WT = Deps::chained;                // write-through stores of the handed-off output
   const u32x4_t* __restrict__ wp = p.wp;
   const bf16_t* __restrict__ x = p.x;
   bf16_t* __restrict__ y = p.y;
@@ -937,7 +941,7 @@ __device__ __forceinline__ void wide_body(const GemmP& p, int block, WideLds<MT,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // residual tile landed
   }
   if (S == 1) {
-    wide_epilogue<MT, NT, EPI, SC1>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, vgroup, r, h,
+    wide_epilogue<MT, NT, EPI, WT>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, vgroup, r, h,
                                rs, p.ss_out, res_lds, sq);
     deps.publish(vgroup);
     return;
@@ -958,7 +962,7 @@ __device__ __forceinline__ void wide_body(const GemmP& p, int block, WideLds<MT,
   if (lane == 0) ticket = atomicAdd(p.tickets + vgroup, 1);
   ticket = __shfl(ticket, 0, 64);
   if (ticket != S - 1) return;
-  wide_epilogue<MT, NT, EPI, SC1>(
+  wide_epilogue<MT, NT, EPI, WT>(
       [&](int m, int t, int e) {
         return __hip_atomic_load(sc + ((m * NT + t) * 16 + e) * 64 + lane, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
@@ -1026,10 +1030,12 @@ __device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<M
   static_assert((KW * MT * NT * 16 * 64 + MT * 32 * SQ_PITCH) * 4 <= 2 * XBUF * 2,
                 "the residual epilogue's squares tile follows the reduction in the X buffers");
   constexpr bool RS = LD::RS;
-  // X and slots produced earlier in the same launch (the chained qkv); the
-  // residual tile of a chained residual update (o_proj, the chain's first
-  // projection) comes from the previous launch: LDS-DMA as standalone
-  constexpr bool SC1 = Deps::chained;
+  // X and slots produced earlier in the same launch (the chained qkv): sc1
+  // loads, or plain ones after the acquire; the residual tile of a chained
+  // residual update (o_proj, the chain's first projection) comes from the
+  // previous launch: LDS-DMA as standalone
+  constexpr bool SC1 = Deps::sc1_loads;
+  constexpr bool WT = Deps::chained;
   const u32x4_t* __restrict__ wp = p.wp;
   const bf16_t* __restrict__ x = p.x;
   bf16_t* __restrict__ y = p.y;
@@ -1175,7 +1181,7 @@ __device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<M
         for (int e = 0; e < 16; ++e) acc[m][t][e] += red[((((w - 1) * MT + m) * NT + t) * 16 + e) * 64 + lane];
   if constexpr (EPI == EPI_RESID) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // residual tile landed
   if (S == 1) {
-    wide_epilogue<MT, NT, EPI, SC1>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, vgroup, r, h,
+    wide_epilogue<MT, NT, EPI, WT>([&](int m, int t, int e) { return acc[m][t][e]; }, y, M, ldy, tile0, vgroup, r, h,
                                rs, p.ss_out, L.s_res, red + KW * MT * NT * 16 * 64);
     deps.publish(vgroup);
     return;
@@ -1193,7 +1199,7 @@ __device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<M
   if (lane == 0) ticket = atomicAdd(p.tickets + vgroup, 1);
   ticket = __shfl(ticket, 0, 64);
   if (ticket != S - 1) return;
-  wide_epilogue<MT, NT, EPI, SC1>(
+  wide_epilogue<MT, NT, EPI, WT>(
       [&](int m, int t, int e) {
         return __hip_atomic_load(sc + ((m * NT + t) * 16 + e) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       },
@@ -1251,8 +1257,13 @@ enum { CTR_O = 0, CTR_D = 1, CTR_FIN = 2, CTR_ERR = 3, CTR_GU = 4, CTR_N = CTR_G
 constexpr int CTR_WORDS = CTR_N * CTR_STRIDE;
 constexpr unsigned long long CHAIN_SPIN_TICKS = 5000000ull;   // 50 ms
 
+template <bool ACQ>
 struct ChainDeps {
   static constexpr bool chained = true;
+  // ACQ: the polling wave acquires at agent scope once the count is reached
+  // (invalidating its XCD's L2) and the workgroup reads the handed-off bytes
+  // with plain, L2-cached loads; !ACQ: every such load is an sc1 load
+  static constexpr bool sc1_loads = !ACQ;
   int* wait_ctr;     // counter(s) to wait on (nullptr: none)
   int wait_target;   // units published per counter
   int wait_split;    // one counter per split of this projection's k-range
@@ -1274,6 +1285,12 @@ struct ChainDeps {
           __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
+      }
+    }
+    if constexpr (ACQ) {
+      if ((int)(threadIdx.x >> 6) == poll_wave) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the invalidate done before the barrier
       }
     }
     __syncthreads();
@@ -1299,8 +1316,9 @@ struct ChainArgs {
 template <int a, int b>
 constexpr int cmax() { return a > b ? a : b; }
 
-template <int W>
+template <int W, bool ACQ>
 __global__ void __launch_bounds__(64 * W) decode_chain_kernel(ChainArgs a) {
+  using Deps = ChainDeps<ACQ>;
   using L0 = WidekLds<1, 1, W, EPI_RESID>;
   using L1 = WideLds<1, 2, W, EPI_SILU_MUL>;
   using L2 = WideLds<1, 1, W, EPI_RESID>;
@@ -1329,24 +1347,24 @@ __global__ void __launch_bounds__(64 * W) decode_chain_kernel(ChainArgs a) {
   for (int it = me; it < a.nblk[0]; it += G)
     item(0, it, [&](int i) {
       widek_body<1, 1, W, EPI_RESID, false>(a.g[0], i, *reinterpret_cast<L0*>(lds), XComb{},
-                                           ChainDeps{nullptr, 0, 0, a.nblk[1] ? pub : nullptr, 0, err});
+                                           Deps{nullptr, 0, 0, a.nblk[1] ? pub : nullptr, 0, err});
     });
   for (int it = me; it < a.nblk[1]; it += G)
     item(1, it, [&](int i) {
       wide_body<1, 2, W, EPI_SILU_MUL>(a.g[1], i, *reinterpret_cast<L1*>(lds),
-                                       ChainDeps{a.wait_target[1] ? c + CTR_O * CTR_STRIDE : nullptr,
+                                       Deps{a.wait_target[1] ? c + CTR_O * CTR_STRIDE : nullptr,
                                                  a.wait_target[1], 0, a.nblk[2] ? pub : nullptr, a.gu_div, err});
     });
   for (int it = me; it < a.nblk[2]; it += G)
     item(2, it, [&](int i) {
       wide_body<1, 1, W, EPI_RESID>(a.g[2], i, *reinterpret_cast<L2*>(lds),
-                                    ChainDeps{a.wait_target[2] ? c + CTR_GU * CTR_STRIDE : nullptr, a.wait_target[2],
+                                    Deps{a.wait_target[2] ? c + CTR_GU * CTR_STRIDE : nullptr, a.wait_target[2],
                                               1, a.nblk[3] ? pub : nullptr, 0, err});
     });
   for (int it = me; it < a.nblk[3]; it += G)
     item(3, it, [&](int i) {
       widek_body<1, 1, W, EPI_STORE, false>(a.g[3], i, *reinterpret_cast<L3*>(lds), XComb{},
-                                           ChainDeps{a.wait_target[3] ? c + CTR_D * CTR_STRIDE : nullptr,
+                                           Deps{a.wait_target[3] ? c + CTR_D * CTR_STRIDE : nullptr,
                                                      a.wait_target[3], 0, nullptr, 0, err});
     });
   // the last worker out re-zeroes the counters (every wait is behind it)
@@ -2004,10 +2022,19 @@ int mivgpu_decode_chain(const MivgpuChainGemm* g, int W, int* ctr, hipStream_t s
   // worker is resident at once, which the in-kernel waits need)
   const int workers = mivgpu_ops_visible_cus();
   if (workers <= 0) return (int)hipErrorInvalidValue;
-  if (W == 2)
-    hipLaunchKernelGGL(decode_chain_kernel<2>, dim3(workers), dim3(128), 0, s, a);
-  else
-    hipLaunchKernelGGL(decode_chain_kernel<4>, dim3(workers), dim3(256), 0, s, a);
+  // hand-off reads: acquire + L2-cached loads (default) or sc1 loads
+  // (MIVGPU_CHAIN_SC1=1, A/B)
+  static const bool sc1 = [] {
+    const char* e = getenv("MIVGPU_CHAIN_SC1");
+    return e && *e && atoi(e) != 0;
+  }();
+  if (W == 2) {
+    if (sc1) hipLaunchKernelGGL((decode_chain_kernel<2, false>), dim3(workers), dim3(128), 0, s, a);
+    else hipLaunchKernelGGL((decode_chain_kernel<2, true>), dim3(workers), dim3(128), 0, s, a);
+  } else {
+    if (sc1) hipLaunchKernelGGL((decode_chain_kernel<4, false>), dim3(workers), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((decode_chain_kernel<4, true>), dim3(workers), dim3(256), 0, s, a);
+  }
   return (int)hipGetLastError();
 }
 

@@ -439,6 +439,7 @@ struct Config {
   uint64_t context_refresh_ns = 20000000;  // at most one KFD read per 20 ms (forced before an OOM)
   bool occupancy = true;                   // charge the governor the sampled wave-occupancy share
   uint64_t occ_period_ns = 2000000;        // sampling period while the governor runs (2 ms)
+  uint64_t peer_busy_ns = 0;               // 0: a peer contends in the samples it has waves beyond a gate's
   uint64_t occ_idle_period_ns = 50000000;  // ... and for utilisation reporting only (50 ms)
   double share_tau_ns = 250e6;             // EWMA time constant of the occupancy averages (>> holds, batches)
   // A/B switches (not grant keys, ignored under a grant file, see
@@ -637,6 +638,7 @@ void load_config() {
   g_cfg.occupancy = !(oc && (!strcmp(oc, "0") || !strcasecmp(oc, "false")));
   const char* op = grant_env("MIVGPU_OCC_PERIOD_US");
   if (op && atoll(op) >= 200) g_cfg.occ_period_ns = (uint64_t)atoll(op) * 1000ull;
+  if (const char* pb = unguarded_env("MIVGPU_PEER_BUSY_MS")) g_cfg.peer_busy_ns = (uint64_t)atoll(pb) * 1000000ull;
   const char* gm = unguarded_env("MIVGPU_GATE_MODE");
   g_cfg.gate_device_mode = gm && !strcmp(gm, "device");
   const char* se = unguarded_env("MIVGPU_SHARE_EST");
@@ -1789,19 +1791,23 @@ bool occ_sample(int dev, uint64_t now) {
   // wave among them: discounting one CU's worth for peers but not for itself
   // billed every symmetric tenant above 1/N -- measured, 8 x 12 % decode
   // tenants held 27 % of the time).
-  // A peer showing only its gate wave is held, not contending: it does not
-  // dilute this process's charge while it holds (measured: a 75 % tenant
-  // next to a 25 % one was charged half of its solo time while the 25 % one
-  // sat in its gate, and settled at 50 % instead of 75 %).
+  // A peer contends while it has more than a gate's wave resident.  One
+  // showing only its gate wave (held) or nothing this sample does not dilute
+  // this process's charge (measured: a 75 % tenant next to a 25 % one was
+  // charged half of its solo time while the 25 % one sat in its gate, and
+  // settled at 50 % instead of 75 %).  MIVGPU_PEER_BUSY_MS > 0 restores a
+  // window of that many ms after the last sample with waves (the round-3
+  // rule, 200).
   long others = 0;
   int busy_peers = 0;
   for (auto& p : o.peers) {
     int v = read_occ(p.fd);
     p.v = v > 0 ? v : 0;
-    p.held = v == kGateWaves;
+    p.held = g_cfg.peer_busy_ns ? v == kGateWaves : v <= kGateWaves;
     if (v > 0) others += v;
     if (v > kGateWaves) p.busy_ns = now;
-    if (p.busy_ns && now - p.busy_ns < kPeerBusyNs && !p.held) ++busy_peers;
+    if (p.busy_ns && now - p.busy_ns < (g_cfg.peer_busy_ns ? g_cfg.peer_busy_ns : kPeerBusyNs) && !p.held)
+      ++busy_peers;
   }
   // The gate's own resident wave is not consumption: discount one unit per
   // gate slot holding right now.
@@ -1884,7 +1890,8 @@ bool occ_sample(int dev, uint64_t now) {
       int comparable = 0;
       double heavier = 0;
       for (const auto& p : o.peers) {
-        if (!p.busy_ns || now - p.busy_ns >= kPeerBusyNs || p.held) continue;
+        if (!p.busy_ns || now - p.busy_ns >= (g_cfg.peer_busy_ns ? g_cfg.peer_busy_ns : kPeerBusyNs) || p.held)
+          continue;
         if (p.avg * kContendFrac > o.own_avg) heavier += p.avg;
         else if (p.avg >= kContendFrac * o.own_avg) ++comparable;
       }

@@ -509,6 +509,10 @@ def child_tamper(args) -> dict:
         first = "allocated"
     except torch.OutOfMemoryError:
         first = "oom"
+    # the launch below must not allocate (an over-grant container gets no
+    # memory at all): its operand exists before the verdict
+    w = torch.zeros(1 << 16, device="cuda")
+    torch.cuda.synchronize()
     print("TAMPERED " + json.dumps({"first": first, "kfd_pid": kfd_pid}), flush=True)
     sys.stdin.readline()                      # the parent's monitor pass(es)
     stop = threading.Event()
@@ -528,8 +532,9 @@ def child_tamper(args) -> dict:
     except torch.OutOfMemoryError:
         second = "oom"
     t0 = time.time()
-    w = torch.ones(1 << 16, device="cuda") + 1         # parked while the control block holds
-    total = float(w.sum().item())
+    w.add_(1)                                 # parked while the control block holds
+    torch.cuda.synchronize()
+    total = float(w[0].item())
     parked_s = time.time() - t0
     stop.set()
     th.join()
