@@ -2024,10 +2024,8 @@ int mivgpu_decode_chain(const MivgpuChainGemm* g, int W, int* ctr, hipStream_t s
   if (workers <= 0) return (int)hipErrorInvalidValue;
   // hand-off reads: acquire + L2-cached loads (default) or sc1 loads
   // (MIVGPU_CHAIN_SC1=1, A/B)
-  static const bool sc1 = [] {
-    const char* e = getenv("MIVGPU_CHAIN_SC1");
-    return e && *e && atoi(e) != 0;
-  }();
+  const char* e = getenv("MIVGPU_CHAIN_SC1");   // per call: tests switch it in one process
+  const bool sc1 = e && *e && atoi(e) != 0;
   if (W == 2) {
     if (sc1) hipLaunchKernelGGL((decode_chain_kernel<2, false>), dim3(workers), dim3(128), 0, s, a);
     else hipLaunchKernelGGL((decode_chain_kernel<2, true>), dim3(workers), dim3(128), 0, s, a);

@@ -227,7 +227,10 @@ class Qwen3Decoder:
         # launches per layer with the attention.  MIVGPU_CHAIN_W: waves per
         # workgroup (2: gate_up / down at their tuned wide plans, o_proj / qkv
         # on 2-wave K-split workgroups); MIVGPU_CHAIN_DOWN_S: down's k-split.
-        self.chain = (self.norm_fused and batch <= 32 and os.environ.get("MIVGPU_CHAIN", "0") == "1")
+        # MIVGPU_CHAIN=gd chains gate_up -> down only (o_proj / qkv stay on
+        # their own 4-wave K-split launches).
+        self.chain_mode = os.environ.get("MIVGPU_CHAIN", "0")
+        self.chain = self.norm_fused and batch <= 32 and self.chain_mode in ("1", "gd")
         self.chain_w = int(os.environ.get("MIVGPU_CHAIN_W", "2"))
         self.chain_down_s = int(os.environ.get("MIVGPU_CHAIN_DOWN_S", "4"))
         if self.norm_fused:
@@ -354,6 +357,12 @@ class Qwen3Decoder:
         chains = []
         for li, lw in enumerate(self.w.layers):
             nxt = self.w.layers[li + 1] if li + 1 < cfg.layers else None
+            if self.chain_mode == "gd":
+                chains.append(ops.DecodeChain(
+                    gu=dict(pl=lw["pgu"], x=self.res, y=self.act, rs=(self.ss_b, self.slots_o, h, eps)),
+                    d=dict(pl=lw["pd"], x=self.act, y=self.res, ss=self.ss_a),
+                    W=self.chain_w, down_splits=self.chain_down_s, ctr=ctr))
+                continue
             chains.append(ops.DecodeChain(
                 o=dict(pl=lw["po"], x=self.attn, y=self.res, ss=self.ss_b),
                 gu=dict(pl=lw["pgu"], x=self.res, y=self.act, rs=(self.ss_b, self.chain_slots_o, h, eps)),
@@ -369,6 +378,18 @@ class Qwen3Decoder:
         cfg, w = self.cfg, self.w
         h, eps = cfg.hidden, cfg.eps
         ops.embed_rmsnorm(w.embed, self.tokens, None, cfg.eps, res=self.res, out=None, ss_out=self.ss_a)
+        if self.chain_mode == "gd":
+            na = 1
+            for li, lw in enumerate(w.layers):
+                lw["pqkv"].norm_call(self.res, out=self.qkv_buf, row_scale=(self.ss_a, na, h, eps))
+                self._attention(li, lw, self.qkv_buf)
+                lw["po"].norm_call(self.attn, out=self.res, residual=True, ss_out=self.ss_b)
+                self._chains[li]()
+                na = self.chain_slots_d
+            ops.rmsnorm(self.res, w.final_norm, eps, out=self.h)
+            logits = self.p_lm(self.h, out=self.logits)
+            self._tail(logits)
+            return logits
         w.layers[0]["pqkv"].norm_call(self.res, out=self.qkv_buf, row_scale=(self.ss_a, 1, h, eps))
         for li, lw in enumerate(w.layers):
             self._attention(li, lw, self.qkv_buf)

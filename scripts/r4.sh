@@ -34,7 +34,8 @@ for s in "$@"; do
              for c in 0 1; do
                MIVGPU_CHAIN=$c run 200 "chain_b${b}_c$c" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch $b
              done
-             MIVGPU_CHAIN=1 MIVGPU_CHAIN_W=4 run 200 "chain_b${b}_w4" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch $b
+             MIVGPU_CHAIN=gd run 200 "chain_b${b}_gd" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch $b
+             MIVGPU_CHAIN=1 MIVGPU_CHAIN_SC1=1 run 200 "chain_b${b}_sc1" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch $b
            done ;;
     hbm) # HBM read bytes over ALL TCC channels (FETCH_SIZE covered half of them):
          # the counter list, then one decode pass with the EA read-request counters summed over instances

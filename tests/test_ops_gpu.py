@@ -737,16 +737,18 @@ def test_decoder_packed_only_long_prefill(monkeypatch):
     _close(a.prefill(prompt), b.prefill(prompt), 5e-2)
 
 
-@pytest.mark.parametrize("B,W", [(1, 2), (5, 2), (32, 2), (5, 4), (32, 4)])
-def test_decoder_chain_matches_reference(monkeypatch, B, W):
+@pytest.mark.parametrize("B,W,mode,sc1", [(1, 2, "1", "0"), (5, 2, "1", "0"), (32, 2, "1", "0"), (5, 4, "1", "0"),
+                                          (32, 4, "1", "0"), (5, 2, "1", "1"), (32, 2, "gd", "0"), (1, 2, "gd", "1")])
+def test_decoder_chain_matches_reference(monkeypatch, B, W, mode, sc1):
     """Chained projections (o_proj -> gate_up -> down -> next qkv in one
     launch, in-kernel waits): 3 steps vs the fp32 reference decoder, no wait
     gave up."""
     from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
 
     monkeypatch.setenv("MIVGPU_NORM_FUSED", "1")
-    monkeypatch.setenv("MIVGPU_CHAIN", "1")
+    monkeypatch.setenv("MIVGPU_CHAIN", mode)
     monkeypatch.setenv("MIVGPU_CHAIN_W", str(W))
+    monkeypatch.setenv("MIVGPU_CHAIN_SC1", sc1)
     a = Qwen3Decoder(QWEN3_TINY, batch=B, max_ctx=96, device="cuda", native=True, seed=14)
     assert a.chain and len(a._chains) == QWEN3_TINY.layers
     b = Qwen3Decoder(QWEN3_TINY, batch=B, max_ctx=96, device="cuda", native=False, seed=14)
