@@ -146,26 +146,28 @@ int main(int argc, char** argv) {
   // and `half` through the runtime's own entry, in alternating order, behind
   // one hold each round.
   const launch_fn direct = reinterpret_cast<launch_fn>(runtime_symbol("hipLaunchKernel"));
-  double hook_ns = -1, plt_ns = -1, direct_ns = -1;
+  double hook_ns = -1, plt_ns = -1, direct_ns = -1, hook_p25 = -1, hook_p75 = -1;
   if (direct) {
     int* nullp = nullptr;
     void* kargs[] = {&nullp};
     const void* fn = reinterpret_cast<const void*>(empty_kernel);
-    const long half = 256, ab_rounds = rounds;
+    // ABBA legs of `leg` launches per round behind one hold: a per-round
+    // difference free of slow drifts (clock, queue depth); median of 400
+    const long leg = 64, ab_rounds = 400;
     std::vector<double> diff;
     double sum_a = 0, sum_b = 0;
     for (long r = 0; r < ab_rounds; ++r) {
       __atomic_store_n(flag, 0, __ATOMIC_RELEASE);
       hold_until<<<1, 64, 0, s>>>(flag);
       double ta = 0, tb = 0;
-      for (int leg = 0; leg < 2; ++leg) {
-        const bool via_sym = (leg == 0) == (r % 2 == 0);
+      for (int l = 0; l < 4; ++l) {
+        const bool via_sym = (l == 0 || l == 3) == (r % 2 == 0);
         const double h0 = now_ns();
         if (via_sym)
-          for (long i = 0; i < half; ++i) hipLaunchKernel(fn, dim3(1), dim3(64), kargs, 0, s);
+          for (long i = 0; i < leg; ++i) hipLaunchKernel(fn, dim3(1), dim3(64), kargs, 0, s);
         else
-          for (long i = 0; i < half; ++i) direct(fn, dim3(1), dim3(64), kargs, 0, s);
-        (via_sym ? ta : tb) = (now_ns() - h0) / (double)half;
+          for (long i = 0; i < leg; ++i) direct(fn, dim3(1), dim3(64), kargs, 0, s);
+        (via_sym ? ta : tb) += (now_ns() - h0) / (double)(2 * leg);
       }
       __atomic_store_n(flag, 1, __ATOMIC_RELEASE);
       CHECK(hipStreamSynchronize(s));
@@ -176,6 +178,8 @@ int main(int argc, char** argv) {
     }
     std::sort(diff.begin(), diff.end());
     hook_ns = diff[diff.size() / 2];
+    hook_p25 = diff[diff.size() / 4];
+    hook_p75 = diff[3 * diff.size() / 4];
     plt_ns = sum_a / (double)ab_rounds;
     direct_ns = sum_b / (double)ab_rounds;
   }
@@ -184,8 +188,9 @@ int main(int argc, char** argv) {
   if (getenv("LAUNCH_BENCH_NO_GRAPH")) {
     CHECK(hipStreamDestroy(s));
     printf("{\"launches\": %ld, \"launch_ns\": %.1f, \"launch_drain_ns\": %.1f, \"host_launch_ns\": %.1f, "
-           "\"hook_ns\": %.1f, \"symbol_launch_ns\": %.1f, \"direct_launch_ns\": %.1f}\n",
-           n, (t1 - t0) / n, (t2 - t0) / n, host_launch_ns, hook_ns, plt_ns, direct_ns);
+           "\"hook_ns\": %.1f, \"hook_p25_ns\": %.1f, \"hook_p75_ns\": %.1f, \"symbol_launch_ns\": %.1f, "
+           "\"direct_launch_ns\": %.1f}\n",
+           n, (t1 - t0) / n, (t2 - t0) / n, host_launch_ns, hook_ns, hook_p25, hook_p75, plt_ns, direct_ns);
     return 0;
   }
   // graph replay: 32 empty kernels per graph
@@ -206,9 +211,9 @@ int main(int argc, char** argv) {
   CHECK(hipGraphDestroy(g));
   CHECK(hipStreamDestroy(s));
   printf("{\"launches\": %ld, \"launch_ns\": %.1f, \"launch_drain_ns\": %.1f, \"host_launch_ns\": %.1f, "
-         "\"hook_ns\": %.1f, \"symbol_launch_ns\": %.1f, \"direct_launch_ns\": %.1f, "
-         "\"graph_replays\": %ld, \"graph_launch_ns\": %.1f, \"graph_drain_ns\": %.1f}\n",
-         n, (t1 - t0) / n, (t2 - t0) / n, host_launch_ns, hook_ns, plt_ns, direct_ns, replays, (g1 - g0) / replays,
-         (g2 - g0) / replays);
+         "\"hook_ns\": %.1f, \"hook_p25_ns\": %.1f, \"hook_p75_ns\": %.1f, \"symbol_launch_ns\": %.1f, "
+         "\"direct_launch_ns\": %.1f, \"graph_replays\": %ld, \"graph_launch_ns\": %.1f, \"graph_drain_ns\": %.1f}\n",
+         n, (t1 - t0) / n, (t2 - t0) / n, host_launch_ns, hook_ns, hook_p25, hook_p75, plt_ns, direct_ns, replays,
+         (g1 - g0) / replays, (g2 - g0) / replays);
   return 0;
 }

@@ -59,6 +59,7 @@ for s in "$@"; do
              > "$R/gpurun_out/$out/chainprof_c$c.json" && rm -rf "$R/gpurun_out/$out/chainprof_c$c"
          done ;;
     launch) run 400 launch_test python -u -m pytest tests/test_shim_gpu.py -v -s $T -k launch_overhead ;;
+    tenant) run 300 tenant_test python -u -m pytest tests/test_shim_interpose_gpu.py -v -s $T -k "tenant_" ;;
     bench) run 400 bench python -u bench.py --out "gpurun_out/$out/bench.json" ;;
     smoke) run 200 smoke python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -166,6 +166,34 @@ def _container(tmp, name):
     return hook, grant, cache, ctl
 
 
+def _kfd_vram() -> dict:
+    """KFD's per-process VRAM (all GPUs) by host pid."""
+    import glob
+
+    out = {}
+    for d in glob.glob("/sys/class/kfd/kfd/proc/*"):
+        tot = 0
+        for f in glob.glob(os.path.join(d, "vram_*")):
+            try:
+                tot += int(open(f).read().strip() or 0)
+            except (OSError, ValueError):
+                pass
+        out[int(os.path.basename(d))] = tot
+    return out
+
+
+def _spawn_hog(mib):
+    """A container process without the shim holding ``mib`` MiB; its KFD
+    (host) pid: the one new KFD process entry holding that much (found from
+    here, the box may run us in a pid namespace)."""
+    before = set(_kfd_vram())
+    p, info = _spawn(["--child", "hog", "--oom-probe-mib", str(mib)], dict(os.environ), "HOG")
+    new = {pid: v for pid, v in _kfd_vram().items() if pid not in before and v >= mib << 20}
+    assert len(new) == 1, (new, info)
+    info["kfd_pid"] = next(iter(new))
+    return p, info
+
+
 def _spawn(args, env, tag):
     import subprocess
     import sys
@@ -218,7 +246,7 @@ def test_tenant_without_the_shim_reported_within_one_pass(tmp):
     api = _api()
     hog = None
     try:
-        hog, info = _spawn(["--child", "hog", "--oom-probe-mib", "4608"], dict(os.environ), "HOG")
+        hog, info = _spawn_hog(4608)
         outs = _monitor(hook, api, [info["kfd_pid"]], passes=1)
         snap = ControlFile(ctl).snapshot()
         evictions = list(api.cluster.evictions)
@@ -255,7 +283,7 @@ def test_tenant_rewriting_its_region_cannot_unblock_itself(tmp):
     se = ""
     try:
         tam, first = _spawn(["--child", "tamper", "--out", cache, "--oom-probe-mib", "3500"], env, "TAMPERED")
-        hog, info = _spawn(["--child", "hog", "--oom-probe-mib", "4096"], dict(os.environ), "HOG")
+        hog, info = _spawn_hog(4096)
         outs = _monitor(hook, api, [first["kfd_pid"], info["kfd_pid"]], passes=2)
         snap = ControlFile(ctl).snapshot()
         tam.stdin.write("go\n")
