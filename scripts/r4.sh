@@ -61,6 +61,9 @@ for s in "$@"; do
     launch) run 400 launch_test python -u -m pytest tests/test_shim_gpu.py -v -s $T -k launch_overhead ;;
     tenant) run 300 tenant_test python -u -m pytest tests/test_shim_interpose_gpu.py -v -s $T -k "tenant_" ;;
     bench) run 400 bench python -u bench.py --out "gpurun_out/$out/bench.json" ;;
+    curve) for n in 1 2 8; do
+             run 400 "bench_s$n" python -u bench.py --slices $n --out "gpurun_out/$out/s$n.json"
+           done ;;
     smoke) run 200 smoke python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
