@@ -427,6 +427,13 @@ REAL_DECL(hipError_t, hipSetDevice, "hip_4.2", (int))
 REAL_DECL(hipError_t, hipMemset, "hip_4.2", (void*, int, size_t))
 
 // ------------------------------------------------------------------ config --
+// Default contention window of the share estimator (ms; 0 = per sample),
+// chosen by measurement (profiles/README.md section 37); measurement builds
+// set it with -D (utils/build.py build_shim_variant).
+#ifndef MIVGPU_PEER_BUSY_MS_DEFAULT
+#define MIVGPU_PEER_BUSY_MS_DEFAULT 10
+#endif
+
 struct Config {
   uint64_t mem_limit[MIVGPU_MAX_DEVICES] = {0};
   int cu_limit[MIVGPU_MAX_DEVICES];  // percent per device (HIP_DEVICE_CORE_LIMIT[_i])
@@ -439,7 +446,9 @@ struct Config {
   uint64_t context_refresh_ns = 20000000;  // at most one KFD read per 20 ms (forced before an OOM)
   bool occupancy = true;                   // charge the governor the sampled wave-occupancy share
   uint64_t occ_period_ns = 2000000;        // sampling period while the governor runs (2 ms)
-  uint64_t peer_busy_ns = 0;               // 0: a peer contends in the samples it has waves beyond a gate's
+  // a peer contends for this long after a sample with waves beyond a gate's
+  // (0: in such samples only); one showing exactly its gate's wave is held
+  uint64_t peer_busy_ns = (uint64_t)MIVGPU_PEER_BUSY_MS_DEFAULT * 1000000ull;
   uint64_t occ_idle_period_ns = 50000000;  // ... and for utilisation reporting only (50 ms)
   double share_tau_ns = 250e6;             // EWMA time constant of the occupancy averages (>> holds, batches)
   // A/B switches (not grant keys, ignored under a grant file, see
@@ -1803,7 +1812,7 @@ bool occ_sample(int dev, uint64_t now) {
   for (auto& p : o.peers) {
     int v = read_occ(p.fd);
     p.v = v > 0 ? v : 0;
-    p.held = g_cfg.peer_busy_ns ? v == kGateWaves : v <= kGateWaves;
+    p.held = g_cfg.peer_busy_ns ? v == kGateWaves : v <= kGateWaves;   // per sample: idle counts as held
     if (v > 0) others += v;
     if (v > kGateWaves) p.busy_ns = now;
     if (p.busy_ns && now - p.busy_ns < (g_cfg.peer_busy_ns ? g_cfg.peer_busy_ns : kPeerBusyNs) && !p.held)

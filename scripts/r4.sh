@@ -60,6 +60,13 @@ for s in "$@"; do
          done ;;
     launch) run 400 launch_test python -u -m pytest tests/test_shim_gpu.py -v -s $T -k launch_overhead ;;
     tenant) run 300 tenant_test python -u -m pytest tests/test_shim_interpose_gpu.py -v -s $T -k "tenant_" ;;
+    govab) # share-estimator contention window A/B (build/variants/libmivgpu_pb<ms>.so)
+         for w in ${GOVAB_WINDOWS:-10 50}; do
+           MIVGPU_SHIM_PATH="$R/build/variants/libmivgpu_pb$w.so" run 300 "govab_s8_pb$w" \
+             python -u bench.py --slices 8 --rounds temporal --out "gpurun_out/$out/govab_s8_pb$w.json"
+           MIVGPU_SHIM_PATH="$R/build/variants/libmivgpu_pb$w.so" run 500 "govab_unequal_pb$w" \
+             python -u -m pytest tests/test_shim_gpu.py -v -s $T -k "unequal or charged_the_share"
+         done ;;
     bench) run 400 bench python -u bench.py --out "gpurun_out/$out/bench.json" ;;
     curve) for n in 1 2 8; do
              run 400 "bench_s$n" python -u bench.py --slices $n --out "gpurun_out/$out/s$n.json"
