@@ -67,6 +67,8 @@ for s in "$@"; do
            MIVGPU_SHIM_PATH="$R/build/variants/libmivgpu_pb$w.so" run 500 "govab_unequal_pb$w" \
              python -u -m pytest tests/test_shim_gpu.py -v -s $T -k "unequal or charged_the_share"
          done ;;
+    serve) run 1100 serving python -u -m k8s_vgpu_scheduler_amd.bench.serving --configs native,vgpu50 \
+             --warmup 30 --runs 200 --long-prompt-tokens 8000 --out-dir "gpurun_out/$out/serving" ;;
     bench) run 400 bench python -u bench.py --out "gpurun_out/$out/bench.json" ;;
     curve) for n in 1 2 8; do
              run 400 "bench_s$n" python -u bench.py --slices $n --out "gpurun_out/$out/s$n.json"
