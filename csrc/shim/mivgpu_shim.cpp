@@ -1684,6 +1684,8 @@ struct OccPeer {
 constexpr double kContendFrac = 0.1;
 // A peer is busy for this long after its last sample with waves resident.
 constexpr uint64_t kPeerBusyNs = 200000000ull;   // 200 ms
+// Idle time after which the host bucket stops accruing entitlement.
+constexpr uint64_t kAccrueIdleNs = 20000000ull;   // 20 ms
 // A governed peer held behind its gate has exactly its gate kernel's wave
 // resident (governor.hip host_bucket_gate: one 64-lane wave).
 constexpr int kGateWaves = 1;
@@ -1704,6 +1706,7 @@ struct OccDev {
   double win_start_share = 0;
   bool bucket = false;         // host bucket started (the device's gate is up)
   double tokens_ns = 0;        // host bucket balance: rate x wall time - GPU time received
+  uint64_t owed_ns = 0;        // last sample in which the process owed GPU work
   uint64_t batch_win_ns = 0;   // batch-size estimate window (host mode)
   uint64_t batch_win_launches = 0;
   double batch_win_share = 0;
@@ -1938,7 +1941,14 @@ bool occ_sample(int dev, uint64_t now) {
       o.bucket = true;
       o.tokens_ns = 0;
     } else {
-      o.tokens_ns += rate * (double)dt - share * run;
+      // Entitlement accrues while the process owes work and through short
+      // gaps (host syncs, batch edges), not over long idle stretches: a
+      // torch.compile'd loop otherwise banked the whole 100 ms burst while
+      // Inductor compiled on the CPU and spent it at the start of its timed
+      // loop (0.311 of unthrottled under a 25 % limit)
+      if (owes) o.owed_ns = now;
+      const bool accrue = owes || (o.owed_ns && now - o.owed_ns < kAccrueIdleNs);
+      o.tokens_ns += (accrue ? rate * (double)dt : 0.0) - share * run;
       if (o.tokens_ns > cap) o.tokens_ns = cap;
       if (o.tokens_ns < -cap) o.tokens_ns = -cap;
     }

@@ -59,6 +59,7 @@ for s in "$@"; do
              > "$R/gpurun_out/$out/chainprof_c$c.json" && rm -rf "$R/gpurun_out/$out/chainprof_c$c"
          done ;;
     launch) run 400 launch_test python -u -m pytest tests/test_shim_gpu.py -v -s $T -k launch_overhead ;;
+    interpose) run 600 interpose_tests python -u -m pytest tests/test_shim_interpose_gpu.py -v -s $T -k "triton or compile" ;;
     tenant) run 300 tenant_test python -u -m pytest tests/test_shim_interpose_gpu.py -v -s $T -k "tenant_" ;;
     govab) # share-estimator contention window A/B (build/variants/libmivgpu_pb<ms>.so)
          for w in ${GOVAB_WINDOWS:-10 50}; do

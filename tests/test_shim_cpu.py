@@ -461,7 +461,7 @@ def test_governor_host_path_on_the_mock(native_build, tmp_path):
     (30, 2, 25, "debt", False, 1.0),    # a 15x lighter peer does not dilute the charge
     (0, 50, 25, "full", True, 0.0),     # queued behind a peer, no waves resident: charged nothing
     (0, 0, 25, "debt", True, 1.0),      # alone and launching, no wave caught resident: still its GPU time
-    (0, 0, 25, "full", False, 0.0),     # alone and idle: nothing
+    (0, 0, 25, "idle", False, 0.0),     # alone and idle: nothing, and no banked burst either
 ])
 def test_host_bucket_charges_the_share_received(native_build, tmp_path, own, peer, limit, trend, busy, frac):
     """Host-bucket mode: the sampler charges the GPU time
@@ -485,6 +485,10 @@ def test_host_bucket_charges_the_share_received(native_build, tmp_path, own, pee
         assert bal["tokens_ns"] < -50_000_000, bal          # 0.9 s at 75 % over the limit: -100 ms bound
     elif trend == "even":
         assert abs(bal["tokens_ns"]) <= 20_000_000, bal      # the bucket starts empty and stays there
+    elif trend == "idle":
+        # entitlement accrues only while work is owed and 20 ms after: 0.9 s
+        # of idling banks at most 25 % x 20 ms, not the 100 ms burst
+        assert 0 <= bal["tokens_ns"] <= 10_000_000, bal
     else:
         assert bal["tokens_ns"] >= 95_000_000, bal           # fills to the 100 ms burst
     # the integral of the received share
