@@ -427,11 +427,11 @@ REAL_DECL(hipError_t, hipSetDevice, "hip_4.2", (int))
 REAL_DECL(hipError_t, hipMemset, "hip_4.2", (void*, int, size_t))
 
 // ------------------------------------------------------------------ config --
-// Default contention window of the share estimator (ms; 0 = per sample),
-// chosen by measurement (profiles/README.md section 37); measurement builds
-// set it with -D (utils/build.py build_shim_variant).
+// A fixed contention window of the share estimator (ms) for measurement
+// builds (-D, utils/build.py build_shim_variant); 0 = the adaptive default
+// (per sample with few peers, 200 ms with many; profiles/README.md section 37).
 #ifndef MIVGPU_PEER_BUSY_MS_DEFAULT
-#define MIVGPU_PEER_BUSY_MS_DEFAULT 10
+#define MIVGPU_PEER_BUSY_MS_DEFAULT 0
 #endif
 
 struct Config {
@@ -446,8 +446,8 @@ struct Config {
   uint64_t context_refresh_ns = 20000000;  // at most one KFD read per 20 ms (forced before an OOM)
   bool occupancy = true;                   // charge the governor the sampled wave-occupancy share
   uint64_t occ_period_ns = 2000000;        // sampling period while the governor runs (2 ms)
-  // a peer contends for this long after a sample with waves beyond a gate's
-  // (0: in such samples only); one showing exactly its gate's wave is held
+  // a fixed contention window (measurement builds; 0 = adaptive: per sample
+  // with few busy peers, kPeerBusyNs with many)
   uint64_t peer_busy_ns = (uint64_t)MIVGPU_PEER_BUSY_MS_DEFAULT * 1000000ull;
   uint64_t occ_idle_period_ns = 50000000;  // ... and for utilisation reporting only (50 ms)
   double share_tau_ns = 250e6;             // EWMA time constant of the occupancy averages (>> holds, batches)
@@ -1684,6 +1684,8 @@ struct OccPeer {
 constexpr double kContendFrac = 0.1;
 // A peer is busy for this long after its last sample with waves resident.
 constexpr uint64_t kPeerBusyNs = 200000000ull;   // 200 ms
+// Up to this many recently busy peers, contention is decided per sample.
+constexpr int kFewPeers = 3;
 // Idle time after which the host bucket stops accruing entitlement.
 constexpr uint64_t kAccrueIdleNs = 20000000ull;   // 20 ms
 // A governed peer held behind its gate has exactly its gate kernel's wave
@@ -1707,6 +1709,7 @@ struct OccDev {
   bool bucket = false;         // host bucket started (the device's gate is up)
   double tokens_ns = 0;        // host bucket balance: rate x wall time - GPU time received
   uint64_t owed_ns = 0;        // last sample in which the process owed GPU work
+  uint64_t window_ns = 0;      // this sample's contention window (0: per sample)
   uint64_t batch_win_ns = 0;   // batch-size estimate window (host mode)
   uint64_t batch_win_launches = 0;
   double batch_win_share = 0;
@@ -1810,17 +1813,28 @@ bool occ_sample(int dev, uint64_t now) {
   // settled at 50 % instead of 75 %).  MIVGPU_PEER_BUSY_MS > 0 restores a
   // window of that many ms after the last sample with waves (the round-3
   // rule, 200).
+  // With many tenants on the GPU the hardware scheduler time-slices their
+  // queues, and a busy peer often shows no waves in a given sample: there a
+  // peer keeps contending for kPeerBusyNs after its last waves (held ones
+  // excluded when their gate's wave is what shows).  With few (measured: 8 x
+  // 12 % temporal tenants at 6.0k tok/s per sample, 7.2k with a 50 ms window,
+  // 8.8k with 200 ms; 75 / 25 % tenants charged 76 / 25 per sample, 50 / 25
+  // with 200 ms) every sample decides.
+  int recent_peers = 0;
+  for (auto& p : o.peers)
+    if (p.busy_ns && now - p.busy_ns < kPeerBusyNs) ++recent_peers;
+  const uint64_t window = g_cfg.peer_busy_ns ? g_cfg.peer_busy_ns : (recent_peers > kFewPeers ? kPeerBusyNs : 0);
   long others = 0;
   int busy_peers = 0;
   for (auto& p : o.peers) {
     int v = read_occ(p.fd);
     p.v = v > 0 ? v : 0;
-    p.held = g_cfg.peer_busy_ns ? v == kGateWaves : v <= kGateWaves;   // per sample: idle counts as held
+    p.held = window ? v == kGateWaves : v <= kGateWaves;   // per sample: no waves beyond a gate's = not contending
     if (v > 0) others += v;
     if (v > kGateWaves) p.busy_ns = now;
-    if (p.busy_ns && now - p.busy_ns < (g_cfg.peer_busy_ns ? g_cfg.peer_busy_ns : kPeerBusyNs) && !p.held)
-      ++busy_peers;
+    if (p.busy_ns && now - p.busy_ns < (window ? window : kPeerBusyNs) && !p.held) ++busy_peers;
   }
+  o.window_ns = window;
   // The gate's own resident wave is not consumption: discount one unit per
   // gate slot holding right now.
   DeviceGate& G = g_gates[dev];
@@ -1902,8 +1916,7 @@ bool occ_sample(int dev, uint64_t now) {
       int comparable = 0;
       double heavier = 0;
       for (const auto& p : o.peers) {
-        if (!p.busy_ns || now - p.busy_ns >= (g_cfg.peer_busy_ns ? g_cfg.peer_busy_ns : kPeerBusyNs) || p.held)
-          continue;
+        if (!p.busy_ns || now - p.busy_ns >= (o.window_ns ? o.window_ns : kPeerBusyNs) || p.held) continue;
         if (p.avg * kContendFrac > o.own_avg) heavier += p.avg;
         else if (p.avg >= kContendFrac * o.own_avg) ++comparable;
       }

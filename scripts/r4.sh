@@ -70,6 +70,10 @@ for s in "$@"; do
          done ;;
     serve) run 1100 serving python -u -m k8s_vgpu_scheduler_amd.bench.serving --configs native,vgpu50 \
              --warmup 30 --runs 200 --long-prompt-tokens 8000 --out-dir "gpurun_out/$out/serving" ;;
+    s8) run 400 s8_auto python -u bench.py --slices 8 --out "gpurun_out/$out/s8_auto.json"
+        run 400 s8_disjoint python -u bench.py --slices 8 --layout disjoint --rounds shim \
+          --out "gpurun_out/$out/s8_disjoint.json" ;;
+    unequal) run 500 unequal_tests python -u -m pytest tests/test_shim_gpu.py -v -s $T -k "unequal or charged_the_share" ;;
     bench) run 400 bench python -u bench.py --out "gpurun_out/$out/bench.json" ;;
     curve) for n in 1 2 8; do
              run 400 "bench_s$n" python -u bench.py --slices $n --out "gpurun_out/$out/s$n.json"
