@@ -1815,8 +1815,8 @@ bool occ_sample(int dev, uint64_t now) {
   // rule, 200).
   // With many tenants on the GPU the hardware scheduler time-slices their
   // queues, and a busy peer often shows no waves in a given sample: there a
-  // peer keeps contending for kPeerBusyNs after its last waves (held ones
-  // excluded when their gate's wave is what shows).  With few (measured: 8 x
+  // peer keeps contending for kPeerBusyNs after its last waves (the round-3
+  // rule).  With few (measured: 8 x
   // 12 % temporal tenants at 6.0k tok/s per sample, 7.2k with a 50 ms window,
   // 8.8k with 200 ms; 75 / 25 % tenants charged 76 / 25 per sample, 50 / 25
   // with 200 ms) every sample decides.
@@ -1829,7 +1829,10 @@ bool occ_sample(int dev, uint64_t now) {
   for (auto& p : o.peers) {
     int v = read_occ(p.fd);
     p.v = v > 0 ? v : 0;
-    p.held = window ? v == kGateWaves : v <= kGateWaves;   // per sample: no waves beyond a gate's = not contending
+    // per sample: no waves beyond a gate's = not contending; in the crowded
+    // regime one resident wave is as often a running peer's last wave as a
+    // held peer's gate (excluding it held 8 x 12 % tenants back to 7.1k)
+    p.held = window ? false : v <= kGateWaves;
     if (v > 0) others += v;
     if (v > kGateWaves) p.busy_ns = now;
     if (p.busy_ns && now - p.busy_ns < (window ? window : kPeerBusyNs) && !p.held) ++busy_peers;
