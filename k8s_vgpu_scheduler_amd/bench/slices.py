@@ -63,11 +63,13 @@ def plan_slices(n: int, shim: bool, gpumem_mib: int | None, spatial: bool = True
     (device/amd/cu_alloc.py): ``disjoint`` = a range of its own per slice;
     ``hybrid`` = slices below a quarter of the GPU share quarter-sized
     ranges (as many as fit), split among them by the governor; ``auto`` =
-    hybrid, the allocator's default (``cuShareSmall``)."""
+    the allocator's default (``cuShareSmall``, off: disjoint)."""
     specs = []
     per = (MI355X_CUS // n) // MI355X_XCDS * MI355X_XCDS   # whole 8-CU granules: XCD-balanced
     unit = MI355X_CUS // 4
-    share = unit // per if (layout in ("auto", "hybrid") and 0 < per < unit) else 1
+    from k8s_vgpu_scheduler_amd.device.amd.device import AMDConfig
+    hybrid = layout == "hybrid" or (layout == "auto" and AMDConfig().cu_share_small)
+    share = unit // per if (hybrid and 0 < per < unit) else 1
     for i in range(n):
         if share > 1:
             q = i // share

@@ -82,10 +82,12 @@ class AMDConfig:
     # MI355X CU topology used by the CU-range allocator (measured, cu_alloc.py)
     xcds_per_device: int = 8
     cu_layout: str = "interleaved"
-    # requests below a quarter of the GPU share a quarter-sized CU range,
-    # time-sliced by the governor (cu_alloc.pick_shared); False = disjoint
-    # ranges of their own
-    cu_share_small: bool = True
+    # True: requests below a quarter of the GPU share a quarter-sized CU
+    # range, time-sliced by the governor (cu_alloc.pick_shared).  Off by
+    # default, from measurement: 8 slices on one MI355X, disjoint 32-CU masks
+    # 8511 tok/s (fairness 0.99) vs shared quarters 8457-8461 and the
+    # temporal governor 8501 (profiles/README.md section 37)
+    cu_share_small: bool = False
     # Node-side (device plugin) knobs, shared through the same config
     device_split_count: int = 8
     device_memory_scaling: float = 1.0

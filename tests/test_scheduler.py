@@ -301,7 +301,16 @@ def _ranges_of(cluster, name):
     return d.usedcores, codec.decode_cu_ranges(annos[CU_RANGES_ANNOS])[0]["n1-gpu0"]
 
 
-def test_small_slices_share_a_quarter_range(cluster):
+@pytest.fixture
+def share_small():
+    """The hybrid layout (cuShareSmall, off by default) for one test."""
+    from k8s_vgpu_scheduler_amd.device import devices as D
+    D.get_devices()["AMD"].cfg.cu_share_small = True
+    yield
+    D.get_devices()["AMD"].cfg.cu_share_small = False
+
+
+def test_small_slices_share_a_quarter_range(cluster, share_small):
     """VERDICT r3 item 2 (hybrid layout): requests below a quarter of the GPU
     share a 64-CU range pairwise (the governor splits it); the ranges of the
     pairs are disjoint and XCD-balanced, and the GPU still holds 8 x 12 %."""
@@ -323,7 +332,7 @@ def test_small_slices_share_a_quarter_range(cluster):
     assert not res.get("NodeNames")
 
 
-def test_shared_ranges_rebuilt_from_annotations(cluster):
+def test_shared_ranges_rebuilt_from_annotations(cluster, share_small):
     """The shared loads survive a scheduler restart (rebuilt from the pods'
     annotations): a third small pod joins the half-full range, not a new one."""
     s = make_sched(cluster, [amd_node("n1", n=1)])
@@ -339,7 +348,7 @@ def test_shared_ranges_rebuilt_from_annotations(cluster):
         cu_alloc.bitmap_from_ranges(_ranges_of(cluster, "a")[1]) == 0
 
 
-def test_small_slice_env_time_slices_its_shared_range(cluster):
+def test_small_slice_env_time_slices_its_shared_range(cluster, share_small):
     """The container of a shared-range slice gets the 64-CU mask and a core
     limit of its own share (12 %): wider than the limit, so the shim's governor
     splits the range (gate_wanted)."""
@@ -359,12 +368,8 @@ def test_small_slice_env_time_slices_its_shared_range(cluster):
 
 
 def test_share_small_off_keeps_disjoint_ranges(cluster):
+    """The default: a sub-quarter request gets a disjoint range of its own."""
     s = make_sched(cluster, [amd_node("n1", n=1)])
-    from k8s_vgpu_scheduler_amd.device import devices as D
-    D.get_devices()["AMD"].cfg.cu_share_small = False
-    try:
-        assert filt(s, cluster, amd_pod("p", mem=1024, cores=12), ["n1"])["NodeNames"] == ["n1"]
-        cus, ranges = _ranges_of(cluster, "p")
-        assert cus == 32 and codec.ranges_count(ranges) == 32
-    finally:
-        D.get_devices()["AMD"].cfg.cu_share_small = True
+    assert filt(s, cluster, amd_pod("p", mem=1024, cores=12), ["n1"])["NodeNames"] == ["n1"]
+    cus, ranges = _ranges_of(cluster, "p")
+    assert cus == 32 and codec.ranges_count(ranges) == 32
