@@ -41,12 +41,16 @@ def summarise(root: str) -> dict:
             row[c] = round(v / n, 1)
         if "FETCH_SIZE" in row and dur > 0:
             row["fetch_TBps"] = round(row["FETCH_SIZE"] * 1024 / dur / 1e3, 2)
-        # EA read requests summed over every TCC instance: 32-byte ones and
-        # the rest at 64 bytes (the memory-side read bytes, all channels)
-        rq, rq32 = row.get("TCC_EA0_RDREQ_sum"), row.get("TCC_EA0_RDREQ_32B_sum")
+        # EA read requests summed over every TCC instance, by size: 128-byte
+        # (TCC_BUBBLE), 32-byte, the rest 64-byte -- rocprofv3's FETCH_SIZE
+        # expression on gfx950, from the raw counters (memory-side read bytes,
+        # all channels)
+        rq, rq32, rq128 = (row.get("TCC_EA0_RDREQ_sum"), row.get("TCC_EA0_RDREQ_32B_sum"),
+                           row.get("TCC_BUBBLE_sum", 0.0))
         if rq is not None and rq32 is not None and dur > 0:
-            row["ea_read_MB"] = round((64 * (rq - rq32) + 32 * rq32) / 1e6, 2)
-            row["ea_read_TBps"] = round((64 * (rq - rq32) + 32 * rq32) / dur / 1e3, 2)
+            b = 128 * rq128 + 64 * (rq - rq128 - rq32) + 32 * rq32
+            row["ea_read_MB"] = round(b / 1e6, 2)
+            row["ea_read_TBps"] = round(b / dur / 1e3, 2)
         out[name] = row
     return dict(sorted(out.items(), key=lambda kv: -kv[1]["mean_us"] * kv[1]["dispatches"]))
 

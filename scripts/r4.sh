@@ -43,7 +43,7 @@ for s in "$@"; do
          timeout -s KILL 60 rocprofv3 -L > "$R/gpurun_out/$out/counters.txt" 2>&1
          for cfg in full cu64; do
            if [ $cfg = cu64 ]; then export HSA_CU_MASK=0:0-63; else unset HSA_CU_MASK; fi
-           run 150 "hbm_$cfg" rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --kernel-trace \
+           run 150 "hbm_$cfg" rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_BUBBLE_sum --kernel-trace \
              --output-format csv -d "$R/gpurun_out/$out/hbm_$cfg" -o run -- \
              python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 3 --warmup 1 --no-graph
            python3 "$R/scripts/probe/pmc_summary.py" "$R/gpurun_out/$out/hbm_$cfg" > "$R/gpurun_out/$out/hbm_$cfg.json" \
