@@ -74,6 +74,12 @@ for s in "$@"; do
         run 400 s8_disjoint python -u bench.py --slices 8 --layout disjoint --rounds shim \
           --out "gpurun_out/$out/s8_disjoint.json" ;;
     unequal) run 500 unequal_tests python -u -m pytest tests/test_shim_gpu.py -v -s $T -k "unequal or charged_the_share" ;;
+    lds) export TMPDIR=/tmp PYTHONPATH=$R
+         run 150 lds_full rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_BF16 \
+           --kernel-trace --output-format csv -d "$R/gpurun_out/$out/lds_full" -o run -- \
+           python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 3 --warmup 1 --no-graph
+         python3 "$R/scripts/probe/pmc_summary.py" "$R/gpurun_out/$out/lds_full" > "$R/gpurun_out/$out/lds_full.json" \
+           && rm -rf "$R/gpurun_out/$out/lds_full" ;;
     bench) run 400 bench python -u bench.py --out "gpurun_out/$out/bench.json" ;;
     curve) for n in 1 2 8; do
              run 400 "bench_s$n" python -u bench.py --slices $n --out "gpurun_out/$out/s$n.json"
