@@ -784,7 +784,9 @@ decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restric
   __shared__ float s_o[WAVES][G][DP];
   __shared__ float s_m[WAVES][G];
   __shared__ float s_l[WAVES][G];
-  __shared__ __attribute__((aligned(16))) bf16_t s_q[G][D];
+  // +8 per row: the Q operand reads 16 B of rows 0..G-1 in the same columns
+  // (ds_read_b128, bank = dword mod 64): 256-byte rows put them all on bank 0
+  __shared__ __attribute__((aligned(16))) bf16_t s_q[G][D + 8];
   __shared__ __attribute__((aligned(16))) bf16_t s_kv[2][D];   // new key (normed, rotated), new value
   __shared__ int s_last;
 
