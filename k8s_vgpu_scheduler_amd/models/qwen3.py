@@ -274,6 +274,22 @@ class Qwen3Decoder:
                 and os.environ.get("MIVGPU_ATTN_XCOMB", "1") != "0"
                 and self.w.layers[0]["po"].xcomb_ok(batch)):
             self.xcomb = (self.o_part, self.ml_part, self.seqlens, self.nsplit, ops.attn_split(), self.T, cfg.heads)
+        # plan overrides of the two big projections, "waves,split" (A/B runs;
+        # unset = the planner's choice)
+        def plan_env(name):
+            v = os.environ.get(name, "")
+            if not v:
+                return {}
+            wv, sp = (int(x) for x in v.split(","))
+            return {"ks": wv, "S": sp}
+        self._gu_plan, self._d_plan = plan_env("MIVGPU_GU_PLAN"), plan_env("MIVGPU_DOWN_PLAN")
+        if self.native and (self._gu_plan or self._d_plan):
+            for lw in self.w.layers:
+                for key, pl in (("pgu", self._gu_plan), ("pd", self._d_plan)):
+                    if pl and key in lw:
+                        plan = ops.skinny_plan(batch, lw[key].K, lw[key].N, lw[key].epi, ks=pl["ks"], S=pl["S"],
+                                               variant=ops.VARIANT_WIDE)
+                        lw[key]._ensure_scratch(plan["scratch_floats"], plan["tickets"], self.device)
         self._chains = self._build_chains() if self.chain else None
         self.graph = None
         self._tail_work = ops.decode_tail_workspace(batch, self.device) if self.native else None
@@ -341,8 +357,8 @@ class Qwen3Decoder:
             else:
                 self._attention(li, lw, qkv)
                 lw["po"].norm_call(self.attn, out=self.res, residual=True, ss_out=self.ss_b)
-            lw["pgu"].norm_call(self.res, out=self.act, row_scale=(self.ss_b, self.slots_o, h, eps))
-            lw["pd"].norm_call(self.act, out=self.res, residual=True, ss_out=self.ss_a)
+            lw["pgu"].norm_call(self.res, out=self.act, row_scale=(self.ss_b, self.slots_o, h, eps), **self._gu_plan)
+            lw["pd"].norm_call(self.act, out=self.res, residual=True, ss_out=self.ss_a, **self._d_plan)
             na = self.slots_d
         ops.rmsnorm(self.res, w.final_norm, eps, out=self.h)
         logits = self.p_lm(self.h, out=self.logits)

@@ -80,6 +80,12 @@ for s in "$@"; do
            python3 -m k8s_vgpu_scheduler_amd.bench.decode --steps 3 --warmup 1 --no-graph
          python3 "$R/scripts/probe/pmc_summary.py" "$R/gpurun_out/$out/lds_full" > "$R/gpurun_out/$out/lds_full.json" \
            && rm -rf "$R/gpurun_out/$out/lds_full" ;;
+    plans) for p in "" "2,2" "2,4" "4,4"; do
+             MIVGPU_GU_PLAN=$p run 200 "gu_${p/,/_}" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 32
+           done
+           for p in "2,8" "2,6" "4,4" "4,8" "1,4"; do
+             MIVGPU_DOWN_PLAN=$p run 200 "down_${p/,/_}" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 32
+           done ;;
     bench) run 400 bench python -u bench.py --out "gpurun_out/$out/bench.json" ;;
     curve) for n in 1 2 8; do
              run 400 "bench_s$n" python -u bench.py --slices $n --out "gpurun_out/$out/s$n.json"
