@@ -53,11 +53,9 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 }
 
 // V^T for the P.V MFMAs: TR = the row-major V tile through the hardware
-// transposed read (ds_read_b64_tr_b16; MIVGPU_FA_TR=1, OPAQUE: =2); !TR = V
-// staged transposed in LDS ([128 dims][32 keys + 8 pad], one 2-byte write per
-// element) and read with plain 8-byte reads (the default: the transposed-read
-// build returned wrong sums on MI355X although a probe of the instruction's
-// semantics passes -- profiles/README.md section 37).
+// transposed read (ds_read_b64_tr_b16; the default, OPAQUE: MIVGPU_FA_TR=2);
+// !TR = V staged transposed in LDS ([128 dims][32 keys + 8 pad], one 2-byte
+// write per element) and read with plain 8-byte reads (MIVGPU_FA_TR=0).
 constexpr int FA_VT_PITCH = FA_BK + 8;
 
 template <int G, bool TR, bool OPAQUE = false>
@@ -208,13 +206,12 @@ prefill_flash_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
             (__attribute__((address_space(3))) i16x4_t*)(&vt_lds[olo]));
         const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (__attribute__((address_space(3))) i16x4_t*)(&vt_lds[ohi]));
-        bf16x8_t a;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          a[j] = __builtin_bit_cast(__bf16, lo[j]);
-          a[4 + j] = __builtin_bit_cast(__bf16, hi[j]);
-        }
-        o[dc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pf[u], o[dc], 0, 0, 0);
+        // the operand from whole 32-bit lanes: built element-wise (a[j] =
+        // bit_cast<__bf16>(lo[j])) hipcc kept only the first dword of each
+        // read, permuted and duplicated -- the "wrong sums" of this variant
+        const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
+        const uint4 a4 = make_uint4(l2.x, l2.y, h2.x, h2.y);
+        o[dc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a4), pf[u], o[dc], 0, 0, 0);
       }
     }
 
@@ -256,11 +253,11 @@ __global__ void __launch_bounds__(64) tr_read_probe_kernel(const int* __restrict
 }
 
 // V^T path, read per launch (prompt-sized launches; tests switch it in one
-// process): 0 = V staged transposed, plain reads (default); 1 = transposed
+// process): 1 = transposed reads (default); 0 = V staged transposed, plain
 // reads; 2 = transposed reads from opaque addresses (no folded offsets).
 int fa_tr() {
   const char* e = getenv("MIVGPU_FA_TR");
-  return e && *e ? atoi(e) : 0;
+  return e && *e ? atoi(e) : 1;
 }
 
 }  // namespace

@@ -21,7 +21,9 @@ for s in "$@"; do
     shim2) run 700 shim2_tests python -u -m pytest tests/test_shim_gpu.py tests/test_shim_interpose_gpu.py -v -s $T \
              -k "unequal or tenant_without or tenant_rewriting" ;;
     attnbench) run 300 prefill_attn python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention \
-                 --out "gpurun_out/$out/prefill_attn.json" ;;
+                 --out "gpurun_out/$out/prefill_attn.json"
+               MIVGPU_FA_TR=0 run 300 prefill_attn_tr0 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention \
+                 --out "gpurun_out/$out/prefill_attn_tr0.json" ;;
     shim) run 700 shim_tests python -u -m pytest tests/test_shim_gpu.py tests/test_shim_interpose_gpu.py -v -s $T ;;
     other) run 700 other_tests python -u -m pytest tests -m gpu -v $T --deselect tests/test_shim_gpu.py \
              --deselect tests/test_shim_interpose_gpu.py ;;
