@@ -75,6 +75,16 @@ for s in "$@"; do
     s8) run 400 s8_auto python -u bench.py --slices 8 --out "gpurun_out/$out/s8_auto.json"
         run 400 s8_disjoint python -u bench.py --slices 8 --layout disjoint --rounds shim \
           --out "gpurun_out/$out/s8_disjoint.json" ;;
+    e2e) run 500 e2e_tests python -u -m pytest tests/test_e2e_gpu.py -v $T ;;
+    s8plan) run 400 s8p_base python -u bench.py --slices 8 --layout disjoint --rounds shim \
+              --out "gpurun_out/$out/s8p_base.json"
+            run 400 s8p_chip python -u bench.py --slices 8 --layout disjoint --rounds shim \
+              --child-env MIVGPU_SLICE_PLAN_CUS=0 --out "gpurun_out/$out/s8p_chip.json"
+            run 400 s8p_chip_nomid python -u bench.py --slices 8 --layout disjoint --rounds shim \
+              --child-env MIVGPU_SLICE_PLAN_CUS=0 --child-env MIVGPU_WIDE_MID_PLAN=0 \
+              --out "gpurun_out/$out/s8p_chip_nomid.json"
+            run 400 s8p_q1 python -u bench.py --slices 8 --layout disjoint --rounds shim --hw-queues 1 \
+              --out "gpurun_out/$out/s8p_q1.json" ;;
     unequal) run 500 unequal_tests python -u -m pytest tests/test_shim_gpu.py -v -s $T -k "unequal or charged_the_share" ;;
     lds) export TMPDIR=/tmp PYTHONPATH=$R
          run 150 lds_full rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_BF16 \
