@@ -1088,20 +1088,32 @@ decode_attn_combine_kernel(const float* __restrict__ o_part, const float* __rest
   // round trip per split.
   const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
   const size_t base = (size_t)b * Hq + h;
+  constexpr int MS = 8;
+  // the first batch of partials is loaded together with seqlens[b] (the
+  // workspace holds nsplit entries, so every index < nsplit is in bounds; the
+  // count read from seqlens masks the stale ones): one round trip, not two
+  float mv[MS], lv[MS], ov[MS];
+#pragma unroll
+  for (int i = 0; i < MS; ++i) {
+    const int sp = i < nsplit ? i : 0;
+    mv[i] = ml_part[(base * nsplit + sp) * 2];
+    lv[i] = ml_part[(base * nsplit + sp) * 2 + 1];
+    ov[i] = o_part[(base * nsplit + sp) * ATT_D + d];
+  }
   if (seqlens) {
     const int L = min(seqlens[b], max_ctx);
     count = min(count, L > 0 ? (L + split_keys - 1) / split_keys : 0);
   }
-  constexpr int MS = 8;
   float M = -INFINITY, num = 0.f, den = 0.f;
   for (int s0 = 0; s0 < count; s0 += MS) {
-    float mv[MS], lv[MS], ov[MS];
+    if (s0 > 0) {
 #pragma unroll
-    for (int i = 0; i < MS; ++i) {
-      const int sp = s0 + i < count ? s0 + i : s0;
-      mv[i] = ml_part[(base * nsplit + sp) * 2];
-      lv[i] = ml_part[(base * nsplit + sp) * 2 + 1];
-      ov[i] = o_part[(base * nsplit + sp) * ATT_D + d];
+      for (int i = 0; i < MS; ++i) {
+        const int sp = s0 + i < count ? s0 + i : s0;
+        mv[i] = ml_part[(base * nsplit + sp) * 2];
+        lv[i] = ml_part[(base * nsplit + sp) * 2 + 1];
+        ov[i] = o_part[(base * nsplit + sp) * ATT_D + d];
+      }
     }
 #pragma unroll
     for (int i = 0; i < MS; ++i) {

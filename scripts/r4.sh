@@ -75,16 +75,21 @@ for s in "$@"; do
     s8) run 400 s8_auto python -u bench.py --slices 8 --out "gpurun_out/$out/s8_auto.json"
         run 400 s8_disjoint python -u bench.py --slices 8 --layout disjoint --rounds shim \
           --out "gpurun_out/$out/s8_disjoint.json" ;;
+    combine) run 300 attn_tests python -u -m pytest tests/test_ops_gpu.py -v -k "attn or attention or decoder" $T
+             for m in 1 2; do
+               MIVGPU_ATTN_FUSED=$m run 200 "comb_m$m" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 32
+             done ;;
     e2e) run 500 e2e_tests python -u -m pytest tests/test_e2e_gpu.py -v $T ;;
     s8plan) run 400 s8p_base python -u bench.py --slices 8 --layout disjoint --rounds shim \
               --out "gpurun_out/$out/s8p_base.json"
             run 400 s8p_chip python -u bench.py --slices 8 --layout disjoint --rounds shim \
               --child-env MIVGPU_SLICE_PLAN_CUS=0 --out "gpurun_out/$out/s8p_chip.json"
-            run 400 s8p_chip_nomid python -u bench.py --slices 8 --layout disjoint --rounds shim \
-              --child-env MIVGPU_SLICE_PLAN_CUS=0 --child-env MIVGPU_WIDE_MID_PLAN=0 \
-              --out "gpurun_out/$out/s8p_chip_nomid.json"
             run 400 s8p_q1 python -u bench.py --slices 8 --layout disjoint --rounds shim --hw-queues 1 \
               --out "gpurun_out/$out/s8p_q1.json" ;;
+    s8temporal) run 400 s8t_12 python -u bench.py --slices 8 --rounds temporal,native \
+              --out "gpurun_out/$out/s8t_12.json"
+            run 400 s8t_13 python -u bench.py --slices 8 --rounds temporal --slice-limits 13,13,13,13,13,13,13,13 \
+              --out "gpurun_out/$out/s8t_13.json" ;;
     unequal) run 500 unequal_tests python -u -m pytest tests/test_shim_gpu.py -v -s $T -k "unequal or charged_the_share" ;;
     lds) export TMPDIR=/tmp PYTHONPATH=$R
          run 150 lds_full rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_BF16 \
