@@ -105,7 +105,7 @@ def main():
                          "the slice processes (results are not MI355X numbers)")
     args = ap.parse_args()
 
-    from k8s_vgpu_scheduler_amd.bench.slices import plan_slices, run_round, spawn_round
+    from k8s_vgpu_scheduler_amd.bench.slices import pct_text, plan_slices, run_round, spawn_round
     from k8s_vgpu_scheduler_amd.utils import build
 
     rank = int(os.environ.get("RANK", "0"))
@@ -123,7 +123,7 @@ def main():
 
     extra_env = dict(kv.split("=", 1) for kv in args.child_env)
 
-    limits = [int(x) for x in args.slice_limits.split(",") if x.strip()]
+    limits = [float(x) for x in args.slice_limits.split(",") if x.strip()]
     if limits and len(limits) != args.slices:
         ap.error(f"--slice-limits has {len(limits)} entries for {args.slices} slices")
 
@@ -261,6 +261,7 @@ def main():
             from k8s_vgpu_scheduler_amd.bench.slices import RoundMonitor
             mon = RoundMonitor([p.cache for p in procs], args.monitor).start()
         r = run_round(procs, barrier=barrier, sync=sync)
+        r["specs"] = [p.spec for p in procs]
         if mon is not None:
             r["monitor"] = mon.stop()
         wall = torch.tensor([r["wall_s"]], dtype=torch.float64)        # CPU: no queues in this process
@@ -311,6 +312,8 @@ def main():
                 "batch_per_slice": args.batch,
                 "gpumem_mib_per_slice": args.gpumem_mib,
                 "gpucores_per_slice": limits or (100 // args.slices if args.slices > 1 else 100),
+                # the grant's HIP_DEVICE_CORE_LIMIT: the CUs charged, as an exact share
+                "core_limit_pct_per_slice": [pct_text(sp.core_pct) for sp in head.get("specs", [])],
                 "isolation": (f"HSA_CU_MASK ({args.layout} layout) + libmivgpu" if not args.no_spatial
                               else f"governor ({args.policy})")
                 + (f" + {args.hw_queues} HW queue/slice" if args.hw_queues and args.slices > 1 else ""),
@@ -343,7 +346,8 @@ def main():
             out["temporal_value"] = round(tr["tok_s"], 2)
             out["temporal_per_slice_tok_s_rank0"] = tps
             out["temporal_fairness_min_over_max"] = round(min(tps) / max(tps), 3) if tps else None
-            out["temporal_isolation"] = f"governor gate (force, {100 // args.slices} % each, occupancy-charged)"
+            lims = sorted({pct_text(sp.core_pct) for sp in tr.get("specs", [])}) or ["?"]
+            out["temporal_isolation"] = f"governor gate (force, {'/'.join(lims)} % each, occupancy-charged)"
             out["temporal_governor_rank0"] = [{k: d.get(k) for k in ("gov_charged_ms", "gov_held_ms", "gov_gates",
                                                                      "share_pct", "util_pct")} for d in tr["done"]]
             if "native" in results:

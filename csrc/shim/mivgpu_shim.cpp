@@ -436,7 +436,11 @@ REAL_DECL(hipError_t, hipMemset, "hip_4.2", (void*, int, size_t))
 
 struct Config {
   uint64_t mem_limit[MIVGPU_MAX_DEVICES] = {0};
-  int cu_limit[MIVGPU_MAX_DEVICES];  // percent per device (HIP_DEVICE_CORE_LIMIT[_i])
+  int cu_limit[MIVGPU_MAX_DEVICES];  // percent per device (HIP_DEVICE_CORE_LIMIT[_i]), rounded half up
+  // the same limit in parts per million of the device: the grant states the
+  // CUs the scheduler charged as an exact share ("12.5" for 32 of 256 CUs),
+  // which whole percents would cut (8 x 12 % left 4 % of the GPU idle)
+  uint32_t cu_limit_ppm[MIVGPU_MAX_DEVICES];
   int cu_mask_count[MIVGPU_MAX_DEVICES] = {0};
   int policy = 0;              // 0 default, 1 force, 2 disable
   int priority = 1;
@@ -485,6 +489,34 @@ uint64_t parse_size(const char* s) {
     }
   }
   return (uint64_t)(v * (double)mult);
+}
+
+// A core limit in percent with up to four decimals ("25", "12.5", "3.125")
+// -> parts per million of the device; 0 = absent or outside (0, 100].
+// Integer arithmetic only, so the monitor (shim/__init__.py core_limit_ppm)
+// derives the same value from the same grant text.
+uint32_t parse_pct_ppm(const char* s) {
+  if (!s) return 0;
+  uint64_t ip = 0, fp = 0;
+  int idig = 0, fdig = 0;
+  const char* p = s;
+  for (; *p >= '0' && *p <= '9'; ++p, ++idig)
+    if (idig < 4) ip = ip * 10 + (uint64_t)(*p - '0');
+  if (idig > 3) return 0;
+  if (*p == '.') {
+    for (++p; *p >= '0' && *p <= '9'; ++p, ++fdig)
+      if (fdig < 4) fp = fp * 10 + (uint64_t)(*p - '0');
+  }
+  if (*p || (idig == 0 && fdig == 0)) return 0;
+  for (int k = fdig < 4 ? fdig : 4; k < 4; ++k) fp *= 10;
+  const uint64_t ppm = ip * 10000 + fp;
+  return (ppm > 0 && ppm <= 1000000) ? (uint32_t)ppm : 0;
+}
+
+// ppm -> whole percent for the region field, rounded half up, at least 1.
+int pct_of_ppm(uint32_t ppm) {
+  const int pct = (int)((ppm + 5000) / 10000);
+  return ppm == 0 ? 0 : (pct < 1 ? 1 : pct);
 }
 
 // Count CUs granted to device `idx` in an HSA_CU_MASK value such as
@@ -617,18 +649,15 @@ void load_config() {
   // HIP_DEVICE_CORE_LIMIT applies to every device; HIP_DEVICE_CORE_LIMIT_<i>
   // (container-local index) overrides it for one device, so a container that
   // holds a compute partition next to a whole GPU is governed per device.
-  int core_all = 100;
-  const char* core = grant_env("HIP_DEVICE_CORE_LIMIT");
-  if (core) {
-    int c = atoi(core);
-    if (c >= 1 && c <= 100) core_all = c;
-  }
+  uint32_t core_all = 1000000;
+  const uint32_t core = parse_pct_ppm(grant_env("HIP_DEVICE_CORE_LIMIT"));
+  if (core) core_all = core;
   for (int i = 0; i < MIVGPU_MAX_DEVICES; ++i) {
     char key[64];
     snprintf(key, sizeof(key), "HIP_DEVICE_CORE_LIMIT_%d", i);
-    const char* v = grant_env(key);
-    const int c = v ? atoi(v) : 0;
-    g_cfg.cu_limit[i] = (c >= 1 && c <= 100) ? c : core_all;
+    const uint32_t c = parse_pct_ppm(grant_env(key));
+    g_cfg.cu_limit_ppm[i] = c ? c : core_all;
+    g_cfg.cu_limit[i] = pct_of_ppm(g_cfg.cu_limit_ppm[i]);
   }
   const char* mask = grant_env("HSA_CU_MASK");
   for (int i = 0; i < MIVGPU_MAX_DEVICES; ++i) g_cfg.cu_mask_count[i] = parse_cu_mask_count(mask, i);
@@ -940,13 +969,14 @@ void bootstrap() {
   if (g_limits.loaded) {
     g_any_limit_static = 0;
     for (int d = 0; d < (g_num_devices > 0 ? g_num_devices : 1); ++d)
-      if (g_cfg.cu_limit[d] > 0 && g_cfg.cu_limit[d] < 100) g_any_limit_static = 1;
+      if (g_cfg.cu_limit_ppm[d] > 0 && g_cfg.cu_limit_ppm[d] < 1000000) g_any_limit_static = 1;
   }
   atexit(on_exit_release);
   for (int d = 0; d < g_num_devices; ++d) {
-    if (g_cfg.mem_limit[d] || g_cfg.cu_limit[d] < 100 || g_cfg.cu_mask_count[d])
-      tmark("mivgpu:config dev=%d limit_mib=%llu cu_limit=%d cu_mask=%d", d,
-            (unsigned long long)(g_cfg.mem_limit[d] >> 20), g_cfg.cu_limit[d], g_cfg.cu_mask_count[d]);
+    if (g_cfg.mem_limit[d] || g_cfg.cu_limit_ppm[d] < 1000000 || g_cfg.cu_mask_count[d])
+      tmark("mivgpu:config dev=%d limit_mib=%llu cu_limit=%d cu_mask=%d cu_limit_ppm=%u", d,
+            (unsigned long long)(g_cfg.mem_limit[d] >> 20), g_cfg.cu_limit[d], g_cfg.cu_mask_count[d],
+            g_cfg.cu_limit_ppm[d]);
     if (g_cfg.mem_limit[d])
       mlog(3, "device %d: HBM limit %llu MiB, CU limit %d%%, CU mask %d CUs", d,
            (unsigned long long)(g_cfg.mem_limit[d] >> 20), g_cfg.cu_limit[d], g_cfg.cu_mask_count[d]);
@@ -976,9 +1006,14 @@ inline uint64_t limit_of(int dev) {
   if (g_limits.loaded || !g_region) return g_cfg.mem_limit[dev];
   return __atomic_load_n(&g_region->mem_limit[dev], __ATOMIC_RELAXED);
 }
-inline uint64_t cu_limit_of(int dev) {
-  if (g_limits.loaded || !g_region) return (uint64_t)g_cfg.cu_limit[dev];
-  return __atomic_load_n(&g_region->cu_limit[dev], __ATOMIC_RELAXED);
+// The core limit in parts per million of the device.  The region holds it in
+// whole percents (the monitor's field); while it still holds the percent this
+// process published, the exact share from the grant stands, a changed value
+// (the monitor's reconcile, a hand-run slice) is taken as it is.
+inline uint64_t cu_limit_ppm_of(int dev) {
+  if (g_limits.loaded || !g_region) return g_cfg.cu_limit_ppm[dev];
+  const uint64_t pct = __atomic_load_n(&g_region->cu_limit[dev], __ATOMIC_RELAXED);
+  return pct == (uint64_t)g_cfg.cu_limit[dev] ? g_cfg.cu_limit_ppm[dev] : pct * 10000ull;
 }
 inline uint64_t cu_mask_of(int dev) {
   if (g_limits.loaded || !g_region) return (uint64_t)g_cfg.cu_mask_count[dev];
@@ -1947,8 +1982,8 @@ bool occ_sample(int dev, uint64_t now) {
   // charged, the balance is bounded by one burst either way.  The gates read
   // it at execution time and hold while it is negative.
   if (hs) {
-    const uint64_t lim = cu_limit_of(dev);
-    const double rate = (lim > 0 && lim < 100) ? (double)lim / 100.0 : 1.0;
+    const uint64_t lim = cu_limit_ppm_of(dev);
+    const double rate = (lim > 0 && lim < 1000000) ? (double)lim / 1e6 : 1.0;
     const double cap = (double)g_cfg.gate_cap_ns;
     if (!o.bucket) {
       // empty, not full: a burst is earned by idling below the limit, not
@@ -2091,16 +2126,17 @@ inline bool gate_wanted(int dev) {
   if (g_cfg.disabled || !g_region) return false;
   int policy = core_policy();
   if (policy == 2) return false;
-  uint64_t lim = cu_limit_of(dev);
+  const uint64_t lim = cu_limit_ppm_of(dev);
   int sw = util_switch();
-  if (lim == 0 || lim >= 100) return false;
+  if (lim == 0 || lim >= 1000000) return false;
   // A CU mask no wider than the limit (within one granule of one CU per XCD:
   // the device plugin rounds grants to whole granules) already enforces it in
   // hardware; time-slicing on top would charge the tenant for a GPU it cannot
   // reach (VERDICT r1 "double throttle").  This holds under policy force too:
   // force asks for the limit to be enforced, and the mask enforces it.
   const uint64_t mask = cu_mask_of(dev);
-  if (mask > 0 && mask * 100 <= lim * (uint64_t)device_cus(dev) + 100ull * (uint64_t)device_xcds(dev)) return false;
+  if (mask > 0 && mask * 1000000ull <= lim * (uint64_t)device_cus(dev) + 1000000ull * (uint64_t)device_xcds(dev))
+    return false;
   if (policy == 1) return true;
   // default: time-slice when there is no mask or the monitor asks for
   // contention enforcement (utilization_switch, feedback.go:74-134)
@@ -2112,7 +2148,7 @@ void enqueue_gate_locked(int dev, DeviceGate& G, int slot, hipStream_t stream, u
   GateSlot& S = G.slots[slot];
   const uint64_t first = S.first_submit_host_ns.load(std::memory_order_relaxed);
   long long submit_dev = first ? (long long)first + G.offset_ns : -1;
-  const uint64_t rate = cu_limit_of(dev) * 10000ull;
+  const uint64_t rate = cu_limit_ppm_of(dev);
   unsigned int rate_ppm = (unsigned int)(rate < 1000000ull ? rate : 1000000ull);
   long long cap = g_cfg.gate_cap_ns, hold = g_cfg.gate_max_hold_ns;
   int slot_arg = slot;
@@ -2354,8 +2390,8 @@ inline bool any_core_limit() {
   if (g_any_limit_static >= 0) return g_any_limit_static != 0;
   const int n = g_num_devices > 0 ? g_num_devices : 1;
   for (int d = 0; d < n; ++d) {
-    const uint64_t cl = cu_limit_of(d);
-    if (cl > 0 && cl < 100) return true;
+    const uint64_t cl = cu_limit_ppm_of(d);
+    if (cl > 0 && cl < 1000000) return true;
   }
   return false;
 }
@@ -3224,6 +3260,8 @@ MIVGPU_EXPORT int mivgpu_parse_cu_mask_count(const char* mask, int idx) {
 }
 
 MIVGPU_EXPORT unsigned long long mivgpu_parse_size(const char* s) { return parse_size(s); }
+MIVGPU_EXPORT unsigned int mivgpu_parse_pct_ppm(const char* s) { return parse_pct_ppm(s); }
+MIVGPU_EXPORT int mivgpu_pct_of_ppm(unsigned int ppm) { return pct_of_ppm(ppm); }
 
 // Usage of this process on `dev` as seen by the shim (bytes); -1 if inactive.
 MIVGPU_EXPORT long long mivgpu_process_usage(int dev) {

@@ -29,6 +29,7 @@ import time
 from dataclasses import dataclass, field
 from pathlib import Path
 
+from k8s_vgpu_scheduler_amd.deviceplugin.allocate import core_limit_text
 from k8s_vgpu_scheduler_amd.shim import shim_env
 
 MI355X_CUS = 256
@@ -40,7 +41,7 @@ class SliceSpec:
     index: int
     gpumem_mib: int | None      # None = no limit
     cu_ranges: list | None      # [(lo, hi), ...] for HSA_CU_MASK, None = all CUs
-    core_pct: int = 100
+    core_pct: float = 100   # the grant's HIP_DEVICE_CORE_LIMIT (exact share of the CUs charged)
     shim: bool = True
     policy: str = "default"
     # HW queues per slice process (GPU_MAX_HW_QUEUES).  HIP's default of 4 per
@@ -49,6 +50,11 @@ class SliceSpec:
     # profiles/README.md §2); the device plugin injects the same value.
     hw_queues: int | None = None
     env: dict = field(default_factory=dict)
+
+
+def pct_text(pct: float) -> str:
+    """A core limit as the device plugin writes it (up to three decimals)."""
+    return f"{pct:.3f}".rstrip("0").rstrip(".")
 
 
 def cu_mask_string(ranges) -> str:
@@ -76,8 +82,10 @@ def plan_slices(n: int, shim: bool, gpumem_mib: int | None, spatial: bool = True
             ranges = [(q * unit, (q + 1) * unit - 1)] if (shim and spatial and n > 1) else None
         else:
             ranges = [(i * per, (i + 1) * per - 1)] if (shim and spatial and n > 1) else None
+        # gpucores 100 // n, charged as whole granules (device/amd/device.py):
+        # the grant states that charge exactly (deviceplugin/allocate.py)
         specs.append(SliceSpec(index=i, gpumem_mib=gpumem_mib if shim else None, cu_ranges=ranges,
-                               core_pct=max(1, 100 // n) if n > 1 else 100, shim=shim,
+                               core_pct=float(core_limit_text(per, MI355X_CUS)) if n > 1 else 100, shim=shim,
                                policy=policy, hw_queues=hw_queues if (shim and n > 1) else None))
     return specs
 
@@ -93,7 +101,7 @@ def slice_env(spec: SliceSpec, physical_gpu: str | None, cache_dir: Path) -> dic
         if spec.gpumem_mib:
             env["HIP_DEVICE_MEMORY_LIMIT_0"] = f"{spec.gpumem_mib}m"
         if spec.core_pct < 100:
-            env["HIP_DEVICE_CORE_LIMIT"] = str(spec.core_pct)
+            env["HIP_DEVICE_CORE_LIMIT"] = pct_text(spec.core_pct)
         env["GPU_CORE_UTILIZATION_POLICY"] = spec.policy
     # the partition and queue count are properties of the slice, with or
     # without the shim (the "masked, no shim" round isolates the shim's cost)

@@ -9,7 +9,8 @@ docs/develop/amd-vgpu.md:47-104.  MI355X translation:
        HSA_CU_MASK            ``i:ranges;...`` for devices with a CU partition
        HIP_DEVICE_MEMORY_LIMIT_i  ``<MiB>m`` hard limit per local device
        HIP_DEVICE_CORE_LIMIT  CU share in % (first device; the reference's single
-                              CUDA_DEVICE_SM_LIMIT, server.go:837)
+                              CUDA_DEVICE_SM_LIMIT, server.go:837), the exact
+                              share of the CUs charged ("12.5" for 32 of 256)
        HIP_DEVICE_CORE_LIMIT_i  CU share in % of local device i (a container
                               can hold a compute partition next to a whole GPU)
        GPU_MAX_HW_QUEUES      2 for shared (fractional) pods: HIP's default 4
@@ -129,10 +130,22 @@ def is_fractional(devreq: list, gpus: dict, cfg: PluginConfig) -> bool:
     return False
 
 
-def _core_pct(d, gpus: dict) -> int:
+def core_limit_text(cus: int, total: int) -> str:
+    """The grant's core limit for ``cus`` charged CUs of ``total``: the exact
+    share in percent, up to three decimals ("25", "12.5", "3.125").  Whole
+    percents cut a 32-CU charge (gpucores 12 rounded up to whole granules) to
+    12 % and left 8 such tenants 4 % of the GPU they were charged for
+    (profiles/README.md section 38); the shim parses up to four decimals."""
+    if cus <= 0:
+        return "0"
+    milli = min(100_000, max(1, (cus * 100_000 + total // 2) // total))   # thousandths of a percent
+    whole, frac = divmod(milli, 1000)
+    return str(whole) if not frac else f"{whole}.{frac:03d}".rstrip("0")
+
+
+def _core_pct(d, gpus: dict) -> str:
     g = gpus.get(d.uuid)
-    total = g.cus if g else 256
-    return 0 if d.usedcores == 0 else max(1, min(100, round(d.usedcores * 100 / total)))
+    return core_limit_text(d.usedcores, g.cus if g else 256)
 
 
 def container_env(devreq: list, gpus: dict, cfg: PluginConfig, cache_file: str) -> dict:

@@ -17,6 +17,7 @@ shim obeys when it has one: a tenant rewriting its region cannot clear them.
 from __future__ import annotations
 
 import logging
+import re
 import threading
 
 from .control import DEFAULT_LEASE_S
@@ -125,14 +126,26 @@ def mask_count(mask: str | None, idx: int) -> int:
     return 0
 
 
+def core_limit_ppm(s: str | None) -> int:
+    """A grant's core limit in percent with up to four decimals ("25", "12.5")
+    -> parts per million of the device; 0 when absent or outside (0, 100].
+    Integer arithmetic, the shim's parse_pct_ppm digit for digit."""
+    m = re.fullmatch(r"([0-9]{0,3})(?:\.([0-9]*))?", s or "")
+    if not m or not (m.group(1) or m.group(2)):
+        return 0
+    ppm = int(m.group(1) or "0") * 10000 + int((m.group(2) or "")[:4].ljust(4, "0"))
+    return ppm if 0 < ppm <= 1_000_000 else 0
+
+
+def pct_of_ppm(ppm: int) -> int:
+    """The region's whole-percent core limit of a ppm share (half up, >= 1)."""
+    return 0 if ppm == 0 else max(1, (ppm + 5000) // 10000)
+
+
 def expected_region(grant: dict) -> dict:
     """Region fields a grant file (deviceplugin/allocate.py) implies."""
     allmem = parse_size(grant.get("HIP_DEVICE_MEMORY_LIMIT"))
-    try:
-        core = int(grant.get("HIP_DEVICE_CORE_LIMIT", "100"))
-    except ValueError:
-        core = 100
-    core = core if 1 <= core <= 100 else 100
+    core = pct_of_ppm(core_limit_ppm(grant.get("HIP_DEVICE_CORE_LIMIT")) or 1000000)
     pol = {"force": 1, "disable": 2}.get(grant.get("GPU_CORE_UTILIZATION_POLICY", "").lower(), 0)
     try:
         prio = int(grant.get("HIP_TASK_PRIORITY", "1"))
@@ -140,11 +153,8 @@ def expected_region(grant: dict) -> dict:
         prio = 1
     cores = []
     for i in range(MAX_DEVICES):
-        try:
-            ci = int(grant.get(f"HIP_DEVICE_CORE_LIMIT_{i}", "0"))
-        except ValueError:
-            ci = 0
-        cores.append(ci if 1 <= ci <= 100 else core)
+        ci = core_limit_ppm(grant.get(f"HIP_DEVICE_CORE_LIMIT_{i}"))
+        cores.append(pct_of_ppm(ci) if ci else core)
     return {"mem_limit": [parse_size(grant.get(f"HIP_DEVICE_MEMORY_LIMIT_{i}")) or allmem
                           for i in range(MAX_DEVICES)],
             "cu_limit": cores, "cu_mask": [mask_count(grant.get("HSA_CU_MASK"), i) for i in range(MAX_DEVICES)],

@@ -60,7 +60,8 @@ def test_container_env(name, devs, cfg, want, absent):
     assert e["MIVGPU_SHARED_CACHE"] == "/tmp/vgpu/x.cache"
 
 
-@pytest.mark.parametrize("cus,want", [(1, "1"), (8, "3"), (64, "25"), (128, "50"), (255, "100"), (256, "100")])
+@pytest.mark.parametrize("cus,want", [(1, "0.391"), (8, "3.125"), (32, "12.5"), (64, "25"), (128, "50"),
+                                      (77, "30.078"), (255, "99.609"), (256, "100")])
 def test_core_limit_percent_rounding(cus, want):
     assert env([cd(mem=10, cus=cus)])["HIP_DEVICE_CORE_LIMIT"] == want
 

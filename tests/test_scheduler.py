@@ -362,7 +362,7 @@ def test_small_slice_env_time_slices_its_shared_range(cluster, share_small):
                                  annos[CU_RANGES_ANNOS])[0]
     gpus = {"n1-gpu0": GPUInfo(index=0, uuid="n1-gpu0", rocr_id="0")}
     env = container_env(dev, gpus, PluginConfig(), "/x.cache")
-    assert env["HIP_DEVICE_CORE_LIMIT"] == "12" or env["HIP_DEVICE_CORE_LIMIT"] == "13"
+    assert env["HIP_DEVICE_CORE_LIMIT"] == "12.5"   # the 32 CUs charged (12 % in whole granules), exactly
     lo_hi = env["HSA_CU_MASK"].split(":")[1]
     assert codec.ranges_count([tuple(map(int, r.split("-"))) for r in lo_hi.split(",")]) == 64
 

@@ -188,7 +188,7 @@ def test_roctx_markers_for_shim_decisions(native_build, tmp_path):
     out = run(native_build, tmp_path, "alloc", 800, "alloc", 800, env=env)
     assert out[0]["rc"] == 0 and out[1]["rc"] == 2
     lines = trace.read_text().splitlines()
-    assert "mark mivgpu:config dev=0 limit_mib=1000 cu_limit=100 cu_mask=0" in lines
+    assert "mark mivgpu:config dev=0 limit_mib=1000 cu_limit=100 cu_mask=0 cu_limit_ppm=1000000" in lines
     assert "mark mivgpu:oom dev=0 req_mib=800 used_mib=800 limit_mib=1000" in lines
     run(native_build, tmp_path, "alloc", 800, "alloc", 800, cache="s.cache",
         env={**env, "MIVGPU_OVERSUBSCRIBE": "true"})
@@ -578,3 +578,38 @@ def test_launch_hook_host_cost(native_build, tmp_path):
                  True, "c") for _ in range(2))
     assert off - base < 250, (base, off)
     assert gov - base < 900, (base, gov)
+
+
+@pytest.mark.parametrize("text,ppm,pct", [("12.5", 125000, 13), ("3.125", 31250, 3), ("25", 250000, 25),
+                                          ("0.391", 3910, 1), ("100", 1000000, 100)])
+def test_sub_percent_core_limit(native_build, tmp_path, text, ppm, pct):
+    """The grant states the CUs charged as an exact share (deviceplugin/
+    allocate.py core_limit_text): the governor takes it to the ppm, the
+    region (the monitor's whole-percent field) holds it rounded half up."""
+    trace = tmp_path / "roctx.txt"
+    env = {"HIP_DEVICE_MEMORY_LIMIT_0": "1000m", "HIP_DEVICE_CORE_LIMIT": text, "MIVGPU_ROCTX": "1",
+           "MIVGPU_ROCTX_LIB": str(native_build["roctx"]), "MOCK_ROCTX_OUT": str(trace)}
+    out = run(native_build, tmp_path, "alloc", 100, env=env, cache="c.cache")
+    assert out[0]["rc"] == 0
+    assert (f"mark mivgpu:config dev=0 limit_mib=1000 cu_limit={pct} cu_mask=0 cu_limit_ppm={ppm}"
+            in trace.read_text().splitlines())
+
+
+@pytest.mark.parametrize("limit,trend", [("62.5", "full"), ("37.5", "debt")])
+def test_host_bucket_accrues_at_the_exact_share(native_build, tmp_path, limit, trend):
+    """Half the GPU received (a comparable busy peer): under a 62.5 % limit
+    the bucket fills, under 37.5 % it runs into debt -- the fraction is not
+    cut to a whole percent on the way."""
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
+    _occ(kfd, 987654, 4242, 10)
+    _occ(kfd, 111, 4242, 30)
+    env = dict(_kfd_env(kfd), HIP_DEVICE_CORE_LIMIT=limit, GPU_CORE_UTILIZATION_POLICY="force",
+               MOCKHIP_GOVERNOR="1", MIVGPU_GATE_BURST_US="100000")
+    out = run(native_build, tmp_path, "kfdctx", 0, "alloc", 100, "launch", 300, "sleep", 900, "launch", 10,
+              "balance", env=env, cache=f"x{limit}.cache")
+    bal = out[-1]
+    assert bal["rc"] == 0, bal
+    if trend == "full":
+        assert bal["tokens_ns"] >= 95_000_000, bal
+    else:
+        assert bal["tokens_ns"] < -50_000_000, bal

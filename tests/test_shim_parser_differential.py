@@ -57,3 +57,22 @@ def test_device_plugin_mask_counted_by_the_shim(native_build, granules):
     env = container_env(devs, {}, PluginConfig(), "/tmp/x.cache")
     for i, g in enumerate(granules):
         assert lib.mivgpu_parse_cu_mask_count(env["HSA_CU_MASK"].encode(), i) == g * 8
+
+
+pct_text = st.one_of(
+    st.integers(0, 1000).map(str),
+    st.tuples(st.integers(0, 999), st.integers(0, 10 ** 6), st.integers(0, 6)).map(
+        lambda t: f"{t[0]}.{str(t[1]).zfill(t[2])[:t[2]]}"),
+    st.text(alphabet="0123456789.+- x", max_size=8))
+
+
+@settings(max_examples=300, deadline=None)
+@given(pct_text)
+def test_core_limit_ppm_agrees(native_build, s):
+    lib = _lib(native_build)
+    lib.mivgpu_parse_pct_ppm.restype = ctypes.c_uint
+    lib.mivgpu_parse_pct_ppm.argtypes = [ctypes.c_char_p]
+    lib.mivgpu_pct_of_ppm.argtypes = [ctypes.c_uint]
+    got = lib.mivgpu_parse_pct_ppm(s.encode())
+    assert got == F.core_limit_ppm(s), s
+    assert lib.mivgpu_pct_of_ppm(got) == F.pct_of_ppm(got), s
