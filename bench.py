@@ -73,8 +73,10 @@ def main():
                          "temporal, native, native_hip_default")
     ap.add_argument("--no-spatial", action="store_true", help="no HSA_CU_MASK (temporal governor)")
     ap.add_argument("--layout", default="auto", choices=["auto", "hybrid", "disjoint"],
-                    help="CU ranges of slices below a quarter GPU: shared quarters split by the governor "
-                         "(hybrid = auto, the allocator's default) or disjoint ranges")
+                    help="CU ranges of slices below a quarter GPU: shared ranges split by the governor "
+                         "(hybrid) or disjoint ranges (auto = the allocator's default, cuShareSmall)")
+    ap.add_argument("--share-unit", type=int, default=64, metavar="CUS",
+                    help="CUs of one shared range in the hybrid layout (64 = a quarter, the allocator's)")
     ap.add_argument("--active-slices", type=int, default=0,
                     help="run only the first K of the --slices planned slices (same masks/limits; 0 = all)")
     ap.add_argument("--monitor", type=float, default=0.0, metavar="SECONDS",
@@ -185,14 +187,15 @@ def main():
         rounds.append(("shim", spawn_round(
             with_env(with_limits(plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib,
                                              spatial=not args.no_spatial, policy=args.policy,
-                                             hw_queues=args.hw_queues or None, layout=args.layout))),
+                                             hw_queues=args.hw_queues or None, layout=args.layout,
+                                             share_unit=args.share_unit))),
             phys, work, log_dir, child_args, "shim")))
     if "masked_noshim" in wanted:
         # the same CU masks and queues without libmivgpu.so: what the shim
         # itself costs (the overhead vs native also contains the
         # partitioning's own benefit)
         bare = plan_slices(args.slices, shim=True, gpumem_mib=None, hw_queues=args.hw_queues or None,
-                           layout=args.layout)
+                           layout=args.layout, share_unit=args.share_unit)
         for sp in bare:
             sp.shim = False
         rounds.append(("masked_noshim", spawn_round(with_env(bare), phys, work / "bare", log_dir, child_args,
@@ -314,7 +317,9 @@ def main():
                 "gpucores_per_slice": limits or (100 // args.slices if args.slices > 1 else 100),
                 # the grant's HIP_DEVICE_CORE_LIMIT: the CUs charged, as an exact share
                 "core_limit_pct_per_slice": [pct_text(sp.core_pct) for sp in head.get("specs", [])],
-                "isolation": (f"HSA_CU_MASK ({args.layout} layout) + libmivgpu" if not args.no_spatial
+                "isolation": (f"HSA_CU_MASK ({args.layout} layout"
+                              + (f", {args.share_unit}-CU shared ranges" if args.layout == "hybrid" else "")
+                              + ") + libmivgpu" if not args.no_spatial
                               else f"governor ({args.policy})")
                 + (f" + {args.hw_queues} HW queue/slice" if args.hw_queues and args.slices > 1 else ""),
             },

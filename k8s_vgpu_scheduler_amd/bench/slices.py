@@ -62,7 +62,8 @@ def cu_mask_string(ranges) -> str:
 
 
 def plan_slices(n: int, shim: bool, gpumem_mib: int | None, spatial: bool = True,
-                policy: str = "default", hw_queues: int | None = 2, layout: str = "auto") -> list[SliceSpec]:
+                policy: str = "default", hw_queues: int | None = 2, layout: str = "auto",
+                share_unit: int = MI355X_CUS // 4) -> list[SliceSpec]:
     """Equal split of one GPU into n slices (CUs in contiguous, XCD-sized runs).
 
     ``layout`` = what the scheduler's CU allocator hands out
@@ -72,7 +73,7 @@ def plan_slices(n: int, shim: bool, gpumem_mib: int | None, spatial: bool = True
     the allocator's default (``cuShareSmall``, off: disjoint)."""
     specs = []
     per = (MI355X_CUS // n) // MI355X_XCDS * MI355X_XCDS   # whole 8-CU granules: XCD-balanced
-    unit = MI355X_CUS // 4
+    unit = share_unit
     from k8s_vgpu_scheduler_amd.device.amd.device import AMDConfig
     hybrid = layout == "hybrid" or (layout == "auto" and AMDConfig().cu_share_small)
     share = unit // per if (hybrid and 0 < per < unit) else 1

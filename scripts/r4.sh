@@ -86,10 +86,12 @@ for s in "$@"; do
               --child-env MIVGPU_SLICE_PLAN_CUS=0 --out "gpurun_out/$out/s8p_chip.json"
             run 400 s8p_q1 python -u bench.py --slices 8 --layout disjoint --rounds shim --hw-queues 1 \
               --out "gpurun_out/$out/s8p_q1.json" ;;
-    s8temporal) run 400 s8t_12 python -u bench.py --slices 8 --rounds temporal,native \
-              --out "gpurun_out/$out/s8t_12.json"
-            run 400 s8t_13 python -u bench.py --slices 8 --rounds temporal --slice-limits 13,13,13,13,13,13,13,13 \
-              --out "gpurun_out/$out/s8t_13.json" ;;
+    s8pool) run 400 s8h128 python -u bench.py --slices 8 --layout hybrid --share-unit 128 --rounds shim --monitor 5 \
+              --out "gpurun_out/$out/s8h128.json"
+            run 400 s8h256 python -u bench.py --slices 8 --layout hybrid --share-unit 256 --rounds shim --monitor 5 \
+              --out "gpurun_out/$out/s8h256.json" ;;
+    s8temporal) run 400 s8t_exact python -u bench.py --slices 8 --rounds temporal,native \
+              --out "gpurun_out/$out/s8t_exact.json" ;;
     unequal) run 500 unequal_tests python -u -m pytest tests/test_shim_gpu.py -v -s $T -k "unequal or charged_the_share" ;;
     lds) export TMPDIR=/tmp PYTHONPATH=$R
          run 150 lds_full rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_BF16 \
