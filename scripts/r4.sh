@@ -90,6 +90,10 @@ for s in "$@"; do
               --out "gpurun_out/$out/s8h128.json"
             run 400 s8h256 python -u bench.py --slices 8 --layout hybrid --share-unit 256 --rounds shim --monitor 5 \
               --out "gpurun_out/$out/s8h256.json" ;;
+    s8gov) run 500 s8g_default python -u bench.py --slices 8 --no-spatial --rounds shim,native --monitor 1 --steps 300 \
+             --out "gpurun_out/$out/s8g_default.json"
+           run 500 s8g_burst python -u bench.py --slices 8 --rounds temporal --steps 300 \
+             --child-env MIVGPU_GATE_BURST_US=200000 --out "gpurun_out/$out/s8g_burst.json" ;;
     s8temporal) run 400 s8t_exact python -u bench.py --slices 8 --rounds temporal,native \
               --out "gpurun_out/$out/s8t_exact.json" ;;
     unequal) run 500 unequal_tests python -u -m pytest tests/test_shim_gpu.py -v -s $T -k "unequal or charged_the_share" ;;
