@@ -60,6 +60,13 @@ for s in "$@"; do
            python3 scripts/probe/trace_step.py "$R/gpurun_out/$out/chainprof_c$c" --steps 8 --json \
              > "$R/gpurun_out/$out/chainprof_c$c.json" && rm -rf "$R/gpurun_out/$out/chainprof_c$c"
          done ;;
+    prof) export TMPDIR=/tmp PYTHONPATH=$R
+          for b in 32 1; do
+            run 200 "prof_b$b" rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/$out/prof_b$b" -o run -- \
+              python3 -m k8s_vgpu_scheduler_amd.bench.decode --batch $b --steps 12 --warmup 2
+            python3 scripts/probe/trace_step.py "$R/gpurun_out/$out/prof_b$b" --steps 8 --json \
+              > "$R/gpurun_out/$out/prof_b$b.json" && rm -rf "$R/gpurun_out/$out/prof_b$b"
+          done ;;
     launch) run 400 launch_test python -u -m pytest tests/test_shim_gpu.py -v -s $T -k launch_overhead ;;
     interpose) run 600 interpose_tests python -u -m pytest tests/test_shim_interpose_gpu.py -v -s $T -k "triton or compile" ;;
     tenant) run 300 tenant_test python -u -m pytest tests/test_shim_interpose_gpu.py -v -s $T -k "tenant_" ;;
