@@ -67,8 +67,13 @@ def test_hipstream_under_shim_has_no_overhead():
     tmp = tempfile.mkdtemp(prefix="mivgpu-lg-")
     # ~0.1 s of copying per run (20 iterations were ~9 ms: one scheduling blip
     # moved the ratio by 5 %)
-    base = run_child("hipstream", {}, False, ["--n", "1024", "--iters", "200"])
-    shim = run_child("hipstream", {"MIVGPU_SHARED_CACHE": os.path.join(tmp, "s.cache")}, True,
-                     ["--n", "1024", "--iters", "200"])
-    assert base["rc"] == 0 and shim["rc"] == 0 and base["exact"] and shim["exact"]
-    assert shim["gbps"] >= 0.95 * base["gbps"], (shim["gbps"], base["gbps"])
+    # A B B A, best of two each: the first run on a fresh box also meets the
+    # clocks ramping (one round measured 4410 vs 4712 GB/s with the shim second)
+    runs = {False: [], True: []}
+    for i, with_shim in enumerate((False, True, True, False)):
+        env = {"MIVGPU_SHARED_CACHE": os.path.join(tmp, f"s{i}.cache")} if with_shim else {}
+        r = run_child("hipstream", env, with_shim, ["--n", "1024", "--iters", "200"])
+        assert r["rc"] == 0 and r["exact"], r
+        runs[with_shim].append(r["gbps"])
+    base, shim = max(runs[False]), max(runs[True])
+    assert shim >= 0.95 * base, runs
