@@ -104,6 +104,9 @@ for s in "$@"; do
     plans2) for p in "" "1,1" "4,1"; do
               MIVGPU_GU_PLAN=$p run 200 "gu2_${p/,/_}" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 32
             done ;;
+    plans3) for p in "" "1,2" "2,2" "1,8"; do
+              MIVGPU_DOWN_PLAN=$p run 200 "d3_${p/,/_}" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 32
+            done ;;
     s8temporal) run 400 s8t_exact python -u bench.py --slices 8 --rounds temporal,native \
               --out "gpurun_out/$out/s8t_exact.json" ;;
     unequal) run 500 unequal_tests python -u -m pytest tests/test_shim_gpu.py -v -s $T -k "unequal or charged_the_share" ;;
