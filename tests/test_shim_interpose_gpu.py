@@ -167,18 +167,21 @@ def _container(tmp, name):
 
 
 def _kfd_vram() -> dict:
-    """KFD's per-process VRAM (all GPUs) by host pid."""
+    """KFD's per-process VRAM on this box's GPU by host pid.  KFD lists every
+    host process that opened /dev/kfd, other jobs on the host's other GPUs
+    too (one round found a 19 GB stranger next to the hog): only ``vram_<our
+    gpu_id>`` counts."""
     import glob
 
+    from k8s_vgpu_scheduler_amd.monitor.hosttruth import single_gpu_ids
+
+    gid = single_gpu_ids("x").get("x")
     out = {}
     for d in glob.glob("/sys/class/kfd/kfd/proc/*"):
-        tot = 0
-        for f in glob.glob(os.path.join(d, "vram_*")):
-            try:
-                tot += int(open(f).read().strip() or 0)
-            except (OSError, ValueError):
-                pass
-        out[int(os.path.basename(d))] = tot
+        try:
+            out[int(os.path.basename(d))] = int(open(os.path.join(d, f"vram_{gid}")).read().strip() or 0)
+        except (OSError, ValueError):
+            pass
     return out
 
 
