@@ -1530,6 +1530,7 @@ hipError_t launch_widek(int kw, const Args& a, hipStream_t s) {
       switch (kw) {
         case 2: MIVGPU_LAUNCH_WIDEK(2, true); break;
         case 4: MIVGPU_LAUNCH_WIDEK(4, true); break;
+        case 8: MIVGPU_LAUNCH_WIDEK(8, true); break;
         default: return hipErrorInvalidValue;
       }
       return hipGetLastError();
@@ -1540,6 +1541,13 @@ hipError_t launch_widek(int kw, const Args& a, hipStream_t s) {
   switch (kw) {
     case 2: MIVGPU_LAUNCH_WIDEK(2, false); break;
     case 4: MIVGPU_LAUNCH_WIDEK(4, false); break;
+    case 8:
+      // 8 k-waves: two 66 KB X buffers, one M-tile only (LDS)
+      if constexpr (MT == 1) {
+        MIVGPU_LAUNCH_WIDEK(8, false);
+        break;
+      }
+      return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 #undef MIVGPU_LAUNCH_WIDEK
@@ -1696,8 +1704,17 @@ bool plan_widek(int M, int K, int N, int epi, int* nt, int* kw, int* S) {
   if (*nt > 0 && *nt != want) return false;
   *nt = want;
   if ((N / 32) % want) return false;
-  if (*kw <= 0) *kw = 4;
-  if (*kw != 2 && *kw != 4) return false;
+  if (*kw <= 0) {
+    // MIVGPU_WIDEK_KW: k-waves per workgroup for A/B runs (8: one M-tile only;
+    // measured whole GPU, qkv + o_proj: batch 32 4.583 vs 4.563 ms, batch 1
+    // 3.415 vs 3.346 -- twice the waves per CU do not stream faster)
+    static const int env = [] {
+      const char* e = getenv("MIVGPU_WIDEK_KW");
+      return e && *e ? atoi(e) : 0;
+    }();
+    *kw = (env == 8 && M <= 32) || env == 2 || env == 4 ? env : 4;
+  }
+  if (*kw != 2 && *kw != 4 && !(*kw == 8 && M <= 32)) return false;
   const int KB = K / 64, GK = *kw * 2;
   // no inter-workgroup split by default: measured on the whole chip (bench/gemm.py,
   // profiles/round3/widek_gemm.json) S = 2 costs qkv 13.6 -> 19.1 us and o_proj

@@ -107,6 +107,13 @@ for s in "$@"; do
     plans3) for p in "" "1,2" "2,2" "1,8"; do
               MIVGPU_DOWN_PLAN=$p run 200 "d3_${p/,/_}" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 32
             done ;;
+    kw8) run 300 kw8_tests python -u -m pytest tests/test_ops_gpu.py tests/test_skinny_gemm_gpu.py -v $T -k "widek or row_norm"
+         for k in "" 8 "" 8; do
+           MIVGPU_WIDEK_KW=$k run 200 "kw8_b32_$k" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 32
+         done
+         for k in "" 8; do
+           MIVGPU_WIDEK_KW=$k run 200 "kw8_b1_$k" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 1
+         done ;;
     s8temporal) run 400 s8t_exact python -u bench.py --slices 8 --rounds temporal,native \
               --out "gpurun_out/$out/s8t_exact.json" ;;
     unequal) run 500 unequal_tests python -u -m pytest tests/test_shim_gpu.py -v -s $T -k "unequal or charged_the_share" ;;

@@ -499,7 +499,7 @@ def test_decoder_norm_fused_prefill_matches_reference(monkeypatch, graph, plen):
 
 @pytest.mark.parametrize("M,N,K", [(1, 6144, 4096), (32, 6144, 4096), (8, 4096, 4096), (32, 4096, 12288),
                                    (48, 4096, 4096)])
-@pytest.mark.parametrize("kw,S", [(4, 0), (2, 1), (4, 2)])
+@pytest.mark.parametrize("kw,S", [(4, 0), (2, 1), (4, 2), (8, 0), (8, 2)])
 def test_skinny_widek_matches_reference(ops, M, N, K, kw, S):
     """K-split wide kernel (variant 3): KW waves interleave one n-tile's
     k-blocks and reduce through LDS, optionally split S ways across
@@ -521,7 +521,7 @@ def test_skinny_widek_matches_reference(ops, M, N, K, kw, S):
 
 
 @pytest.mark.parametrize("M,K,inter", [(1, 4096, 12288), (32, 4096, 12288), (48, 1024, 2048), (5, 512, 1024)])
-@pytest.mark.parametrize("kw,S", [(4, 0), (2, 1), (4, 2)])
+@pytest.mark.parametrize("kw,S", [(4, 0), (2, 1), (4, 2), (8, 0)])
 def test_skinny_widek_silu_matches_reference(ops, M, K, inter, kw, S):
     """K-split kernel on gate/up tile pairs with the SiLU(gate)*up epilogue
     (Qwen3-8B gate_up and small shapes) vs fp32, twice (slabs left clean)."""

@@ -141,7 +141,7 @@ def _rms_ref(x, w, eps=1e-6):
     return xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
 
 
-@pytest.mark.parametrize("variant", ["wide", "widek"])
+@pytest.mark.parametrize("variant", ["wide", "widek", "widek8"])
 @pytest.mark.parametrize("S", [0, 1, 4])
 @pytest.mark.parametrize("M", [1, 5, 32, 48])
 def test_row_norm_fusion_chain(M, S, variant):
@@ -158,21 +158,26 @@ def test_row_norm_fusion_chain(M, S, variant):
     wg = (torch.randn(N2, K, device="cuda", generator=g) * 0.02).bfloat16()
     po = ops.PackedLinear(wo)
     pg = ops.PackedLinear(wg, col_scale=wn)
-    if variant == "widek":
+    ks = 8 if variant == "widek8" else 0    # 8 k-waves per workgroup: one M-tile only
+    if variant.startswith("widek"):
         po.variant = pg.variant = ops.VARIANT_WIDEK
-        assert ops.skinny_plan(M, K, N1, ops.EPI_STORE, 0, 0, S, ops.VARIANT_WIDEK)["variant"] == ops.VARIANT_WIDEK
+        pl = ops.skinny_plan(M, K, N1, ops.EPI_STORE, 0, ks, S, ops.VARIANT_WIDEK)
+        if ks == 8 and M > 32:
+            assert pl["variant"] != ops.VARIANT_WIDEK
+            return
+        assert pl["variant"] == ops.VARIANT_WIDEK
     slots = po.slots(M)
     ss = torch.full((slots * ops.SS_ROWS,), float("nan"), device="cuda")   # every used slot must be written
     r1 = res.clone()
     for _ in range(2):   # split-K scratch / tickets must come back clean
         r1.copy_(res)
-        po.norm_call(x, out=r1, residual=True, ss_out=ss, S=S)
+        po.norm_call(x, out=r1, residual=True, ss_out=ss, S=S, ks=ks)
         exp_res = res.float() + _ref(x, wo)
         _close(r1, exp_res)
         got_ss = ss.view(slots, ops.SS_ROWS)[:, :M].sum(0)
         _close(got_ss, r1.float().pow(2).sum(-1), 1e-3)
         y = torch.empty(M, N2, device="cuda", dtype=torch.bfloat16)
-        pg.norm_call(r1, out=y, row_scale=(ss, slots, K, 1e-6), S=S)
+        pg.norm_call(r1, out=y, row_scale=(ss, slots, K, 1e-6), S=S, ks=ks)
         _close(y, _rms_ref(r1, wn) @ wg.float().t())
 
 
