@@ -88,6 +88,15 @@ class AMDConfig:
     # 8511 tok/s (fairness 0.99) vs shared quarters 8457-8461 and the
     # temporal governor 8501 (profiles/README.md section 37)
     cu_share_small: bool = False
+    # False: no CU partitions at all -- a gpucores request is charged its
+    # granules as before, but the container gets no HSA_CU_MASK and the shim's
+    # temporal governor holds it to that charge (the reference's time-sharing
+    # model).  Measured, 8 x 12 % decode tenants: -0.5 % vs native over 300
+    # steps (fairness 0.994) against -4 to -5 % for disjoint 32-CU partitions,
+    # which in turn keep every tenant's CUs its own (profiles/README.md
+    # section 38).  Applies to every pod of the node's GPUs: masked and
+    # unmasked tenants on one GPU would share the masked ones' CUs.
+    cu_partition: bool = True
     # Node-side (device plugin) knobs, shared through the same config
     device_split_count: int = 8
     device_memory_scaling: float = 1.0
@@ -110,7 +119,7 @@ class AMDConfig:
              "xcdsPerDevice": "xcds_per_device", "cuLayout": "cu_layout",
              "deviceSplitCount": "device_split_count", "deviceMemoryScaling": "device_memory_scaling",
              "deviceCoreScaling": "device_core_scaling", "allowTenantOptOut": "allow_tenant_opt_out",
-             "cuShareSmall": "cu_share_small"}
+             "cuShareSmall": "cu_share_small", "cuPartition": "cu_partition"}
         kw = {}
         for k, v in (d or {}).items():
             if k in m:
@@ -513,7 +522,7 @@ class AMDDevices(D.Devices):
                 bump(R.CARD_COMPUTE_UNITS_EXHAUSTED)
                 continue
             info = {}
-            if 0 < cu < dev.totalcore:
+            if 0 < cu < dev.totalcore and self.cfg.cu_partition:
                 if self.cfg.cu_share_small and cu < cu_alloc.share_unit(topo) and topo.xcds > 1:
                     ranges = cu_alloc.pick_shared(dev.custominfo.get("cu_used", 0),
                                                   dev.custominfo.get("cu_shared", {}), cu, topo)

@@ -373,3 +373,39 @@ def test_share_small_off_keeps_disjoint_ranges(cluster):
     assert filt(s, cluster, amd_pod("p", mem=1024, cores=12), ["n1"])["NodeNames"] == ["n1"]
     cus, ranges = _ranges_of(cluster, "p")
     assert cus == 32 and codec.ranges_count(ranges) == 32
+
+
+@pytest.fixture
+def no_partition():
+    """cuPartition: false (time-sharing only) for one test."""
+    from k8s_vgpu_scheduler_amd.device import devices as D
+    D.get_devices()["AMD"].cfg.cu_partition = False
+    yield
+    D.get_devices()["AMD"].cfg.cu_partition = True
+
+
+def test_time_sharing_mode_charges_granules_without_masks(cluster, no_partition):
+    """cuPartition: false -- eight 12 % pods fill the GPU by their granule
+    charge (32 CUs each), a ninth does not fit; the containers get no CU mask
+    and the exact charge as their governed core limit."""
+    from k8s_vgpu_scheduler_amd.deviceplugin.allocate import PluginConfig, container_env
+    from k8s_vgpu_scheduler_amd.smi import GPUInfo
+
+    s = make_sched(cluster, [amd_node("n1", n=1)])
+    for i in range(8):
+        assert filt(s, cluster, amd_pod(f"p{i}", mem=32768, cores=12), ["n1"])["NodeNames"] == ["n1"], i
+    assert not filt(s, cluster, amd_pod("p8", mem=1024, cores=12), ["n1"]).get("NodeNames")
+    annos = cluster.get_pod("default", "p0")["metadata"]["annotations"]
+    devs = codec.decode_pod_devices({"AMD": SUPPORT_ANNOS}, annos)["AMD"]
+    if annos.get(CU_RANGES_ANNOS):
+        devs = codec.attach_cu_ranges(devs, annos[CU_RANGES_ANNOS])
+    dev = devs[0]
+    assert dev[0].usedcores == 32 and not (dev[0].custominfo or {}).get("cu_ranges")
+    env = container_env(dev, {"n1-gpu0": GPUInfo(index=0, uuid="n1-gpu0", rocr_id="0")}, PluginConfig(), "/x.cache")
+    assert "HSA_CU_MASK" not in env and env["HIP_DEVICE_CORE_LIMIT"] == "12.5"
+
+
+def test_cu_partition_config_key():
+    from k8s_vgpu_scheduler_amd.device.amd.device import AMDConfig
+    assert AMDConfig.from_dict({"cuPartition": False}).cu_partition is False
+    assert AMDConfig().cu_partition is True
