@@ -218,11 +218,13 @@ class E2ECluster:
     """One node, the three binaries, the API server and the kubelet."""
 
     def __init__(self, workdir: str | None = None, node: str = "node1", smi_backend: str = "fake",
-                 fake_gpus: int = 2, split: int = 4, extra_env: dict | None = None, log_level: int = 3):
+                 fake_gpus: int = 2, split: int = 4, extra_env: dict | None = None, log_level: int = 3,
+                 device_config: dict | None = None):
         self.dir = Path(workdir or tempfile.mkdtemp(prefix="mivgpu-e2e-"))
         self.node, self.smi_backend, self.fake_gpus, self.split = node, smi_backend, fake_gpus, split
         self.extra_env = extra_env or {}
         self.log_level = log_level
+        self.device_config = device_config   # the scheduler's --device-config-file contents ({"amd": {...}})
         self.procs: dict[str, subprocess.Popen] = {}
         self.ports = {k: free_port() for k in ("http", "sched_metrics", "mon_metrics")}
         self.hook = self.dir / "hook"
@@ -247,7 +249,12 @@ class E2ECluster:
         self.api.cluster.create("nodes", make_node(self.node))
         self.kubelet = FakeKubelet(self.dir, self.api, self.node).start()
         kc = ["--kubeconfig", self.kubeconfig]
-        self._spawn("scheduler", [*kc, "--http_bind", f"127.0.0.1:{self.ports['http']}",
+        dc = []
+        if self.device_config:
+            import yaml
+            (self.dir / "device-config.yaml").write_text(yaml.safe_dump(self.device_config))
+            dc = ["--device-config-file", str(self.dir / "device-config.yaml")]
+        self._spawn("scheduler", [*kc, *dc, "--http_bind", f"127.0.0.1:{self.ports['http']}",
                                   "--metrics-bind-address", f"127.0.0.1:{self.ports['sched_metrics']}",
                                   "--scheduler-name", "hami-scheduler", "-v", str(self.log_level)])
         self._spawn("device_plugin", [*kc, "--node-name", self.node, "--kubelet-socket", self.kubelet.socket,

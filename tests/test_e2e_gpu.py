@@ -142,3 +142,28 @@ def test_gputype_and_uuid_selection_on_the_real_node(cluster):
             cl.start_containers("default", name)    # Allocate releases the node lock Bind took
         cl.delete_pod("default", name)
 
+
+
+def test_time_sharing_mode_on_the_real_node(tmp_path_factory):
+    """devices.amd.cuPartition: false end to end: a gpucores-12 pod is charged
+    32 CUs, its container gets no CU mask (its grid reaches all 256 CUs on the
+    8 XCDs) and the temporal governor holds it near the exact 12.5 % charge."""
+    with E2ECluster(str(tmp_path_factory.mktemp("e2e-ts")), smi_backend="amdsmi", split=8,
+                    device_config={"amd": {"cuPartition": False}}) as cl:
+        cl.submit(amd_pod("ts", mem=8192, cores=12))
+        assert cl.schedule("default", "ts") == "node1"
+        alloc = cl.start_containers("default", "ts")[0]
+        env = container_env(alloc)
+        env["PYTHONPATH"] = str(REPO)
+        assert "HSA_CU_MASK" not in env and env["HIP_DEVICE_CORE_LIMIT"] == "12.5", env
+        hw = _probe(env, "hwid")
+        assert hw["distinct"] == 256 and hw["xccs"] == list(range(8)), hw
+        mm = ["--n", "8192", "--iters", "1000"]   # ~0.9 s unthrottled: the bucket's burst is a small part
+        free = dict(env)
+        free.pop("LD_PRELOAD", None)
+        base = _probe(free, "matmul", *mm)
+        held = _probe(env, "matmul", *mm)
+        ratio = held["tflops"] / base["tflops"]
+        print(json.dumps({"ratio": round(ratio, 3), "held_ms": held.get("gate_held_ms"), "gates": held.get("gates")}))
+        assert 0.08 <= ratio <= 0.2, ratio
+        cl.delete_pod("default", "ts")
