@@ -114,6 +114,10 @@ for s in "$@"; do
          for k in "" 8; do
            MIVGPU_WIDEK_KW=$k run 200 "kw8_b1_$k" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 1
          done ;;
+    s8queues) for q in 3 4; do
+                run 500 "s8q$q" python -u bench.py --slices 8 --layout disjoint --rounds shim,native --hw-queues $q \
+                  --out "gpurun_out/$out/s8q$q.json"
+              done ;;
     s8temporal) run 400 s8t_exact python -u bench.py --slices 8 --rounds temporal,native \
               --out "gpurun_out/$out/s8t_exact.json" ;;
     unequal) run 500 unequal_tests python -u -m pytest tests/test_shim_gpu.py -v -s $T -k "unequal or charged_the_share" ;;
