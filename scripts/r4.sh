@@ -118,6 +118,14 @@ for s in "$@"; do
                 run 500 "s8q$q" python -u bench.py --slices 8 --layout disjoint --rounds shim,native --hw-queues $q \
                   --out "gpurun_out/$out/s8q$q.json"
               done ;;
+    l2) export TMPDIR=/tmp PYTHONPATH=$R
+        for b in 32 1; do
+          run 150 "l2_b$b" rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum --kernel-trace \
+            --output-format csv -d "$R/gpurun_out/$out/l2_b$b" -o run -- \
+            python3 -m k8s_vgpu_scheduler_amd.bench.decode --batch $b --steps 3 --warmup 1 --no-graph
+          python3 "$R/scripts/probe/pmc_summary.py" "$R/gpurun_out/$out/l2_b$b" > "$R/gpurun_out/$out/l2_b$b.json" \
+            && rm -rf "$R/gpurun_out/$out/l2_b$b"
+        done ;;
     s8temporal) run 400 s8t_exact python -u bench.py --slices 8 --rounds temporal,native \
               --out "gpurun_out/$out/s8t_exact.json" ;;
     unequal) run 500 unequal_tests python -u -m pytest tests/test_shim_gpu.py -v -s $T -k "unequal or charged_the_share" ;;
