@@ -76,6 +76,8 @@ def plan_slices(n: int, shim: bool, gpumem_mib: int | None, spatial: bool = True
     unit = share_unit
     from k8s_vgpu_scheduler_amd.device.amd.device import AMDConfig
     hybrid = layout == "hybrid" or (layout == "auto" and AMDConfig().cu_share_small)
+    if layout == "auto" and not AMDConfig().cu_partition:
+        spatial = False   # the allocator's time-sharing mode: no CU ranges at all
     share = unit // per if (hybrid and 0 < per < unit) else 1
     for i in range(n):
         if share > 1:
