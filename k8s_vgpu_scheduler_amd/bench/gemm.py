@@ -129,7 +129,7 @@ def main():
             if a.sweep and M in {int(v) for v in a.sweep_rows.split(",")}:
                 sw = {}
                 for variant, tag, kss in ((ops.VARIANT_CLASSIC, "", (1, 2, 4, 8)), (ops.VARIANT_WIDE, "wide_", (1, 2, 4)),
-                                          (ops.VARIANT_WIDEK, "widek_", (2, 4))):
+                                          (ops.VARIANT_WIDEK, "widek_", (2, 4, 8))):
                     for nt in (1, 2):
                         for ks in kss:
                             for S in (1, 2, 4, 8, 16):
