@@ -446,6 +446,27 @@ __device__ __forceinline__ void wide_store_x(bf16_t* xs, const u32x4_t (&xr)[XC]
   }
 }
 
+// The K-split kernel's X tile by LDS-DMA (MIVGPU_WIDEK_DMAX=1, A/B): with 8
+// k-blocks per group a row of the group's X is 1 KB, one 64-lane 16-byte
+// global_load_lds straight into its padded LDS row -- no VGPR staging, no
+// ds_write; the wave's loads complete in issue order, so waiting for all but
+// the W loads issued after it (vmcnt) covers the tile.  Measured slower
+// (decode step 4.654-4.678 vs 4.573-4.575 ms, batch 32): the compiler cannot
+// tell the DMA's LDS buffer from the one the MFMAs read and waits for every
+// load in flight (vmcnt(0)) before those reads in every other group, so the
+// next group's W no longer streams across the MFMAs.  Kept as an A/B option.
+template <int MT, int GK, int PITCH, int WAVES>
+__device__ __forceinline__ void widek_dma_x(bf16_t* xs, const bf16_t* __restrict__ x, int M, int ldx, int kb, int wave,
+                                            int lane) {
+  static_assert(GK * 64 * 2 == 64 * 16, "one row of the group's X is one 64-lane 16-byte DMA");
+#pragma unroll
+  for (int i = 0; i < MT * 32 / WAVES; ++i) {
+    const int r = wave + i * WAVES;   // wave-uniform
+    const bf16_t* g = x + (size_t)min(r, M - 1) * ldx + kb * 64 + lane * 8;
+    __builtin_amdgcn_global_load_lds(g, xs + r * PITCH, 16, 0, 0);
+  }
+}
+
 // X from decode-attention split partials instead of a bf16 matrix (batch 1):
 // the K-split kernel builds the whole combined row in LDS once, before its W
 // loop, computed as decode_attn_combine_kernel does (csrc/ops/model_ops.hip:
@@ -1013,11 +1034,12 @@ struct WidekLds {
   alignas(16) bf16_t s_res[EPI == EPI_RESID ? MT * 32 * 32 : 8];
 };
 
-template <int MT, int NT, int KW, int EPI, bool COMB, class Deps>
+template <int MT, int NT, int KW, int EPI, bool COMB, class Deps, bool DMAX = false>
 __device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<MT, NT, KW, EPI>& L,
                                            const XComb& xcomb, const Deps& deps) {
   static_assert((EPI == EPI_SILU_MUL) == (NT == 2) && NT <= 2, "widek: one tile, or a gate/up pair for SiLU*up");
   static_assert(!(COMB && Deps::chained), "the X-combine variant runs standalone");
+  static_assert(!DMAX || (!COMB && !Deps::chained && KW == 4), "LDS-DMA X: standalone, 4 k-waves");
   using LD = WidekLds<MT, NT, KW, EPI>;
   constexpr int U = LD::U;
   constexpr int GK = LD::GK;
@@ -1117,14 +1139,22 @@ __device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<M
         stepc(fa, fb, kb, false);
       }
     } else {
-      u32x4_t xr[XC];
-      wide_load_x<MT, GK, XC, SC1>(xr, x, M, ldx, kb0, tid, NTHREADS);
+      u32x4_t xr[DMAX ? 1 : XC];
+      if constexpr (DMAX) {
+        widek_dma_x<MT, GK, PITCH, KW>(xs, x, M, ldx, kb0, kw, lane);
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        wide_load_x<MT, GK, XC, SC1>(xr, x, M, ldx, kb0, tid, NTHREADS);
+      }
       if constexpr (!Deps::chained) wide_load_w<NT, U>(fa, wbase, ws, kb0 + kw * U, lane);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (RS) {
         if (p.rs_part) rs_finish<MT, NTHREADS>(rsv, p.rs_inv_dim, p.rs_eps, L.s_rs, L.s_rtmp, tid);
       }
-      wide_store_x<MT, GK, XC, PITCH>(xs, xr, tid, NTHREADS);
+      if constexpr (DMAX)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(U * NT * 4) : "memory");   // all but this wave's W loads
+      else
+        wide_store_x<MT, GK, XC, PITCH>(xs, xr, tid, NTHREADS);
       __syncthreads();
     }
   }
@@ -1133,17 +1163,29 @@ __device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<M
   // group from registers + this wave's columns of the LDS tile, stage X
   auto step = [&](const WFrag<NT>(&cur)[U], WFrag<NT>(&nxt)[U], const bf16_t* xc, bf16_t* xn, int kb,
                   bool prefetch) {
-    u32x4_t xr[XC];
+    u32x4_t xr[DMAX ? 1 : XC];
     if (prefetch) {
-      wide_load_x<MT, GK, XC, SC1>(xr, x, M, ldx, kb + GK, tid, NTHREADS);
+      if constexpr (DMAX) {
+        widek_dma_x<MT, GK, PITCH, KW>(xn, x, M, ldx, kb + GK, kw, lane);
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        wide_load_x<MT, GK, XC, SC1>(xr, x, M, ldx, kb + GK, tid, NTHREADS);
+      }
       wide_load_w<NT, U>(nxt, wbase, ws, kb + GK + kw * U, lane);
     }
     DB_FENCE();
     wide_mma<MT, NT, U, PITCH>(cur, xc + kw * U * 64, acc, r, h);
     DB_FENCE();
     if (prefetch) {
-      wide_store_x<MT, GK, XC, PITCH>(xn, xr, tid, NTHREADS);
-      __syncthreads();
+      if constexpr (DMAX) {
+        // the X tile landed (this wave's DMA); a bare barrier: __syncthreads'
+        // fence would also wait for the W loads still in flight
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(U * NT * 4) : "memory");
+        __builtin_amdgcn_s_barrier();
+      } else {
+        wide_store_x<MT, GK, XC, PITCH>(xn, xr, tid, NTHREADS);
+        __syncthreads();
+      }
     }
   };
   int g = 0, kb = kb0;
@@ -1210,10 +1252,10 @@ __device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<M
   deps.publish(vgroup);
 }
 
-template <int MT, int NT, int KW, int EPI, bool COMB = false>
+template <int MT, int NT, int KW, int EPI, bool COMB = false, bool DMAX = false>
 __global__ void __launch_bounds__(64 * KW) skinny_widek_kernel(GemmP p, XComb xcomb) {
   __shared__ WidekLds<MT, NT, KW, EPI> lds;
-  widek_body<MT, NT, KW, EPI, COMB>(p, blockIdx.x, lds, xcomb, NoDeps{});
+  widek_body<MT, NT, KW, EPI, COMB, NoDeps, DMAX>(p, blockIdx.x, lds, xcomb, NoDeps{});
 }
 
 // ============================================================================
@@ -1537,6 +1579,15 @@ hipError_t launch_widek(int kw, const Args& a, hipStream_t s) {
     }
   } else if (comb) {
     return hipErrorInvalidValue;
+  }
+  static const bool dmax = [] {
+    const char* e = getenv("MIVGPU_WIDEK_DMAX");
+    return e && *e == '1';
+  }();
+  if (dmax && kw == 4) {
+    hipLaunchKernelGGL((skinny_widek_kernel<MT, NT, 4, EPI, false, true>), dim3(blocks), dim3(256), 0, s, gemm_p(a),
+                       a.xcomb);
+    return hipGetLastError();
   }
   switch (kw) {
     case 2: MIVGPU_LAUNCH_WIDEK(2, false); break;

@@ -126,6 +126,11 @@ for s in "$@"; do
           python3 "$R/scripts/probe/pmc_summary.py" "$R/gpurun_out/$out/l2_b$b" > "$R/gpurun_out/$out/l2_b$b.json" \
             && rm -rf "$R/gpurun_out/$out/l2_b$b"
         done ;;
+    dmax) run 300 dmax_tests env MIVGPU_WIDEK_DMAX=1 python -u -m pytest tests/test_ops_gpu.py tests/test_skinny_gemm_gpu.py -v $T -k "widek or row_norm or decoder"
+          for d in 0 1 0 1; do
+            MIVGPU_WIDEK_DMAX=$d run 200 "dmax_b32_$d" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 32
+            grep -h ms_per_step "gpurun_out/$out/dmax_b32_$d.log" >> "gpurun_out/$out/dmax_summary.txt"
+          done ;;
     s8temporal) run 400 s8t_exact python -u bench.py --slices 8 --rounds temporal,native \
               --out "gpurun_out/$out/s8t_exact.json" ;;
     unequal) run 500 unequal_tests python -u -m pytest tests/test_shim_gpu.py -v -s $T -k "unequal or charged_the_share" ;;
