@@ -130,6 +130,68 @@ typedef struct {
   uint64_t unused[43];
 } mivgpu_control_t; /* 512 B */
 
+/* Share board (version 1): ONE wave-occupancy sampler per GPU.
+ *
+ * The governor charges a tenant the GPU time it receives: its share of the
+ * resident wavefronts KFD reports per process.  Sampled by every tenant on
+ * its own clock, those shares are not comparable across tenants (each one's
+ * samples land at times correlated with its own work).  The reference
+ * serialises utilisation sampling across containers through the host lock
+ * directory /tmp/vgpulock (pkg/device-plugin/nvidiadevice/nvinternal/plugin/
+ * server.go:853-864); here one owner per GPU reads EVERY process's
+ * cu_occupancy in the same pass and publishes, per KFD pid, the integrals the
+ * tenants charge from:
+ *   obs_ns  -- time over passes in which the process was not sitting in a
+ *              governor gate (cu_occupancy 0 or > one CU unit),
+ *   frac_ns -- over the same passes, the integral of its share of the GPU:
+ *              w / W (w = its waves, W = all processes' waves), 1 when no
+ *              process has waves resident (its dispatch gaps are its own),
+ *   recv_ns -- the integral of w / W (GPU time received; utilisation),
+ *   busy_ns -- time with its waves resident.
+ * A tenant charges (delta frac_ns / delta obs_ns) x its own non-held time.
+ *
+ * The owner is the node sampler (mivgpu-boardd, run by the monitor; the
+ * board directory is mounted READ-ONLY into containers, so no tenant can
+ * write its own share) or, where the directory is writable and no node
+ * sampler is live, the shim that holds flock() on <dir>/gpu-<id>.owner.
+ * File: <dir>/gpu-<kfd gpu_id>.board.  Writes are bracketed by `seq`
+ * (odd while a pass writes: a seqlock). */
+#define MIVGPU_BOARD_MAGIC 0x4D495642u /* 'MIVB' */
+#define MIVGPU_BOARD_VERSION 1
+#define MIVGPU_BOARD_SLOTS 64
+#define MIVGPU_BOARD_OWNER_NONE 0
+#define MIVGPU_BOARD_OWNER_NODE 1
+#define MIVGPU_BOARD_OWNER_SHIM 2
+
+typedef struct {
+  int32_t pid;        /* KFD (host) pid, 0 = free slot                        */
+  int32_t occupancy;  /* cu_occupancy at the last pass                        */
+  uint64_t seen_ns;   /* CLOCK_MONOTONIC of the last pass that listed it      */
+  uint64_t obs_ns;
+  uint64_t frac_ns;
+  uint64_t recv_ns;
+  uint64_t busy_ns;
+  uint64_t unused[2];
+} mivgpu_board_slot_t; /* 64 B */
+
+typedef struct {
+  uint32_t magic;
+  int32_t version;
+  int32_t gpu_id;         /* KFD gpu_id of the GPU                            */
+  int32_t owner_kind;     /* MIVGPU_BOARD_OWNER_*                             */
+  int32_t owner_pid;      /* pid of the owner (its own namespace)             */
+  int32_t nslots;         /* slots in use (high-water index + 1)              */
+  uint64_t seq;           /* seqlock                                          */
+  uint64_t beat_ns;       /* CLOCK_MONOTONIC of the last completed pass       */
+  uint64_t period_ns;     /* the owner's current sampling period              */
+  uint64_t passes;
+  uint64_t want_fast_ns;  /* writable boards: a governed tenant's latest ask for fast passes */
+  uint64_t busy_ns;       /* time with any process's waves resident           */
+  uint64_t pass_ns;       /* cost of the last pass                            */
+  uint64_t unused[6];
+  mivgpu_board_slot_t slots[MIVGPU_BOARD_SLOTS];
+} mivgpu_board_t; /* 128 + 4096 B */
+
 /* Field ids understood by mivgpu_abi_offsetof() (exported by libmivgpu.so). */
 enum {
   MIVGPU_F_MAGIC = 0,
@@ -158,6 +220,11 @@ enum {
   MIVGPU_F_CTL_OVER,
   MIVGPU_F_CTL_EXCESS,
   MIVGPU_F_SIZEOF_CTL,
+  MIVGPU_F_BOARD_SEQ,
+  MIVGPU_F_BOARD_BEAT,
+  MIVGPU_F_BOARD_SLOTS,
+  MIVGPU_F_SIZEOF_BOARD,
+  MIVGPU_F_SIZEOF_BOARD_SLOT,
   MIVGPU_F_COUNT
 };
 

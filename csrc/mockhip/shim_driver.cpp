@@ -383,6 +383,12 @@ int main(int argc, char** argv) {
       if (st) (void)st(0, &busy, &held, &gates);
       printf("{\"op\":\"balance\",\"rc\":%d,\"tokens_ns\":%lld,\"received_ns\":%llu,\"held_ns\":%llu,"
              "\"gates\":%llu}\n", rc, t, r, held, gates);
+    } else if (!strcmp(c, "sampler")) {
+      // the sampler's own account (share board, local estimate), as JSON
+      auto f = (int (*)(int, char*, int))dlsym(RTLD_DEFAULT, "mivgpu_sampler_info");
+      static char buf[16384];
+      int n = f ? f(0, buf, (int)sizeof(buf)) : -2;
+      printf("{\"op\":\"sampler\",\"rc\":%d,\"info\":%s}\n", n < 0 ? n : 0, n > 0 ? buf : "null");
     } else if (!strcmp(c, "setenv") || !strcmp(c, "putenv") || !strcmp(c, "unsetenv")) {
       const char* k = argv[++i];
       int rc;

@@ -1,0 +1,309 @@
+// Share board: one wave-occupancy sampler per GPU (ABI in mivgpu/shared_region.h).
+//
+// Shared by the shim (libmivgpu.so: a tenant reads its share from the board
+// and, on a writable board with no live node sampler, may hold the owner
+// role) and the node sampler (mivgpu-boardd, started by the monitor).
+//
+// Reference behaviour replaced: HAMi-core serialises utilisation sampling of
+// all containers on a node through the host lock directory /tmp/vgpulock
+// (pkg/device-plugin/nvidiadevice/nvinternal/plugin/server.go:853-864) so one
+// process samples NVML for everyone.  Here the owner reads every KFD process's
+// cu_occupancy on a GPU in the same pass (~7 us per read on MI355X) and
+// integrates each one's share, so the shares every tenant is charged come from
+// the same instants and sum to the GPU's busy time.
+#ifndef MIVGPU_BOARD_H
+#define MIVGPU_BOARD_H
+
+#include <errno.h>
+#include <fcntl.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/file.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include "mivgpu/shared_region.h"
+
+namespace mivgpu_board {
+
+// A process with at most this many CU units of waves resident is taken to sit
+// in its governor gate (governor.hip: one 64-lane wave per held stream; KFD
+// rounds waves up to whole CUs, so up to 32 held streams read as 1) or to run
+// kernels too small to matter: not contending.
+constexpr int kGateUnits = 1;
+// A slot whose pid has not been listed for this long is freed.
+constexpr uint64_t kSlotStaleNs = 1000000000ull;
+// Passes longer apart than this do not invent history (a stalled owner).
+constexpr uint64_t kMaxDtNs = 100000000ull;
+
+struct Reading {
+  int pid;
+  int v;   // cu_occupancy, < 0 = unreadable this pass
+};
+
+struct Handle {
+  mivgpu_board_t* b = nullptr;
+  int fd = -1;
+  int owner_fd = -1;
+  bool writable = false;
+  bool owner = false;
+  int gpu_id = -1;
+  uint64_t last_pass_ns = 0;   // owner: the previous pass
+  char dir[256] = {0};
+};
+
+// fstat under the shim's glibc floor (glibc_floor.h: fstat became a real
+// symbol in GLIBC_2.33); plain fstat for the node sampler.
+inline int board_fstat(int fd, struct stat* st) {
+#ifdef MIVGPU_GLIBC_FLOOR_H
+  return mivgpu_fstat(fd, st);
+#else
+  return fstat(fd, st);
+#endif
+}
+
+inline void board_path(char* out, size_t n, const char* dir, int gpu_id, const char* ext) {
+  snprintf(out, n, "%s/gpu-%d.%s", dir, gpu_id, ext);
+}
+
+// Create <dir>/gpu-<id>.board if it does not exist: built under a private
+// name and linked into place, so a reader never maps a half-initialised file.
+inline bool create_board(const char* dir, int gpu_id) {
+  if (mkdir(dir, 0777) == 0) (void)chmod(dir, 0777);   // tenants of other uids share it
+  char path[512], tmp[560];
+  board_path(path, sizeof(path), dir, gpu_id, "board");
+  snprintf(tmp, sizeof(tmp), "%s/.gpu-%d.board.%d", dir, gpu_id, (int)getpid());
+  int fd = open(tmp, O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
+  if (fd < 0) return false;
+  (void)fchmod(fd, 0666);
+  bool ok = ftruncate(fd, (off_t)sizeof(mivgpu_board_t)) == 0;
+  if (ok) {
+    mivgpu_board_t init;
+    memset(&init, 0, sizeof(init));
+    init.magic = MIVGPU_BOARD_MAGIC;
+    init.version = MIVGPU_BOARD_VERSION;
+    init.gpu_id = gpu_id;
+    ok = pwrite(fd, &init, sizeof(init), 0) == (ssize_t)sizeof(init);
+  }
+  close(fd);
+  if (ok && link(tmp, path) != 0 && errno != EEXIST) ok = false;
+  unlink(tmp);
+  return ok;
+}
+
+// Map the board of KFD GPU `gpu_id` in `dir`: read-write where the directory
+// allows it (a shim may then become the owner), read-only otherwise (the
+// production mount: only the node sampler writes).
+inline bool open_board(Handle& h, const char* dir, int gpu_id, bool may_create) {
+  if (!dir || !*dir || gpu_id < 0) return false;
+  char path[512];
+  board_path(path, sizeof(path), dir, gpu_id, "board");
+  int fd = open(path, O_RDWR | O_CLOEXEC);
+  bool writable = fd >= 0;
+  if (fd < 0 && errno == ENOENT && may_create && create_board(dir, gpu_id)) {
+    fd = open(path, O_RDWR | O_CLOEXEC);
+    writable = fd >= 0;
+  }
+  if (fd < 0) {
+    fd = open(path, O_RDONLY | O_CLOEXEC);
+    writable = false;
+  }
+  if (fd < 0) return false;
+  struct stat st;
+  if (board_fstat(fd, &st) != 0 || (size_t)st.st_size < sizeof(mivgpu_board_t)) {
+    close(fd);
+    return false;
+  }
+  void* m = mmap(nullptr, sizeof(mivgpu_board_t), PROT_READ | (writable ? PROT_WRITE : 0), MAP_SHARED, fd, 0);
+  if (m == MAP_FAILED) {
+    close(fd);
+    return false;
+  }
+  mivgpu_board_t* b = static_cast<mivgpu_board_t*>(m);
+  if (b->magic != MIVGPU_BOARD_MAGIC || b->version != MIVGPU_BOARD_VERSION || b->gpu_id != gpu_id) {
+    munmap(m, sizeof(mivgpu_board_t));
+    close(fd);
+    return false;
+  }
+  h.b = b;
+  h.fd = fd;
+  h.writable = writable;
+  h.gpu_id = gpu_id;
+  snprintf(h.dir, sizeof(h.dir), "%s", dir);
+  return true;
+}
+
+inline bool node_owner_live(const mivgpu_board_t* b, int self_pid, uint64_t now) {
+  const int kind = __atomic_load_n(&b->owner_kind, __ATOMIC_ACQUIRE);
+  const uint64_t beat = __atomic_load_n(&b->beat_ns, __ATOMIC_ACQUIRE);
+  return kind == MIVGPU_BOARD_OWNER_NODE && __atomic_load_n(&b->owner_pid, __ATOMIC_RELAXED) != self_pid &&
+         beat + 1000000000ull > now;
+}
+
+// Shim side: take the owner role with a non-blocking flock on
+// <dir>/gpu-<id>.owner (released by the kernel when the process dies).
+inline bool try_own(Handle& h, int self_pid, uint64_t now) {
+  if (!h.b || !h.writable || h.owner) return h.owner;
+  if (node_owner_live(h.b, self_pid, now)) return false;
+  if (h.owner_fd < 0) {
+    char path[512];
+    board_path(path, sizeof(path), h.dir, h.gpu_id, "owner");
+    h.owner_fd = open(path, O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+    if (h.owner_fd < 0) return false;
+    (void)fchmod(h.owner_fd, 0666);
+  }
+  if (flock(h.owner_fd, LOCK_EX | LOCK_NB) != 0) return false;
+  h.owner = true;
+  h.last_pass_ns = 0;
+  __atomic_store_n(&h.b->owner_pid, self_pid, __ATOMIC_RELAXED);
+  __atomic_store_n(&h.b->owner_kind, (int32_t)MIVGPU_BOARD_OWNER_SHIM, __ATOMIC_RELEASE);
+  return true;
+}
+
+inline void release_own(Handle& h) {
+  if (!h.owner) return;
+  h.owner = false;
+  if (h.owner_fd >= 0) (void)flock(h.owner_fd, LOCK_UN);
+}
+
+// How a pass splits the GPU among the processes with waves resident: by
+// their waves (default), or equally (A/B).
+enum Split { kSplitRatio = 0, kSplitEqual = 1 };
+
+// One owner pass over `n` readings (every KFD process on the GPU, this pass).
+// Call with h.owner (or from the node sampler); `kind`/`owner_pid` go to the
+// header.
+inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_t period_ns, int kind,
+                       int owner_pid, int split, uint64_t pass_cost_ns) {
+  mivgpu_board_t* b = h.b;
+  if (!b || !h.writable) return;
+  uint64_t dt = h.last_pass_ns && now > h.last_pass_ns ? now - h.last_pass_ns : 0;
+  if (dt > kMaxDtNs) dt = kMaxDtNs;
+  h.last_pass_ns = now;
+  long W = 0;
+  int resident = 0;
+  for (int i = 0; i < n; ++i)
+    if (r[i].v > kGateUnits) {
+      W += r[i].v;
+      ++resident;
+    }
+  const uint64_t s0 = __atomic_load_n(&b->seq, __ATOMIC_RELAXED);
+  __atomic_store_n(&b->seq, s0 | 1ull, __ATOMIC_RELAXED);
+  __atomic_thread_fence(__ATOMIC_RELEASE);
+  int hi = __atomic_load_n(&b->nslots, __ATOMIC_RELAXED);
+  if (hi < 0 || hi > MIVGPU_BOARD_SLOTS) hi = MIVGPU_BOARD_SLOTS;
+  for (int i = 0; i < n; ++i) {
+    if (r[i].pid <= 0 || r[i].v < 0) continue;
+    int slot = -1, free_slot = -1;
+    for (int k = 0; k < MIVGPU_BOARD_SLOTS; ++k) {
+      const int p = b->slots[k].pid;
+      if (p == r[i].pid) {
+        slot = k;
+        break;
+      }
+      if (free_slot < 0 && (p == 0 || b->slots[k].seen_ns + kSlotStaleNs < now)) free_slot = k;
+    }
+    if (slot < 0) {
+      if (free_slot < 0) continue;   // more than 64 processes on one GPU: the rest go unboarded
+      slot = free_slot;
+      mivgpu_board_slot_t& s = b->slots[slot];
+      memset(&s, 0, sizeof(s));
+      s.pid = r[i].pid;
+      if (slot + 1 > hi) hi = slot + 1;
+    }
+    mivgpu_board_slot_t& s = b->slots[slot];
+    const int v = r[i].v;
+    const long w = v > kGateUnits ? v : 0;
+    s.occupancy = v;
+    s.seen_ns = now;
+    if (!dt) continue;
+    double f, got;
+    if (W > 0) {
+      got = split == kSplitEqual ? (w > 0 ? 1.0 / (double)resident : 0.0) : (double)w / (double)W;
+      f = got;
+    } else {
+      got = 0.0;
+      f = 1.0;   // nobody resident: a process owing work is alone between its own kernels
+    }
+    const bool gated = v > 0 && v <= kGateUnits;
+    if (!gated) {
+      s.obs_ns += dt;
+      s.frac_ns += (uint64_t)(f * (double)dt + 0.5);
+    }
+    s.recv_ns += (uint64_t)(got * (double)dt + 0.5);
+    if (w > 0) s.busy_ns += dt;
+  }
+  // slots of processes gone for a while are freed (a new process may get the pid)
+  for (int k = 0; k < hi; ++k)
+    if (b->slots[k].pid && b->slots[k].seen_ns + kSlotStaleNs < now) memset(&b->slots[k], 0, sizeof(b->slots[k]));
+  while (hi > 0 && b->slots[hi - 1].pid == 0) --hi;
+  b->nslots = hi;
+  if (W > 0) b->busy_ns += dt;
+  b->passes += 1;
+  b->period_ns = period_ns;
+  b->pass_ns = pass_cost_ns;
+  b->owner_pid = owner_pid;
+  b->owner_kind = kind;
+  __atomic_store_n(&b->beat_ns, now, __ATOMIC_RELAXED);
+  __atomic_store_n(&b->seq, (s0 | 1ull) + 1ull, __ATOMIC_RELEASE);
+}
+
+struct View {
+  int owner_kind = 0;
+  int owner_pid = 0;
+  int occupancy = 0;
+  uint64_t beat_ns = 0;
+  uint64_t period_ns = 0;
+  uint64_t passes = 0;
+  uint64_t obs_ns = 0;
+  uint64_t frac_ns = 0;
+  uint64_t recv_ns = 0;
+  uint64_t busy_ns = 0;
+};
+
+// Seqlock read of `pid`'s slot; `hint` caches its index.  False when the pid
+// has no slot or the owner kept writing.
+inline bool read_slot(const mivgpu_board_t* b, int pid, int* hint, View* out) {
+  if (!b || pid <= 0) return false;
+  for (int attempt = 0; attempt < 8; ++attempt) {
+    const uint64_t s1 = __atomic_load_n(&b->seq, __ATOMIC_ACQUIRE);
+    if (s1 & 1ull) {
+      usleep(1);
+      continue;
+    }
+    int k = (hint && *hint >= 0 && *hint < MIVGPU_BOARD_SLOTS && b->slots[*hint].pid == pid) ? *hint : -1;
+    if (k < 0)
+      for (int i = 0; i < MIVGPU_BOARD_SLOTS; ++i)
+        if (b->slots[i].pid == pid) {
+          k = i;
+          break;
+        }
+    View v;
+    v.owner_kind = b->owner_kind;
+    v.owner_pid = b->owner_pid;
+    v.beat_ns = b->beat_ns;
+    v.period_ns = b->period_ns;
+    v.passes = b->passes;
+    if (k >= 0) {
+      const mivgpu_board_slot_t& s = b->slots[k];
+      v.occupancy = s.occupancy;
+      v.obs_ns = s.obs_ns;
+      v.frac_ns = s.frac_ns;
+      v.recv_ns = s.recv_ns;
+      v.busy_ns = s.busy_ns;
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    if (__atomic_load_n(&b->seq, __ATOMIC_RELAXED) != s1) continue;
+    if (k < 0) return false;
+    if (hint) *hint = k;
+    *out = v;
+    return true;
+  }
+  return false;
+}
+
+}  // namespace mivgpu_board
+
+#endif  // MIVGPU_BOARD_H

@@ -63,6 +63,7 @@
 #include <vector>
 
 #include "mivgpu/shared_region.h"
+#include "board.h"
 
 #define MIVGPU_EXPORT extern "C" __attribute__((visibility("default")))
 
@@ -247,16 +248,28 @@ MIVGPU_NO_SANITIZE void* libc_sym(const char* name) {
   return nullptr;
 }
 
+// The shim's own dynamic section (linker-provided): identifies its link_map entry.
+extern "C" ElfW(Dyn) _DYNAMIC[];
+
 // Last resort when no libc/libdl dlsym is found (never on a glibc system):
-// look `name` up in the loaded objects ourselves -- every object for the
-// pseudo-handles, the handle's own map otherwise (a glibc handle IS its
-// link_map) -- so lookups keep working, unversioned, instead of aborting.
+// look `name` up in the loaded objects ourselves -- every object for
+// RTLD_DEFAULT, the objects AFTER the shim for RTLD_NEXT (from the head, the
+// preloaded shim's own hooks would be found first and resolve() would bind
+// the real entry points to themselves), the handle's own map
+// otherwise (a glibc handle IS its link_map) -- so lookups keep working,
+// unversioned, instead of aborting.
 MIVGPU_NO_SANITIZE void* fallback_dlsym(void* handle, const char* name) {
   if (handle && handle != RTLD_DEFAULT && handle != RTLD_NEXT) {
     const struct link_map* m = static_cast<const struct link_map*>(handle);
     return elf_lookup_in(m->l_addr, m->l_ld, name);
   }
-  for (const struct link_map* m = _r_debug.r_map; m; m = m->l_next)
+  const struct link_map* m = _r_debug.r_map;
+  if (handle == RTLD_NEXT) {
+    while (m && m->l_ld != _DYNAMIC) m = m->l_next;
+    if (!m) return nullptr;   // the shim is not in the link map: nothing is "next"
+    m = m->l_next;
+  }
+  for (; m; m = m->l_next)
     if (void* p = elf_lookup_in(m->l_addr, m->l_ld, name)) return p;
   return nullptr;
 }
@@ -465,6 +478,13 @@ struct Config {
   bool share_instant = false;
   bool share_ratio = false;
   char kfd_sysfs[256] = "/sys/class/kfd/kfd";
+  // The GPU's share board directory (board.h; grant key MIVGPU_BOARD_DIR,
+  // "none" = off).  Default /tmp/mivgpu-board, or off when KFD sysfs is
+  // redirected (tests: a fake KFD must not meet a real GPU's board).
+  char board_dir[256] = "/tmp/mivgpu-board";
+  // MIVGPU_BOARD_SPLIT=equal (A/B): a board owner splits each pass equally
+  // among the processes with waves resident instead of by their waves
+  int board_split = 0;
   uint64_t gate_min_interval_ns = 200000;  // >= 200 us of host submission per gate
   bool gate_trace = false;                 // gates also write their trace ring (mivgpu_gate_trace)
   int64_t gate_cap_ns = 100000000;         // 100 ms burst (absorbs share-measurement noise)
@@ -608,7 +628,7 @@ bool is_grant_key(const char* key) {
                                       "MIVGPU_ACCOUNT_CONTEXT", "ROCR_VISIBLE_DEVICES", "MIVGPU_KFD_SYSFS",
                                       "MIVGPU_OCCUPANCY", "MIVGPU_OCC_PERIOD_US", "MIVGPU_GATE_INTERVAL_US",
                                       "MIVGPU_GATE_BURST_US", "MIVGPU_SHARE_TAU_MS", "GPU_MAX_HW_QUEUES",
-                                      "MIVGPU_GATE_MAX_HOLD_US", "MIVGPU_CONTROL_FILE"};
+                                      "MIVGPU_GATE_MAX_HOLD_US", "MIVGPU_CONTROL_FILE", "MIVGPU_BOARD_DIR"};
   for (const char* k : kKeys)
     if (!strcmp(key, k)) return true;
   return !strncmp(key, "HIP_DEVICE_MEMORY_LIMIT_", 24) || !strncmp(key, "HIP_DEVICE_CORE_LIMIT_", 22);
@@ -687,7 +707,14 @@ void load_config() {
   const char* crm = unguarded_env("MIVGPU_CONTEXT_REFRESH_MS");
   if (crm && *crm) g_cfg.context_refresh_ns = (uint64_t)atoll(crm) * 1000000ull;
   const char* kfd = grant_env("MIVGPU_KFD_SYSFS");
-  if (kfd && *kfd) snprintf(g_cfg.kfd_sysfs, sizeof(g_cfg.kfd_sysfs), "%s", kfd);
+  if (kfd && *kfd) {
+    snprintf(g_cfg.kfd_sysfs, sizeof(g_cfg.kfd_sysfs), "%s", kfd);
+    g_cfg.board_dir[0] = 0;
+  }
+  const char* bd = grant_env("MIVGPU_BOARD_DIR");
+  if (bd) snprintf(g_cfg.board_dir, sizeof(g_cfg.board_dir), "%s", strcmp(bd, "none") ? bd : "");
+  const char* bs = unguarded_env("MIVGPU_BOARD_SPLIT");
+  g_cfg.board_split = bs && !strcmp(bs, "equal") ? mivgpu_board::kSplitEqual : mivgpu_board::kSplitRatio;
   const char* gt = getenv("MIVGPU_GATE_TRACE");
   g_cfg.gate_trace = gt && (!strcmp(gt, "1") || !strcasecmp(gt, "true"));
   const char* gi = grant_env("MIVGPU_GATE_INTERVAL_US");
@@ -1026,7 +1053,11 @@ inline int core_policy() {
 // The monitor's contention switch (feedback.go:74-134): from the control file
 // when there is one, else from the region.
 inline int util_switch() {
-  if (g_ctl) return ctl_live() ? __atomic_load_n(&g_ctl->utilization_switch, __ATOMIC_RELAXED) : 0;
+  if (g_ctl) {
+    // the flag first: the lease check (a clock read) only when it is set
+    const int sw = __atomic_load_n(&g_ctl->utilization_switch, __ATOMIC_RELAXED);
+    return sw && ctl_live() ? sw : 0;
+  }
   return g_region ? __atomic_load_n(&g_region->utilization_switch, __ATOMIC_RELAXED) : 0;
 }
 
@@ -1710,17 +1741,17 @@ struct OccPeer {
   int fd;
   uint64_t busy_ns;   // last sample that saw waves of it resident (beyond a gate wave)
   int v;              // its reading this sample
-  bool held;          // this sample saw only its gate wave: held, not contending
   double avg;         // EWMA of its readings over this process's owing samples
 };
 // Busy peers whose average resident waves are within this factor of this
 // process's own (either way) contend as equals; a peer this many times
 // lighter is ignored, one this many times heavier is shared with by ratio.
 constexpr double kContendFrac = 0.1;
-// A peer is busy for this long after its last sample with waves resident.
+// Local estimate (no live share board): a peer is busy for this long after
+// its last sample with waves resident.
 constexpr uint64_t kPeerBusyNs = 200000000ull;   // 200 ms
-// Up to this many recently busy peers, contention is decided per sample.
-constexpr int kFewPeers = 3;
+// A board whose owner has not completed a pass for this long is not used.
+constexpr uint64_t kBoardStaleNs = 50000000ull;   // 50 ms
 // Idle time after which the host bucket stops accruing entitlement.
 constexpr uint64_t kAccrueIdleNs = 20000000ull;   // 20 ms
 // A governed peer held behind its gate has exactly its gate kernel's wave
@@ -1758,6 +1789,19 @@ struct OccDev {
   // published after its interval) carried into the next interval
   int64_t held_prev[64] = {};
   double held_carry = 0;
+  // share board (board.h): the GPU's one sampler
+  mivgpu_board::Handle board;
+  uint64_t board_open_ns = 0;  // last attempt to map it
+  uint64_t board_try_ns = 0;   // last attempt to take the owner role
+  uint64_t board_wave_ns = 0;  // owner: last pass with any process's waves resident
+  int board_hint = -1;
+  bool board_prev_ok = false;
+  uint64_t board_prev_obs = 0, board_prev_frac = 0;
+  double board_share = -1;     // the board's mean share over the latest observed interval
+  mivgpu_board::View board_view;
+  uint64_t board_charged = 0;  // samples charged from the board / from the local estimate
+  uint64_t local_charged = 0;
+  std::vector<mivgpu_board::Reading> readings;
 };
 // Background stamper idle threshold and the batch bounds (see stamper_main
 // and maybe_gate below).
@@ -1807,12 +1851,74 @@ void occ_rescan(OccDev& o, uint64_t now) {
     for (auto& p : o.peers)
       if (p.pid == pid && p.fd >= 0) { fd = p.fd; busy = p.busy_ns; avg = p.avg; p.fd = -1; break; }
     if (fd < 0) fd = open_occ((int)pid, o.gpu_id);   // no stats_<gpu_id>: not on this GPU
-    if (fd >= 0) next.push_back(OccPeer{(int)pid, fd, busy, 0, false, avg});
+    if (fd >= 0) next.push_back(OccPeer{(int)pid, fd, busy, 0, avg});
   }
   closedir(d);
   for (auto& p : o.peers)
     if (p.fd >= 0) close(p.fd);
   o.peers.swap(next);
+}
+
+std::atomic<bool> g_board_fast{false};   // an owner pass saw waves or a governed tenant asked within 1 s
+
+// The share board of the sampler's GPU: map it (retried every second), hold
+// or give up the owner role, run the owner pass over this sample's readings
+// (this process and every peer on the GPU), then read this process's slot.
+// Returns the mean share over the passes since the previous sample in which
+// this process was not held, or -1 when no live board covers it.
+double board_step(OccDev& o, uint64_t now, int own_raw, bool gating) {
+  namespace mb = mivgpu_board;
+  if (!g_cfg.board_dir[0]) return -1;
+  if (!o.board.b) {
+    if (o.board_open_ns && now - o.board_open_ns < 1000000000ull) return -1;
+    o.board_open_ns = now;
+    if (!mb::open_board(o.board, g_cfg.board_dir, o.gpu_id, true)) return -1;
+    mlog(3, "KFD gpu %d: share board %s/gpu-%d.board mapped %s", o.gpu_id, g_cfg.board_dir, o.gpu_id,
+         o.board.writable ? "read-write" : "read-only");
+  }
+  mivgpu_board_t* b = o.board.b;
+  const int self = o.own_pid;
+  if (o.board.owner) {
+    if (mb::node_owner_live(b, self, now)) {
+      mb::release_own(o.board);
+      mlog(3, "KFD gpu %d: node sampler live, share board owner role released", o.gpu_id);
+    }
+  } else if (o.board.writable && gating && now - o.board_try_ns >= 50000000ull) {
+    o.board_try_ns = now;
+    if (mb::try_own(o.board, self, now)) mlog(3, "KFD gpu %d: share board owner (pid %d)", o.gpu_id, self);
+  }
+  if (o.board.owner) {
+    o.readings.clear();
+    o.readings.push_back(mb::Reading{self, own_raw});
+    for (const auto& p : o.peers) o.readings.push_back(mb::Reading{p.pid, p.v});
+    for (const auto& r : o.readings)
+      if (r.v > mb::kGateUnits) o.board_wave_ns = now;
+    const bool fast = now - o.board_wave_ns < 1000000000ull ||
+                      __atomic_load_n(&b->want_fast_ns, __ATOMIC_RELAXED) + 1000000000ull > now;
+    g_board_fast.store(fast, std::memory_order_relaxed);
+    mb::owner_pass(o.board, o.readings.data(), (int)o.readings.size(), now,
+                   fast ? g_cfg.occ_period_ns : g_cfg.occ_idle_period_ns, MIVGPU_BOARD_OWNER_SHIM, self,
+                   g_cfg.board_split, mono_ns() - now);
+  } else if (o.board.writable && gating) {
+    __atomic_store_n(&b->want_fast_ns, now, __ATOMIC_RELAXED);
+  }
+  mb::View v;
+  if (!mb::read_slot(b, self, &o.board_hint, &v) || v.beat_ns + kBoardStaleNs < now) {
+    o.board_prev_ok = false;
+    return -1;
+  }
+  if (o.board_prev_ok && v.obs_ns >= o.board_prev_obs && v.frac_ns >= o.board_prev_frac) {
+    const uint64_t dobs = v.obs_ns - o.board_prev_obs;
+    if (dobs > 0) {
+      const double f = (double)(v.frac_ns - o.board_prev_frac) / (double)dobs;
+      o.board_share = f > 1.0 ? 1.0 : f;
+    }
+  }
+  o.board_prev_ok = true;
+  o.board_prev_obs = v.obs_ns;
+  o.board_prev_frac = v.frac_ns;
+  o.board_view = v;
+  return o.board_share;
 }
 
 // One sample of device `dev`.  Returns false if the device has no KFD view.
@@ -1841,38 +1947,26 @@ bool occ_sample(int dev, uint64_t now) {
   // wave among them: discounting one CU's worth for peers but not for itself
   // billed every symmetric tenant above 1/N -- measured, 8 x 12 % decode
   // tenants held 27 % of the time).
-  // A peer contends while it has more than a gate's wave resident.  One
-  // showing only its gate wave (held) or nothing this sample does not dilute
-  // this process's charge (measured: a 75 % tenant next to a 25 % one was
-  // charged half of its solo time while the 25 % one sat in its gate, and
-  // settled at 50 % instead of 75 %).  MIVGPU_PEER_BUSY_MS > 0 restores a
-  // window of that many ms after the last sample with waves (the round-3
-  // rule, 200).
-  // With many tenants on the GPU the hardware scheduler time-slices their
-  // queues, and a busy peer often shows no waves in a given sample: there a
-  // peer keeps contending for kPeerBusyNs after its last waves (the round-3
-  // rule).  With few (measured: 8 x
-  // 12 % temporal tenants at 6.0k tok/s per sample, 7.2k with a 50 ms window,
-  // 8.8k with 200 ms; 75 / 25 % tenants charged 76 / 25 per sample, 50 / 25
-  // with 200 ms) every sample decides.
-  int recent_peers = 0;
-  for (auto& p : o.peers)
-    if (p.busy_ns && now - p.busy_ns < kPeerBusyNs) ++recent_peers;
-  const uint64_t window = g_cfg.peer_busy_ns ? g_cfg.peer_busy_ns : (recent_peers > kFewPeers ? kPeerBusyNs : 0);
+  // Local estimate (used only while no share board is live, board.h): a peer
+  // contends while it showed more than a gate's wave within the last 200 ms
+  // (the round-3 rule; MIVGPU_PEER_BUSY_MS sets another window).  Per-sample
+  // decisions made by each tenant on its own clock charged four symmetric
+  // 25 % tenants 100 / 33 / 100 / 100 % of their busy time: a
+  // time-sliced busy peer often shows no waves in a given sample.
+  const uint64_t window = g_cfg.peer_busy_ns ? g_cfg.peer_busy_ns : kPeerBusyNs;
   long others = 0;
   int busy_peers = 0;
   for (auto& p : o.peers) {
     int v = read_occ(p.fd);
     p.v = v > 0 ? v : 0;
-    // per sample: no waves beyond a gate's = not contending; in the crowded
-    // regime one resident wave is as often a running peer's last wave as a
-    // held peer's gate (excluding it held 8 x 12 % tenants back to 7.1k)
-    p.held = window ? false : v <= kGateWaves;
     if (v > 0) others += v;
     if (v > kGateWaves) p.busy_ns = now;
-    if (p.busy_ns && now - p.busy_ns < (window ? window : kPeerBusyNs) && !p.held) ++busy_peers;
+    if (p.busy_ns && now - p.busy_ns < window) ++busy_peers;
   }
   o.window_ns = window;
+  const int own_raw = own;
+  const bool gating = coarse_ns() - g_last_gate_ns[dev].load(std::memory_order_relaxed) < 1000000000ull;
+  const double board_f = board_step(o, now, own_raw, gating);
   // The gate's own resident wave is not consumption: discount one unit per
   // gate slot holding right now.
   DeviceGate& G = g_gates[dev];
@@ -1945,7 +2039,13 @@ bool occ_sample(int dev, uint64_t now) {
   double share = 0.0;
   int state = 4;
   if (owes) {
-    if (g_cfg.share_ratio) {
+    if (board_f >= 0) {
+      // the GPU's one sampler: this process's mean share of the resident
+      // waves over the passes since the previous sample in which it was not
+      // held, taken at the same instants as every other tenant's
+      share = board_f;
+      ++o.board_charged;
+    } else if (g_cfg.share_ratio) {
       const double tot = o.own_avg + o.others_avg;
       share = tot > 0 ? o.own_avg / tot : 1.0 / (double)(1 + busy_peers);
     } else if (g_cfg.share_instant && o.inst_avg >= 0) {
@@ -1954,13 +2054,14 @@ bool occ_sample(int dev, uint64_t now) {
       int comparable = 0;
       double heavier = 0;
       for (const auto& p : o.peers) {
-        if (!p.busy_ns || now - p.busy_ns >= (o.window_ns ? o.window_ns : kPeerBusyNs) || p.held) continue;
+        if (!p.busy_ns || now - p.busy_ns >= o.window_ns) continue;
         if (p.avg * kContendFrac > o.own_avg) heavier += p.avg;
         else if (p.avg >= kContendFrac * o.own_avg) ++comparable;
       }
       const double base = o.own_avg + heavier > 0 ? o.own_avg / (o.own_avg + heavier) : 1.0;
       share = base / (double)(1 + comparable);
     }
+    if (board_f < 0) ++o.local_charged;
     state = own > 0 ? 0 : (others > 0 ? 3 : 1);
   }
   const int mask = (int)cu_mask_of(dev);
@@ -2087,6 +2188,7 @@ void* occ_main(void*) {
     const uint64_t t = coarse_ns();
     bool fast = false;
     for (int d = 0; d < g_num_devices; ++d) fast |= t - g_last_gate_ns[d].load(std::memory_order_relaxed) < 1000000000ull;
+    fast |= g_board_fast.load(std::memory_order_relaxed);   // the GPU's board owner samples for every tenant
     usleep((useconds_t)((fast ? g_cfg.occ_period_ns : g_cfg.occ_idle_period_ns) / 1000));
     std::lock_guard<std::mutex> pass(g_occ_pass_mu);
     if (g_exiting.load(std::memory_order_acquire)) return nullptr;
@@ -2127,8 +2229,7 @@ inline bool gate_wanted(int dev) {
   int policy = core_policy();
   if (policy == 2) return false;
   const uint64_t lim = cu_limit_ppm_of(dev);
-  int sw = util_switch();
-  if (lim == 0 || lim >= 1000000) return false;
+  if (lim == 0 || lim >= 1000000) return false;   // no core limit: no switch or clock read either
   // A CU mask no wider than the limit (within one granule of one CU per XCD:
   // the device plugin rounds grants to whole granules) already enforces it in
   // hardware; time-slicing on top would charge the tenant for a GPU it cannot
@@ -2140,7 +2241,7 @@ inline bool gate_wanted(int dev) {
   if (policy == 1) return true;
   // default: time-slice when there is no mask or the monitor asks for
   // contention enforcement (utilization_switch, feedback.go:74-134)
-  return mask == 0 || sw == 1;
+  return mask == 0 || util_switch() == 1;
 }
 
 // Enqueue one gate on `stream` for slot S (caller holds G.mu, G.ok).
@@ -3251,6 +3352,11 @@ MIVGPU_EXPORT long mivgpu_abi_offsetof(int field) {
     case MIVGPU_F_CTL_OVER: return offsetof(mivgpu_control_t, over_grant);
     case MIVGPU_F_CTL_EXCESS: return offsetof(mivgpu_control_t, host_excess);
     case MIVGPU_F_SIZEOF_CTL: return sizeof(mivgpu_control_t);
+    case MIVGPU_F_BOARD_SEQ: return offsetof(mivgpu_board_t, seq);
+    case MIVGPU_F_BOARD_BEAT: return offsetof(mivgpu_board_t, beat_ns);
+    case MIVGPU_F_BOARD_SLOTS: return offsetof(mivgpu_board_t, slots);
+    case MIVGPU_F_SIZEOF_BOARD: return sizeof(mivgpu_board_t);
+    case MIVGPU_F_SIZEOF_BOARD_SLOT: return sizeof(mivgpu_board_slot_t);
     default: return -1;
   }
 }
@@ -3327,6 +3433,59 @@ MIVGPU_EXPORT int mivgpu_occ_timing(unsigned long long* passes, unsigned long lo
   if (total_ns) *total_ns = g_occ_pass_ns;
   if (max_ns) *max_ns = g_occ_pass_max_ns;
   return 0;
+}
+
+// The sampler's view of `dev` as one JSON object (NUL-terminated, at most n
+// bytes; returns the length or -1): the share board (owner role, owner, the
+// board's age, every process's integrals), the samples charged from the board
+// or the local estimate, the local estimate's peers, the state split.  What a
+// failed governor test prints so the record explains itself.
+MIVGPU_EXPORT int mivgpu_sampler_info(int dev, char* buf, int n) {
+  if (dev < 0 || dev >= MIVGPU_MAX_DEVICES || !buf || n < 64) return -1;
+  std::lock_guard<std::mutex> pass(g_occ_pass_mu);
+  const OccDev& o = g_occ[dev];
+  int len = 0;
+  auto put = [&](const char* fmt, ...) __attribute__((format(printf, 2, 3))) {
+    if (len >= n - 1) return;
+    va_list ap;
+    va_start(ap, fmt);
+    const int w = vsnprintf(buf + len, (size_t)(n - len), fmt, ap);
+    va_end(ap);
+    if (w > 0) len = len + w < n - 1 ? len + w : n - 1;
+  };
+  const uint64_t now = mono_ns();
+  put("{\"live\":%d,\"gpu_id\":%d,\"pid\":%d,\"samples\":%llu,\"board_charged\":%llu,\"local_charged\":%llu,"
+      "\"window_ms\":%.1f,\"share_avg\":%.4f,\"board_share\":%.4f,\"state_ms\":[%.1f,%.1f,%.1f,%.1f,%.1f]",
+      o.live ? 1 : 0, o.gpu_id, o.own_pid, (unsigned long long)o.samples, (unsigned long long)o.board_charged,
+      (unsigned long long)o.local_charged, o.window_ns / 1e6, o.share_avg, o.board_share, o.state_ns[0] / 1e6,
+      o.state_ns[1] / 1e6, o.state_ns[2] / 1e6, o.state_ns[3] / 1e6, o.state_ns[4] / 1e6);
+  put(",\"peers\":[");
+  for (size_t i = 0; i < o.peers.size(); ++i) {
+    const OccPeer& p = o.peers[i];
+    put("%s{\"pid\":%d,\"v\":%d,\"avg\":%.2f,\"busy_age_ms\":%.1f}", i ? "," : "", p.pid, p.v, p.avg,
+        p.busy_ns ? (now - p.busy_ns) / 1e6 : -1.0);
+  }
+  put("],\"board\":");
+  const mivgpu_board_t* b = o.board.b;
+  if (!b) {
+    put("{\"dir\":\"%s\",\"open\":0}}", g_cfg.board_dir);
+    return len;
+  }
+  put("{\"dir\":\"%s\",\"open\":1,\"writable\":%d,\"owner\":%d,\"owner_kind\":%d,\"owner_pid\":%d,"
+      "\"beat_age_ms\":%.2f,\"passes\":%llu,\"period_us\":%.0f,\"busy_ms\":%.1f,\"slots\":[",
+      g_cfg.board_dir, o.board.writable ? 1 : 0, o.board.owner ? 1 : 0, b->owner_kind, b->owner_pid,
+      b->beat_ns ? ((double)now - (double)b->beat_ns) / 1e6 : -1.0, (unsigned long long)b->passes,
+      b->period_ns / 1e3, b->busy_ns / 1e6);
+  bool first = true;
+  for (int k = 0; k < MIVGPU_BOARD_SLOTS; ++k) {
+    const mivgpu_board_slot_t& s = b->slots[k];
+    if (!s.pid) continue;
+    put("%s{\"pid\":%d,\"occ\":%d,\"obs_ms\":%.1f,\"frac_ms\":%.1f,\"recv_ms\":%.1f,\"busy_ms\":%.1f}",
+        first ? "" : ",", s.pid, s.occupancy, s.obs_ns / 1e6, s.frac_ns / 1e6, s.recv_ns / 1e6, s.busy_ns / 1e6);
+    first = false;
+  }
+  put("]}}");
+  return len;
 }
 
 // Copy up to `n` most recent gate trace entries (8 x int64 each) into `out`;

@@ -101,6 +101,9 @@ def slice_env(spec: SliceSpec, physical_gpu: str | None, cache_dir: Path) -> dic
     if spec.shim:
         env.update(shim_env(""))
         env["MIVGPU_SHARED_CACHE"] = str(cache_dir / f"slice{spec.index}.cache")
+        # the GPU's share board (one sampler for every slice): writable, so a
+        # governed slice holds the owner role as on a node without a monitor
+        env["MIVGPU_BOARD_DIR"] = str(cache_dir / "board")
         if spec.gpumem_mib:
             env["HIP_DEVICE_MEMORY_LIMIT_0"] = f"{spec.gpumem_mib}m"
         if spec.core_pct < 100:
@@ -356,6 +359,14 @@ def _governor_stats() -> dict:
               "sampler_pass_us_max"):
         if k in g:
             out["gov_" + k] = g[k]
+    si = g.get("sampler")
+    if si:
+        # how the share was charged: from the GPU's one sampler (board) or the
+        # local estimate, and whose board it was
+        bd = si.get("board") or {}
+        out["sampler"] = {"board_charged": si.get("board_charged"), "local_charged": si.get("local_charged"),
+                          "board_share": si.get("board_share"), "board_owner": bd.get("owner"),
+                          "owner_kind": bd.get("owner_kind"), "board_slots": len(bd.get("slots") or [])}
     cache = os.environ.get("MIVGPU_SHARED_CACHE")
     if cache and os.path.exists(cache):
         from k8s_vgpu_scheduler_amd.monitor.region import SharedRegion

@@ -3,7 +3,9 @@
 Reference: cmd/vGPUmonitor/main.go:57-172, feedback.go, metrics.go.  Validates
 HOOK_PATH, watches this node's pods only (server-side field selector
 spec.nodeName, pkg/monitor/nvidia/cudevshr.go:308) for the container lister,
-samples KFD wave occupancy, serves Prometheus (``--legacy-metrics`` adds the
+samples KFD wave occupancy, runs the node's share-board sampler (one
+occupancy sampler per GPU whose shares the governed tenants are charged,
+monitor/board.py), serves Prometheus (``--legacy-metrics`` adds the
 pre-2.x series), and runs the 5 s feedback loop -- paused while the device
 plugin holds the compute-partition apply lock (main.go:79-109).  Each pass
 also enforces every granted container's HBM from KFD host truth, driven by
@@ -49,8 +51,16 @@ def main(argv=None):
                     help="what happens to a container over its HBM grant (host truth) for --over-grant-passes "
                          "passes: block its launches (control file), evict its pod (Eviction API), or SIGKILL "
                          "its host processes holding VRAM")
+    ap.add_argument("--shimless-action", choices=("none", "evict", "kill"), default=None,
+                    help="a container holding VRAM with no live libmivgpu.so that is over its HBM grant or on a "
+                         "GPU only the governor limits (time-sharing) is evicted / killed after --over-grant-passes "
+                         "passes whatever --over-grant-action says (default: evict; kill under "
+                         "--over-grant-action kill)")
     ap.add_argument("--over-grant-passes", type=int, default=3,
                     help="consecutive over-grant passes before --over-grant-action evict/kill")
+    ap.add_argument("--board-period-us", type=int, default=2000,
+                    help="the node share-board sampler's period while any GPU has waves resident "
+                         "(mivgpu-boardd: one wave-occupancy sampler per GPU for every tenant; 0 = off)")
     ap.add_argument("-v", type=int, default=2)
     a = ap.parse_args(argv)
     setup_logging(a.v)
@@ -68,6 +78,10 @@ def main(argv=None):
         log.warning("no amd-smi backend (%s): host metrics disabled", e)
         backend = None
     occ = OccupancySampler(period_s=a.occupancy_period).start() if a.occupancy_period > 0 else None
+    board = None
+    if a.board_period_us > 0:
+        from k8s_vgpu_scheduler_amd.monitor.board import BoardSampler, board_host_dir
+        board = BoardSampler(board_host_dir(a.hook_path), period_us=a.board_period_us).start()
     truth = escalation = None
     if not a.no_host_truth:
         from k8s_vgpu_scheduler_amd.monitor.escalate import OverGrantPolicy
@@ -75,7 +89,8 @@ def main(argv=None):
         from k8s_vgpu_scheduler_amd.scheduler.events import EventRecorder
         events = EventRecorder(client, component="hami-vgpu-monitor")
         truth = HostTruth(kfd_gpu_ids(backend), events=events)
-        escalation = OverGrantPolicy(a.over_grant_action, a.over_grant_passes, client=client, events=events)
+        escalation = OverGrantPolicy(a.over_grant_action, a.over_grant_passes, client=client, events=events,
+                                     shimless_action=a.shimless_action)
     reg = CollectorRegistry()
     reg.register(MonitorCollector(lister, backend, a.node_name, occupancy=occ, legacy=a.legacy_metrics,
                                   truth=truth, escalation=escalation))
@@ -84,7 +99,11 @@ def main(argv=None):
     stop = threading.Event()
     pause = threading.Event()
     threading.Thread(target=watch_partition_lock, args=(pause, stop), name="partition-lock", daemon=True).start()
-    watch_and_feedback(lister, stop, pause=pause, truth=truth, escalation=escalation)
+    try:
+        watch_and_feedback(lister, stop, pause=pause, truth=truth, escalation=escalation)
+    finally:
+        if board is not None:
+            board.stop()
     return 0
 
 

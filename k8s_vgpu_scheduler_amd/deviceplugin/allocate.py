@@ -48,6 +48,7 @@ import uuid as _uuid
 from dataclasses import dataclass, field
 
 from k8s_vgpu_scheduler_amd.device.codec import format_ranges, ranges_count
+from k8s_vgpu_scheduler_amd.monitor.board import CONTAINER_BOARD_DIR, board_host_dir
 from k8s_vgpu_scheduler_amd.monitor.control import CONTAINER_CONTROL_PATH, control_host_path
 from k8s_vgpu_scheduler_amd.monitor.control import create as create_control
 
@@ -58,7 +59,8 @@ GRANT_KEYS = ("HIP_DEVICE_MEMORY_LIMIT", "HIP_DEVICE_CORE_LIMIT", "HSA_CU_MASK",
               "HIP_TASK_PRIORITY", "MIVGPU_OVERSUBSCRIBE", "MIVGPU_SHARED_CACHE", "MIVGPU_DEVICE_UUIDS",
               "ROCR_VISIBLE_DEVICES", "MIVGPU_ACCOUNT_CONTEXT", "MIVGPU_KFD_SYSFS", "MIVGPU_OCCUPANCY",
               "MIVGPU_OCC_PERIOD_US", "MIVGPU_GATE_INTERVAL_US", "MIVGPU_GATE_BURST_US", "MIVGPU_SHARE_TAU_MS",
-              "MIVGPU_DISABLE_CONTROL", "GPU_MAX_HW_QUEUES", "MIVGPU_GATE_MAX_HOLD_US", "MIVGPU_CONTROL_FILE")
+              "MIVGPU_DISABLE_CONTROL", "GPU_MAX_HW_QUEUES", "MIVGPU_GATE_MAX_HOLD_US", "MIVGPU_CONTROL_FILE",
+              "MIVGPU_BOARD_DIR")
 # per-device forms of grant keys (HIP_DEVICE_MEMORY_LIMIT_<i>, HIP_DEVICE_CORE_LIMIT_<i>)
 GRANT_PREFIXES = ("HIP_DEVICE_MEMORY_LIMIT_", "HIP_DEVICE_CORE_LIMIT_")
 
@@ -173,6 +175,8 @@ def container_env(devreq: list, gpus: dict, cfg: PluginConfig, cache_file: str) 
                 env[f"HIP_DEVICE_CORE_LIMIT_{i}"] = str(p)
     env["MIVGPU_SHARED_CACHE"] = cache_file
     env["MIVGPU_CONTROL_FILE"] = CONTAINER_CONTROL_PATH
+    # the GPU's share board, written by the node sampler only (read-only mount)
+    env["MIVGPU_BOARD_DIR"] = CONTAINER_BOARD_DIR
     env["MIVGPU_DEVICE_UUIDS"] = ",".join(d.uuid for d in devreq)
     if cfg.device_memory_scaling > 1:
         env["MIVGPU_OVERSUBSCRIBE"] = "true"
@@ -213,11 +217,13 @@ def allocate_container(pod: dict, ctr: dict, devreq: list, gpus: dict, cfg: Plug
         os.chmod(tmp, 0o444)
         os.replace(tmp, limits)
         create_control(control)
+        os.makedirs(board_host_dir(hook), exist_ok=True)
     mounts = [
         {"container_path": CONTAINER_LIB, "host_path": f"{hook}/vgpu/libmivgpu.so", "read_only": True},
         {"container_path": f"{hook}/vgpu", "host_path": host_dir, "read_only": False},
         {"container_path": LIMITS_PATH, "host_path": limits, "read_only": True},
         {"container_path": CONTAINER_CONTROL_PATH, "host_path": control, "read_only": True},
+        {"container_path": CONTAINER_BOARD_DIR, "host_path": board_host_dir(hook), "read_only": True},
     ]
     # the pod-spec opt-out drops the preload -- only where opting out is allowed
     # (a fractional pod would otherwise escape every limit; the webhook also

@@ -191,7 +191,7 @@ def container_env(alloc: dict, base: dict | None = None) -> dict:
     env = dict(base if base is not None else os.environ)
     env.update(alloc["envs"])
     mounts = alloc["mounts"]
-    for k in ("MIVGPU_SHARED_CACHE", "MIVGPU_CONTROL_FILE"):
+    for k in ("MIVGPU_SHARED_CACHE", "MIVGPU_CONTROL_FILE", "MIVGPU_BOARD_DIR"):
         if k in env:
             env[k] = host_path(env[k], mounts)
     from k8s_vgpu_scheduler_amd.deviceplugin.allocate import LIMITS_PATH, grant_text, parse_grant
@@ -200,7 +200,7 @@ def container_env(alloc: dict, base: dict | None = None) -> dict:
         # the shim reads the grant from the read-only mount; on the host the
         # same file (with its region path mapped) is named by MIVGPU_LIMITS_FILE
         g = parse_grant(Path(grant["host_path"]).read_text())
-        for k in ("MIVGPU_SHARED_CACHE", "MIVGPU_CONTROL_FILE"):
+        for k in ("MIVGPU_SHARED_CACHE", "MIVGPU_CONTROL_FILE", "MIVGPU_BOARD_DIR"):
             if k in g:
                 g[k] = host_path(g[k], mounts)
         hp = Path(grant["host_path"] + ".host")

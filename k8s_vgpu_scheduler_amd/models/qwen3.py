@@ -5,13 +5,14 @@ The reference's only benchmark is vLLM serving Qwen3-8B bf16 at TP=1
 slice vs. natively.  This module is the MI355X-native stand-in for that
 workload: a Qwen3-8B-shaped decoder (GQA 32q/8kv x 128, per-head QK RMSNorm,
 NeoX RoPE theta 1e6, SwiGLU 12288, vocab 151936) whose decode step runs
-  * the weight-streaming projections (gate_up with SiLU*up fused into its
-    epilogue, down, lm_head; o_proj inside a CU partition of <= 96 CUs, qkv
-    in one of <= 160) on the hand-written skinny MFMA GEMM
-    (csrc/ops/skinny_gemm.hip, wide workgroups sharing an LDS X tile) over
-    fragment-packed weights, for batch <= 32;
-  * qkv and o_proj on the whole chip on hipBLASLt (``F.linear``), where the
-    library is faster at these 33-50 MB shapes (profiles/gemm_wide_*, cu128/);
+  * every weight-streaming projection of the decode step (qkv, o_proj,
+    gate_up with SiLU*up fused into its epilogue, down, lm_head) on the
+    hand-written skinny MFMA GEMM (csrc/ops/skinny_gemm.hip) over
+    fragment-packed weights, for batch <= 32: the wide variant (workgroups
+    sharing an LDS X tile) for gate_up / down / lm_head, the K-split variant
+    (skinny_widek_kernel) for qkv and o_proj (the kernel trace,
+    profiles/round4/bench/decode_trace_b32.json);
+  * the prompt (prefill) projections on hipBLASLt (``F.linear``);
   * every other op on the hand-written gfx950 kernels of libmivgpu_ops.so,
   * the whole step captured in one hipGraph (launch overhead -> one replay).
 No network: weights are random normal(0, 0.02) of the exact architecture.
@@ -89,6 +90,18 @@ class Qwen3Weights:
             ))
         self.final_norm = ones(h)
         self.lm_head = self.embed if cfg.tie_embeddings else rnd(cfg.vocab, h)
+
+
+def _gpu_shared() -> bool:
+    """This process runs on part of a GPU: a CU mask, or a core limit the
+    temporal governor enforces (the device plugin's grant)."""
+    if os.environ.get("HSA_CU_MASK"):
+        return True
+    lim = os.environ.get("HIP_DEVICE_CORE_LIMIT", "")
+    try:
+        return bool(lim) and 0 < float(lim) < 100
+    except ValueError:
+        return False
 
 
 class Qwen3Decoder:
@@ -231,6 +244,14 @@ class Qwen3Decoder:
         # their own 4-wave K-split launches).
         self.chain_mode = os.environ.get("MIVGPU_CHAIN", "0")
         self.chain = self.norm_fused and batch <= 32 and self.chain_mode in ("1", "gd")
+        if self.chain and _gpu_shared():
+            # the chain's workgroups wait in-kernel for their producers: on a
+            # CU-masked or time-shared GPU they may never be co-resident, the
+            # kernel gives up after its spin timeout and the step is wrong
+            # (ADVICE r4), so it is refused there
+            import warnings
+            warnings.warn("MIVGPU_CHAIN ignored: the GPU is partitioned or time-shared (HSA_CU_MASK / core limit)")
+            self.chain = False
         self.chain_w = int(os.environ.get("MIVGPU_CHAIN_W", "2"))
         self.chain_down_s = int(os.environ.get("MIVGPU_CHAIN_DOWN_S", "4"))
         if self.norm_fused:
@@ -725,5 +746,11 @@ class Qwen3Decoder:
     def step(self):
         if self.graph is not None:
             self.graph.replay()
-            return None
-        return self._step_impl()
+            out = None
+        else:
+            out = self._step_impl()
+        if self.chain and any(c.gave_up() for c in self._chains[:1]):
+            # a chain that timed out left wrong projections: never return them
+            raise RuntimeError("decode chain gave up waiting for its producers (workgroups not co-resident); "
+                               "run without MIVGPU_CHAIN")
+        return out

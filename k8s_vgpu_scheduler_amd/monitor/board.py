@@ -1,0 +1,181 @@
+"""Share boards: one wave-occupancy sampler per GPU (monitor side).
+
+ctypes mirror of ``mivgpu_board_t`` (csrc/include/mivgpu/shared_region.h,
+owner logic in csrc/shim/board.h) plus the node sampler's process.
+
+The governor charges a tenant the GPU time it receives: its share of the
+resident wavefronts KFD reports per process.  When each tenant sampled that
+on its own clock, four symmetric 25 % tenants were charged 100 / 33 / 100 /
+100 % of their busy time.  The reference serialises
+utilisation sampling across containers through the host lock directory
+``/tmp/vgpulock`` (pkg/device-plugin/nvidiadevice/nvinternal/plugin/
+server.go:853-864); here ONE owner per GPU reads every process's
+``cu_occupancy`` in the same pass and publishes per-pid integrals in
+``<board dir>/gpu-<kfd gpu_id>.board``:
+
+* production: the monitor runs ``mivgpu-boardd`` (``BoardSampler``) on
+  ``$HOOK_PATH/vgpu/board``, which the device plugin mounts READ-ONLY into
+  every vGPU container (``deviceplugin/allocate.py``) -- no tenant can write
+  the share it is charged;
+* without a node sampler (hand-run slices, the bench), a shim that governs
+  the GPU takes the owner role with ``flock`` on ``gpu-<id>.owner``.
+
+The monitor also reads the boards for per-process utilisation (``recv_ns``).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import logging
+import mmap
+import os
+import subprocess
+import time
+from pathlib import Path
+
+BOARD_MAGIC = 0x4D495642
+BOARD_VERSION = 1
+BOARD_SLOTS = 64
+OWNER_NONE, OWNER_NODE, OWNER_SHIM = 0, 1, 2
+CONTAINER_BOARD_DIR = "/var/run/mivgpu/board"    # the grant's MIVGPU_BOARD_DIR (read-only mount)
+
+log = logging.getLogger("mivgpu.board")
+
+
+class BoardSlot(C.Structure):
+    _fields_ = [("pid", C.c_int32), ("occupancy", C.c_int32), ("seen_ns", C.c_uint64), ("obs_ns", C.c_uint64),
+                ("frac_ns", C.c_uint64), ("recv_ns", C.c_uint64), ("busy_ns", C.c_uint64),
+                ("unused", C.c_uint64 * 2)]
+
+
+class BoardHeader(C.Structure):
+    _fields_ = [("magic", C.c_uint32), ("version", C.c_int32), ("gpu_id", C.c_int32), ("owner_kind", C.c_int32),
+                ("owner_pid", C.c_int32), ("nslots", C.c_int32), ("seq", C.c_uint64), ("beat_ns", C.c_uint64),
+                ("period_ns", C.c_uint64), ("passes", C.c_uint64), ("want_fast_ns", C.c_uint64),
+                ("busy_ns", C.c_uint64), ("pass_ns", C.c_uint64), ("unused", C.c_uint64 * 6),
+                ("slots", BoardSlot * BOARD_SLOTS)]
+
+
+BOARD_SIZE = C.sizeof(BoardHeader)
+assert C.sizeof(BoardSlot) == 64 and BOARD_SIZE == 128 + 64 * BOARD_SLOTS
+
+
+def offsets() -> dict:
+    """Field offsets for the ABI test against mivgpu_abi_offsetof()."""
+    # MIVGPU_F_BOARD_SEQ .. MIVGPU_F_SIZEOF_BOARD_SLOT (enum order in shared_region.h)
+    return {26: BoardHeader.seq.offset, 27: BoardHeader.beat_ns.offset, 28: BoardHeader.slots.offset,
+            29: BOARD_SIZE, 30: C.sizeof(BoardSlot)}
+
+
+def board_path(board_dir: str, gpu_id: int) -> Path:
+    return Path(board_dir) / f"gpu-{gpu_id}.board"
+
+
+def board_host_dir(hook_path: str) -> str:
+    return f"{hook_path}/vgpu/board"
+
+
+class Board:
+    """One GPU's board mapped read-only (monitor, tests)."""
+
+    def __init__(self, path):
+        self.path = str(path)
+        fd = os.open(self.path, os.O_RDONLY | os.O_CLOEXEC)
+        try:
+            if os.fstat(fd).st_size < BOARD_SIZE:
+                raise ValueError(f"{path}: not a share board")
+            self.mm = mmap.mmap(fd, BOARD_SIZE, mmap.MAP_SHARED, mmap.PROT_READ)
+        finally:
+            os.close(fd)
+        h = BoardHeader.from_buffer_copy(self.mm)
+        if h.magic != BOARD_MAGIC or h.version != BOARD_VERSION:
+            self.mm.close()
+            raise ValueError(f"{path}: bad board magic/version")
+
+    def close(self):
+        self.mm.close()
+
+    def snapshot(self, tries: int = 50) -> BoardHeader:
+        """A consistent copy (seqlock: retried while the owner writes)."""
+        off = BoardHeader.seq.offset
+        for _ in range(tries):
+            s1 = int.from_bytes(self.mm[off:off + 8], "little")
+            if s1 & 1:
+                time.sleep(0.0001)
+                continue
+            h = BoardHeader.from_buffer_copy(self.mm)
+            if h.seq == s1:
+                return h
+        return BoardHeader.from_buffer_copy(self.mm)
+
+    def slots(self) -> dict[int, BoardSlot]:
+        h = self.snapshot()
+        return {s.pid: s for s in h.slots if s.pid}
+
+    def live(self, max_age_s: float = 0.05) -> bool:
+        h = self.snapshot()
+        return h.beat_ns > 0 and time.monotonic_ns() - h.beat_ns < max_age_s * 1e9
+
+
+def shares(before: BoardHeader, after: BoardHeader) -> dict[int, dict]:
+    """Per pid between two snapshots: the mean share charged while not held
+    (frac / obs) and the share of the window received (recv / wall)."""
+    b = {s.pid: s for s in before.slots if s.pid}
+    wall = max(1, after.beat_ns - before.beat_ns)
+    out = {}
+    for s in after.slots:
+        if not s.pid:
+            continue
+        p = b.get(s.pid)
+        obs = s.obs_ns - (p.obs_ns if p else 0)
+        frac = s.frac_ns - (p.frac_ns if p else 0)
+        recv = s.recv_ns - (p.recv_ns if p else 0)
+        out[s.pid] = {"charged_share": frac / obs if obs > 0 else None, "received": recv / wall,
+                      "obs_ms": obs / 1e6, "occupancy": s.occupancy}
+    return out
+
+
+def boardd_path() -> Path:
+    return Path(__file__).resolve().parents[1] / "lib" / "mivgpu-boardd"
+
+
+class BoardSampler:
+    """The node sampler process (``mivgpu-boardd``), owned by the monitor."""
+
+    def __init__(self, board_dir: str, kfd_sysfs: str | None = None, period_us: int = 2000,
+                 idle_period_us: int = 20000, binary: str | None = None):
+        self.dir = board_dir
+        self.kfd = kfd_sysfs or os.environ.get("MIVGPU_KFD_SYSFS", "/sys/class/kfd/kfd")
+        self.args = ["--period-us", str(period_us), "--idle-period-us", str(idle_period_us)]
+        self.binary = binary or str(boardd_path())
+        self.proc: subprocess.Popen | None = None
+
+    def available(self) -> bool:
+        return os.access(self.binary, os.X_OK) and os.path.isdir(os.path.join(self.kfd, "proc"))
+
+    def start(self) -> "BoardSampler":
+        if self.proc is not None or not self.available():
+            if self.proc is None:
+                log.warning("share-board sampler not started (binary %s, KFD %s)", self.binary, self.kfd)
+            return self
+        os.makedirs(self.dir, exist_ok=True)
+        try:
+            os.chmod(self.dir, 0o755)     # containers read it through a read-only mount
+        except OSError:
+            pass
+        self.proc = subprocess.Popen([self.binary, "--dir", self.dir, "--kfd-sysfs", self.kfd, *self.args,
+                                      "--exit-with-parent"], stdout=subprocess.DEVNULL, stderr=None)
+        log.info("share-board sampler pid %d on %s", self.proc.pid, self.dir)
+        return self
+
+    def alive(self) -> bool:
+        return self.proc is not None and self.proc.poll() is None
+
+    def stop(self):
+        if self.proc is not None and self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(timeout=5)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+                self.proc.wait()

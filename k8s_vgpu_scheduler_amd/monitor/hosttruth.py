@@ -25,7 +25,11 @@ Every pass (the reference's 5 s feedback period, cmd/vGPUmonitor/feedback.go:
   container has no shared region with a live process: its image ignored the
   preload, or it deleted its region file): a ``VGPUShimNotLoaded`` Warning
   event and ``mivgpu_container_shim_loaded 0``; such a container is enforced
-  from KFD alone (over grant -> the escalation of monitor/escalate.py);
+  from KFD alone: over its grant, or on a GPU only the governor would limit
+  (a fractional core limit with no CU mask: nothing bounds its compute), it
+  is evicted after ``--over-grant-passes`` passes whatever
+  ``--over-grant-action`` says (monitor/escalate.py: a block verdict cannot
+  reach a process without the shim);
 * **excess** (truth beyond the region's own counter -- all of the truth for a
   container with no live region -- read before and after
   the KFD reads so that an allocation in flight never counts, and published
@@ -68,6 +72,9 @@ class Grant:
     mem: list[int]                  # bytes per container-local device (0 = unlimited)
     path: str = ""
     mtime: float = 0.0
+    # per device: a fractional core limit with no CU mask -- only the shim's
+    # governor limits that container's compute (cuPartition: false)
+    governed: list[bool] = field(default_factory=list)
 
     @property
     def key(self) -> str:
@@ -98,7 +105,24 @@ def load_grants(limits_dir: Path | str) -> dict[str, Grant]:
         g = parse_grant(text)
         uuids = [u for u in (g.get("MIVGPU_DEVICE_UUIDS") or "").split(",") if u]
         mem = expected_region(g)["mem_limit"][:max(1, len(uuids))]
-        out[f.stem] = Grant(uid, ctr, uuids, mem, str(f), mtime)
+        out[f.stem] = Grant(uid, ctr, uuids, mem, str(f), mtime, governed=_governed(g, max(1, len(uuids))))
+    return out
+
+
+def _governed(g: dict, n: int) -> list[bool]:
+    """Devices whose compute only the governor limits: a core limit below
+    100 % and no HSA_CU_MASK entry for the device."""
+    from .feedback import core_limit_ppm
+
+    masked = set()
+    for part in (g.get("HSA_CU_MASK") or "").split(";"):
+        dev, sep, _ = part.partition(":")
+        if sep and dev.strip().isdigit():
+            masked.add(int(dev))
+    out = []
+    for i in range(n):
+        ppm = core_limit_ppm(g.get(f"HIP_DEVICE_CORE_LIMIT_{i}") or g.get("HIP_DEVICE_CORE_LIMIT") or "")
+        out.append(0 < ppm < 1_000_000 and i not in masked)
     return out
 
 
@@ -110,6 +134,11 @@ class Verdict:
     shim_loaded: bool = True
     excess: list[int] = field(default_factory=list)         # per device, published to the control file
     pids: dict[int, list[int]] = field(default_factory=dict)  # device index -> host pids holding VRAM
+    own_over: bool = False          # its own processes hold more than its grant
+    pod_over: bool = False          # the pod is over only through processes outside every slot
+    hidden: list[int] = field(default_factory=list)          # those pod processes (host pids)
+    no_live_shim: bool = False      # this pass: VRAM held, no process under the shim (before the 2-pass filter)
+    ungoverned: bool = False        # no live shim on a device only the governor limits (time-sharing)
 
 
 class HostTruth:
@@ -210,13 +239,16 @@ class HostTruth:
                 gm = g.mem[i] if i < len(g.mem) else 0
                 grant_sum += gm
                 if gm and t > gm + self.slack:
-                    v.over = True
+                    v.over = v.own_over = True
                     self._report(OVER_GRANT_REASON, g, pod_info,
                                  f"container {g.container} holds {t >> 20} MiB of HBM on device {i} (KFD), over "
                                  f"its grant of {gm >> 20} MiB: launches blocked until it is back under")
                 holds = t > 0 if len(lst) == 1 else (pod_total - attributed > self.slack)
                 if not live and holds:
                     v.shim_loaded = False
+                    v.no_live_shim = True
+                    if i < len(g.governed) and g.governed[i]:
+                        v.ungoverned = True
                 if live:
                     counted = max(before.get(g.key, 0), after.get(g.key, 0))
                     ex = max(0, t - counted)
@@ -231,8 +263,14 @@ class HostTruth:
                     self._excess_prev.pop((g.key, i), None)
             # pod processes outside every slot (a hidden tenant process)
             if len(lst) > 1 and grant_sum and pod_total - attributed > self.slack and pod_total > grant_sum + self.slack:
+                # the excess is held outside every slot: those processes, not
+                # the containers' own, are the ones to stop
+                seen = {p for *_, own in charged for p in own}
+                hidden = sorted(p for p, b in per_pid.items() if b > 0 and p not in seen)
                 for g, i, *_ in charged:
-                    verdict(g).over = True
+                    vv = verdict(g)
+                    vv.over = vv.pod_over = True
+                    vv.hidden = sorted(set(vv.hidden) | set(hidden))
                     self._report(OVER_GRANT_REASON, g, pod_info,
                                  f"pod holds {pod_total >> 20} MiB of HBM on device {i} (KFD), over the "
                                  f"{grant_sum >> 20} MiB granted to its containers: launches blocked")

@@ -90,6 +90,9 @@ def gate_stats() -> dict:
             out["sampler_pass_us_max"] = round(mx.value / 1e3, 1)
     except AttributeError:
         pass
+    info = sampler_info()
+    if info is not None:
+        out["sampler"] = info
     try:
         tr = ctypes.CDLL(None).mivgpu_gate_trace
         buf = (ctypes.c_longlong * (128 * 8))()
@@ -98,6 +101,28 @@ def gate_stats() -> dict:
     except AttributeError:
         pass
     return out
+
+
+def sampler_info(dev: int = 0) -> dict | None:
+    """The preloaded shim's own account of how it charges the governor
+    (mivgpu_sampler_info): the share board (owner role, owner, age, every
+    process's integrals), samples charged from the board or the local
+    estimate, the local estimate's peers and the sampler's state split."""
+    import ctypes
+    import json
+
+    try:
+        fn = ctypes.CDLL(None).mivgpu_sampler_info
+    except AttributeError:
+        return None
+    buf = ctypes.create_string_buffer(32768)
+    n = fn(dev, buf, len(buf))
+    if n <= 0:
+        return None
+    try:
+        return json.loads(buf.value.decode(errors="replace"))
+    except ValueError:
+        return {"raw": buf.value.decode(errors="replace")[:2000]}
 
 
 def child_stream(args) -> dict:

@@ -21,6 +21,7 @@
 #   mall        projection GEMMs cold vs with their weights prefetched into the Infinity Cache
 #   serving     TTFT / per-token latency, native vs vGPU slices (bench/serving.py)
 #   mixed       governed server + 3 governed decode tenants; 8 x 12 % temporal over 600 steps
+#   board       share board: 4 x 25 % / 8 x 12.5 % temporal vs native, unequal limits, time-sharing e2e
 #   prefill     prefill microbench + rocprofv3 kernel summary, whole GPU and 64 CUs
 # Results go to gpurun_out/<suite>/ (copy the ones to keep into profiles/).
 set -o pipefail
@@ -167,6 +168,18 @@ case $suite in
     step 900 serving python -u -m k8s_vgpu_scheduler_amd.bench.serving --configs temporal25,temporal25+3 \
       --warmup 10 --runs 60 --max-tokens 128 --out-dir "$out/serving"
     step 500 t8 python -u bench.py --slices 8 --rounds temporal,native --steps 600 --out "$out/t8.json" ;;
+  board)
+    # the share board (one occupancy sampler per GPU): 4 x 25 % temporal vs
+    # native, unequal limits, 8 x 12.5 % temporal, the time-sharing e2e test
+    step 400 t4 python -u bench.py --rounds temporal,native --steps 100 --out "$out/t4.json"
+    step 300 alone python -u bench.py --slices 1 --mode shim --steps 300 --warmup 5 --out "$out/alone.json"
+    step 400 u75 python -u bench.py --slices 2 --no-spatial --mode shim --policy force --slice-limits 75,25 \
+      --steps 300 --warmup 5 --out "$out/u75_25.json"
+    step 400 u50 python -u bench.py --slices 3 --no-spatial --mode shim --policy force --slice-limits 50,25,25 \
+      --steps 300 --warmup 5 --out "$out/u50_25_25.json"
+    step 400 t8 python -u bench.py --slices 8 --rounds temporal,native --steps 100 --out "$out/t8.json"
+    step 300 e2e python -u -m pytest tests/test_e2e_gpu.py -v -s --timeout 240 --timeout-method thread \
+      -k time_sharing ;;
   prefill)
     step 120 native python3 -m k8s_vgpu_scheduler_amd.bench.prefill
     HSA_CU_MASK=0:0-63 step 120 cu64 python3 -m k8s_vgpu_scheduler_amd.bench.prefill

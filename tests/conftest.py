@@ -19,4 +19,5 @@ def native_build():
     from k8s_vgpu_scheduler_amd.utils import build
     build.build_shim()
     mock_lib, driver = build.build_mock()
-    return {"shim": build.SHIM_SO, "mock_lib": mock_lib, "driver": driver, "roctx": build.MOCK_ROCTX}
+    return {"shim": build.SHIM_SO, "mock_lib": mock_lib, "driver": driver, "roctx": build.MOCK_ROCTX,
+            "boardd": build.build_boardd()}

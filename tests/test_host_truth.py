@@ -267,3 +267,93 @@ def test_lease_expires_without_the_monitor(tmp_path):
     assert snap["block"] == 1
     import time
     assert snap["lease_until_ns"] <= time.time_ns()
+
+
+def _two_container_pod(tmp_path, hidden_gib=5):
+    kfd = tmp_path / "kfd"
+    for pid, v in ((5001, GIB), (5002, GIB), (5003, hidden_gib * GIB)):
+        _kfd(kfd, pid, 42, v)
+    for ctr, pid in (("a", 5001), ("b", 5002)):
+        _grant(tmp_path, "u9", ctr, 2048)
+        r = make_container(tmp_path, "u9", ctr, uuid="GPU-aa", used=GIB, limit=2 * GIB)
+        r.r.procs[0].hostpid = pid
+        r.close()
+    lister = ContainerLister(str(tmp_path), lambda: [pod("u9", "p9")], resync_interval=3600)
+    truth = HostTruth(lambda: {"GPU-aa": 42}, kfd_root=kfd, pod_pids=lambda uid: [5001, 5002, 5003])
+    return kfd, lister, truth
+
+
+def test_kill_targets_the_hidden_process_not_the_compliant_containers(tmp_path):
+    """a pod over its grant only through a process outside every
+    slot: `kill` stops exactly that process (5003), never the compliant
+    containers' own processes (5001, 5002)."""
+    kfd, lister, truth = _two_container_pod(tmp_path)
+    killed = []
+    pol = OverGrantPolicy("kill", passes=1, kill=lambda pid, sig: killed.append(pid))
+    out = feedback.feedback_pass(lister, truth, pol)
+    assert out["over"] == {("u9", "a"), ("u9", "b")}
+    assert set(killed) == {5003} and {a[3][0] for a in out["actions"]} == {5003}, out["actions"]
+    v = truth.state()["verdicts"][("u9", "a")]
+    assert v.pod_over and not v.own_over and v.hidden == [5003]
+
+
+def test_kill_targets_a_container_over_through_its_own_processes(tmp_path):
+    kfd, lister, truth = _two_container_pod(tmp_path, hidden_gib=0)
+    _kfd(kfd, 5001, 42, 3 * GIB)            # container a: over its 2 GiB on its own
+    killed = []
+    pol = OverGrantPolicy("kill", passes=1, kill=lambda pid, sig: killed.append(pid))
+    out = feedback.feedback_pass(lister, truth, pol)
+    assert out["over"] == {("u9", "a")} and killed == [5001], out
+
+
+def _shimless(tmp_path, vram, core="", mask=""):
+    """A granted container holding VRAM with no shared region (the image
+    ignored the preload)."""
+    kfd = tmp_path / "kfd"
+    _kfd(kfd, 4711, 42, vram)
+    _grant(tmp_path, "u1", "main", 4096)
+    f = tmp_path / "vgpu" / "limits" / "u1_main.conf"
+    f.write_text(f.read_text() + (f"HIP_DEVICE_CORE_LIMIT={core}\n" if core else "")
+                 + (f"HSA_CU_MASK={mask}\n" if mask else ""))
+    lister = ContainerLister(str(tmp_path), lambda: [pod("u1", "p1")], resync_interval=3600)
+    truth = HostTruth(lambda: {"GPU-aa": 42}, kfd_root=kfd, pod_pids=lambda uid: [4711])
+    cluster = FakeCluster()
+    cluster.create("pods", make_pod("p1", "default"))
+    return lister, truth, cluster
+
+
+def test_shimless_over_grant_is_evicted_even_under_block(tmp_path):
+    """ADVICE r4 / VERDICT r4 item 5: a block verdict cannot reach a process
+    without the shim, so a shimless container over its grant is evicted after
+    the configured passes even with --over-grant-action block."""
+    from k8s_vgpu_scheduler_amd.monitor.escalate import SHIMLESS_EVICTED_REASON
+    lister, truth, cluster = _shimless(tmp_path, 6 * GIB)
+    events = EventRecorder(None)
+    pol = OverGrantPolicy("block", passes=3, client=cluster, events=events)
+    for _ in range(2):
+        assert feedback.feedback_pass(lister, truth, pol)["actions"] == []
+    out = feedback.feedback_pass(lister, truth, pol)
+    assert out["actions"] == [("evict", "u1", "main", "default/p1")] and cluster.evictions == [("default", "p1")]
+    assert SHIMLESS_EVICTED_REASON in [e[0] for e in events.recorded]
+
+
+def test_shimless_container_on_a_time_shared_gpu_is_evicted(tmp_path):
+    """cuPartition: false: a 12.5 % core limit and no CU mask -- only the
+    governor would limit its compute.  Without the shim it is evicted after
+    3 passes although it is within its HBM grant; the same container with a
+    CU mask (the hardware holds its compute) is only reported."""
+    lister, truth, cluster = _shimless(tmp_path, GIB, core="12.5")
+    pol = OverGrantPolicy("block", passes=3, client=cluster)
+    acts = [feedback.feedback_pass(lister, truth, pol)["actions"] for _ in range(3)]
+    assert acts[:2] == [[], []] and acts[2] == [("evict", "u1", "main", "default/p1")], acts
+    masked = tmp_path / "masked"
+    lister, truth, cluster = _shimless(masked, GIB, core="12.5", mask="0:0-31")
+    pol = OverGrantPolicy("block", passes=3, client=cluster)
+    assert all(feedback.feedback_pass(lister, truth, pol)["actions"] == [] for _ in range(4))
+    assert truth.state()["no_shim"] == {("u1", "main")}
+
+
+def test_shimless_action_none_keeps_the_old_behaviour(tmp_path):
+    lister, truth, cluster = _shimless(tmp_path, 6 * GIB)
+    pol = OverGrantPolicy("block", passes=1, client=cluster, shimless_action="none")
+    assert all(feedback.feedback_pass(lister, truth, pol)["actions"] == [] for _ in range(3))
