@@ -192,6 +192,37 @@ typedef struct {
   mivgpu_board_slot_t slots[MIVGPU_BOARD_SLOTS];
 } mivgpu_board_t; /* 128 + 4096 B */
 
+/* Tenant flags (version 1): <dir>/flags/gpu-<kfd gpu_id>.flags, the one
+ * file of the board directory the tenants write (a read-write mount nested in
+ * the read-only board mount).  Each shim claims an entry for its KFD pid and
+ * publishes, every sampler pass, whether its streams sit in a governor gate
+ * (HELD: its one resident wave per held stream is not work) and whether it
+ * owes GPU work (OWES: split the time nobody has waves resident).  The owner
+ * reads them in its pass; a process without a fresh entry is judged from its
+ * occupancy alone (one CU unit = a gate).  A tenant that lies here only moves
+ * its own charge or drops another process to the occupancy-only rule: the
+ * shares themselves stay in the owner-written board. */
+#define MIVGPU_FLAGS_MAGIC 0x4D495646u /* 'MIVF' */
+#define MIVGPU_FLAGS_VERSION 1
+#define MIVGPU_FLAGS_SLOTS 256
+#define MIVGPU_FLAG_HELD 1
+#define MIVGPU_FLAG_OWES 2
+
+typedef struct {
+  int32_t pid;        /* KFD pid, 0 = free                                   */
+  int32_t state;      /* MIVGPU_FLAG_*                                       */
+  uint64_t stamp_ns;  /* CLOCK_MONOTONIC of the last publish                 */
+} mivgpu_flag_t; /* 16 B */
+
+typedef struct {
+  uint32_t magic;
+  int32_t version;
+  int32_t gpu_id;
+  int32_t reserved;
+  uint64_t unused[6];
+  mivgpu_flag_t flags[MIVGPU_FLAGS_SLOTS];
+} mivgpu_board_flags_t; /* 64 + 4096 B */
+
 /* Field ids understood by mivgpu_abi_offsetof() (exported by libmivgpu.so). */
 enum {
   MIVGPU_F_MAGIC = 0,
@@ -225,6 +256,8 @@ enum {
   MIVGPU_F_BOARD_SLOTS,
   MIVGPU_F_SIZEOF_BOARD,
   MIVGPU_F_SIZEOF_BOARD_SLOT,
+  MIVGPU_F_FLAGS_ENTRIES,
+  MIVGPU_F_SIZEOF_FLAGS,
   MIVGPU_F_COUNT
 };
 

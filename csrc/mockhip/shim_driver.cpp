@@ -38,6 +38,9 @@
 //   setenv|putenv <KEY> <VAL>, unsetenv <KEY>   a tenant rewriting its environment
 //   balance            the governor's host-bucket balance on device 0
 //   launchfor <ms>     hipLaunchKernel every 100 us for <ms> (a busy tenant)
+//   smi <lib>          dlopen an SMI library (csrc/mockhip/mock_smi.cpp) and run
+//                      the memory queries amd-smi / rocm-smi use
+//   sampler            mivgpu_sampler_info: the occupancy sampler's account
 //   stress <threads> <iters> <max MiB>
 //                    threads doing random hipMalloc/hipFree and
 //                    hipMemCreate/hipMemRelease, one kernel launch per
@@ -383,6 +386,32 @@ int main(int argc, char** argv) {
       if (st) (void)st(0, &busy, &held, &gates);
       printf("{\"op\":\"balance\",\"rc\":%d,\"tokens_ns\":%lld,\"received_ns\":%llu,\"held_ns\":%llu,"
              "\"gates\":%llu}\n", rc, t, r, held, gates);
+    } else if (!strcmp(c, "smi")) {
+      // what amd-smi / rocm-smi do: dlopen the library, dlsym the queries
+      void* lib = dlopen(argv[++i], RTLD_NOW | RTLD_LOCAL);
+      typedef int (*mem_fn)(void*, int, uint64_t*);
+      typedef int (*rmem_fn)(uint32_t, int, uint64_t*);
+      struct vu { uint32_t total, used, reserved[2]; } u = {0, 0, {0, 0}};
+      struct vi { int type; char vendor[256]; uint64_t size; uint32_t width; uint64_t bw; uint64_t reserved[37]; } vinf;
+      memset(&vinf, 0, sizeof(vinf));
+      uint64_t t = 0, us = 0, gtt = 0, rt = 0, ru = 0;
+      int ok = lib != nullptr;
+      if (ok) {
+        auto mt = (mem_fn)dlsym(lib, "amdsmi_get_gpu_memory_total");
+        auto mu = (mem_fn)dlsym(lib, "amdsmi_get_gpu_memory_usage");
+        auto vuf = (int (*)(void*, vu*))dlsym(lib, "amdsmi_get_gpu_vram_usage");
+        auto vif = (int (*)(void*, vi*))dlsym(lib, "amdsmi_get_gpu_vram_info");
+        auto rt_f = (rmem_fn)dlsym(lib, "rsmi_dev_memory_total_get");
+        auto ru_f = (rmem_fn)dlsym(lib, "rsmi_dev_memory_usage_get");
+        ok = mt && mu && vuf && vif && rt_f && ru_f && !mt((void*)1, 0, &t) && !mu((void*)1, 0, &us) &&
+             !mt((void*)1, 2, &gtt) && !vuf((void*)1, &u) && !vif((void*)1, &vinf) && !rt_f(0, 0, &rt) &&
+             !ru_f(0, 0, &ru);
+      }
+      printf("{\"op\":\"smi\",\"ok\":%d,\"total_mib\":%llu,\"used_mib\":%llu,\"gtt_mib\":%llu,"
+             "\"vram_total_mb\":%u,\"vram_used_mb\":%u,\"vram_size_mb\":%llu,\"rsmi_total_mib\":%llu,"
+             "\"rsmi_used_mib\":%llu}\n", ok, (unsigned long long)(t >> 20), (unsigned long long)(us >> 20),
+             (unsigned long long)(gtt >> 20), u.total, u.used, (unsigned long long)vinf.size,
+             (unsigned long long)(rt >> 20), (unsigned long long)(ru >> 20));
     } else if (!strcmp(c, "sampler")) {
       // the sampler's own account (share board, local estimate), as JSON
       auto f = (int (*)(int, char*, int))dlsym(RTLD_DEFAULT, "mivgpu_sampler_info");

@@ -52,6 +52,8 @@ struct Handle {
   int gpu_id = -1;
   uint64_t last_pass_ns = 0;   // owner: the previous pass
   char dir[256] = {0};
+  mivgpu_board_flags_t* flags = nullptr;   // <dir>/flags/gpu-<id>.flags (tenant-written)
+  int flag_slot = -1;                      // this tenant's entry
 };
 
 // fstat under the shim's glibc floor (glibc_floor.h: fstat became a real
@@ -135,6 +137,93 @@ inline bool open_board(Handle& h, const char* dir, int gpu_id, bool may_create) 
   return true;
 }
 
+// Map (creating it if needed) <dir>/flags/gpu-<id>.flags read-write: the one
+// tenant-writable file of the board directory.  False when it cannot be
+// written (the owner then judges every process from its occupancy alone).
+inline bool open_flags(Handle& h) {
+  if (h.flags) return true;
+  char fdir[300], path[600];
+  snprintf(fdir, sizeof(fdir), "%s/flags", h.dir);
+  if (mkdir(fdir, 0777) == 0) (void)chmod(fdir, 0777);
+  snprintf(path, sizeof(path), "%s/gpu-%d.flags", fdir, h.gpu_id);
+  int fd = open(path, O_RDWR | O_CLOEXEC);
+  if (fd < 0 && errno == ENOENT) {
+    char tmp[640];
+    snprintf(tmp, sizeof(tmp), "%s/.gpu-%d.flags.%d", fdir, h.gpu_id, (int)getpid());
+    int t = open(tmp, O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
+    if (t >= 0) {
+      (void)fchmod(t, 0666);
+      mivgpu_board_flags_t init;
+      memset(&init, 0, sizeof(init));
+      init.magic = MIVGPU_FLAGS_MAGIC;
+      init.version = MIVGPU_FLAGS_VERSION;
+      init.gpu_id = h.gpu_id;
+      const bool ok = pwrite(t, &init, sizeof(init), 0) == (ssize_t)sizeof(init);
+      close(t);
+      if (ok) (void)link(tmp, path);
+      unlink(tmp);
+    }
+    fd = open(path, O_RDWR | O_CLOEXEC);
+  }
+  if (fd < 0) return false;
+  struct stat st;
+  if (board_fstat(fd, &st) != 0 || (size_t)st.st_size < sizeof(mivgpu_board_flags_t)) {
+    close(fd);
+    return false;
+  }
+  void* m = mmap(nullptr, sizeof(mivgpu_board_flags_t), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (m == MAP_FAILED) return false;
+  mivgpu_board_flags_t* f = static_cast<mivgpu_board_flags_t*>(m);
+  if (f->magic != MIVGPU_FLAGS_MAGIC || f->version != MIVGPU_FLAGS_VERSION || f->gpu_id != h.gpu_id) {
+    munmap(m, sizeof(mivgpu_board_flags_t));
+    return false;
+  }
+  h.flags = f;
+  return true;
+}
+
+// Tenant side: publish this pass's state under its KFD pid (an entry claimed
+// once, by CAS on a free or stale one).
+inline void publish_flags(Handle& h, int pid, int state, uint64_t now) {
+  if (!h.flags || pid <= 0) return;
+  mivgpu_flag_t* e = h.flag_slot >= 0 ? &h.flags->flags[h.flag_slot] : nullptr;
+  if (!e || __atomic_load_n(&e->pid, __ATOMIC_RELAXED) != pid) {
+    h.flag_slot = -1;
+    for (int k = 0; k < MIVGPU_FLAGS_SLOTS && h.flag_slot < 0; ++k) {
+      mivgpu_flag_t* c = &h.flags->flags[k];
+      int cur = __atomic_load_n(&c->pid, __ATOMIC_ACQUIRE);
+      if (cur == pid) h.flag_slot = k;
+    }
+    for (int k = 0; k < MIVGPU_FLAGS_SLOTS && h.flag_slot < 0; ++k) {
+      mivgpu_flag_t* c = &h.flags->flags[k];
+      int cur = __atomic_load_n(&c->pid, __ATOMIC_ACQUIRE);
+      const bool stale = cur != 0 && __atomic_load_n(&c->stamp_ns, __ATOMIC_RELAXED) + 2000000000ull < now;
+      if ((cur == 0 || stale) &&
+          __atomic_compare_exchange_n(&c->pid, &cur, pid, false, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED))
+        h.flag_slot = k;
+    }
+    if (h.flag_slot < 0) return;
+    e = &h.flags->flags[h.flag_slot];
+  }
+  __atomic_store_n(&e->state, state, __ATOMIC_RELAXED);
+  __atomic_store_n(&e->stamp_ns, now, __ATOMIC_RELEASE);
+}
+
+// Owner side: a process's published state, -1 when it has no fresh entry.
+constexpr uint64_t kFlagFreshNs = 20000000ull;   // 20 ms: ten tenant passes
+inline int read_flags(const mivgpu_board_flags_t* f, int pid, uint64_t now) {
+  if (!f || pid <= 0) return -1;
+  for (int k = 0; k < MIVGPU_FLAGS_SLOTS; ++k) {
+    const mivgpu_flag_t* e = &f->flags[k];
+    if (__atomic_load_n(&e->pid, __ATOMIC_ACQUIRE) != pid) continue;
+    const uint64_t st = __atomic_load_n(&e->stamp_ns, __ATOMIC_ACQUIRE);
+    if (st + kFlagFreshNs < now) return -1;
+    return __atomic_load_n(&e->state, __ATOMIC_RELAXED);
+  }
+  return -1;
+}
+
 inline bool node_owner_live(const mivgpu_board_t* b, int self_pid, uint64_t now) {
   const int kind = __atomic_load_n(&b->owner_kind, __ATOMIC_ACQUIRE);
   const uint64_t beat = __atomic_load_n(&b->beat_ns, __ATOMIC_ACQUIRE);
@@ -174,7 +263,17 @@ enum Split { kSplitRatio = 0, kSplitEqual = 1 };
 
 // One owner pass over `n` readings (every KFD process on the GPU, this pass).
 // Call with h.owner (or from the node sampler); `kind`/`owner_pid` go to the
-// header.
+// header.  Per process:
+//   held   -- its flags say its streams sit in a governor gate, or (no fresh
+//             flags) it shows exactly a gate's CU unit: not contending, and
+//             the pass is not observed for it;
+//   w      -- its resident CU units when not held (a running tenant's small
+//             kernels count: a queued tenant is not charged the GPU while
+//             they run);
+//   f      -- w / W when any process has waves resident (W = all w); when
+//             none has, the owing tenants (flags) split the pass equally (a
+//             process without flags is charged it whole: it is alone between
+//             its own kernels).
 inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_t period_ns, int kind,
                        int owner_pid, int split, uint64_t pass_cost_ns) {
   mivgpu_board_t* b = h.b;
@@ -182,13 +281,26 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
   uint64_t dt = h.last_pass_ns && now > h.last_pass_ns ? now - h.last_pass_ns : 0;
   if (dt > kMaxDtNs) dt = kMaxDtNs;
   h.last_pass_ns = now;
+  if (h.flags == nullptr) (void)open_flags(h);
+  constexpr int kMaxRead = 256;
+  int st[kMaxRead];
+  long wv[kMaxRead];
   long W = 0;
-  int resident = 0;
-  for (int i = 0; i < n; ++i)
-    if (r[i].v > kGateUnits) {
-      W += r[i].v;
+  int resident = 0, owing = 0;
+  if (n > kMaxRead) n = kMaxRead;
+  for (int i = 0; i < n; ++i) {
+    st[i] = read_flags(h.flags, r[i].pid, now);
+    const int v = r[i].v;
+    bool held;
+    if (st[i] >= 0) held = (st[i] & MIVGPU_FLAG_HELD) != 0;
+    else held = v > 0 && v <= kGateUnits;
+    wv[i] = (!held && v > 0) ? v : 0;
+    if (st[i] >= 0 && (st[i] & MIVGPU_FLAG_OWES) && !held) ++owing;
+    if (wv[i] > 0) {
+      W += wv[i];
       ++resident;
     }
+  }
   const uint64_t s0 = __atomic_load_n(&b->seq, __ATOMIC_RELAXED);
   __atomic_store_n(&b->seq, s0 | 1ull, __ATOMIC_RELAXED);
   __atomic_thread_fence(__ATOMIC_RELEASE);
@@ -215,7 +327,8 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
     }
     mivgpu_board_slot_t& s = b->slots[slot];
     const int v = r[i].v;
-    const long w = v > kGateUnits ? v : 0;
+    const long w = wv[i];
+    const bool held = st[i] >= 0 ? (st[i] & MIVGPU_FLAG_HELD) != 0 : (v > 0 && v <= kGateUnits);
     s.occupancy = v;
     s.seen_ns = now;
     if (!dt) continue;
@@ -225,10 +338,10 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
       f = got;
     } else {
       got = 0.0;
-      f = 1.0;   // nobody resident: a process owing work is alone between its own kernels
+      const bool owes = st[i] >= 0 && (st[i] & MIVGPU_FLAG_OWES);
+      f = st[i] < 0 ? 1.0 : (owes && owing > 0 ? 1.0 / (double)owing : 1.0);
     }
-    const bool gated = v > 0 && v <= kGateUnits;
-    if (!gated) {
+    if (!held) {
       s.obs_ns += dt;
       s.frac_ns += (uint64_t)(f * (double)dt + 0.5);
     }

@@ -217,13 +217,20 @@ def allocate_container(pod: dict, ctr: dict, devreq: list, gpus: dict, cfg: Plug
         os.chmod(tmp, 0o444)
         os.replace(tmp, limits)
         create_control(control)
-        os.makedirs(board_host_dir(hook), exist_ok=True)
+        os.makedirs(os.path.join(board_host_dir(hook), "flags"), exist_ok=True)
+        try:
+            os.chmod(os.path.join(board_host_dir(hook), "flags"), 0o777)
+        except OSError:
+            pass
     mounts = [
         {"container_path": CONTAINER_LIB, "host_path": f"{hook}/vgpu/libmivgpu.so", "read_only": True},
         {"container_path": f"{hook}/vgpu", "host_path": host_dir, "read_only": False},
         {"container_path": LIMITS_PATH, "host_path": limits, "read_only": True},
         {"container_path": CONTAINER_CONTROL_PATH, "host_path": control, "read_only": True},
         {"container_path": CONTAINER_BOARD_DIR, "host_path": board_host_dir(hook), "read_only": True},
+        # the tenants' held / owing flags: the one writable part of the board
+        {"container_path": f"{CONTAINER_BOARD_DIR}/flags", "host_path": f"{board_host_dir(hook)}/flags",
+         "read_only": False},
     ]
     # the pod-spec opt-out drops the preload -- only where opting out is allowed
     # (a fractional pod would otherwise escape every limit; the webhook also

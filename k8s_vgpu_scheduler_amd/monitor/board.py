@@ -16,7 +16,9 @@ server.go:853-864); here ONE owner per GPU reads every process's
 * production: the monitor runs ``mivgpu-boardd`` (``BoardSampler``) on
   ``$HOOK_PATH/vgpu/board``, which the device plugin mounts READ-ONLY into
   every vGPU container (``deviceplugin/allocate.py``) -- no tenant can write
-  the share it is charged;
+  the share it is charged -- with one read-write subdirectory, ``flags/``,
+  where each tenant's shim publishes whether it is held in its governor gate
+  or owes work (the owner's pass reads them);
 * without a node sampler (hand-run slices, the bench), a shim that governs
   the GPU takes the owner role with ``flock`` on ``gpu-<id>.owner``.
 
@@ -59,12 +61,70 @@ class BoardHeader(C.Structure):
 BOARD_SIZE = C.sizeof(BoardHeader)
 assert C.sizeof(BoardSlot) == 64 and BOARD_SIZE == 128 + 64 * BOARD_SLOTS
 
+FLAGS_MAGIC = 0x4D495646
+FLAGS_VERSION = 1
+FLAGS_SLOTS = 256
+FLAG_HELD, FLAG_OWES = 1, 2
+
+
+class Flag(C.Structure):
+    _fields_ = [("pid", C.c_int32), ("state", C.c_int32), ("stamp_ns", C.c_uint64)]
+
+
+class Flags(C.Structure):
+    _fields_ = [("magic", C.c_uint32), ("version", C.c_int32), ("gpu_id", C.c_int32), ("reserved", C.c_int32),
+                ("unused", C.c_uint64 * 6), ("flags", Flag * FLAGS_SLOTS)]
+
+
+FLAGS_SIZE = C.sizeof(Flags)
+assert FLAGS_SIZE == 64 + 16 * FLAGS_SLOTS
+
 
 def offsets() -> dict:
     """Field offsets for the ABI test against mivgpu_abi_offsetof()."""
-    # MIVGPU_F_BOARD_SEQ .. MIVGPU_F_SIZEOF_BOARD_SLOT (enum order in shared_region.h)
+    # MIVGPU_F_BOARD_SEQ .. MIVGPU_F_SIZEOF_FLAGS (enum order in shared_region.h)
     return {26: BoardHeader.seq.offset, 27: BoardHeader.beat_ns.offset, 28: BoardHeader.slots.offset,
-            29: BOARD_SIZE, 30: C.sizeof(BoardSlot)}
+            29: BOARD_SIZE, 30: C.sizeof(BoardSlot), 31: Flags.flags.offset, 32: FLAGS_SIZE}
+
+
+def flags_path(board_dir: str, gpu_id: int) -> Path:
+    return Path(board_dir) / "flags" / f"gpu-{gpu_id}.flags"
+
+
+class FlagsFile:
+    """The tenant-written flags of one GPU mapped read-write (tests stand in
+    for tenants with it; the owner reads it in its pass)."""
+
+    def __init__(self, board_dir: str, gpu_id: int, create: bool = True):
+        p = flags_path(board_dir, gpu_id)
+        if create and not p.exists():
+            p.parent.mkdir(parents=True, exist_ok=True)
+            f = Flags()
+            f.magic, f.version, f.gpu_id = FLAGS_MAGIC, FLAGS_VERSION, gpu_id
+            tmp = p.with_name(p.name + f".{os.getpid()}")
+            tmp.write_bytes(bytes(f))
+            try:
+                os.link(tmp, p)
+            except FileExistsError:
+                pass
+            tmp.unlink()
+        fd = os.open(p, os.O_RDWR | os.O_CLOEXEC)
+        try:
+            self.mm = mmap.mmap(fd, FLAGS_SIZE, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        finally:
+            os.close(fd)
+        self.f = Flags.from_buffer(self.mm)
+
+    def publish(self, pid: int, state: int):
+        slot = next((e for e in self.f.flags if e.pid == pid), None) or next(e for e in self.f.flags if e.pid == 0)
+        slot.pid, slot.state, slot.stamp_ns = pid, state, time.monotonic_ns()
+
+    def entries(self) -> dict[int, tuple[int, int]]:
+        return {e.pid: (e.state, e.stamp_ns) for e in self.f.flags if e.pid}
+
+    def close(self):
+        del self.f
+        self.mm.close()
 
 
 def board_path(board_dir: str, gpu_id: int) -> Path:
@@ -158,9 +218,10 @@ class BoardSampler:
             if self.proc is None:
                 log.warning("share-board sampler not started (binary %s, KFD %s)", self.binary, self.kfd)
             return self
-        os.makedirs(self.dir, exist_ok=True)
+        os.makedirs(os.path.join(self.dir, "flags"), exist_ok=True)
         try:
-            os.chmod(self.dir, 0o755)     # containers read it through a read-only mount
+            os.chmod(self.dir, 0o755)     # containers read it through a read-only mount ...
+            os.chmod(os.path.join(self.dir, "flags"), 0o777)   # ... and write their flags in this one
         except OSError:
             pass
         self.proc = subprocess.Popen([self.binary, "--dir", self.dir, "--kfd-sysfs", self.kfd, *self.args,

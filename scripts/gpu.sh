@@ -178,6 +178,7 @@ case $suite in
     step 400 u50 python -u bench.py --slices 3 --no-spatial --mode shim --policy force --slice-limits 50,25,25 \
       --steps 300 --warmup 5 --out "$out/u50_25_25.json"
     step 400 t8 python -u bench.py --slices 8 --rounds temporal,native --steps 100 --out "$out/t8.json"
+    step 200 smi python -u -m pytest tests/test_smi_gpu.py -v -s --timeout 120 --timeout-method thread
     step 300 e2e python -u -m pytest tests/test_e2e_gpu.py -v -s --timeout 240 --timeout-method thread \
       -k time_sharing ;;
   prefill)

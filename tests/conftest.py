@@ -20,4 +20,4 @@ def native_build():
     build.build_shim()
     mock_lib, driver = build.build_mock()
     return {"shim": build.SHIM_SO, "mock_lib": mock_lib, "driver": driver, "roctx": build.MOCK_ROCTX,
-            "boardd": build.build_boardd()}
+            "boardd": build.build_boardd(), "mock_smi": build.MOCK_SMI}

@@ -196,3 +196,50 @@ def test_read_only_board_is_never_owned(native_build, tmp_path):
         os.chmod(d, 0o755)
     assert info["board"]["open"] == 1 and info["board"]["writable"] == 0 and info["board"]["owner"] == 0, info
     assert info["board_charged"] == 0 and info["local_charged"] > 0, info
+
+
+def test_tenant_flags_decide_held_and_gap_splits(native_build, tmp_path):
+    """The tenants' flags (board dir /flags, written by each shim) tell the
+    owner who sits in a gate and who owes work: a tenant running small kernels
+    (1 CU unit) counts as resident, so a queued tenant is not charged while it
+    runs; a held tenant (flags) is neither resident nor observed; with nobody
+    resident the owing tenants split the pass."""
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
+    d = tmp_path / "board"
+    fl = B.FlagsFile(str(d), 4242)
+    # 111 runs tiny kernels, 222 is queued behind it (owes, nothing resident), 333 is held
+    _occ(kfd, 111, 4242, 1)
+    _occ(kfd, 222, 4242, 0)
+    _occ(kfd, 333, 4242, 1)
+    node = subprocess.Popen(_boardd(native_build, kfd, d))
+    try:
+        t_end = time.time() + 0.5
+        while time.time() < t_end:
+            fl.publish(111, B.FLAG_OWES)
+            fl.publish(222, B.FLAG_OWES)
+            fl.publish(333, B.FLAG_HELD)
+            time.sleep(0.005)
+        b = B.Board(B.board_path(d, 4242))
+        s1 = b.snapshot()
+        # now nobody resident: 111 and 222 owe, split the gap
+        _occ(kfd, 111, 4242, 0)
+        time.sleep(0.05)
+        mid = b.snapshot()
+        t_end = time.time() + 0.5
+        while time.time() < t_end:
+            fl.publish(111, B.FLAG_OWES)
+            fl.publish(222, B.FLAG_OWES)
+            fl.publish(333, B.FLAG_HELD)
+            time.sleep(0.005)
+        s2 = b.snapshot()
+        b.close()
+    finally:
+        node.terminate()
+        node.wait(timeout=10)
+        fl.close()
+    first = {s.pid: s for s in s1.slots if s.pid}
+    assert first[111].frac_ns == first[111].obs_ns > 0           # its small kernels: the whole GPU
+    assert first[222].obs_ns > 0 and first[222].frac_ns == 0      # queued behind them: charged nothing
+    assert first[333].obs_ns == 0                                 # held: not observed
+    sh = B.shares(mid, s2)
+    assert abs(sh[111]["charged_share"] - 0.5) < 0.05 and abs(sh[222]["charged_share"] - 0.5) < 0.05, sh

@@ -78,3 +78,44 @@ def test_health_usage_and_events(backends):
     # or reports that it is unavailable; it must never raise
     ev = b.wait_health_events(gs, 0.5)
     assert ev is None or all(isinstance(e, smi.HealthEvent) for e in ev)
+
+
+_SMI_PROBE = r"""
+import json, amdsmi
+amdsmi.amdsmi_init()
+h = amdsmi.amdsmi_get_processor_handles()[0]
+t = amdsmi.amdsmi_get_gpu_memory_total(h, amdsmi.AmdSmiMemoryType.VRAM)
+u = amdsmi.amdsmi_get_gpu_memory_usage(h, amdsmi.AmdSmiMemoryType.VRAM)
+v = amdsmi.amdsmi_get_gpu_vram_usage(h)
+print(json.dumps({"total_mib": t >> 20, "used_mib": u >> 20, "vram_total": v["vram_total"],
+                  "vram_used": v["vram_used"]}))
+amdsmi.amdsmi_shut_down()
+"""
+
+
+def test_amdsmi_inside_a_slice_reports_the_grant(tmp_path):
+    """`import amdsmi` in a 36 GiB slice (the shim
+    preloaded, the grant naming this GPU) reports 36864 MiB total and the
+    container's usage; the same query without the shim reports the card."""
+    import subprocess
+    import sys
+
+    from k8s_vgpu_scheduler_amd.shim import shim_env
+
+    g = smi.detect("amdsmi").gpus()[0]
+    base = dict(os.environ)
+    base.pop("LD_PRELOAD", None)
+
+    def probe(env):
+        r = subprocess.run([sys.executable, "-c", _SMI_PROBE], env=env, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    native = probe(base)
+    sl = dict(base, **shim_env(""), HIP_DEVICE_MEMORY_LIMIT_0="36864m", MIVGPU_DEVICE_UUIDS=g.uuid,
+              MIVGPU_SHARED_CACHE=str(tmp_path / "smi.cache"))
+    inside = probe(sl)
+    print(json.dumps({"native": native, "slice": inside, "uuid": g.uuid}))
+    assert native["total_mib"] > 280_000 and native["vram_total"] > 280_000, native
+    assert inside["total_mib"] == 36864 and inside["vram_total"] == 36864, inside
+    assert inside["used_mib"] <= 36864 and inside["vram_used"] <= 36864, inside
