@@ -237,6 +237,216 @@ prefill_flash_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
   }
 }
 
+// ============================================================================
+// Eight-wave variant (the default for G <= 8): 64-key tiles, 32 * RT query
+// rows per workgroup (RT = 8 / G row tiles of 32, so every workgroup has 8
+// waves: two per SIMD, one wave's softmax beside its partner's MFMAs), every
+// wave one (head, row tile).  Measured on the kernel above (32-key tiles, 4
+// waves, one per SIMD): 307 TFLOP/s at L = 8192 -- the softmax's vector work
+// per 32x32 MFMA gap (scale, mask, max, exp, sum, the O rescale: ~680 cycles
+// of issue against the ~384 the 16 MFMAs of a tile hide, MI355X_MICROARCH.md
+// 'vector-instruction ISSUE cost') set the pace.  Here:
+//   * the scale goes into the exponent's FMA (one v_fma + one v_exp per
+//     score), the max is taken on the raw scores;
+//   * masks only on the diagonal half-tile; halves wholly above a wave's
+//     diagonal skip their MFMAs;
+//   * the O / l rescale runs only when some row's max grew by more than 8
+//     (log2 units; the stale max keeps every p <= 256, exact in fp32 and
+//     bf16 range): after the first tiles it is almost never taken;
+//   * 64-key tiles: half the barriers and max exchanges per key;
+//   * one barrier per tile: the next tile's K/V land in registers during this
+//     tile's MFMAs and are stored into the other LDS buffer after them.
+constexpr int F2_BK = 64;
+constexpr int F2_TILE = F2_BK * FA_D;     // elements per K (or V) tile: 16 KB
+constexpr int F2_CHUNKS = F2_TILE / 8;    // 1024 16-byte chunks
+constexpr float F2_RESCALE = 8.f;         // lazy O rescale threshold (log2 units)
+
+template <int G, int RT>
+__global__ void __launch_bounds__(G * RT * 64, 2)
+prefill_flash8_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                      bf16_t* __restrict__ out, int L, int Hq, float scale_log2) {
+  constexpr int NW = G * RT, NT = NW * 64;
+  constexpr int PER = F2_CHUNKS / NT;      // 16-byte chunks per thread per tile (K and V each)
+  static_assert(PER * NT == F2_CHUNKS && NW == 8, "eight waves, the tile split evenly");
+  constexpr int ROWS = 32 * RT;
+  __shared__ __attribute__((aligned(16))) bf16_t ks[2][F2_TILE];
+  __shared__ __attribute__((aligned(16))) bf16_t vs[2][F2_TILE];
+
+  const int nqb = (L + ROWS - 1) / ROWS;
+  const int qb = nqb - 1 - (int)blockIdx.x;       // heaviest (longest) blocks first
+  const int hk = blockIdx.y;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int g = w % G, rt = w / G;                // head of the group, row tile
+  const int r = lane & 31, h = lane >> 5;
+  const int l0 = qb * ROWS + 32 * rt;             // this wave's first query row
+  const int blk_end = min(L, (qb + 1) * ROWS);    // the block needs keys < blk_end
+  const int ntiles = (blk_end + F2_BK - 1) / F2_BK;
+
+  const bf16_t* kb = k + (size_t)hk * L * FA_D;
+  const bf16_t* vb = v + (size_t)hk * L * FA_D;
+
+  bf16x8_t qf[8];
+  {
+    const int qrow = min(l0 + r, L - 1);
+    const bf16_t* qp = q + (((size_t)hk * G + g) * L + qrow) * FA_D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8_t*>(qp + 16 * s);
+  }
+
+  // the next tile in registers: two 16-byte chunks of K and of V per thread
+  // (named values, not an array: an array here was kept in scratch and LDS)
+  static_assert(PER == 2, "two chunks per thread");
+  const int c0 = t, c1 = t + NT;                  // chunk c -> row c >> 4, 16-byte chunk c & 15
+  const int ko0 = k_off(c0 >> 4, c0 & 15), ko1 = k_off(c1 >> 4, c1 & 15);
+  const int vo0 = v_off(c0 >> 4, c0 & 15), vo1 = v_off(c1 >> 4, c1 & 15);
+  uint4 k0r, k1r, v0r, v1r;
+  auto load_tile = [&](int kt) {
+    const int r0 = min(kt * F2_BK + (c0 >> 4), L - 1);   // rows past L: masked (causal)
+    const int r1 = min(kt * F2_BK + (c1 >> 4), L - 1);
+    k0r = *reinterpret_cast<const uint4*>(kb + (size_t)r0 * FA_D + (c0 & 15) * 8);
+    v0r = *reinterpret_cast<const uint4*>(vb + (size_t)r0 * FA_D + (c0 & 15) * 8);
+    k1r = *reinterpret_cast<const uint4*>(kb + (size_t)r1 * FA_D + (c1 & 15) * 8);
+    v1r = *reinterpret_cast<const uint4*>(vb + (size_t)r1 * FA_D + (c1 & 15) * 8);
+  };
+  auto store_tile = [&](int buf) {
+    *reinterpret_cast<uint4*>(&ks[buf][ko0]) = k0r;
+    *reinterpret_cast<uint4*>(&vs[buf][vo0]) = v0r;
+    *reinterpret_cast<uint4*>(&ks[buf][ko1]) = k1r;
+    *reinterpret_cast<uint4*>(&vs[buf][vo1]) = v1r;
+  };
+
+  f32x16_t o[4];
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[dc][i] = 0.f;
+  float m = -INFINITY, lsum = 0.f;
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < ntiles) load_tile(kt + 1);     // in flight during this tile's MFMAs
+    const int kbase = kt * F2_BK;
+    if (kbase <= l0 + 31) {                     // some key of the tile is visible to this wave
+      // halves of 32 keys: visible (kbase + 32hf <= l0), diagonal when equal
+      const bool act1 = kbase + 32 <= l0;
+      const bf16_t* kt_lds = ks[buf];
+      f32x16_t s0, s1;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s0[i] = 0.f, s1[i] = 0.f;
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&kt_lds[k_off(r, 2 * st + h)]);
+        s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[st], s0, 0, 0, 0);
+      }
+      if (act1) {
+#pragma unroll
+        for (int st = 0; st < 8; ++st) {
+          const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&kt_lds[k_off(32 + r, 2 * st + h)]);
+          s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[st], s1, 0, 0, 0);
+        }
+      }
+      // causal mask on the diagonal half only: key (i&3) + 8(i>>2) + 4h of the
+      // half against query r of the row tile
+      if (kbase == l0) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if ((i & 3) + 8 * (i >> 2) + 4 * h > r) s0[i] = -INFINITY;
+      } else if (act1 && kbase + 32 == l0) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if ((i & 3) + 8 * (i >> 2) + 4 * h > r) s1[i] = -INFINITY;
+      }
+      float mx = s0[0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s0[i]);
+      if (act1) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s1[i]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mt = mx * scale_log2;         // finite: key kbase <= every query of the wave
+      if (__ballot(mt > m + F2_RESCALE)) {
+        const float mnew = fmaxf(m, mt);
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);   // 0 on the first tile (m = -inf)
+        m = mnew;
+        lsum *= alpha;
+#pragma unroll
+        for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[dc][i] *= alpha;
+      }
+      float psum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(s0[i], scale_log2, -m));
+        s0[i] = p;
+        psum += p;
+      }
+      if (act1) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(s1[i], scale_log2, -m));
+          s1[i] = p;
+          psum += p;
+        }
+      }
+      lsum += psum;
+
+      // O^T += V^T . P^T over the visible 16-key k-steps; V^T by transposed reads
+      const bf16_t* vt_lds = vs[buf];
+      const int gi = lane & 15, qq = gi >> 2, pp = gi & 3;
+      const int colblk = 16 * ((lane >> 4) & 1);
+      auto pv = [&](const f32x16_t& sh, int u) {
+        bf16x8_t pf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[j] = (__bf16)sh[8 * (u & 1) + j];
+        const int row_lo = 16 * u + 4 * h + qq, row_hi = row_lo + 8;
+#pragma unroll
+        for (int dc = 0; dc < 4; ++dc) {
+          const int col = 32 * dc + colblk + 4 * pp;
+          const int olo = v_off(row_lo, col >> 3) + (col & 7), ohi = v_off(row_hi, col >> 3) + (col & 7);
+          const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) i16x4_t*)(&vt_lds[olo]));
+          const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) i16x4_t*)(&vt_lds[ohi]));
+          const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
+          const uint4 a4 = make_uint4(l2.x, l2.y, h2.x, h2.y);
+          o[dc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a4), pf, o[dc], 0, 0, 0);
+        }
+      };
+      pv(s0, 0);
+      pv(s0, 1);
+      if (act1) {
+        pv(s1, 2);
+        pv(s1, 3);
+      }
+    }
+    if (kt + 1 < ntiles) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  const float inv = 1.f / ltot;
+  const int qpos = l0 + r;
+  if (qpos < L) {
+    bf16_t* op = out + (size_t)qpos * Hq * FA_D + (size_t)(hk * G + g) * FA_D;
+#pragma unroll
+    for (int dc = 0; dc < 4; ++dc)
+#pragma unroll
+      for (int i4 = 0; i4 < 4; ++i4) {
+        const int d = 32 * dc + 8 * i4 + 4 * h;
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(o[dc][4 * i4 + 0] * inv) | ((uint32_t)f2bf(o[dc][4 * i4 + 1] * inv) << 16);
+        pk.y = (uint32_t)f2bf(o[dc][4 * i4 + 2] * inv) | ((uint32_t)f2bf(o[dc][4 * i4 + 3] * inv) << 16);
+        *reinterpret_cast<uint2*>(op + d) = pk;
+      }
+  }
+}
+
 // ds_read_b64_tr_b16 semantics probe: LDS holds element e = e; lane l reads
 // at element offset addr[l]; out[4l + i] = element i it received.
 // OFF: a constant element offset the compiler folds into the instruction's
@@ -258,6 +468,16 @@ __global__ void __launch_bounds__(64) tr_read_probe_kernel(const int* __restrict
 int fa_tr() {
   const char* e = getenv("MIVGPU_FA_TR");
   return e && *e ? atoi(e) : 1;
+}
+
+// Which kernel: 8 = the eight-wave 64-key-tile kernel (default), 4 = the
+// 32-key-tile kernel (A/B; also taken whenever MIVGPU_FA_TR asks for one of
+// its V^T variants).
+int fa_kernel() {
+  const char* e = getenv("MIVGPU_FA_KERNEL");
+  if (e && *e) return atoi(e);
+  const char* tr = getenv("MIVGPU_FA_TR");
+  return tr && *tr && atoi(tr) != 1 ? 4 : 8;
 }
 
 }  // namespace
@@ -293,6 +513,18 @@ int mivgpu_prefill_attention(const void* q, const void* k, const void* v, void* 
     else if (tr == 2) MIVGPU_FA(GG, true, true);         \
     else MIVGPU_FA(GG, false, false);                    \
     break;
+  if (fa_kernel() == 8) {
+    const int rows = 32 * (8 / G);
+    const dim3 grid8((L + rows - 1) / rows, Hkv);
+    switch (G) {
+      case 1: hipLaunchKernelGGL((prefill_flash8_kernel<1, 8>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
+      case 2: hipLaunchKernelGGL((prefill_flash8_kernel<2, 4>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
+      case 4: hipLaunchKernelGGL((prefill_flash8_kernel<4, 2>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
+      case 8: hipLaunchKernelGGL((prefill_flash8_kernel<8, 1>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
+      default: return -1;
+    }
+    return (int)hipGetLastError();
+  }
   const int tr = fa_tr();
   switch (G) {
     MIVGPU_FA_G(1)
