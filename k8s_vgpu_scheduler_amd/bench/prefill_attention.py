@@ -54,7 +54,7 @@ def main(argv=None):
         t = _time(lambda: ops.prefill_attention(q, k, v, Hq, scale, out=out), a.reps)
         row = {"L": L, "heads": Hq, "kv_heads": Hkv, "flash_ms": round(t * 1e3, 3),
                "flash_tflops": round(flops / t / 1e12, 1), "cus": ops.visible_cus(),
-               "vt_path": os.environ.get("MIVGPU_FA_TR", "1")}
+               "vt_path": os.environ.get("MIVGPU_FA_TR", "1"), "kernel": os.environ.get("MIVGPU_FA_KERNEL", "8")}
         if L <= a.eager_max:
             i = torch.arange(L, device="cuda")
             mask = torch.zeros(L, L, device="cuda").masked_fill_(i[None, :] > i[:, None], float("-inf")).repeat(G, 1)

@@ -22,6 +22,7 @@
 #   serving     TTFT / per-token latency, native vs vGPU slices (bench/serving.py)
 #   mixed       governed server + 3 governed decode tenants; 8 x 12 % temporal over 600 steps
 #   board       share board: 4 x 25 % / 8 x 12.5 % temporal vs native, unequal limits, time-sharing e2e
+#   attn        prefill flash attention: tests, eight-wave vs 32-key-tile kernel at 512 / 2048 / 8192
 #   prefill     prefill microbench + rocprofv3 kernel summary, whole GPU and 64 CUs
 # Results go to gpurun_out/<suite>/ (copy the ones to keep into profiles/).
 set -o pipefail
@@ -181,6 +182,14 @@ case $suite in
     step 200 smi python -u -m pytest tests/test_smi_gpu.py -v -s --timeout 120 --timeout-method thread
     step 300 e2e python -u -m pytest tests/test_e2e_gpu.py -v -s --timeout 240 --timeout-method thread \
       -k time_sharing ;;
+  attn)
+    # prefill flash attention: numerics vs fp32, then the eight-wave kernel
+    # against the 32-key-tile one at 512 / 2048 / 8192 positions
+    step 300 tests python -u -m pytest tests/test_ops_gpu.py -v --timeout 120 --timeout-method thread -k "prefill_flash or tr_read"
+    step 200 fa8 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention --lens 512,2048,8192 --eager-max 0 \
+      --out "$out/fa8.json"
+    MIVGPU_FA_KERNEL=4 step 200 fa4 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention --lens 512,2048,8192 \
+      --eager-max 0 --out "$out/fa4.json" ;;
   prefill)
     step 120 native python3 -m k8s_vgpu_scheduler_amd.bench.prefill
     HSA_CU_MASK=0:0-63 step 120 cu64 python3 -m k8s_vgpu_scheduler_amd.bench.prefill

@@ -407,3 +407,23 @@ def test_unequal_temporal_limits_get_their_shares(tmp, limits):
             assert abs(row["busy_share_pct"] - lim) <= 3.0, rows
         assert 0.9 * lim / 100 <= row["frac"] <= 1.8 * lim / 100, rows
         assert row["charged_ms"] > 0, rows        # the host bucket's debit is reported
+
+
+def test_four_symmetric_temporal_tenants_run_like_native(tmp):
+    """four 25 % decode tenants under the temporal governor
+    (policy force, no CU masks) against the same four processes native, in
+    the bench's own config.  Each tenant is charged its share of the resident
+    waves as ONE sampler per GPU reads them (the share board): four symmetric
+    tenants are charged ~25 % of the wall time each, so none is held beyond
+    noise -- the governed round runs within 3 % of native, fairly, and each
+    tenant's received GPU time is 25 +- 5 % of the wall time."""
+    r = _bench(["--rounds", "temporal,native", "--steps", "100", "--warmup", "5"], timeout=500)
+    gov = r["temporal_governor_rank0"]
+    print(json.dumps({"temporal": r["temporal_value"], "native": r["native_value"],
+                      "fairness": r["temporal_fairness_min_over_max"], "governor": gov}))
+    assert r["temporal_value"] >= 0.97 * r["native_value"], r
+    assert r["temporal_fairness_min_over_max"] >= 0.97, r
+    for g in gov:
+        assert g["gov_gates"] > 0, gov                                   # the governor ran
+        assert g["busy_share_pct"] is not None and 20.0 <= g["busy_share_pct"] <= 30.0, gov
+        assert (g.get("sampler") or {}).get("board_charged", 0) > 0, gov    # charged from the board
