@@ -48,6 +48,12 @@ def physical_gpu_for(local_rank: int) -> str:
     return str(local_rank)
 
 
+def _share_cus(cus: int) -> int:
+    from k8s_vgpu_scheduler_amd.device.amd.cu_alloc import CUTopology, share_unit
+    from k8s_vgpu_scheduler_amd.device.amd.device import AMDConfig
+    return share_unit(CUTopology(256, 8), cus or AMDConfig().cu_share_unit)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -75,8 +81,8 @@ def main():
     ap.add_argument("--layout", default="auto", choices=["auto", "hybrid", "disjoint"],
                     help="CU ranges of slices below a quarter GPU: shared ranges split by the governor "
                          "(hybrid) or disjoint ranges (auto = the allocator's default, cuShareSmall)")
-    ap.add_argument("--share-unit", type=int, default=64, metavar="CUS",
-                    help="CUs of one shared range in the hybrid layout (64 = a quarter, the allocator's)")
+    ap.add_argument("--share-unit", type=int, default=0, metavar="CUS",
+                    help="CUs of one shared range in the hybrid layout (0 = the allocator's cuShareUnit: a quarter)")
     ap.add_argument("--active-slices", type=int, default=0,
                     help="run only the first K of the --slices planned slices (same masks/limits; 0 = all)")
     ap.add_argument("--monitor", type=float, default=0.0, metavar="SECONDS",
@@ -318,7 +324,7 @@ def main():
                 # the grant's HIP_DEVICE_CORE_LIMIT: the CUs charged, as an exact share
                 "core_limit_pct_per_slice": [pct_text(sp.core_pct) for sp in head.get("specs", [])],
                 "isolation": (f"HSA_CU_MASK ({args.layout} layout"
-                              + (f", {args.share_unit}-CU shared ranges" if args.layout == "hybrid" else "")
+                              + (f", {_share_cus(args.share_unit)}-CU shared ranges" if args.layout == "hybrid" else "")
                               + ") + libmivgpu" if not args.no_spatial
                               else f"governor ({args.policy})")
                 + (f" + {args.hw_queues} HW queue/slice" if args.hw_queues and args.slices > 1 else ""),

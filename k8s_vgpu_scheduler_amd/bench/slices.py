@@ -73,8 +73,11 @@ def plan_slices(n: int, shim: bool, gpumem_mib: int | None, spatial: bool = True
     the allocator's default (``cuShareSmall``, off: disjoint)."""
     specs = []
     per = (MI355X_CUS // n) // MI355X_XCDS * MI355X_XCDS   # whole 8-CU granules: XCD-balanced
-    unit = share_unit
+    from k8s_vgpu_scheduler_amd.device.amd.cu_alloc import CUTopology
+    from k8s_vgpu_scheduler_amd.device.amd.cu_alloc import share_unit as _unit
     from k8s_vgpu_scheduler_amd.device.amd.device import AMDConfig
+    # 0: the allocator's shared-range size (cuShareUnit, a quarter by default)
+    unit = _unit(CUTopology(MI355X_CUS, MI355X_XCDS), share_unit or AMDConfig().cu_share_unit)
     hybrid = layout == "hybrid" or (layout == "auto" and AMDConfig().cu_share_small)
     if layout == "auto" and not AMDConfig().cu_partition:
         spatial = False   # the allocator's time-sharing mode: no CU ranges at all

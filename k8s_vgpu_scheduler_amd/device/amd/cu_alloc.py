@@ -131,8 +131,11 @@ def pick(used_bitmap: int, n: int, topo: CUTopology) -> list[tuple[int, int]] | 
 # isolate the pairs from each other spatially.
 
 
-def share_unit(topo: CUTopology) -> int:
-    """CUs of one shared range: a quarter of the GPU in whole granules."""
+def share_unit(topo: CUTopology, cus: int = 0) -> int:
+    """CUs of one shared range: ``cus`` rounded down to whole granules (at
+    least one, at most the GPU), or a quarter of the GPU when 0."""
+    if cus > 0:
+        return max(topo.xcds, min(topo.total, cus // topo.xcds * topo.xcds))
     return max(topo.xcds, topo.total // 4 // topo.xcds * topo.xcds)
 
 
@@ -165,12 +168,13 @@ def merge_shared(a: dict | None, b: dict | None) -> dict:
     return out
 
 
-def pick_shared(used_bitmap: int, shared_load: dict, n: int, topo: CUTopology) -> list[tuple[int, int]] | None:
+def pick_shared(used_bitmap: int, shared_load: dict, n: int, topo: CUTopology,
+                unit_cus: int = 0) -> list[tuple[int, int]] | None:
     """Range for a small request of ``n`` CUs (n < share_unit): the most loaded
     existing shared range it still fits in (best fit packs the ranges), else
-    a new quarter-sized range from the free granules.  ``shared_load``:
-    ``{range_key: CUs granted on it}``."""
-    unit = share_unit(topo)
+    a new range of ``share_unit(topo, unit_cus)`` CUs from the free granules.
+    ``shared_load``: ``{range_key: CUs granted on it}``."""
+    unit = share_unit(topo, unit_cus)
     if not 0 < n < unit:
         return None
     fits = [(load, key) for key, load in shared_load.items()

@@ -88,6 +88,10 @@ class AMDConfig:
     # 8511 tok/s (fairness 0.99) vs shared quarters 8457-8461 and the
     # temporal governor 8501 (profiles/README.md section 37)
     cu_share_small: bool = False
+    # CUs of one shared range for cuShareSmall (0 = a quarter of the GPU; 256 =
+    # every small request on the GPU shares one range, time-sliced by the
+    # governor, while requests of a share unit or more keep ranges of their own)
+    cu_share_unit: int = 0
     # False: no CU partitions at all -- a gpucores request is charged its
     # granules as before, but the container gets no HSA_CU_MASK and the shim's
     # temporal governor holds it to that charge (the reference's time-sharing
@@ -119,7 +123,7 @@ class AMDConfig:
              "xcdsPerDevice": "xcds_per_device", "cuLayout": "cu_layout",
              "deviceSplitCount": "device_split_count", "deviceMemoryScaling": "device_memory_scaling",
              "deviceCoreScaling": "device_core_scaling", "allowTenantOptOut": "allow_tenant_opt_out",
-             "cuShareSmall": "cu_share_small", "cuPartition": "cu_partition"}
+             "cuShareSmall": "cu_share_small", "cuShareUnit": "cu_share_unit", "cuPartition": "cu_partition"}
         kw = {}
         for k, v in (d or {}).items():
             if k in m:
@@ -523,9 +527,11 @@ class AMDDevices(D.Devices):
                 continue
             info = {}
             if 0 < cu < dev.totalcore and self.cfg.cu_partition:
-                if self.cfg.cu_share_small and cu < cu_alloc.share_unit(topo) and topo.xcds > 1:
+                unit = cu_alloc.share_unit(topo, int(self.cfg.cu_share_unit or 0))
+                if self.cfg.cu_share_small and cu < unit and topo.xcds > 1:
                     ranges = cu_alloc.pick_shared(dev.custominfo.get("cu_used", 0),
-                                                  dev.custominfo.get("cu_shared", {}), cu, topo)
+                                                  dev.custominfo.get("cu_shared", {}), cu, topo,
+                                                  int(self.cfg.cu_share_unit or 0))
                 else:
                     ranges = cu_alloc.pick(dev.custominfo.get("cu_used", 0), cu, topo)
                 if ranges is None:
