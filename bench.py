@@ -48,6 +48,31 @@ def physical_gpu_for(local_rank: int) -> str:
     return str(local_rank)
 
 
+def native_rccl_check(rank: int, world: int, local_rank: int, barrier) -> dict:
+    """Run mivgpu-rccl-check on every rank (untimed, after the slices): the
+    communicator id goes through a file named by the rendezvous port; rank 0's
+    view is reported (exit code, rows, failures)."""
+    import subprocess
+
+    from k8s_vgpu_scheduler_amd.utils import build
+    uid = f"/tmp/mivgpu-rccl-{os.environ.get('MASTER_PORT', '0')}.uid"
+    if rank == 0 and os.path.exists(uid):
+        os.unlink(uid)
+    barrier()
+    try:
+        r = subprocess.run([str(build.RCCL_CHECK), "--rank", str(rank), "--nranks", str(world), "--device",
+                            str(local_rank), "--uid", uid, "--sizes", "1048576,16777216,268435456", "--iters", "10",
+                            "--warmup", "3"], capture_output=True, text=True, timeout=300)
+    except subprocess.TimeoutExpired:
+        return {"rc": "timeout"}
+    rows = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    out = {"rc": r.returncode, "all_ok": r.returncode == 0 and bool(rows) and all(x["ok"] for x in rows),
+           "rows": [{k: x[k] for k in ("op", "bytes", "ms", "busbw_gbs", "ok")} for x in rows]}
+    if r.returncode:
+        out["stderr"] = r.stderr[-600:]
+    return out
+
+
 def _share_cus(cus: int) -> int:
     from k8s_vgpu_scheduler_amd.device.amd.cu_alloc import CUTopology, share_unit
     from k8s_vgpu_scheduler_amd.device.amd.device import AMDConfig
@@ -295,6 +320,12 @@ def main():
                       torch.device("cpu" if cpu else f"cuda:{local_rank}"))
         sizes = (64 << 10, 1 << 20) if cpu else (1 << 20, 16 << 20, 256 << 20)
         coll = [measure("all_reduce", nb, env, iters=10, warmup=3) for nb in sizes]
+    # ... and the native validator (csrc/bench/rccl_check.cpp): all-reduce,
+    # all-gather and reduce-scatter through librccl directly, every element
+    # checked, one child process per rank on this rank's GPU
+    rccl_native = None
+    if world > 1 and not args.no_collectives and not cpu and build.RCCL_CHECK.exists():
+        rccl_native = native_rccl_check(rank, world, local_rank, barrier)
 
     if rank == 0:
         head = results.get("shim") or results.get("native") or next(iter(results.values()))
@@ -394,6 +425,8 @@ def main():
             out["allreduce_between_gpus"] = [{k: r[k] for k in ("bytes", "us", "busbw_gbps", "correct")}
                                               for r in coll]
             out["allreduce_peak_busbw_gbps"] = max(r["busbw_gbps"] for r in coll)
+        if rccl_native is not None:
+            out["rccl_native_check"] = rccl_native
         line = json.dumps(out)
         print(line, flush=True)
         if args.out:
