@@ -171,7 +171,8 @@ case $suite in
     step 500 t8 python -u bench.py --slices 8 --rounds temporal,native --steps 600 --out "$out/t8.json" ;;
   board)
     # the share board (one occupancy sampler per GPU): 4 x 25 % temporal vs
-    # native, unequal limits, 8 x 12.5 % temporal, the time-sharing e2e test
+    # native, unequal limits, 8 x 12.5 % temporal; then the prefill attention
+    # A/B, the SMI / RCCL tests and the time-sharing e2e test
     step 400 t4 python -u bench.py --rounds temporal,native --steps 100 --out "$out/t4.json"
     step 300 alone python -u bench.py --slices 1 --mode shim --steps 300 --warmup 5 --out "$out/alone.json"
     step 400 u75 python -u bench.py --slices 2 --no-spatial --mode shim --policy force --slice-limits 75,25 \
@@ -179,24 +180,16 @@ case $suite in
     step 400 u50 python -u bench.py --slices 3 --no-spatial --mode shim --policy force --slice-limits 50,25,25 \
       --steps 300 --warmup 5 --out "$out/u50_25_25.json"
     step 400 t8 python -u bench.py --slices 8 --rounds temporal,native --steps 100 --out "$out/t8.json"
-    step 200 smi python -u -m pytest tests/test_smi_gpu.py tests/test_rccl_gpu.py -v -s --timeout 120 \
-      --timeout-method thread
-    step 300 e2e python -u -m pytest tests/test_e2e_gpu.py -v -s --timeout 240 --timeout-method thread \
-      -k time_sharing
     step 300 attn_tests python -u -m pytest tests/test_ops_gpu.py -v --timeout 120 --timeout-method thread \
       -k "prefill_flash or tr_read"
     step 200 fa8 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention --lens 512,2048,8192 --eager-max 0 \
       --out "$out/fa8.json"
     MIVGPU_FA_KERNEL=4 step 200 fa4 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention \
-      --lens 512,2048,8192 --eager-max 0 --out "$out/fa4.json" ;;
-  attn)
-    # prefill flash attention: numerics vs fp32, then the eight-wave kernel
-    # against the 32-key-tile one at 512 / 2048 / 8192 positions
-    step 300 tests python -u -m pytest tests/test_ops_gpu.py -v --timeout 120 --timeout-method thread -k "prefill_flash or tr_read"
-    step 200 fa8 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention --lens 512,2048,8192 --eager-max 0 \
-      --out "$out/fa8.json"
-    MIVGPU_FA_KERNEL=4 step 200 fa4 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention --lens 512,2048,8192 \
-      --eager-max 0 --out "$out/fa4.json" ;;
+      --lens 512,2048,8192 --eager-max 0 --out "$out/fa4.json"
+    step 200 smi python -u -m pytest tests/test_smi_gpu.py tests/test_rccl_gpu.py -v -s --timeout 120 \
+      --timeout-method thread
+    step 300 e2e python -u -m pytest tests/test_e2e_gpu.py -v -s --timeout 240 --timeout-method thread \
+      -k time_sharing ;;
   prefill)
     step 120 native python3 -m k8s_vgpu_scheduler_amd.bench.prefill
     HSA_CU_MASK=0:0-63 step 120 cu64 python3 -m k8s_vgpu_scheduler_amd.bench.prefill
