@@ -1,0 +1,190 @@
+// Prompt-sized ("prefill") GEMM on gfx950 matrix cores:  Y[M][N] = X[M][K] . W^T
+// with W in the decode kernels' fragment-packed layout (skinny_gemm.hip):
+//   16-byte chunk ((t*KB + kb)*4 + j)*64 + l  =  W[32t + (l&31)][64kb + 32(l>>5) + 8j .. +8]
+// so a slice keeps ONE copy of its weights: the library path it replaces
+// (PackedLinear.prompt) unpacked every projection into a row-major scratch
+// copy per call (read + write of the whole weight) before hipBLASLt, and ran
+// SiLU*up as a separate pass.
+//
+// Tile: 256 x 256 per workgroup, K in 64-wide k-blocks, 8 waves (2 per SIMD)
+// as 4 (M) x 2 (N), each wave 64 rows x 128 columns = 2 x 4 accumulators of
+// v_mfma_f32_32x32x16_bf16 (128 VGPRs).  Per k-block the workgroup stages X
+// [256][64] (row-major, 16-byte chunks XOR-swizzled by (row >> 1) & 7 so the
+// A-fragment ds_read_b128s of a 16-lane group hit distinct banks) and the
+// packed W of its 8 n-tiles (already in fragment order: every B-fragment read
+// is 64 lanes x 16 contiguous bytes) in LDS, double-buffered (128 KB); the next
+// k-block's 64 KB land in registers during this block's 32 MFMAs per wave and
+// go to the other buffer after them, one barrier per k-block.  Arithmetic
+// intensity 128 FLOP per staged byte: at the bf16 MFMA rate a CU takes in
+// ~75 GB/s, served from L2 / the Infinity Cache (X and W of one projection fit
+// in its 256 MB).  Workgroups are dealt to XCDs round-robin (b % 8); each
+// XCD's share is walked in groups of 4 M-panels across all N so its L2 holds
+// the panels it re-reads.
+//
+// Epilogues: store bf16, or SiLU(gate) * up for the interleaved gate/up
+// weight (n-tile 2c = gate rows, 2c+1 = up rows of channel block c: a wave's
+// 4 n-tiles are 2 whole pairs) -> Y[M][N/2].
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef uint16_t bf16_t;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+constexpr int PG_BM = 256, PG_BN = 256, PG_NT = PG_BN / 32;   // 8 n-tiles of 32 columns
+constexpr int PG_THREADS = 512;
+constexpr int PG_A_ELEMS = PG_BM * 64;                       // one X k-block: 32 KB
+constexpr int PG_W_CHUNKS = PG_NT * 256;                     // one W k-block: 8 tiles x 4 KB
+constexpr int PG_GM = 4;                                     // M-panels per XCD group
+
+__device__ __forceinline__ int a_off(int row, int c) { return row * 64 + ((c ^ ((row >> 1) & 7)) << 3); }
+
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(PG_THREADS, 2)
+prefill_gemm_kernel(const uint4* __restrict__ wp, const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int M,
+                    int K, int N, int ldx, int ldy) {
+  __shared__ __attribute__((aligned(16))) bf16_t as[2][PG_A_ELEMS];
+  __shared__ __attribute__((aligned(16))) uint4 ws[2][PG_W_CHUNKS];
+
+  // tile of this workgroup: XCD-grouped order (blocks b, b+8, ... share an XCD)
+  const int nM = (M + PG_BM - 1) / PG_BM, nN = N / PG_BN;
+  const int nb = nM * nN;
+  const int b = blockIdx.x;
+  const int per_xcd = (nb + 7) / 8;
+  int u = (b & 7) * per_xcd + (b >> 3);
+  if ((b & 7) * per_xcd + (b >> 3) >= nb || (b >> 3) >= per_xcd) u = b;   // ragged tail: identity
+  const int group = u / (PG_GM * nN), within = u % (PG_GM * nN);
+  const int gm = min(PG_GM, nM - group * PG_GM);
+  const int mb = group * PG_GM + within % gm, nbk = within / gm;
+  const int m0 = mb * PG_BM, t0 = nbk * PG_NT;                 // first row, first n-tile
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w & 3, wn = w >> 2;
+  const int r = lane & 31, h = lane >> 5;
+  const int KB = K >> 6;
+
+  // staging: 4 X chunks + 4 W chunks of 16 B per thread per k-block
+  uint4 xa0, xa1, xa2, xa3, wa0, wa1, wa2, wa3;
+  const int q0 = tid, q1 = tid + PG_THREADS, q2 = tid + 2 * PG_THREADS, q3 = tid + 3 * PG_THREADS;
+  auto xsrc = [&](int q, int kb) {
+    const int row = min(m0 + (q >> 3), M - 1);   // rows past M: never stored
+    return reinterpret_cast<const uint4*>(x + (size_t)row * ldx + kb * 64 + (q & 7) * 8);
+  };
+  auto wsrc = [&](int q, int kb) { return wp + ((size_t)(t0 + (q >> 8)) * KB + kb) * 256 + (q & 255); };
+  auto load = [&](int kb) {
+    xa0 = *xsrc(q0, kb);
+    xa1 = *xsrc(q1, kb);
+    xa2 = *xsrc(q2, kb);
+    xa3 = *xsrc(q3, kb);
+    wa0 = *wsrc(q0, kb);
+    wa1 = *wsrc(q1, kb);
+    wa2 = *wsrc(q2, kb);
+    wa3 = *wsrc(q3, kb);
+  };
+  auto store = [&](int buf) {
+    *reinterpret_cast<uint4*>(&as[buf][a_off(q0 >> 3, q0 & 7)]) = xa0;
+    *reinterpret_cast<uint4*>(&as[buf][a_off(q1 >> 3, q1 & 7)]) = xa1;
+    *reinterpret_cast<uint4*>(&as[buf][a_off(q2 >> 3, q2 & 7)]) = xa2;
+    *reinterpret_cast<uint4*>(&as[buf][a_off(q3 >> 3, q3 & 7)]) = xa3;
+    ws[buf][q0] = wa0;
+    ws[buf][q1] = wa1;
+    ws[buf][q2] = wa2;
+    ws[buf][q3] = wa3;
+  };
+
+  f32x16_t acc[2][4];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[mt][i][e] = 0.f;
+
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kb = 0; kb < KB; ++kb) {
+    const int buf = kb & 1;
+    if (kb + 1 < KB) load(kb + 1);
+    const bf16_t* a_l = as[buf];
+    const uint4* w_l = ws[buf];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bf16x8_t af[2], bfr[4];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+        af[mt] = *reinterpret_cast<const bf16x8_t*>(&a_l[a_off(wm * 64 + mt * 32 + r, j + 4 * h)]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bfr[i] = __builtin_bit_cast(bf16x8_t, w_l[(wn * 4 + i) * 256 + j * 64 + lane]);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[mt][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mt], bfr[i], acc[mt][i], 0, 0, 0);
+    }
+    if (kb + 1 < KB) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds column r of each 32x32 tile, rows (e&3) + 8(e>>2) + 4h
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int rbase = m0 + wm * 64 + mt * 32 + 4 * h;
+    if constexpr (EPI == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int col = (t0 + wn * 4 + i) * 32 + r;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = rbase + (e & 3) + 8 * (e >> 2);
+          if (row < M) y[(size_t)row * ldy + col] = f2bf(acc[mt][i][e]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int c = (t0 + wn * 4) / 2 + p;          // channel block of the gate/up pair
+        const int col = c * 32 + r;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = rbase + (e & 3) + 8 * (e >> 2);
+          const float g = acc[mt][2 * p][e], up = acc[mt][2 * p + 1][e];
+          if (row < M) y[(size_t)row * ldy + col] = f2bf(g / (1.f + __expf(-g)) * up);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Y[M][N] (epi 0) or Y[M][N/2] = SiLU(gate) * up (epi 1, interleaved gate/up
+// weight) from X[M][K] (row stride ldx) and the fragment-packed W (tile-major
+// layout only).  N a multiple of 256, K of 64; any M >= 1.
+int mivgpu_prefill_gemm(const void* wp, const void* x, void* y, int M, int K, int N, int ldx, int ldy, int epi,
+                        hipStream_t s) {
+  if (M <= 0 || K <= 0 || (K & 63) || N <= 0 || (N % PG_BN) || ldx < K || (ldx & 7) || (epi != 0 && epi != 1))
+    return (int)hipErrorInvalidValue;
+  if (ldy < (epi ? N / 2 : N)) return (int)hipErrorInvalidValue;
+  const int blocks = ((M + PG_BM - 1) / PG_BM) * (N / PG_BN);
+  if (epi == 0)
+    hipLaunchKernelGGL(prefill_gemm_kernel<0>, dim3(blocks), dim3(PG_THREADS), 0, s, (const uint4*)wp,
+                       (const bf16_t*)x, (bf16_t*)y, M, K, N, ldx, ldy);
+  else
+    hipLaunchKernelGGL(prefill_gemm_kernel<1>, dim3(blocks), dim3(PG_THREADS), 0, s, (const uint4*)wp,
+                       (const bf16_t*)x, (bf16_t*)y, M, K, N, ldx, ldy);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -54,6 +54,7 @@ def lib():
         L.mivgpu_hwid_probe.argtypes = [vp, i, vp]
         L.mivgpu_pack_weight.argtypes = [vp, vp, i, i, vp]
         L.mivgpu_unpack_weight.argtypes = [vp, vp, i, i, i, vp]
+        L.mivgpu_prefill_gemm.argtypes = [vp, vp, vp, i, i, i, i, i, i, vp]
         L.mivgpu_skinny_gemm.argtypes = [vp, vp, vp, i, i, i, i, i, i, i, i, i, i, vp, vp, vp]
         L.mivgpu_skinny_gemm_norm.argtypes = [vp, vp, vp, i, i, i, i, i, i, i, i, i, i, vp, vp, vp, i, f, f, vp, vp]
         ip, lp = ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_longlong)
@@ -71,7 +72,8 @@ def lib():
                    "mivgpu_stream_copy", "mivgpu_stream_read", "mivgpu_ops_visible_cus",
                    "mivgpu_ops_kv_packed", "mivgpu_decode_attention_fused", "mivgpu_skinny_gemm_norm",
                    "mivgpu_prefill_qk_norm_rope_kv", "mivgpu_prefill_attention", "mivgpu_unpack_weight",
-                   "mivgpu_decode_chain", "mivgpu_chain_counter_words", "mivgpu_chain_err_word"):
+                   "mivgpu_decode_chain", "mivgpu_chain_counter_words", "mivgpu_chain_err_word",
+                   "mivgpu_prefill_gemm"):
             getattr(L, fn).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -504,6 +506,30 @@ EPI_RESID = 2
 SS_ROWS = 128   # rows per sum-of-squares slot (csrc/ops/skinny_gemm.hip SS_ROWS)
 
 
+def prefill_gemm_ok(N: int, K: int) -> bool:
+    """The native prefill GEMM takes this weight (tile-major packing, N a
+    multiple of 256, K of 64) and is not switched off (MIVGPU_PREFILL_GEMM=lib)."""
+    return (os.environ.get("MIVGPU_PREFILL_GEMM", "native") != "lib" and N % 256 == 0 and K % 64 == 0
+            and os.environ.get("MIVGPU_SKINNY_KMAJOR", "0") in ("", "0", "-1"))
+
+
+def prefill_gemm(wp: torch.Tensor, x: torch.Tensor, N: int, K: int, silu_mul: bool = False,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+    """Y = X . W^T (or SiLU(gate) * up of an interleaved gate/up weight) for
+    prompt-sized X [M, K] bf16 against the fragment-packed W (pack_weight)."""
+    if x.dtype != torch.bfloat16 or x.dim() != 2 or x.shape[1] != K or x.stride(1) != 1:
+        raise ValueError(f"prefill_gemm: X must be [M, {K}] bf16 with unit column stride, got {tuple(x.shape)}")
+    M = x.shape[0]
+    cols = N // 2 if silu_mul else N
+    if out is None:
+        out = torch.empty(M, cols, dtype=torch.bfloat16, device=x.device)
+    if out.shape[0] < M or out.shape[1] < cols or out.stride(1) != 1:
+        raise ValueError("prefill_gemm: out too small")
+    _check(lib().mivgpu_prefill_gemm(_p(wp), _p(x), _p(out), M, K, N, x.stride(0), out.stride(0),
+                                     1 if silu_mul else 0, _stream()), "prefill_gemm")
+    return out
+
+
 class PackedLinear:
     """A weight held only in packed form, applied with the skinny MFMA GEMM.
 
@@ -575,11 +601,15 @@ class PackedLinear:
         return out
 
     def prompt(self, x: torch.Tensor) -> torch.Tensor:
-        """X . W^T for prompt-sized X (hundreds to thousands of rows): the packed
-        weight unpacked once into the shared scratch, then the library GEMM
-        (hipBLASLt) -- instead of re-streaming the packed weight once per
-        128-row chunk.  SiLU*up for a gate/up weight.  (A folded col_scale
-        stays folded: the caller normalises X without a weight.)"""
+        """X . W^T for prompt-sized X (hundreds to thousands of rows), SiLU*up
+        for a gate/up weight.  (A folded col_scale stays folded: the caller
+        normalises X without a weight.)  The hand-written prefill GEMM
+        (csrc/ops/prefill_gemm.hip) reads the packed weight directly, SiLU*up
+        in its epilogue; MIVGPU_PREFILL_GEMM=lib (or a shape it does not take)
+        unpacks the weight into the shared scratch and runs the library GEMM
+        (hipBLASLt) instead."""
+        if prefill_gemm_ok(self.N, self.K):
+            return prefill_gemm(self.wp, x, self.N, self.K, silu_mul=self.silu_mul)
         w = unpack_weight(self.wp, self.N, self.K, unpack_scratch(self.N * self.K, self.wp.device),
                           deinterleave=self.silu_mul)
         y = torch.nn.functional.linear(x, w)

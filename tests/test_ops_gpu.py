@@ -787,3 +787,36 @@ def test_decoder_chain_8b_layers_graph(monkeypatch):
         ch.tokens.copy_(ref_dec.tokens)
     assert not ch._chains[0].gave_up()
     assert int(ch._chains[0].ctr.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("M,K,N,silu", [(256, 128, 256, False), (100, 4096, 512, False), (1000, 4096, 6144, False),
+                                        (2048, 12288, 4096, False), (300, 4096, 1024, True),
+                                        (2048, 4096, 24576, True)])
+def test_prefill_gemm_vs_fp32(ops, M, K, N, silu):
+    """The hand-written prefill GEMM (csrc/ops/prefill_gemm.hip) on the
+    fragment-packed weight vs the fp32 product of the plain weight: ragged M,
+    every Qwen3-8B projection shape, SiLU*up on the interleaved gate/up
+    weight (the decode kernels' packing, ops.interleave_gate_up)."""
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    x = (torch.randn(M, K, generator=g, device="cuda") * 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=g, device="cuda") * 0.02).to(torch.bfloat16)
+    wp = ops.pack_weight(ops.interleave_gate_up(w) if silu else w)
+    out = ops.prefill_gemm(wp, x, N, K, silu_mul=silu)
+    want = x.float() @ w.float().t()
+    if silu:
+        gate, up = want[:, :N // 2], want[:, N // 2:]
+        want = torch.nn.functional.silu(gate) * up
+    assert out.shape == want.shape and torch.isfinite(out.float()).all()
+    _close(out, want, 2e-2)
+
+
+def test_prefill_gemm_strided_rows(ops):
+    """X and Y with row strides wider than K / N (views into bigger buffers)."""
+    M, K, N = 300, 256, 512
+    big = torch.randn(M, K + 64, device="cuda").to(torch.bfloat16)
+    x = big[:, :K]
+    w = (torch.randn(N, K, device="cuda") * 0.05).to(torch.bfloat16)
+    ybuf = torch.zeros(M, N + 32, device="cuda", dtype=torch.bfloat16)
+    ops.prefill_gemm(ops.pack_weight(w), x, N, K, out=ybuf[:, :N])
+    _close(ybuf[:, :N], x.float() @ w.float().t(), 2e-2)
+    assert (ybuf[:, N:] == 0).all()
