@@ -22,7 +22,7 @@
 #   serving     TTFT / per-token latency, native vs vGPU slices (bench/serving.py)
 #   mixed       governed server + 3 governed decode tenants; 8 x 12 % temporal over 600 steps
 #   board       share board: 4 x 25 % / 8 x 12.5 % temporal vs native, unequal limits, time-sharing e2e
-#   attn        prefill flash attention: tests, eight-wave vs 32-key-tile kernel at 512 / 2048 / 8192
+#   kern        prefill kernels: flash attention A/B at 512 / 2048 / 8192, packed-weight GEMM vs hipBLASLt
 #   prefill     prefill microbench + rocprofv3 kernel summary, whole GPU and 64 CUs
 # Results go to gpurun_out/<suite>/ (copy the ones to keep into profiles/).
 set -o pipefail
@@ -171,8 +171,8 @@ case $suite in
     step 500 t8 python -u bench.py --slices 8 --rounds temporal,native --steps 600 --out "$out/t8.json" ;;
   board)
     # the share board (one occupancy sampler per GPU): 4 x 25 % temporal vs
-    # native, unequal limits, 8 x 12.5 % temporal; then the prefill attention
-    # A/B, the SMI / RCCL tests and the time-sharing e2e test
+    # native, unequal limits, 8 x 12.5 % temporal; then the SMI / RCCL tests
+    # and the time-sharing e2e test
     step 400 t4 python -u bench.py --rounds temporal,native --steps 100 --out "$out/t4.json"
     step 300 alone python -u bench.py --slices 1 --mode shim --steps 300 --warmup 5 --out "$out/alone.json"
     step 400 u75 python -u bench.py --slices 2 --no-spatial --mode shim --policy force --slice-limits 75,25 \
@@ -180,16 +180,20 @@ case $suite in
     step 400 u50 python -u bench.py --slices 3 --no-spatial --mode shim --policy force --slice-limits 50,25,25 \
       --steps 300 --warmup 5 --out "$out/u50_25_25.json"
     step 400 t8 python -u bench.py --slices 8 --rounds temporal,native --steps 100 --out "$out/t8.json"
-    step 300 attn_tests python -u -m pytest tests/test_ops_gpu.py -v --timeout 120 --timeout-method thread \
-      -k "prefill_flash or tr_read"
-    step 200 fa8 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention --lens 512,2048,8192 --eager-max 0 \
-      --out "$out/fa8.json"
-    MIVGPU_FA_KERNEL=4 step 200 fa4 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention \
-      --lens 512,2048,8192 --eager-max 0 --out "$out/fa4.json"
     step 200 smi python -u -m pytest tests/test_smi_gpu.py tests/test_rccl_gpu.py -v -s --timeout 120 \
       --timeout-method thread
     step 300 e2e python -u -m pytest tests/test_e2e_gpu.py -v -s --timeout 240 --timeout-method thread \
       -k time_sharing ;;
+  kern)
+    # prefill kernels: flash attention (eight-wave vs 32-key-tile kernel) and
+    # the packed-weight GEMM (vs unpack + hipBLASLt), numerics then timing
+    step 300 tests python -u -m pytest tests/test_ops_gpu.py -v --timeout 120 --timeout-method thread \
+      -k "prefill_flash or tr_read or prefill_gemm"
+    step 200 fa8 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention --lens 512,2048,8192 --eager-max 0 \
+      --out "$out/fa8.json"
+    MIVGPU_FA_KERNEL=4 step 200 fa4 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention --lens 512,2048,8192 \
+      --eager-max 0 --out "$out/fa4.json"
+    step 300 pgemm python -u -m k8s_vgpu_scheduler_amd.bench.prefill_gemm --rows 2048,8192 --out "$out/pgemm.json" ;;
   prefill)
     step 120 native python3 -m k8s_vgpu_scheduler_amd.bench.prefill
     HSA_CU_MASK=0:0-63 step 120 cu64 python3 -m k8s_vgpu_scheduler_amd.bench.prefill
