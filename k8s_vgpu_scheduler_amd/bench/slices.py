@@ -81,7 +81,8 @@ def plan_slices(n: int, shim: bool, gpumem_mib: int | None, spatial: bool = True
     hybrid = layout == "hybrid" or (layout == "auto" and AMDConfig().cu_share_small)
     if layout == "auto" and not AMDConfig().cu_partition:
         spatial = False   # the allocator's time-sharing mode: no CU ranges at all
-    share = unit // per if (hybrid and 0 < per < unit) else 1
+    quarter = _unit(CUTopology(MI355X_CUS, MI355X_XCDS))
+    share = unit // per if (hybrid and 0 < per < quarter and per < unit) else 1
     for i in range(n):
         if share > 1:
             q = i // share

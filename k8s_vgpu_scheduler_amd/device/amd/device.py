@@ -527,8 +527,9 @@ class AMDDevices(D.Devices):
                 continue
             info = {}
             if 0 < cu < dev.totalcore and self.cfg.cu_partition:
-                unit = cu_alloc.share_unit(topo, int(self.cfg.cu_share_unit or 0))
-                if self.cfg.cu_share_small and cu < unit and topo.xcds > 1:
+                # small = below a quarter of the GPU; the range it shares is
+                # cuShareUnit CUs wide (a quarter by default)
+                if self.cfg.cu_share_small and cu < cu_alloc.share_unit(topo) and topo.xcds > 1:
                     ranges = cu_alloc.pick_shared(dev.custominfo.get("cu_used", 0),
                                                   dev.custominfo.get("cu_shared", {}), cu, topo,
                                                   int(self.cfg.cu_share_unit or 0))
