@@ -367,6 +367,28 @@ def test_small_slice_env_time_slices_its_shared_range(cluster, share_small):
     assert codec.ranges_count([tuple(map(int, r.split("-"))) for r in lo_hi.split(",")]) == 64
 
 
+def test_small_slices_pool_into_one_wide_range(cluster, share_small):
+    """cuShareUnit: 256 -- every sub-quarter request on the GPU shares ONE
+    whole-GPU range (time-sliced by the governor, the share board charging
+    each its share), while a quarter-or-larger request keeps a range of its
+    own: once the small pods took the pool, a 25 % pod no longer fits."""
+    from k8s_vgpu_scheduler_amd.device import devices as D
+    cfg = D.get_devices()["AMD"].cfg
+    cfg.cu_share_unit = 256
+    try:
+        s = make_sched(cluster, [amd_node("n1", n=1)])
+        keys = set()
+        for i in range(4):
+            assert filt(s, cluster, amd_pod(f"p{i}", mem=8192, cores=12), ["n1"])["NodeNames"] == ["n1"], i
+            cus, ranges = _ranges_of(cluster, f"p{i}")
+            assert cus == 32 and codec.ranges_count(ranges) == 256
+            keys.add(cu_alloc.range_key(ranges))
+        assert len(keys) == 1
+        assert not filt(s, cluster, amd_pod("big", mem=8192, cores=25), ["n1"]).get("NodeNames")
+    finally:
+        cfg.cu_share_unit = 0
+
+
 def test_share_small_off_keeps_disjoint_ranges(cluster):
     """The default: a sub-quarter request gets a disjoint range of its own."""
     s = make_sched(cluster, [amd_node("n1", n=1)])
