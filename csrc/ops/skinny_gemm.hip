@@ -1020,9 +1020,9 @@ __global__ void __launch_bounds__(64 * WV) skinny_wide_kernel(GemmP p) {
 // scales the rows of a store by the producer's slots (rs_issue / rs_finish).
 // NT = 2 with EPI_SILU_MUL: a gate tile and its up tile (gate_up), both
 // carried by every k-wave, SiLU(gate)*up by the reducing wave.
-template <int MT, int NT, int KW, int EPI>
+template <int MT, int NT, int KW, int EPI, int UU = 2>
 struct WidekLds {
-  static constexpr int U = 2;                        // k-blocks per wave per group
+  static constexpr int U = UU;                       // k-blocks per wave per group
   static constexpr int GK = KW * U;                  // k-blocks per group (the X tile)
   static constexpr int PITCH = GK * 64 + 8;          // +16 B per row: conflict-free ds_read_b128
   static constexpr int XBUF = MT * 32 * PITCH;
@@ -1034,13 +1034,13 @@ struct WidekLds {
   alignas(16) bf16_t s_res[EPI == EPI_RESID ? MT * 32 * 32 : 8];
 };
 
-template <int MT, int NT, int KW, int EPI, bool COMB, class Deps, bool DMAX = false>
-__device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<MT, NT, KW, EPI>& L,
+template <int MT, int NT, int KW, int EPI, bool COMB, class Deps, bool DMAX = false, int UU = 2>
+__device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<MT, NT, KW, EPI, UU>& L,
                                            const XComb& xcomb, const Deps& deps) {
   static_assert((EPI == EPI_SILU_MUL) == (NT == 2) && NT <= 2, "widek: one tile, or a gate/up pair for SiLU*up");
   static_assert(!(COMB && Deps::chained), "the X-combine variant runs standalone");
-  static_assert(!DMAX || (!COMB && !Deps::chained && KW == 4), "LDS-DMA X: standalone, 4 k-waves");
-  using LD = WidekLds<MT, NT, KW, EPI>;
+  static_assert(!DMAX || (!COMB && !Deps::chained && KW == 4 && UU == 2), "LDS-DMA X: standalone, 4 k-waves");
+  using LD = WidekLds<MT, NT, KW, EPI, UU>;
   constexpr int U = LD::U;
   constexpr int GK = LD::GK;
   constexpr int PITCH = LD::PITCH;
@@ -1252,10 +1252,10 @@ __device__ __forceinline__ void widek_body(const GemmP& p, int block, WidekLds<M
   deps.publish(vgroup);
 }
 
-template <int MT, int NT, int KW, int EPI, bool COMB = false, bool DMAX = false>
+template <int MT, int NT, int KW, int EPI, bool COMB = false, bool DMAX = false, int UU = 2>
 __global__ void __launch_bounds__(64 * KW) skinny_widek_kernel(GemmP p, XComb xcomb) {
-  __shared__ WidekLds<MT, NT, KW, EPI> lds;
-  widek_body<MT, NT, KW, EPI, COMB, NoDeps, DMAX>(p, blockIdx.x, lds, xcomb, NoDeps{});
+  __shared__ WidekLds<MT, NT, KW, EPI, UU> lds;
+  widek_body<MT, NT, KW, EPI, COMB, NoDeps, DMAX, UU>(p, blockIdx.x, lds, xcomb, NoDeps{});
 }
 
 // ============================================================================
@@ -1561,6 +1561,15 @@ hipError_t launch_wide_resid(int mt, int wv, const Args& a, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
+// k-blocks per wave per group of the K-split kernel (MIVGPU_WIDEK_U, A/B): 2 or 4
+int widek_u() {
+  static const int u = [] {
+    const char* e = getenv("MIVGPU_WIDEK_U");
+    return e && atoi(e) == 4 ? 4 : 2;
+  }();
+  return u;
+}
+
 template <int MT, int NT, int EPI>
 hipError_t launch_widek(int kw, const Args& a, hipStream_t s) {
   const int blocks = (a.N / 32) / NT * a.S;
@@ -1588,6 +1597,16 @@ hipError_t launch_widek(int kw, const Args& a, hipStream_t s) {
     hipLaunchKernelGGL((skinny_widek_kernel<MT, NT, 4, EPI, false, true>), dim3(blocks), dim3(256), 0, s, gemm_p(a),
                        a.xcomb);
     return hipGetLastError();
+  }
+  // MIVGPU_WIDEK_U=4 (A/B): four k-blocks per wave per group instead of two --
+  // twice the weight bytes in flight per workgroup (16 KB per wave), one X
+  // tile of 16 k-blocks per group (two 66 KB buffers: one M-tile, 4 k-waves)
+  if constexpr (MT == 1 && NT == 1) {
+    if (kw == 4 && widek_u() == 4) {
+      hipLaunchKernelGGL((skinny_widek_kernel<1, 1, 4, EPI, false, false, 4>), dim3(blocks), dim3(256), 0, s,
+                         gemm_p(a), a.xcomb);
+      return hipGetLastError();
+    }
   }
   switch (kw) {
     case 2: MIVGPU_LAUNCH_WIDEK(2, false); break;
@@ -1766,7 +1785,7 @@ bool plan_widek(int M, int K, int N, int epi, int* nt, int* kw, int* S) {
     *kw = (env == 8 && M <= 32) || env == 2 || env == 4 ? env : 4;
   }
   if (*kw != 2 && *kw != 4 && !(*kw == 8 && M <= 32)) return false;
-  const int KB = K / 64, GK = *kw * 2;
+  const int KB = K / 64, GK = *kw * ((*kw == 4 && M <= 32 && epi == EPI_STORE) ? widek_u() : 2);
   // no inter-workgroup split by default: measured on the whole chip (bench/gemm.py,
   // profiles/round3/widek_gemm.json) S = 2 costs qkv 13.6 -> 19.1 us and o_proj
   // 12.2 -> 15.6 us at 32 rows (the atomics + last-arriver tail)

@@ -22,7 +22,8 @@
 #   serving     TTFT / per-token latency, native vs vGPU slices (bench/serving.py)
 #   mixed       governed server + 3 governed decode tenants; 8 x 12 % temporal over 600 steps
 #   board       share board: 4 x 25 % / 8 x 12.5 % temporal vs native, unequal limits, time-sharing e2e
-#   kern        prefill kernels: flash attention A/B at 512 / 2048 / 8192, packed-weight GEMM vs hipBLASLt
+#   kern        prefill kernels: flash attention A/B at 512 / 2048 / 8192, packed-weight GEMM vs hipBLASLt;
+#               decode K-split GEMM two vs four k-blocks per group
 #   prefill     prefill microbench + rocprofv3 kernel summary, whole GPU and 64 CUs
 # Results go to gpurun_out/<suite>/ (copy the ones to keep into profiles/).
 set -o pipefail
@@ -193,7 +194,16 @@ case $suite in
       --out "$out/fa8.json"
     MIVGPU_FA_KERNEL=4 step 200 fa4 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention --lens 512,2048,8192 \
       --eager-max 0 --out "$out/fa4.json"
-    step 300 pgemm python -u -m k8s_vgpu_scheduler_amd.bench.prefill_gemm --rows 2048,8192 --out "$out/pgemm.json" ;;
+    step 300 pgemm python -u -m k8s_vgpu_scheduler_amd.bench.prefill_gemm --rows 2048,8192 --out "$out/pgemm.json"
+    # decode K-split GEMM: two vs four k-blocks per wave per group (MIVGPU_WIDEK_U)
+    MIVGPU_WIDEK_U=4 step 300 widek_u4_tests python -u -m pytest tests/test_ops_gpu.py -v --timeout 120 \
+      --timeout-method thread -k "widek"
+    for u in 2 4; do
+      MIVGPU_WIDEK_U=$u step 300 "gemm_u$u" python -u -m k8s_vgpu_scheduler_amd.bench.gemm --shapes qkv,o_proj,down \
+        --batches 1,32 --out "$out/gemm_u$u.json"
+      MIVGPU_WIDEK_U=$u step 300 "dec_u$u" python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 200
+      MIVGPU_WIDEK_U=$u step 300 "dec_b1_u$u" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 1 --steps 200
+    done ;;
   prefill)
     step 120 native python3 -m k8s_vgpu_scheduler_amd.bench.prefill
     HSA_CU_MASK=0:0-63 step 120 cu64 python3 -m k8s_vgpu_scheduler_amd.bench.prefill
