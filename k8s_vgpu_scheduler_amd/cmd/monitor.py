@@ -56,6 +56,9 @@ def main(argv=None):
                          "GPU only the governor limits (time-sharing) is evicted / killed after --over-grant-passes "
                          "passes whatever --over-grant-action says (default: evict; kill under "
                          "--over-grant-action kill)")
+    ap.add_argument("--proc-root", default="/proc",
+                    help="process table the host-truth pass maps pods to host pids from (a directory laid out like "
+                         "/proc: <pid>/status and <pid>/cgroup; the e2e tests point it at a copy naming pod cgroups)")
     ap.add_argument("--over-grant-passes", type=int, default=3,
                     help="consecutive over-grant passes before --over-grant-action evict/kill")
     ap.add_argument("--board-period-us", type=int, default=2000,
@@ -88,7 +91,7 @@ def main(argv=None):
         from k8s_vgpu_scheduler_amd.monitor.hosttruth import HostTruth, kfd_gpu_ids
         from k8s_vgpu_scheduler_amd.scheduler.events import EventRecorder
         events = EventRecorder(client, component="hami-vgpu-monitor")
-        truth = HostTruth(kfd_gpu_ids(backend), events=events)
+        truth = HostTruth(kfd_gpu_ids(backend), events=events, proc_root=a.proc_root)
         escalation = OverGrantPolicy(a.over_grant_action, a.over_grant_passes, client=client, events=events,
                                      shimless_action=a.shimless_action)
     reg = CollectorRegistry()

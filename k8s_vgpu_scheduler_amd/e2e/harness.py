@@ -219,12 +219,13 @@ class E2ECluster:
 
     def __init__(self, workdir: str | None = None, node: str = "node1", smi_backend: str = "fake",
                  fake_gpus: int = 2, split: int = 4, extra_env: dict | None = None, log_level: int = 3,
-                 device_config: dict | None = None):
+                 device_config: dict | None = None, monitor_args: list[str] | None = None):
         self.dir = Path(workdir or tempfile.mkdtemp(prefix="mivgpu-e2e-"))
         self.node, self.smi_backend, self.fake_gpus, self.split = node, smi_backend, fake_gpus, split
         self.extra_env = extra_env or {}
         self.log_level = log_level
         self.device_config = device_config   # the scheduler's --device-config-file contents ({"amd": {...}})
+        self.monitor_args = list(monitor_args or [])   # extra mivgpu-monitor flags
         self.procs: dict[str, subprocess.Popen] = {}
         self.ports = {k: free_port() for k in ("http", "sched_metrics", "mon_metrics")}
         self.hook = self.dir / "hook"
@@ -265,7 +266,8 @@ class E2ECluster:
             wait_for(lambda: (self.hook / "vgpu" / "ld.so.preload").exists(), 60, "device plugin install")
             self._spawn("monitor", [*kc, "--node-name", self.node, "--hook-path", str(self.hook),
                                     "--metrics-bind-address", f"127.0.0.1:{self.ports['mon_metrics']}",
-                                    "--smi-backend", self.smi_backend, "-v", str(self.log_level)])
+                                    "--smi-backend", self.smi_backend, "-v", str(self.log_level),
+                                    *self.monitor_args])
             wait_for(lambda: requests.get(self.url("/healthz"), timeout=2).ok, 60, "scheduler /healthz")
             wait_for(lambda: self.kubelet.registrations, 60, "device plugin registration with the kubelet")
             wait_for(lambda: "hami.io/node-amd-register" in

@@ -184,7 +184,7 @@ case $suite in
     step 200 smi python -u -m pytest tests/test_smi_gpu.py tests/test_rccl_gpu.py -v -s --timeout 120 \
       --timeout-method thread
     step 300 e2e python -u -m pytest tests/test_e2e_gpu.py -v -s --timeout 240 --timeout-method thread \
-      -k time_sharing ;;
+      -k "time_sharing or shimless" ;;
   kern)
     # prefill kernels: flash attention (eight-wave vs 32-key-tile kernel) and
     # the packed-weight GEMM (vs unpack + hipBLASLt), numerics then timing

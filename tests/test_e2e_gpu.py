@@ -173,3 +173,48 @@ def test_time_sharing_mode_on_the_real_node(tmp_path_factory):
         bd = (held.get("sampler") or {}).get("board") or {}
         assert bd.get("owner_kind") == 1 and not bd.get("owner") and held["sampler"]["board_charged"] > 0, diag
         cl.delete_pod("default", "ts")
+
+
+def test_shimless_container_on_time_shared_gpu_is_evicted(tmp_path_factory):
+    """under cuPartition: false nothing but the governor
+    limits a fractional container's compute, so a container that runs without
+    the preload (its image ignored /etc/ld.so.preload) is evicted by the
+    monitor within --over-grant-passes (3) feedback passes, although the
+    over-grant action is the default block.  The monitor maps the pod to its
+    host pids from the cgroup (hostpid.py); this box runs the "container" as a
+    plain process, so the test hands the monitor a process table in which that
+    process's cgroup names the pod."""
+    import os
+    import time
+    root = tmp_path_factory.mktemp("e2e-shimless")
+    procs = root / "proc"
+    procs.mkdir()
+    with E2ECluster(str(root / "cl"), smi_backend="amdsmi", split=8, device_config={"amd": {"cuPartition": False}},
+                    monitor_args=["--proc-root", str(procs)]) as cl:
+        cl.submit(amd_pod("rogue", mem=8192, cores=12))
+        assert cl.schedule("default", "rogue") == "node1"
+        alloc = cl.start_containers("default", "rogue")[0]
+        uid = cl.api.cluster.get("pods", "rogue", "default")["metadata"]["uid"]
+        env = container_env(alloc)
+        env["PYTHONPATH"] = str(REPO)
+        env.pop("LD_PRELOAD", None)
+        p = _probe(env, "matmul", "--n", "2048", "--iters", "50", "--oom-probe-mib", "2048", "--hold-s", "90",
+                   wait=False)
+        try:
+            d = procs / str(p.pid)
+            d.mkdir()
+            (d / "status").write_text(f"Name:\tpython\nNSpid:\t{p.pid}\n")
+            (d / "cgroup").write_text(f"0::/kubepods.slice/kubepods-burstable.slice/pod{uid}/cri-rogue\n")
+            t0 = time.monotonic()
+            wait_for(lambda: os.path.exists(f"/sys/class/kfd/kfd/proc/{p.pid}"), 120, "the probe to open the GPU")
+            seen = time.monotonic()
+            wait_for(lambda: ("default", "rogue") in cl.api.cluster.evictions, 60,
+                     "the monitor to evict the shimless pod")
+            took = time.monotonic() - seen
+            print(json.dumps({"evicted_after_s": round(took, 1), "since_start_s": round(time.monotonic() - t0, 1)}))
+            # the first pass after the GPU open, then at most 3 more 5 s passes
+            assert took <= 4 * 5 + 3, took
+            assert "VGPUShimlessEvicted" in cl.logs("monitor") or "without libmivgpu.so" in cl.logs("monitor")
+        finally:
+            p.kill()
+            p.communicate()
