@@ -195,6 +195,12 @@ case $suite in
     MIVGPU_FA_KERNEL=4 step 200 fa4 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention --lens 512,2048,8192 \
       --eager-max 0 --out "$out/fa4.json"
     step 300 pgemm python -u -m k8s_vgpu_scheduler_amd.bench.prefill_gemm --rows 2048,8192 --out "$out/pgemm.json"
+    # 8k-token TTFT (<= 120 ms), whole GPU and a 50 % (128-CU) slice, packed GEMM vs library
+    step 300 ttft8k python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 --ctx 9216 --iters 5
+    HSA_CU_MASK=0:0-127 step 300 ttft8k_cu128 python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 \
+      --ctx 9216 --iters 5
+    MIVGPU_PREFILL_GEMM=lib step 300 ttft8k_lib python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 \
+      --ctx 9216 --iters 5
     # decode K-split GEMM: two vs four k-blocks per wave per group (MIVGPU_WIDEK_U)
     MIVGPU_WIDEK_U=4 step 300 widek_u4_tests python -u -m pytest tests/test_ops_gpu.py -v --timeout 120 \
       --timeout-method thread -k "widek"
