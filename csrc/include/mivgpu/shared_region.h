@@ -147,8 +147,21 @@ typedef struct {
  *              w / W (w = its waves, W = all processes' waves), 1 when no
  *              process has waves resident (its dispatch gaps are its own),
  *   recv_ns -- the integral of w / W (GPU time received; utilisation),
- *   busy_ns -- time with its waves resident.
+ *   busy_ns -- time with its waves resident,
+ *   vt_ns   -- its virtual time while the GPU is fully subscribed (below):
+ *              the integral of frac / its core limit,
+ *   lead_ns -- -1 while the GPU is not fully subscribed, else its GPU time
+ *              received beyond its weighted fair share: (vt - the smallest
+ *              vt of the running contenders) x its limit.
  * A tenant charges (delta frac_ns / delta obs_ns) x its own non-held time.
+ * Fully subscribed: the core limits of the processes contending for the GPU
+ * (owing work or held in a gate, within 20 ms; a process without flags counts
+ * as 100 %) add up to the whole GPU.  Then every tenant's token bucket is at
+ * equilibrium (the time they are charged sums to the time they accrue), so a
+ * bucket balance -- and any debt carried in from a phase alone -- never
+ * recovers and holds cascade; the tenants are held on their lead instead
+ * (weighted fair sharing, work-conserving: the tenant furthest behind always
+ * runs).
  *
  * The owner is the node sampler (mivgpu-boardd, run by the monitor; the
  * board directory is mounted READ-ONLY into containers, so no tenant can
@@ -157,7 +170,7 @@ typedef struct {
  * File: <dir>/gpu-<kfd gpu_id>.board.  Writes are bracketed by `seq`
  * (odd while a pass writes: a seqlock). */
 #define MIVGPU_BOARD_MAGIC 0x4D495642u /* 'MIVB' */
-#define MIVGPU_BOARD_VERSION 1
+#define MIVGPU_BOARD_VERSION 2
 #define MIVGPU_BOARD_SLOTS 64
 #define MIVGPU_BOARD_OWNER_NONE 0
 #define MIVGPU_BOARD_OWNER_NODE 1
@@ -171,7 +184,8 @@ typedef struct {
   uint64_t frac_ns;
   uint64_t recv_ns;
   uint64_t busy_ns;
-  uint64_t unused[2];
+  uint64_t vt_ns;
+  int64_t lead_ns;
 } mivgpu_board_slot_t; /* 64 B */
 
 typedef struct {
@@ -192,18 +206,19 @@ typedef struct {
   mivgpu_board_slot_t slots[MIVGPU_BOARD_SLOTS];
 } mivgpu_board_t; /* 128 + 4096 B */
 
-/* Tenant flags (version 1): <dir>/flags/gpu-<kfd gpu_id>.flags, the one
+/* Tenant flags (version 2): <dir>/flags/gpu-<kfd gpu_id>.flags, the one
  * file of the board directory the tenants write (a read-write mount nested in
  * the read-only board mount).  Each shim claims an entry for its KFD pid and
  * publishes, every sampler pass, whether its streams sit in a governor gate
- * (HELD: its one resident wave per held stream is not work) and whether it
- * owes GPU work (OWES: split the time nobody has waves resident).  The owner
+ * (HELD: its one resident wave per held stream is not work), whether it
+ * owes GPU work (OWES: split the time nobody has waves resident) and its core
+ * limit (the weight of its fair share).  The owner
  * reads them in its pass; a process without a fresh entry is judged from its
  * occupancy alone (one CU unit = a gate).  A tenant that lies here only moves
  * its own charge or drops another process to the occupancy-only rule: the
  * shares themselves stay in the owner-written board. */
 #define MIVGPU_FLAGS_MAGIC 0x4D495646u /* 'MIVF' */
-#define MIVGPU_FLAGS_VERSION 1
+#define MIVGPU_FLAGS_VERSION 2
 #define MIVGPU_FLAGS_SLOTS 256
 #define MIVGPU_FLAG_HELD 1
 #define MIVGPU_FLAG_OWES 2
@@ -212,7 +227,10 @@ typedef struct {
   int32_t pid;        /* KFD pid, 0 = free                                   */
   int32_t state;      /* MIVGPU_FLAG_*                                       */
   uint64_t stamp_ns;  /* CLOCK_MONOTONIC of the last publish                 */
-} mivgpu_flag_t; /* 16 B */
+  uint32_t limit_ppm; /* core limit, ppm of the GPU (0 = none: 100 %)        */
+  uint32_t reserved;
+  uint64_t unused;
+} mivgpu_flag_t; /* 32 B */
 
 typedef struct {
   uint32_t magic;
@@ -221,7 +239,7 @@ typedef struct {
   int32_t reserved;
   uint64_t unused[6];
   mivgpu_flag_t flags[MIVGPU_FLAGS_SLOTS];
-} mivgpu_board_flags_t; /* 64 + 4096 B */
+} mivgpu_board_flags_t; /* 64 + 8192 B */
 
 /* Field ids understood by mivgpu_abi_offsetof() (exported by libmivgpu.so). */
 enum {

@@ -37,6 +37,16 @@ constexpr int kGateUnits = 1;
 constexpr uint64_t kSlotStaleNs = 1000000000ull;
 // Passes longer apart than this do not invent history (a stalled owner).
 constexpr uint64_t kMaxDtNs = 100000000ull;
+// Fair-share mode (shared_region.h vt_ns / lead_ns): entered when the GPU
+// has been fully subscribed -- the backlogged processes' core limits adding
+// up to the whole GPU -- in most passes of the last ~10 ms (EWMA >= 0.8), left
+// below 0.5.
+constexpr uint64_t kSubTauNs = 10000000ull;
+constexpr double kSubEnter = 0.8, kSubLeave = 0.5;
+// Fair-share mode: a tenant's lead over the furthest-behind contender is
+// bounded here (virtual time beyond it is dropped: a tenant cannot bank an
+// unbounded lead that holds it for seconds).
+constexpr uint64_t kMaxLeadNs = 200000000ull;
 
 struct Reading {
   int pid;
@@ -54,6 +64,11 @@ struct Handle {
   char dir[256] = {0};
   mivgpu_board_flags_t* flags = nullptr;   // <dir>/flags/gpu-<id>.flags (tenant-written)
   int flag_slot = -1;                      // this tenant's entry
+  // owner-private fair-share state
+  bool was_backlogged[MIVGPU_BOARD_SLOTS] = {};   // per board slot, the previous pass
+  double sub_ewma = 0;                            // share of recent passes fully subscribed
+  bool fair = false;                              // fair-share mode
+  uint64_t vmin = 0;                              // the previous pass's smallest running virtual time
 };
 
 // fstat under the shim's glibc floor (glibc_floor.h: fstat became a real
@@ -183,9 +198,9 @@ inline bool open_flags(Handle& h) {
   return true;
 }
 
-// Tenant side: publish this pass's state under its KFD pid (an entry claimed
-// once, by CAS on a free or stale one).
-inline void publish_flags(Handle& h, int pid, int state, uint64_t now) {
+// Tenant side: publish this pass's state and its core limit (ppm, 0 = none)
+// under its KFD pid (an entry claimed once, by CAS on a free or stale one).
+inline void publish_flags(Handle& h, int pid, int state, uint32_t limit_ppm, uint64_t now) {
   if (!h.flags || pid <= 0) return;
   mivgpu_flag_t* e = h.flag_slot >= 0 ? &h.flags->flags[h.flag_slot] : nullptr;
   if (!e || __atomic_load_n(&e->pid, __ATOMIC_RELAXED) != pid) {
@@ -207,18 +222,23 @@ inline void publish_flags(Handle& h, int pid, int state, uint64_t now) {
     e = &h.flags->flags[h.flag_slot];
   }
   __atomic_store_n(&e->state, state, __ATOMIC_RELAXED);
+  __atomic_store_n(&e->limit_ppm, limit_ppm, __ATOMIC_RELAXED);
   __atomic_store_n(&e->stamp_ns, now, __ATOMIC_RELEASE);
 }
 
-// Owner side: a process's published state, -1 when it has no fresh entry.
+// Owner side: a process's published state, -1 when it has no fresh entry;
+// `limit_ppm` gets its core limit (1e6 when it has none).
 constexpr uint64_t kFlagFreshNs = 20000000ull;   // 20 ms: ten tenant passes
-inline int read_flags(const mivgpu_board_flags_t* f, int pid, uint64_t now) {
+inline int read_flags(const mivgpu_board_flags_t* f, int pid, uint64_t now, uint32_t* limit_ppm = nullptr) {
+  if (limit_ppm) *limit_ppm = 1000000u;
   if (!f || pid <= 0) return -1;
   for (int k = 0; k < MIVGPU_FLAGS_SLOTS; ++k) {
     const mivgpu_flag_t* e = &f->flags[k];
     if (__atomic_load_n(&e->pid, __ATOMIC_ACQUIRE) != pid) continue;
     const uint64_t st = __atomic_load_n(&e->stamp_ns, __ATOMIC_ACQUIRE);
     if (st + kFlagFreshNs < now) return -1;
+    const uint32_t lim = __atomic_load_n(&e->limit_ppm, __ATOMIC_RELAXED);
+    if (limit_ppm && lim > 0 && lim < 1000000u) *limit_ppm = lim;
     return __atomic_load_n(&e->state, __ATOMIC_RELAXED);
   }
   return -1;
@@ -274,6 +294,16 @@ enum Split { kSplitRatio = 0, kSplitEqual = 1 };
 //             none has, the owing tenants (flags) split the pass equally (a
 //             process without flags is charged it whole: it is alone between
 //             its own kernels).
+// Then the fair-share state (shared_region.h, vt_ns / lead_ns): a process is
+// backlogged in a pass when it owes work or sits in a gate (flags; one
+// without flags: waves resident), weighted by its core limit (flags; 100 %
+// without).  In fair-share mode (the backlogged weights filling the GPU in
+// most recent passes) each backlogged process's virtual time advances by the
+// GPU share it received / its weight; one not backlogged, or held while
+// behind, is pulled up to the smallest running virtual time (no credit is
+// banked while away), and every process's lead is (vt - that minimum) x its
+// weight.  Outside the mode lead_ns = -1: the tenants' own token buckets cap
+// them.
 inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_t period_ns, int kind,
                        int owner_pid, int split, uint64_t pass_cost_ns) {
   mivgpu_board_t* b = h.b;
@@ -283,13 +313,15 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
   h.last_pass_ns = now;
   if (h.flags == nullptr) (void)open_flags(h);
   constexpr int kMaxRead = 256;
-  int st[kMaxRead];
+  int st[kMaxRead], sl[kMaxRead];
+  uint32_t lim[kMaxRead];
   long wv[kMaxRead];
+  double use[kMaxRead];
   long W = 0;
   int resident = 0, owing = 0;
   if (n > kMaxRead) n = kMaxRead;
   for (int i = 0; i < n; ++i) {
-    st[i] = read_flags(h.flags, r[i].pid, now);
+    st[i] = read_flags(h.flags, r[i].pid, now, &lim[i]);
     const int v = r[i].v;
     bool held;
     if (st[i] >= 0) held = (st[i] & MIVGPU_FLAG_HELD) != 0;
@@ -306,7 +338,13 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
   __atomic_thread_fence(__ATOMIC_RELEASE);
   int hi = __atomic_load_n(&b->nslots, __ATOMIC_RELAXED);
   if (hi < 0 || hi > MIVGPU_BOARD_SLOTS) hi = MIVGPU_BOARD_SLOTS;
+  double sum_w = 0;   // backlogged processes' weights
+  int backlogged = 0;
+  bool bl[kMaxRead];
   for (int i = 0; i < n; ++i) {
+    sl[i] = -1;
+    use[i] = 0;
+    bl[i] = false;
     if (r[i].pid <= 0 || r[i].v < 0) continue;
     int slot = -1, free_slot = -1;
     for (int k = 0; k < MIVGPU_BOARD_SLOTS; ++k) {
@@ -323,23 +361,33 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
       mivgpu_board_slot_t& s = b->slots[slot];
       memset(&s, 0, sizeof(s));
       s.pid = r[i].pid;
+      s.lead_ns = -1;
+      h.was_backlogged[slot] = false;
       if (slot + 1 > hi) hi = slot + 1;
     }
+    sl[i] = slot;
     mivgpu_board_slot_t& s = b->slots[slot];
     const int v = r[i].v;
     const long w = wv[i];
     const bool held = st[i] >= 0 ? (st[i] & MIVGPU_FLAG_HELD) != 0 : (v > 0 && v <= kGateUnits);
+    const bool owes = st[i] >= 0 && (st[i] & MIVGPU_FLAG_OWES);
     s.occupancy = v;
     s.seen_ns = now;
+    bl[i] = st[i] >= 0 ? (held || owes) : w > 0;
+    if (bl[i]) {
+      sum_w += (double)lim[i] / 1e6;
+      ++backlogged;
+    }
     if (!dt) continue;
     double f, got;
     if (W > 0) {
       got = split == kSplitEqual ? (w > 0 ? 1.0 / (double)resident : 0.0) : (double)w / (double)W;
       f = got;
+      use[i] = got;
     } else {
       got = 0.0;
-      const bool owes = st[i] >= 0 && (st[i] & MIVGPU_FLAG_OWES);
       f = st[i] < 0 ? 1.0 : (owes && owing > 0 ? 1.0 / (double)owing : 1.0);
+      use[i] = owes && owing > 0 ? 1.0 / (double)owing : 0.0;
     }
     if (!held) {
       s.obs_ns += dt;
@@ -348,6 +396,52 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
     s.recv_ns += (uint64_t)(got * (double)dt + 0.5);
     if (w > 0) s.busy_ns += dt;
   }
+  // fair-share mode while the backlogged weights fill the GPU
+  if (dt) {
+    const double x = (backlogged >= 2 && sum_w >= 0.999) ? 1.0 : 0.0;
+    const double a = (double)dt / (double)kSubTauNs < 1.0 ? (double)dt / (double)kSubTauNs : 1.0;
+    h.sub_ewma += a * (x - h.sub_ewma);
+  }
+  const bool entering = !h.fair && h.sub_ewma >= kSubEnter;
+  h.fair = h.fair ? h.sub_ewma >= kSubLeave : entering;
+  auto running = [&](int i) { return bl[i] && !(st[i] >= 0 && (st[i] & MIVGPU_FLAG_HELD)); };
+  if (h.fair) {
+    if (entering) {
+      // everyone starts level
+      uint64_t top = 0;
+      for (int i = 0; i < n; ++i)
+        if (sl[i] >= 0 && b->slots[sl[i]].vt_ns > top) top = b->slots[sl[i]].vt_ns;
+      for (int i = 0; i < n; ++i)
+        if (sl[i] >= 0) b->slots[sl[i]].vt_ns = top;
+      h.vmin = top;
+    }
+    for (int i = 0; i < n; ++i) {
+      const int k = sl[i];
+      if (k < 0 || !bl[i]) continue;
+      mivgpu_board_slot_t& s = b->slots[k];
+      if (!h.was_backlogged[k] && s.vt_ns < h.vmin) s.vt_ns = h.vmin;   // joins at the running minimum
+      s.vt_ns += (uint64_t)(use[i] * (double)dt * 1e6 / (double)lim[i] + 0.5);
+    }
+    uint64_t vmin = UINT64_MAX;
+    for (int i = 0; i < n; ++i)
+      if (sl[i] >= 0 && running(i) && b->slots[sl[i]].vt_ns < vmin) vmin = b->slots[sl[i]].vt_ns;
+    if (vmin == UINT64_MAX) vmin = h.vmin;
+    for (int i = 0; i < n; ++i) {
+      const int k = sl[i];
+      if (k < 0) continue;
+      mivgpu_board_slot_t& s = b->slots[k];
+      if (s.vt_ns < vmin) s.vt_ns = vmin;
+      const uint64_t cap = vmin + (uint64_t)((double)kMaxLeadNs * 1e6 / (double)lim[i]);
+      if (s.vt_ns > cap) s.vt_ns = cap;
+      s.lead_ns = (int64_t)((double)(s.vt_ns - vmin) * (double)lim[i] / 1e6 + 0.5);
+    }
+    h.vmin = vmin;
+  } else {
+    for (int i = 0; i < n; ++i)
+      if (sl[i] >= 0) b->slots[sl[i]].lead_ns = -1;
+  }
+  for (int i = 0; i < n; ++i)
+    if (sl[i] >= 0) h.was_backlogged[sl[i]] = bl[i];
   // slots of processes gone for a while are freed (a new process may get the pid)
   for (int k = 0; k < hi; ++k)
     if (b->slots[k].pid && b->slots[k].seen_ns + kSlotStaleNs < now) memset(&b->slots[k], 0, sizeof(b->slots[k]));
@@ -374,6 +468,8 @@ struct View {
   uint64_t frac_ns = 0;
   uint64_t recv_ns = 0;
   uint64_t busy_ns = 0;
+  uint64_t vt_ns = 0;
+  int64_t lead_ns = -1;
 };
 
 // Seqlock read of `pid`'s slot; `hint` caches its index.  False when the pid
@@ -406,6 +502,8 @@ inline bool read_slot(const mivgpu_board_t* b, int pid, int* hint, View* out) {
       v.frac_ns = s.frac_ns;
       v.recv_ns = s.recv_ns;
       v.busy_ns = s.busy_ns;
+      v.vt_ns = s.vt_ns;
+      v.lead_ns = s.lead_ns;
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
     if (__atomic_load_n(&b->seq, __ATOMIC_RELAXED) != s1) continue;

@@ -1755,6 +1755,9 @@ constexpr uint64_t kPeerBusyNs = 200000000ull;   // 200 ms
 constexpr uint64_t kBoardStaleNs = 50000000ull;   // 50 ms
 // Idle time after which the host bucket stops accruing entitlement.
 constexpr uint64_t kAccrueIdleNs = 20000000ull;   // 20 ms
+// Fair-share mode (board.h): lead over the furthest-behind backlogged tenant
+// at which the gate holds (GPU time beyond the weighted fair share).
+constexpr uint64_t kFairLagNs = 5000000ull;        // 5 ms
 // A governed peer held behind its gate has exactly its gate kernel's wave
 // resident (governor.hip host_bucket_gate: one 64-lane wave).
 constexpr int kGateWaves = 1;
@@ -1803,6 +1806,9 @@ struct OccDev {
   mivgpu_board::View board_view;
   uint64_t board_charged = 0;  // samples charged from the board / from the local estimate
   uint64_t local_charged = 0;
+  uint64_t fair_samples = 0;   // samples in fair-share mode / held there on the lead
+  uint64_t fair_held_samples = 0;
+  int64_t last_lead_ns = -1;
   std::vector<mivgpu_board::Reading> readings;
 };
 // Background stamper idle threshold and the batch bounds (see stamper_main
@@ -1868,7 +1874,7 @@ std::atomic<bool> g_board_fast{false};   // an owner pass saw waves or a governe
 // (this process and every peer on the GPU), then read this process's slot.
 // Returns the mean share over the passes since the previous sample in which
 // this process was not held, or -1 when no live board covers it.
-double board_step(OccDev& o, uint64_t now, int own_raw, bool gating, int flags) {
+double board_step(OccDev& o, uint64_t now, int own_raw, bool gating, int flags, uint32_t limit_ppm) {
   namespace mb = mivgpu_board;
   if (!g_cfg.board_dir[0]) return -1;
   if (!o.board.b) {
@@ -1882,7 +1888,7 @@ double board_step(OccDev& o, uint64_t now, int own_raw, bool gating, int flags) 
     o.board_flags_ns = now;
     if (!mb::open_flags(o.board)) mlog(3, "KFD gpu %d: board flags not writable; the owner reads occupancy only", o.gpu_id);
   }
-  mb::publish_flags(o.board, o.own_pid, flags, now);
+  mb::publish_flags(o.board, o.own_pid, flags, limit_ppm, now);
   mivgpu_board_t* b = o.board.b;
   const int self = o.own_pid;
   if (o.board.owner) {
@@ -1912,6 +1918,7 @@ double board_step(OccDev& o, uint64_t now, int own_raw, bool gating, int flags) 
   mb::View v;
   if (!mb::read_slot(b, self, &o.board_hint, &v) || v.beat_ns + kBoardStaleNs < now) {
     o.board_prev_ok = false;
+    o.board_view.lead_ns = -1;
     return -1;
   }
   if (o.board_prev_ok && v.obs_ns >= o.board_prev_obs && v.frac_ns >= o.board_prev_frac) {
@@ -2034,7 +2041,12 @@ bool occ_sample(int dev, uint64_t now) {
   // owner pass if this process holds the role, read this process's share
   const bool gating = coarse_ns() - g_last_gate_ns[dev].load(std::memory_order_relaxed) < 1000000000ull;
   const int flags = (holding > 0 ? MIVGPU_FLAG_HELD : 0) | ((pending || own > 0) && holding == 0 ? MIVGPU_FLAG_OWES : 0);
-  const double board_f = board_step(o, now, own_raw, gating, flags);
+  const uint64_t lim_ppm = cu_limit_ppm_of(dev);
+  const double board_f = board_step(o, now, own_raw, gating, flags,
+                                    lim_ppm > 0 && lim_ppm < 1000000 ? (uint32_t)lim_ppm : 0u);
+  // fair-share mode (board.h): the GPU is fully subscribed by backlogged
+  // tenants; this process is held on its lead over the furthest-behind one
+  const int64_t lead = board_f >= 0 ? o.board_view.lead_ns : -1;
   const bool owes = own > 0 || pending || holding > 0 || held_dt > 0;
   const double a = (double)dt / g_cfg.share_tau_ns < 1.0 ? (double)dt / g_cfg.share_tau_ns : 1.0;
   if (owes && holding == 0) {
@@ -2114,7 +2126,23 @@ bool occ_sample(int dev, uint64_t now) {
       if (o.tokens_ns > cap) o.tokens_ns = cap;
       if (o.tokens_ns < -cap) o.tokens_ns = -cap;
     }
-    __atomic_store_n(reinterpret_cast<int64_t*>(const_cast<uint64_t*>(&hs[kHsHostTokens])), (int64_t)o.tokens_ns,
+    // Fully subscribed, every tenant's bucket is at equilibrium: what they are
+    // charged sums to what they accrue, so holding one only moves its GPU time
+    // to the others and a debt (one carried in from a phase alone, or noise)
+    // is never repaid -- measured, four symmetric 25 % tenants held 0.4-1.1 s
+    // each over a 1.6 s run, at 0.82 of native.  There the tenant is held on
+    // its lead over the furthest-behind backlogged tenant instead (the tenant
+    // furthest behind always runs: work-conserving, shares by core limit) and
+    // its bucket carries no debt out of the mode.
+    double eff = o.tokens_ns;
+    if (lead >= 0) {
+      if (o.tokens_ns < 0) o.tokens_ns = 0;
+      eff = (double)kFairLagNs - (double)lead;
+      ++o.fair_samples;
+      if (eff < 0) ++o.fair_held_samples;
+    }
+    o.last_lead_ns = lead;
+    __atomic_store_n(reinterpret_cast<int64_t*>(const_cast<uint64_t*>(&hs[kHsHostTokens])), (int64_t)eff,
                      __ATOMIC_RELAXED);
   }
   // Host mode: size the batches between gates to ~2 ms of GPU time from the
@@ -3679,10 +3707,13 @@ MIVGPU_EXPORT int mivgpu_sampler_info(int dev, char* buf, int n) {
   };
   const uint64_t now = mono_ns();
   put("{\"live\":%d,\"gpu_id\":%d,\"pid\":%d,\"samples\":%llu,\"board_charged\":%llu,\"local_charged\":%llu,"
-      "\"window_ms\":%.1f,\"share_avg\":%.4f,\"board_share\":%.4f,\"state_ms\":[%.1f,%.1f,%.1f,%.1f,%.1f]",
+      "\"window_ms\":%.1f,\"share_avg\":%.4f,\"board_share\":%.4f,\"state_ms\":[%.1f,%.1f,%.1f,%.1f,%.1f],"
+      "\"fair_samples\":%llu,\"fair_held_samples\":%llu,\"lead_ms\":%.3f,\"tokens_ms\":%.3f",
       o.live ? 1 : 0, o.gpu_id, o.own_pid, (unsigned long long)o.samples, (unsigned long long)o.board_charged,
       (unsigned long long)o.local_charged, o.window_ns / 1e6, o.share_avg, o.board_share, o.state_ns[0] / 1e6,
-      o.state_ns[1] / 1e6, o.state_ns[2] / 1e6, o.state_ns[3] / 1e6, o.state_ns[4] / 1e6);
+      o.state_ns[1] / 1e6, o.state_ns[2] / 1e6, o.state_ns[3] / 1e6, o.state_ns[4] / 1e6,
+      (unsigned long long)o.fair_samples, (unsigned long long)o.fair_held_samples,
+      o.last_lead_ns >= 0 ? o.last_lead_ns / 1e6 : -1.0, o.tokens_ns / 1e6);
   put(",\"peers\":[");
   for (size_t i = 0; i < o.peers.size(); ++i) {
     const OccPeer& p = o.peers[i];
@@ -3704,8 +3735,10 @@ MIVGPU_EXPORT int mivgpu_sampler_info(int dev, char* buf, int n) {
   for (int k = 0; k < MIVGPU_BOARD_SLOTS; ++k) {
     const mivgpu_board_slot_t& s = b->slots[k];
     if (!s.pid) continue;
-    put("%s{\"pid\":%d,\"occ\":%d,\"obs_ms\":%.1f,\"frac_ms\":%.1f,\"recv_ms\":%.1f,\"busy_ms\":%.1f}",
-        first ? "" : ",", s.pid, s.occupancy, s.obs_ns / 1e6, s.frac_ns / 1e6, s.recv_ns / 1e6, s.busy_ns / 1e6);
+    put("%s{\"pid\":%d,\"occ\":%d,\"obs_ms\":%.1f,\"frac_ms\":%.1f,\"recv_ms\":%.1f,\"busy_ms\":%.1f,"
+        "\"lead_ms\":%.3f}",
+        first ? "" : ",", s.pid, s.occupancy, s.obs_ns / 1e6, s.frac_ns / 1e6, s.recv_ns / 1e6, s.busy_ns / 1e6,
+        s.lead_ns >= 0 ? s.lead_ns / 1e6 : -1.0);
     first = false;
   }
   put("]}}");

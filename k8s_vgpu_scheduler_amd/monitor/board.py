@@ -17,8 +17,8 @@ server.go:853-864); here ONE owner per GPU reads every process's
   ``$HOOK_PATH/vgpu/board``, which the device plugin mounts READ-ONLY into
   every vGPU container (``deviceplugin/allocate.py``) -- no tenant can write
   the share it is charged -- with one read-write subdirectory, ``flags/``,
-  where each tenant's shim publishes whether it is held in its governor gate
-  or owes work (the owner's pass reads them);
+  where each tenant's shim publishes whether it is held in its governor gate,
+  whether it owes work and its core limit (the owner's pass reads them);
 * without a node sampler (hand-run slices, the bench), a shim that governs
   the GPU takes the owner role with ``flock`` on ``gpu-<id>.owner``.
 
@@ -36,7 +36,7 @@ import time
 from pathlib import Path
 
 BOARD_MAGIC = 0x4D495642
-BOARD_VERSION = 1
+BOARD_VERSION = 2
 BOARD_SLOTS = 64
 OWNER_NONE, OWNER_NODE, OWNER_SHIM = 0, 1, 2
 CONTAINER_BOARD_DIR = "/var/run/mivgpu/board"    # the grant's MIVGPU_BOARD_DIR (read-only mount)
@@ -47,7 +47,7 @@ log = logging.getLogger("mivgpu.board")
 class BoardSlot(C.Structure):
     _fields_ = [("pid", C.c_int32), ("occupancy", C.c_int32), ("seen_ns", C.c_uint64), ("obs_ns", C.c_uint64),
                 ("frac_ns", C.c_uint64), ("recv_ns", C.c_uint64), ("busy_ns", C.c_uint64),
-                ("unused", C.c_uint64 * 2)]
+                ("vt_ns", C.c_uint64), ("lead_ns", C.c_int64)]
 
 
 class BoardHeader(C.Structure):
@@ -62,13 +62,14 @@ BOARD_SIZE = C.sizeof(BoardHeader)
 assert C.sizeof(BoardSlot) == 64 and BOARD_SIZE == 128 + 64 * BOARD_SLOTS
 
 FLAGS_MAGIC = 0x4D495646
-FLAGS_VERSION = 1
+FLAGS_VERSION = 2
 FLAGS_SLOTS = 256
 FLAG_HELD, FLAG_OWES = 1, 2
 
 
 class Flag(C.Structure):
-    _fields_ = [("pid", C.c_int32), ("state", C.c_int32), ("stamp_ns", C.c_uint64)]
+    _fields_ = [("pid", C.c_int32), ("state", C.c_int32), ("stamp_ns", C.c_uint64), ("limit_ppm", C.c_uint32),
+                ("reserved", C.c_uint32), ("unused", C.c_uint64)]
 
 
 class Flags(C.Structure):
@@ -77,7 +78,7 @@ class Flags(C.Structure):
 
 
 FLAGS_SIZE = C.sizeof(Flags)
-assert FLAGS_SIZE == 64 + 16 * FLAGS_SLOTS
+assert FLAGS_SIZE == 64 + 32 * FLAGS_SLOTS
 
 
 def offsets() -> dict:
@@ -115,9 +116,9 @@ class FlagsFile:
             os.close(fd)
         self.f = Flags.from_buffer(self.mm)
 
-    def publish(self, pid: int, state: int):
+    def publish(self, pid: int, state: int, limit_ppm: int = 0):
         slot = next((e for e in self.f.flags if e.pid == pid), None) or next(e for e in self.f.flags if e.pid == 0)
-        slot.pid, slot.state, slot.stamp_ns = pid, state, time.monotonic_ns()
+        slot.pid, slot.state, slot.limit_ppm, slot.stamp_ns = pid, state, limit_ppm, time.monotonic_ns()
 
     def entries(self) -> dict[int, tuple[int, int]]:
         return {e.pid: (e.state, e.stamp_ns) for e in self.f.flags if e.pid}
@@ -191,7 +192,8 @@ def shares(before: BoardHeader, after: BoardHeader) -> dict[int, dict]:
         frac = s.frac_ns - (p.frac_ns if p else 0)
         recv = s.recv_ns - (p.recv_ns if p else 0)
         out[s.pid] = {"charged_share": frac / obs if obs > 0 else None, "received": recv / wall,
-                      "obs_ms": obs / 1e6, "occupancy": s.occupancy}
+                      "obs_ms": obs / 1e6, "occupancy": s.occupancy,
+                      "lead_ms": s.lead_ns / 1e6 if s.lead_ns >= 0 else None}
     return out
 
 

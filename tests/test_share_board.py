@@ -243,3 +243,88 @@ def test_tenant_flags_decide_held_and_gap_splits(native_build, tmp_path):
     assert first[333].obs_ns == 0                                 # held: not observed
     sh = B.shares(mid, s2)
     assert abs(sh[111]["charged_share"] - 0.5) < 0.05 and abs(sh[222]["charged_share"] - 0.5) < 0.05, sh
+
+
+def _fair_run(native_build, tmp_path, tenants, seconds=0.4, occ_after=None):
+    """boardd over a fake KFD; ``tenants``: {pid: (occupancy, state, limit_ppm)}
+    (state None = no flags).  Returns the board slots after ``seconds`` of
+    publishing every 5 ms."""
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
+    for pid, (v, _, _) in tenants.items():
+        _occ(kfd, pid, 4242, v)
+    d = tmp_path / "board"
+    fl = B.FlagsFile(str(d), 4242)
+    node = subprocess.Popen(_boardd(native_build, kfd, d))
+    try:
+        t_end = time.time() + seconds
+        while time.time() < t_end:
+            for pid, (_, st, lim) in tenants.items():
+                if st is not None:
+                    fl.publish(pid, st, lim)
+            time.sleep(0.005)
+        b = B.Board(B.board_path(d, 4242))
+        s = b.slots()
+        b.close()
+    finally:
+        node.terminate()
+        node.wait(timeout=10)
+        fl.close()
+    return s
+
+
+def test_fully_subscribed_symmetric_tenants_run_level(native_build, tmp_path):
+    """Four backlogged 25 % tenants fill the GPU: fair-share mode, and with
+    equal shares no tenant leads (none is held) -- the token buckets, at
+    equilibrium there, held 0.4-1.1 s of a 1.6 s run each (0.82 of native)."""
+    s = _fair_run(native_build, tmp_path, {p: (10, B.FLAG_OWES, 250000) for p in (111, 222, 333, 444)})
+    assert all(s[p].lead_ns >= 0 for p in (111, 222, 333, 444)), {p: s[p].lead_ns for p in s}
+    assert max(s[p].lead_ns for p in (111, 222, 333, 444)) < 2_000_000, {p: s[p].lead_ns for p in s}
+
+
+def test_fair_share_leads_follow_the_core_limits(native_build, tmp_path):
+    """75 % and 25 % tenants sharing the GPU evenly (equal waves): the 25 %
+    one runs ahead of its weighted share and leads (its gate holds past 5 ms);
+    the 75 % one, furthest behind, leads by nothing."""
+    s = _fair_run(native_build, tmp_path, {111: (10, B.FLAG_OWES, 750000), 222: (10, B.FLAG_OWES, 250000)})
+    assert s[111].lead_ns == 0 and s[222].lead_ns > 5_000_000, (s[111].lead_ns, s[222].lead_ns)
+    # bounded: a lead never exceeds kMaxLeadNs (200 ms) of GPU time
+    assert s[222].lead_ns <= 200_000_000
+
+
+def test_undersubscribed_gpu_keeps_the_token_buckets(native_build, tmp_path):
+    """Two 25 % tenants do not fill the GPU: no fair-share mode (lead -1), so
+    their own token buckets cap each at 25 % even with the GPU half idle."""
+    s = _fair_run(native_build, tmp_path, {111: (10, B.FLAG_OWES, 250000), 222: (10, B.FLAG_OWES, 250000)})
+    assert s[111].lead_ns == -1 and s[222].lead_ns == -1
+
+
+def test_idle_or_held_tenant_banks_no_credit(native_build, tmp_path):
+    """In fair-share mode a tenant that is not backlogged, or held while
+    behind, is pulled up to the furthest-behind running tenant: it leads by
+    nothing and has banked nothing; an unmanaged process with waves resident
+    counts as backlogged at 100 %."""
+    s = _fair_run(native_build, tmp_path, {111: (10, B.FLAG_OWES, 500000), 222: (10, B.FLAG_OWES, 500000),
+                                           333: (0, 0, 250000), 444: (1, B.FLAG_HELD, 250000),
+                                           555: (10, None, 0)})
+    assert all(s[p].lead_ns >= 0 for p in (111, 222, 333, 444, 555)), {p: s[p].lead_ns for p in s}
+    assert s[333].lead_ns == 0 and s[444].lead_ns == 0
+    # equal waves: the 100 % process is furthest behind, the 50 % tenants lead
+    assert s[555].lead_ns == 0 and s[111].lead_ns > 0 and s[222].lead_ns > 0
+
+
+def test_governed_tenants_filling_the_gpu_are_held_on_their_lead(native_build, tmp_path):
+    """Two governed 50 % tenants (the shim, mock HIP runtime) with equal waves
+    fill the GPU: their sampler runs in fair-share mode (the board's lead,
+    published by the shim that owns it) instead of the token bucket, and
+    neither is held -- nothing leads."""
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
+    _occ(kfd, 987654, 4242, 10)
+    _occ(kfd, 987655, 4242, 10)
+    d = tmp_path / "board"
+    cmds = ["kfdctx", 0, "alloc", 100, "launch", 300, "launchfor", 900, "sampler"]
+    a = _drive(native_build, tmp_path, cmds, _governed(kfd, d, 987654), "fa.cache")
+    b = _drive(native_build, tmp_path, cmds, _governed(kfd, d, 987655), "fb.cache")
+    ia, ib = _sampler(_outputs(a)), _sampler(_outputs(b))
+    for i in (ia, ib):
+        assert i["fair_samples"] > 50, i
+        assert i["fair_held_samples"] <= 0.05 * i["fair_samples"], i
