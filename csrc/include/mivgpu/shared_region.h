@@ -241,6 +241,30 @@ typedef struct {
   mivgpu_flag_t flags[MIVGPU_FLAGS_SLOTS];
 } mivgpu_board_flags_t; /* 64 + 8192 B */
 
+/* Node-written core limits (version 1): <dir>/gpu-<kfd gpu_id>.limits, in
+ * the read-only board mount.  The monitor writes, every feedback pass, the
+ * core limit of each host pid it attributes to a granted container on the GPU
+ * (grant files x the pod's processes, host truth); the owner pass weighs a
+ * process with min(this, its flags' limit), so a tenant cannot raise its fair
+ * share by publishing a larger limit.  Written under a private name and
+ * renamed into place. */
+#define MIVGPU_LIMITS_MAGIC 0x4D49564Cu /* 'MIVL' */
+#define MIVGPU_LIMITS_VERSION 1
+#define MIVGPU_LIMITS_MAX 1024
+
+typedef struct {
+  int32_t pid;        /* host (KFD) pid                                       */
+  uint32_t limit_ppm; /* core limit of its container on this GPU              */
+} mivgpu_limit_entry_t;
+
+typedef struct {
+  uint32_t magic;
+  int32_t version;
+  int32_t gpu_id;
+  int32_t count;      /* entries that follow (<= MIVGPU_LIMITS_MAX)           */
+  mivgpu_limit_entry_t entries[];
+} mivgpu_board_limits_t;
+
 /* Field ids understood by mivgpu_abi_offsetof() (exported by libmivgpu.so). */
 enum {
   MIVGPU_F_MAGIC = 0,

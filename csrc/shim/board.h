@@ -64,6 +64,10 @@ struct Handle {
   char dir[256] = {0};
   mivgpu_board_flags_t* flags = nullptr;   // <dir>/flags/gpu-<id>.flags (tenant-written)
   int flag_slot = -1;                      // this tenant's entry
+  // node-written core limits (<dir>/gpu-<id>.limits), reloaded every 100 ms
+  mivgpu_limit_entry_t* lims = nullptr;
+  int nlims = 0;
+  uint64_t lims_ns = 0;
   // owner-private fair-share state
   bool was_backlogged[MIVGPU_BOARD_SLOTS] = {};   // per board slot, the previous pass
   double sub_ewma = 0;                            // share of recent passes fully subscribed
@@ -226,6 +230,33 @@ inline void publish_flags(Handle& h, int pid, int state, uint32_t limit_ppm, uin
   __atomic_store_n(&e->stamp_ns, now, __ATOMIC_RELEASE);
 }
 
+// Owner side: (re)load the node-written core limits, at most every 100 ms.
+inline void load_limits(Handle& h, uint64_t now) {
+  if (h.lims_ns && now - h.lims_ns < 100000000ull) return;
+  h.lims_ns = now;
+  h.nlims = 0;
+  char path[512];
+  board_path(path, sizeof(path), h.dir, h.gpu_id, "limits");
+  const int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return;
+  mivgpu_board_limits_t hdr;
+  if (pread(fd, &hdr, sizeof(hdr), 0) == (ssize_t)sizeof(hdr) && hdr.magic == MIVGPU_LIMITS_MAGIC &&
+      hdr.version == MIVGPU_LIMITS_VERSION && hdr.gpu_id == h.gpu_id && hdr.count > 0 &&
+      hdr.count <= MIVGPU_LIMITS_MAX) {
+    if (!h.lims) h.lims = new mivgpu_limit_entry_t[MIVGPU_LIMITS_MAX];
+    const ssize_t want = (ssize_t)(hdr.count * sizeof(mivgpu_limit_entry_t));
+    if (pread(fd, h.lims, (size_t)want, sizeof(hdr)) == want) h.nlims = hdr.count;
+  }
+  close(fd);
+}
+
+// The node-written core limit of `pid` (ppm), 0 when it has none.
+inline uint32_t node_limit(const Handle& h, int pid) {
+  for (int k = 0; k < h.nlims; ++k)
+    if (h.lims[k].pid == pid) return h.lims[k].limit_ppm;
+  return 0;
+}
+
 // Owner side: a process's published state, -1 when it has no fresh entry;
 // `limit_ppm` gets its core limit (1e6 when it has none).
 constexpr uint64_t kFlagFreshNs = 20000000ull;   // 20 ms: ten tenant passes
@@ -297,8 +328,9 @@ enum Split { kSplitRatio = 0, kSplitEqual = 1 };
 // Then the fair-share state (shared_region.h, vt_ns / lead_ns): a process is
 // backlogged in a pass when it owes work or sits in a gate (flags; one
 // without flags: waves resident), weighted by its core limit (flags; 100 %
-// without).  In fair-share mode (the backlogged weights filling the GPU in
-// most recent passes) each backlogged process's virtual time advances by the
+// without; the monitor's node-written limit caps it).  In fair-share mode
+// (the backlogged weights filling the GPU in most recent passes) each
+// backlogged process's virtual time advances by the
 // GPU share it received / its weight; one not backlogged, or held while
 // behind, is pulled up to the smallest running virtual time (no credit is
 // banked while away), and every process's lead is (vt - that minimum) x its
@@ -312,6 +344,7 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
   if (dt > kMaxDtNs) dt = kMaxDtNs;
   h.last_pass_ns = now;
   if (h.flags == nullptr) (void)open_flags(h);
+  load_limits(h, now);
   constexpr int kMaxRead = 256;
   int st[kMaxRead], sl[kMaxRead];
   uint32_t lim[kMaxRead];
@@ -322,6 +355,8 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
   if (n > kMaxRead) n = kMaxRead;
   for (int i = 0; i < n; ++i) {
     st[i] = read_flags(h.flags, r[i].pid, now, &lim[i]);
+    const uint32_t nl = node_limit(h, r[i].pid);   // the grant's, when the monitor knows the process
+    if (nl > 0 && nl < lim[i]) lim[i] = nl;
     const int v = r[i].v;
     bool held;
     if (st[i] >= 0) held = (st[i] & MIVGPU_FLAG_HELD) != 0;

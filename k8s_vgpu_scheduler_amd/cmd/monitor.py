@@ -103,7 +103,8 @@ def main(argv=None):
     pause = threading.Event()
     threading.Thread(target=watch_partition_lock, args=(pause, stop), name="partition-lock", daemon=True).start()
     try:
-        watch_and_feedback(lister, stop, pause=pause, truth=truth, escalation=escalation)
+        watch_and_feedback(lister, stop, pause=pause, truth=truth, escalation=escalation,
+                           board_dir=board.dir if board is not None else None)
     finally:
         if board is not None:
             board.stop()

@@ -132,6 +132,32 @@ def board_path(board_dir: str, gpu_id: int) -> Path:
     return Path(board_dir) / f"gpu-{gpu_id}.board"
 
 
+LIMITS_MAGIC = 0x4D49564C
+LIMITS_VERSION = 1
+LIMITS_MAX = 1024
+
+
+def limits_path(board_dir: str, gpu_id: int) -> Path:
+    return Path(board_dir) / f"gpu-{gpu_id}.limits"
+
+
+def write_limits(board_dir: str, gpu_id: int, limits: dict[int, int]) -> Path:
+    """The node-written core limits of one GPU (``mivgpu_board_limits_t``):
+    ``{host pid: limit ppm}``; the owner pass weighs each process with the
+    smaller of this and its flags' limit.  Written under a private name and
+    renamed into place (the owner re-reads it every 100 ms)."""
+    import struct
+    items = sorted((int(p), int(v)) for p, v in limits.items() if p > 0 and 0 < v < 1_000_000)[:LIMITS_MAX]
+    blob = struct.pack("<IiiI", LIMITS_MAGIC, LIMITS_VERSION, gpu_id, len(items))
+    blob += b"".join(struct.pack("<iI", p, v) for p, v in items)
+    path = limits_path(board_dir, gpu_id)
+    tmp = path.with_name(f".{path.name}.{os.getpid()}")
+    tmp.write_bytes(blob)
+    os.chmod(tmp, 0o644)
+    os.replace(tmp, path)
+    return path
+
+
 def board_host_dir(hook_path: str) -> str:
     return f"{hook_path}/vgpu/board"
 

@@ -17,6 +17,7 @@ shim obeys when it has one: a tenant rewriting its region cannot clear them.
 from __future__ import annotations
 
 import logging
+import os
 import re
 import threading
 
@@ -216,12 +217,15 @@ def publish_controls(lister: ContainerLister, grants: dict, decisions: dict, ver
     return n
 
 
-def feedback_pass(lister: ContainerLister, truth=None, escalation=None, lease_s: float = DEFAULT_LEASE_S) -> dict:
+def feedback_pass(lister: ContainerLister, truth=None, escalation=None, lease_s: float = DEFAULT_LEASE_S,
+                  board_dir: str | None = None) -> dict:
     """One pass: map host pids, restore the region mirrors of the limits from
     the grants, enforce HBM from host truth (hosttruth.HostTruth, optional:
     over grant, shim not loaded, excess), the priority feedback, the
     verdicts into the read-only control files, then the over-grant
-    escalation (escalate.OverGrantPolicy, optional)."""
+    escalation (escalate.OverGrantPolicy, optional).  With host truth and a
+    share-board directory, each GPU's node-written core limits (board.py
+    write_limits: the grant's limit of every process host truth attributes)."""
     from .hosttruth import load_grants
 
     lister.update()
@@ -231,6 +235,13 @@ def feedback_pass(lister: ContainerLister, truth=None, escalation=None, lease_s:
     verdicts: dict = {}
     if truth is not None:
         verdicts = truth.enforce(lister, grants, lister.pod)
+        if board_dir and os.path.isdir(board_dir):
+            from .board import write_limits
+            for gid, w in getattr(truth, "weights", {}).items():
+                try:
+                    write_limits(board_dir, gid, w)
+                except OSError as e:
+                    log.warning("share board limits for gpu %d: %s", gid, e)
     over = {k for k, v in verdicts.items() if v.over}
     decisions: dict = {}
     ut = observe(lister, over, decisions)
@@ -241,7 +252,8 @@ def feedback_pass(lister: ContainerLister, truth=None, escalation=None, lease_s:
 
 
 def watch_and_feedback(lister: ContainerLister, stop: threading.Event, period: float = 5.0,
-                       pause: threading.Event | None = None, truth=None, escalation=None):
+                       pause: threading.Event | None = None, truth=None, escalation=None,
+                       board_dir: str | None = None):
     """The 5 s loop; skipped while ``pause`` is set (a compute-partition apply
     is in progress, cmd/vGPUmonitor/main.go:79-109).  The control-file lease
     covers four periods, so a paused or dead monitor releases its verdicts."""
@@ -249,6 +261,6 @@ def watch_and_feedback(lister: ContainerLister, stop: threading.Event, period: f
         if pause is not None and pause.is_set():
             continue
         try:
-            feedback_pass(lister, truth, escalation, lease_s=max(DEFAULT_LEASE_S, 4 * period))
+            feedback_pass(lister, truth, escalation, lease_s=max(DEFAULT_LEASE_S, 4 * period), board_dir=board_dir)
         except Exception:  # noqa: BLE001
             log.exception("feedback iteration failed")

@@ -75,6 +75,8 @@ class Grant:
     # per device: a fractional core limit with no CU mask -- only the shim's
     # governor limits that container's compute (cuPartition: false)
     governed: list[bool] = field(default_factory=list)
+    # per device: the core limit in ppm of the GPU (0 = none)
+    core_ppm: list[int] = field(default_factory=list)
 
     @property
     def key(self) -> str:
@@ -105,7 +107,19 @@ def load_grants(limits_dir: Path | str) -> dict[str, Grant]:
         g = parse_grant(text)
         uuids = [u for u in (g.get("MIVGPU_DEVICE_UUIDS") or "").split(",") if u]
         mem = expected_region(g)["mem_limit"][:max(1, len(uuids))]
-        out[f.stem] = Grant(uid, ctr, uuids, mem, str(f), mtime, governed=_governed(g, max(1, len(uuids))))
+        n = max(1, len(uuids))
+        out[f.stem] = Grant(uid, ctr, uuids, mem, str(f), mtime, governed=_governed(g, n), core_ppm=_core_ppm(g, n))
+    return out
+
+
+def _core_ppm(g: dict, n: int) -> list[int]:
+    """Each device's core limit in ppm (0 = none), as the shim parses it."""
+    from .feedback import core_limit_ppm
+
+    out = []
+    for i in range(n):
+        ppm = core_limit_ppm(g.get(f"HIP_DEVICE_CORE_LIMIT_{i}") or g.get("HIP_DEVICE_CORE_LIMIT") or "")
+        out.append(ppm if 0 < ppm < 1_000_000 else 0)
     return out
 
 
@@ -164,6 +178,9 @@ class HostTruth:
         self._excess_prev: dict[tuple, int] = {}
         self._suspect: set[tuple] = set()      # no live shim in the previous pass
         self._reported: set[tuple] = set()     # (reason, pod_uid, container) with an event out
+        # KFD gpu_id -> {host pid: core limit ppm} of the processes attributed
+        # to a limited container (the share boards' node-written limits)
+        self.weights: dict[int, dict[int, int]] = {}
 
     # ------------------------------------------------------------ sources
     def vram(self, host_pid: int, gpu_id: int) -> int:
@@ -202,6 +219,7 @@ class HostTruth:
                 if u in ids:
                     users.setdefault((g.pod_uid, u), []).append((g, i))
         verdicts: dict[tuple, Verdict] = {}
+        weights: dict[int, dict[int, int]] = {gid: {} for gid in ids.values()}
 
         def verdict(g: Grant) -> Verdict:
             v = verdicts.get((g.pod_uid, g.container))
@@ -233,6 +251,11 @@ class HostTruth:
                 charged.append((g, i, c, live, t, own))
             grant_sum = 0
             for g, i, c, live, t, own in charged:
+                ppm = g.core_ppm[i] if i < len(g.core_ppm) else 0
+                if ppm:
+                    w = weights.setdefault(gid, {})
+                    for p in own:
+                        w[p] = min(w.get(p, ppm), ppm)
                 v = verdict(g)
                 v.truth[i] = t
                 v.pids[i] = sorted(own)
@@ -300,6 +323,7 @@ class HostTruth:
             self.truth = {(u, c, i): t for (u, c), v in verdicts.items() for i, t in v.truth.items()}
             self.over = {k for k, v in verdicts.items() if v.over}
             self.no_shim = {k for k, v in verdicts.items() if not v.shim_loaded}
+            self.weights = weights
             # an event again once the condition cleared and came back
             self._reported = {r for r in self._reported
                               if (r[0] == OVER_GRANT_REASON and (r[1], r[2]) in self.over)

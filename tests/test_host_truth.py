@@ -357,3 +357,20 @@ def test_shimless_action_none_keeps_the_old_behaviour(tmp_path):
     lister, truth, cluster = _shimless(tmp_path, 6 * GIB)
     pol = OverGrantPolicy("block", passes=1, client=cluster, shimless_action="none")
     assert all(feedback.feedback_pass(lister, truth, pol)["actions"] == [] for _ in range(3))
+
+
+def test_feedback_writes_the_share_boards_node_limits(tmp_path):
+    """Each pass the monitor writes, per GPU, the core limit of every process
+    host truth attributes to a limited container (board.py write_limits):
+    the share board's owner weighs a tenant with it, so a tenant cannot buy a
+    larger fair share by publishing a larger limit in its flags."""
+    import struct
+    from k8s_vgpu_scheduler_amd.monitor import board as B
+    lister, truth, _ = _shimless(tmp_path, GIB, core="12.5")
+    bd = tmp_path / "board"
+    bd.mkdir()
+    feedback.feedback_pass(lister, truth, None, board_dir=str(bd))
+    raw = B.limits_path(str(bd), 42).read_bytes()
+    magic, ver, gid, n = struct.unpack_from("<IiiI", raw)
+    assert (magic, ver, gid, n) == (B.LIMITS_MAGIC, B.LIMITS_VERSION, 42, 1)
+    assert struct.unpack_from("<iI", raw, 16) == (4711, 125000)

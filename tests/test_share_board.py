@@ -328,3 +328,18 @@ def test_governed_tenants_filling_the_gpu_are_held_on_their_lead(native_build, t
     for i in (ia, ib):
         assert i["fair_samples"] > 50, i
         assert i["fair_held_samples"] <= 0.05 * i["fair_samples"], i
+
+
+def test_node_written_limits_cap_what_a_tenant_publishes(native_build, tmp_path):
+    """A 25 % tenant claiming 100 % in its flags next to an honest 75 % one:
+    with the monitor's limits file (the grant's 25 %) the owner weighs it 25 %,
+    so it is the one that leads; without the file its claim would have put
+    the honest tenant in the lead."""
+    d = tmp_path / "board"
+    d.mkdir()
+    B.write_limits(str(d), 4242, {222: 250000})
+    s = _fair_run(native_build, tmp_path, {111: (10, B.FLAG_OWES, 750000), 222: (10, B.FLAG_OWES, 0)})
+    assert s[111].lead_ns == 0 and s[222].lead_ns > 5_000_000, (s[111].lead_ns, s[222].lead_ns)
+    B.limits_path(str(d), 4242).unlink()
+    s = _fair_run(native_build, tmp_path / "nofile", {111: (10, B.FLAG_OWES, 750000), 222: (10, B.FLAG_OWES, 0)})
+    assert s[222].lead_ns == 0 and s[111].lead_ns > 0, (s[111].lead_ns, s[222].lead_ns)
