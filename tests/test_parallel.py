@@ -36,7 +36,7 @@ def _run(world, tmp_path, extra=()):
     return json.loads(open(out).read())
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_collectives_exact_on_gloo(world, tmp_path):
     doc = _run(world, tmp_path)
     assert doc["world"] == world and doc["backend"] == "gloo"
