@@ -202,7 +202,9 @@ typedef struct {
   uint64_t want_fast_ns;  /* writable boards: a governed tenant's latest ask for fast passes */
   uint64_t busy_ns;       /* time with any process's waves resident           */
   uint64_t pass_ns;       /* cost of the last pass                            */
-  uint64_t unused[6];
+  uint64_t sub_passes;    /* passes with the backlogged weights filling the GPU */
+  uint64_t fair_passes;   /* passes in fair-share mode                        */
+  uint64_t unused[4];
   mivgpu_board_slot_t slots[MIVGPU_BOARD_SLOTS];
 } mivgpu_board_t; /* 128 + 4096 B */
 

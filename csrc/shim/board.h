@@ -37,12 +37,19 @@ constexpr int kGateUnits = 1;
 constexpr uint64_t kSlotStaleNs = 1000000000ull;
 // Passes longer apart than this do not invent history (a stalled owner).
 constexpr uint64_t kMaxDtNs = 100000000ull;
-// Fair-share mode (shared_region.h vt_ns / lead_ns): entered when the GPU
-// has been fully subscribed -- the backlogged processes' core limits adding
-// up to the whole GPU -- in most passes of the last ~10 ms (EWMA >= 0.8), left
-// below 0.5.
+// Fair-share mode (shared_region.h vt_ns / lead_ns): a process counts as
+// backlogged while it was backlogged in at least half of the passes of the
+// last ~10 ms (EWMA), so that one tenant's host gap does not break the
+// subscription of eight; the mode is entered when the GPU has been fully
+// subscribed -- those processes' core limits adding up to the whole GPU -- in
+// most passes of the last ~10 ms (EWMA >= 0.8), left below 0.5.
 constexpr uint64_t kSubTauNs = 10000000ull;
 constexpr double kSubEnter = 0.8, kSubLeave = 0.5;
+// Fair-share mode: credit a process keeps while it is not backlogged (its
+// virtual time trails the smallest running one by at most this much GPU
+// time): a tenant returning from a short gap is still behind the ones that
+// ran without it, one away for long has banked no more than this.
+constexpr uint64_t kCreditNs = 5000000ull;
 // Fair-share mode: a tenant's lead over the furthest-behind contender is
 // bounded here (virtual time beyond it is dropped: a tenant cannot bank an
 // unbounded lead that holds it for seconds).
@@ -70,6 +77,8 @@ struct Handle {
   uint64_t lims_ns = 0;
   // owner-private fair-share state
   bool was_backlogged[MIVGPU_BOARD_SLOTS] = {};   // per board slot, the previous pass
+  double bl_ewma[MIVGPU_BOARD_SLOTS] = {};        // per board slot, share of recent passes backlogged
+  uint32_t last_lim[MIVGPU_BOARD_SLOTS] = {};     // per board slot, the weight of its last fresh flags
   double sub_ewma = 0;                            // share of recent passes fully subscribed
   bool fair = false;                              // fair-share mode
   uint64_t vmin = 0;                              // the previous pass's smallest running virtual time
@@ -330,11 +339,11 @@ enum Split { kSplitRatio = 0, kSplitEqual = 1 };
 // without flags: waves resident), weighted by its core limit (flags; 100 %
 // without; the monitor's node-written limit caps it).  In fair-share mode
 // (the backlogged weights filling the GPU in most recent passes) each
-// backlogged process's virtual time advances by the
-// GPU share it received / its weight; one not backlogged, or held while
-// behind, is pulled up to the smallest running virtual time (no credit is
-// banked while away), and every process's lead is (vt - that minimum) x its
-// weight.  Outside the mode lead_ns = -1: the tenants' own token buckets cap
+// backlogged process's virtual time advances by the GPU share it received /
+// its weight; one not backlogged, or held while behind, keeps at most
+// kCreditNs of credit below the smallest running virtual time (a short gap
+// does not forgive the ones that ran without it, a long one banks nothing
+// more), and every process's lead is (vt - that minimum) x its weight.  Outside the mode lead_ns = -1: the tenants' own token buckets cap
 // them.
 inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_t period_ns, int kind,
                        int owner_pid, int split, uint64_t pass_cost_ns) {
@@ -398,6 +407,8 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
       s.pid = r[i].pid;
       s.lead_ns = -1;
       h.was_backlogged[slot] = false;
+      h.bl_ewma[slot] = 0;
+      h.last_lim[slot] = 0;
       if (slot + 1 > hi) hi = slot + 1;
     }
     sl[i] = slot;
@@ -408,8 +419,16 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
     const bool owes = st[i] >= 0 && (st[i] & MIVGPU_FLAG_OWES);
     s.occupancy = v;
     s.seen_ns = now;
+    // a tenant whose flags went stale for a moment (its sampler thread
+    // descheduled) keeps the weight of its last fresh ones
+    if (st[i] >= 0) h.last_lim[slot] = lim[i];
+    else if (h.last_lim[slot]) lim[i] = h.last_lim[slot];
     bl[i] = st[i] >= 0 ? (held || owes) : w > 0;
-    if (bl[i]) {
+    if (dt) {
+      const double a = (double)dt / (double)kSubTauNs < 1.0 ? (double)dt / (double)kSubTauNs : 1.0;
+      h.bl_ewma[slot] += a * ((bl[i] ? 1.0 : 0.0) - h.bl_ewma[slot]);
+    }
+    if (h.bl_ewma[slot] >= 0.5) {
       sum_w += (double)lim[i] / 1e6;
       ++backlogged;
     }
@@ -437,6 +456,7 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
     const double a = (double)dt / (double)kSubTauNs < 1.0 ? (double)dt / (double)kSubTauNs : 1.0;
     h.sub_ewma += a * (x - h.sub_ewma);
   }
+  if (backlogged >= 2 && sum_w >= 0.999) b->sub_passes += 1;
   const bool entering = !h.fair && h.sub_ewma >= kSubEnter;
   h.fair = h.fair ? h.sub_ewma >= kSubLeave : entering;
   auto running = [&](int i) { return bl[i] && !(st[i] >= 0 && (st[i] & MIVGPU_FLAG_HELD)); };
@@ -454,7 +474,9 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
       const int k = sl[i];
       if (k < 0 || !bl[i]) continue;
       mivgpu_board_slot_t& s = b->slots[k];
-      if (!h.was_backlogged[k] && s.vt_ns < h.vmin) s.vt_ns = h.vmin;   // joins at the running minimum
+      // joins within its credit of the running minimum (a new process too)
+      const uint64_t credit = (uint64_t)((double)kCreditNs * 1e6 / (double)lim[i]);
+      if (!h.was_backlogged[k] && s.vt_ns + credit < h.vmin) s.vt_ns = h.vmin - credit;
       s.vt_ns += (uint64_t)(use[i] * (double)dt * 1e6 / (double)lim[i] + 0.5);
     }
     uint64_t vmin = UINT64_MAX;
@@ -465,12 +487,18 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
       const int k = sl[i];
       if (k < 0) continue;
       mivgpu_board_slot_t& s = b->slots[k];
-      if (s.vt_ns < vmin) s.vt_ns = vmin;
+      if (running(i)) {
+        if (s.vt_ns < vmin) s.vt_ns = vmin;
+      } else {
+        const uint64_t credit = (uint64_t)((double)kCreditNs * 1e6 / (double)lim[i]);
+        if (s.vt_ns + credit < vmin) s.vt_ns = vmin - credit;
+      }
       const uint64_t cap = vmin + (uint64_t)((double)kMaxLeadNs * 1e6 / (double)lim[i]);
       if (s.vt_ns > cap) s.vt_ns = cap;
-      s.lead_ns = (int64_t)((double)(s.vt_ns - vmin) * (double)lim[i] / 1e6 + 0.5);
+      s.lead_ns = s.vt_ns > vmin ? (int64_t)((double)(s.vt_ns - vmin) * (double)lim[i] / 1e6 + 0.5) : 0;
     }
     h.vmin = vmin;
+    b->fair_passes += 1;
   } else {
     for (int i = 0; i < n; ++i)
       if (sl[i] >= 0) b->slots[sl[i]].lead_ns = -1;

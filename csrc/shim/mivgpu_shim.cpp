@@ -3727,10 +3727,11 @@ MIVGPU_EXPORT int mivgpu_sampler_info(int dev, char* buf, int n) {
     return len;
   }
   put("{\"dir\":\"%s\",\"open\":1,\"writable\":%d,\"owner\":%d,\"owner_kind\":%d,\"owner_pid\":%d,"
-      "\"beat_age_ms\":%.2f,\"passes\":%llu,\"period_us\":%.0f,\"busy_ms\":%.1f,\"slots\":[",
+      "\"beat_age_ms\":%.2f,\"passes\":%llu,\"sub_passes\":%llu,\"fair_passes\":%llu,\"period_us\":%.0f,"
+      "\"busy_ms\":%.1f,\"slots\":[",
       g_cfg.board_dir, o.board.writable ? 1 : 0, o.board.owner ? 1 : 0, b->owner_kind, b->owner_pid,
       b->beat_ns ? ((double)now - (double)b->beat_ns) / 1e6 : -1.0, (unsigned long long)b->passes,
-      b->period_ns / 1e3, b->busy_ns / 1e6);
+      (unsigned long long)b->sub_passes, (unsigned long long)b->fair_passes, b->period_ns / 1e3, b->busy_ns / 1e6);
   bool first = true;
   for (int k = 0; k < MIVGPU_BOARD_SLOTS; ++k) {
     const mivgpu_board_slot_t& s = b->slots[k];

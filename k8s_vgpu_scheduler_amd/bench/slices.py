@@ -370,7 +370,11 @@ def _governor_stats() -> dict:
         bd = si.get("board") or {}
         out["sampler"] = {"board_charged": si.get("board_charged"), "local_charged": si.get("local_charged"),
                           "board_share": si.get("board_share"), "board_owner": bd.get("owner"),
-                          "owner_kind": bd.get("owner_kind"), "board_slots": len(bd.get("slots") or [])}
+                          "owner_kind": bd.get("owner_kind"), "board_slots": len(bd.get("slots") or []),
+                          # fair-share mode (board.h): samples in it / held there on the lead
+                          "fair_samples": si.get("fair_samples"), "fair_held_samples": si.get("fair_held_samples"),
+                          "board_passes": bd.get("passes"), "board_sub_passes": bd.get("sub_passes"),
+                          "board_fair_passes": bd.get("fair_passes")}
     cache = os.environ.get("MIVGPU_SHARED_CACHE")
     if cache and os.path.exists(cache):
         from k8s_vgpu_scheduler_amd.monitor.region import SharedRegion

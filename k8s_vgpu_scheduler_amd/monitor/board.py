@@ -54,7 +54,8 @@ class BoardHeader(C.Structure):
     _fields_ = [("magic", C.c_uint32), ("version", C.c_int32), ("gpu_id", C.c_int32), ("owner_kind", C.c_int32),
                 ("owner_pid", C.c_int32), ("nslots", C.c_int32), ("seq", C.c_uint64), ("beat_ns", C.c_uint64),
                 ("period_ns", C.c_uint64), ("passes", C.c_uint64), ("want_fast_ns", C.c_uint64),
-                ("busy_ns", C.c_uint64), ("pass_ns", C.c_uint64), ("unused", C.c_uint64 * 6),
+                ("busy_ns", C.c_uint64), ("pass_ns", C.c_uint64), ("sub_passes", C.c_uint64),
+                ("fair_passes", C.c_uint64), ("unused", C.c_uint64 * 4),
                 ("slots", BoardSlot * BOARD_SLOTS)]
 
 

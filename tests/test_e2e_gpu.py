@@ -183,9 +183,23 @@ def test_shimless_container_on_time_shared_gpu_is_evicted(tmp_path_factory):
     over-grant action is the default block.  The monitor maps the pod to its
     host pids from the cgroup (hostpid.py); this box runs the "container" as a
     plain process, so the test hands the monitor a process table in which that
-    process's cgroup names the pod."""
+    process's cgroup names the pod.  The box runs jobs in a pid namespace: the
+    probe's host pid is the KFD process entry that appears with its 2 GiB on
+    the GPU."""
     import os
     import time
+
+    kfd_proc = "/sys/class/kfd/kfd/proc"
+
+    def vram(pid):   # the most it holds on any GPU
+        best = 0
+        try:
+            for f in os.listdir(f"{kfd_proc}/{pid}"):
+                if f.startswith("vram_"):
+                    best = max(best, int(open(f"{kfd_proc}/{pid}/{f}").read().strip() or 0))
+        except (OSError, ValueError):
+            pass
+        return best
     root = tmp_path_factory.mktemp("e2e-shimless")
     procs = root / "proc"
     procs.mkdir()
@@ -198,16 +212,23 @@ def test_shimless_container_on_time_shared_gpu_is_evicted(tmp_path_factory):
         env = container_env(alloc)
         env["PYTHONPATH"] = str(REPO)
         env.pop("LD_PRELOAD", None)
+        before = set(os.listdir(kfd_proc))
         p = _probe(env, "matmul", "--n", "2048", "--iters", "50", "--oom-probe-mib", "2048", "--hold-s", "90",
                    wait=False)
         try:
-            d = procs / str(p.pid)
-            d.mkdir()
-            (d / "status").write_text(f"Name:\tpython\nNSpid:\t{p.pid}\n")
-            (d / "cgroup").write_text(f"0::/kubepods.slice/kubepods-burstable.slice/pod{uid}/cri-rogue\n")
             t0 = time.monotonic()
-            wait_for(lambda: os.path.exists(f"/sys/class/kfd/kfd/proc/{p.pid}"), 120, "the probe to open the GPU")
+
+            def host_pid():
+                assert p.poll() is None, p.communicate()[1][-2000:]
+                new = [int(e) for e in set(os.listdir(kfd_proc)) - before
+                       if e.isdigit() and vram(e) >= 2048 * MIB]
+                return new[0] if len(new) == 1 else None
+            hp = wait_for(host_pid, 120, "the probe to hold its 2 GiB on the GPU")
             seen = time.monotonic()
+            d = procs / str(hp)
+            d.mkdir()
+            (d / "status").write_text(f"Name:\tpython\nNSpid:\t{hp}\t{p.pid}\n")
+            (d / "cgroup").write_text(f"0::/kubepods.slice/kubepods-burstable.slice/pod{uid}/cri-rogue\n")
             wait_for(lambda: ("default", "rogue") in cl.api.cluster.evictions, 60,
                      "the monitor to evict the shimless pod")
             took = time.monotonic() - seen
