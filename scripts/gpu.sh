@@ -22,6 +22,7 @@
 #   serving     TTFT / per-token latency, native vs vGPU slices (bench/serving.py)
 #   mixed       governed server + 3 governed decode tenants; 8 x 12 % temporal over 600 steps
 #   board       share board: 4 x 25 % / 8 x 12.5 % temporal vs native, unequal limits, time-sharing e2e
+#   eight       8 slices: disjoint ranges vs one pooled whole-GPU range (cuShareUnit 256), monitor on/off
 #   kern        prefill kernels: flash attention A/B at 512 / 2048 / 8192, packed-weight GEMM vs hipBLASLt;
 #               decode K-split GEMM two vs four k-blocks per group
 #   prefill     prefill microbench + rocprofv3 kernel summary, whole GPU and 64 CUs
@@ -185,6 +186,18 @@ case $suite in
       --timeout-method thread
     step 300 e2e python -u -m pytest tests/test_e2e_gpu.py -v -s --timeout 240 --timeout-method thread \
       -k "time_sharing or shimless" ;;
+  eight)
+    # 8 slices per GPU: disjoint 32-CU ranges vs the eight
+    # pooled into one whole-GPU shared range (cuShareUnit 256) with and without
+    # the node monitor's utilisation switch, 100 and 20 steps, vs native
+    step 400 disjoint python -u bench.py --slices 8 --rounds shim,native --layout disjoint --steps 100 \
+      --out "$out/disjoint.json"
+    step 400 h256 python -u bench.py --slices 8 --rounds shim,native --layout hybrid --share-unit 256 --steps 100 \
+      --out "$out/h256.json"
+    step 400 h256_mon python -u bench.py --slices 8 --rounds shim,native --layout hybrid --share-unit 256 \
+      --steps 100 --monitor 0.5 --out "$out/h256_mon.json"
+    step 400 h256_20 python -u bench.py --slices 8 --rounds shim,native --layout hybrid --share-unit 256 \
+      --steps 20 --warmup 5 --out "$out/h256_20.json" ;;
   kern)
     # prefill kernels: flash attention (eight-wave vs 32-key-tile kernel) and
     # the packed-weight GEMM (vs unpack + hipBLASLt), numerics then timing
