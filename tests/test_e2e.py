@@ -104,3 +104,42 @@ def test_gputype_and_uuid_selection(cluster):
             if "use-gpu-uuid" in str(annos):
                 assert devs[1].id in json.dumps(alloc), alloc
         cl.delete_pod("default", name)
+
+
+def test_shimless_container_on_a_time_shared_node_is_evicted(tmp_path):
+    """The shimless-eviction path end to end on the CPU (the GPU test's twin,
+    tests/test_e2e_gpu.py): the real binaries on a time-sharing node
+    (cuPartition: false), a fake KFD holding the container's VRAM under a host
+    pid the monitor maps to the pod through the cgroup, no shim region: the
+    monitor evicts the pod within --over-grant-passes (3) 5 s passes under the
+    default block action."""
+    import time
+    kfd = tmp_path / "kfd"
+    for i, (gid, bus) in enumerate(((4242, 0x11), (5151, 0x12)), start=1):
+        n = kfd / "topology" / "nodes" / str(i)
+        n.mkdir(parents=True)
+        (n / "gpu_id").write_text(f"{gid}\n")
+        (n / "properties").write_text(f"simd_count 1024\nlocation_id {bus << 8}\ndomain 0\n")
+    procs = tmp_path / "proc"
+    procs.mkdir()
+    with E2ECluster(str(tmp_path / "cl"), fake_gpus=2, split=8, device_config={"amd": {"cuPartition": False}},
+                    extra_env={"MIVGPU_KFD_SYSFS": str(kfd)}, monitor_args=["--proc-root", str(procs)]) as cl:
+        cl.submit(amd_pod("rogue", mem=8192, cores=12))
+        assert cl.schedule("default", "rogue") == "node1"
+        alloc = cl.start_containers("default", "rogue")[0]
+        env = container_env(alloc)
+        uid = cl.api.cluster.get("pods", "rogue", "default")["metadata"]["uid"]
+        gid = {"GPU-0000": 4242, "GPU-0001": 5151}[env["MIVGPU_DEVICE_UUIDS"].split(",")[0]]
+        hp = 777777
+        (kfd / "proc" / str(hp)).mkdir(parents=True)
+        (kfd / "proc" / str(hp) / f"vram_{gid}").write_text(f"{2 << 30}\n")
+        (procs / str(hp)).mkdir()
+        (procs / str(hp) / "status").write_text(f"Name:\tpython\nNSpid:\t{hp}\t42\n")
+        (procs / str(hp) / "cgroup").write_text(f"0::/kubepods.slice/pod{uid}/cri-rogue\n")
+        t0 = time.monotonic()
+        try:
+            wait_for(lambda: ("default", "rogue") in cl.api.cluster.evictions, 40,
+                     "the monitor to evict the shimless pod")
+        except TimeoutError:
+            pytest.fail("not evicted; monitor log:\n" + cl.logs("monitor")[-4000:])
+        assert time.monotonic() - t0 <= 4 * 5 + 5

@@ -229,8 +229,13 @@ def test_shimless_container_on_time_shared_gpu_is_evicted(tmp_path_factory):
             d.mkdir()
             (d / "status").write_text(f"Name:\tpython\nNSpid:\t{hp}\t{p.pid}\n")
             (d / "cgroup").write_text(f"0::/kubepods.slice/kubepods-burstable.slice/pod{uid}/cri-rogue\n")
-            wait_for(lambda: ("default", "rogue") in cl.api.cluster.evictions, 60,
-                     "the monitor to evict the shimless pod")
+            try:
+                wait_for(lambda: ("default", "rogue") in cl.api.cluster.evictions, 60,
+                         "the monitor to evict the shimless pod")
+            except TimeoutError:
+                host = samples(cl.metrics("mon_metrics"), "hami_host_gpu_memory_used_bytes")
+                pytest.fail(f"not evicted (host pid {hp}, host truth {host}); monitor log:\n"
+                            + cl.logs("monitor")[-4000:])
             took = time.monotonic() - seen
             print(json.dumps({"evicted_after_s": round(took, 1), "since_start_s": round(time.monotonic() - t0, 1)}))
             # the first pass after the GPU open, then at most 3 more 5 s passes
