@@ -151,8 +151,8 @@ typedef struct {
  *   vt_ns   -- its virtual time while the GPU is fully subscribed (below):
  *              the integral of frac / its core limit,
  *   lead_ns -- -1 while the GPU is not fully subscribed, else its GPU time
- *              received beyond its weighted fair share: (vt - the smallest
- *              vt of the running contenders) x its limit.
+ *              received beyond its weighted fair share: (vt - the mean vt of
+ *              the running contenders) x its limit, >= 0.
  * A tenant charges (delta frac_ns / delta obs_ns) x its own non-held time.
  * Fully subscribed: the core limits of the processes contending for the GPU
  * (owing work or held in a gate, within 20 ms; a process without flags counts
@@ -160,8 +160,7 @@ typedef struct {
  * equilibrium (the time they are charged sums to the time they accrue), so a
  * bucket balance -- and any debt carried in from a phase alone -- never
  * recovers and holds cascade; the tenants are held on their lead instead
- * (weighted fair sharing, work-conserving: the tenant furthest behind always
- * runs).
+ * (weighted fair sharing, work-conserving: the tenants behind always run).
  *
  * The owner is the node sampler (mivgpu-boardd, run by the monitor; the
  * board directory is mounted READ-ONLY into containers, so no tenant can

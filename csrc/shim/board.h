@@ -343,7 +343,8 @@ enum Split { kSplitRatio = 0, kSplitEqual = 1 };
 // its weight; one not backlogged, or held while behind, keeps at most
 // kCreditNs of credit below the smallest running virtual time (a short gap
 // does not forgive the ones that ran without it, a long one banks nothing
-// more), and every process's lead is (vt - that minimum) x its weight.  Outside the mode lead_ns = -1: the tenants' own token buckets cap
+// more), and every process's lead is (vt - the running processes' mean vt)
+// x its weight.  Outside the mode lead_ns = -1: the tenants' own token buckets cap
 // them.
 inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_t period_ns, int kind,
                        int owner_pid, int split, uint64_t pass_cost_ns) {
@@ -480,8 +481,15 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
       s.vt_ns += (uint64_t)(use[i] * (double)dt * 1e6 / (double)lim[i] + 0.5);
     }
     uint64_t vmin = UINT64_MAX;
+    double vsum = 0;
+    int nrun = 0;
     for (int i = 0; i < n; ++i)
-      if (sl[i] >= 0 && running(i) && b->slots[sl[i]].vt_ns < vmin) vmin = b->slots[sl[i]].vt_ns;
+      if (sl[i] >= 0 && running(i)) {
+        const uint64_t vt = b->slots[sl[i]].vt_ns;
+        if (vt < vmin) vmin = vt;
+        vsum += (double)vt;
+        ++nrun;
+      }
     if (vmin == UINT64_MAX) vmin = h.vmin;
     for (int i = 0; i < n; ++i) {
       const int k = sl[i];
@@ -495,7 +503,12 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
       }
       const uint64_t cap = vmin + (uint64_t)((double)kMaxLeadNs * 1e6 / (double)lim[i]);
       if (s.vt_ns > cap) s.vt_ns = cap;
-      s.lead_ns = s.vt_ns > vmin ? (int64_t)((double)(s.vt_ns - vmin) * (double)lim[i] / 1e6 + 0.5) : 0;
+      // the lead is taken over the running processes' mean virtual time:
+      // against the minimum, the spread of eight tenants' noisy estimates
+      // alone put every one but the last behind its gate a third of the time
+      const double vmean = nrun ? vsum / nrun : (double)vmin;
+      const double ahead = (double)s.vt_ns - vmean;
+      s.lead_ns = ahead > 0 ? (int64_t)(ahead * (double)lim[i] / 1e6 + 0.5) : 0;
     }
     h.vmin = vmin;
     b->fair_passes += 1;

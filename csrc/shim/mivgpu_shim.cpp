@@ -1755,9 +1755,11 @@ constexpr uint64_t kPeerBusyNs = 200000000ull;   // 200 ms
 constexpr uint64_t kBoardStaleNs = 50000000ull;   // 50 ms
 // Idle time after which the host bucket stops accruing entitlement.
 constexpr uint64_t kAccrueIdleNs = 20000000ull;   // 20 ms
-// Fair-share mode (board.h): lead over the furthest-behind backlogged tenant
-// at which the gate holds (GPU time beyond the weighted fair share).
-constexpr uint64_t kFairLagNs = 5000000ull;        // 5 ms
+// Fair-share mode (board.h): lead over the backlogged tenants' mean at which
+// the gate holds (GPU time beyond the weighted fair share).  Per decode step
+// a tenant's wave-share estimate scatters by ~0.7 ms at eight tenants; a
+// 5 ms lag held symmetric tenants 20-40 % of their samples on noise.
+constexpr uint64_t kFairLagNs = 10000000ull;       // 10 ms
 // A governed peer held behind its gate has exactly its gate kernel's wave
 // resident (governor.hip host_bucket_gate: one 64-lane wave).
 constexpr int kGateWaves = 1;
@@ -2131,12 +2133,14 @@ bool occ_sample(int dev, uint64_t now) {
     // to the others and a debt (one carried in from a phase alone, or noise)
     // is never repaid -- measured, four symmetric 25 % tenants held 0.4-1.1 s
     // each over a 1.6 s run, at 0.82 of native.  There the tenant is held on
-    // its lead over the furthest-behind backlogged tenant instead (the tenant
-    // furthest behind always runs: work-conserving, shares by core limit) and
-    // its bucket carries no debt out of the mode.
+    // its lead over the backlogged tenants' mean instead (the tenants behind
+    // always run: work-conserving, shares by core limit) and its bucket
+    // carries nothing out of the mode: no debt, and no burst either (a 25 %
+    // tenant left alone by a 75 % one that finished spent up to the whole
+    // 100 ms burst it had banked while held on its lead: 27 % of the GPU).
     double eff = o.tokens_ns;
     if (lead >= 0) {
-      if (o.tokens_ns < 0) o.tokens_ns = 0;
+      o.tokens_ns = 0;
       eff = (double)kFairLagNs - (double)lead;
       ++o.fair_samples;
       if (eff < 0) ++o.fair_held_samples;
