@@ -303,6 +303,7 @@ def child_main(argv):
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
     torch.cuda.synchronize()
     rx0 = _received_ns()
+    c0 = _timed_counters()
     t_start = time.time()
     t0 = time.perf_counter()
     evs[0].record()
@@ -317,6 +318,11 @@ def child_main(argv):
             "tpot_ms_p50": tpot[len(tpot) // 2],
             "tpot_ms_p99": tpot[min(len(tpot) - 1, int(0.99 * len(tpot)))]}
     rx1 = _received_ns()
+    c1 = _timed_counters()
+    if c0 and c1:
+        # the governor over the timed steps only (its totals include the load
+        # and warmup, when the slices ran at different times)
+        done["timed"] = {k: round(c1[k] - c0[k], 1) for k in c1 if k in c0}
     if rx0 is not None and rx1 is not None:
         # GPU time the slice received over the timed steps (the governor's
         # share integral), as a share of the wall time
@@ -341,6 +347,33 @@ def _received_ns():
     if fn(0, ctypes.byref(t), ctypes.byref(r)) != 0:
         return None
     return r.value
+
+
+def _timed_counters() -> dict:
+    """Governor counters to difference over the timed steps (empty without
+    the shim): held time and gates, the sampler's samples in fair-share mode
+    and held there, and the share board's passes (all / fully subscribed /
+    in fair-share mode)."""
+    import ctypes
+    if not os.environ.get("LD_PRELOAD"):
+        return {}
+    out = {}
+    try:
+        b, h, g = ctypes.c_ulonglong(), ctypes.c_ulonglong(), ctypes.c_ulonglong()
+        if ctypes.CDLL(None).mivgpu_gate_stats(0, ctypes.byref(b), ctypes.byref(h), ctypes.byref(g)) == 0:
+            out.update({"held_ms": h.value / 1e6, "gates": g.value})
+    except (OSError, AttributeError):
+        return out
+    from k8s_vgpu_scheduler_amd.shim.probe import sampler_info
+    si = sampler_info() or {}
+    bd = si.get("board") or {}
+    for k in ("samples", "fair_samples", "fair_held_samples"):
+        if k in si:
+            out[k] = si[k]
+    for k in ("passes", "sub_passes", "fair_passes"):
+        if k in bd:
+            out["board_" + k] = bd[k]
+    return out
 
 
 def _governor_stats() -> dict:

@@ -22,6 +22,7 @@
 #   serving     TTFT / per-token latency, native vs vGPU slices (bench/serving.py)
 #   mixed       governed server + 3 governed decode tenants; 8 x 12 % temporal over 600 steps
 #   board       share board: 4 x 25 % / 8 x 12.5 % temporal vs native, unequal limits, time-sharing e2e
+#   fair        temporal (fair-share governor) vs native: 4 slices at 20 / 100 steps, 8 slices
 #   eight       8 slices: disjoint ranges vs one pooled whole-GPU range (cuShareUnit 256), monitor on/off
 #   kern        prefill kernels: flash attention A/B at 512 / 2048 / 8192, packed-weight GEMM vs hipBLASLt;
 #               decode K-split GEMM two vs four k-blocks per group
@@ -186,6 +187,11 @@ case $suite in
       --timeout-method thread
     step 300 e2e python -u -m pytest tests/test_e2e_gpu.py -v -s --timeout 240 --timeout-method thread \
       -k "time_sharing or shimless" ;;
+  fair)
+    # the fair-share governor in the driver's own bench config (20 steps) and at 100 steps, 4 and 8 tenants
+    step 300 t4_20 python -u bench.py --rounds temporal,native --steps 20 --warmup 5 --out "$out/t4_20.json"
+    step 400 t4 python -u bench.py --rounds temporal,native --steps 100 --out "$out/t4.json"
+    step 400 t8 python -u bench.py --slices 8 --rounds temporal,native --steps 100 --out "$out/t8.json" ;;
   eight)
     # 8 slices per GPU: disjoint 32-CU ranges vs the eight
     # pooled into one whole-GPU shared range (cuShareUnit 256) with and without
