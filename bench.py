@@ -371,7 +371,8 @@ def main():
         if any("gov_gates" in d or "share_pct" in d for d in head["done"]):
             out["governor_rank0"] = [{k: d.get(k) for k in ("gov_charged_ms", "gov_held_ms", "gov_gates",
                                                             "share_pct", "util_pct", "busy_share_pct",
-                                                            "seconds", "sampler", "timed")} for d in head["done"]]
+                                                            "seconds", "sampler", "timed", "gov_sampler_pass_us_mean",
+                                                            "gov_sampler_pass_us_max")} for d in head["done"]]
         if "native" in results and "shim" in results:
             nat = results["native"]["tok_s"]
             out["native_value"] = round(nat, 2)
@@ -392,7 +393,8 @@ def main():
             out["temporal_isolation"] = f"governor gate (force, {'/'.join(lims)} % each, occupancy-charged)"
             out["temporal_governor_rank0"] = [{k: d.get(k) for k in ("gov_charged_ms", "gov_held_ms", "gov_gates",
                                                                      "share_pct", "util_pct", "busy_share_pct",
-                                                                     "sampler", "timed")} for d in tr["done"]]
+                                                                     "sampler", "timed", "gov_sampler_pass_us_mean",
+                                                                     "gov_sampler_pass_us_max")} for d in tr["done"]]
             if "native" in results:
                 out["temporal_overhead_pct"] = round((1.0 - tr["tok_s"] / results["native"]["tok_s"]) * 100.0, 2)
         if "eager_shim" in results and "eager_noshim" in results:

@@ -50,6 +50,9 @@ constexpr double kSubEnter = 0.8, kSubLeave = 0.5;
 // time): a tenant returning from a short gap is still behind the ones that
 // ran without it, one away for long has banked no more than this.
 constexpr uint64_t kCreditNs = 5000000ull;
+// Fair-share mode: a tenant whose flags went stale still counts as backlogged
+// by its last fresh state for this long.
+constexpr uint64_t kStateGraceNs = 100000000ull;
 // Fair-share mode: a tenant's lead over the furthest-behind contender is
 // bounded here (virtual time beyond it is dropped: a tenant cannot bank an
 // unbounded lead that holds it for seconds).
@@ -79,6 +82,8 @@ struct Handle {
   bool was_backlogged[MIVGPU_BOARD_SLOTS] = {};   // per board slot, the previous pass
   double bl_ewma[MIVGPU_BOARD_SLOTS] = {};        // per board slot, share of recent passes backlogged
   uint32_t last_lim[MIVGPU_BOARD_SLOTS] = {};     // per board slot, the weight of its last fresh flags
+  int last_state[MIVGPU_BOARD_SLOTS] = {};        // ... their state, and when they were fresh
+  uint64_t last_state_ns[MIVGPU_BOARD_SLOTS] = {};
   double sub_ewma = 0;                            // share of recent passes fully subscribed
   bool fair = false;                              // fair-share mode
   uint64_t vmin = 0;                              // the previous pass's smallest running virtual time
@@ -410,6 +415,7 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
       h.was_backlogged[slot] = false;
       h.bl_ewma[slot] = 0;
       h.last_lim[slot] = 0;
+      h.last_state_ns[slot] = 0;
       if (slot + 1 > hi) hi = slot + 1;
     }
     sl[i] = slot;
@@ -422,9 +428,21 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
     s.seen_ns = now;
     // a tenant whose flags went stale for a moment (its sampler thread
     // descheduled) keeps the weight of its last fresh ones
-    if (st[i] >= 0) h.last_lim[slot] = lim[i];
-    else if (h.last_lim[slot]) lim[i] = h.last_lim[slot];
-    bl[i] = st[i] >= 0 ? (held || owes) : w > 0;
+    if (st[i] >= 0) {
+      h.last_lim[slot] = lim[i];
+      h.last_state[slot] = st[i];
+      h.last_state_ns[slot] = now;
+    } else if (h.last_lim[slot]) {
+      lim[i] = h.last_lim[slot];
+    }
+    // backlogged: by its flags; by the last fresh ones within kStateGraceNs
+    // (measured: with eight tenants their samplers ran every ~5.5 ms, not 2,
+    // and a stall past the 20 ms freshness dropped a queued tenant out of the
+    // subscription half the time); without flags, waves resident
+    if (st[i] >= 0) bl[i] = held || owes;
+    else if (h.last_state_ns[slot] && now - h.last_state_ns[slot] < kStateGraceNs)
+      bl[i] = (h.last_state[slot] & (MIVGPU_FLAG_HELD | MIVGPU_FLAG_OWES)) != 0 || w > 0;
+    else bl[i] = w > 0;
     if (dt) {
       const double a = (double)dt / (double)kSubTauNs < 1.0 ? (double)dt / (double)kSubTauNs : 1.0;
       h.bl_ewma[slot] += a * ((bl[i] ? 1.0 : 0.0) - h.bl_ewma[slot]);

@@ -1811,6 +1811,7 @@ struct OccDev {
   uint64_t fair_samples = 0;   // samples in fair-share mode / held there on the lead
   uint64_t fair_held_samples = 0;
   int64_t last_lead_ns = -1;
+  double fair_recv_ns = 0;     // GPU time received since fair-share mode began
   std::vector<mivgpu_board::Reading> readings;
 };
 // Background stamper idle threshold and the batch bounds (see stamper_main
@@ -2138,12 +2139,21 @@ bool occ_sample(int dev, uint64_t now) {
     // carries nothing out of the mode: no debt, and no burst either (a 25 %
     // tenant left alone by a 75 % one that finished spent up to the whole
     // 100 ms burst it had banked while held on its lead: 27 % of the GPU).
+    // The lag grows with the GPU time received in the mode: 3 % of it, at
+    // least 10 ms.  The wave-share estimate is not exact per tenant (four
+    // symmetric 25 % tenants: one was held 120 ms of a 100-step run on it and
+    // came out slowest, fairness 0.93 where the hardware alone gave 0.995);
+    // unequal limits drift by far more than 3 % and are still held.
     double eff = o.tokens_ns;
     if (lead >= 0) {
       o.tokens_ns = 0;
-      eff = (double)kFairLagNs - (double)lead;
+      o.fair_recv_ns += share * run;
+      const double lag = 0.03 * o.fair_recv_ns > (double)kFairLagNs ? 0.03 * o.fair_recv_ns : (double)kFairLagNs;
+      eff = lag - (double)lead;
       ++o.fair_samples;
       if (eff < 0) ++o.fair_held_samples;
+    } else {
+      o.fair_recv_ns = 0;
     }
     o.last_lead_ns = lead;
     __atomic_store_n(reinterpret_cast<int64_t*>(const_cast<uint64_t*>(&hs[kHsHostTokens])), (int64_t)eff,
