@@ -1973,7 +1973,16 @@ bool occ_sample(int dev, uint64_t now) {
   const uint64_t window = g_cfg.peer_busy_ns ? g_cfg.peer_busy_ns : kPeerBusyNs;
   long others = 0;
   int busy_peers = 0;
+  // With a live board only its owner reads the peers: every cu_occupancy read
+  // walks the waves of all eight XCDs in the driver, and eight tenants each
+  // reading all nine processes every 2 ms stretched their sampler passes to
+  // ~5.5 ms (flags going stale, the subscription test failing half the time).
+  const bool read_peers = o.board.owner || !o.board_prev_ok;
   for (auto& p : o.peers) {
+    if (!read_peers) {
+      p.v = 0;
+      continue;
+    }
     int v = read_occ(p.fd);
     p.v = v > 0 ? v : 0;
     if (v > 0) others += v;
