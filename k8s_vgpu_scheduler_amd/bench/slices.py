@@ -68,9 +68,10 @@ def plan_slices(n: int, shim: bool, gpumem_mib: int | None, spatial: bool = True
 
     ``layout`` = what the scheduler's CU allocator hands out
     (device/amd/cu_alloc.py): ``disjoint`` = a range of its own per slice;
-    ``hybrid`` = slices below a quarter of the GPU share quarter-sized
-    ranges (as many as fit), split among them by the governor; ``auto`` =
-    the allocator's default (``cuShareSmall``, off: disjoint)."""
+    ``hybrid`` = slices below a quarter of the GPU share ranges of
+    ``share_unit`` CUs (as many as fit), split among them by the governor; ``auto`` =
+    the allocator's default (``cuShareSmall``, on: shared ranges of
+    ``cuShareUnit`` CUs, the whole GPU by default)."""
     specs = []
     per = (MI355X_CUS // n) // MI355X_XCDS * MI355X_XCDS   # whole 8-CU granules: XCD-balanced
     from k8s_vgpu_scheduler_amd.device.amd.cu_alloc import CUTopology

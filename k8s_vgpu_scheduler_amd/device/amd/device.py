@@ -82,16 +82,19 @@ class AMDConfig:
     # MI355X CU topology used by the CU-range allocator (measured, cu_alloc.py)
     xcds_per_device: int = 8
     cu_layout: str = "interleaved"
-    # True: requests below a quarter of the GPU share a quarter-sized CU
-    # range, time-sliced by the governor (cu_alloc.pick_shared).  Off by
-    # default, from measurement: 8 slices on one MI355X, disjoint 32-CU masks
-    # 8511 tok/s (fairness 0.99) vs shared quarters 8457-8461 and the
-    # temporal governor 8501 (profiles/README.md section 37)
-    cu_share_small: bool = False
+    # True: requests below a quarter of the GPU share a CU range of
+    # cuShareUnit CUs, time-sliced by the governor (cu_alloc.pick_shared); a
+    # small request that finds no shared range with room and no free range of
+    # that width takes a range of its own.  On by default with the whole GPU
+    # as the unit: small pods pool on GPUs of their own, quarter-or-larger pods
+    # keep disjoint ranges elsewhere.  Measured, 8 slices on one MI355X
+    # (profiles/README.md section 40): pooled 8891 tok/s vs native 8875
+    # (fairness 0.996) against disjoint 32-CU ranges 8502 (-4.5 %).
+    cu_share_small: bool = True
     # CUs of one shared range for cuShareSmall (0 = a quarter of the GPU; 256 =
     # every small request on the GPU shares one range, time-sliced by the
     # governor, while requests of a share unit or more keep ranges of their own)
-    cu_share_unit: int = 0
+    cu_share_unit: int = 256
     # False: no CU partitions at all -- a gpucores request is charged its
     # granules as before, but the container gets no HSA_CU_MASK and the shim's
     # temporal governor holds it to that charge (the reference's time-sharing
@@ -528,12 +531,15 @@ class AMDDevices(D.Devices):
             info = {}
             if 0 < cu < dev.totalcore and self.cfg.cu_partition:
                 # small = below a quarter of the GPU; the range it shares is
-                # cuShareUnit CUs wide (a quarter by default)
+                # cuShareUnit CUs wide (the whole GPU by default)
+                ranges = None
                 if self.cfg.cu_share_small and cu < cu_alloc.share_unit(topo) and topo.xcds > 1:
                     ranges = cu_alloc.pick_shared(dev.custominfo.get("cu_used", 0),
                                                   dev.custominfo.get("cu_shared", {}), cu, topo,
                                                   int(self.cfg.cu_share_unit or 0))
-                else:
+                if ranges is None:
+                    # no shared range with room and no free one that wide (a
+                    # GPU already partitioned among larger pods): its own range
                     ranges = cu_alloc.pick(dev.custominfo.get("cu_used", 0), cu, topo)
                 if ranges is None:
                     bump(R.CARD_CU_FRAGMENTED)

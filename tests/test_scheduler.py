@@ -303,11 +303,14 @@ def _ranges_of(cluster, name):
 
 @pytest.fixture
 def share_small():
-    """The hybrid layout (cuShareSmall, off by default) for one test."""
+    """The hybrid layout with quarter-sized shared ranges (cuShareSmall with
+    cuShareUnit 0; the default pools small pods into one whole-GPU range)."""
     from k8s_vgpu_scheduler_amd.device import devices as D
-    D.get_devices()["AMD"].cfg.cu_share_small = True
+    cfg = D.get_devices()["AMD"].cfg
+    old = (cfg.cu_share_small, cfg.cu_share_unit)
+    cfg.cu_share_small, cfg.cu_share_unit = True, 0
     yield
-    D.get_devices()["AMD"].cfg.cu_share_small = False
+    cfg.cu_share_small, cfg.cu_share_unit = old
 
 
 def test_small_slices_share_a_quarter_range(cluster, share_small):
@@ -390,11 +393,50 @@ def test_small_slices_pool_into_one_wide_range(cluster, share_small):
 
 
 def test_share_small_off_keeps_disjoint_ranges(cluster):
-    """The default: a sub-quarter request gets a disjoint range of its own."""
-    s = make_sched(cluster, [amd_node("n1", n=1)])
-    assert filt(s, cluster, amd_pod("p", mem=1024, cores=12), ["n1"])["NodeNames"] == ["n1"]
-    cus, ranges = _ranges_of(cluster, "p")
-    assert cus == 32 and codec.ranges_count(ranges) == 32
+    """cuShareSmall: false -- a sub-quarter request gets a disjoint range of its own."""
+    from k8s_vgpu_scheduler_amd.device import devices as D
+    cfg = D.get_devices()["AMD"].cfg
+    old = cfg.cu_share_small
+    cfg.cu_share_small = False
+    try:
+        s = make_sched(cluster, [amd_node("n1", n=1)])
+        assert filt(s, cluster, amd_pod("p", mem=1024, cores=12), ["n1"])["NodeNames"] == ["n1"]
+        cus, ranges = _ranges_of(cluster, "p")
+        assert cus == 32 and codec.ranges_count(ranges) == 32
+    finally:
+        cfg.cu_share_small = old
+
+
+def test_default_pools_small_pods_and_partitions_the_rest(cluster):
+    """The defaults (cuShareSmall, cuShareUnit 256): on an
+    empty GPU eight 12 % pods pool into one whole-GPU range; a quarter pod
+    goes to a GPU of its own with a disjoint 64-CU range; a small pod landing
+    on that partitioned GPU, where no whole-GPU range is free, still gets a
+    disjoint range of its own instead of failing."""
+    s = make_sched(cluster, [amd_node("n1", n=2)])
+    assert filt(s, cluster, amd_pod("q", mem=1024, cores=25), ["n1"])["NodeNames"] == ["n1"]
+    qdev = codec.decode_container_devices(
+        cluster.get_pod("default", "q")["metadata"]["annotations"][SUPPORT_ANNOS].split(";")[0])[0].uuid
+    qranges = codec.decode_cu_ranges(cluster.get_pod("default", "q")["metadata"]["annotations"][CU_RANGES_ANNOS])[0]
+    assert codec.ranges_count(qranges[qdev]) == 64
+    for i in range(8):
+        assert filt(s, cluster, amd_pod(f"p{i}", mem=1024, cores=12), ["n1"])["NodeNames"] == ["n1"], i
+    devs = {}
+    for i in range(8):
+        annos = cluster.get_pod("default", f"p{i}")["metadata"]["annotations"]
+        d = codec.decode_container_devices(annos[SUPPORT_ANNOS].split(";")[0])[0]
+        devs.setdefault(d.uuid, []).append(codec.ranges_count(codec.decode_cu_ranges(annos[CU_RANGES_ANNOS])[0][d.uuid]))
+    pooled = [u for u in devs if u != qdev]
+    assert pooled and all(n == 256 for u in pooled for n in devs[u]), devs
+    assert all(n == 32 for n in devs.get(qdev, [])), devs
+    # the pool is full (8 x 32 CUs): a ninth small pod lands on the quarter pod's GPU, on a range of its own
+    if sum(len(v) for u, v in devs.items() if u != qdev) == 8:
+        assert filt(s, cluster, amd_pod("p8", mem=1024, cores=12), ["n1"])["NodeNames"] == ["n1"]
+        annos = cluster.get_pod("default", "p8")["metadata"]["annotations"]
+        d = codec.decode_container_devices(annos[SUPPORT_ANNOS].split(";")[0])[0]
+        r = codec.decode_cu_ranges(annos[CU_RANGES_ANNOS])[0][d.uuid]
+        assert d.uuid == qdev and codec.ranges_count(r) == 32
+        assert cu_alloc.bitmap_from_ranges(r) & cu_alloc.bitmap_from_ranges(qranges[qdev]) == 0
 
 
 @pytest.fixture
