@@ -362,6 +362,7 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
   load_limits(h, now);
   constexpr int kMaxRead = 256;
   int st[kMaxRead], sl[kMaxRead];
+  bool hd[kMaxRead];
   uint32_t lim[kMaxRead];
   long wv[kMaxRead];
   double use[kMaxRead];
@@ -374,8 +375,13 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
     if (nl > 0 && nl < lim[i]) lim[i] = nl;
     const int v = r[i].v;
     bool held;
-    if (st[i] >= 0) held = (st[i] & MIVGPU_FLAG_HELD) != 0;
+    // HELD flags are up to one tenant pass old: a tenant already released
+    // (more than a gate's waves resident) runs.  Trusting the flag charged
+    // such tenants nothing while the owner's own flags, always fresh, charged
+    // it in full -- the owner came out slowest (held 0.8 s of a 2.9 s run).
+    if (st[i] >= 0) held = (st[i] & MIVGPU_FLAG_HELD) != 0 && v <= kGateUnits;
     else held = v > 0 && v <= kGateUnits;
+    hd[i] = held;
     wv[i] = (!held && v > 0) ? v : 0;
     if (st[i] >= 0 && (st[i] & MIVGPU_FLAG_OWES) && !held) ++owing;
     if (wv[i] > 0) {
@@ -422,7 +428,7 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
     mivgpu_board_slot_t& s = b->slots[slot];
     const int v = r[i].v;
     const long w = wv[i];
-    const bool held = st[i] >= 0 ? (st[i] & MIVGPU_FLAG_HELD) != 0 : (v > 0 && v <= kGateUnits);
+    const bool held = hd[i];
     const bool owes = st[i] >= 0 && (st[i] & MIVGPU_FLAG_OWES);
     s.occupancy = v;
     s.seen_ns = now;
@@ -478,7 +484,7 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
   if (backlogged >= 2 && sum_w >= 0.999) b->sub_passes += 1;
   const bool entering = !h.fair && h.sub_ewma >= kSubEnter;
   h.fair = h.fair ? h.sub_ewma >= kSubLeave : entering;
-  auto running = [&](int i) { return bl[i] && !(st[i] >= 0 && (st[i] & MIVGPU_FLAG_HELD)); };
+  auto running = [&](int i) { return bl[i] && !hd[i]; };
   if (h.fair) {
     if (entering) {
       // everyone starts level

@@ -191,7 +191,10 @@ case $suite in
     # the fair-share governor in the driver's own bench config (20 steps) and at 100 steps, 4 and 8 tenants
     step 300 t4_20 python -u bench.py --rounds temporal,native --steps 20 --warmup 5 --out "$out/t4_20.json"
     step 400 t4 python -u bench.py --rounds temporal,native --steps 100 --out "$out/t4.json"
-    step 400 t8 python -u bench.py --slices 8 --rounds temporal,native --steps 100 --out "$out/t8.json" ;;
+    step 400 t8 python -u bench.py --slices 8 --rounds temporal,native --steps 100 --out "$out/t8.json"
+    # 8 slices with the default layout (pooled whole-GPU range), driver-like 20 steps and 100
+    step 400 s8_20 python -u bench.py --slices 8 --rounds shim,native --steps 20 --warmup 5 --out "$out/s8_20.json"
+    step 400 s8 python -u bench.py --slices 8 --rounds shim,native --steps 100 --out "$out/s8.json" ;;
   eight)
     # 8 slices per GPU: disjoint 32-CU ranges vs the eight
     # pooled into one whole-GPU shared range (cuShareUnit 256) with and without
