@@ -23,6 +23,7 @@
 #   mixed       governed server + 3 governed decode tenants; 8 x 12 % temporal over 600 steps
 #   board       share board: 4 x 25 % / 8 x 12.5 % temporal vs native, unequal limits, time-sharing e2e
 #   fair        temporal (fair-share governor) vs native: 4 slices at 20 / 100 steps, 8 slices
+#   fair2       fair-share governor: 4 / 8 symmetric tenants, 75/25 and 50/25/25
 #   eight       8 slices: disjoint ranges vs one pooled whole-GPU range (cuShareUnit 256), monitor on/off
 #   kern        prefill kernels: flash attention A/B at 512 / 2048 / 8192, packed-weight GEMM vs hipBLASLt;
 #               decode K-split GEMM two vs four k-blocks per group
@@ -195,6 +196,14 @@ case $suite in
     # 8 slices with the default layout (pooled whole-GPU range), driver-like 20 steps and 100
     step 400 s8_20 python -u bench.py --slices 8 --rounds shim,native --steps 20 --warmup 5 --out "$out/s8_20.json"
     step 400 s8 python -u bench.py --slices 8 --rounds shim,native --steps 100 --out "$out/s8.json" ;;
+  fair2)
+    # the fair-share governor: 4 / 8 symmetric tenants at 100 steps, unequal limits (75/25, 50/25/25)
+    step 400 t4 python -u bench.py --rounds temporal,native --steps 100 --out "$out/t4.json"
+    step 400 t8 python -u bench.py --slices 8 --rounds temporal,native --steps 100 --out "$out/t8.json"
+    step 400 u75 python -u bench.py --slices 2 --no-spatial --mode shim --policy force --slice-limits 75,25 \
+      --steps 300 --warmup 5 --out "$out/u75_25.json"
+    step 400 u50 python -u bench.py --slices 3 --no-spatial --mode shim --policy force --slice-limits 50,25,25 \
+      --steps 300 --warmup 5 --out "$out/u50_25_25.json" ;;
   eight)
     # 8 slices per GPU: disjoint 32-CU ranges vs the eight
     # pooled into one whole-GPU shared range (cuShareUnit 256) with and without

@@ -343,3 +343,13 @@ def test_node_written_limits_cap_what_a_tenant_publishes(native_build, tmp_path)
     B.limits_path(str(d), 4242).unlink()
     s = _fair_run(native_build, tmp_path / "nofile", {111: (10, B.FLAG_OWES, 750000), 222: (10, B.FLAG_OWES, 0)})
     assert s[222].lead_ns == 0 and s[111].lead_ns > 0, (s[111].lead_ns, s[222].lead_ns)
+
+
+def test_fair_share_counts_presence_not_wave_shape(native_build, tmp_path):
+    """Two equal-weight tenants with different kernel shapes (40 vs 10 CU
+    units resident) both run all the time: the fair-share virtual time counts
+    presence, so neither leads (the wave ratio, which the buckets charge,
+    would have held the wider one on the shape of its kernels)."""
+    s = _fair_run(native_build, tmp_path, {111: (40, B.FLAG_OWES, 500000), 222: (10, B.FLAG_OWES, 500000)})
+    assert s[111].lead_ns == 0 and s[222].lead_ns == 0, (s[111].lead_ns, s[222].lead_ns)
+    assert s[111].frac_ns > 3 * s[222].frac_ns       # the charge still follows the waves
