@@ -114,6 +114,9 @@ def main():
                     help="run the node monitor's feedback pass (priority + utilization_switch) over the shim "
                          "rounds' regions every SECONDS while they run (0 = off)")
     ap.add_argument("--policy", default="default", choices=["default", "force", "disable"])
+    ap.add_argument("--board", default="node", choices=["node", "shim"],
+                    help="owner of the GPU's share board in the shim rounds: the node sampler (mivgpu-boardd, "
+                         "as the monitor runs it) or a governed slice's shim")
     ap.add_argument("--slice-limits", default="",
                     help="comma list of per-slice core limits (%%) for the shim and temporal rounds, e.g. 75,25 "
                          "(unequal tenants; default 100/N each)")
@@ -294,7 +297,18 @@ def main():
         if args.monitor > 0 and name in ("shim", "temporal"):
             from k8s_vgpu_scheduler_amd.bench.slices import RoundMonitor
             mon = RoundMonitor([p.cache for p in procs], args.monitor).start()
-        r = run_round(procs, barrier=barrier, sync=sync)
+        # the GPU's share board owned by the node sampler, as the monitor runs
+        # it in production (--board shim: a governed slice takes the role)
+        boardd = None
+        bdir = next((p.board_dir for p in procs if getattr(p, "board_dir", None)), None)
+        if args.board == "node" and bdir and not cpu:
+            from k8s_vgpu_scheduler_amd.monitor.board import BoardSampler
+            boardd = BoardSampler(bdir).start()
+        try:
+            r = run_round(procs, barrier=barrier, sync=sync)
+        finally:
+            if boardd is not None:
+                boardd.stop()
         r["specs"] = [p.spec for p in procs]
         if mon is not None:
             r["monitor"] = mon.stop()

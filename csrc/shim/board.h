@@ -367,7 +367,7 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
   long wv[kMaxRead];
   double use[kMaxRead];
   long W = 0;
-  int resident = 0, owing = 0;
+  int resident = 0, owing = 0, present = 0;
   if (n > kMaxRead) n = kMaxRead;
   for (int i = 0; i < n; ++i) {
     st[i] = read_flags(h.flags, r[i].pid, now, &lim[i]);
@@ -388,6 +388,7 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
       W += wv[i];
       ++resident;
     }
+    if (wv[i] > kGateUnits) ++present;   // more than a gate's (or a stale HELD flag's) one CU unit
   }
   const uint64_t s0 = __atomic_load_n(&b->seq, __ATOMIC_RELAXED);
   __atomic_store_n(&b->seq, s0 | 1ull, __ATOMIC_RELAXED);
@@ -468,7 +469,7 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
       // ratio charged below scatters with each kernel's shape: eight
       // identical decode tenants came out 0.87 apart in throughput after
       // being held on it, where the hardware alone gives 0.996.
-      use[i] = w > 0 ? 1.0 / (double)resident : 0.0;
+      use[i] = w > kGateUnits ? 1.0 / (double)present : 0.0;
     } else {
       got = 0.0;
       f = st[i] < 0 ? 1.0 : (owes && owing > 0 ? 1.0 / (double)owing : 1.0);

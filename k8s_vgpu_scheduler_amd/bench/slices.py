@@ -192,6 +192,7 @@ class SliceProc:
             full.pop("CUDA_VISIBLE_DEVICES", None)
         self.spec = spec
         self.cache = env.get("MIVGPU_SHARED_CACHE")
+        self.board_dir = env.get("MIVGPU_BOARD_DIR")
         self.log = open(log_path, "w")
         self.p = subprocess.Popen(
             [sys.executable, "-m", "k8s_vgpu_scheduler_amd.bench.slices", "--child", *args],
