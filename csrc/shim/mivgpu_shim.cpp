@@ -489,6 +489,7 @@ struct Config {
   uint64_t gate_min_interval_ns = 200000;  // >= 200 us of host submission per gate
   bool gate_trace = false;                 // gates also write their trace ring (mivgpu_gate_trace)
   int64_t gate_cap_ns = 100000000;         // 100 ms burst (absorbs share-measurement noise)
+  double fair_lag_frac = 0.03;             // fair-share lag: this part of the GPU time received in the mode
   int64_t gate_max_hold_ns = 25000000;     // 25 ms per gate, bounds every spin (larger debts: later gates)
   char cache_path[512] = {0};
 };
@@ -629,7 +630,8 @@ bool is_grant_key(const char* key) {
                                       "MIVGPU_ACCOUNT_CONTEXT", "ROCR_VISIBLE_DEVICES", "MIVGPU_KFD_SYSFS",
                                       "MIVGPU_OCCUPANCY", "MIVGPU_OCC_PERIOD_US", "MIVGPU_GATE_INTERVAL_US",
                                       "MIVGPU_GATE_BURST_US", "MIVGPU_SHARE_TAU_MS", "GPU_MAX_HW_QUEUES",
-                                      "MIVGPU_GATE_MAX_HOLD_US", "MIVGPU_CONTROL_FILE", "MIVGPU_BOARD_DIR"};
+                                      "MIVGPU_GATE_MAX_HOLD_US", "MIVGPU_CONTROL_FILE", "MIVGPU_BOARD_DIR",
+                                      "MIVGPU_FAIR_LAG_PCT"};
   for (const char* k : kKeys)
     if (!strcmp(key, k)) return true;
   return !strncmp(key, "HIP_DEVICE_MEMORY_LIMIT_", 24) || !strncmp(key, "HIP_DEVICE_CORE_LIMIT_", 22);
@@ -718,6 +720,9 @@ void load_config() {
   g_cfg.board_split = bs && !strcmp(bs, "equal") ? mivgpu_board::kSplitEqual : mivgpu_board::kSplitRatio;
   const char* gt = getenv("MIVGPU_GATE_TRACE");
   g_cfg.gate_trace = gt && (!strcmp(gt, "1") || !strcasecmp(gt, "true"));
+  // fair-share lag: percent of the GPU time received in the mode (grant key)
+  const char* fl = grant_env("MIVGPU_FAIR_LAG_PCT");
+  if (fl && atof(fl) >= 0 && atof(fl) <= 50) g_cfg.fair_lag_frac = atof(fl) / 100.0;
   const char* gi = grant_env("MIVGPU_GATE_INTERVAL_US");
   if (gi) g_cfg.gate_min_interval_ns = (uint64_t)atoll(gi) * 1000ull;
   const char* cap = grant_env("MIVGPU_GATE_BURST_US");
@@ -2157,7 +2162,8 @@ bool occ_sample(int dev, uint64_t now) {
     if (lead >= 0) {
       o.tokens_ns = 0;
       o.fair_recv_ns += share * run;
-      const double lag = 0.03 * o.fair_recv_ns > (double)kFairLagNs ? 0.03 * o.fair_recv_ns : (double)kFairLagNs;
+      const double rel = g_cfg.fair_lag_frac * o.fair_recv_ns;
+      const double lag = rel > (double)kFairLagNs ? rel : (double)kFairLagNs;
       eff = lag - (double)lead;
       ++o.fair_samples;
       if (eff < 0) ++o.fair_held_samples;

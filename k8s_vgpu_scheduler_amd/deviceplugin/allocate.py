@@ -60,7 +60,7 @@ GRANT_KEYS = ("HIP_DEVICE_MEMORY_LIMIT", "HIP_DEVICE_CORE_LIMIT", "HSA_CU_MASK",
               "ROCR_VISIBLE_DEVICES", "MIVGPU_ACCOUNT_CONTEXT", "MIVGPU_KFD_SYSFS", "MIVGPU_OCCUPANCY",
               "MIVGPU_OCC_PERIOD_US", "MIVGPU_GATE_INTERVAL_US", "MIVGPU_GATE_BURST_US", "MIVGPU_SHARE_TAU_MS",
               "MIVGPU_DISABLE_CONTROL", "GPU_MAX_HW_QUEUES", "MIVGPU_GATE_MAX_HOLD_US", "MIVGPU_CONTROL_FILE",
-              "MIVGPU_BOARD_DIR")
+              "MIVGPU_BOARD_DIR", "MIVGPU_FAIR_LAG_PCT")
 # per-device forms of grant keys (HIP_DEVICE_MEMORY_LIMIT_<i>, HIP_DEVICE_CORE_LIMIT_<i>)
 GRANT_PREFIXES = ("HIP_DEVICE_MEMORY_LIMIT_", "HIP_DEVICE_CORE_LIMIT_")
 
