@@ -26,6 +26,7 @@
 // 4 n-tiles are 2 whole pairs) -> Y[M][N/2].
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace {
 
@@ -165,6 +166,157 @@ prefill_gemm_kernel(const uint4* __restrict__ wp, const bf16_t* __restrict__ x, 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Version 2 (MIVGPU_PREFILL_GEMM=native, the default variant): the same tile,
+// waves and epilogues, staged by LDS-DMA in a four-deep ring of 32-wide
+// k-slices.  Version 1 staged 64-wide k-blocks through registers with one
+// k-block in flight: the next block's loads had ~1 k-block of MFMAs (about
+// the L2/MALL latency under load) to land, and the kernel ran at 39 % of the
+// MFMA peak (984 TFLOP/s, qkv at 8192 rows).  Here every wave issues four
+// 16-byte global_load_lds per slice (two X, two W: 1 KB each, lane-linear in
+// LDS), three slices ahead; a slice is retired by the wave's own counted
+// s_waitcnt vmcnt (never 0 in the loop) and one raw s_barrier, after which
+// the ring slot read one slice earlier is refilled.  All LDS is one array (a
+// second __shared__ object makes hipcc wait vmcnt(0) before every ds_read).
+//   X slice (kb, half hs): per row the 16-byte chunks {2hs, 2hs+1, 4+2hs,
+//     5+2hs} of the 64-wide k-block -- MFMA step jj in {0,1} of the slice
+//     reads chunk jj + 2h, the same k-permutation as the packed W -- 64 B per
+//     row, chunk cc stored at slot cc ^ ((row >> 2) & 3): a ds_read_b128
+//     group of 16 rows covers all 16 slots of a 256-B bank row; the DMA's
+//     per-lane SOURCE address realises the swizzle.
+//   W slice: for each of the 8 n-tiles the packed chunks j = 2hs, 2hs+1 (2 x
+//     1 KB, already in fragment order).
+constexpr int PG2_STAGES = 4;
+constexpr int PG2_SLICE_U4 = 2048;                    // uint4 per slice: X 1024 + W 1024 (32 KB)
+
+template <int EPI>
+__global__ void __launch_bounds__(PG_THREADS, 2)
+prefill_gemm2_kernel(const uint4* __restrict__ wp, const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int M,
+                     int K, int N, int ldx, int ldy) {
+  __shared__ __attribute__((aligned(16))) uint4 ring[PG2_STAGES * PG2_SLICE_U4];
+
+  const int nM = (M + PG_BM - 1) / PG_BM, nN = N / PG_BN;
+  const int nb = nM * nN;
+  const int b = blockIdx.x;
+  // XCD-grouped order, bijective for any grid (blocks b, b+8, ... share an XCD)
+  const int q = nb / 8, rr = nb % 8, xcd = b & 7;
+  const int u = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
+  const int group = u / (PG_GM * nN), within = u % (PG_GM * nN);
+  const int gm = min(PG_GM, nM - group * PG_GM);
+  const int mb = group * PG_GM + within % gm, nbk = within / gm;
+  const int m0 = mb * PG_BM, t0 = nbk * PG_NT;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w & 3, wn = w >> 2;
+  const int r = lane & 31, h = lane >> 5;
+  const int KB = K >> 6;
+  const int S = 2 * KB;                                 // 32-wide k-slices
+
+  // this lane's DMA sources: X rows 32w + 16i + lane/4 (i = 0, 1), slot lane%4
+  const int xs_row0 = 32 * w + (lane >> 2);
+  const int xcc = (lane & 3) ^ ((lane >> 4) & 3);      // in-slice chunk of the slot (row>>2 & 3 = lane>>4 & 3)
+  const int xg = (xcc & 1) + 4 * (xcc >> 1);           // + 2hs: chunk of the 64-wide k-block
+  const bf16_t* xsrc0 = x + (size_t)min(m0 + xs_row0, M - 1) * ldx + xg * 8;
+  const bf16_t* xsrc1 = x + (size_t)min(m0 + xs_row0 + 16, M - 1) * ldx + xg * 8;
+  // W: this wave's n-tile w, both halves of the slice
+  const uint4* wsrc = wp + ((size_t)(t0 + w) * KB) * 256 + lane;
+
+  auto issue = [&](int sl) {
+    const int kb = sl >> 1, hs = sl & 1;
+    uint4* dst = ring + (sl & (PG2_STAGES - 1)) * PG2_SLICE_U4;
+    // X: rows 32w .. 32w + 31 (two 16-row DMAs), W: tile w, j = 2hs, 2hs + 1
+    __builtin_amdgcn_global_load_lds(xsrc0 + kb * 64 + hs * 16, dst + (32 * w) * 4, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(xsrc1 + kb * 64 + hs * 16, dst + (32 * w + 16) * 4, 16, 0, 0);
+    const uint4* ws = wsrc + (kb * 4 + 2 * hs) * 64;
+    __builtin_amdgcn_global_load_lds(ws, dst + 1024 + (2 * w) * 64, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(ws + 64, dst + 1024 + (2 * w + 1) * 64, 16, 0, 0);
+  };
+
+  f32x16_t acc[2][4];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[mt][i][e] = 0.f;
+
+  // A-fragment LDS slots of this lane (uint4 index within a slice): row
+  // wm*64 + mt*32 + r, in-slice chunk jj + 2h, swizzled by (row >> 2) & 3
+  int aidx[2][2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int row = wm * 64 + mt * 32 + r;
+      aidx[mt][jj] = row * 4 + ((jj + 2 * h) ^ ((row >> 2) & 3));
+    }
+
+  issue(0);
+  if (S > 1) issue(1);
+  if (S > 2) issue(2);
+  for (int sl = 0; sl < S; ++sl) {
+    // retire slice sl: this wave's loads of the (up to) two later slices stay in flight
+    const int ahead = S - 1 - sl;
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // every wave is past its reads of slice sl - 1: refill that slot
+    if (sl + 3 < S) issue(sl + 3);
+    const uint4* cur = ring + (sl & (PG2_STAGES - 1)) * PG2_SLICE_U4;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      bf16x8_t af[2], bfr[4];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) af[mt] = __builtin_bit_cast(bf16x8_t, cur[aidx[mt][jj]]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bfr[i] = __builtin_bit_cast(bf16x8_t, cur[1024 + ((wn * 4 + i) * 2 + jj) * 64 + lane]);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[mt][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mt], bfr[i], acc[mt][i], 0, 0, 0);
+    }
+  }
+
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int rbase = m0 + wm * 64 + mt * 32 + 4 * h;
+    if constexpr (EPI == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int col = (t0 + wn * 4 + i) * 32 + r;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = rbase + (e & 3) + 8 * (e >> 2);
+          if (row < M) y[(size_t)row * ldy + col] = f2bf(acc[mt][i][e]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int c = (t0 + wn * 4) / 2 + p;
+        const int col = c * 32 + r;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = rbase + (e & 3) + 8 * (e >> 2);
+          const float g = acc[mt][2 * p][e], up = acc[mt][2 * p + 1][e];
+          if (row < M) y[(size_t)row * ldy + col] = f2bf(g / (1.f + __expf(-g)) * up);
+        }
+      }
+    }
+  }
+}
+
+int prefill_gemm_version() {
+  static const int v = [] {
+    const char* e = getenv("MIVGPU_PREFILL_GEMM_V");
+    return e && atoi(e) == 1 ? 1 : 2;
+  }();
+  return v;
+}
+
 }  // namespace
 
 extern "C" {
@@ -178,6 +330,15 @@ int mivgpu_prefill_gemm(const void* wp, const void* x, void* y, int M, int K, in
     return (int)hipErrorInvalidValue;
   if (ldy < (epi ? N / 2 : N)) return (int)hipErrorInvalidValue;
   const int blocks = ((M + PG_BM - 1) / PG_BM) * (N / PG_BN);
+  if (prefill_gemm_version() == 2) {
+    if (epi == 0)
+      hipLaunchKernelGGL(prefill_gemm2_kernel<0>, dim3(blocks), dim3(PG_THREADS), 0, s, (const uint4*)wp,
+                         (const bf16_t*)x, (bf16_t*)y, M, K, N, ldx, ldy);
+    else
+      hipLaunchKernelGGL(prefill_gemm2_kernel<1>, dim3(blocks), dim3(PG_THREADS), 0, s, (const uint4*)wp,
+                         (const bf16_t*)x, (bf16_t*)y, M, K, N, ldx, ldy);
+    return (int)hipGetLastError();
+  }
   if (epi == 0)
     hipLaunchKernelGGL(prefill_gemm_kernel<0>, dim3(blocks), dim3(PG_THREADS), 0, s, (const uint4*)wp,
                        (const bf16_t*)x, (bf16_t*)y, M, K, N, ldx, ldy);

@@ -508,8 +508,12 @@ SS_ROWS = 128   # rows per sum-of-squares slot (csrc/ops/skinny_gemm.hip SS_ROWS
 
 def prefill_gemm_ok(N: int, K: int) -> bool:
     """The native prefill GEMM takes this weight (tile-major packing, N a
-    multiple of 256, K of 64) and is not switched off (MIVGPU_PREFILL_GEMM=lib)."""
-    return (os.environ.get("MIVGPU_PREFILL_GEMM", "native") != "lib" and N % 256 == 0 and K % 64 == 0
+    multiple of 256, K of 64) and is selected (MIVGPU_PREFILL_GEMM=native).
+    The default is the library path: measured on MI355X
+    (profiles/round5/kern/pgemm.json) the register-staged 256x256 kernel ran
+    984 TFLOP/s on the 8192-row qkv against hipBLASLt's 1505 (unpack + GEMM
+    291 vs 419 us), and the 8k-token prefill took 127.4 vs 120.7 ms."""
+    return (os.environ.get("MIVGPU_PREFILL_GEMM", "lib") == "native" and N % 256 == 0 and K % 64 == 0
             and os.environ.get("MIVGPU_SKINNY_KMAJOR", "0") in ("", "0", "-1"))
 
 

@@ -25,8 +25,8 @@
 #   fair        temporal (fair-share governor) vs native: 4 slices at 20 / 100 steps, 8 slices
 #   fair2       fair-share governor: 4 / 8 symmetric tenants, 75/25 and 50/25/25
 #   eight       8 slices: disjoint ranges vs one pooled whole-GPU range (cuShareUnit 256), monitor on/off
-#   kern        prefill kernels: flash attention A/B at 512 / 2048 / 8192, packed-weight GEMM vs hipBLASLt;
-#               decode K-split GEMM two vs four k-blocks per group
+#   kern        prefill kernels: flash attention at 512 / 2048 / 8192, packed-weight GEMM v2 / v1 vs hipBLASLt,
+#               8k-token TTFT (library and native GEMM)
 #   prefill     prefill microbench + rocprofv3 kernel summary, whole GPU and 64 CUs
 # Results go to gpurun_out/<suite>/ (copy the ones to keep into profiles/).
 set -o pipefail
@@ -218,29 +218,19 @@ case $suite in
       --steps 20 --warmup 5 --out "$out/h256_20.json" ;;
   kern)
     # prefill kernels: flash attention (eight-wave vs 32-key-tile kernel) and
-    # the packed-weight GEMM (vs unpack + hipBLASLt), numerics then timing
+    # the packed-weight GEMM (LDS-DMA ring v2 vs register-staged v1 vs unpack +
+    # hipBLASLt), numerics then timing, then the 8k-token TTFT
     step 300 tests python -u -m pytest tests/test_ops_gpu.py -v --timeout 120 --timeout-method thread \
       -k "prefill_flash or tr_read or prefill_gemm"
     step 200 fa8 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention --lens 512,2048,8192 --eager-max 0 \
       --out "$out/fa8.json"
-    MIVGPU_FA_KERNEL=4 step 200 fa4 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_attention --lens 512,2048,8192 \
-      --eager-max 0 --out "$out/fa4.json"
     step 300 pgemm python -u -m k8s_vgpu_scheduler_amd.bench.prefill_gemm --rows 2048,8192 --out "$out/pgemm.json"
-    # 8k-token TTFT (<= 120 ms), whole GPU and a 50 % (128-CU) slice, packed GEMM vs library
+    MIVGPU_PREFILL_GEMM_V=1 step 300 pgemm_v1 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_gemm --rows 8192 \
+      --out "$out/pgemm_v1.json"
+    # 8k-token TTFT (<= 120 ms): library GEMM path (default) and the native GEMM
     step 300 ttft8k python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 --ctx 9216 --iters 5
-    HSA_CU_MASK=0:0-127 step 300 ttft8k_cu128 python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 \
-      --ctx 9216 --iters 5
-    MIVGPU_PREFILL_GEMM=lib step 300 ttft8k_lib python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 \
-      --ctx 9216 --iters 5
-    # decode K-split GEMM: two vs four k-blocks per wave per group (MIVGPU_WIDEK_U)
-    MIVGPU_WIDEK_U=4 step 300 widek_u4_tests python -u -m pytest tests/test_ops_gpu.py -v --timeout 120 \
-      --timeout-method thread -k "widek"
-    for u in 2 4; do
-      MIVGPU_WIDEK_U=$u step 300 "gemm_u$u" python -u -m k8s_vgpu_scheduler_amd.bench.gemm --shapes qkv,o_proj,down \
-        --batches 1,32 --out "$out/gemm_u$u.json"
-      MIVGPU_WIDEK_U=$u step 300 "dec_u$u" python -u -m k8s_vgpu_scheduler_amd.bench.decode --steps 200
-      MIVGPU_WIDEK_U=$u step 300 "dec_b1_u$u" python -u -m k8s_vgpu_scheduler_amd.bench.decode --batch 1 --steps 200
-    done ;;
+    MIVGPU_PREFILL_GEMM=native step 300 ttft8k_native python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 \
+      --ctx 9216 --iters 5 ;;
   prefill)
     step 120 native python3 -m k8s_vgpu_scheduler_amd.bench.prefill
     HSA_CU_MASK=0:0-63 step 120 cu64 python3 -m k8s_vgpu_scheduler_amd.bench.prefill
