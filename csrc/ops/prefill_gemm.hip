@@ -189,11 +189,12 @@ prefill_gemm_kernel(const uint4* __restrict__ wp, const bf16_t* __restrict__ x, 
 constexpr int PG2_STAGES = 4;
 constexpr int PG2_SLICE_U4 = 2048;                    // uint4 per slice: X 1024 + W 1024 (32 KB)
 
-template <int EPI>
+template <int EPI, int ST = PG2_STAGES, bool PRIO = false>
 __global__ void __launch_bounds__(PG_THREADS, 2)
 prefill_gemm2_kernel(const uint4* __restrict__ wp, const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int M,
                      int K, int N, int ldx, int ldy) {
-  __shared__ __attribute__((aligned(16))) uint4 ring[PG2_STAGES * PG2_SLICE_U4];
+  static_assert(ST == 4 || ST == 5, "ring of 4 (128 KB) or 5 (160 KB) slices");
+  __shared__ __attribute__((aligned(16))) uint4 ring[ST * PG2_SLICE_U4];
 
   const int nM = (M + PG_BM - 1) / PG_BM, nN = N / PG_BN;
   const int nb = nM * nN;
@@ -224,7 +225,7 @@ prefill_gemm2_kernel(const uint4* __restrict__ wp, const bf16_t* __restrict__ x,
 
   auto issue = [&](int sl) {
     const int kb = sl >> 1, hs = sl & 1;
-    uint4* dst = ring + (sl & (PG2_STAGES - 1)) * PG2_SLICE_U4;
+    uint4* dst = ring + (sl % ST) * PG2_SLICE_U4;
     // X: rows 32w .. 32w + 31 (two 16-row DMAs), W: tile w, j = 2hs, 2hs + 1
     __builtin_amdgcn_global_load_lds(xsrc0 + kb * 64 + hs * 16, dst + (32 * w) * 4, 16, 0, 0);
     __builtin_amdgcn_global_load_lds(xsrc1 + kb * 64 + hs * 16, dst + (32 * w + 16) * 4, 16, 0, 0);
@@ -252,19 +253,20 @@ prefill_gemm2_kernel(const uint4* __restrict__ wp, const bf16_t* __restrict__ x,
       aidx[mt][jj] = row * 4 + ((jj + 2 * h) ^ ((row >> 2) & 3));
     }
 
-  issue(0);
-  if (S > 1) issue(1);
-  if (S > 2) issue(2);
+  for (int p = 0; p < ST - 1; ++p)
+    if (p < S) issue(p);
   for (int sl = 0; sl < S; ++sl) {
-    // retire slice sl: this wave's loads of the (up to) two later slices stay in flight
-    const int ahead = S - 1 - sl;
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    // retire slice sl: this wave's loads of the (up to) ST - 2 later slices stay in flight
+    const int ahead = min(ST - 2, S - 1 - sl);
+    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     // every wave is past its reads of slice sl - 1: refill that slot
-    if (sl + 3 < S) issue(sl + 3);
-    const uint4* cur = ring + (sl & (PG2_STAGES - 1)) * PG2_SLICE_U4;
+    if (sl + ST - 1 < S) issue(sl + ST - 1);
+    const uint4* cur = ring + (sl % ST) * PG2_SLICE_U4;
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
       bf16x8_t af[2], bfr[4];
@@ -278,6 +280,7 @@ prefill_gemm2_kernel(const uint4* __restrict__ wp, const bf16_t* __restrict__ x,
         for (int i = 0; i < 4; ++i)
           acc[mt][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mt], bfr[i], acc[mt][i], 0, 0, 0);
     }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   }
 
 #pragma unroll
@@ -309,6 +312,39 @@ prefill_gemm2_kernel(const uint4* __restrict__ wp, const bf16_t* __restrict__ x,
   }
 }
 
+// v2 build (A/B): MIVGPU_PREFILL_GEMM_ST = 4 or 5 ring slices,
+// MIVGPU_PREFILL_GEMM_PRIO = 1 raises the wave priority over its MFMAs
+int prefill_gemm2_cfg() {
+  static const int c = [] {
+    const char* st = getenv("MIVGPU_PREFILL_GEMM_ST");
+    const char* pr = getenv("MIVGPU_PREFILL_GEMM_PRIO");
+    return (st && atoi(st) == 5 ? 1 : 0) | (pr && atoi(pr) == 1 ? 2 : 0);
+  }();
+  return c;
+}
+
+template <int EPI>
+void launch_gemm2(int blocks, hipStream_t s, const uint4* wp, const bf16_t* x, bf16_t* y, int M, int K, int N, int ldx,
+                  int ldy) {
+  switch (prefill_gemm2_cfg()) {
+    case 1:
+      hipLaunchKernelGGL((prefill_gemm2_kernel<EPI, 5, false>), dim3(blocks), dim3(PG_THREADS), 0, s, wp, x, y, M, K, N,
+                         ldx, ldy);
+      break;
+    case 2:
+      hipLaunchKernelGGL((prefill_gemm2_kernel<EPI, 4, true>), dim3(blocks), dim3(PG_THREADS), 0, s, wp, x, y, M, K, N,
+                         ldx, ldy);
+      break;
+    case 3:
+      hipLaunchKernelGGL((prefill_gemm2_kernel<EPI, 5, true>), dim3(blocks), dim3(PG_THREADS), 0, s, wp, x, y, M, K, N,
+                         ldx, ldy);
+      break;
+    default:
+      hipLaunchKernelGGL((prefill_gemm2_kernel<EPI, 4, false>), dim3(blocks), dim3(PG_THREADS), 0, s, wp, x, y, M, K,
+                         N, ldx, ldy);
+  }
+}
+
 int prefill_gemm_version() {
   static const int v = [] {
     const char* e = getenv("MIVGPU_PREFILL_GEMM_V");
@@ -332,11 +368,9 @@ int mivgpu_prefill_gemm(const void* wp, const void* x, void* y, int M, int K, in
   const int blocks = ((M + PG_BM - 1) / PG_BM) * (N / PG_BN);
   if (prefill_gemm_version() == 2) {
     if (epi == 0)
-      hipLaunchKernelGGL(prefill_gemm2_kernel<0>, dim3(blocks), dim3(PG_THREADS), 0, s, (const uint4*)wp,
-                         (const bf16_t*)x, (bf16_t*)y, M, K, N, ldx, ldy);
+      launch_gemm2<0>(blocks, s, (const uint4*)wp, (const bf16_t*)x, (bf16_t*)y, M, K, N, ldx, ldy);
     else
-      hipLaunchKernelGGL(prefill_gemm2_kernel<1>, dim3(blocks), dim3(PG_THREADS), 0, s, (const uint4*)wp,
-                         (const bf16_t*)x, (bf16_t*)y, M, K, N, ldx, ldy);
+      launch_gemm2<1>(blocks, s, (const uint4*)wp, (const bf16_t*)x, (bf16_t*)y, M, K, N, ldx, ldy);
     return (int)hipGetLastError();
   }
   if (epi == 0)

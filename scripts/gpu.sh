@@ -231,6 +231,14 @@ case $suite in
     step 300 ttft8k python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 --ctx 9216 --iters 5
     MIVGPU_PREFILL_GEMM=native step 300 ttft8k_native python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 \
       --ctx 9216 --iters 5 ;;
+  pg2)
+    # prefill GEMM v2 ring depth (4 / 5 slices) x wave priority over the MFMAs: numerics, then 8192 rows
+    MIVGPU_PREFILL_GEMM_ST=5 MIVGPU_PREFILL_GEMM_PRIO=1 step 300 tests python -u -m pytest tests/test_ops_gpu.py -v \
+      --timeout 120 --timeout-method thread -k "prefill_gemm"
+    for st in 4 5; do for pr in 0 1; do
+      MIVGPU_PREFILL_GEMM_ST=$st MIVGPU_PREFILL_GEMM_PRIO=$pr step 300 "pg_st${st}_p${pr}" python -u -m \
+        k8s_vgpu_scheduler_amd.bench.prefill_gemm --rows 8192 --out "$out/pg_st${st}_p${pr}.json"
+    done; done ;;
   prefill)
     step 120 native python3 -m k8s_vgpu_scheduler_amd.bench.prefill
     HSA_CU_MASK=0:0-63 step 120 cu64 python3 -m k8s_vgpu_scheduler_amd.bench.prefill
