@@ -387,9 +387,10 @@ def main():
                                                             "share_pct", "util_pct", "busy_share_pct",
                                                             "seconds", "sampler", "timed", "gov_sampler_pass_us_mean",
                                                             "gov_sampler_pass_us_max")} for d in head["done"]]
+        if "native" in results:
+            out["native_value"] = round(results["native"]["tok_s"], 2)
         if "native" in results and "shim" in results:
             nat = results["native"]["tok_s"]
-            out["native_value"] = round(nat, 2)
             out["isolation_overhead_pct"] = round((1.0 - head["tok_s"] / nat) * 100.0, 2)
             nd = results["native"]["done"]
             out["native_tpot_ms_p50_rank0"] = [round(d.get("tpot_ms_p50", 0), 3) for d in nd]
