@@ -12,7 +12,12 @@ NeoX RoPE theta 1e6, SwiGLU 12288, vocab 151936) whose decode step runs
     sharing an LDS X tile) for gate_up / down / lm_head, the K-split variant
     (skinny_widek_kernel) for qkv and o_proj (the kernel trace,
     profiles/round4/bench/decode_trace_b32.json);
-  * the prompt (prefill) projections on hipBLASLt (``F.linear``);
+  * the prompt (prefill) projections: up to 1023 rows in 128-row chunks on
+    the skinny kernels, longer prompts on the packed weight unpacked once
+    into a shared scratch and hipBLASLt (PackedLinear.prompt; the hand-written
+    packed-weight GEMM, csrc/ops/prefill_gemm.hip, with
+    MIVGPU_PREFILL_GEMM=native), the causal attention on the flash kernel
+    (csrc/ops/prefill_attn.hip);
   * every other op on the hand-written gfx950 kernels of libmivgpu_ops.so,
   * the whole step captured in one hipGraph (launch overhead -> one replay).
 No network: weights are random normal(0, 0.02) of the exact architecture.
