@@ -312,6 +312,197 @@ prefill_gemm2_kernel(const uint4* __restrict__ wp, const bf16_t* __restrict__ x,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Version 3: v2's ring with the two wave groups in ping-pong.  v2 ran 16
+// MFMAs per wave between barriers and every wave issued its fragment reads
+// right after the barrier: both waves of a SIMD waited on LDS at once (the
+// ring depth and wave priority did not move it, profiles §40).  Here group 0
+// (waves 0-3, n-columns 0-127) and group 1 (waves 4-7, 128-255) -- one wave of
+// each per SIMD -- alternate: two barriers per slice, and between them one
+// group's wave runs its 16 MFMAs (raised priority) while the other's reads
+// the fragments it multiplies next.
+//   phase A_s: group 0 MFMAs on slice s (fragments read in B_{s-1}),
+//              group 1 reads slice s;
+//   phase B_s: group 1 MFMAs on slice s, group 0 reads slice s + 1.
+// Every wave retires its own DMA of slice s + 1 (counted vmcnt) before B_s,
+// so slice s + 1 is complete for both readers after that barrier; the slot
+// of slice s - 1 is refilled after A_s, when both groups are past it.
+template <int EPI>
+__global__ void __launch_bounds__(PG_THREADS, 2)
+prefill_gemm3_kernel(const uint4* __restrict__ wp, const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int M,
+                     int K, int N, int ldx, int ldy) {
+  constexpr int ST = PG2_STAGES;
+  __shared__ __attribute__((aligned(16))) uint4 ring[ST * PG2_SLICE_U4];
+
+  const int nM = (M + PG_BM - 1) / PG_BM, nN = N / PG_BN;
+  const int nb = nM * nN;
+  const int b = blockIdx.x;
+  const int q = nb / 8, rr = nb % 8, xcd = b & 7;
+  const int u = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
+  const int group = u / (PG_GM * nN), within = u % (PG_GM * nN);
+  const int gm = min(PG_GM, nM - group * PG_GM);
+  const int mb = group * PG_GM + within % gm, nbk = within / gm;
+  const int m0 = mb * PG_BM, t0 = nbk * PG_NT;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w & 3, wn = w >> 2;   // wn: the ping-pong group
+  const int r = lane & 31, h = lane >> 5;
+  const int KB = K >> 6;
+  const int S = 2 * KB;
+
+  const int xs_row0 = 32 * w + (lane >> 2);
+  const int xcc = (lane & 3) ^ ((lane >> 4) & 3);
+  const int xg = (xcc & 1) + 4 * (xcc >> 1);
+  const bf16_t* xsrc0 = x + (size_t)min(m0 + xs_row0, M - 1) * ldx + xg * 8;
+  const bf16_t* xsrc1 = x + (size_t)min(m0 + xs_row0 + 16, M - 1) * ldx + xg * 8;
+  const uint4* wsrc = wp + ((size_t)(t0 + w) * KB) * 256 + lane;
+
+  auto issue = [&](int sl) {
+    const int kb = sl >> 1, hs = sl & 1;
+    uint4* dst = ring + (sl % ST) * PG2_SLICE_U4;
+    __builtin_amdgcn_global_load_lds(xsrc0 + kb * 64 + hs * 16, dst + (32 * w) * 4, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(xsrc1 + kb * 64 + hs * 16, dst + (32 * w + 16) * 4, 16, 0, 0);
+    const uint4* ws = wsrc + (kb * 4 + 2 * hs) * 64;
+    __builtin_amdgcn_global_load_lds(ws, dst + 1024 + (2 * w) * 64, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(ws + 64, dst + 1024 + (2 * w + 1) * 64, 16, 0, 0);
+  };
+  // retire this wave's DMA of slice `sl` (slices up to sl + ST - 2 issued)
+  auto retire = [&](int sl) {
+    const int later = min(ST - 2, S - 1 - sl);   // slices issued after sl
+    if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  f32x16_t acc[2][4];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[mt][i][e] = 0.f;
+  int aidx[2][2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int row = wm * 64 + mt * 32 + r;
+      aidx[mt][jj] = row * 4 + ((jj + 2 * h) ^ ((row >> 2) & 3));
+    }
+  // fragments of one slice: A (2 row tiles) and B (4 column tiles) for both 16-wide k-steps
+  bf16x8_t a00, a01, a10, a11, b00, b01, b02, b03, b10, b11, b12, b13;
+#define PG3_READ(SL)                                                                              \
+  do {                                                                                            \
+    const uint4* cur_ = ring + ((SL) % ST) * PG2_SLICE_U4;                                        \
+    const uint4* bw_ = cur_ + 1024 + (wn * 4 * 2) * 64 + lane;                                    \
+    a00 = __builtin_bit_cast(bf16x8_t, cur_[aidx[0][0]]);                                         \
+    a01 = __builtin_bit_cast(bf16x8_t, cur_[aidx[1][0]]);                                         \
+    a10 = __builtin_bit_cast(bf16x8_t, cur_[aidx[0][1]]);                                         \
+    a11 = __builtin_bit_cast(bf16x8_t, cur_[aidx[1][1]]);                                         \
+    b00 = __builtin_bit_cast(bf16x8_t, bw_[0 * 128]);                                             \
+    b01 = __builtin_bit_cast(bf16x8_t, bw_[1 * 128]);                                             \
+    b02 = __builtin_bit_cast(bf16x8_t, bw_[2 * 128]);                                             \
+    b03 = __builtin_bit_cast(bf16x8_t, bw_[3 * 128]);                                             \
+    b10 = __builtin_bit_cast(bf16x8_t, bw_[0 * 128 + 64]);                                        \
+    b11 = __builtin_bit_cast(bf16x8_t, bw_[1 * 128 + 64]);                                        \
+    b12 = __builtin_bit_cast(bf16x8_t, bw_[2 * 128 + 64]);                                        \
+    b13 = __builtin_bit_cast(bf16x8_t, bw_[3 * 128 + 64]);                                        \
+  } while (0)
+#define PG3_MFMA(A, B, C) C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B, C, 0, 0, 0)
+#define PG3_MMA()                                                                                 \
+  do {                                                                                            \
+    __builtin_amdgcn_s_setprio(1);                                                                \
+    PG3_MFMA(a00, b00, acc[0][0]); PG3_MFMA(a00, b01, acc[0][1]);                                 \
+    PG3_MFMA(a00, b02, acc[0][2]); PG3_MFMA(a00, b03, acc[0][3]);                                 \
+    PG3_MFMA(a01, b00, acc[1][0]); PG3_MFMA(a01, b01, acc[1][1]);                                 \
+    PG3_MFMA(a01, b02, acc[1][2]); PG3_MFMA(a01, b03, acc[1][3]);                                 \
+    PG3_MFMA(a10, b10, acc[0][0]); PG3_MFMA(a10, b11, acc[0][1]);                                 \
+    PG3_MFMA(a10, b12, acc[0][2]); PG3_MFMA(a10, b13, acc[0][3]);                                 \
+    PG3_MFMA(a11, b10, acc[1][0]); PG3_MFMA(a11, b11, acc[1][1]);                                 \
+    PG3_MFMA(a11, b12, acc[1][2]); PG3_MFMA(a11, b13, acc[1][3]);                                 \
+    __builtin_amdgcn_s_setprio(0);                                                                \
+  } while (0)
+
+  // One loop body for both groups; group 1 runs it one barrier behind group 0
+  // (an extra barrier after the prologue; group 0 adds one at the end):
+  //   body k:  barrier X_k . issue slice k + ST - 1 + g . MMA(k) . retire
+  //            slice k + 1 + g . barrier Y_k . READ(k + 1)
+  // Group 0's X_k / Y_k are the workgroup's barriers 2k+1 / 2k+2, group 1's
+  // are 2k+2 / 2k+3, so group 1 READs slice k while group 0 MMAs on it, and
+  // the other way round.  Slice k is read in [Y_{k-1}, X_k] by group 0 and
+  // in [X_k, Y_k] by group 1 (global barriers): every wave retires it before
+  // Y_{k-1} (group 1 one barrier earlier, hence k + 1 + g), and its slot is
+  // refilled only after Y_k (group 1 issues one slice further, hence + g).
+  const int g = wn;
+  for (int p = 0; p < ST - 1 + g; ++p)
+    if (p < S) issue(p);
+  // retire slice 0: (ST - 2 + g) later slices stay in flight
+  if (g) {
+    if (S >= 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (S == 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (S == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    retire(0);
+  }
+  barrier();                                   // P: slice 0 complete
+  if (g) barrier();                            // group 1: one barrier behind
+  PG3_READ(0);
+  for (int k = 0; k < S; ++k) {
+    barrier();                                 // X_k
+    if (k + ST - 1 + g < S) issue(k + ST - 1 + g);
+    PG3_MMA();
+    {
+      // retire slice k + 1 + g: the slices issued after it stay in flight
+      const int top = min(S - 1, k + ST - 1 + g);   // last slice issued so far
+      const int later = top - (k + 1 + g);
+      if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    barrier();                                 // Y_k
+    if (k + 1 < S) PG3_READ(k + 1);
+  }
+  if (!g) barrier();                           // group 0 matches group 1's last barrier
+#undef PG3_READ
+#undef PG3_MFMA
+#undef PG3_MMA
+
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int rbase = m0 + wm * 64 + mt * 32 + 4 * h;
+    if constexpr (EPI == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int col = (t0 + wn * 4 + i) * 32 + r;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = rbase + (e & 3) + 8 * (e >> 2);
+          if (row < M) y[(size_t)row * ldy + col] = f2bf(acc[mt][i][e]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int c = (t0 + wn * 4) / 2 + p;
+        const int col = c * 32 + r;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = rbase + (e & 3) + 8 * (e >> 2);
+          const float g = acc[mt][2 * p][e], up = acc[mt][2 * p + 1][e];
+          if (row < M) y[(size_t)row * ldy + col] = f2bf(g / (1.f + __expf(-g)) * up);
+        }
+      }
+    }
+  }
+}
+
 // v2 build (A/B): MIVGPU_PREFILL_GEMM_ST = 4 or 5 ring slices,
 // MIVGPU_PREFILL_GEMM_PRIO = 1 raises the wave priority over its MFMAs
 int prefill_gemm2_cfg() {
@@ -348,7 +539,8 @@ void launch_gemm2(int blocks, hipStream_t s, const uint4* wp, const bf16_t* x, b
 int prefill_gemm_version() {
   static const int v = [] {
     const char* e = getenv("MIVGPU_PREFILL_GEMM_V");
-    return e && atoi(e) == 1 ? 1 : 2;
+    const int n = e ? atoi(e) : 3;
+    return n == 1 || n == 2 ? n : 3;
   }();
   return v;
 }
@@ -366,6 +558,15 @@ int mivgpu_prefill_gemm(const void* wp, const void* x, void* y, int M, int K, in
     return (int)hipErrorInvalidValue;
   if (ldy < (epi ? N / 2 : N)) return (int)hipErrorInvalidValue;
   const int blocks = ((M + PG_BM - 1) / PG_BM) * (N / PG_BN);
+  if (prefill_gemm_version() == 3) {
+    if (epi == 0)
+      hipLaunchKernelGGL(prefill_gemm3_kernel<0>, dim3(blocks), dim3(PG_THREADS), 0, s, (const uint4*)wp,
+                         (const bf16_t*)x, (bf16_t*)y, M, K, N, ldx, ldy);
+    else
+      hipLaunchKernelGGL(prefill_gemm3_kernel<1>, dim3(blocks), dim3(PG_THREADS), 0, s, (const uint4*)wp,
+                         (const bf16_t*)x, (bf16_t*)y, M, K, N, ldx, ldy);
+    return (int)hipGetLastError();
+  }
   if (prefill_gemm_version() == 2) {
     if (epi == 0)
       launch_gemm2<0>(blocks, s, (const uint4*)wp, (const bf16_t*)x, (bf16_t*)y, M, K, N, ldx, ldy);

@@ -239,6 +239,15 @@ case $suite in
       MIVGPU_PREFILL_GEMM_ST=$st MIVGPU_PREFILL_GEMM_PRIO=$pr step 300 "pg_st${st}_p${pr}" python -u -m \
         k8s_vgpu_scheduler_amd.bench.prefill_gemm --rows 8192 --out "$out/pg_st${st}_p${pr}.json"
     done; done ;;
+  pg3)
+    # prefill GEMM v3 (ping-pong wave groups) vs v2: numerics, 2048 / 8192 rows, 8k-token TTFT on it
+    step 300 tests python -u -m pytest tests/test_ops_gpu.py -v --timeout 120 --timeout-method thread -k "prefill_gemm"
+    step 300 pg_v3 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_gemm --rows 2048,8192 --out "$out/pg_v3.json"
+    MIVGPU_PREFILL_GEMM_V=2 step 300 pg_v2 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_gemm --rows 8192 \
+      --out "$out/pg_v2.json"
+    MIVGPU_PREFILL_GEMM=native step 300 ttft8k_native python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 \
+      --ctx 9216 --iters 5
+    step 300 ttft8k_lib python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 --ctx 9216 --iters 5 ;;
   prefill)
     step 120 native python3 -m k8s_vgpu_scheduler_amd.bench.prefill
     HSA_CU_MASK=0:0-63 step 120 cu64 python3 -m k8s_vgpu_scheduler_amd.bench.prefill
