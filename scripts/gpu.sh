@@ -248,6 +248,18 @@ case $suite in
     MIVGPU_PREFILL_GEMM=native step 300 ttft8k_native python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 \
       --ctx 9216 --iters 5
     step 300 ttft8k_lib python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 --ctx 9216 --iters 5 ;;
+  pgpmc)
+    # counters of the prefill GEMM (v3) next to hipBLASLt's kernels on the same shapes (8192 rows)
+    cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
+    pg="python3 -m k8s_vgpu_scheduler_amd.bench.prefill_gemm --rows 8192 --reps 3"
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$out/p/a" -o run -- $pg \
+      > "$out/a.log" 2>&1 || exit 1
+    timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_BF16 \
+      SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS --kernel-trace --output-format csv -d "$out/p/b" -o run -- $pg \
+      > "$out/b.log" 2>&1 || exit 1
+    timeout -s KILL 120 rocprofv3 --pmc TCP_TCC_READ_REQ_sum SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_SALU \
+      --kernel-trace --output-format csv -d "$out/p/c" -o run -- $pg > "$out/c.log" 2>&1 || exit 1
+    python3 "$R/scripts/probe/pmc_summary.py" "$out/p" > "$out/pgemm_pmc.json" && rm -rf "$out/p" ;;
   prefill)
     step 120 native python3 -m k8s_vgpu_scheduler_amd.bench.prefill
     HSA_CU_MASK=0:0-63 step 120 cu64 python3 -m k8s_vgpu_scheduler_amd.bench.prefill
