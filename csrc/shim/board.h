@@ -53,6 +53,9 @@ constexpr uint64_t kCreditNs = 5000000ull;
 // Fair-share mode: a tenant whose flags went stale still counts as backlogged
 // by its last fresh state for this long.
 constexpr uint64_t kStateGraceNs = 100000000ull;
+// Fair-share mode: an OWES flag counts while the process had waves of its own
+// resident within this long.
+constexpr uint64_t kOwesEvidenceNs = 50000000ull;
 // Fair-share mode: a tenant's lead over the furthest-behind contender is
 // bounded here (virtual time beyond it is dropped: a tenant cannot bank an
 // unbounded lead that holds it for seconds).
@@ -84,6 +87,7 @@ struct Handle {
   uint32_t last_lim[MIVGPU_BOARD_SLOTS] = {};     // per board slot, the weight of its last fresh flags
   int last_state[MIVGPU_BOARD_SLOTS] = {};        // ... their state, and when they were fresh
   uint64_t last_state_ns[MIVGPU_BOARD_SLOTS] = {};
+  uint64_t wave_ns[MIVGPU_BOARD_SLOTS] = {};      // per board slot, the last pass with its waves resident
   double sub_ewma = 0;                            // share of recent passes fully subscribed
   bool fair = false;                              // fair-share mode
   uint64_t vmin = 0;                              // the previous pass's smallest running virtual time
@@ -423,6 +427,7 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
       h.bl_ewma[slot] = 0;
       h.last_lim[slot] = 0;
       h.last_state_ns[slot] = 0;
+      h.wave_ns[slot] = 0;
       if (slot + 1 > hi) hi = slot + 1;
     }
     sl[i] = slot;
@@ -446,9 +451,17 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
     // (measured: with eight tenants their samplers ran every ~5.5 ms, not 2,
     // and a stall past the 20 ms freshness dropped a queued tenant out of the
     // subscription half the time); without flags, waves resident
-    if (st[i] >= 0) bl[i] = held || owes;
+    // Flags are tenant-writable, so they only count with evidence in the
+    // readings: HELD with its gate's wave resident, OWES with waves of its own
+    // resident within kOwesEvidenceNs.  A tenant faking an idle neighbour's
+    // flags could otherwise declare the GPU fully subscribed and escape its
+    // own cap in the fair-share mode.
+    if (w > kGateUnits) h.wave_ns[slot] = now;
+    const bool evidence = h.wave_ns[slot] && now - h.wave_ns[slot] < kOwesEvidenceNs;
+    if (st[i] >= 0) bl[i] = (held && v > 0) || (owes && evidence);
     else if (h.last_state_ns[slot] && now - h.last_state_ns[slot] < kStateGraceNs)
-      bl[i] = (h.last_state[slot] & (MIVGPU_FLAG_HELD | MIVGPU_FLAG_OWES)) != 0 || w > 0;
+      bl[i] = ((h.last_state[slot] & MIVGPU_FLAG_HELD) && v > 0) ||
+              ((h.last_state[slot] & MIVGPU_FLAG_OWES) && evidence) || w > 0;
     else bl[i] = w > 0;
     if (dt) {
       const double a = (double)dt / (double)kSubTauNs < 1.0 ? (double)dt / (double)kSubTauNs : 1.0;

@@ -353,3 +353,15 @@ def test_fair_share_counts_presence_not_wave_shape(native_build, tmp_path):
     s = _fair_run(native_build, tmp_path, {111: (40, B.FLAG_OWES, 500000), 222: (10, B.FLAG_OWES, 500000)})
     assert s[111].lead_ns == 0 and s[222].lead_ns == 0, (s[111].lead_ns, s[222].lead_ns)
     assert s[111].frac_ns > 3 * s[222].frac_ns       # the charge still follows the waves
+
+
+def test_faked_flags_of_an_idle_neighbour_do_not_subscribe_the_gpu(native_build, tmp_path):
+    """The flags file is tenant-writable: a 25 % tenant marking an idle 75 %
+    neighbour OWES (or HELD) would make the GPU look fully subscribed and lift
+    its own cap in fair-share mode.  Flags count only with evidence in the
+    readings (HELD: its gate's wave resident; OWES: its own waves within
+    50 ms), so the GPU stays undersubscribed and the buckets cap both."""
+    s = _fair_run(native_build, tmp_path, {111: (10, B.FLAG_OWES, 250000), 222: (0, B.FLAG_OWES, 750000)})
+    assert s[111].lead_ns == -1 and s[222].lead_ns == -1, (s[111].lead_ns, s[222].lead_ns)
+    s = _fair_run(native_build, tmp_path / "held", {111: (10, B.FLAG_OWES, 250000), 222: (0, B.FLAG_HELD, 750000)})
+    assert s[111].lead_ns == -1 and s[222].lead_ns == -1, (s[111].lead_ns, s[222].lead_ns)
