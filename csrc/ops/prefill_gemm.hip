@@ -503,6 +503,129 @@ prefill_gemm3_kernel(const uint4* __restrict__ wp, const bf16_t* __restrict__ x,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Version 4 (A/B, MIVGPU_PREFILL_GEMM_V=4): the same ring and tile with FOUR
+// waves, one per SIMD, each 128 x 128 (4 x 4 accumulators: 256 fp32 registers,
+// the 512-register file of a lone wave) -- the shape of hipBLASLt's kernel on
+// these GEMMs (profiles §40): per MFMA half the LDS fragment reads of the
+// 64 x 128 waves (16 reads feed 32 MFMAs per slice) and one barrier per 32
+// MFMAs.  Each wave DMAs 64 X rows and two W tiles per slice (8 x 1 KB).
+template <int EPI>
+__global__ void __launch_bounds__(256, 1)
+prefill_gemm4_kernel(const uint4* __restrict__ wp, const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int M,
+                     int K, int N, int ldx, int ldy) {
+  constexpr int ST = PG2_STAGES;
+  __shared__ __attribute__((aligned(16))) uint4 ring[ST * PG2_SLICE_U4];
+
+  const int nM = (M + PG_BM - 1) / PG_BM, nN = N / PG_BN;
+  const int nb = nM * nN;
+  const int b = blockIdx.x;
+  const int q = nb / 8, rr = nb % 8, xcd = b & 7;
+  const int u = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
+  const int group = u / (PG_GM * nN), within = u % (PG_GM * nN);
+  const int gm = min(PG_GM, nM - group * PG_GM);
+  const int mb = group * PG_GM + within % gm, nbk = within / gm;
+  const int m0 = mb * PG_BM, t0 = nbk * PG_NT;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w & 1, wn = w >> 1;
+  const int r = lane & 31, h = lane >> 5;
+  const int KB = K >> 6;
+  const int S = 2 * KB;
+
+  // DMA sources: X rows 64w + 16i + lane/4 (i = 0..3), W tiles 2w, 2w + 1
+  const int xcc = (lane & 3) ^ ((lane >> 4) & 3);
+  const int xg = (xcc & 1) + 4 * (xcc >> 1);
+  const bf16_t* xsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) xsrc[i] = x + (size_t)min(m0 + 64 * w + 16 * i + (lane >> 2), M - 1) * ldx + xg * 8;
+  const uint4* wsrc0 = wp + ((size_t)(t0 + 2 * w) * KB) * 256 + lane;
+  const uint4* wsrc1 = wp + ((size_t)(t0 + 2 * w + 1) * KB) * 256 + lane;
+
+  auto issue = [&](int sl) {
+    const int kb = sl >> 1, hs = sl & 1;
+    uint4* dst = ring + (sl % ST) * PG2_SLICE_U4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds(xsrc[i] + kb * 64 + hs * 16, dst + (64 * w + 16 * i) * 4, 16, 0, 0);
+    const int wo = (kb * 4 + 2 * hs) * 64;
+    __builtin_amdgcn_global_load_lds(wsrc0 + wo, dst + 1024 + (4 * w) * 64, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(wsrc0 + wo + 64, dst + 1024 + (4 * w + 1) * 64, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(wsrc1 + wo, dst + 1024 + (4 * w + 2) * 64, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(wsrc1 + wo + 64, dst + 1024 + (4 * w + 3) * 64, 16, 0, 0);
+  };
+
+  f32x16_t acc[4][4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[mt][i][e] = 0.f;
+  int aidx[4][2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int row = wm * 128 + mt * 32 + r;
+      aidx[mt][jj] = row * 4 + ((jj + 2 * h) ^ ((row >> 2) & 3));
+    }
+
+  for (int p = 0; p < ST - 1; ++p)
+    if (p < S) issue(p);
+  for (int sl = 0; sl < S; ++sl) {
+    const int later = min(ST - 2, S - 1 - sl);   // 8 DMAs per slice per wave
+    if (later >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (later == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (sl + ST - 1 < S) issue(sl + ST - 1);
+    const uint4* cur = ring + (sl % ST) * PG2_SLICE_U4;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      bf16x8_t af[4], bfr[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) af[mt] = __builtin_bit_cast(bf16x8_t, cur[aidx[mt][jj]]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bfr[i] = __builtin_bit_cast(bf16x8_t, cur[1024 + ((wn * 4 + i) * 2 + jj) * 64 + lane]);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[mt][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mt], bfr[i], acc[mt][i], 0, 0, 0);
+    }
+  }
+
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const int rbase = m0 + wm * 128 + mt * 32 + 4 * h;
+    if constexpr (EPI == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int col = (t0 + wn * 4 + i) * 32 + r;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = rbase + (e & 3) + 8 * (e >> 2);
+          if (row < M) y[(size_t)row * ldy + col] = f2bf(acc[mt][i][e]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int c = (t0 + wn * 4) / 2 + p;
+        const int col = c * 32 + r;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = rbase + (e & 3) + 8 * (e >> 2);
+          const float g = acc[mt][2 * p][e], up = acc[mt][2 * p + 1][e];
+          if (row < M) y[(size_t)row * ldy + col] = f2bf(g / (1.f + __expf(-g)) * up);
+        }
+      }
+    }
+  }
+}
+
 // v2 build (A/B): MIVGPU_PREFILL_GEMM_ST = 4 or 5 ring slices,
 // MIVGPU_PREFILL_GEMM_PRIO = 1 raises the wave priority over its MFMAs
 int prefill_gemm2_cfg() {
@@ -540,7 +663,7 @@ int prefill_gemm_version() {
   static const int v = [] {
     const char* e = getenv("MIVGPU_PREFILL_GEMM_V");
     const int n = e ? atoi(e) : 3;
-    return n == 1 || n == 2 ? n : 3;
+    return n == 1 || n == 2 || n == 4 ? n : 3;
   }();
   return v;
 }
@@ -558,6 +681,15 @@ int mivgpu_prefill_gemm(const void* wp, const void* x, void* y, int M, int K, in
     return (int)hipErrorInvalidValue;
   if (ldy < (epi ? N / 2 : N)) return (int)hipErrorInvalidValue;
   const int blocks = ((M + PG_BM - 1) / PG_BM) * (N / PG_BN);
+  if (prefill_gemm_version() == 4) {
+    if (epi == 0)
+      hipLaunchKernelGGL(prefill_gemm4_kernel<0>, dim3(blocks), dim3(256), 0, s, (const uint4*)wp, (const bf16_t*)x,
+                         (bf16_t*)y, M, K, N, ldx, ldy);
+    else
+      hipLaunchKernelGGL(prefill_gemm4_kernel<1>, dim3(blocks), dim3(256), 0, s, (const uint4*)wp, (const bf16_t*)x,
+                         (bf16_t*)y, M, K, N, ldx, ldy);
+    return (int)hipGetLastError();
+  }
   if (prefill_gemm_version() == 3) {
     if (epi == 0)
       hipLaunchKernelGGL(prefill_gemm3_kernel<0>, dim3(blocks), dim3(PG_THREADS), 0, s, (const uint4*)wp,

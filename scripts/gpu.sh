@@ -248,6 +248,15 @@ case $suite in
     MIVGPU_PREFILL_GEMM=native step 300 ttft8k_native python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 \
       --ctx 9216 --iters 5
     step 300 ttft8k_lib python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 --ctx 9216 --iters 5 ;;
+  pg4)
+    # prefill GEMM v4 (four waves, 128x128 each) vs v3: numerics, 8192 rows, TTFT on it
+    MIVGPU_PREFILL_GEMM_V=4 step 300 tests python -u -m pytest tests/test_ops_gpu.py -v --timeout 120 \
+      --timeout-method thread -k "prefill_gemm"
+    MIVGPU_PREFILL_GEMM_V=4 step 300 pg_v4 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_gemm --rows 2048,8192 \
+      --out "$out/pg_v4.json"
+    step 300 pg_v3 python -u -m k8s_vgpu_scheduler_amd.bench.prefill_gemm --rows 8192 --out "$out/pg_v3.json"
+    MIVGPU_PREFILL_GEMM=native MIVGPU_PREFILL_GEMM_V=4 step 300 ttft8k_v4 python -u -m \
+      k8s_vgpu_scheduler_amd.bench.prefill --len 8192 --ctx 9216 --iters 5 ;;
   pgpmc)
     # counters of the prefill GEMM (v3) next to hipBLASLt's kernels on the same shapes (8192 rows)
     cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
