@@ -149,9 +149,8 @@ typedef struct {
  *   recv_ns -- the integral of w / W (GPU time received; utilisation),
  *   busy_ns -- time with its waves resident,
  *   vt_ns   -- its virtual time while the GPU is fully subscribed (below):
- *              the integral of (its wave ratio + its presence, 1 / the
- *              processes with waves resident, while it has) / 2 / its core
- *              limit,
+ *              the integral of its presence (1 / the processes with waves
+ *              resident, while it has) / its core limit,
  *   lead_ns -- -1 while the GPU is not fully subscribed, else its GPU time
  *              received beyond its weighted fair share: (vt - the mean vt of
  *              the running contenders) x its limit, >= 0.

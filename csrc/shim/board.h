@@ -348,9 +348,8 @@ enum Split { kSplitRatio = 0, kSplitEqual = 1 };
 // without flags: waves resident), weighted by its core limit (flags; 100 %
 // without; the monitor's node-written limit caps it).  In fair-share mode
 // (the backlogged weights filling the GPU in most recent passes) each
-// backlogged process's virtual time advances by half its wave ratio and half
-// its presence (an equal part of each pass among the processes with waves
-// resident) / its weight; one not backlogged, or held while behind, keeps at most
+// backlogged process's virtual time advances by its presence (an equal part
+// of each pass among the processes with waves resident) / its weight; one not backlogged, or held while behind, keeps at most
 // kCreditNs of credit below the smallest running virtual time (a short gap
 // does not forgive the ones that ran without it, a long one banks nothing
 // more), and every process's lead is (vt - the running processes' mean vt)
@@ -457,7 +456,11 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
     // resident within kOwesEvidenceNs.  A tenant faking an idle neighbour's
     // flags could otherwise declare the GPU fully subscribed and escape its
     // own cap in the fair-share mode.
-    if (w > kGateUnits) h.wave_ns[slot] = now;
+    // evidence of its own activity: waves beyond a gate's, or its gate's wave
+    // while its flags say HELD (a tenant released from a long hold owes at
+    // once; measured, without this a 25 % tenant dropped out of the
+    // subscription after every hold of more than 50 ms and took 28-30 %)
+    if (w > kGateUnits || (held && v > 0)) h.wave_ns[slot] = now;
     const bool evidence = h.wave_ns[slot] && now - h.wave_ns[slot] < kOwesEvidenceNs;
     if (st[i] >= 0) bl[i] = (held && v > 0) || (owes && evidence);
     else if (h.last_state_ns[slot] && now - h.last_state_ns[slot] < kStateGraceNs)
@@ -477,17 +480,14 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
     if (W > 0) {
       got = split == kSplitEqual ? (w > 0 ? 1.0 / (double)resident : 0.0) : (double)w / (double)W;
       f = got;
-      // the fair-share virtual time advances by half the wave ratio charged
-      // here and half presence (an equal part of the pass for each process
-      // with waves resident, the reference's NVML per-process utilisation
-      // being time-sliced presence).  The ratio alone scatters with each
-      // kernel's shape -- eight identical decode tenants held on it came out
-      // 0.87 apart in throughput, where the hardware alone gives 0.996 --
-      // and presence alone lets a capped tenant whose kernels are wider than
-      // its neighbour's take more than its cap in wave share (a 25 % tenant
-      // next to a 75 % one: 28 %).
-      const double pres = w > kGateUnits ? 1.0 / (double)present : 0.0;
-      use[i] = 0.5 * pres + 0.5 * ((double)w / (double)W);
+      // the fair-share virtual time advances by presence: an equal part of
+      // the pass for each process with waves resident (the reference's
+      // NVML per-process utilisation is time-sliced presence).  The wave
+      // ratio charged below scatters with each kernel's shape: eight
+      // identical decode tenants came out 0.87 apart in throughput after
+      // being held on it, where the hardware alone gives 0.996 (half ratio,
+      // half presence: 0.91, and a 25 % tenant next to a 75 % one at 30 %).
+      use[i] = w > kGateUnits ? 1.0 / (double)present : 0.0;
     } else {
       got = 0.0;
       f = st[i] < 0 ? 1.0 : (owes && owing > 0 ? 1.0 / (double)owing : 1.0);
