@@ -53,9 +53,11 @@ constexpr uint64_t kCreditNs = 5000000ull;
 // Fair-share mode: a tenant whose flags went stale still counts as backlogged
 // by its last fresh state for this long.
 constexpr uint64_t kStateGraceNs = 100000000ull;
-// Fair-share mode: an OWES flag counts while the process had waves of its own
-// resident within this long.
-constexpr uint64_t kOwesEvidenceNs = 50000000ull;
+// Fair-share mode: a HELD or OWES flag counts while the process had waves of
+// its own resident within this long (a held tenant runs a graph between its
+// gates at least every ~25 ms hold; an idle one faked busy by a neighbour
+// drops out after this).
+constexpr uint64_t kEvidenceNs = 200000000ull;
 // Fair-share mode: a tenant's lead over the furthest-behind contender is
 // bounded here (virtual time beyond it is dropped: a tenant cannot bank an
 // unbounded lead that holds it for seconds).
@@ -452,20 +454,16 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
     // and a stall past the 20 ms freshness dropped a queued tenant out of the
     // subscription half the time); without flags, waves resident
     // Flags are tenant-writable, so they only count with evidence in the
-    // readings: HELD with its gate's wave resident, OWES with waves of its own
-    // resident within kOwesEvidenceNs.  A tenant faking an idle neighbour's
-    // flags could otherwise declare the GPU fully subscribed and escape its
-    // own cap in the fair-share mode.
-    // evidence of its own activity: waves beyond a gate's, or its gate's wave
-    // while its flags say HELD (a tenant released from a long hold owes at
-    // once; measured, without this a 25 % tenant dropped out of the
-    // subscription after every hold of more than 50 ms and took 28-30 %)
+    // readings: the process had waves beyond a gate's resident, or its gate's
+    // wave, within kEvidenceNs.  A tenant faking an idle neighbour's flags
+    // could otherwise declare the GPU fully subscribed and escape its own cap
+    // in the fair-share mode.  (Demanding the gate's wave at every pass of a
+    // hold instead, a held 25 % tenant next to a 75 % one measured 28 %.)
     if (w > kGateUnits || (held && v > 0)) h.wave_ns[slot] = now;
-    const bool evidence = h.wave_ns[slot] && now - h.wave_ns[slot] < kOwesEvidenceNs;
-    if (st[i] >= 0) bl[i] = (held && v > 0) || (owes && evidence);
+    const bool evidence = h.wave_ns[slot] && now - h.wave_ns[slot] < kEvidenceNs;
+    if (st[i] >= 0) bl[i] = (held || owes) && evidence;
     else if (h.last_state_ns[slot] && now - h.last_state_ns[slot] < kStateGraceNs)
-      bl[i] = ((h.last_state[slot] & MIVGPU_FLAG_HELD) && v > 0) ||
-              ((h.last_state[slot] & MIVGPU_FLAG_OWES) && evidence) || w > 0;
+      bl[i] = ((h.last_state[slot] & (MIVGPU_FLAG_HELD | MIVGPU_FLAG_OWES)) && evidence) || w > 0;
     else bl[i] = w > 0;
     if (dt) {
       const double a = (double)dt / (double)kSubTauNs < 1.0 ? (double)dt / (double)kSubTauNs : 1.0;
