@@ -384,7 +384,9 @@ def test_unequal_temporal_limits_get_their_shares(tmp, limits):
     within 3 points.  A tenant below its cap -- the 75 % or 50 % one next to
     25 % tenants, whose co-running kernels take more than their split of
     the GPU -- is work-conserving: never held, it gets what the others
-    leave.  Throughput relative to an unthrottled slice is at least 0.9 x
+    leave.  Each tenant's share of the tokens all of them produced is its
+    limit's share of the limits within 10 % (the check that does not read the
+    estimator).  Throughput relative to an unthrottled slice is at least 0.9 x
     every tenant's entitlement and at most 1.8 x (co-running decode tenants
     share the GPU at a gain -- 4 slices deliver 1.38 x one slice's tokens --
     and unevenly between two of them); a disabled governor (each tenant
@@ -400,8 +402,16 @@ def test_unequal_temporal_limits_get_their_shares(tmp, limits):
              "busy_share_pct": gov[i]["busy_share_pct"], "held_ms": gov[i]["gov_held_ms"],
              "charged_ms": gov[i]["gov_charged_ms"]} for i, lim in enumerate(limits)]
     print(json.dumps({"limits": limits, "alone_tok_s": alone, "slices": rows}))
+    # independent of the estimator: the tokens each tenant
+    # produced, as a share of all of them, follow the limits within 10 %
+    total = sum(per[:len(limits)])
+    for row, lim in zip(rows, limits):
+        row["token_share"] = round(row["tok_s"] / total, 3)
+    print(json.dumps({"token_shares": [r["token_share"] for r in rows]}))
     for row in rows:
         lim = row["limit"]
+        want = lim / sum(limits)
+        assert abs(row["token_share"] / want - 1.0) <= 0.10, rows
         assert row["busy_share_pct"] is not None and row["busy_share_pct"] <= lim + 3.0, rows   # the cap
         if row["held_ms"] > 200:       # held: at its cap
             assert abs(row["busy_share_pct"] - lim) <= 3.0, rows
