@@ -114,9 +114,10 @@ def main():
                     help="run the node monitor's feedback pass (priority + utilization_switch) over the shim "
                          "rounds' regions every SECONDS while they run (0 = off)")
     ap.add_argument("--policy", default="default", choices=["default", "force", "disable"])
-    ap.add_argument("--board", default="node", choices=["node", "shim"],
+    ap.add_argument("--board", default="auto", choices=["auto", "node", "shim"],
                     help="owner of the GPU's share board in the shim rounds: the node sampler (mivgpu-boardd, "
-                         "as the monitor runs it) or a governed slice's shim")
+                         "as the monitor runs it) or a governed slice's shim; auto = node on one GPU, shim with "
+                         "several ranks (one node sampler per rank would read every GPU's processes)")
     ap.add_argument("--slice-limits", default="",
                     help="comma list of per-slice core limits (%%) for the shim and temporal rounds, e.g. 75,25 "
                          "(unequal tenants; default 100/N each)")
@@ -301,7 +302,7 @@ def main():
         # it in production (--board shim: a governed slice takes the role)
         boardd = None
         bdir = next((p.board_dir for p in procs if getattr(p, "board_dir", None)), None)
-        if args.board == "node" and bdir and not cpu:
+        if (args.board == "node" or (args.board == "auto" and world == 1)) and bdir and not cpu:
             from k8s_vgpu_scheduler_amd.monitor.board import BoardSampler
             boardd = BoardSampler(bdir).start()
         try:
