@@ -271,32 +271,26 @@ decode_tail_kernel(const bf16_t* __restrict__ logits, int ld, int vocab, int64_t
 // head-grouped [Hkv][G][rows][D] (the G query heads sharing a KV head are one
 // contiguous block of rows for the attention GEMMs), and K/V also go to
 // k_plain / v_plain [Hkv][rows][D] when given (the prompt's own attention).
+// Prefill runs TPW tokens per wave (qk_norm_rope_kv_kernel<PACKED, 8>): a
+// one-token wave has 256 B in flight, and with the CU's workgroup slots full
+// that capped an 8192-token prompt at ~1.7 TB/s (135 us per layer); eight
+// tokens' loads are issued before the first token is processed.
 template <bool PACKED>
-__global__ void __launch_bounds__(64)
-qk_norm_rope_kv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ qw,
-                       const bf16_t* __restrict__ kw, const int* __restrict__ pos,
-                       bf16_t* __restrict__ q_out, bf16_t* __restrict__ k_cache,
-                       bf16_t* __restrict__ v_cache, int Hq, int Hkv, int max_ctx, float eps,
-                       float theta, int cache_b, bf16_t* __restrict__ k_plain,
-                       bf16_t* __restrict__ v_plain) {
+__device__ __forceinline__ void qk_one(const bf16_t* __restrict__ qkv_row, float x0, float x1, int b, int h,
+                                       int l, int p, int rows, const bf16_t* __restrict__ qw,
+                                       const bf16_t* __restrict__ kw, bf16_t* __restrict__ q_out,
+                                       bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache, int Hq,
+                                       int Hkv, int max_ctx, float eps, float inv_freq, int cache_b,
+                                       bf16_t* __restrict__ k_plain, bf16_t* __restrict__ v_plain) {
   constexpr int D = 128;
-  const int b = blockIdx.x;
-  const int h = blockIdx.y;
-  const int l = threadIdx.x;
-  const int rows = gridDim.x;
   const int cb = cache_b >= 0 ? cache_b : b;
-  const int row_stride = (Hq + 2 * Hkv) * D;
-  const bf16_t* src = qkv + (size_t)b * row_stride + (size_t)h * D;
-  float x0 = bf2f(src[l]);
-  float x1 = bf2f(src[l + 64]);
-  const int p = pos[b];
   const bool in_range = p >= 0 && p < max_ctx;  // never write past the cache
   if (h >= Hq + Hkv) {  // V head: plain copy into the cache
     const int hv = h - Hq - Hkv;
     if (v_plain) {
       bf16_t* dst = v_plain + ((size_t)hv * rows + b) * D;
-      dst[l] = src[l];
-      dst[l + 64] = src[l + 64];
+      dst[l] = qkv_row[l];
+      dst[l + 64] = qkv_row[l + 64];
     }
     if (!in_range) return;
     if (PACKED) {  // V group [dt 8][q 4][r 16][e 8]: key = 8q + e, dim = 16dt + r
@@ -317,8 +311,6 @@ qk_norm_rope_kv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict_
   const float inv = rsqrtf(ss / (float)D + eps);
   x0 = x0 * inv * bf2f(nw[l]);
   x1 = x1 * inv * bf2f(nw[l + 64]);
-  // inv_freq = theta^(-2l/D)
-  const float inv_freq = exp2f(-(2.0f * (float)l / (float)D) * log2f(theta));
   float s, c;
   sincosf((float)p * inv_freq, &s, &c);
   const float o0 = x0 * c - x1 * s;
@@ -351,6 +343,41 @@ qk_norm_rope_kv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict_
   }
   dst[l] = f2bf(o0);
   dst[l + 64] = f2bf(o1);
+}
+
+// grid = (ceil(rows / TPW), Hq + 2*Hkv), one wave of 64 lanes.
+template <bool PACKED, int TPW>
+__global__ void __launch_bounds__(64)
+qk_norm_rope_kv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ qw,
+                       const bf16_t* __restrict__ kw, const int* __restrict__ pos,
+                       bf16_t* __restrict__ q_out, bf16_t* __restrict__ k_cache,
+                       bf16_t* __restrict__ v_cache, int Hq, int Hkv, int max_ctx, float eps,
+                       float theta, int cache_b, bf16_t* __restrict__ k_plain,
+                       bf16_t* __restrict__ v_plain, int rows) {
+  constexpr int D = 128;
+  const int b0 = blockIdx.x * TPW;
+  const int h = blockIdx.y;
+  const int l = threadIdx.x;
+  const int row_stride = (Hq + 2 * Hkv) * D;
+  float x0[TPW], x1[TPW];
+  int p[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {  // every token's loads in flight first
+    const int b = min(b0 + t, rows - 1);
+    const bf16_t* src = qkv + (size_t)b * row_stride + (size_t)h * D;
+    x0[t] = bf2f(src[l]);
+    x1[t] = bf2f(src[l + 64]);
+    p[t] = pos[b];
+  }
+  // inv_freq = theta^(-2l/D)
+  const float inv_freq = exp2f(-(2.0f * (float)l / (float)D) * log2f(theta));
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int b = b0 + t;
+    if (b >= rows) break;  // wave-uniform
+    qk_one<PACKED>(qkv + (size_t)b * row_stride + (size_t)h * D, x0[t], x1[t], b, h, l, p[t], rows, qw, kw,
+                   q_out, k_cache, v_cache, Hq, Hkv, max_ctx, eps, inv_freq, cache_b, k_plain, v_plain);
+  }
 }
 
 // ---------------------------------------------- GQA split-K decode attention --
@@ -1236,15 +1263,15 @@ int mivgpu_qk_norm_rope_kv(const void* qkv, const void* qw, const void* kw, cons
   if (head_dim != 128 || B <= 0) return -1;
   if (attn_impl()) {
     if (max_ctx % ATT_KPW) return -1;
-    hipLaunchKernelGGL(qk_norm_rope_kv_kernel<true>, dim3(B, Hq + 2 * Hkv), dim3(64), 0, s,
+    hipLaunchKernelGGL((qk_norm_rope_kv_kernel<true, 1>), dim3(B, Hq + 2 * Hkv), dim3(64), 0, s,
                        (const bf16_t*)qkv, (const bf16_t*)qw, (const bf16_t*)kw, pos,
                        (bf16_t*)q_out, (bf16_t*)k_cache, (bf16_t*)v_cache, Hq, Hkv, max_ctx, eps,
-                       theta, -1, (bf16_t*)nullptr, (bf16_t*)nullptr);
+                       theta, -1, (bf16_t*)nullptr, (bf16_t*)nullptr, B);
   } else {
-    hipLaunchKernelGGL(qk_norm_rope_kv_kernel<false>, dim3(B, Hq + 2 * Hkv), dim3(64), 0, s,
+    hipLaunchKernelGGL((qk_norm_rope_kv_kernel<false, 1>), dim3(B, Hq + 2 * Hkv), dim3(64), 0, s,
                        (const bf16_t*)qkv, (const bf16_t*)qw, (const bf16_t*)kw, pos,
                        (bf16_t*)q_out, (bf16_t*)k_cache, (bf16_t*)v_cache, Hq, Hkv, max_ctx, eps,
-                       theta, -1, (bf16_t*)nullptr, (bf16_t*)nullptr);
+                       theta, -1, (bf16_t*)nullptr, (bf16_t*)nullptr, B);
   }
   return (int)hipGetLastError();
 }
@@ -1257,17 +1284,19 @@ int mivgpu_prefill_qk_norm_rope_kv(const void* qkv, const void* qw, const void* 
                                    int rows, int cache_b, int Hq, int Hkv, int head_dim, int max_ctx, float eps,
                                    float theta, hipStream_t s) {
   if (head_dim != 128 || rows <= 0 || cache_b < 0 || Hkv <= 0 || Hq % Hkv) return -1;
+  constexpr int kPrefillTpw = 8;
+  const int grid_x = (rows + kPrefillTpw - 1) / kPrefillTpw;
   if (attn_impl()) {
     if (max_ctx % ATT_KPW) return -1;
-    hipLaunchKernelGGL(qk_norm_rope_kv_kernel<true>, dim3(rows, Hq + 2 * Hkv), dim3(64), 0, s,
+    hipLaunchKernelGGL((qk_norm_rope_kv_kernel<true, kPrefillTpw>), dim3(grid_x, Hq + 2 * Hkv), dim3(64), 0, s,
                        (const bf16_t*)qkv, (const bf16_t*)qw, (const bf16_t*)kw, pos, (bf16_t*)q_out,
                        (bf16_t*)k_cache, (bf16_t*)v_cache, Hq, Hkv, max_ctx, eps, theta, cache_b,
-                       (bf16_t*)k_plain, (bf16_t*)v_plain);
+                       (bf16_t*)k_plain, (bf16_t*)v_plain, rows);
   } else {
-    hipLaunchKernelGGL(qk_norm_rope_kv_kernel<false>, dim3(rows, Hq + 2 * Hkv), dim3(64), 0, s,
+    hipLaunchKernelGGL((qk_norm_rope_kv_kernel<false, kPrefillTpw>), dim3(grid_x, Hq + 2 * Hkv), dim3(64), 0, s,
                        (const bf16_t*)qkv, (const bf16_t*)qw, (const bf16_t*)kw, pos, (bf16_t*)q_out,
                        (bf16_t*)k_cache, (bf16_t*)v_cache, Hq, Hkv, max_ctx, eps, theta, cache_b,
-                       (bf16_t*)k_plain, (bf16_t*)v_plain);
+                       (bf16_t*)k_plain, (bf16_t*)v_plain, rows);
   }
   return (int)hipGetLastError();
 }

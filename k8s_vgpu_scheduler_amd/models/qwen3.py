@@ -204,7 +204,11 @@ class Qwen3Decoder:
                     # GEMMs (hipBLASLt 24.6 vs wide 46 us at 128 rows; +34 MB/layer)
                     keep = ops.visible_cus() > int(os.environ.get("MIVGPU_SLICE_PLAN_CUS", "96"))
                     lw["po"] = ops.PackedLinear(lw["wo"] if keep else lw.pop("wo"))
-                lw["pd"] = ops.PackedLinear(lw.pop("wd"))
+                # the plain down weight too where gate_up keeps its own: an
+                # 8192-token prompt otherwise unpacks it for the library GEMM
+                # in every layer (+100 MB/layer)
+                keep_d = keep_gu and os.environ.get("MIVGPU_KEEP_PLAIN_DOWN", "1") == "1"
+                lw["pd"] = ops.PackedLinear(lw["wd"] if keep_d else lw.pop("wd"))
                 for key, name in (("pqkv", "qkv"), ("po", "o"), ("pd", "down"), ("pgu", "gu")):
                     if name in widek and key in lw:
                         lw[key].variant = ops.VARIANT_WIDEK
@@ -551,27 +555,50 @@ class Qwen3Decoder:
             pl.norm_call(x[s:e], out=out[s:e], row_scale=(self.ss_pf, 1, self.cfg.hidden, self.cfg.eps))
         return out
 
-    def _normed_proj(self, lw, name, x, ln):
+    def _normed_proj(self, lw, name, x, ln, h=None):
         """Norm-fused decoder, prefill: RMSNorm(x) . W^T (SiLU*up for gate_up)
         on the plain weight after a separate norm where one is kept and the
         rows are prompt-sized, on the packed copy unpacked for the library GEMM
         for long prompts (its folded norm weight: X normalised without one),
-        else on the packed copy with the folded norm and row scales."""
+        else on the packed copy with the folded norm and row scales.  ``h``:
+        the normalised rows _add_then_norm already produced for this call."""
         packed, plain = {"qkv": ("pqkv", "wqkv"), "gu": ("pgu", "wgu")}[name]
         if plain in lw and x.shape[0] > 64:
-            y = F.linear(self._norm(x, ln), lw[plain])
+            y = F.linear(self._norm(x, ln) if h is None else h, lw[plain])
             return ops.silu_mul(y) if name == "gu" else y
         if x.shape[0] >= self.PROMPT_UNPACK_ROWS:
-            return lw[packed].prompt(self._norm(x, self._ones))
+            return lw[packed].prompt(self._norm(x, self._ones) if h is None else h)
         return self._rows_normed(lw[packed], x)     # gate_up: SiLU*up fused in the epilogue
+
+    def _add_then_norm(self, lw, name, y, res, ln):
+        """res += y in place and, where the next _normed_proj(name) normalises
+        the whole rows first, that norm in the same launch (add_rmsnorm: one
+        pass over the residual instead of an add and a norm kernel, 2 x 64 MB
+        less traffic per layer at 8192 rows).  Returns those rows or None."""
+        packed, plain = {"qkv": ("pqkv", "wqkv"), "gu": ("pgu", "wgu")}[name]
+        rows = res.shape[0]
+        if self.native and plain in lw and rows > 64:
+            return ops.add_rmsnorm(y, res, ln, self.cfg.eps)
+        if self.native and rows >= self.PROMPT_UNPACK_ROWS:
+            return ops.add_rmsnorm(y, res, self._ones, self.cfg.eps)
+        res.add_(y)
+        return None
 
     def _prefill_impl_norm_fused(self, bufs: dict, b: int):
         cfg, w = self.cfg, self.w
         res = torch.index_select(w.embed, 0, bufs["ids"])
+        h = None
         for li, lw in enumerate(w.layers):
-            q, k, v = self._prefill_qk(li, lw, self._normed_proj(lw, "qkv", res, lw["ln1"]), bufs["pos"], b)
-            res = res + self._proj(lw, "o", self._prefill_attention(q, k, v, bufs["mask"]))
-            res = res + self._proj(lw, "d", self._normed_proj(lw, "gu", res, lw["ln2"]))
+            qkv = self._normed_proj(lw, "qkv", res, lw["ln1"], h)
+            q, k, v = self._prefill_qk(li, lw, qkv, bufs["pos"], b)
+            o = self._proj(lw, "o", self._prefill_attention(q, k, v, bufs["mask"]))
+            h = self._add_then_norm(lw, "gu", o, res, lw["ln2"])
+            d = self._proj(lw, "d", self._normed_proj(lw, "gu", res, lw["ln2"], h))
+            if li + 1 < len(w.layers):
+                nxt = w.layers[li + 1]
+                h = self._add_then_norm(nxt, "qkv", d, res, nxt["ln1"])
+            else:
+                res.add_(d)
         last = torch.index_select(res, 0, bufs["last"])
         logits = self._rows(self.p_lm, self._norm(last, w.final_norm))
         torch.argmax(logits, dim=-1, out=self.tokens[b:b + 1])

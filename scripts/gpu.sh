@@ -275,5 +275,16 @@ case $suite in
     cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
     step 200 prof rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof" -o run -- \
       python3 -m k8s_vgpu_scheduler_amd.bench.prefill --iters 10 ;;
+  pf8k)
+    # prefill numerics, 8k TTFT with / without the kept plain down weight, and where the
+    # 8192-token prefill's time goes: per-kernel totals over 3 graph replays
+    step 600 tests python -u -m pytest tests/test_serving_gpu.py tests/test_ops_gpu.py tests/test_prefill_canary_gpu.py \
+      -v --timeout 120 --timeout-method thread -k "prefill or decoder or rope"
+    step 300 ttft8k python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 --ctx 9216 --iters 5
+    MIVGPU_KEEP_PLAIN_DOWN=0 step 300 ttft8k_nodown python -u -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 \
+      --ctx 9216 --iters 5
+    cd /tmp && export TMPDIR=/tmp PYTHONPATH=$R
+    step 300 prof rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof" -o run -- \
+      python3 -m k8s_vgpu_scheduler_amd.bench.prefill --len 8192 --ctx 9216 --iters 3 ;;
   *) echo "unknown suite $suite"; exit 2 ;;
 esac
