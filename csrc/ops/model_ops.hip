@@ -369,6 +369,40 @@ qk_norm_rope_kv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict_
     x1[t] = bf2f(src[l + 64]);
     p[t] = pos[b];
   }
+  if constexpr (PACKED && TPW == 8) {
+    // V head, eight consecutive positions from a multiple of 8 (a prompt):
+    // they are the eight keys of one 16-byte run per dim of the packed group,
+    // so each lane stores its two dims' runs whole (2 stores, not 16 2-byte)
+    bool run = h >= Hq + Hkv && cache_b >= 0 && b0 + TPW <= rows && (p[0] & 7) == 0 && p[0] >= 0 &&
+               p[0] + TPW <= max_ctx;
+#pragma unroll
+    for (int t = 1; t < TPW; ++t) run = run && p[t] == p[0] + t;
+    if (run) {
+      const int hv = h - Hq - Hkv;
+      if (v_plain) {
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          bf16_t* dst = v_plain + ((size_t)hv * rows + b0 + t) * D;
+          dst[l] = f2bf(x0[t]);  // bf16 -> fp32 -> bf16 is exact
+          dst[l + 64] = f2bf(x1[t]);
+        }
+      }
+      bf16_t* grp = v_cache + ((size_t)cache_b * Hkv + hv) * (size_t)max_ctx * D + (size_t)(p[0] >> 5) * (32 * D);
+      const int kq = (p[0] & 31) >> 3;
+      uint4 r0, r1;
+      r0.x = (uint32_t)f2bf(x0[0]) | ((uint32_t)f2bf(x0[1]) << 16);
+      r0.y = (uint32_t)f2bf(x0[2]) | ((uint32_t)f2bf(x0[3]) << 16);
+      r0.z = (uint32_t)f2bf(x0[4]) | ((uint32_t)f2bf(x0[5]) << 16);
+      r0.w = (uint32_t)f2bf(x0[6]) | ((uint32_t)f2bf(x0[7]) << 16);
+      r1.x = (uint32_t)f2bf(x1[0]) | ((uint32_t)f2bf(x1[1]) << 16);
+      r1.y = (uint32_t)f2bf(x1[2]) | ((uint32_t)f2bf(x1[3]) << 16);
+      r1.z = (uint32_t)f2bf(x1[4]) | ((uint32_t)f2bf(x1[5]) << 16);
+      r1.w = (uint32_t)f2bf(x1[6]) | ((uint32_t)f2bf(x1[7]) << 16);
+      *(uint4*)(grp + (((l >> 4) * 4 + kq) * 16 + (l & 15)) * 8) = r0;
+      *(uint4*)(grp + ((((l + 64) >> 4) * 4 + kq) * 16 + (l & 15)) * 8) = r1;
+      return;
+    }
+  }
   // inv_freq = theta^(-2l/D)
   const float inv_freq = exp2f(-(2.0f * (float)l / (float)D) * log2f(theta));
 #pragma unroll
