@@ -345,7 +345,8 @@ __device__ __forceinline__ void qk_one(const bf16_t* __restrict__ qkv_row, float
   dst[l + 64] = f2bf(o1);
 }
 
-// grid = (ceil(rows / TPW), Hq + 2*Hkv), one wave of 64 lanes.
+// grid = (ceil(rows / TPW), Hq + 2*Hkv), one wave of 64 lanes.  (Four
+// head-waves per workgroup measured the same: 99.3 vs 99.6 us at 8192 rows.)
 template <bool PACKED, int TPW>
 __global__ void __launch_bounds__(64)
 qk_norm_rope_kv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ qw,
