@@ -216,14 +216,27 @@ typedef struct {
  * owes GPU work (OWES: split the time nobody has waves resident) and its core
  * limit (the weight of its fair share).  The owner
  * reads them in its pass; a process without a fresh entry is judged from its
- * occupancy alone (one CU unit = a gate).  A tenant that lies here only moves
- * its own charge or drops another process to the occupancy-only rule: the
- * shares themselves stay in the owner-written board. */
+ * occupancy alone (one CU unit = a gate).
+ *
+ * Production (a node sampler): every container has a flags
+ * directory of its OWN -- host <dir>/flags/<pod uid>_<container>/, mounted
+ * read-write at MIVGPU_BOARD_FLAGS_DIR -- and the monitor writes, next to the
+ * node limits, <dir>/gpu-<id>.owners: which container each host pid belongs
+ * to (host truth).  The node sampler reads a pid's flags only from the file
+ * of the container that owns it, so a tenant cannot publish entries for a
+ * neighbour's pid or fill the slots its neighbours publish in; a pid's
+ * weight is the node-written limit whenever the monitor wrote one.  The node
+ * sampler never creates, truncates or follows a symlink to any file under a
+ * tenant-writable directory.  Without a node sampler (hand-run slices, the
+ * bench) the tenants share <dir>/flags/gpu-<id>.flags as before.
+ * GATED: the tenant's governor gated this device within the last second --
+ * the node sampler runs its fast passes only while some tenant is gated. */
 #define MIVGPU_FLAGS_MAGIC 0x4D495646u /* 'MIVF' */
 #define MIVGPU_FLAGS_VERSION 2
 #define MIVGPU_FLAGS_SLOTS 256
 #define MIVGPU_FLAG_HELD 1
 #define MIVGPU_FLAG_OWES 2
+#define MIVGPU_FLAG_GATED 4
 
 typedef struct {
   int32_t pid;        /* KFD pid, 0 = free                                   */
@@ -247,9 +260,16 @@ typedef struct {
  * the read-only board mount.  The monitor writes, every feedback pass, the
  * core limit of each host pid it attributes to a granted container on the GPU
  * (grant files x the pod's processes, host truth); the owner pass weighs a
- * process with min(this, its flags' limit), so a tenant cannot raise its fair
- * share by publishing a larger limit.  Written under a private name and
- * renamed into place. */
+ * process with this limit whenever there is one (its flags' limit only
+ * otherwise), so a tenant cannot move its own or a neighbour's fair share by
+ * publishing a limit.  Written under a private name and renamed into place.
+ *
+ * Owners (text, next to it): <dir>/gpu-<kfd gpu_id>.owners --
+ *   "MIVGPU-OWNERS 1 <gpu_id>\n" then "<host pid> <pod uid>_<container>\n"
+ * per process host truth attributes; the key names the container's flags
+ * directory <dir>/flags/<key>/ (characters [A-Za-z0-9_.-], at most 127). */
+#define MIVGPU_OWNERS_MAX 1024
+#define MIVGPU_OWNER_KEY_MAX 128
 #define MIVGPU_LIMITS_MAGIC 0x4D49564Cu /* 'MIVL' */
 #define MIVGPU_LIMITS_VERSION 1
 #define MIVGPU_LIMITS_MAX 1024

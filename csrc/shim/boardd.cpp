@@ -109,7 +109,7 @@ void rescan(const char* kfd, std::vector<Gpu>& gpus) {
 int main(int argc, char** argv) {
   const char* dir = nullptr;
   const char* kfd = "/sys/class/kfd/kfd";
-  uint64_t period_ns = 2000000, idle_ns = 20000000, max_passes = 0;
+  uint64_t period_ns = 2000000, idle_ns = 20000000, dormant_ns = 100000000, max_passes = 0;
   int split = mivgpu_board::kSplitRatio;
   for (int i = 1; i < argc; ++i) {
     const char* a = argv[i];
@@ -118,11 +118,12 @@ int main(int argc, char** argv) {
     else if (!strcmp(a, "--kfd-sysfs") && v) { kfd = v; ++i; }
     else if (!strcmp(a, "--period-us") && v) { period_ns = strtoull(v, nullptr, 10) * 1000ull; ++i; }
     else if (!strcmp(a, "--idle-period-us") && v) { idle_ns = strtoull(v, nullptr, 10) * 1000ull; ++i; }
+    else if (!strcmp(a, "--dormant-period-us") && v) { dormant_ns = strtoull(v, nullptr, 10) * 1000ull; ++i; }
     else if (!strcmp(a, "--passes") && v) { max_passes = strtoull(v, nullptr, 10); ++i; }
     else if (!strcmp(a, "--split") && v) { split = !strcmp(v, "equal") ? mivgpu_board::kSplitEqual : split; ++i; }
     else if (!strcmp(a, "--exit-with-parent")) { prctl(PR_SET_PDEATHSIG, SIGTERM); }
     else {
-      fprintf(stderr, "usage: %s --dir DIR [--kfd-sysfs PATH] [--period-us N] [--idle-period-us N] [--passes N] "
+      fprintf(stderr, "usage: %s --dir DIR [--kfd-sysfs PATH] [--period-us N] [--idle-period-us N] [--dormant-period-us N] [--passes N] "
               "[--split ratio|equal] [--exit-with-parent]\n", argv[0]);
       return 2;
     }
@@ -133,6 +134,7 @@ int main(int argc, char** argv) {
   }
   if (period_ns < 200000) period_ns = 200000;
   if (idle_ns < period_ns) idle_ns = period_ns;
+  if (dormant_ns < idle_ns) dormant_ns = idle_ns;
   signal(SIGTERM, on_signal);
   signal(SIGINT, on_signal);
   std::vector<Gpu> gpus;
@@ -144,6 +146,7 @@ int main(int argc, char** argv) {
       continue;
     }
     g.h.owner = true;   // the node sampler owns unconditionally; shims yield to a live one
+    g.h.node = true;    // tenant files: read only, never created, never through a symlink
     gpus.push_back(std::move(g));
   }
   if (gpus.empty()) {
@@ -160,7 +163,13 @@ int main(int argc, char** argv) {
       list_ns = now;
       rescan(kfd, gpus);
     }
-    const bool fast = wave_ns && now - wave_ns < 1000000000ull;
+    // fast passes only while a governed tenant asks for them (GATED flags
+    // within the last second) and waves are resident; dormant without one:
+    // CU-masked tenants are never charged from the board
+    bool demand = false;
+    for (const Gpu& g : gpus) demand |= g.h.demand_ns && now - g.h.demand_ns < 1000000000ull;
+    const bool fast = demand && wave_ns && now - wave_ns < 1000000000ull;
+    const uint64_t wait_ns = fast ? period_ns : (demand ? idle_ns : dormant_ns);
     for (Gpu& g : gpus) {
       const uint64_t t0 = mono_ns();
       g.rd.clear();
@@ -169,11 +178,11 @@ int main(int argc, char** argv) {
         g.rd.push_back(mivgpu_board::Reading{kv.first, v});
         if (v > mivgpu_board::kGateUnits) wave_ns = t0;
       }
-      mivgpu_board::owner_pass(g.h, g.rd.data(), (int)g.rd.size(), t0, fast ? period_ns : idle_ns,
-                               MIVGPU_BOARD_OWNER_NODE, self, split, mono_ns() - t0);
+      mivgpu_board::owner_pass(g.h, g.rd.data(), (int)g.rd.size(), t0, wait_ns, MIVGPU_BOARD_OWNER_NODE, self,
+                               split, mono_ns() - t0);
     }
     if (max_passes && ++passes >= max_passes) break;
-    const uint64_t sleep_ns = fast ? period_ns : idle_ns;
+    const uint64_t sleep_ns = wait_ns;
     timespec ts{(time_t)(sleep_ns / 1000000000ull), (long)(sleep_ns % 1000000000ull)};
     nanosleep(&ts, nullptr);
   }

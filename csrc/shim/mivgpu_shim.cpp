@@ -483,6 +483,7 @@ struct Config {
   // "none" = off).  Default /tmp/mivgpu-board, or off when KFD sysfs is
   // redirected (tests: a fake KFD must not meet a real GPU's board).
   char board_dir[256] = "/tmp/mivgpu-board";
+  char board_flags_dir[256] = "";   // this container's own flags directory ("" = <board_dir>/flags)
   // MIVGPU_BOARD_SPLIT=equal (A/B): a board owner splits each pass equally
   // among the processes with waves resident instead of by their waves
   int board_split = 0;
@@ -631,7 +632,7 @@ bool is_grant_key(const char* key) {
                                       "MIVGPU_OCCUPANCY", "MIVGPU_OCC_PERIOD_US", "MIVGPU_GATE_INTERVAL_US",
                                       "MIVGPU_GATE_BURST_US", "MIVGPU_SHARE_TAU_MS", "GPU_MAX_HW_QUEUES",
                                       "MIVGPU_GATE_MAX_HOLD_US", "MIVGPU_CONTROL_FILE", "MIVGPU_BOARD_DIR",
-                                      "MIVGPU_FAIR_LAG_PCT"};
+                                      "MIVGPU_BOARD_FLAGS_DIR", "MIVGPU_FAIR_LAG_PCT"};
   for (const char* k : kKeys)
     if (!strcmp(key, k)) return true;
   return !strncmp(key, "HIP_DEVICE_MEMORY_LIMIT_", 24) || !strncmp(key, "HIP_DEVICE_CORE_LIMIT_", 22);
@@ -716,6 +717,8 @@ void load_config() {
   }
   const char* bd = grant_env("MIVGPU_BOARD_DIR");
   if (bd) snprintf(g_cfg.board_dir, sizeof(g_cfg.board_dir), "%s", strcmp(bd, "none") ? bd : "");
+  const char* bfd = grant_env("MIVGPU_BOARD_FLAGS_DIR");
+  if (bfd && *bfd) snprintf(g_cfg.board_flags_dir, sizeof(g_cfg.board_flags_dir), "%s", bfd);
   const char* bs = unguarded_env("MIVGPU_BOARD_SPLIT");
   g_cfg.board_split = bs && !strcmp(bs, "equal") ? mivgpu_board::kSplitEqual : mivgpu_board::kSplitRatio;
   const char* gt = getenv("MIVGPU_GATE_TRACE");
@@ -1889,6 +1892,7 @@ double board_step(OccDev& o, uint64_t now, int own_raw, bool gating, int flags, 
     if (o.board_open_ns && now - o.board_open_ns < 1000000000ull) return -1;
     o.board_open_ns = now;
     if (!mb::open_board(o.board, g_cfg.board_dir, o.gpu_id, true)) return -1;
+    snprintf(o.board.flags_dir, sizeof(o.board.flags_dir), "%s", g_cfg.board_flags_dir);
     mlog(3, "KFD gpu %d: share board %s/gpu-%d.board mapped %s", o.gpu_id, g_cfg.board_dir, o.gpu_id,
          o.board.writable ? "read-write" : "read-only");
   }
@@ -1924,7 +1928,11 @@ double board_step(OccDev& o, uint64_t now, int own_raw, bool gating, int flags, 
     __atomic_store_n(&b->want_fast_ns, now, __ATOMIC_RELAXED);
   }
   mb::View v;
-  if (!mb::read_slot(b, self, &o.board_hint, &v) || v.beat_ns + kBoardStaleNs < now) {
+  // stale: older than 50 ms, or than three of the owner's own passes (a node
+  // sampler with no governed tenant runs dormant, 100 ms apart)
+  const bool got = mb::read_slot(b, self, &o.board_hint, &v);
+  const uint64_t stale_ns = v.period_ns && 3 * v.period_ns > kBoardStaleNs ? 3 * v.period_ns : kBoardStaleNs;
+  if (!got || v.beat_ns + stale_ns < now) {
     o.board_prev_ok = false;
     o.board_view.lead_ns = -1;
     return -1;
@@ -2057,7 +2065,10 @@ bool occ_sample(int dev, uint64_t now) {
   // the GPU's share board: publish this pass's state (held / owing), run the
   // owner pass if this process holds the role, read this process's share
   const bool gating = coarse_ns() - g_last_gate_ns[dev].load(std::memory_order_relaxed) < 1000000000ull;
-  const int flags = (holding > 0 ? MIVGPU_FLAG_HELD : 0) | ((pending || own > 0) && holding == 0 ? MIVGPU_FLAG_OWES : 0);
+  // GATED: the node sampler runs its fast passes only while some tenant is
+  // governed (a CU-masked tenant never gates: sampling for it is pure cost)
+  const int flags = (holding > 0 ? MIVGPU_FLAG_HELD : 0) |
+                    ((pending || own > 0) && holding == 0 ? MIVGPU_FLAG_OWES : 0) | (gating ? MIVGPU_FLAG_GATED : 0);
   const uint64_t lim_ppm = cu_limit_ppm_of(dev);
   const double board_f = board_step(o, now, own_raw, gating, flags,
                                     lim_ppm > 0 && lim_ppm < 1000000 ? (uint32_t)lim_ppm : 0u);

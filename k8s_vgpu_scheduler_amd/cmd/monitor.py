@@ -64,6 +64,9 @@ def main(argv=None):
     ap.add_argument("--board-period-us", type=int, default=2000,
                     help="the node share-board sampler's period while any GPU has waves resident "
                          "(mivgpu-boardd: one wave-occupancy sampler per GPU for every tenant; 0 = off)")
+    ap.add_argument("--state-file", default=os.environ.get("MIVGPU_MONITOR_STATE", ""),
+                    help="write each feedback pass's host-truth state (uuid -> KFD gpu_id map and how it matched, "
+                         "host pids per pod, vram per pid, grants, verdicts, escalation counters) to this JSON file")
     ap.add_argument("-v", type=int, default=2)
     a = ap.parse_args(argv)
     setup_logging(a.v)
@@ -96,7 +99,7 @@ def main(argv=None):
                                      shimless_action=a.shimless_action)
     reg = CollectorRegistry()
     reg.register(MonitorCollector(lister, backend, a.node_name, occupancy=occ, legacy=a.legacy_metrics,
-                                  truth=truth, escalation=escalation))
+                                  truth=truth, escalation=escalation, board=board))
     host, _, port = a.metrics_bind_address.rpartition(":")
     start_http_server(int(port), addr=host or "0.0.0.0", registry=reg)
     stop = threading.Event()
@@ -104,7 +107,8 @@ def main(argv=None):
     threading.Thread(target=watch_partition_lock, args=(pause, stop), name="partition-lock", daemon=True).start()
     try:
         watch_and_feedback(lister, stop, pause=pause, truth=truth, escalation=escalation,
-                           board_dir=board.dir if board is not None else None)
+                           board_dir=board.dir if board is not None else None, state_file=a.state_file or None,
+                           board=board)
     finally:
         if board is not None:
             board.stop()

@@ -129,14 +129,20 @@ def pick(used_bitmap: int, n: int, topo: CUTopology) -> list[tuple[int, int]] | 
 # limit is the request's share of the GPU, below the mask's width, so the
 # shim time-slices it: mivgpu_shim.cpp gate_wanted).  The quarters still
 # isolate the pairs from each other spatially.  Round 5 makes the unit the
-# whole GPU by default (AMDConfig.cu_share_unit = 256): 8 pooled slices ran at
+# whole GPU by default (AMDConfig.cu_share_unit = WHOLE_GPU): 8 pooled slices ran at
 # native (8889 vs 8887 tok/s, fairness 0.996) against 8502 on disjoint ranges;
 # device.py falls back to a disjoint range where no pool range is free.
 
 
+WHOLE_GPU = -1     # cuShareUnit: the whole device, whatever its CU count
+
+
 def share_unit(topo: CUTopology, cus: int = 0) -> int:
     """CUs of one shared range: ``cus`` rounded down to whole granules (at
-    least one, at most the GPU), or a quarter of the GPU when 0."""
+    least one, at most the GPU), the whole GPU when negative (``WHOLE_GPU``)
+    or at least the GPU's CU count, a quarter of the GPU when 0."""
+    if cus < 0 or cus >= topo.total:
+        return topo.total
     if cus > 0:
         return max(topo.xcds, min(topo.total, cus // topo.xcds * topo.xcds))
     return max(topo.xcds, topo.total // 4 // topo.xcds * topo.xcds)

@@ -91,10 +91,13 @@ class AMDConfig:
     # (profiles/README.md section 40): pooled 8891 tok/s vs native 8875
     # (fairness 0.996) against disjoint 32-CU ranges 8502 (-4.5 %).
     cu_share_small: bool = True
-    # CUs of one shared range for cuShareSmall (0 = a quarter of the GPU; 256 =
-    # every small request on the GPU shares one range, time-sliced by the
-    # governor, while requests of a share unit or more keep ranges of their own)
-    cu_share_unit: int = 256
+    # CUs of one shared range for cuShareSmall (0 = a quarter of the GPU; -1,
+    # the default, or any value >= the GPU's CUs = the whole GPU, whatever its
+    # CU count: every small request on the GPU shares one range, time-sliced
+    # by the governor, while requests of a quarter or more keep ranges of
+    # their own).  ADVICE r5: the literal 256 clamped to 256 CUs on a larger
+    # part, so the pool got a CU mask and lost its governor and host truth.
+    cu_share_unit: int = -1
     # False: no CU partitions at all -- a gpucores request is charged its
     # granules as before, but the container gets no HSA_CU_MASK and the shim's
     # temporal governor holds it to that charge (the reference's time-sharing

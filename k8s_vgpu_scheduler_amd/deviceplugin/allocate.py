@@ -48,7 +48,8 @@ import uuid as _uuid
 from dataclasses import dataclass, field
 
 from k8s_vgpu_scheduler_amd.device.codec import format_ranges, ranges_count
-from k8s_vgpu_scheduler_amd.monitor.board import CONTAINER_BOARD_DIR, board_host_dir
+from k8s_vgpu_scheduler_amd.monitor.board import (CONTAINER_BOARD_DIR, CONTAINER_FLAGS_DIR, board_host_dir,
+                                                  container_flags_dir)
 from k8s_vgpu_scheduler_amd.monitor.control import CONTAINER_CONTROL_PATH, control_host_path
 from k8s_vgpu_scheduler_amd.monitor.control import create as create_control
 
@@ -60,7 +61,7 @@ GRANT_KEYS = ("HIP_DEVICE_MEMORY_LIMIT", "HIP_DEVICE_CORE_LIMIT", "HSA_CU_MASK",
               "ROCR_VISIBLE_DEVICES", "MIVGPU_ACCOUNT_CONTEXT", "MIVGPU_KFD_SYSFS", "MIVGPU_OCCUPANCY",
               "MIVGPU_OCC_PERIOD_US", "MIVGPU_GATE_INTERVAL_US", "MIVGPU_GATE_BURST_US", "MIVGPU_SHARE_TAU_MS",
               "MIVGPU_DISABLE_CONTROL", "GPU_MAX_HW_QUEUES", "MIVGPU_GATE_MAX_HOLD_US", "MIVGPU_CONTROL_FILE",
-              "MIVGPU_BOARD_DIR", "MIVGPU_FAIR_LAG_PCT")
+              "MIVGPU_BOARD_DIR", "MIVGPU_BOARD_FLAGS_DIR", "MIVGPU_FAIR_LAG_PCT")
 # per-device forms of grant keys (HIP_DEVICE_MEMORY_LIMIT_<i>, HIP_DEVICE_CORE_LIMIT_<i>)
 GRANT_PREFIXES = ("HIP_DEVICE_MEMORY_LIMIT_", "HIP_DEVICE_CORE_LIMIT_")
 
@@ -177,6 +178,8 @@ def container_env(devreq: list, gpus: dict, cfg: PluginConfig, cache_file: str) 
     env["MIVGPU_CONTROL_FILE"] = CONTAINER_CONTROL_PATH
     # the GPU's share board, written by the node sampler only (read-only mount)
     env["MIVGPU_BOARD_DIR"] = CONTAINER_BOARD_DIR
+    # this container's own flags directory (not shared with its neighbours)
+    env["MIVGPU_BOARD_FLAGS_DIR"] = CONTAINER_FLAGS_DIR
     env["MIVGPU_DEVICE_UUIDS"] = ",".join(d.uuid for d in devreq)
     if cfg.device_memory_scaling > 1:
         env["MIVGPU_OVERSUBSCRIBE"] = "true"
@@ -217,9 +220,11 @@ def allocate_container(pod: dict, ctr: dict, devreq: list, gpus: dict, cfg: Plug
         os.chmod(tmp, 0o444)
         os.replace(tmp, limits)
         create_control(control)
-        os.makedirs(os.path.join(board_host_dir(hook), "flags"), exist_ok=True)
+        fdir = container_flags_dir(board_host_dir(hook), f"{uid}_{ctr.get('name', '')}")
+        shutil.rmtree(fdir, ignore_errors=True)
+        os.makedirs(fdir, exist_ok=True)
         try:
-            os.chmod(os.path.join(board_host_dir(hook), "flags"), 0o777)
+            os.chmod(fdir, 0o777)       # the container's uid is not known here
         except OSError:
             pass
     mounts = [
@@ -228,8 +233,11 @@ def allocate_container(pod: dict, ctr: dict, devreq: list, gpus: dict, cfg: Plug
         {"container_path": LIMITS_PATH, "host_path": limits, "read_only": True},
         {"container_path": CONTAINER_CONTROL_PATH, "host_path": control, "read_only": True},
         {"container_path": CONTAINER_BOARD_DIR, "host_path": board_host_dir(hook), "read_only": True},
-        # the tenants' held / owing flags: the one writable part of the board
-        {"container_path": f"{CONTAINER_BOARD_DIR}/flags", "host_path": f"{board_host_dir(hook)}/flags",
+        # this container's held / owing flags: the one board file it writes,
+        # in a directory of its own (the node sampler reads a pid's flags only
+        # from the directory of the container host truth attributes it to)
+        {"container_path": CONTAINER_FLAGS_DIR,
+         "host_path": container_flags_dir(board_host_dir(hook), f"{uid}_{ctr.get('name', '')}"),
          "read_only": False},
     ]
     # the pod-spec opt-out drops the preload -- only where opting out is allowed

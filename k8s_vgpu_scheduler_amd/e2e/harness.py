@@ -191,7 +191,7 @@ def container_env(alloc: dict, base: dict | None = None) -> dict:
     env = dict(base if base is not None else os.environ)
     env.update(alloc["envs"])
     mounts = alloc["mounts"]
-    for k in ("MIVGPU_SHARED_CACHE", "MIVGPU_CONTROL_FILE", "MIVGPU_BOARD_DIR"):
+    for k in ("MIVGPU_SHARED_CACHE", "MIVGPU_CONTROL_FILE", "MIVGPU_BOARD_DIR", "MIVGPU_BOARD_FLAGS_DIR"):
         if k in env:
             env[k] = host_path(env[k], mounts)
     from k8s_vgpu_scheduler_amd.deviceplugin.allocate import LIMITS_PATH, grant_text, parse_grant
@@ -200,7 +200,7 @@ def container_env(alloc: dict, base: dict | None = None) -> dict:
         # the shim reads the grant from the read-only mount; on the host the
         # same file (with its region path mapped) is named by MIVGPU_LIMITS_FILE
         g = parse_grant(Path(grant["host_path"]).read_text())
-        for k in ("MIVGPU_SHARED_CACHE", "MIVGPU_CONTROL_FILE", "MIVGPU_BOARD_DIR"):
+        for k in ("MIVGPU_SHARED_CACHE", "MIVGPU_CONTROL_FILE", "MIVGPU_BOARD_DIR", "MIVGPU_BOARD_FLAGS_DIR"):
             if k in g:
                 g[k] = host_path(g[k], mounts)
         hp = Path(grant["host_path"] + ".host")
@@ -235,7 +235,7 @@ class E2ECluster:
         env = dict(os.environ)
         env.update({"PYTHONPATH": str(REPO) + os.pathsep + env.get("PYTHONPATH", ""),
                     "MIVGPU_FAKE_GPUS": str(self.fake_gpus), "NODE_NAME": self.node,
-                    "HAMI_RESYNC_INTERVAL": "1"})
+                    "HAMI_RESYNC_INTERVAL": "1s"})
         env.update(self.extra_env)
         logf = open(self.dir / f"{name}.log", "w")
         self.procs[name] = subprocess.Popen([sys.executable, "-m", f"k8s_vgpu_scheduler_amd.cmd.{name}", *args],
@@ -267,7 +267,7 @@ class E2ECluster:
             self._spawn("monitor", [*kc, "--node-name", self.node, "--hook-path", str(self.hook),
                                     "--metrics-bind-address", f"127.0.0.1:{self.ports['mon_metrics']}",
                                     "--smi-backend", self.smi_backend, "-v", str(self.log_level),
-                                    *self.monitor_args])
+                                    "--state-file", str(self.dir / "monitor_state.json"), *self.monitor_args])
             wait_for(lambda: requests.get(self.url("/healthz"), timeout=2).ok, 60, "scheduler /healthz")
             wait_for(lambda: self.kubelet.registrations, 60, "device plugin registration with the kubelet")
             wait_for(lambda: "hami.io/node-amd-register" in
@@ -305,6 +305,14 @@ class E2ECluster:
 
     def logs(self, name: str) -> str:
         return (self.dir / f"{name}.log").read_text(errors="replace")
+
+    def monitor_state(self) -> dict:
+        """The monitor's last feedback pass (``--state-file``): host truth's
+        uuid -> gpu_id map, pids per pod, vram per pid, verdicts, counters."""
+        try:
+            return json.loads((self.dir / "monitor_state.json").read_text())
+        except (OSError, ValueError):
+            return {}
 
     def alive(self) -> dict:
         return {k: p.poll() for k, p in self.procs.items()}

@@ -16,9 +16,14 @@ server.go:853-864); here ONE owner per GPU reads every process's
 * production: the monitor runs ``mivgpu-boardd`` (``BoardSampler``) on
   ``$HOOK_PATH/vgpu/board``, which the device plugin mounts READ-ONLY into
   every vGPU container (``deviceplugin/allocate.py``) -- no tenant can write
-  the share it is charged -- with one read-write subdirectory, ``flags/``,
-  where each tenant's shim publishes whether it is held in its governor gate,
-  whether it owes work and its core limit (the owner's pass reads them);
+  the share it is charged -- and one read-write flags directory per
+  container (``flags/<pod uid>_<container>/``, mounted at
+  ``MIVGPU_BOARD_FLAGS_DIR`` in that container only) where its shim publishes
+  whether it is held in its governor gate, whether it owes work, whether it
+  gates at all and its core limit; the owner reads a pid's flags only from
+  the directory of the container host truth attributes it to
+  (``gpu-<id>.owners``, written by the monitor) and weighs it with the
+  node-written limit (``gpu-<id>.limits``) -- ADVICE r5;
 * without a node sampler (hand-run slices, the bench), a shim that governs
   the GPU takes the owner role with ``flock`` on ``gpu-<id>.owner``.
 
@@ -65,7 +70,7 @@ assert C.sizeof(BoardSlot) == 64 and BOARD_SIZE == 128 + 64 * BOARD_SLOTS
 FLAGS_MAGIC = 0x4D495646
 FLAGS_VERSION = 2
 FLAGS_SLOTS = 256
-FLAG_HELD, FLAG_OWES = 1, 2
+FLAG_HELD, FLAG_OWES, FLAG_GATED = 1, 2, 4
 
 
 class Flag(C.Structure):
@@ -97,8 +102,8 @@ class FlagsFile:
     """The tenant-written flags of one GPU mapped read-write (tests stand in
     for tenants with it; the owner reads it in its pass)."""
 
-    def __init__(self, board_dir: str, gpu_id: int, create: bool = True):
-        p = flags_path(board_dir, gpu_id)
+    def __init__(self, board_dir: str, gpu_id: int, create: bool = True, flags_dir: str | None = None):
+        p = Path(flags_dir) / f"gpu-{gpu_id}.flags" if flags_dir else flags_path(board_dir, gpu_id)
         if create and not p.exists():
             p.parent.mkdir(parents=True, exist_ok=True)
             f = Flags()
@@ -144,8 +149,8 @@ def limits_path(board_dir: str, gpu_id: int) -> Path:
 
 def write_limits(board_dir: str, gpu_id: int, limits: dict[int, int]) -> Path:
     """The node-written core limits of one GPU (``mivgpu_board_limits_t``):
-    ``{host pid: limit ppm}``; the owner pass weighs each process with the
-    smaller of this and its flags' limit.  Written under a private name and
+    ``{host pid: limit ppm}``; the owner pass weighs each process with this
+    limit whenever there is one (its flags' limit is ignored then).  Written under a private name and
     renamed into place (the owner re-reads it every 100 ms)."""
     import struct
     items = sorted((int(p), int(v)) for p, v in limits.items() if p > 0 and 0 < v < 1_000_000)[:LIMITS_MAX]
@@ -157,6 +162,43 @@ def write_limits(board_dir: str, gpu_id: int, limits: dict[int, int]) -> Path:
     os.chmod(tmp, 0o644)
     os.replace(tmp, path)
     return path
+
+
+def owners_path(board_dir: str, gpu_id: int) -> Path:
+    return Path(board_dir) / f"gpu-{gpu_id}.owners"
+
+
+_KEY_OK = set("abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789_.-")
+
+
+def valid_key(key: str) -> bool:
+    """A container key (``<pod uid>_<container>``) as the node sampler
+    accepts it (board.h ``valid_key``)."""
+    return 0 < len(key) < 128 and key not in (".", "..") and set(key) <= _KEY_OK
+
+
+def write_owners(board_dir: str, gpu_id: int, owners: dict[int, str]) -> Path:
+    """Host truth's ``{host pid: container key}`` of one GPU
+    (``<dir>/gpu-<id>.owners``): the node sampler reads a pid's flags only
+    from ``<dir>/flags/<key>/``, so no tenant can speak for a neighbour
+    (ADVICE r5).  Written under a private name and renamed into place."""
+    lines = [f"MIVGPU-OWNERS 1 {gpu_id}"]
+    lines += [f"{int(p)} {k}" for p, k in sorted(owners.items()) if int(p) > 0 and valid_key(k)][:1024]
+    path = owners_path(board_dir, gpu_id)
+    tmp = path.with_name(f".{path.name}.{os.getpid()}")
+    tmp.write_text("\n".join(lines) + "\n")
+    os.chmod(tmp, 0o644)
+    os.replace(tmp, path)
+    return path
+
+
+def container_flags_dir(board_dir: str, key: str) -> str:
+    """The host directory of one container's flags (mounted read-write at
+    ``CONTAINER_FLAGS_DIR`` in that container only)."""
+    return os.path.join(board_dir, "flags", key)
+
+
+CONTAINER_FLAGS_DIR = "/var/run/mivgpu/board-flags"    # the grant's MIVGPU_BOARD_FLAGS_DIR
 
 
 def board_host_dir(hook_path: str) -> str:
@@ -249,8 +291,12 @@ class BoardSampler:
             return self
         os.makedirs(os.path.join(self.dir, "flags"), exist_ok=True)
         try:
-            os.chmod(self.dir, 0o755)     # containers read it through a read-only mount ...
-            os.chmod(os.path.join(self.dir, "flags"), 0o777)   # ... and write their flags in this one
+            # containers read the board through a read-only mount, and write
+            # their flags only in their own flags/<key>/ (deviceplugin/
+            # allocate.py); no tenant can create, replace or unlink anything
+            # the root sampler opens here
+            os.chmod(self.dir, 0o755)
+            os.chmod(os.path.join(self.dir, "flags"), 0o755)
         except OSError:
             pass
         self.proc = subprocess.Popen([self.binary, "--dir", self.dir, "--kfd-sysfs", self.kfd, *self.args,
@@ -260,6 +306,29 @@ class BoardSampler:
 
     def alive(self) -> bool:
         return self.proc is not None and self.proc.poll() is None
+
+    def ensure(self, now: float | None = None) -> bool:
+        """Restart the sampler if it exited (no tenant can take
+        the owner role over a read-only board, so a dead sampler would leave
+        every tenant on its own local estimate).  Backs off 1 s, 2 s, ... up
+        to 60 s between attempts; returns whether a sampler runs now."""
+        if self.alive():
+            self._backoff = 0.0
+            return True
+        if self.proc is None and not self.available():
+            return False
+        t = time.monotonic() if now is None else now
+        if t < getattr(self, "_next_try", 0.0):
+            return False
+        rc = self.proc.poll() if self.proc is not None else None
+        self.restarts = getattr(self, "restarts", 0) + 1
+        self._backoff = min(60.0, max(1.0, 2 * getattr(self, "_backoff", 0.0)))
+        self._next_try = t + self._backoff
+        log.warning("share-board sampler exited (rc %s): restarting (attempt %d, next retry in %.0f s)",
+                    rc, self.restarts, self._backoff)
+        self.proc = None
+        self.start()
+        return self.alive()
 
     def stop(self):
         if self.proc is not None and self.proc.poll() is None:

@@ -236,10 +236,11 @@ def feedback_pass(lister: ContainerLister, truth=None, escalation=None, lease_s:
     if truth is not None:
         verdicts = truth.enforce(lister, grants, lister.pod)
         if board_dir and os.path.isdir(board_dir):
-            from .board import write_limits
+            from .board import write_limits, write_owners
             for gid, w in getattr(truth, "weights", {}).items():
                 try:
                     write_limits(board_dir, gid, w)
+                    write_owners(board_dir, gid, getattr(truth, "owners", {}).get(gid, {}))
                 except OSError as e:
                     log.warning("share board limits for gpu %d: %s", gid, e)
     over = {k for k, v in verdicts.items() if v.over}
@@ -253,14 +254,50 @@ def feedback_pass(lister: ContainerLister, truth=None, escalation=None, lease_s:
 
 def watch_and_feedback(lister: ContainerLister, stop: threading.Event, period: float = 5.0,
                        pause: threading.Event | None = None, truth=None, escalation=None,
-                       board_dir: str | None = None):
+                       board_dir: str | None = None, state_file: str | None = None, board=None):
     """The 5 s loop; skipped while ``pause`` is set (a compute-partition apply
     is in progress, cmd/vGPUmonitor/main.go:79-109).  The control-file lease
-    covers four periods, so a paused or dead monitor releases its verdicts."""
+    covers four periods, so a paused or dead monitor releases its verdicts.
+    ``state_file``: each pass's host-truth state as JSON (``write_state``)."""
+    n = 0
     while not stop.wait(period):
         if pause is not None and pause.is_set():
             continue
+        n += 1
+        res = None
+        if board is not None:
+            board.ensure()      # the node's share-board sampler (monitor/board.py), restarted if it died
         try:
-            feedback_pass(lister, truth, escalation, lease_s=max(DEFAULT_LEASE_S, 4 * period), board_dir=board_dir)
+            res = feedback_pass(lister, truth, escalation, lease_s=max(DEFAULT_LEASE_S, 4 * period),
+                                board_dir=board_dir)
         except Exception:  # noqa: BLE001
             log.exception("feedback iteration failed")
+        if state_file:
+            write_state(state_file, n, res, truth, escalation)
+
+
+def write_state(path: str, n: int, res: dict | None, truth=None, escalation=None):
+    """Atomically replace ``path`` with this pass's state as JSON (the
+    monitor's ``--state-file``: what host truth saw and decided, readable
+    by an operator or a failed e2e test)."""
+    import json
+    import time as _t
+
+    st = {"pass": n, "time": _t.time(), "ok": res is not None}
+    if res is not None:
+        st["no_shim"] = sorted("/".join(k) for k in res.get("no_shim", ()))
+        st["over"] = sorted("/".join(k) for k in res.get("over", ()))
+        st["actions"] = [[str(x) for x in a] for a in res.get("actions", ())]
+    if truth is not None and hasattr(truth, "debug_state"):
+        st["host_truth"] = truth.debug_state()
+    if escalation is not None:
+        st["escalation"] = {"shimless": {"/".join(k): v for k, v in escalation.shimless.items()},
+                            "over": {"/".join(k): v for k, v in escalation.count.items()},
+                            "evicted": sorted(escalation.evicted), "actions": dict(escalation.actions)}
+    tmp = f"{path}.{os.getpid()}.tmp"
+    try:
+        with open(tmp, "w") as f:
+            json.dump(st, f, default=str)
+        os.replace(tmp, path)
+    except OSError as e:
+        log.debug("state file %s: %s", path, e)

@@ -181,6 +181,9 @@ class HostTruth:
         # KFD gpu_id -> {host pid: core limit ppm} of the processes attributed
         # to a limited container (the share boards' node-written limits)
         self.weights: dict[int, dict[int, int]] = {}
+        # KFD gpu_id -> {host pid: container key} (the share boards' owners)
+        self.owners: dict[int, dict[int, str]] = {}
+        self._pass: dict = {}
 
     # ------------------------------------------------------------ sources
     def vram(self, host_pid: int, gpu_id: int) -> int:
@@ -210,7 +213,8 @@ class HostTruth:
         if grants is None:
             grants = load_grants(lister.base.parent / "limits")
         regions = {f"{c.pod_uid}_{c.container}": c for c in lister.list_containers()}
-        ids = self.gpu_ids() or {}
+        ensure = getattr(self.gpu_ids, "ensure", None)
+        ids = (ensure({u for g in grants.values() for u in g.uuids}) if ensure is not None else self.gpu_ids()) or {}
         pods = self._pids_by_pod({g.pod_uid for g in grants.values()})
         # (pod, uuid) -> [(grant, device index)]
         users: dict[tuple, list] = {}
@@ -220,6 +224,8 @@ class HostTruth:
                     users.setdefault((g.pod_uid, u), []).append((g, i))
         verdicts: dict[tuple, Verdict] = {}
         weights: dict[int, dict[int, int]] = {gid: {} for gid in ids.values()}
+        seen_vram: dict[str, dict[int, int]] = {}
+        owners: dict[int, dict[int, str]] = {gid: {} for gid in ids.values()}
 
         def verdict(g: Grant) -> Verdict:
             v = verdicts.get((g.pod_uid, g.container))
@@ -234,6 +240,7 @@ class HostTruth:
             before = {g.key: self._dev_used(regions.get(g.key), i) for g, i in lst}
             pids = set(pods.get(uid, []))
             per_pid = {hp: self.vram(hp, gid) for hp in pids}
+            seen_vram[f"{uid}/{gid}"] = per_pid
             pod_total = sum(per_pid.values())
             after = {g.key: self._dev_used(regions.get(g.key), i) for g, i in lst}
             attributed = 0
@@ -251,6 +258,8 @@ class HostTruth:
                 charged.append((g, i, c, live, t, own))
             grant_sum = 0
             for g, i, c, live, t, own in charged:
+                for p in own:
+                    owners.setdefault(gid, {})[p] = g.key
                 ppm = g.core_ppm[i] if i < len(g.core_ppm) else 0
                 if ppm:
                     w = weights.setdefault(gid, {})
@@ -324,6 +333,9 @@ class HostTruth:
             self.over = {k for k, v in verdicts.items() if v.over}
             self.no_shim = {k for k, v in verdicts.items() if not v.shim_loaded}
             self.weights = weights
+            self.owners = owners
+            self._pass = {"ids": dict(ids), "pod_pids": {u: sorted(p) for u, p in pods.items()},
+                          "vram": seen_vram, "regions": sorted(regions)}
             # an event again once the condition cleared and came back
             self._reported = {r for r in self._reported
                               if (r[0] == OVER_GRANT_REASON and (r[1], r[2]) in self.over)
@@ -365,22 +377,120 @@ class HostTruth:
             return {"truth": dict(self.truth), "over": set(self.over), "no_shim": set(self.no_shim),
                     "verdicts": dict(self.verdicts), "grants": dict(self.grants)}
 
+    def debug_state(self) -> dict:
+        """The last pass as JSON-able data: the uuid -> gpu_id map (and how
+        each uuid was matched, with both tables), the host pids found per
+        pod, ``vram_<gid>`` per pid, every grant's ``governed``/``core_ppm``
+        and every verdict's flags -- what a failed e2e run must show
+        (VERDICT r5 item 1)."""
+        with self._mu:
+            p = dict(self._pass)
+            out = {"ids": p.get("ids", {}), "pod_pids": p.get("pod_pids", {}),
+                   "vram": {k: {str(pid): b for pid, b in v.items()} for k, v in p.get("vram", {}).items()},
+                   "regions": p.get("regions", []),
+                   "grants": {k: {"uuids": g.uuids, "mem": g.mem, "governed": g.governed, "core_ppm": g.core_ppm}
+                              for k, g in self.grants.items()},
+                   "verdicts": {f"{u}_{c}": {"truth": v.truth, "over": v.over, "shim_loaded": v.shim_loaded,
+                                             "no_live_shim": v.no_live_shim, "ungoverned": v.ungoverned,
+                                             "pids": v.pids, "excess": v.excess}
+                                for (u, c), v in self.verdicts.items()}}
+        how = getattr(self.gpu_ids, "how", None)
+        if how is not None:
+            out["matched_by"] = dict(how)
+            out["tables"] = getattr(self.gpu_ids, "tables", {})
+        return out
 
-def kfd_gpu_ids(backend, kfd_root: Path | str = KFD_ROOT) -> Callable[[], dict]:
-    """``{uuid: gpu_id}`` of the node's GPUs (by PCI location, like the
-    occupancy sampler), refreshed when a uuid is missing."""
-    from .occupancy import gpu_ids_by_bdf
 
-    cache: dict = {}
+class GpuIdMap:
+    """``{device uuid: KFD gpu_id}`` of the node's GPUs.
 
-    def get() -> dict:
-        if not cache and backend is not None:
-            by_bdf = gpu_ids_by_bdf(Path(kfd_root))
-            for g in backend.gpus():
-                if g.bdf in by_bdf:
-                    cache[g.uuid] = by_bdf[g.bdf]
-        return cache
-    return get
+    Round 5's map matched amd-smi's BDF string against the one built from the
+    KFD node's ``domain``/``location_id`` only, and cached the first result:
+    a miss left the uuid unmapped for good, and host truth silently issued no
+    verdict for it.  Each uuid is now resolved by the
+    first source that answers:
+
+    1. the backend's own KFD id for the device (amd-smi
+       ``amdsmi_get_gpu_kfd_info`` ``kfd_id``) when KFD has a node with it;
+    2. the PCI location, both sides normalised (case, missing domain);
+    3. the KFD node whose ``unique_id`` names the uuid (``GPU-%016x``, the
+       form the backends register, smi/__init__.py ``_rocr_id_from_kfd``);
+    4. one backend GPU and one KFD GPU node: the same device.
+
+    A uuid asked for but unmapped triggers a rebuild (at most every
+    ``retry_s``) and one warning that lists both tables, so a record says
+    which side disagreed."""
+
+    def __init__(self, backend, kfd_root: Path | str = KFD_ROOT, retry_s: float = 10.0):
+        self.backend = backend
+        self.kfd_root = Path(kfd_root)
+        self.retry_s = retry_s
+        self.map: dict[str, int] = {}
+        self.how: dict[str, str] = {}
+        self.tables: dict = {"backend": [], "kfd": []}
+        self._built = -1e18
+        self._warned: set[str] = set()
+
+    def __call__(self) -> dict:
+        if not self.map:
+            self.refresh()
+        return self.map
+
+    def refresh(self) -> dict:
+        import time
+
+        from .occupancy import kfd_gpu_nodes, norm_bdf
+
+        now = time.monotonic()
+        if now - self._built < self.retry_s and self.map:
+            return self.map
+        self._built = now
+        nodes = kfd_gpu_nodes(self.kfd_root)
+        try:
+            gpus = list(self.backend.gpus()) if self.backend is not None else []
+        except Exception as e:  # noqa: BLE001 -- a transient amd-smi failure: retried next pass
+            log.warning("host truth: listing the backend's GPUs failed: %s", e)
+            gpus = []
+        by_uuid = {n["uuid"].lower(): n["gpu_id"] for n in nodes if n["uuid"]}
+        by_bdf = {n["bdf"]: n["gpu_id"] for n in nodes if n["bdf"]}
+        gids = {n["gpu_id"] for n in nodes}
+        out, how = {}, {}
+        for g in gpus:
+            kid = (getattr(g, "extra", None) or {}).get("gpu_id")
+            try:
+                kid = int(kid) if kid is not None else None
+            except (TypeError, ValueError):
+                kid = None
+            if kid in gids:
+                out[g.uuid], how[g.uuid] = kid, "backend_kfd_id"
+            elif norm_bdf(getattr(g, "bdf", "")) in by_bdf:
+                out[g.uuid], how[g.uuid] = by_bdf[norm_bdf(g.bdf)], "bdf"
+            elif str(g.uuid).lower() in by_uuid:
+                out[g.uuid], how[g.uuid] = by_uuid[str(g.uuid).lower()], "unique_id"
+        if not out and len(gpus) == 1 and len(nodes) == 1:
+            out[gpus[0].uuid], how[gpus[0].uuid] = nodes[0]["gpu_id"], "single_gpu"
+        self.map, self.how = out, how
+        self.tables = {"backend": [{"uuid": g.uuid, "bdf": getattr(g, "bdf", ""),
+                                    "kfd_id": (getattr(g, "extra", None) or {}).get("gpu_id")} for g in gpus],
+                       "kfd": nodes}
+        return out
+
+    def ensure(self, uuids) -> dict:
+        """The map, rebuilt when one of ``uuids`` is missing from it."""
+        missing = [u for u in uuids if u not in self.map]
+        if missing:
+            self.refresh()
+            for u in missing:
+                if u not in self.map and u not in self._warned:
+                    self._warned.add(u)
+                    log.warning("host truth: granted device %s matches no KFD GPU node, no verdict for it: "
+                                "backend %s, KFD %s", u, self.tables["backend"], self.tables["kfd"])
+        return self.map
+
+
+def kfd_gpu_ids(backend, kfd_root: Path | str = KFD_ROOT) -> GpuIdMap:
+    """``{uuid: gpu_id}`` of the node's GPUs (``GpuIdMap``)."""
+    return GpuIdMap(backend, kfd_root)
 
 
 def single_gpu_ids(uuid: str, kfd_root: Path | str = KFD_ROOT) -> dict:

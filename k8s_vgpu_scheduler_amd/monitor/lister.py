@@ -110,6 +110,8 @@ class ContainerLister:
                             f.unlink()
                         except OSError:
                             pass
+                    # its share-board flags directory (deviceplugin/allocate.py)
+                    shutil.rmtree(self.base.parent / "board" / "flags" / d.name, ignore_errors=True)
                 continue
             with self._mu:
                 known = d.name in self.containers

@@ -19,7 +19,7 @@ import time
 
 from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily
 
-from .occupancy import gpu_ids_by_bdf
+from .occupancy import gpu_ids_by_bdf, norm_bdf
 
 CTR_LABELS = ["namespace", "pod", "container", "vdevice_index", "device_uuid"]
 LEGACY_CTR_LABELS = ["podnamespace", "podname", "ctrname", "vdeviceid", "deviceuuid"]
@@ -28,8 +28,9 @@ LEGACY_HOST_LABELS = ["nodeid", "deviceidx", "deviceuuid", "devicetype"]
 
 class MonitorCollector:
     def __init__(self, lister, backend=None, node_name: str = "", occupancy=None, legacy: bool = False,
-                 truth=None, escalation=None):
+                 truth=None, escalation=None, board=None):
         self.lister = lister
+        self.board = board        # monitor.board.BoardSampler (the node share-board sampler) or None
         self.truth = truth        # monitor.hosttruth.HostTruth (host-truth HBM usage) or None
         self.escalation = escalation   # monitor.escalate.OverGrantPolicy or None
         self.backend = backend
@@ -38,8 +39,19 @@ class MonitorCollector:
         self.legacy = legacy
         self._gpu_ids: dict[str, int] | None = None
 
-    def _gpu_id(self, bdf: str) -> int | None:
-        if self.occ is None or not bdf:
+    def _gpu_id(self, g) -> int | None:
+        """The KFD gpu_id of backend GPU ``g``: host truth's uuid map when the
+        monitor runs one (KFD unique_id first, hosttruth.GpuIdMap), else the
+        normalised PCI location."""
+        if self.occ is None or g is None:
+            return None
+        m = getattr(self.truth, "gpu_ids", None) if self.truth is not None else None
+        if m is not None and hasattr(m, "ensure"):
+            gid = m.ensure([g.uuid]).get(g.uuid)
+            if gid is not None:
+                return gid
+        bdf = norm_bdf(getattr(g, "bdf", ""))
+        if not bdf:
             return None
         if self._gpu_ids is None or bdf not in self._gpu_ids:
             self._gpu_ids = gpu_ids_by_bdf(self.occ.root)
@@ -62,7 +74,7 @@ class MonitorCollector:
         if self.backend is not None:
             for g in self.backend.gpus():
                 gpus[g.uuid] = g
-                gid = self._gpu_id(g.bdf)
+                gid = self._gpu_id(g)
                 n = self.occ.active_tenants(gid) if gid is not None else None
                 if n is not None:
                     tenants.add_metric([self.node, str(g.index), g.uuid], float(n))
@@ -216,6 +228,14 @@ class MonitorCollector:
                 if a != "block":
                     acts.add_metric([self.node, a], float(n))
             yield acts
+        if self.board is not None:
+            up = GaugeMetricFamily("mivgpu_board_sampler_up",
+                                   "1 while the node share-board sampler (mivgpu-boardd) runs", labels=["node"])
+            up.add_metric([self.node], 1.0 if self.board.alive() else 0.0)
+            rs = CounterMetricFamily("mivgpu_board_sampler_restarts", "Times the monitor restarted mivgpu-boardd",
+                                     labels=["node"])
+            rs.add_metric([self.node], float(getattr(self.board, "restarts", 0)))
+            yield from (up, rs)
         if self.legacy:
             yield from (l_used, l_limit, l_desc, l_cutil, l_lastk)
 
@@ -226,7 +246,7 @@ class MonitorCollector:
         procs = r.active_procs()
         if any(p.util[i].share_ns for p in procs):
             return float(min(100, sum(p.util[i].util_pct for p in procs)))
-        gid = self._gpu_id(g.bdf) if g is not None else None
+        gid = self._gpu_id(g)
         pids = [p.hostpid for p in procs if p.hostpid > 0]
         if gid is None or not pids:
             return 0.0

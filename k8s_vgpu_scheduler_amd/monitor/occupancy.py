@@ -43,10 +43,12 @@ def _props(path: Path) -> dict:
     return out
 
 
-def gpu_ids_by_bdf(root: Path = KFD_ROOT) -> dict[str, int]:
-    """``{"0000:75:00.0": gpu_id}`` for every GPU node of the KFD topology."""
-    out = {}
-    nodes = root / "topology" / "nodes"
+def kfd_gpu_nodes(root: Path = KFD_ROOT) -> list[dict]:
+    """Every GPU node of the KFD topology: ``{"node", "gpu_id", "bdf",
+    "uuid"}`` (``uuid`` is ``GPU-<unique_id as 16 hex digits>``, the form the
+    backends register, smi/__init__.py ``_rocr_id_from_kfd``; "" without one)."""
+    out = []
+    nodes = Path(root) / "topology" / "nodes"
     try:
         entries = sorted(nodes.iterdir(), key=lambda p: int(p.name) if p.name.isdigit() else -1)
     except OSError:
@@ -60,11 +62,31 @@ def gpu_ids_by_bdf(root: Path = KFD_ROOT) -> dict[str, int]:
             continue
         p = _props(n / "properties")
         loc, dom = p.get("location_id"), p.get("domain", 0)
-        if loc is None:
-            continue
-        bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7:x}"
-        out[bdf] = gid
+        bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7:x}" if loc is not None else ""
+        uid = p.get("unique_id")
+        out.append({"node": int(n.name) if n.name.isdigit() else -1, "gpu_id": gid, "bdf": bdf,
+                    "uuid": f"GPU-{uid:016x}" if uid else ""})
     return out
+
+
+def norm_bdf(bdf: str) -> str:
+    """``0000:A4:00.0`` / ``a4:00.0`` -> ``0000:a4:00.0`` (amd-smi and sysfs
+    spell the same function differently on some stacks)."""
+    s = str(bdf or "").strip().lower()
+    if not s:
+        return ""
+    if s.count(":") == 1:
+        s = "0000:" + s
+    dom, _, rest = s.partition(":")
+    try:
+        return f"{int(dom, 16):04x}:{rest}"
+    except ValueError:
+        return s
+
+
+def gpu_ids_by_bdf(root: Path = KFD_ROOT) -> dict[str, int]:
+    """``{"0000:75:00.0": gpu_id}`` for every GPU node of the KFD topology."""
+    return {n["bdf"]: n["gpu_id"] for n in kfd_gpu_nodes(root) if n["bdf"]}
 
 
 def read_occupancy(root: Path = KFD_ROOT) -> dict[int, dict[int, int]]:

@@ -98,3 +98,26 @@ def test_unbalanced_mask_detected():
     assert not A.is_balanced([(0, 3)], topo)      # XCDs 0..3 only
     assert not A.is_balanced([], topo)
     assert A.is_balanced([(0, 7)], topo)
+
+
+def test_whole_gpu_share_unit_on_a_304_cu_part():
+    """cuShareUnit's default means the whole GPU, not 256 CUs.  On
+    a 304-CU part the pool range covers every CU, so the device plugin emits
+    no HSA_CU_MASK for a pooled pod: the shim's governor time-slices it, and
+    host truth treats a shimless one as ungoverned."""
+    from k8s_vgpu_scheduler_amd.deviceplugin.allocate import PluginConfig, container_env
+    from k8s_vgpu_scheduler_amd.device.amd.device import AMDConfig
+    from k8s_vgpu_scheduler_amd.device.types import ContainerDevice
+    from k8s_vgpu_scheduler_amd.smi import GPUInfo
+    topo = A.CUTopology(total=304, xcds=8)
+    assert AMDConfig().cu_share_unit == A.WHOLE_GPU
+    assert A.share_unit(topo, A.WHOLE_GPU) == 304 and A.share_unit(topo, 512) == 304
+    assert A.share_unit(A.CUTopology(), A.WHOLE_GPU) == 256
+    assert A.share_unit(topo, 0) == 72 and A.share_unit(topo, 64) == 64
+    r = A.pick_shared(0, {}, 32, topo, A.WHOLE_GPU)
+    assert A.bitmap_from_ranges(r) == (1 << 304) - 1
+    g = GPUInfo(index=0, uuid="GPU-x", rocr_id="GPU-x", name="MI355X", memory_mib=294912, cus=304)
+    d = ContainerDevice(idx=0, uuid="GPU-x", type="AMD", usedmem=8192, usedcores=32,
+                        custominfo={"cu_ranges": r})
+    env = container_env([d], {"GPU-x": g}, PluginConfig(hook_path="/tmp/none"), "/tmp/none/x.cache")
+    assert "HSA_CU_MASK" not in env and env["HIP_DEVICE_CORE_LIMIT"]

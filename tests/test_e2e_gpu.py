@@ -234,10 +234,15 @@ def test_shimless_container_on_time_shared_gpu_is_evicted(tmp_path_factory):
                          "the monitor to evict the shimless pod")
             except TimeoutError:
                 host = samples(cl.metrics("mon_metrics"), "hami_host_gpu_memory_used_bytes")
-                pytest.fail(f"not evicted (host pid {hp}, host truth {host}); monitor log:\n"
-                            + cl.logs("monitor")[-4000:])
+                held = {f: open(f"{kfd_proc}/{hp}/{f}").read().strip()
+                        for f in os.listdir(f"{kfd_proc}/{hp}") if f.startswith("vram_")}
+                pytest.fail(f"not evicted (host pid {hp} holds {held}, amd-smi {host}); monitor state:\n"
+                            + json.dumps(cl.monitor_state(), default=str)[-6000:] + "\nmonitor log:\n"
+                            + cl.logs("monitor")[-3000:])
             took = time.monotonic() - seen
-            print(json.dumps({"evicted_after_s": round(took, 1), "since_start_s": round(time.monotonic() - t0, 1)}))
+            st = cl.monitor_state().get("host_truth", {})
+            print(json.dumps({"evicted_after_s": round(took, 1), "since_start_s": round(time.monotonic() - t0, 1),
+                              "matched_by": st.get("matched_by"), "ids": st.get("ids")}))
             # the first pass after the GPU open, then at most 3 more 5 s passes
             assert took <= 4 * 5 + 3, took
             assert "VGPUShimlessEvicted" in cl.logs("monitor") or "without libmivgpu.so" in cl.logs("monitor")

@@ -374,3 +374,145 @@ def test_feedback_writes_the_share_boards_node_limits(tmp_path):
     magic, ver, gid, n = struct.unpack_from("<IiiI", raw)
     assert (magic, ver, gid, n) == (B.LIMITS_MAGIC, B.LIMITS_VERSION, 42, 1)
     assert struct.unpack_from("<iI", raw, 16) == (4711, 125000)
+    # and which container each of those pids belongs to (the owner reads a
+    # pid's flags only from that container's directory)
+    assert B.owners_path(str(bd), 42).read_text().splitlines() == ["MIVGPU-OWNERS 1 42", "4711 u1_main"]
+
+
+# ---------------------------------------------------------------- GPU id map
+def _kfd_node(root, node, gid, loc=None, dom=0, unique=None):
+    d = root / "topology" / "nodes" / str(node)
+    d.mkdir(parents=True, exist_ok=True)
+    (d / "gpu_id").write_text(f"{gid}\n")
+    props = [f"simd_count {0 if not gid else 1024}"]
+    if loc is not None:
+        props += [f"location_id {loc}", f"domain {dom}"]
+    if unique is not None:
+        props.append(f"unique_id {unique}")
+    (d / "properties").write_text("\n".join(props) + "\n")
+
+
+class _G:
+    def __init__(self, uuid, bdf="", kfd_id=None):
+        self.uuid, self.bdf, self.extra = uuid, bdf, {"gpu_id": kfd_id}
+
+
+class _B:
+    def __init__(self, gpus):
+        self._g = gpus
+        self.calls = 0
+
+    def gpus(self):
+        self.calls += 1
+        return list(self._g)
+
+
+def test_gpu_id_map_sources(tmp_path):
+    """a fresh box whose amd-smi BDF did not match the
+    KFD node left the map empty and host truth silent.  Each uuid now maps by
+    amd-smi's own KFD id, else by the normalised BDF, else by the KFD
+    unique_id, else (one GPU each side) by elimination."""
+    from k8s_vgpu_scheduler_amd.monitor.hosttruth import GpuIdMap
+    kfd = tmp_path / "kfd"
+    _kfd_node(kfd, 0, 0)                                    # the CPU node
+    _kfd_node(kfd, 1, 1111, loc=0xa400, unique=0x3f037090857f9b8e)
+    _kfd_node(kfd, 2, 2222, loc=0xf100, dom=1, unique=0x22)
+    _kfd_node(kfd, 3, 3333, loc=0x0500, unique=0x33)
+    b = _B([_G("GPU-x", bdf="garbage", kfd_id=2222),       # amd-smi's kfd_id wins
+            _G("GPU-y", bdf="0001:F1:00.0"),                 # upper-case BDF, other domain: no kfd_id
+            _G("GPU-0000000000000033", bdf="")])             # only the unique_id answers
+    m = GpuIdMap(b, kfd)
+    assert m() == {"GPU-x": 2222, "GPU-y": 2222, "GPU-0000000000000033": 3333}
+    assert m.how == {"GPU-x": "backend_kfd_id", "GPU-y": "bdf", "GPU-0000000000000033": "unique_id"}
+    # a lone GPU whose identities all disagree: matched by elimination
+    one = tmp_path / "one"
+    _kfd_node(one, 0, 0)
+    _kfd_node(one, 1, 4444, loc=0x7500)
+    m1 = GpuIdMap(_B([_G("GPU-z", bdf="0000:76:00.0", kfd_id=9)]), one)
+    assert m1() == {"GPU-z": 4444} and m1.how == {"GPU-z": "single_gpu"}
+
+
+def test_gpu_id_map_rebuilds_for_a_missing_uuid_and_warns_once(tmp_path, caplog):
+    from k8s_vgpu_scheduler_amd.monitor.hosttruth import GpuIdMap
+    kfd = tmp_path / "kfd"
+    _kfd_node(kfd, 1, 1111, loc=0xa400)
+    _kfd_node(kfd, 2, 2222, loc=0xa500)
+    b = _B([_G("GPU-a", bdf="0000:a4:00.0")])
+    m = GpuIdMap(b, kfd, retry_s=0.0)
+    assert m() == {"GPU-a": 1111}
+    b._g.append(_G("GPU-b", bdf="0000:a5:00.0"))          # a GPU the first listing did not return
+    assert m.ensure({"GPU-a", "GPU-b"}) == {"GPU-a": 1111, "GPU-b": 2222}
+    with caplog.at_level("WARNING"):
+        m.ensure({"GPU-nope"})
+        m.ensure({"GPU-nope"})
+    warn = [r for r in caplog.records if "GPU-nope" in r.getMessage()]
+    assert len(warn) == 1 and "0000:a4:00.0" in warn[0].getMessage()
+
+
+def test_shimless_eviction_through_the_real_id_map_and_proc_table(tmp_path):
+    """The fresh-box shape of the GPU e2e test, on the CPU: a KFD tree whose
+    BDF does not match amd-smi's string, a /proc-like table naming the pod's
+    cgroup, the probe's VRAM in ``vram_<gid>``, no region.  The container is
+    evicted in the third pass and the state file says why."""
+    import json
+    from k8s_vgpu_scheduler_amd.monitor.hosttruth import GpuIdMap
+    kfd = tmp_path / "kfd"
+    _kfd_node(kfd, 0, 0)
+    _kfd_node(kfd, 1, 56525, loc=0xa400, unique=0x3f037090857f9b8e)
+    _kfd(kfd, 47662, 56525, 2 * GIB + 5)
+    procs = tmp_path / "proc"
+    (procs / "47662").mkdir(parents=True)
+    (procs / "47662" / "status").write_text("Name:\tpython\nNSpid:\t47662\t1234\n")
+    (procs / "47662" / "cgroup").write_text("0::/kubepods.slice/kubepods-burstable.slice/podu1/cri-rogue\n")
+    base = tmp_path / "hook"
+    d = base / "vgpu" / "limits"
+    d.mkdir(parents=True)
+    (d / "u1_main.conf").write_text("HIP_DEVICE_MEMORY_LIMIT_0=8192m\nHIP_DEVICE_CORE_LIMIT=12.5\n"
+                                    "MIVGPU_DEVICE_UUIDS=GPU-3f037090857f9b8e\n")
+    create(control_host_path(str(base), "u1", "main"))
+    cluster = FakeCluster()
+    cluster.create("pods", make_pod("rogue", uid="u1"))
+    lister = ContainerLister(str(base), lambda: cluster.list("pods"), resync_interval=3600)
+    b = _B([_G("GPU-3f037090857f9b8e", bdf="0000:A4:00.0 ")])
+    truth = HostTruth(GpuIdMap(b, kfd), kfd_root=kfd, proc_root=str(procs))
+    pol = OverGrantPolicy("block", passes=3, client=cluster)
+    st = tmp_path / "state.json"
+    acts = []
+    for n in range(1, 4):
+        res = feedback.feedback_pass(lister, truth, pol)
+        feedback.write_state(str(st), n, res, truth, pol)
+        acts.append(res["actions"])
+    assert acts[2] == [("evict", "u1", "main", "default/rogue")], (acts, json.loads(st.read_text()))
+    s = json.loads(st.read_text())["host_truth"]
+    assert s["ids"] == {"GPU-3f037090857f9b8e": 56525} and s["matched_by"]["GPU-3f037090857f9b8e"] == "bdf"
+    assert s["pod_pids"] == {"u1": [47662]} and s["vram"]["u1/56525"] == {"47662": 2 * GIB + 5}
+    assert s["grants"]["u1_main"]["governed"] == [True] and s["grants"]["u1_main"]["core_ppm"] == [125000]
+    v = s["verdicts"]["u1_main"]
+    assert v["no_live_shim"] and v["ungoverned"] and not v["shim_loaded"]
+
+
+def test_board_sampler_is_restarted_with_backoff(tmp_path):
+    """the monitor restarts a dead mivgpu-boardd and exports it."""
+    import stat
+    from k8s_vgpu_scheduler_amd.monitor.board import BoardSampler
+    fake = tmp_path / "boardd"
+    fake.write_text("#!/bin/sh\nexit 3\n")
+    fake.chmod(fake.stat().st_mode | stat.S_IEXEC)
+    kfd = tmp_path / "kfd"
+    (kfd / "proc").mkdir(parents=True)
+    s = BoardSampler(str(tmp_path / "board"), kfd_sysfs=str(kfd), binary=str(fake)).start()
+    s.proc.wait()
+    assert not s.alive()
+    s.ensure(now=1000.0)
+    assert s.restarts == 1
+    s.proc.wait()
+    s.ensure(now=1000.5)          # inside the 1 s backoff: no attempt
+    assert s.restarts == 1
+    s.ensure(now=1001.5)
+    assert s.restarts == 2 and s._backoff == 2.0
+    s.proc.wait()
+    reg = CollectorRegistry()
+    lister = ContainerLister(str(tmp_path), lambda: [], resync_interval=3600)
+    reg.register(MonitorCollector(lister, None, "n1", board=s))
+    text = generate_latest(reg).decode()
+    assert 'mivgpu_board_sampler_up{node="n1"} 0.0' in text and "mivgpu_board_sampler_restarts_total" in text

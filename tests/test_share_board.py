@@ -366,3 +366,116 @@ def test_faked_flags_of_an_idle_neighbour_do_not_subscribe_the_gpu(native_build,
     assert s[111].lead_ns == -1 and s[222].lead_ns == -1, (s[111].lead_ns, s[222].lead_ns)
     s = _fair_run(native_build, tmp_path / "held", {111: (10, B.FLAG_OWES, 250000), 222: (0, B.FLAG_HELD, 750000)})
     assert s[111].lead_ns == -1 and s[222].lead_ns == -1, (s[111].lead_ns, s[222].lead_ns)
+
+
+# ------------------------------------------------ the root sampler
+def test_node_sampler_never_writes_or_follows_tenant_files(native_build, tmp_path):
+    """mivgpu-boardd runs as root next to tenant-writable flags directories.
+    A tenant planting a symlink (to a file only root may change) or a FIFO
+    where the sampler looks for flags gets neither written nor followed, and
+    the sampler does not block; it creates nothing under the flags tree."""
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
+    _occ(kfd, 111, 4242, 10)
+    d = tmp_path / "board"
+    (d / "flags" / "podA_main").mkdir(parents=True)
+    victim = tmp_path / "victim"
+    victim.write_bytes(b"precious")
+    (d / "flags" / "gpu-4242.flags").symlink_to(victim)
+    (d / "flags" / "podA_main" / "gpu-4242.flags").symlink_to(victim)
+    os.mkfifo(d / "flags" / "podB_main")          # not a directory: skipped
+    (d / "flags" / "podC_main").mkdir()
+    os.mkfifo(d / "flags" / "podC_main" / "gpu-4242.flags")
+    before = sorted(str(p.relative_to(d)) for p in d.rglob("*"))
+    subprocess.run(_boardd(native_build, kfd, d, "--passes", "30"), check=True, timeout=30)
+    assert victim.read_bytes() == b"precious"
+    assert (d / "flags" / "gpu-4242.flags").is_symlink()
+    after = sorted(str(p.relative_to(d)) for p in d.rglob("*"))
+    assert [p for p in after if p.startswith("flags")] == [p for p in before if p.startswith("flags")]
+    b = B.Board(B.board_path(d, 4242))
+    s = b.slots()
+    b.close()
+    assert s[111].obs_ns > 0               # the pass ran, on occupancy alone
+
+
+def _keyed_run(native_build, tmp_path, tenants, forged, owners, seconds=0.4):
+    """boardd with one flags directory per container.  ``tenants``:
+    {pid: (key, occupancy, state, limit)}; ``forged``: [(key, pid, state,
+    limit)] written into that key's file for a pid it does not own;
+    ``owners``: {pid: key} (the monitor's host-truth map) or None."""
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
+    d = tmp_path / "board"
+    files = {}
+    for pid, (key, v, _, _) in tenants.items():
+        _occ(kfd, pid, 4242, v)
+        (d / "flags" / key).mkdir(parents=True, exist_ok=True)
+        files[key] = B.FlagsFile(str(d), 4242, flags_dir=str(d / "flags" / key))
+    if owners is not None:
+        B.write_owners(str(d), 4242, owners)
+    node = subprocess.Popen(_boardd(native_build, kfd, d))
+    try:
+        t_end = time.time() + seconds
+        while time.time() < t_end:
+            for key, pid, st, lim in forged:       # the forger writes first: the lower slot
+                files[key].publish(pid, st, lim)
+            for pid, (key, _, st, lim) in tenants.items():
+                files[key].publish(pid, st, lim)
+            time.sleep(0.005)
+        b = B.Board(B.board_path(d, 4242))
+        s = b.slots()
+        b.close()
+    finally:
+        node.terminate()
+        node.wait(timeout=10)
+        for f in files.values():
+            f.close()
+    return s
+
+
+def test_a_tenant_cannot_speak_for_its_neighbour(native_build, tmp_path):
+    """tenant A writes, in its own flags file, an entry for its
+    neighbour B's pid -- HELD while B runs small kernels, or a 10 % limit
+    while both fill the GPU at 50 % each.  With host truth's owners file the
+    node sampler reads B's state only from B's directory: B stays observed
+    and nobody leads.  Unattributed, A's word against B's counts for neither."""
+    ten = {111: ("podA_main", 10, B.FLAG_OWES, 500000), 222: ("podB_main", 1, B.FLAG_OWES, 500000)}
+    forged = [("podA_main", 222, B.FLAG_HELD, 500000)]
+    s = _keyed_run(native_build, tmp_path / "held", ten, forged, {111: "podA_main", 222: "podB_main"})
+    assert s[222].obs_ns > 0, s[222].obs_ns                  # B's own OWES: running, observed
+    s = _keyed_run(native_build, tmp_path / "conflict", ten, forged, None)
+    assert s[222].obs_ns == 0                               # no single source: the occupancy rule (a gate)
+    ten = {111: ("podA_main", 10, B.FLAG_OWES, 500000), 222: ("podB_main", 10, B.FLAG_OWES, 500000)}
+    forged = [("podA_main", 222, B.FLAG_OWES, 100000)]
+    s = _keyed_run(native_build, tmp_path / "weight", ten, forged, {111: "podA_main", 222: "podB_main"})
+    assert s[111].lead_ns >= 0 and max(s[111].lead_ns, s[222].lead_ns) < 2_000_000, (s[111].lead_ns,
+                                                                                      s[222].lead_ns)
+
+
+def test_node_sampler_is_dormant_until_a_tenant_gates(native_build, tmp_path):
+    """CU-masked tenants never gate, so sampling every
+    2 ms for them is pure cost.  The node sampler runs 100 ms passes until a
+    tenant's flags say GATED, then its fast period."""
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
+    _occ(kfd, 111, 4242, 10)
+    d = tmp_path / "board"
+    (d / "flags" / "podA_main").mkdir(parents=True)
+    fl = B.FlagsFile(str(d), 4242, flags_dir=str(d / "flags" / "podA_main"))
+    node = subprocess.Popen([str(native_build["boardd"]), "--dir", str(d), "--kfd-sysfs", str(kfd)])
+    try:
+        def period(state, secs=0.6):
+            t_end = time.time() + secs
+            while time.time() < t_end:
+                fl.publish(111, state, 250000)
+                time.sleep(0.005)
+            b = B.Board(B.board_path(d, 4242))
+            h = b.snapshot()
+            b.close()
+            return h.period_ns, h.passes
+        p0, n0 = period(B.FLAG_OWES)
+        p1, n1 = period(B.FLAG_OWES | B.FLAG_GATED)
+        p2, n2 = period(B.FLAG_OWES | B.FLAG_GATED)
+    finally:
+        node.terminate()
+        node.wait(timeout=10)
+        fl.close()
+    assert p0 == 100_000_000 and n0 <= 10, (p0, n0)
+    assert p1 == p2 == 2_000_000 and n2 - n1 > 100, (p1, p2, n1, n2)
