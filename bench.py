@@ -73,6 +73,24 @@ def native_rccl_check(rank: int, world: int, local_rank: int, barrier) -> dict:
     return out
 
 
+def gov_row(d: dict) -> dict:
+    """One slice's governor row, every field over the TIMED window (VERDICT r5
+    item 6: the instantaneous share sample disagreed with the integral):
+    GPU-time share received (the share integral), held ms and gates, the
+    sampler's fair-share samples and those held on the lead, and the share
+    board's passes; plus the lifetime totals (load + warmup + timed)."""
+    t = d.get("timed") or {}
+    return {"busy_share_pct": d.get("busy_share_pct"), "received_gpu_ms": d.get("received_gpu_ms"),
+            "held_ms": t.get("held_ms"), "gates": t.get("gates"), "fair_samples": t.get("fair_samples"),
+            "fair_held_samples": t.get("fair_held_samples"), "samples": t.get("samples"),
+            "board_passes": t.get("board_passes"), "board_fair_passes": t.get("board_fair_passes"),
+            "seconds": d.get("seconds"), "sampler": d.get("sampler"),
+            "lifetime": {"charged_ms": d.get("gov_charged_ms"), "held_ms": d.get("gov_held_ms"),
+                         "gates": d.get("gov_gates")},
+            "sampler_pass_us_mean": d.get("gov_sampler_pass_us_mean"),
+            "sampler_pass_us_max": d.get("gov_sampler_pass_us_max")}
+
+
 def _share_cus(cus: int) -> int:
     from k8s_vgpu_scheduler_amd.device.amd.cu_alloc import CUTopology, share_unit
     from k8s_vgpu_scheduler_amd.device.amd.device import AMDConfig
@@ -110,14 +128,22 @@ def main():
                     help="CUs of one shared range in the hybrid layout (0 = the allocator's cuShareUnit: a quarter)")
     ap.add_argument("--active-slices", type=int, default=0,
                     help="run only the first K of the --slices planned slices (same masks/limits; 0 = all)")
-    ap.add_argument("--monitor", type=float, default=0.0, metavar="SECONDS",
+    ap.add_argument("--monitor", type=float, default=5.0, metavar="SECONDS",
                     help="run the node monitor's feedback pass (priority + utilization_switch) over the shim "
-                         "rounds' regions every SECONDS while they run (0 = off)")
+                         "rounds' regions every SECONDS while they run, as production does (the reference's 5 s "
+                         "feedback period, cmd/vGPUmonitor/feedback.go:143; 0 = off)")
     ap.add_argument("--policy", default="default", choices=["default", "force", "disable"])
-    ap.add_argument("--board", default="auto", choices=["auto", "node", "shim"],
+    ap.add_argument("--board", default="auto", choices=["auto", "node", "shim", "off"],
                     help="owner of the GPU's share board in the shim rounds: the node sampler (mivgpu-boardd, "
                          "as the monitor runs it) or a governed slice's shim; auto = node on one GPU, shim with "
-                         "several ranks (one node sampler per rank would read every GPU's processes)")
+                         "several ranks (one node sampler per rank would read every GPU's processes); off = no "
+                         "board at all (A/B of the sampler's cost)")
+    ap.add_argument("--overhead-pairs", type=int, default=4,
+                    help="shim / masked-no-shim round pairs for shim_overhead_pct, interleaved ABBA (the first "
+                         "pair is the headline round and its bare twin; 1 = no extra rounds)")
+    ap.add_argument("--unequal-limits", default="75,25",
+                    help="core limits (%%) of the unequal temporal round (governor, policy force, no masks: the "
+                         "round that must throttle); empty = skip")
     ap.add_argument("--slice-limits", default="",
                     help="comma list of per-slice core limits (%%) for the shim and temporal rounds, e.g. 75,25 "
                          "(unequal tenants; default 100/N each)")
@@ -166,6 +192,8 @@ def main():
 
     def with_env(specs):
         for sp in specs:
+            if args.board == "off" and sp.shim:
+                sp.env["MIVGPU_BOARD_DIR"] = "none"
             sp.env.update(extra_env)
         return specs[:args.active_slices] if args.active_slices > 0 else specs
 
@@ -206,6 +234,18 @@ def main():
         wanted += ["governed_ref", "governed"]
     if args.eager_steps > 0 and args.mode == "all" and not args.rounds and not cpu:
         wanted += ["eager_shim", "eager_noshim"]
+    # a temporal round that must throttle: unequal limits
+    unequal = [float(x) for x in args.unequal_limits.split(",") if x.strip()]
+    if unequal and args.mode == "all" and not args.rounds and not cpu and args.slices > 1:
+        wanted += ["temporal_unequal"]
+    # extra shim / masked-no-shim pairs, interleaved ABBA after everything else
+    # (one 0.28 s sample must not swing the shim's cost)
+    pairs = []
+    if "shim" in wanted and "masked_noshim" in wanted and args.overhead_pairs > 1:
+        for k in range(1, args.overhead_pairs):
+            pair = [f"masked_noshim#{k}", f"shim#{k}"] if k % 2 else [f"shim#{k}", f"masked_noshim#{k}"]
+            pairs.append(pair)
+            wanted += pair
     gov_args = list(child_args)
     gov_args[gov_args.index("--steps") + 1] = str(max(args.gov_steps, args.steps))
     rounds = []
@@ -218,14 +258,13 @@ def main():
         gspec[0].core_pct = args.gov_limit
         rounds.append(("governed", spawn_round(with_env(gspec), phys, work / "gov", log_dir, gov_args,
                                                "governed")))
-    if "shim" in wanted:
-        rounds.append(("shim", spawn_round(
-            with_env(with_limits(plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib,
-                                             spatial=not args.no_spatial, policy=args.policy,
-                                             hw_queues=args.hw_queues or None, layout=args.layout,
-                                             share_unit=args.share_unit))),
-            phys, work, log_dir, child_args, "shim")))
-    if "masked_noshim" in wanted:
+    def shim_specs():
+        return with_env(with_limits(plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib,
+                                                spatial=not args.no_spatial, policy=args.policy,
+                                                hw_queues=args.hw_queues or None, layout=args.layout,
+                                                share_unit=args.share_unit)))
+
+    def bare_specs():
         # the same CU masks and queues without libmivgpu.so: what the shim
         # itself costs (the overhead vs native also contains the
         # partitioning's own benefit)
@@ -233,8 +272,17 @@ def main():
                            layout=args.layout, share_unit=args.share_unit)
         for sp in bare:
             sp.shim = False
-        rounds.append(("masked_noshim", spawn_round(with_env(bare), phys, work / "bare", log_dir, child_args,
-                                                    "masked_noshim")))
+        return with_env(bare)
+
+    for nm in wanted:
+        base = nm.split("#")[0]
+        sub = nm.replace("#", "_")
+        if base == "shim":
+            rounds.append((nm, spawn_round(shim_specs(), phys, work if nm == "shim" else work / sub, log_dir,
+                                           child_args, sub)))
+        elif base == "masked_noshim":
+            rounds.append((nm, spawn_round(bare_specs(), phys, work / ("bare" if nm == base else sub), log_dir,
+                                           child_args, sub)))
     if "temporal" in wanted:
         # the same slices time-shared by the governor gate instead of CU masks
         # (BASELINE config 3: "4 pods x 25% gpucores, CU-throttle governor kernel")
@@ -242,6 +290,15 @@ def main():
             with_env(with_limits(plan_slices(args.slices, shim=True, gpumem_mib=args.gpumem_mib, spatial=False,
                                              policy="force", hw_queues=args.hw_queues or None))),
             phys, work / "temporal", log_dir, child_args, "temporal")))
+    if "temporal_unequal" in wanted:
+        # unequal tenants time-shared by the governor: must throttle (each held
+        # to its limit's share of the GPU, not an equal split)
+        uspecs = plan_slices(len(unequal), shim=True, gpumem_mib=args.gpumem_mib, spatial=False, policy="force",
+                             hw_queues=args.hw_queues or None)
+        for sp, lim in zip(uspecs, unequal):
+            sp.core_pct = lim
+        rounds.append(("temporal_unequal", spawn_round(with_env(uspecs), phys, work / "unequal", log_dir,
+                                                       child_args, "temporal_unequal")))
     if "native" in wanted:
         rounds.append(("native", spawn_round(native_specs(args.hw_queues), phys, work, log_dir, child_args,
                                              "native")))
@@ -295,14 +352,14 @@ def main():
         if i and gap > 0 and not cpu:
             time.sleep(gap)
         mon = None
-        if args.monitor > 0 and name in ("shim", "temporal"):
+        if args.monitor > 0 and name.split("#")[0] in ("shim", "temporal", "temporal_unequal"):
             from k8s_vgpu_scheduler_amd.bench.slices import RoundMonitor
             mon = RoundMonitor([p.cache for p in procs], args.monitor).start()
         # the GPU's share board owned by the node sampler, as the monitor runs
         # it in production (--board shim: a governed slice takes the role)
         boardd = None
         bdir = next((p.board_dir for p in procs if getattr(p, "board_dir", None)), None)
-        if (args.board == "node" or (args.board == "auto" and world == 1)) and bdir and not cpu:
+        if (args.board == "node" or (args.board == "auto" and world == 1)) and bdir and bdir != "none" and not cpu:
             from k8s_vgpu_scheduler_amd.monitor.board import BoardSampler
             boardd = BoardSampler(bdir).start()
         try:
@@ -383,11 +440,8 @@ def main():
             "tpot_ms_p50_rank0": [round(d.get("tpot_ms_p50", 0), 3) for d in head["done"]],
             "tpot_ms_p99_rank0": [round(d.get("tpot_ms_p99", 0), 3) for d in head["done"]],
         }
-        if any("gov_gates" in d or "share_pct" in d for d in head["done"]):
-            out["governor_rank0"] = [{k: d.get(k) for k in ("gov_charged_ms", "gov_held_ms", "gov_gates",
-                                                            "share_pct", "util_pct", "busy_share_pct",
-                                                            "seconds", "sampler", "timed", "gov_sampler_pass_us_mean",
-                                                            "gov_sampler_pass_us_max")} for d in head["done"]]
+        if any("gov_gates" in d or "busy_share_pct" in d for d in head["done"]):
+            out["governor_rank0"] = [gov_row(d) for d in head["done"]]
         if "native" in results:
             out["native_value"] = round(results["native"]["tok_s"], 2)
         if "native" in results and "shim" in results:
@@ -398,7 +452,22 @@ def main():
         if "masked_noshim" in results and "shim" in results:
             bare = results["masked_noshim"]["tok_s"]
             out["masked_noshim_value"] = round(bare, 2)
-            out["shim_overhead_pct"] = round((1.0 - head["tok_s"] / bare) * 100.0, 2)
+            # every interleaved pair (the headline round and its bare twin first)
+            prs = [("shim", "masked_noshim")] + [(f"shim#{k}", f"masked_noshim#{k}")
+                                                 for k in range(1, args.overhead_pairs)]
+            prs = [(a, b) for a, b in prs if a in results and b in results]
+            per = [round((1.0 - results[a]["tok_s"] / results[b]["tok_s"]) * 100.0, 2) for a, b in prs]
+            ssum = sum(results[a]["tok_s"] for a, _ in prs)
+            bsum = sum(results[b]["tok_s"] for _, b in prs)
+            out["shim_overhead_pct"] = round((1.0 - ssum / bsum) * 100.0, 2)
+            out["shim_overhead"] = {
+                "what": "1 - shim / masked-no-shim aggregate tok/s, pooled over interleaved ABBA pairs",
+                "pairs": len(prs), "per_pair_pct": per,
+                "spread_pct": [min(per), max(per)] if per else None,
+                "shim_tok_s": [round(results[a]["tok_s"], 1) for a, _ in prs],
+                "masked_noshim_tok_s": [round(results[b]["tok_s"], 1) for _, b in prs],
+                "headline_pair_pct": per[0] if per else None,
+                "board": args.board, "monitor_period_s": args.monitor}
         if "temporal" in results:
             tr = results["temporal"]
             tps = [round(d["tok_s"], 1) for d in tr["done"]]
@@ -407,12 +476,24 @@ def main():
             out["temporal_fairness_min_over_max"] = round(min(tps) / max(tps), 3) if tps else None
             lims = sorted({pct_text(sp.core_pct) for sp in tr.get("specs", [])}) or ["?"]
             out["temporal_isolation"] = f"governor gate (force, {'/'.join(lims)} % each, occupancy-charged)"
-            out["temporal_governor_rank0"] = [{k: d.get(k) for k in ("gov_charged_ms", "gov_held_ms", "gov_gates",
-                                                                     "share_pct", "util_pct", "busy_share_pct",
-                                                                     "sampler", "timed", "gov_sampler_pass_us_mean",
-                                                                     "gov_sampler_pass_us_max")} for d in tr["done"]]
+            out["temporal_governor_rank0"] = [gov_row(d) for d in tr["done"]]
             if "native" in results:
                 out["temporal_overhead_pct"] = round((1.0 - tr["tok_s"] / results["native"]["tok_s"]) * 100.0, 2)
+        if "temporal_unequal" in results:
+            tu = results["temporal_unequal"]
+            tps = [d["tok_s"] for d in tu["done"]]
+            lims = [sp.core_pct for sp in tu.get("specs", [])]
+            out["temporal_unequal"] = {
+                "what": "governor gate, policy force, no CU masks, unequal core limits: must throttle",
+                "limits_pct": [pct_text(x) for x in lims],
+                "aggregate_tok_s": round(tu["tok_s"], 1),
+                "per_slice_tok_s": [round(x, 1) for x in tps],
+                "share_of_aggregate_pct": [round(100.0 * x / sum(tps), 1) for x in tps] if tps else None,
+                "gpu_share_pct": [d.get("busy_share_pct") for d in tu["done"]],
+                "held_ms": [(d.get("timed") or {}).get("held_ms") for d in tu["done"]],
+                "governor_rank0": [gov_row(d) for d in tu["done"]]}
+            if "native" in results:
+                out["temporal_unequal"]["fraction_of_native"] = round(tu["tok_s"] / results["native"]["tok_s"], 4)
         if "eager_shim" in results and "eager_noshim" in results:
             es, en = results["eager_shim"], results["eager_noshim"]
             out["eager_launch_bound"] = {
@@ -422,7 +503,7 @@ def main():
                 "shim_overhead_pct": round((1.0 - es["tok_s"] / en["tok_s"]) * 100.0, 2),
                 "ms_per_step_shim": round(es["max_wall_s"] / args.eager_steps * 1e3, 3),
                 "ms_per_step_noshim": round(en["max_wall_s"] / args.eager_steps * 1e3, 3)}
-        for nm in ("shim", "temporal"):
+        for nm in ("shim", "temporal", "temporal_unequal"):
             if nm in results and "monitor" in results[nm]:
                 out[f"{nm}_monitor"] = results[nm]["monitor"]
         if "governed" in results and "governed_ref" in results:

@@ -221,7 +221,7 @@ def test_temporal_slices_charged_the_share_they_receive(tmp):
     # the governor really ran and charged each tenant its half (a disabled one
     # enqueues no gates and reports no charge)
     for g in on["governor_rank0"]:
-        assert g["gov_gates"] > 0 and g["gov_charged_ms"] > 0, on["governor_rank0"]
+        assert g["lifetime"]["gates"] > 0 and g["lifetime"]["charged_ms"] > 0, on["governor_rank0"]
         assert abs(g["busy_share_pct"] - 50.0) <= 5.0, on["governor_rank0"]
 
 
@@ -401,8 +401,8 @@ def test_unequal_temporal_limits_get_their_shares(tmp, limits):
     per = r["per_slice_tok_s_rank0"]
     gov = r["governor_rank0"]
     rows = [{"limit": lim, "tok_s": per[i], "frac": round(per[i] / alone, 3),
-             "busy_share_pct": gov[i]["busy_share_pct"], "held_ms": gov[i]["gov_held_ms"],
-             "charged_ms": gov[i]["gov_charged_ms"]} for i, lim in enumerate(limits)]
+             "busy_share_pct": gov[i]["busy_share_pct"], "held_ms": gov[i]["lifetime"]["held_ms"],
+             "charged_ms": gov[i]["lifetime"]["charged_ms"]} for i, lim in enumerate(limits)]
     print(json.dumps({"limits": limits, "alone_tok_s": alone, "slices": rows}))
     # independent of the estimator: the tokens each tenant
     # produced, as a share of all of them, follow the limits within 10 %
@@ -436,6 +436,6 @@ def test_four_symmetric_temporal_tenants_run_like_native(tmp):
     assert r["temporal_value"] >= 0.97 * r["native_value"], r
     assert r["temporal_fairness_min_over_max"] >= 0.97, r
     for g in gov:
-        assert g["gov_gates"] > 0, gov                                   # the governor ran
+        assert g["lifetime"]["gates"] > 0, gov                           # the governor ran
         assert g["busy_share_pct"] is not None and 20.0 <= g["busy_share_pct"] <= 30.0, gov
         assert (g.get("sampler") or {}).get("board_charged", 0) > 0, gov    # charged from the board
