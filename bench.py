@@ -138,6 +138,8 @@ def main():
                          "as the monitor runs it) or a governed slice's shim; auto = node on one GPU, shim with "
                          "several ranks (one node sampler per rank would read every GPU's processes); off = no "
                          "board at all (A/B of the sampler's cost)")
+    ap.add_argument("--presence-window-us", type=int, default=-1,
+                    help="share-board fair-share presence window (experiments; -1 = the owner's default)")
     ap.add_argument("--overhead-pairs", type=int, default=4,
                     help="shim / masked-no-shim round pairs for shim_overhead_pct, interleaved ABBA (the first "
                          "pair is the headline round and its bare twin; 1 = no extra rounds)")
@@ -194,6 +196,8 @@ def main():
         for sp in specs:
             if args.board == "off" and sp.shim:
                 sp.env["MIVGPU_BOARD_DIR"] = "none"
+            if args.presence_window_us >= 0 and sp.shim:
+                sp.env["MIVGPU_PRESENCE_WINDOW_US"] = str(args.presence_window_us)
             sp.env.update(extra_env)
         return specs[:args.active_slices] if args.active_slices > 0 else specs
 
@@ -361,7 +365,8 @@ def main():
         bdir = next((p.board_dir for p in procs if getattr(p, "board_dir", None)), None)
         if (args.board == "node" or (args.board == "auto" and world == 1)) and bdir and bdir != "none" and not cpu:
             from k8s_vgpu_scheduler_amd.monitor.board import BoardSampler
-            boardd = BoardSampler(bdir).start()
+            boardd = BoardSampler(bdir, extra_args=(["--presence-window-us", str(args.presence_window_us)]
+                                                    if args.presence_window_us >= 0 else [])).start()
         try:
             r = run_round(procs, barrier=barrier, sync=sync)
         finally:

@@ -69,6 +69,8 @@ constexpr uint64_t kEvidenceNs = 200000000ull;
 // bounded here (virtual time beyond it is dropped: a tenant cannot bank an
 // unbounded lead that holds it for seconds).
 constexpr uint64_t kMaxLeadNs = 200000000ull;
+// Fair-share mode: default presence window (Handle::presence_ns).
+constexpr uint64_t kPresenceNs = 20000000ull;
 
 struct Reading {
   int pid;
@@ -118,6 +120,14 @@ struct Handle {
   int last_state[MIVGPU_BOARD_SLOTS] = {};        // ... their state, and when they were fresh
   uint64_t last_state_ns[MIVGPU_BOARD_SLOTS] = {};
   uint64_t wave_ns[MIVGPU_BOARD_SLOTS] = {};      // per board slot, the last pass with its waves resident
+  uint64_t run_ns[MIVGPU_BOARD_SLOTS] = {};       // per board slot, the last pass with more than a gate's waves
+  // fair-share presence window: a backlogged, unheld process counts as
+  // present while it had more than a gate's waves resident within this long
+  // (0 = at this pass's instant only, the round-5 rule).  A decode tenant's
+  // stream of short kernels is caught between two of them in some passes and
+  // not others; eight symmetric tenants were charged 12.0-13.8 % on the
+  // instant.
+  uint64_t presence_ns = kPresenceNs;
   double sub_ewma = 0;                            // share of recent passes fully subscribed
   bool fair = false;                              // fair-share mode
   uint64_t vmin = 0;                              // the previous pass's smallest running virtual time
@@ -648,6 +658,7 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
       h.last_lim[slot] = 0;
       h.last_state_ns[slot] = 0;
       h.wave_ns[slot] = 0;
+      h.run_ns[slot] = 0;
       if (slot + 1 > hi) hi = slot + 1;
     }
     sl[i] = slot;
@@ -678,6 +689,7 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
     // in the fair-share mode.  (Demanding the gate's wave at every pass of a
     // hold instead, a held 25 % tenant next to a 75 % one measured 28 %.)
     if (w > kGateUnits || (held && v > 0)) h.wave_ns[slot] = now;
+    if (w > kGateUnits) h.run_ns[slot] = now;
     const bool evidence = h.wave_ns[slot] && now - h.wave_ns[slot] < kEvidenceNs;
     if (st[i] >= 0) bl[i] = (held || owes) && evidence;
     else if (h.last_state_ns[slot] && now - h.last_state_ns[slot] < kStateGraceNs)
@@ -715,6 +727,19 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
     }
     s.recv_ns += (uint64_t)(got * (double)dt + 0.5);
     if (w > 0) s.busy_ns += dt;
+  }
+  // presence over a window: every backlogged, unheld process whose waves ran
+  // within presence_ns shares the pass equally (a dispatch gap at the pass's
+  // instant does not make it absent; a starved one drops out after the window)
+  if (h.presence_ns && W > 0 && dt) {
+    int npres = 0;
+    for (int i = 0; i < n; ++i)
+      if (sl[i] >= 0 && bl[i] && !hd[i] && h.run_ns[sl[i]] && now - h.run_ns[sl[i]] < h.presence_ns) ++npres;
+    for (int i = 0; i < n; ++i) {
+      if (sl[i] < 0) continue;
+      const bool p = bl[i] && !hd[i] && h.run_ns[sl[i]] && now - h.run_ns[sl[i]] < h.presence_ns;
+      use[i] = p && npres ? 1.0 / (double)npres : 0.0;
+    }
   }
   // fair-share mode while the backlogged weights fill the GPU
   if (dt) {

@@ -9,12 +9,18 @@
 // (pkg/device-plugin/nvidiadevice/nvinternal/plugin/server.go:853-864).
 //
 //   mivgpu-boardd --dir DIR [--kfd-sysfs /sys/class/kfd/kfd] [--period-us 2000]
-//                 [--idle-period-us 20000] [--passes N] [--exit-with-parent]
+//                 [--idle-period-us 20000] [--dormant-period-us 100000]
+//                 [--presence-window-us 20000] [--passes N] [--exit-with-parent]
 //
 // Every pass reads <kfd>/proc/<pid>/stats_<gpu_id>/cu_occupancy of every KFD
 // process (~7 us per read on MI355X) and writes each GPU's board; the process
-// list is re-scanned every 100 ms.  Fast passes while any GPU had waves
-// resident within the last second, idle passes otherwise.
+// list is re-scanned every 100 ms.  Fast passes while a tenant is governed
+// (GATED flags within the last second) and waves were resident within the
+// last second, idle passes while one is governed but the GPU is idle, and
+// dormant passes while no tenant is governed (CU-masked tenants only).
+// Tenant files are read with pread, never mapped, created or followed
+// through a symlink; a pid's flags come only from the directory
+// of the container the monitor attributes it to (<dir>/gpu-<id>.owners).
 #include <dirent.h>
 #include <signal.h>
 #include <stdlib.h>
@@ -110,6 +116,7 @@ int main(int argc, char** argv) {
   const char* dir = nullptr;
   const char* kfd = "/sys/class/kfd/kfd";
   uint64_t period_ns = 2000000, idle_ns = 20000000, dormant_ns = 100000000, max_passes = 0;
+  uint64_t presence_ns = mivgpu_board::kPresenceNs;
   int split = mivgpu_board::kSplitRatio;
   for (int i = 1; i < argc; ++i) {
     const char* a = argv[i];
@@ -120,10 +127,11 @@ int main(int argc, char** argv) {
     else if (!strcmp(a, "--idle-period-us") && v) { idle_ns = strtoull(v, nullptr, 10) * 1000ull; ++i; }
     else if (!strcmp(a, "--dormant-period-us") && v) { dormant_ns = strtoull(v, nullptr, 10) * 1000ull; ++i; }
     else if (!strcmp(a, "--passes") && v) { max_passes = strtoull(v, nullptr, 10); ++i; }
+    else if (!strcmp(a, "--presence-window-us") && v) { presence_ns = strtoull(v, nullptr, 10) * 1000ull; ++i; }
     else if (!strcmp(a, "--split") && v) { split = !strcmp(v, "equal") ? mivgpu_board::kSplitEqual : split; ++i; }
     else if (!strcmp(a, "--exit-with-parent")) { prctl(PR_SET_PDEATHSIG, SIGTERM); }
     else {
-      fprintf(stderr, "usage: %s --dir DIR [--kfd-sysfs PATH] [--period-us N] [--idle-period-us N] [--dormant-period-us N] [--passes N] "
+      fprintf(stderr, "usage: %s --dir DIR [--kfd-sysfs PATH] [--period-us N] [--idle-period-us N] [--dormant-period-us N] [--presence-window-us N] [--passes N] "
               "[--split ratio|equal] [--exit-with-parent]\n", argv[0]);
       return 2;
     }
@@ -147,6 +155,7 @@ int main(int argc, char** argv) {
     }
     g.h.owner = true;   // the node sampler owns unconditionally; shims yield to a live one
     g.h.node = true;    // tenant files: read only, never created, never through a symlink
+    g.h.presence_ns = presence_ns;
     gpus.push_back(std::move(g));
   }
   if (gpus.empty()) {

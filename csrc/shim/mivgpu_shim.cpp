@@ -484,6 +484,7 @@ struct Config {
   // redirected (tests: a fake KFD must not meet a real GPU's board).
   char board_dir[256] = "/tmp/mivgpu-board";
   char board_flags_dir[256] = "";   // this container's own flags directory ("" = <board_dir>/flags)
+  uint64_t presence_ns = mivgpu_board::kPresenceNs;   // fair-share presence window when this shim owns the board
   // MIVGPU_BOARD_SPLIT=equal (A/B): a board owner splits each pass equally
   // among the processes with waves resident instead of by their waves
   int board_split = 0;
@@ -719,6 +720,8 @@ void load_config() {
   if (bd) snprintf(g_cfg.board_dir, sizeof(g_cfg.board_dir), "%s", strcmp(bd, "none") ? bd : "");
   const char* bfd = grant_env("MIVGPU_BOARD_FLAGS_DIR");
   if (bfd && *bfd) snprintf(g_cfg.board_flags_dir, sizeof(g_cfg.board_flags_dir), "%s", bfd);
+  const char* pw = unguarded_env("MIVGPU_PRESENCE_WINDOW_US");
+  if (pw && *pw) g_cfg.presence_ns = (uint64_t)atoll(pw) * 1000ull;
   const char* bs = unguarded_env("MIVGPU_BOARD_SPLIT");
   g_cfg.board_split = bs && !strcmp(bs, "equal") ? mivgpu_board::kSplitEqual : mivgpu_board::kSplitRatio;
   const char* gt = getenv("MIVGPU_GATE_TRACE");
@@ -1893,6 +1896,7 @@ double board_step(OccDev& o, uint64_t now, int own_raw, bool gating, int flags, 
     o.board_open_ns = now;
     if (!mb::open_board(o.board, g_cfg.board_dir, o.gpu_id, true)) return -1;
     snprintf(o.board.flags_dir, sizeof(o.board.flags_dir), "%s", g_cfg.board_flags_dir);
+    o.board.presence_ns = g_cfg.presence_ns;
     mlog(3, "KFD gpu %d: share board %s/gpu-%d.board mapped %s", o.gpu_id, g_cfg.board_dir, o.gpu_id,
          o.board.writable ? "read-write" : "read-only");
   }

@@ -274,10 +274,10 @@ class BoardSampler:
     """The node sampler process (``mivgpu-boardd``), owned by the monitor."""
 
     def __init__(self, board_dir: str, kfd_sysfs: str | None = None, period_us: int = 2000,
-                 idle_period_us: int = 20000, binary: str | None = None):
+                 idle_period_us: int = 20000, binary: str | None = None, extra_args: list | None = None):
         self.dir = board_dir
         self.kfd = kfd_sysfs or os.environ.get("MIVGPU_KFD_SYSFS", "/sys/class/kfd/kfd")
-        self.args = ["--period-us", str(period_us), "--idle-period-us", str(idle_period_us)]
+        self.args = ["--period-us", str(period_us), "--idle-period-us", str(idle_period_us), *(extra_args or [])]
         self.binary = binary or str(boardd_path())
         self.proc: subprocess.Popen | None = None
 

@@ -26,8 +26,9 @@ from test_shim_cpu import _fake_kfd, _kfd_env, _occ
 
 
 def _boardd(native_build, kfd, d, *extra):
+    # every pass 2 ms apart: fast, idle and dormant (no GATED tenant) alike
     return [str(native_build["boardd"]), "--dir", str(d), "--kfd-sysfs", str(kfd), "--period-us", "2000",
-            "--idle-period-us", "2000", *extra]
+            "--idle-period-us", "2000", "--dormant-period-us", "2000", *extra]
 
 
 def _drive(native_build, tmp_path, cmds, env, cache):
@@ -479,3 +480,50 @@ def test_node_sampler_is_dormant_until_a_tenant_gates(native_build, tmp_path):
         fl.close()
     assert p0 == 100_000_000 and n0 <= 10, (p0, n0)
     assert p1 == p2 == 2_000_000 and n2 - n1 > 100, (p1, p2, n1, n2)
+
+
+def _flicker_run(native_build, tmp_path, window_us, seconds=0.8):
+    """Two 50 % tenants, both always backlogged (OWES): 111 keeps 10 CU units
+    resident, 222's kernels leave gaps (its occupancy reads 10 and 0 in
+    turns, 8 ms each).  Returns the board slots."""
+    kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
+    _occ(kfd, 111, 4242, 10)
+    _occ(kfd, 222, 4242, 10)
+    d = tmp_path / "board"
+    fl = B.FlagsFile(str(d), 4242)
+    node = subprocess.Popen(_boardd(native_build, kfd, d, "--presence-window-us", str(window_us)))
+    f222 = open(kfd / "proc" / "222" / "stats_4242" / "cu_occupancy", "r+b", buffering=0)
+    try:
+        t0 = time.time()
+        t_end = t0 + seconds
+        while time.time() < t_end:
+            fl.publish(111, B.FLAG_OWES, 500000)
+            fl.publish(222, B.FLAG_OWES, 500000)
+            # 8 ms with waves, 8 ms between kernels (rewritten in place, same
+            # width: the sampler keeps the file open and never reads it empty)
+            f222.seek(0)
+            f222.write(b"10\n" if int((time.time() - t0) / 0.008) % 2 == 0 else b" 0\n")
+            f222.flush()
+            time.sleep(0.001)
+        b = B.Board(B.board_path(d, 4242))
+        s = b.slots()
+        b.close()
+    finally:
+        node.terminate()
+        node.wait(timeout=10)
+        fl.close()
+        f222.close()
+    return s
+
+
+def test_fair_share_presence_spans_dispatch_gaps(native_build, tmp_path):
+    """presence read at the pass's instant
+    charged a tenant caught between kernels less than its neighbour, so the
+    neighbour led and was held although both ran all the time.  With the
+    presence window (default 20 ms) both count in every pass: neither leads;
+    at the instant (window 0) the always-resident tenant leads."""
+    s = _flicker_run(native_build, tmp_path / "win", 20000)
+    win = max(s[111].lead_ns, s[222].lead_ns)
+    s = _flicker_run(native_build, tmp_path / "inst", 0)
+    inst = s[111].lead_ns
+    assert win < 15_000_000 and inst > 40_000_000 and s[222].lead_ns == 0, (win, inst, s[222].lead_ns)
