@@ -65,9 +65,11 @@ def native_rccl_check(rank: int, world: int, local_rank: int, barrier) -> dict:
                             "--warmup", "3"], capture_output=True, text=True, timeout=300)
     except subprocess.TimeoutExpired:
         return {"rc": "timeout"}
-    rows = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    rows = [x for x in lines if "op" in x]
+    comm = next((x["comm"] for x in lines if "comm" in x), None)
     out = {"rc": r.returncode, "all_ok": r.returncode == 0 and bool(rows) and all(x["ok"] for x in rows),
-           "rows": [{k: x[k] for k in ("op", "bytes", "ms", "busbw_gbs", "ok")} for x in rows]}
+           "comm": comm, "rows": [{k: x[k] for k in ("op", "bytes", "ms", "busbw_gbs", "ok")} for x in rows]}
     if r.returncode:
         out["stderr"] = r.stderr[-600:]
     return out
@@ -375,6 +377,7 @@ def main():
         r["specs"] = [p.spec for p in procs]
         if mon is not None:
             r["monitor"] = mon.stop()
+        r["local_tokens"] = float(r["tokens"])
         wall = torch.tensor([r["wall_s"]], dtype=torch.float64)        # CPU: no queues in this process
         toks = torch.tensor([float(r["tokens"])], dtype=torch.float64)
         if world > 1:
@@ -403,6 +406,19 @@ def main():
     rccl_native = None
     if world > 1 and not args.no_collectives and not cpu and build.RCCL_CHECK.exists():
         rccl_native = native_rccl_check(rank, world, local_rank, barrier)
+    # every rank's own view, so an N-GPU record reads from one line: its GPU,
+    # its slices' tokens/s and wall time in the headline round, and what its
+    # RCCL validator measured and saw
+    per_rank = None
+    if world > 1:
+        hname = "shim" if "shim" in results else ("native" if "native" in results else next(iter(results)))
+        mine = {"rank": rank, "local_rank": local_rank, "gpu": phys, "host": os.uname().nodename,
+                "tok_s": round(results[hname]["local_tokens"] / results[hname]["wall_s"], 2),
+                "wall_s": round(results[hname]["wall_s"], 4),
+                "per_slice_tok_s": [round(d["tok_s"], 1) for d in results[hname]["done"]],
+                "rccl": rccl_native}
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
 
     if rank == 0:
         head = results.get("shim") or results.get("native") or next(iter(results.values()))
@@ -531,6 +547,10 @@ def main():
             out["allreduce_peak_busbw_gbps"] = max(r["busbw_gbps"] for r in coll)
         if rccl_native is not None:
             out["rccl_native_check"] = rccl_native
+        if per_rank is not None:
+            out["per_rank"] = per_rank
+            out["rccl_ranks_seen"] = sorted({(pr.get("rccl") or {}).get("comm", {}).get("nranks", -1)
+                                             for pr in per_rank if pr})
         line = json.dumps(out)
         print(line, flush=True)
         if args.out:

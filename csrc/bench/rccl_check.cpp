@@ -146,6 +146,20 @@ int main(int argc, char** argv) {
   }
   ncclComm_t comm;
   NCCLCHECK(ncclCommInitRank(&comm, nranks, id, rank));
+  {
+    // what RCCL saw: its rank count and this rank's device, by PCI location
+    int count = -1, urank = -1, dev = -1;
+    NCCLCHECK(ncclCommCount(comm, &count));
+    NCCLCHECK(ncclCommUserRank(comm, &urank));
+    NCCLCHECK(ncclCommCuDevice(comm, &dev));
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) snprintf(bus, sizeof(bus), "?");
+    char ver[32] = {0};
+    int v = 0;
+    if (ncclGetVersion(&v) == ncclSuccess) snprintf(ver, sizeof(ver), "%d", v);
+    printf("{\"comm\":{\"rank\":%d,\"nranks\":%d,\"device\":%d,\"pci_bus_id\":\"%s\",\"rccl_version\":\"%s\"}}\n",
+           urank, count, dev, bus, ver);
+  }
   hipStream_t s;
   HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   unsigned long long* bad_d;

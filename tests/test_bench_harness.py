@@ -45,8 +45,13 @@ def test_bench_json_contract_cpu_rehearsal(nproc):
         ar = out["allreduce_between_gpus"]
         assert [r["bytes"] for r in ar] == [64 << 10, 1 << 20] and all(r["correct"] for r in ar)
         assert out["allreduce_peak_busbw_gbps"] == max(r["busbw_gbps"] for r in ar) > 0
+        # every rank's own view in the one line
+        pr = out["per_rank"]
+        assert [p["rank"] for p in pr] == list(range(nproc)) and all(p["tok_s"] > 0 for p in pr)
+        assert sum(p["tok_s"] for p in pr) >= out["value"] * 0.98        # the aggregate uses the max wall
+        assert all(len(p["per_slice_tok_s"]) == 2 for p in pr)
     else:
-        assert "allreduce_between_gpus" not in out
+        assert "allreduce_between_gpus" not in out and "per_rank" not in out
 
 
 @pytest.mark.parametrize("nproc", [4, 8])
@@ -61,3 +66,4 @@ def test_bench_json_contract_at_4_and_8_ranks(nproc):
     assert out["value"] == pytest.approx(tokens / (out["ms_per_step"] * 2 / 1000), rel=0.02)
     ar = out["allreduce_between_gpus"]
     assert all(r["correct"] for r in ar)
+    assert [p["rank"] for p in out["per_rank"]] == list(range(nproc))

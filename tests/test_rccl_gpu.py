@@ -22,8 +22,11 @@ def _run(tmp_path, env, tag):
     r = subprocess.run([str(exe), "--rank", "0", "--nranks", "1", "--uid", str(tmp_path / f"{tag}.uid"),
                         "--sizes", "1048576,67108864", "--iters", "5", "--warmup", "2"],
                        env=env, capture_output=True, text=True, timeout=180)
-    rows = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
-    return r, rows
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    comm = [x["comm"] for x in lines if "comm" in x]
+    # what RCCL saw, reported before the rows (bench.py carries it per rank)
+    assert r.returncode != 0 or (comm and comm[0]["nranks"] == 1 and comm[0]["rank"] == 0), lines
+    return r, [x for x in lines if "op" in x]
 
 
 def test_native_rccl_check_one_rank(tmp_path):
