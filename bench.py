@@ -303,8 +303,10 @@ def main():
                              hw_queues=args.hw_queues or None)
         for sp, lim in zip(uspecs, unequal):
             sp.core_pct = lim
+        # the governor rounds' step count (>= 2 s of GPU work): a 20-step
+        # window is mostly the buckets' initial burst
         rounds.append(("temporal_unequal", spawn_round(with_env(uspecs), phys, work / "unequal", log_dir,
-                                                       child_args, "temporal_unequal")))
+                                                       gov_args, "temporal_unequal")))
     if "native" in wanted:
         rounds.append(("native", spawn_round(native_specs(args.hw_queues), phys, work, log_dir, child_args,
                                              "native")))
@@ -370,7 +372,11 @@ def main():
             boardd = BoardSampler(bdir, extra_args=(["--presence-window-us", str(args.presence_window_us)]
                                                     if args.presence_window_us >= 0 else [])).start()
         try:
-            r = run_round(procs, barrier=barrier, sync=sync)
+            # with the monitor: one pass once every slice is READY, then a few
+            # untimed steps, so the timed window sees the switch as production
+            # keeps it (on while several tenants are busy)
+            r = run_round(procs, barrier=barrier, sync=sync, before_go=mon.pass_now if mon else None,
+                          rewarm=max(3, args.warmup) if mon else 0)
         finally:
             if boardd is not None:
                 boardd.stop()
@@ -506,6 +512,7 @@ def main():
             lims = [sp.core_pct for sp in tu.get("specs", [])]
             out["temporal_unequal"] = {
                 "what": "governor gate, policy force, no CU masks, unequal core limits: must throttle",
+                "steps": max(args.gov_steps, args.steps),
                 "limits_pct": [pct_text(x) for x in lims],
                 "aggregate_tok_s": round(tu["tok_s"], 1),
                 "per_slice_tok_s": [round(x, 1) for x in tps],
@@ -513,8 +520,6 @@ def main():
                 "gpu_share_pct": [d.get("busy_share_pct") for d in tu["done"]],
                 "held_ms": [(d.get("timed") or {}).get("held_ms") for d in tu["done"]],
                 "governor_rank0": [gov_row(d) for d in tu["done"]]}
-            if "native" in results:
-                out["temporal_unequal"]["fraction_of_native"] = round(tu["tok_s"] / results["native"]["tok_s"], 4)
         if "eager_shim" in results and "eager_noshim" in results:
             es, en = results["eager_shim"], results["eager_noshim"]
             out["eager_launch_bound"] = {

@@ -147,6 +147,8 @@ class RoundMonitor:
         self.caches, self.period = [c for c in caches if c], period
         self._stop = threading.Event()
         self._th = threading.Thread(target=self._run, name="round-monitor", daemon=True)
+        self._mu = threading.Lock()
+        self._regions = {}
         self.passes = 0
         self.switch_seen = 0
 
@@ -155,26 +157,34 @@ class RoundMonitor:
         return self
 
     def _run(self):
+        while not self._stop.wait(self.period):
+            self.pass_now()
+
+    def pass_now(self):
+        """One feedback pass now (the harness runs it once every slice is
+        READY, so the switch is engaged before the timed window -- in
+        production it stays on between the 5 s passes)."""
         from k8s_vgpu_scheduler_amd.monitor.feedback import observe
         from k8s_vgpu_scheduler_amd.monitor.region import SharedRegion
-        regions = {}
-        while not self._stop.wait(self.period):
+        with self._mu:
             for c in self.caches:
-                if c not in regions and os.path.exists(c):
+                if c not in self._regions and os.path.exists(c):
                     try:
-                        regions[c] = SharedRegion(c)
+                        self._regions[c] = SharedRegion(c)
                     except (OSError, ValueError):
                         pass
-            cs = [self._C(r) for r in regions.values()]
+            cs = [self._C(r) for r in self._regions.values()]
             observe(type("L", (), {"list_containers": lambda _self: cs})())
             self.passes += 1
             self.switch_seen += sum(1 for x in cs if x.region.utilization_switch() == 1)
-        for r in regions.values():
-            r.close()
 
     def stop(self) -> dict:
         self._stop.set()
         self._th.join(timeout=10)
+        with self._mu:
+            for r in self._regions.values():
+                r.close()
+            self._regions = {}
         return {"period_s": self.period, "passes": self.passes, "switch_on_slice_passes": self.switch_seen}
 
 
@@ -297,7 +307,16 @@ def child_main(argv):
         ready["kfd_entry_found"] = bool(me and me[0].hostpid)
         reg.close()
     print("READY " + json.dumps(ready), flush=True)
-    if sys.stdin.readline().strip() != "GO":
+    cmd = sys.stdin.readline().strip()
+    while cmd.startswith("WARM"):
+        # more untimed steps after the harness ran a monitor pass (the
+        # governor's utilisation switch engaged before the timed window)
+        for _ in range(int(cmd.split()[1]) if len(cmd.split()) > 1 else a.warmup):
+            dec.step()
+        torch.cuda.synchronize()
+        print("WARMED {}", flush=True)
+        cmd = sys.stdin.readline().strip()
+    if cmd != "GO":
         return 0
     if a.loop:
         return _loop_until_stop(a, dec, torch.cuda.synchronize)
@@ -433,7 +452,13 @@ def _child_cpu(a, cfg, Qwen3Decoder):
     print("READY " + json.dumps({"load_s": round(time.time() - t_load, 2), "mem_total_mib": 0, "mem_free_mib": 0,
                                  "allocated_mib": 0, "cus": 0, "preload": os.environ.get("LD_PRELOAD", ""),
                                  "cu_mask": os.environ.get("HSA_CU_MASK", "")}), flush=True)
-    if sys.stdin.readline().strip() != "GO":
+    cmd = sys.stdin.readline().strip()
+    while cmd.startswith("WARM"):
+        for _ in range(int(cmd.split()[1]) if len(cmd.split()) > 1 else a.warmup):
+            dec.step()
+        print("WARMED {}", flush=True)
+        cmd = sys.stdin.readline().strip()
+    if cmd != "GO":
         return 0
     if a.loop:
         return _loop_until_stop(a, dec, lambda: None)
@@ -485,11 +510,21 @@ def spawn_round(specs, physical_gpu, cache_dir: Path, log_dir: Path, child_args,
     return procs
 
 
-def run_round(procs, barrier=None, sync=None, load_timeout=900, run_timeout=900) -> dict:
-    """Drive one spawned round through LOAD/READY/GO/DONE; returns timings."""
+def run_round(procs, barrier=None, sync=None, load_timeout=900, run_timeout=900, before_go=None,
+              rewarm: int = 0) -> dict:
+    """Drive one spawned round through LOAD/READY/GO/DONE; returns timings.
+    ``before_go()``: called once every slice is READY (a monitor pass); then
+    ``rewarm`` more untimed steps per slice (WARM/WARMED) before GO."""
     for p in procs:
         p.send("LOAD")
     readies = [p.expect("READY", load_timeout) for p in procs]
+    if before_go is not None:
+        before_go()
+    if rewarm > 0:
+        for p in procs:
+            p.send(f"WARM {rewarm}")
+        for p in procs:
+            p.expect("WARMED", load_timeout)
     if barrier:
         barrier()
     if sync:
