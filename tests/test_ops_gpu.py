@@ -581,18 +581,21 @@ def test_decoder_qkv_on_wide_kernel_matches_reference(monkeypatch):
         b.tokens.copy_(a.tokens)
 
 
-@pytest.mark.parametrize("L,T,cb", [(92, 256, 1), (37, 64, 0), (300, 256, 2)])
-def test_prefill_qk_norm_rope_kv(ops, L, T, cb):
+@pytest.mark.parametrize("L,T,cb,off", [(92, 256, 1, 0), (37, 64, 0, 0), (300, 256, 2, 0), (8192, 8192, 0, 0),
+                                        (333, 512, 1, 3), (64, 96, 2, 40)])
+def test_prefill_qk_norm_rope_kv(ops, L, T, cb, off):
     """Prompt rows of one sequence into cache row ``cb``: head-grouped q, plain
     K/V and the cache append vs the per-row decode kernel's fp32 reference
-    (positions >= T are dropped from the cache, kept in the plain copies)."""
+    (positions >= T are dropped from the cache, kept in the plain copies).
+    ``off``: the prompt starts at that position (an unaligned start takes the
+    vectorised kernel's element-store path for V)."""
     Hq, Hkv, D, B = 32, 8, 128, 3
     G = Hq // Hkv
     g = torch.Generator(device="cuda").manual_seed(L)
     qkv = torch.randn(L, (Hq + 2 * Hkv) * D, device="cuda", generator=g).bfloat16()
     qw = (1 + 0.1 * torch.randn(D, device="cuda", generator=g)).bfloat16()
     kw = (1 + 0.1 * torch.randn(D, device="cuda", generator=g)).bfloat16()
-    pos = torch.arange(L, dtype=torch.int32, device="cuda")
+    pos = torch.arange(L, dtype=torch.int32, device="cuda") + off
     k_log = torch.randn(B, Hkv, T, D, device="cuda", generator=g).bfloat16()
     v_log = torch.randn(B, Hkv, T, D, device="cuda", generator=g).bfloat16()
     kc, vc = ops.k_to_cache_layout(k_log), ops.v_to_cache_layout(v_log)
@@ -602,21 +605,23 @@ def test_prefill_qk_norm_rope_kv(ops, L, T, cb):
     ops.prefill_qk_norm_rope_kv(qkv, qw, kw, pos, q, kp, vp, kc, vc, cb, Hq, Hkv, D, 1e-6, 1e6)
     # reference: each prompt row as its own decode row with a private logical cache
     q_ref = torch.empty(L, Hq, D, device="cuda", dtype=torch.bfloat16)
-    kr = torch.zeros(L, Hkv, max(T, L), D, device="cuda", dtype=torch.bfloat16)
+    kr = torch.zeros(L, Hkv, max(T, L + off), D, device="cuda", dtype=torch.bfloat16)
     vr = torch.zeros_like(kr)
     ref.qk_norm_rope_kv(qkv, qw, kw, pos, q_ref, kr, vr, Hq, Hkv, D, 1e-6, 1e6)
-    k_rows = torch.stack([kr[i, :, i] for i in range(L)], 1)              # [Hkv, L, D]
-    v_rows = torch.stack([vr[i, :, i] for i in range(L)], 1)
+    k_rows = torch.stack([kr[i, :, i + off] for i in range(L)], 1)        # [Hkv, L, D]
+    v_rows = torch.stack([vr[i, :, i + off] for i in range(L)], 1)
     torch.cuda.synchronize()
     _close(q, q_ref.view(L, Hkv, G, D).permute(1, 2, 0, 3).reshape(Hkv, G * L, D), 2e-2)
     _close(kp, k_rows, 2e-2)
     assert torch.equal(vp, v_rows)
-    n = min(L, T)
+    n = max(0, min(L, T - off))
     k_new, v_new = ops.k_from_cache_layout(kc), ops.v_from_cache_layout(vc)
-    _close(k_new[cb, :, :n], k_rows[:, :n], 2e-2)
-    assert torch.equal(v_new[cb, :, :n], v_rows[:, :n])
+    _close(k_new[cb, :, off:off + n], k_rows[:, :n], 2e-2)
+    assert torch.equal(v_new[cb, :, off:off + n], v_rows[:, :n])
     # nothing else in the caches moved
-    assert torch.equal(k_new[cb, :, n:], k_log[cb, :, n:]) and torch.equal(v_new[cb, :, n:], v_log[cb, :, n:])
+    assert torch.equal(k_new[cb, :, off + n:], k_log[cb, :, off + n:])
+    assert torch.equal(v_new[cb, :, off + n:], v_log[cb, :, off + n:])
+    assert torch.equal(k_new[cb, :, :off], k_log[cb, :, :off]) and torch.equal(v_new[cb, :, :off], v_log[cb, :, :off])
     for o in range(B):
         if o != cb:
             assert torch.equal(k_new[o], k_log[o]) and torch.equal(v_new[o], v_log[o])
