@@ -79,7 +79,10 @@ def main(argv=None):
     inf.start()
     lister = ContainerLister(a.hook_path, inf.list)
     try:
-        backend = detect(a.smi_backend)
+        # one lock around every amd-smi call: scrapes and the feedback pass
+        # run on different threads
+        from k8s_vgpu_scheduler_amd.smi import SerializedBackend
+        backend = SerializedBackend(detect(a.smi_backend))
     except RuntimeError as e:
         log.warning("no amd-smi backend (%s): host metrics disabled", e)
         backend = None

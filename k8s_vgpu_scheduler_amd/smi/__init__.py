@@ -609,6 +609,30 @@ class FakeBackend(Backend):
         return self.util.get(g.uuid, {"gfx": 0.0, "umc": 0.0})
 
 
+class SerializedBackend:
+    """Every call into the wrapped backend under one lock.  The monitor calls
+    its backend from the metrics HTTP thread (every scrape) and from the
+    feedback thread (host truth's uuid -> KFD gpu_id map); amd-smi's library
+    does not document its calls as thread-safe, so they never overlap."""
+
+    def __init__(self, inner):
+        import threading
+        self._inner = inner
+        self._mu = threading.RLock()
+        self.name = getattr(inner, "name", "base")
+
+    def __getattr__(self, attr):
+        v = getattr(self._inner, attr)
+        if not callable(v):
+            return v
+        mu = self._mu
+
+        def call(*a, **kw):
+            with mu:
+                return v(*a, **kw)
+        return call
+
+
 def detect(prefer: str | None = None) -> Backend:
     prefer = prefer or os.environ.get("MIVGPU_SMI_BACKEND")
     if prefer == "fake":

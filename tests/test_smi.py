@@ -46,3 +46,31 @@ def test_sysfs_backend_reads_topology_and_partitions(tmp_path):
     assert (pci / "0000:1b:00.0" / "current_compute_partition").read_text() == "DPX\n"
     # the event source is amd-smi's; sysfs has none and says so
     assert b.wait_health_events(gs, 0.01) is None
+
+
+def test_serialized_backend_never_overlaps_calls():
+    """The monitor wraps its backend so that scrapes (HTTP thread) and the
+    feedback pass (host truth's GPU id map) never call amd-smi at once."""
+    import threading
+    import time
+
+    from k8s_vgpu_scheduler_amd.smi import FakeBackend, SerializedBackend
+
+    class Probe(FakeBackend):
+        inside = 0
+        worst = 0
+
+        def gpus(self):
+            Probe.inside += 1
+            Probe.worst = max(Probe.worst, Probe.inside)
+            time.sleep(0.002)
+            Probe.inside -= 1
+            return super().gpus()
+
+    b = SerializedBackend(Probe(2))
+    ths = [threading.Thread(target=lambda: [b.gpus() for _ in range(10)]) for _ in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert Probe.worst == 1 and b.name == "fake" and len(b.gpus()) == 2
