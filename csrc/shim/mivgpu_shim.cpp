@@ -2165,9 +2165,9 @@ bool occ_sample(int dev, uint64_t now) {
     // each over a 1.6 s run, at 0.82 of native.  There the tenant is held on
     // its lead over the backlogged tenants' mean instead (the tenants behind
     // always run: work-conserving, shares by core limit) and its bucket
-    // carries nothing out of the mode: no debt, and no burst either (a 25 %
-    // tenant left alone by a 75 % one that finished spent up to the whole
-    // 100 ms burst it had banked while held on its lead: 27 % of the GPU).
+    // carries no debt and no burst out of the mode, only the mode's own lag
+    // (a 25 % tenant left alone by a 75 % one that finished spent up to the
+    // whole 100 ms burst it had banked while held on its lead: 27 % of the GPU).
     // The lag grows with the GPU time received in the mode: 3 % of it, at
     // least 10 ms.  The wave-share estimate is not exact per tenant (four
     // symmetric 25 % tenants: one was held 120 ms of a 100-step run on it and
@@ -2175,7 +2175,12 @@ bool occ_sample(int dev, uint64_t now) {
     // unequal limits drift by far more than 3 % and are still held.
     double eff = o.tokens_ns;
     if (lead >= 0) {
-      o.tokens_ns = 0;
+      // out of the mode with the mode's own slack (kFairLagNs), not empty:
+      // eight pooled tenants pausing together (a batch edge) left the mode,
+      // and coming back each started its bucket at zero, went a few ms into
+      // debt before the mode re-engaged and sat out a 25 ms hold -- every
+      // tenant, every time (5 % of a 20-step window, round 6)
+      o.tokens_ns = (double)kFairLagNs;
       o.fair_recv_ns += share * run;
       const double rel = g_cfg.fair_lag_frac * o.fair_recv_ns;
       const double lag = rel > (double)kFairLagNs ? rel : (double)kFairLagNs;
