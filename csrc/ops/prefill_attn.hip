@@ -264,7 +264,7 @@ constexpr float F2_RESCALE = 8.f;         // lazy O rescale threshold (log2 unit
 template <int G, int RT>
 __global__ void __launch_bounds__(G * RT * 64, 2)
 prefill_flash8_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-                      bf16_t* __restrict__ out, int L, int Hq, float scale_log2) {
+                      bf16_t* __restrict__ out, int L, int Hq, float scale_log2, int prio_half) {
   constexpr int NW = G * RT, NT = NW * 64;
   constexpr int PER = F2_CHUNKS / NT;      // 16-byte chunks per thread per tile (K and V each)
   static_assert(PER * NT == F2_CHUNKS && NW == 8, "eight waves, the tile split evenly");
@@ -322,6 +322,10 @@ prefill_flash8_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k
 #pragma unroll
     for (int i = 0; i < 16; ++i) o[dc][i] = 0.f;
   float m = -INFINITY, lsum = 0.f;
+  // static priority for the second-dispatched half (MI355X_MICROARCH.md, two
+  // waves per SIMD item 4: the younger half loses VALU arbitration on every
+  // segment; one s_setprio before the loop, no per-segment flips)
+  if (prio_half && w >= NW / 2) __builtin_amdgcn_s_setprio(1);
 
   load_tile(0);
   store_tile(0);
@@ -514,13 +518,17 @@ int mivgpu_prefill_attention(const void* q, const void* k, const void* v, void* 
     else MIVGPU_FA(GG, false, false);                    \
     break;
   if (fa_kernel() == 8) {
+    static const int prio = [] {
+      const char* e = getenv("MIVGPU_FA_PRIO");
+      return e && *e ? atoi(e) : 0;
+    }();
     const int rows = 32 * (8 / G);
     const dim3 grid8((L + rows - 1) / rows, Hkv);
     switch (G) {
-      case 1: hipLaunchKernelGGL((prefill_flash8_kernel<1, 8>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
-      case 2: hipLaunchKernelGGL((prefill_flash8_kernel<2, 4>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
-      case 4: hipLaunchKernelGGL((prefill_flash8_kernel<4, 2>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
-      case 8: hipLaunchKernelGGL((prefill_flash8_kernel<8, 1>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
+      case 1: hipLaunchKernelGGL((prefill_flash8_kernel<1, 8>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2, prio); break;
+      case 2: hipLaunchKernelGGL((prefill_flash8_kernel<2, 4>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2, prio); break;
+      case 4: hipLaunchKernelGGL((prefill_flash8_kernel<4, 2>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2, prio); break;
+      case 8: hipLaunchKernelGGL((prefill_flash8_kernel<8, 1>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2, prio); break;
       default: return -1;
     }
     return (int)hipGetLastError();

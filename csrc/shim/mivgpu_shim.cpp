@@ -2141,11 +2141,15 @@ bool occ_sample(int dev, uint64_t now) {
     const double rate = (lim > 0 && lim < 1000000) ? (double)lim / 1e6 : 1.0;
     const double cap = (double)g_cfg.gate_cap_ns;
     if (!o.bucket) {
-      // empty, not full: a burst is earned by idling below the limit, not
-      // granted at start (a 100 ms start burst put a 1.5 s job at 0.32 of its
-      // unthrottled rate under a 25 % limit)
+      // nearly empty, not full: a burst is earned by idling below the limit,
+      // not granted at start (a 100 ms start burst put a 1.5 s job at 0.32 of
+      // its unthrottled rate under a 25 % limit).  It starts with the
+      // fair-share mode's lag (10 ms), as a tenant leaving the mode does:
+      // eight pooled tenants whose governor the monitor's switch engaged all
+      // at once each went a few ms into debt on the wave-share noise before
+      // the mode took over and sat out a 25 ms hold (round 6)
       o.bucket = true;
-      o.tokens_ns = 0;
+      o.tokens_ns = (double)kFairLagNs;
     } else {
       // Entitlement accrues while the process owes work and through short
       // gaps (host syncs, batch edges), not over long idle stretches: a
