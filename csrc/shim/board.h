@@ -718,7 +718,14 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
       use[i] = w > kGateUnits ? 1.0 / (double)present : 0.0;
     } else {
       got = 0.0;
-      f = st[i] < 0 ? 1.0 : (owes && owing > 0 ? 1.0 / (double)owing : 1.0);
+      // nobody resident: the owing tenants split the pass; a tenant whose
+      // fresh flags say it owes nothing is charged nothing (it was charged
+      // the whole pass, and a tenant sampling across the moment it started
+      // to owe carried those passes into its first owing sample: eight
+      // pooled tenants starting together each went into debt and sat out a
+      // 25-30 ms hold, round 6); without flags a process is charged the pass
+      // whole (alone between its own kernels)
+      f = st[i] < 0 ? 1.0 : (owes && owing > 0 ? 1.0 / (double)owing : 0.0);
       use[i] = owes && owing > 0 ? 1.0 / (double)owing : 0.0;
     }
     if (!held) {

@@ -209,10 +209,12 @@ def test_tenant_flags_decide_held_and_gap_splits(native_build, tmp_path):
     kfd = _fake_kfd(tmp_path / "kfd", [(4242, 0x75 << 8, 0)])
     d = tmp_path / "board"
     fl = B.FlagsFile(str(d), 4242)
-    # 111 runs tiny kernels, 222 is queued behind it (owes, nothing resident), 333 is held
+    # 111 runs tiny kernels, 222 is queued behind it (owes, nothing resident), 333 is held,
+    # 444 is idle (fresh flags, owes nothing)
     _occ(kfd, 111, 4242, 1)
     _occ(kfd, 222, 4242, 0)
     _occ(kfd, 333, 4242, 1)
+    _occ(kfd, 444, 4242, 0)
     node = subprocess.Popen(_boardd(native_build, kfd, d))
     try:
         t_end = time.time() + 0.5
@@ -220,6 +222,7 @@ def test_tenant_flags_decide_held_and_gap_splits(native_build, tmp_path):
             fl.publish(111, B.FLAG_OWES)
             fl.publish(222, B.FLAG_OWES)
             fl.publish(333, B.FLAG_HELD)
+            fl.publish(444, 0)
             time.sleep(0.005)
         b = B.Board(B.board_path(d, 4242))
         s1 = b.snapshot()
@@ -232,6 +235,7 @@ def test_tenant_flags_decide_held_and_gap_splits(native_build, tmp_path):
             fl.publish(111, B.FLAG_OWES)
             fl.publish(222, B.FLAG_OWES)
             fl.publish(333, B.FLAG_HELD)
+            fl.publish(444, 0)
             time.sleep(0.005)
         s2 = b.snapshot()
         b.close()
@@ -245,6 +249,10 @@ def test_tenant_flags_decide_held_and_gap_splits(native_build, tmp_path):
     assert first[333].obs_ns == 0                                 # held: not observed
     sh = B.shares(mid, s2)
     assert abs(sh[111]["charged_share"] - 0.5) < 0.05 and abs(sh[222]["charged_share"] - 0.5) < 0.05, sh
+    # idle with fresh flags: observed, charged nothing -- while others run, and
+    # in the passes nobody is resident (it owes nothing)
+    assert first[444].obs_ns > 0 and first[444].frac_ns == 0
+    assert sh[444]["obs_ms"] > 0 and sh[444]["charged_share"] == 0, sh
 
 
 def _fair_run(native_build, tmp_path, tenants, seconds=0.4, occ_after=None):
