@@ -340,10 +340,21 @@ def child_main(argv):
             "tpot_ms_p99": tpot[min(len(tpot) - 1, int(0.99 * len(tpot)))]}
     rx1 = _received_ns()
     c1 = _timed_counters()
+    if c0.get("tokens_ms") is not None:
+        # the governor's state when GO arrived (a bucket already in debt
+        # holds the first gates of the window) and at the end
+        done["gov_at_go"] = {k: c0.get(k) for k in ("tokens_ms", "lead_ms", "fair_samples")}
+        done["gov_at_end"] = {k: c1.get(k) for k in ("tokens_ms", "lead_ms", "fair_samples")}
     if c0 and c1:
         # the governor over the timed steps only (its totals include the load
         # and warmup, when the slices ran at different times)
-        done["timed"] = {k: round(c1[k] - c0[k], 1) for k in c1 if k in c0}
+        done["timed"] = {k: round(c1[k] - c0[k], 1) for k in c1 if k in c0 and k not in ("tokens_ms", "lead_ms")}
+        if os.environ.get("MIVGPU_GATE_TRACE") == "1":
+            from k8s_vgpu_scheduler_amd.shim.probe import gate_stats
+            # the window's holds: [hold ms, bucket ms at the gate] of the last gates
+            tr = gate_stats().get("trace") or []
+            n = int(done["timed"].get("gates", 0))
+            done["hold_trace"] = [[round(e[4] / 1e6, 2), round(e[5] / 1e6, 2)] for e in tr[-n:] if e[4] > 0]
     if rx0 is not None and rx1 is not None:
         # GPU time the slice received over the timed steps (the governor's
         # share integral), as a share of the wall time
@@ -388,7 +399,7 @@ def _timed_counters() -> dict:
     from k8s_vgpu_scheduler_amd.shim.probe import sampler_info
     si = sampler_info() or {}
     bd = si.get("board") or {}
-    for k in ("samples", "fair_samples", "fair_held_samples"):
+    for k in ("samples", "fair_samples", "fair_held_samples", "tokens_ms", "lead_ms"):
         if k in si:
             out[k] = si[k]
     for k in ("passes", "sub_passes", "fair_passes"):

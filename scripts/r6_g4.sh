@@ -1,0 +1,14 @@
+#!/bin/bash
+set -o pipefail
+O=gpurun_out/r6i
+mkdir -p $O
+run() {  # name, args...
+  local n=$1; shift
+  timeout -k 10 400 python -u bench.py "$@" --out $O/$n.json > $O/$n.log 2>&1 || { echo "$n failed rc=$?"; tail -20 $O/$n.log; exit 1; }
+  python -c "import json;d=json.load(open('$O/$n.json'));print('$n',d['value'],d.get('native_value'),d.get('slice_fairness_min_over_max'),d.get('temporal_value'),d.get('temporal_fairness_min_over_max'),d.get('shim_overhead_pct'),[g.get('held_ms') for g in d.get('governor_rank0',[])])"
+}
+run s8_mon20a --slices 8 --rounds shim,native --steps 20 --warmup 5
+run s8_mon20b --slices 8 --rounds shim,native --steps 20 --warmup 5
+run s8_mon100 --slices 8 --rounds shim,native --steps 100 --warmup 5
+run t8_20 --slices 8 --rounds temporal,native --steps 20 --warmup 5
+bash scripts/r6_fa.sh
