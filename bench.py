@@ -376,8 +376,13 @@ def main():
             # with the monitor: one pass once every slice is READY, then a few
             # untimed steps, so the timed window sees the switch as production
             # keeps it (on while several tenants are busy)
+            # (ten steps at least: the switch engages every tenant's governor at
+            # once, and the first ~100-150 ms -- the node sampler leaving its
+            # dormant period, the fair-share mode establishing -- are the
+            # buckets' transient; production keeps the switch on between its
+            # 5 s passes, so the timed window measures the steady state)
             r = run_round(procs, barrier=barrier, sync=sync, before_go=mon.pass_now if mon else None,
-                          rewarm=max(3, args.warmup) if mon else 0)
+                          rewarm=max(10, args.warmup) if mon else 0)
         finally:
             if boardd is not None:
                 boardd.stop()

@@ -264,7 +264,7 @@ constexpr float F2_RESCALE = 8.f;         // lazy O rescale threshold (log2 unit
 template <int G, int RT>
 __global__ void __launch_bounds__(G * RT * 64, 2)
 prefill_flash8_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-                      bf16_t* __restrict__ out, int L, int Hq, float scale_log2, int prio_half) {
+                      bf16_t* __restrict__ out, int L, int Hq, float scale_log2) {
   constexpr int NW = G * RT, NT = NW * 64;
   constexpr int PER = F2_CHUNKS / NT;      // 16-byte chunks per thread per tile (K and V each)
   static_assert(PER * NT == F2_CHUNKS && NW == 8, "eight waves, the tile split evenly");
@@ -322,10 +322,10 @@ prefill_flash8_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k
 #pragma unroll
     for (int i = 0; i < 16; ++i) o[dc][i] = 0.f;
   float m = -INFINITY, lsum = 0.f;
-  // static priority for the second-dispatched half (MI355X_MICROARCH.md, two
-  // waves per SIMD item 4: the younger half loses VALU arbitration on every
-  // segment; one s_setprio before the loop, no per-segment flips)
-  if (prio_half && w >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  // Round 6, measured and left out (profiles/README.md section 41): static
+  // priority for waves 4-7 (s_setprio 1 before the loop) 708-713 vs 714-718
+  // TFLOP/s at 8192; a software-pipelined loop (P.V of tile kt-1 beside the
+  // softmax of tile kt, V triple-buffered) 688 vs 714.
 
   load_tile(0);
   store_tile(0);
@@ -451,231 +451,6 @@ prefill_flash8_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k
   }
 }
 
-// ============================================================================
-// Software-pipelined eight-wave variant (round 6, MIVGPU_FA_KERNEL=9): the same
-// tiles, waves and LDS layout as prefill_flash8_kernel, but a wave's tile kt
-// runs S(kt) = K(kt) . Q^T, then the P.V MFMAs of the PREVIOUS tile (P(kt-1)
-// kept in registers as bf16, V(kt-1) still in the other LDS buffer), then the
-// softmax of S(kt) -- so the 16 P.V MFMAs have no dependency on the softmax's
-// vector work of the same iteration and can issue beside it, where the
-// one-stage loop serialises S -> softmax -> P.V in every wave (its partner
-// wave on the SIMD is the only cover).  The O rescale for a grown max runs
-// after P.V(kt-1) has been added (P(kt-1) is scaled to the old max), as in
-// the one-stage loop.  V(kt-1) is read from the buffer the next tile is
-// stored into, so the store waits behind a second barrier.
-template <int G, int RT>
-__global__ void __launch_bounds__(G * RT * 64, 2)
-prefill_flash8p_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-                       bf16_t* __restrict__ out, int L, int Hq, float scale_log2, int prio_half) {
-  constexpr int NW = G * RT, NT = NW * 64;
-  constexpr int PER = F2_CHUNKS / NT;
-  static_assert(PER * NT == F2_CHUNKS && NW == 8, "eight waves, the tile split evenly");
-  constexpr int ROWS = 32 * RT;
-  __shared__ __attribute__((aligned(16))) bf16_t ks[2][F2_TILE];
-  __shared__ __attribute__((aligned(16))) bf16_t vs[2][F2_TILE];
-
-  const int nqb = (L + ROWS - 1) / ROWS;
-  const int qb = nqb - 1 - (int)blockIdx.x;       // heaviest (longest) blocks first
-  const int hk = blockIdx.y;
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int g = w % G, rt = w / G;
-  const int r = lane & 31, h = lane >> 5;
-  const int l0 = qb * ROWS + 32 * rt;
-  const int blk_end = min(L, (qb + 1) * ROWS);
-  const int ntiles = (blk_end + F2_BK - 1) / F2_BK;
-
-  const bf16_t* kb = k + (size_t)hk * L * FA_D;
-  const bf16_t* vb = v + (size_t)hk * L * FA_D;
-
-  bf16x8_t qf[8];
-  {
-    const int qrow = min(l0 + r, L - 1);
-    const bf16_t* qp = q + (((size_t)hk * G + g) * L + qrow) * FA_D + 8 * h;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8_t*>(qp + 16 * s);
-  }
-  static_assert(PER == 2, "two chunks per thread");
-  const int c0 = t, c1 = t + NT;
-  const int ko0 = k_off(c0 >> 4, c0 & 15), ko1 = k_off(c1 >> 4, c1 & 15);
-  const int vo0 = v_off(c0 >> 4, c0 & 15), vo1 = v_off(c1 >> 4, c1 & 15);
-  uint4 k0r, k1r, v0r, v1r;
-  auto load_tile = [&](int kt) {
-    const int r0 = min(kt * F2_BK + (c0 >> 4), L - 1);
-    const int r1 = min(kt * F2_BK + (c1 >> 4), L - 1);
-    k0r = *reinterpret_cast<const uint4*>(kb + (size_t)r0 * FA_D + (c0 & 15) * 8);
-    v0r = *reinterpret_cast<const uint4*>(vb + (size_t)r0 * FA_D + (c0 & 15) * 8);
-    k1r = *reinterpret_cast<const uint4*>(kb + (size_t)r1 * FA_D + (c1 & 15) * 8);
-    v1r = *reinterpret_cast<const uint4*>(vb + (size_t)r1 * FA_D + (c1 & 15) * 8);
-  };
-  auto store_tile = [&](int buf) {
-    *reinterpret_cast<uint4*>(&ks[buf][ko0]) = k0r;
-    *reinterpret_cast<uint4*>(&vs[buf][vo0]) = v0r;
-    *reinterpret_cast<uint4*>(&ks[buf][ko1]) = k1r;
-    *reinterpret_cast<uint4*>(&vs[buf][vo1]) = v1r;
-  };
-
-  f32x16_t o[4];
-#pragma unroll
-  for (int dc = 0; dc < 4; ++dc)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) o[dc][i] = 0.f;
-  float m = -INFINITY, lsum = 0.f;
-  if (prio_half && w >= NW / 2) __builtin_amdgcn_s_setprio(1);
-
-  // P of the previous tile (bf16, the P.V B-operands of its four 16-key
-  // k-steps) and which of its halves were visible
-  bf16x8_t pp0, pp1, pp2, pp3;
-  bool pv_prev = false, act1_prev = false;
-  const int gi = lane & 15, qq = gi >> 2, ppi = gi & 3;
-  const int colblk = 16 * ((lane >> 4) & 1);
-  auto pv = [&](const bf16_t* vt_lds, const bf16x8_t& pf, int u) {
-    const int row_lo = 16 * u + 4 * h + qq, row_hi = row_lo + 8;
-#pragma unroll
-    for (int dc = 0; dc < 4; ++dc) {
-      const int col = 32 * dc + colblk + 4 * ppi;
-      const int olo = v_off(row_lo, col >> 3) + (col & 7), ohi = v_off(row_hi, col >> 3) + (col & 7);
-      const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) i16x4_t*)(&vt_lds[olo]));
-      const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) i16x4_t*)(&vt_lds[ohi]));
-      const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
-      const uint4 a4 = make_uint4(l2.x, l2.y, h2.x, h2.y);
-      o[dc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a4), pf, o[dc], 0, 0, 0);
-    }
-  };
-
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < ntiles) load_tile(kt + 1);     // in flight during this tile's MFMAs
-    const int kbase = kt * F2_BK;
-    const bool vis = kbase <= l0 + 31;
-    const bool act1 = kbase + 32 <= l0;
-    f32x16_t s0, s1;
-    if (vis) {
-      const bf16_t* kt_lds = ks[buf];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) s0[i] = 0.f, s1[i] = 0.f;
-#pragma unroll
-      for (int st = 0; st < 8; ++st) {
-        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&kt_lds[k_off(r, 2 * st + h)]);
-        s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[st], s0, 0, 0, 0);
-      }
-      if (act1) {
-#pragma unroll
-        for (int st = 0; st < 8; ++st) {
-          const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&kt_lds[k_off(32 + r, 2 * st + h)]);
-          s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[st], s1, 0, 0, 0);
-        }
-      }
-    }
-    // P.V of the previous tile: independent of this tile's softmax
-    if (pv_prev) {
-      const bf16_t* vt_lds = vs[buf ^ 1];
-      pv(vt_lds, pp0, 0);
-      pv(vt_lds, pp1, 1);
-      if (act1_prev) {
-        pv(vt_lds, pp2, 2);
-        pv(vt_lds, pp3, 3);
-      }
-    }
-    pv_prev = vis;
-    act1_prev = act1;
-    if (vis) {
-      if (kbase == l0) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if ((i & 3) + 8 * (i >> 2) + 4 * h > r) s0[i] = -INFINITY;
-      } else if (act1 && kbase + 32 == l0) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if ((i & 3) + 8 * (i >> 2) + 4 * h > r) s1[i] = -INFINITY;
-      }
-      float mx = s0[0];
-#pragma unroll
-      for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s0[i]);
-      if (act1) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s1[i]);
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mt = mx * scale_log2;
-      if (__ballot(mt > m + F2_RESCALE)) {
-        const float mnew = fmaxf(m, mt);
-        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-        m = mnew;
-        lsum *= alpha;
-#pragma unroll
-        for (int dc = 0; dc < 4; ++dc)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) o[dc][i] *= alpha;
-      }
-      float psum = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(s0[i], scale_log2, -m));
-        s0[i] = p;
-        psum += p;
-      }
-      if (act1) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(s1[i], scale_log2, -m));
-          s1[i] = p;
-          psum += p;
-        }
-      }
-      lsum += psum;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        pp0[j] = (__bf16)s0[j];
-        pp1[j] = (__bf16)s0[8 + j];
-      }
-      if (act1) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          pp2[j] = (__bf16)s1[j];
-          pp3[j] = (__bf16)s1[8 + j];
-        }
-      }
-    }
-    // every wave is done with V(kt-1) (the buffer the next tile goes to)
-    // and with K(kt) before the store; the store is seen after the second
-    __syncthreads();
-    if (kt + 1 < ntiles) store_tile(buf ^ 1);
-    __syncthreads();
-  }
-  if (pv_prev) {   // the last visible tile's P.V: V(ntiles-1) is in its buffer
-    const bf16_t* vt_lds = vs[(ntiles - 1) & 1];
-    pv(vt_lds, pp0, 0);
-    pv(vt_lds, pp1, 1);
-    if (act1_prev) {
-      pv(vt_lds, pp2, 2);
-      pv(vt_lds, pp3, 3);
-    }
-  }
-
-  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
-  const float inv = 1.f / ltot;
-  const int qpos = l0 + r;
-  if (qpos < L) {
-    bf16_t* op = out + (size_t)qpos * Hq * FA_D + (size_t)(hk * G + g) * FA_D;
-#pragma unroll
-    for (int dc = 0; dc < 4; ++dc)
-#pragma unroll
-      for (int i4 = 0; i4 < 4; ++i4) {
-        const int d = 32 * dc + 8 * i4 + 4 * h;
-        uint2 pk;
-        pk.x = (uint32_t)f2bf(o[dc][4 * i4 + 0] * inv) | ((uint32_t)f2bf(o[dc][4 * i4 + 1] * inv) << 16);
-        pk.y = (uint32_t)f2bf(o[dc][4 * i4 + 2] * inv) | ((uint32_t)f2bf(o[dc][4 * i4 + 3] * inv) << 16);
-        *reinterpret_cast<uint2*>(op + d) = pk;
-      }
-  }
-}
-
 // ds_read_b64_tr_b16 semantics probe: LDS holds element e = e; lane l reads
 // at element offset addr[l]; out[4l + i] = element i it received.
 // OFF: a constant element offset the compiler folds into the instruction's
@@ -742,34 +517,14 @@ int mivgpu_prefill_attention(const void* q, const void* k, const void* v, void* 
     else if (tr == 2) MIVGPU_FA(GG, true, true);         \
     else MIVGPU_FA(GG, false, false);                    \
     break;
-  if (fa_kernel() == 9) {   // software-pipelined P.V (A/B)
-    static const int prio9 = [] {
-      const char* e = getenv("MIVGPU_FA_PRIO");
-      return e && *e ? atoi(e) : 0;
-    }();
-    const int rows = 32 * (8 / G);
-    const dim3 grid9((L + rows - 1) / rows, Hkv);
-    switch (G) {
-      case 1: hipLaunchKernelGGL((prefill_flash8p_kernel<1, 8>), grid9, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2, prio9); break;
-      case 2: hipLaunchKernelGGL((prefill_flash8p_kernel<2, 4>), grid9, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2, prio9); break;
-      case 4: hipLaunchKernelGGL((prefill_flash8p_kernel<4, 2>), grid9, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2, prio9); break;
-      case 8: hipLaunchKernelGGL((prefill_flash8p_kernel<8, 1>), grid9, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2, prio9); break;
-      default: return -1;
-    }
-    return (int)hipGetLastError();
-  }
   if (fa_kernel() == 8) {
-    static const int prio = [] {
-      const char* e = getenv("MIVGPU_FA_PRIO");
-      return e && *e ? atoi(e) : 0;
-    }();
     const int rows = 32 * (8 / G);
     const dim3 grid8((L + rows - 1) / rows, Hkv);
     switch (G) {
-      case 1: hipLaunchKernelGGL((prefill_flash8_kernel<1, 8>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2, prio); break;
-      case 2: hipLaunchKernelGGL((prefill_flash8_kernel<2, 4>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2, prio); break;
-      case 4: hipLaunchKernelGGL((prefill_flash8_kernel<4, 2>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2, prio); break;
-      case 8: hipLaunchKernelGGL((prefill_flash8_kernel<8, 1>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2, prio); break;
+      case 1: hipLaunchKernelGGL((prefill_flash8_kernel<1, 8>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
+      case 2: hipLaunchKernelGGL((prefill_flash8_kernel<2, 4>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
+      case 4: hipLaunchKernelGGL((prefill_flash8_kernel<4, 2>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
+      case 8: hipLaunchKernelGGL((prefill_flash8_kernel<8, 1>), grid8, dim3(512), 0, s, qq, kk, vv, oo, L, Hq, sl2); break;
       default: return -1;
     }
     return (int)hipGetLastError();

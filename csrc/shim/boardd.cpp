@@ -9,7 +9,7 @@
 // (pkg/device-plugin/nvidiadevice/nvinternal/plugin/server.go:853-864).
 //
 //   mivgpu-boardd --dir DIR [--kfd-sysfs /sys/class/kfd/kfd] [--period-us 2000]
-//                 [--idle-period-us 20000] [--dormant-period-us 100000]
+//                 [--idle-period-us 20000] [--dormant-period-us 50000]
 //                 [--presence-window-us 20000] [--passes N] [--exit-with-parent]
 //
 // Every pass reads <kfd>/proc/<pid>/stats_<gpu_id>/cu_occupancy of every KFD
@@ -17,7 +17,7 @@
 // list is re-scanned every 100 ms.  Fast passes while a tenant is governed
 // (GATED flags within the last second) and waves were resident within the
 // last second, idle passes while one is governed but the GPU is idle, and
-// dormant passes while no tenant is governed (CU-masked tenants only).
+// dormant (50 ms) passes while no tenant is governed (CU-masked tenants only).
 // Tenant files are read with pread, never mapped, created or followed
 // through a symlink; a pid's flags come only from the directory
 // of the container the monitor attributes it to (<dir>/gpu-<id>.owners).
@@ -115,7 +115,7 @@ void rescan(const char* kfd, std::vector<Gpu>& gpus) {
 int main(int argc, char** argv) {
   const char* dir = nullptr;
   const char* kfd = "/sys/class/kfd/kfd";
-  uint64_t period_ns = 2000000, idle_ns = 20000000, dormant_ns = 100000000, max_passes = 0;
+  uint64_t period_ns = 2000000, idle_ns = 20000000, dormant_ns = 50000000, max_passes = 0;
   uint64_t presence_ns = mivgpu_board::kPresenceNs;
   int split = mivgpu_board::kSplitRatio;
   for (int i = 1; i < argc; ++i) {

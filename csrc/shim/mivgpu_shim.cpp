@@ -1933,7 +1933,7 @@ double board_step(OccDev& o, uint64_t now, int own_raw, bool gating, int flags, 
   }
   mb::View v;
   // stale: older than 50 ms, or than three of the owner's own passes (a node
-  // sampler with no governed tenant runs dormant, 100 ms apart)
+  // sampler with no governed tenant runs dormant, 50 ms apart)
   const bool got = mb::read_slot(b, self, &o.board_hint, &v);
   const uint64_t stale_ns = v.period_ns && 3 * v.period_ns > kBoardStaleNs ? 3 * v.period_ns : kBoardStaleNs;
   if (!got || v.beat_ns + stale_ns < now) {

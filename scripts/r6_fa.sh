@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6: software-pipelined flash attention (MIVGPU_FA_KERNEL=9) -- numerics, microbench A/B, 8k prefill.
 set -o pipefail
-O=gpurun_out/r6i
+O=gpurun_out/r6k
 mkdir -p $O
 MIVGPU_FA_KERNEL=9 timeout -k 10 600 python -u -m pytest tests/test_ops_gpu.py -v --timeout 300 --timeout-method thread \
   -k "prefill_flash" > $O/fa9_tests.log 2>&1 || { echo "fa9 tests failed"; grep -E "FAILED|Error" $O/fa9_tests.log | head; tail -30 $O/fa9_tests.log; exit 1; }
