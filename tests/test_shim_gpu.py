@@ -197,13 +197,36 @@ def test_roctx_markers_on_rocprofv3_timeline(tmp):
 
 
 def _bench(args, timeout=240):
+    """bench.py in a child; its slices' logs go to a fresh directory (under
+    $MIVGPU_TEST_BENCH_LOGS when set) whose tails a failure or a timeout
+    prints, so a slow or stuck slice explains itself."""
+    import glob
     import subprocess
     import sys
+    import tempfile
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], capture_output=True, text=True,
-                       timeout=timeout)
-    assert r.returncode == 0, r.stderr[-3000:]
+    base = os.environ.get("MIVGPU_TEST_BENCH_LOGS")
+    if base:
+        os.makedirs(base, exist_ok=True)
+    logs = tempfile.mkdtemp(prefix="bench-", dir=base)
+    env = dict(os.environ, MIVGPU_BENCH_LOGS=logs)
+
+    def tails():
+        out = []
+        for f in sorted(glob.glob(os.path.join(logs, "*.log"))):
+            try:
+                out.append(f"--- {os.path.basename(f)}\n" + open(f, errors="replace").read()[-600:])
+            except OSError:
+                pass
+        return "\n".join(out)[-6000:]
+    try:
+        r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], capture_output=True, text=True,
+                           timeout=timeout, env=env)
+    except subprocess.TimeoutExpired as e:
+        pytest.fail(f"bench.py {' '.join(args)} still running after {timeout} s; slice logs:\n{tails()}\n"
+                    f"stderr: {(e.stderr or b'')[-2000:]!r}")
+    assert r.returncode == 0, r.stderr[-3000:] + "\n" + tails()
     return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
 
 
@@ -449,7 +472,7 @@ def test_eight_temporal_tenants_run_like_native(tmp):
     and its neighbours are not held for it.  Round 5 (presence at the
     instant): 0.955 / fairness 0.941 on one box, 0.87 on another; round 6:
     0.989 / 0.984."""
-    r = _bench(["--slices", "8", "--rounds", "temporal,native", "--steps", "100", "--warmup", "5"], timeout=600)
+    r = _bench(["--slices", "8", "--rounds", "temporal,native", "--steps", "100", "--warmup", "5"], timeout=170)
     gov = r["temporal_governor_rank0"]
     print(json.dumps({"temporal": r["temporal_value"], "native": r["native_value"],
                       "fairness": r["temporal_fairness_min_over_max"],
@@ -467,7 +490,7 @@ def test_eight_pooled_slices_with_the_monitor_switch(tmp):
     contending tenants, as production runs it (the reference turns the
     utilisation switch on for every busy tenant of equal priority,
     cmd/vGPUmonitor/feedback.go:56-72): within 3 % of native, fair."""
-    r = _bench(["--slices", "8", "--rounds", "shim,native", "--steps", "100", "--warmup", "5"], timeout=600)
+    r = _bench(["--slices", "8", "--rounds", "shim,native", "--steps", "100", "--warmup", "5"], timeout=170)
     mon = r.get("shim_monitor") or {}
     print(json.dumps({"shim": r["value"], "native": r["native_value"], "fairness": r["slice_fairness_min_over_max"],
                       "monitor": mon}))
