@@ -52,6 +52,13 @@ constexpr uint64_t kMaxDtNs = 100000000ull;
 // most passes of the last ~10 ms (EWMA >= 0.8), left below 0.5.
 constexpr uint64_t kSubTauNs = 10000000ull;
 constexpr double kSubEnter = 0.8, kSubLeave = 0.5;
+// ... and the subscription EWMA falls with this longer time constant (leaves
+// the mode ~35 ms after the GPU stopped being full): symmetric tenants that
+// finish a phase together do not hand the last runner straight to its token
+// bucket -- alone it is charged the whole GPU, and eight pooled 12.5 %
+// tenants measured the last one held 75 ms at the end of a 100-step window
+// (round 6); a tenant left alone for longer is still capped by its bucket.
+constexpr uint64_t kSubFallTauNs = 50000000ull;
 // Fair-share mode: credit a process keeps while it is not backlogged (its
 // virtual time trails the smallest running one by at most this much GPU
 // time): a tenant returning from a short gap is still behind the ones that
@@ -751,7 +758,8 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
   // fair-share mode while the backlogged weights fill the GPU
   if (dt) {
     const double x = (backlogged >= 2 && sum_w >= 0.999) ? 1.0 : 0.0;
-    const double a = (double)dt / (double)kSubTauNs < 1.0 ? (double)dt / (double)kSubTauNs : 1.0;
+    const double tau = (double)(x >= h.sub_ewma ? kSubTauNs : kSubFallTauNs);
+    const double a = (double)dt / tau < 1.0 ? (double)dt / tau : 1.0;
     h.sub_ewma += a * (x - h.sub_ewma);
   }
   if (backlogged >= 2 && sum_w >= 0.999) b->sub_passes += 1;
