@@ -114,6 +114,9 @@ def main():
     ap.add_argument("--ctx", type=int, default=1024, help="KV context length at decode start")
     ap.add_argument("--gpumem-mib", type=int, default=36864, help="HBM hard limit per slice")
     ap.add_argument("--model", default="qwen3-8b", choices=["qwen3-8b", "qwen3-tiny"])
+    ap.add_argument("--layers", type=int, default=0,
+                    help="decoder layers per slice (0 = the model's own 36); GPU tests use fewer to keep eight-slice "
+                         "rounds short -- such a line is labelled and is not the headline config")
     ap.add_argument("--mode", default="all", choices=["all", "both", "shim", "native"],
                     help="all = shim + masked_noshim + temporal + native (same queues) + native (HIP default "
                          "queues) rounds; both = shim + native")
@@ -185,7 +188,7 @@ def main():
     work = Path(tempfile.mkdtemp(prefix=f"mivgpu-bench-r{rank}-"))
     log_dir = Path(os.environ.get("MIVGPU_BENCH_LOGS", work))
     log_dir.mkdir(parents=True, exist_ok=True)
-    child_args = ["--model", args.model, "--batch", str(args.batch), "--ctx", str(args.ctx),
+    child_args = ["--model", args.model, "--layers", str(args.layers), "--batch", str(args.batch), "--ctx", str(args.ctx),
                   "--steps", str(args.steps), "--warmup", str(args.warmup), "--device", args.device]
     cpu = args.device == "cpu"
 
@@ -449,7 +452,8 @@ def main():
             "dtype": "bf16" if not cpu else "fp32-reference (CPU rehearsal)",
             "data": "synthetic (random-init weights, random KV context)",
             "config": {
-                "model": "Qwen3-8B" if args.model == "qwen3-8b" else "Qwen3-tiny",
+                "model": ("Qwen3-8B" if args.model == "qwen3-8b" else "Qwen3-tiny")
+                + (f" ({args.layers} layers, test config)" if args.layers > 0 else ""),
                 "global_batch": world * args.slices * args.batch,
                 "seq_len": args.ctx,
                 "parallelism": f"dp{world} x {args.slices} vGPU slices/GPU",

@@ -725,14 +725,14 @@ inline void owner_pass(Handle& h, const Reading* r, int n, uint64_t now, uint64_
       use[i] = w > kGateUnits ? 1.0 / (double)present : 0.0;
     } else {
       got = 0.0;
-      // nobody resident: the owing tenants split the pass; a tenant whose
-      // fresh flags say it owes nothing is charged nothing (it was charged
-      // the whole pass, and a tenant sampling across the moment it started
-      // to owe carried those passes into its first owing sample: eight
-      // pooled tenants starting together each went into debt and sat out a
-      // 25-30 ms hold, round 6); without flags a process is charged the pass
-      // whole (alone between its own kernels)
-      f = st[i] < 0 ? 1.0 : (owes && owing > 0 ? 1.0 / (double)owing : 0.0);
+      // nobody resident: the owing tenants split the pass; any other process
+      // is charged it whole -- alone between its own kernels, a tenant's
+      // flags can read "owes nothing" at the pass that falls in a dispatch
+      // gap (round 6 tried charging those nothing: a lone tenant under a
+      // 12.5 % limit then ran at 0.27 of unthrottled, a Triton loop under 25 %
+      // at 0.48; a tenant only charges a sample in which it owes work, so an
+      // idle one pays nothing anyway)
+      f = st[i] < 0 ? 1.0 : (owes && owing > 0 ? 1.0 / (double)owing : 1.0);
       use[i] = owes && owing > 0 ? 1.0 / (double)owing : 0.0;
     }
     if (!held) {

@@ -255,6 +255,7 @@ class SliceProc:
 def child_main(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="qwen3-8b")
+    ap.add_argument("--layers", type=int, default=0, help="decoder layers (0 = the model's own; tests only)")
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--ctx", type=int, default=1024)
     ap.add_argument("--steps", type=int, default=20)
@@ -280,6 +281,9 @@ def child_main(argv):
     from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_8B, QWEN3_TINY, Qwen3Decoder
 
     cfg = {"qwen3-8b": QWEN3_8B, "qwen3-tiny": QWEN3_TINY}[a.model]
+    if a.layers > 0:
+        import dataclasses
+        cfg = dataclasses.replace(cfg, layers=a.layers)
     if a.device == "cpu":
         return _child_cpu(a, cfg, Qwen3Decoder)
     t_load = time.time()

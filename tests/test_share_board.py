@@ -249,10 +249,11 @@ def test_tenant_flags_decide_held_and_gap_splits(native_build, tmp_path):
     assert first[333].obs_ns == 0                                 # held: not observed
     sh = B.shares(mid, s2)
     assert abs(sh[111]["charged_share"] - 0.5) < 0.05 and abs(sh[222]["charged_share"] - 0.5) < 0.05, sh
-    # idle with fresh flags: observed, charged nothing -- while others run, and
-    # in the passes nobody is resident (it owes nothing)
+    # idle with fresh flags: observed and charged nothing while others run;
+    # in the passes nobody is resident it is charged whole, as a tenant alone
+    # between its kernels (the shim charges only samples in which it owes)
     assert first[444].obs_ns > 0 and first[444].frac_ns == 0
-    assert sh[444]["obs_ms"] > 0 and sh[444]["charged_share"] == 0, sh
+    assert sh[444]["obs_ms"] > 0 and sh[444]["charged_share"] > 0.9, sh
 
 
 def _fair_run(native_build, tmp_path, tenants, seconds=0.4, occ_after=None):

@@ -472,7 +472,10 @@ def test_eight_temporal_tenants_run_like_native(tmp):
     and its neighbours are not held for it.  Round 5 (presence at the
     instant): 0.955 / fairness 0.941 on one box, 0.87 on another; round 6:
     0.989 / 0.984."""
-    r = _bench(["--slices", "8", "--rounds", "temporal,native", "--steps", "100", "--warmup", "5"], timeout=170)
+    # 12 of the 36 layers: the same kernels and shapes, a third of the load
+    # time -- eight governed slices load at 12.5 % each
+    r = _bench(["--slices", "8", "--rounds", "temporal,native", "--steps", "100", "--warmup", "5", "--layers", "12"],
+               timeout=170)
     gov = r["temporal_governor_rank0"]
     print(json.dumps({"temporal": r["temporal_value"], "native": r["native_value"],
                       "fairness": r["temporal_fairness_min_over_max"],
@@ -490,7 +493,8 @@ def test_eight_pooled_slices_with_the_monitor_switch(tmp):
     contending tenants, as production runs it (the reference turns the
     utilisation switch on for every busy tenant of equal priority,
     cmd/vGPUmonitor/feedback.go:56-72): within 3 % of native, fair."""
-    r = _bench(["--slices", "8", "--rounds", "shim,native", "--steps", "100", "--warmup", "5"], timeout=170)
+    r = _bench(["--slices", "8", "--rounds", "shim,native", "--steps", "100", "--warmup", "5", "--layers", "12"],
+               timeout=170)
     mon = r.get("shim_monitor") or {}
     print(json.dumps({"shim": r["value"], "native": r["native_value"], "fairness": r["slice_fairness_min_over_max"],
                       "monitor": mon}))
