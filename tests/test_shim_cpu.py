@@ -487,8 +487,9 @@ def test_host_bucket_charges_the_share_received(native_build, tmp_path, own, pee
         assert abs(bal["tokens_ns"]) <= 20_000_000, bal      # the bucket starts empty and stays there
     elif trend == "idle":
         # entitlement accrues only while work is owed and 20 ms after: 0.9 s
-        # of idling banks at most 25 % x 20 ms, not the 100 ms burst
-        assert 0 <= bal["tokens_ns"] <= 10_000_000, bal
+        # of idling banks at most 25 % x 20 ms on top of the 10 ms the bucket
+        # starts with (the fair-share lag, round 6), not the 100 ms burst
+        assert 0 <= bal["tokens_ns"] <= 15_000_000, bal
     else:
         assert bal["tokens_ns"] >= 95_000_000, bal           # fills to the 100 ms burst
     # the integral of the received share
