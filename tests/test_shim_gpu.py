@@ -234,7 +234,9 @@ def test_temporal_slices_charged_the_share_they_receive(tmp):
     """Two 50 % tenants under the temporal governor: each is charged its
     measured share of the resident wavefronts (~1/2 while both run), not the
     wall time, so together they run like two unthrottled slices."""
-    common = ["--slices", "2", "--no-spatial", "--mode", "shim", "--steps", "40", "--warmup", "5"]
+    # 100 steps: over 40 (0.3 s) two symmetric tenants' wave shares came out
+    # 41 / 60 on one box while their throughput was equal (fairness 1.0)
+    common = ["--slices", "2", "--no-spatial", "--mode", "shim", "--steps", "100", "--warmup", "5"]
     free = _bench(common)
     on = _bench(common + ["--policy", "force"])
     print(json.dumps({"governed": on["value"], "unthrottled": free["value"],
