@@ -585,9 +585,19 @@ def child_hog(args) -> dict:
     torch.cuda.synchronize()
     new = sorted((set(os.listdir(kfd)) if os.path.isdir(kfd) else set()) - before)
 
-    def vram(pid):   # this process's VRAM on any GPU, as KFD counts it
+    # KFD lists every process of the HOST, other jobs on other GPUs too: only
+    # this GPU's vram_<gpu_id> counts when the topology names one GPU
+    from k8s_vgpu_scheduler_amd.monitor.hosttruth import single_gpu_ids
+
+    try:
+        gid = single_gpu_ids("x").get("x")
+    except OSError:
+        gid = None
+    pattern = f"vram_{gid}" if gid else "vram_*"
+
+    def vram(pid):   # this process's VRAM as KFD counts it
         tot = 0
-        for f in glob.glob(os.path.join(kfd, pid, "vram_*")):
+        for f in glob.glob(os.path.join(kfd, pid, pattern)):
             try:
                 tot += int(open(f).read().strip() or 0)
             except (OSError, ValueError):

@@ -189,17 +189,24 @@ def test_shimless_container_on_time_shared_gpu_is_evicted(tmp_path_factory):
     import os
     import time
 
-    kfd_proc = "/sys/class/kfd/kfd/proc"
+    from k8s_vgpu_scheduler_amd.monitor.hosttruth import kfd_gpu_ids
+    from k8s_vgpu_scheduler_amd.smi import detect
 
-    def vram(pid):   # the most it holds on any GPU
-        best = 0
+    kfd_proc = "/sys/class/kfd/kfd/proc"
+    # KFD's proc directory lists every process of the HOST, on every GPU --
+    # other jobs' too.  Round 5's test took the one new entry holding >= 2 GiB
+    # on ANY GPU as the probe; on the driver's box that was another job on
+    # another GPU (its entry was gone when the test gave up), so the monitor,
+    # reading only this GPU's vram_<gid>, had nothing to evict.  Only THIS
+    # GPU's entries count (keep box-dependent assertions keyed to
+    # this GPU's KFD entries).
+    ids = kfd_gpu_ids(detect("amdsmi"))
+
+    def vram(pid, gid):
         try:
-            for f in os.listdir(f"{kfd_proc}/{pid}"):
-                if f.startswith("vram_"):
-                    best = max(best, int(open(f"{kfd_proc}/{pid}/{f}").read().strip() or 0))
+            return int(open(f"{kfd_proc}/{pid}/vram_{gid}").read().strip() or 0)
         except (OSError, ValueError):
-            pass
-        return best
+            return 0
     root = tmp_path_factory.mktemp("e2e-shimless")
     procs = root / "proc"
     procs.mkdir()
@@ -212,6 +219,9 @@ def test_shimless_container_on_time_shared_gpu_is_evicted(tmp_path_factory):
         env = container_env(alloc)
         env["PYTHONPATH"] = str(REPO)
         env.pop("LD_PRELOAD", None)
+        dev = env["MIVGPU_DEVICE_UUIDS"].split(",")[0]
+        gid = ids.ensure([dev]).get(dev)
+        assert gid, (dev, ids.tables)
         before = set(os.listdir(kfd_proc))
         p = _probe(env, "matmul", "--n", "2048", "--iters", "50", "--oom-probe-mib", "2048", "--hold-s", "90",
                    wait=False)
@@ -221,7 +231,7 @@ def test_shimless_container_on_time_shared_gpu_is_evicted(tmp_path_factory):
             def host_pid():
                 assert p.poll() is None, p.communicate()[1][-2000:]
                 new = [int(e) for e in set(os.listdir(kfd_proc)) - before
-                       if e.isdigit() and vram(e) >= 2048 * MIB]
+                       if e.isdigit() and vram(e, gid) >= 2048 * MIB]
                 return new[0] if len(new) == 1 else None
             hp = wait_for(host_pid, 120, "the probe to hold its 2 GiB on the GPU")
             seen = time.monotonic()
@@ -234,9 +244,9 @@ def test_shimless_container_on_time_shared_gpu_is_evicted(tmp_path_factory):
                          "the monitor to evict the shimless pod")
             except TimeoutError:
                 host = samples(cl.metrics("mon_metrics"), "hami_host_gpu_memory_used_bytes")
-                held = {f: open(f"{kfd_proc}/{hp}/{f}").read().strip()
-                        for f in os.listdir(f"{kfd_proc}/{hp}") if f.startswith("vram_")}
-                pytest.fail(f"not evicted (host pid {hp} holds {held}, amd-smi {host}); monitor state:\n"
+                held = vram(hp, gid)
+                pytest.fail(f"not evicted (host pid {hp} holds {held >> 20} MiB on KFD gpu {gid}, probe alive "
+                            f"{p.poll() is None}, amd-smi {host}); monitor state:\n"
                             + json.dumps(cl.monitor_state(), default=str)[-6000:] + "\nmonitor log:\n"
                             + cl.logs("monitor")[-3000:])
             took = time.monotonic() - seen

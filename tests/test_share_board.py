@@ -217,7 +217,9 @@ def test_tenant_flags_decide_held_and_gap_splits(native_build, tmp_path):
     _occ(kfd, 444, 4242, 0)
     node = subprocess.Popen(_boardd(native_build, kfd, d))
     try:
-        t_end = time.time() + 0.5
+        # the first passes may precede the first flags (a loaded CPU): count
+        # only what is charged once every tenant has published
+        t_end = time.time() + 0.2
         while time.time() < t_end:
             fl.publish(111, B.FLAG_OWES)
             fl.publish(222, B.FLAG_OWES)
@@ -225,6 +227,14 @@ def test_tenant_flags_decide_held_and_gap_splits(native_build, tmp_path):
             fl.publish(444, 0)
             time.sleep(0.005)
         b = B.Board(B.board_path(d, 4242))
+        s0 = b.snapshot()
+        t_end = time.time() + 0.4
+        while time.time() < t_end:
+            fl.publish(111, B.FLAG_OWES)
+            fl.publish(222, B.FLAG_OWES)
+            fl.publish(333, B.FLAG_HELD)
+            fl.publish(444, 0)
+            time.sleep(0.005)
         s1 = b.snapshot()
         # now nobody resident: 111 and 222 owe, split the gap
         _occ(kfd, 111, 4242, 0)
@@ -243,7 +253,13 @@ def test_tenant_flags_decide_held_and_gap_splits(native_build, tmp_path):
         node.terminate()
         node.wait(timeout=10)
         fl.close()
-    first = {s.pid: s for s in s1.slots if s.pid}
+    base = {s.pid: s for s in s0.slots if s.pid}
+
+    class _D:   # counters accrued between s0 and s1
+        def __init__(self, a, z):
+            self.frac_ns = a.frac_ns - (z.frac_ns if z else 0)
+            self.obs_ns = a.obs_ns - (z.obs_ns if z else 0)
+    first = {s.pid: _D(s, base.get(s.pid)) for s in s1.slots if s.pid}
     assert first[111].frac_ns == first[111].obs_ns > 0           # its small kernels: the whole GPU
     assert first[222].obs_ns > 0 and first[222].frac_ns == 0      # queued behind them: charged nothing
     assert first[333].obs_ns == 0                                 # held: not observed
