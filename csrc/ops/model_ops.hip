@@ -1106,12 +1106,14 @@ decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restric
     __syncthreads();
 
     // ---- Q operand from LDS
+
     u32x4_t qr[4];
-    {
+    auto load_q = [&]() __attribute__((always_inline)) {
       const int g = r16 < G ? r16 : 0;
 #pragma unroll
       for (int s = 0; s < 4; ++s) qr[s] = *reinterpret_cast<const u32x4_t*>(&s_q[g][32 * s + 8 * q4]);
-    }
+    };
+    load_q();
 
     // ---- per group: the wave owning the new key patches its fragments (its
     // loads may predate the append), scores, online softmax, P.V accumulated
@@ -1195,7 +1197,16 @@ decode_attn_fused_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restric
     // every score masked: a neutral partial): its loads were issued before the
     // prep math, and a use inside a branch lets LLVM sink them behind the
     // barrier (measured 42 vs 26 us per layer).
-    if constexpr (MULTI) {
+    if constexpr (MULTI && WAVES >= 12) {
+      // twelve waves, one register buffer (a 768-thread workgroup leaves 168
+      // registers per lane, two buffers take 226): the other eleven waves'
+      // loads cover each one's round trip per group
+#pragma clang loop unroll(disable)
+      for (int it = 0; it < nit; ++it) {
+        if (it > 0) load_kv(kra, vra, it);
+        group(kra, vra, it);
+      }
+    } else if constexpr (MULTI) {
       // two register buffers: the next group's loads go out before this group's math
       int it = 0;
       while (true) {
@@ -1631,6 +1642,25 @@ int mivgpu_decode_attention_fused(const void* qkv, const void* q_norm_w, const v
   const int G = Hq / Hkv;
   const int waves = attn_impl();
   if (max_ctx % ATT_KPW || G + 2 > waves) return -1;
+  // One split per (b, kv-head) with four query heads per kv-head: twelve-wave
+  // workgroups (one per CU at batch 32 x 8 kv-heads; 158 VGPRs, three waves
+  // per SIMD -- sixteen spilled) that merge their waves in LDS and write the
+  // output, no partials and no combine launch: 25.5 us per layer vs 26.0 +
+  // 4.9 for five 8-wave splits + combine (profiles/round6/w12/).
+  // MIVGPU_ATTN_W12=0 keeps the 8-wave kernel.
+  static const bool w12 = [] {
+    const char* e = getenv("MIVGPU_ATTN_W12");
+    return !e || atoi(e) != 0;
+  }();
+  if (w12 && nsplit == 1 && G == 4 && !defer_combine) {
+    const int iters12 = (max_ctx + 12 * ATT_KPW - 1) / (12 * ATT_KPW);
+    const float sl2 = scale * 1.44269504f, lt = log2f(theta);
+    hipLaunchKernelGGL((decode_attn_fused_kernel<4, 12, true, false, true>), dim3(1, Hkv, B), dim3(768), 0, s,
+                       (const bf16_t*)qkv, (const bf16_t*)q_norm_w, (const bf16_t*)k_norm_w, pos, seqlens,
+                       (bf16_t*)k_cache, (bf16_t*)v_cache, (bf16_t*)out, (float*)o_part, (float*)ml_part, counters,
+                       Hq, Hkv, max_ctx, 1, iters12, sl2, eps, lt);
+    return (int)hipGetLastError();
+  }
   // 32-key groups per wave so that nsplit splits cover max_ctx; nsplit = 1
   // (one workgroup per (b, kv-head), each wave looping over its groups) writes
   // the output itself and needs no combine

@@ -283,7 +283,7 @@ class Qwen3Decoder:
         # key splits: the fused kernel covers the context with any count
         # (ops.attn_fused_splits); the unfused one needs attn_split() keys each
         if self.attn_fused:
-            self.nsplit = ops.attn_fused_splits(batch, cfg.kv_heads, self.T)
+            self.nsplit = ops.attn_fused_splits(batch, cfg.kv_heads, self.T, cfg.heads)
         else:
             self.nsplit = max(1, math.ceil(self.T / (ops.attn_split() if self.native else 256)))
         self.o_part = torch.zeros(batch * cfg.heads * self.nsplit * cfg.head_dim, dtype=torch.float32,

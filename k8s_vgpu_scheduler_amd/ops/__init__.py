@@ -343,7 +343,14 @@ def attn_fused_ok(n_q_heads: int, n_kv_heads: int, head_dim: int = 128) -> bool:
 ATTN_MAX_SPLITS = 16
 
 
-def attn_fused_splits(B: int, n_kv_heads: int, max_ctx: int) -> int:
+def attn_w12() -> bool:
+    """Twelve-wave one-split attention workgroups (mivgpu_decode_attention_fused
+    with nsplit 1 and 4 query heads per kv-head); MIVGPU_ATTN_W12=0 turns them
+    off (read by the C launcher too)."""
+    return os.environ.get("MIVGPU_ATTN_W12", "1") != "0"
+
+
+def attn_fused_splits(B: int, n_kv_heads: int, max_ctx: int, n_q_heads: int | None = None) -> int:
     """Key splits for decode_attention_fused.  One split per attn_split()
     keys (one 32-key group per wave: several workgroups share a CU and hide
     each other's load latency) up to ATTN_MAX_SPLITS; a longer context keeps
@@ -351,13 +358,20 @@ def attn_fused_splits(B: int, n_kv_heads: int, max_ctx: int) -> int:
     waves loop over several groups, so the workspace and the combine stay
     bounded.  One split per (b, kv-head) writes the output itself (no combine
     launch) but at batch 32 ran slower than 5 splits + combine (43 vs 31 us,
-    profiles/README.md section 35).  MIVGPU_ATTN_SPLITS=n forces n (0 = one
-    split per attn_split() keys)."""
+    profiles/README.md section 35).  With four query heads per kv-head and at
+    least one (b, kv-head) per visible CU, ONE split on twelve-wave
+    workgroups (attn_w12) merges its waves in LDS and writes the output: 25.5
+    us per layer with no combine launch vs 26.0 + 4.9 at batch 32 (decode
+    step 4.46 vs 4.59 ms, profiles/round6/w12/).  MIVGPU_ATTN_SPLITS=n forces
+    n (0 = one split per attn_split() keys)."""
     full = max(1, -(-max_ctx // attn_split()))
     env = os.environ.get("MIVGPU_ATTN_SPLITS")
     if env is not None and env.strip():
         n = int(env)
         return full if n <= 0 else n
+    if (n_q_heads is not None and n_q_heads == 4 * n_kv_heads and attn_w12()
+            and B * n_kv_heads >= visible_cus()):
+        return 1
     if full <= ATTN_MAX_SPLITS:
         return full
     return min(full, max(ATTN_MAX_SPLITS, -(-2 * visible_cus() // max(1, B * n_kv_heads))))

@@ -292,7 +292,8 @@ v = torch.randn(B, Hkv, T, D, device="cuda", generator=g).bfloat16()
 pos = torch.tensor([5, 511, 796], dtype=torch.int32, device="cuda")
 seqlens = pos + 1
 kc, vc = ops.k_to_cache_layout(k), ops.v_to_cache_layout(v)
-nsplit = math.ceil(T / ops.attn_split())
+import os
+nsplit = int(os.environ.get("FUSED_NSPLIT", "0")) or math.ceil(T / ops.attn_split())
 out = torch.empty(B, Hq * D, device="cuda", dtype=torch.bfloat16)
 o_part = torch.empty(B * Hq * nsplit * D, device="cuda")
 ml = torch.empty(B * Hq * nsplit * 2, device="cuda")
@@ -313,16 +314,24 @@ print("ERR", err, int(cnt.abs().sum()))
 """
 
 
-@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("mode", ["1", "2", "w12", "s1"])
 @pytest.mark.parametrize("mask", ["", "0:0-63"])
 def test_decode_attention_fused_modes(mode, mask):
     """Both fusion modes (separate combine kernel / last-arriver combine) in a
-    fresh process, whole GPU and a 64-CU partition, 3 launches in a row."""
+    fresh process, whole GPU and a 64-CU partition, 3 launches in a row; w12:
+    one split per (b, kv-head) on twelve-wave workgroups (MIVGPU_ATTN_W12),
+    three 384-key rounds per wave at the deepest position; s1: one split on
+    the eight-wave kernel."""
     import os
     import subprocess
     import sys
 
     env = dict(os.environ, MIVGPU_ATTN_FUSED=mode)
+    env.pop("MIVGPU_ATTN_W12", None)
+    if mode == "w12":
+        env.update(MIVGPU_ATTN_FUSED="1", MIVGPU_ATTN_W12="1", FUSED_NSPLIT="1")
+    elif mode == "s1":   # one split on the eight-wave kernel
+        env.update(MIVGPU_ATTN_FUSED="1", MIVGPU_ATTN_W12="0", FUSED_NSPLIT="1")
     env.pop("HSA_CU_MASK", None)
     if mask:
         env["HSA_CU_MASK"] = mask
@@ -462,6 +471,31 @@ def test_decoder_attention_combine_in_o_proj(monkeypatch, B, xcomb):
     b.fill_context(600)
     lens = torch.tensor([600 - 170 * i for i in range(B)], dtype=torch.int32, device="cuda")
     for d in (a, b):   # rows of different lengths: some splits of the short rows hold no keys
+        d.pos.copy_(lens)
+        d.seqlens.copy_(lens + 1)
+    for _ in range(3):
+        la, lb = a.step(), b.step()
+        _close(la, lb, 5e-2)
+        b.tokens.copy_(a.tokens)
+
+
+def test_decoder_one_split_attention_matches_reference(monkeypatch):
+    """One attention split per (b, kv-head), as batch 32 x 8 kv-heads selects
+    on the whole chip: twelve-wave workgroups (the eight-wave one-split kernel
+    runs in test_decode_attention_fused_modes[s1]), 3 norm-fused steps at a
+    600-key context with rows of different lengths vs the fp32 reference."""
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
+
+    monkeypatch.setenv("MIVGPU_NORM_FUSED", "1")
+    monkeypatch.setenv("MIVGPU_ATTN_SPLITS", "1")
+    monkeypatch.delenv("MIVGPU_ATTN_W12", raising=False)
+    a = Qwen3Decoder(QWEN3_TINY, batch=4, max_ctx=700, device="cuda", native=True, seed=13)
+    assert a.attn_fused and a.nsplit == 1 and a.xcomb is None
+    b = Qwen3Decoder(QWEN3_TINY, batch=4, max_ctx=700, device="cuda", native=False, seed=13)
+    a.fill_context(600)
+    b.fill_context(600)
+    lens = torch.tensor([600, 431, 9, 300], dtype=torch.int32, device="cuda")
+    for d in (a, b):
         d.pos.copy_(lens)
         d.seqlens.copy_(lens + 1)
     for _ in range(3):
