@@ -341,6 +341,7 @@ def attn_fused_ok(n_q_heads: int, n_kv_heads: int, head_dim: int = 128) -> bool:
 
 
 ATTN_MAX_SPLITS = 16
+W12_MAX_CTX = 2048
 
 
 def attn_w12() -> bool:
@@ -362,7 +363,9 @@ def attn_fused_splits(B: int, n_kv_heads: int, max_ctx: int, n_q_heads: int | No
     least one (b, kv-head) per visible CU, ONE split on twelve-wave
     workgroups (attn_w12) merges its waves in LDS and writes the output: 25.5
     us per layer with no combine launch vs 26.0 + 4.9 at batch 32 (decode
-    step 4.46 vs 4.59 ms, profiles/round6/w12/).  MIVGPU_ATTN_SPLITS=n forces
+    step 4.46 vs 4.59 ms, profiles/round6/w12/); up to W12_MAX_CTX keys of
+    cache, so that one long row among short ones (continuous batching) is
+    never a single workgroup's 8k-key stream.  MIVGPU_ATTN_SPLITS=n forces
     n (0 = one split per attn_split() keys)."""
     full = max(1, -(-max_ctx // attn_split()))
     env = os.environ.get("MIVGPU_ATTN_SPLITS")
@@ -370,7 +373,7 @@ def attn_fused_splits(B: int, n_kv_heads: int, max_ctx: int, n_q_heads: int | No
         n = int(env)
         return full if n <= 0 else n
     if (n_q_heads is not None and n_q_heads == 4 * n_kv_heads and attn_w12()
-            and B * n_kv_heads >= visible_cus()):
+            and B * n_kv_heads >= visible_cus() and max_ctx <= W12_MAX_CTX):
         return 1
     if full <= ATTN_MAX_SPLITS:
         return full

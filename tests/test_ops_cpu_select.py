@@ -27,6 +27,9 @@ def test_splits_kept_where_the_one_split_grid_is_too_small(cus):
     assert ops.attn_fused_splits(31, 8, 1088, 32) == 5        # 248 < 256 CUs
     assert ops.attn_fused_splits(32, 8, 1088, 16) == 5        # two query heads per kv-head: no twelve-wave kernel
     assert ops.attn_fused_splits(32, 8, 1088) == 5            # caller did not say the head count
+    # a long cache: a long row among short ones must not be one workgroup's stream
+    assert ops.attn_fused_splits(32, 8, 2048, 32) == 1
+    assert ops.attn_fused_splits(32, 8, 8448, 32) == 16
 
 
 def test_one_split_env_overrides(cus, monkeypatch):
