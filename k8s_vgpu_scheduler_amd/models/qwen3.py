@@ -584,18 +584,47 @@ class Qwen3Decoder:
         res.add_(y)
         return None
 
+    def _gemm_into_residual(self, lw, name, x, res, nxt, nxt_name):
+        """res += x . W^T inside the library GEMM (beta = 1, C = res), then the
+        next projection's whole-row RMSNorm as its own pass where
+        _add_then_norm would have fused it: at 8192 rows 64 MB less traffic
+        per call than writing y and running add_rmsnorm -- 8k prefill 116.21
+        vs 116.96 ms, faster in 5 of 5 interleaved pairs
+        (profiles/round6/addmm/).  MIVGPU_PREFILL_ADDMM=0 writes y.  Returns
+        (handled, normalised rows or None)."""
+        plain = {"o": "wo", "d": "wd"}[name]
+        if not (self.native and self._pf_addmm and plain in lw and x.shape[0] > 64):
+            return False, None
+        res.addmm_(x, lw[plain].t())
+        if nxt is None:
+            return True, None
+        ln = nxt["ln1"] if nxt_name == "qkv" else nxt["ln2"]
+        if {"qkv": "wqkv", "gu": "wgu"}[nxt_name] in nxt:
+            return True, ops.rmsnorm(res, ln, self.cfg.eps)
+        if res.shape[0] >= self.PROMPT_UNPACK_ROWS:
+            return True, ops.rmsnorm(res, self._ones, self.cfg.eps)
+        return True, None
+
     def _prefill_impl_norm_fused(self, bufs: dict, b: int):
         cfg, w = self.cfg, self.w
+        self._pf_addmm = os.environ.get("MIVGPU_PREFILL_ADDMM", "1") == "1"
         res = torch.index_select(w.embed, 0, bufs["ids"])
         h = None
         for li, lw in enumerate(w.layers):
             qkv = self._normed_proj(lw, "qkv", res, lw["ln1"], h)
             q, k, v = self._prefill_qk(li, lw, qkv, bufs["pos"], b)
-            o = self._proj(lw, "o", self._prefill_attention(q, k, v, bufs["mask"]))
-            h = self._add_then_norm(lw, "gu", o, res, lw["ln2"])
-            d = self._proj(lw, "d", self._normed_proj(lw, "gu", res, lw["ln2"], h))
-            if li + 1 < len(w.layers):
-                nxt = w.layers[li + 1]
+            att = self._prefill_attention(q, k, v, bufs["mask"])
+            done, h = self._gemm_into_residual(lw, "o", att, res, lw, "gu")
+            if not done:
+                o = self._proj(lw, "o", att)
+                h = self._add_then_norm(lw, "gu", o, res, lw["ln2"])
+            act = self._normed_proj(lw, "gu", res, lw["ln2"], h)
+            nxt = w.layers[li + 1] if li + 1 < len(w.layers) else None
+            done, h = self._gemm_into_residual(lw, "d", act, res, nxt, "qkv")
+            if done:
+                continue
+            d = self._proj(lw, "d", act)
+            if nxt is not None:
                 h = self._add_then_norm(nxt, "qkv", d, res, nxt["ln1"])
             else:
                 res.add_(d)
