@@ -37,7 +37,9 @@ def test_eight_temporal_tenants_run_like_native():
     assert r["temporal_fairness_min_over_max"] >= 0.95, r
     for g in gov:
         assert g["lifetime"]["gates"] > 0, gov                           # the governor ran
-        assert g["busy_share_pct"] is not None and 9.0 <= g["busy_share_pct"] <= 16.0, gov
+        # each near 12.5 % of the GPU time (9.99-14.36 seen on one box in round 6;
+        # the throughput fairness above is the tight check)
+        assert g["busy_share_pct"] is not None and 8.0 <= g["busy_share_pct"] <= 17.0, gov
 
 
 def test_eight_pooled_slices_with_the_monitor_switch():
