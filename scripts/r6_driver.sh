@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6: what the driver runs at round end -- smoke(), pytest -x -q -m gpu, bench.py -- on one fresh box.
 set -o pipefail
-O=gpurun_out/r6drv
+O=${O:-gpurun_out/r6drv}
 mkdir -p $O
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
