@@ -681,6 +681,46 @@ def test_prefill_flash_attention(ops, L, Hq, Hkv):
     _close(out[:4], want[:4], 1e-2)
 
 
+@pytest.mark.parametrize("xcd", ["0", "1"])
+@pytest.mark.parametrize("L,Hq,Hkv", [(1000, 32, 8), (300, 8, 2), (64, 16, 16)])
+def test_prefill_flash_attention_grid_orders(ops, monkeypatch, xcd, L, Hq, Hkv):
+    """Both block orders of the eight-wave flash kernel (read per launch):
+    the XCD-aware 1-D grid (kv head = block mod Hkv, the default) and the 2-D
+    (query block, kv head) grid, against the fp32 reference -- Hkv = 8 (one
+    head per XCD), 2 and 16 (heads sharing / spanning XCDs)."""
+    monkeypatch.setenv("MIVGPU_FA_XCD", xcd)
+    g = torch.Generator(device="cuda").manual_seed(L * Hkv)
+    G, D = Hq // Hkv, 128
+    q = torch.randn(Hkv, G * L, D, generator=g, device="cuda").to(torch.bfloat16)
+    k = torch.randn(Hkv, L, D, generator=g, device="cuda").to(torch.bfloat16)
+    v = torch.randn(Hkv, L, D, generator=g, device="cuda").to(torch.bfloat16)
+    scale = 1.0 / math.sqrt(D)
+    out = ops.prefill_attention(q, k, v, Hq, scale)
+    _close(out, ref.prefill_attention(q, k, v, Hq, scale), 2e-2)
+
+
+@pytest.mark.parametrize("addmm", ["0", "1"])
+def test_decoder_prefill_residual_paths_match_reference(monkeypatch, addmm):
+    """The norm-fused prompt path with the residual add inside the library
+    GEMM (MIVGPU_PREFILL_ADDMM=1, the default) and with y written and
+    add_rmsnorm (0): the prompt's logits and the first decode steps against
+    the fp32 reference decoder."""
+    from k8s_vgpu_scheduler_amd.models.qwen3 import QWEN3_TINY, Qwen3Decoder
+
+    monkeypatch.setenv("MIVGPU_NORM_FUSED", "1")
+    monkeypatch.setenv("MIVGPU_PREFILL_ADDMM", addmm)
+    a = Qwen3Decoder(QWEN3_TINY, batch=2, max_ctx=400, device="cuda", native=True, seed=21)
+    b = Qwen3Decoder(QWEN3_TINY, batch=2, max_ctx=400, device="cuda", native=False, seed=21)
+    prompt = torch.randint(0, QWEN3_TINY.vocab, (300,), generator=torch.Generator().manual_seed(5))
+    la, lb = a.prefill(prompt, b=1), b.prefill(prompt, b=1)
+    _close(la, lb, 5e-2)
+    b.tokens.copy_(a.tokens)
+    for _ in range(2):
+        sa, sb = a.step(), b.step()
+        _close(sa[1], sb[1], 5e-2)
+        b.tokens.copy_(a.tokens)
+
+
 @pytest.mark.parametrize("off", [0, 1024])
 def test_tr_read_semantics(ops, off):
     """ds_read_b64_tr_b16 (the flash kernel's V^T operand): per 16-lane group,
