@@ -91,7 +91,8 @@ def gov_row(d: dict) -> dict:
                          "gates": d.get("gov_gates")},
             "sampler_pass_us_mean": d.get("gov_sampler_pass_us_mean"),
             "sampler_pass_us_max": d.get("gov_sampler_pass_us_max"),
-            "at_go": d.get("gov_at_go"), "at_end": d.get("gov_at_end"), "hold_trace": d.get("hold_trace")}
+            "at_go": d.get("gov_at_go"), "at_end": d.get("gov_at_end"), "hold_trace": d.get("hold_trace"),
+            "nonfair": d.get("gov_nonfair")}
 
 
 def _share_cus(cus: int) -> int:

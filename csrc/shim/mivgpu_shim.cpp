@@ -1821,6 +1821,14 @@ struct OccDev {
   uint64_t local_charged = 0;
   uint64_t fair_samples = 0;   // samples in fair-share mode / held there on the lead
   uint64_t fair_held_samples = 0;
+  // the samples outside the fair-share mode, last 16 (sampler_info "nonfair"):
+  // interval, share charged, run time, bucket after, previous sample in the mode
+  struct NonFair {
+    uint64_t t_ns, dt_ns;
+    double share, run_ns, tokens_ns;
+    int prev_fair;
+  } nonfair[16];
+  uint64_t nonfair_n = 0;
   int64_t last_lead_ns = -1;
   double fair_recv_ns = 0;     // GPU time received since fair-share mode began
   std::vector<mivgpu_board::Reading> readings;
@@ -2177,6 +2185,10 @@ bool occ_sample(int dev, uint64_t now) {
     // symmetric 25 % tenants: one was held 120 ms of a 100-step run on it and
     // came out slowest, fairness 0.93 where the hardware alone gave 0.995);
     // unequal limits drift by far more than 3 % and are still held.
+    if (lead < 0) {
+      OccDev::NonFair& nf = o.nonfair[o.nonfair_n++ % 16];
+      nf = OccDev::NonFair{now, dt, share, run, o.tokens_ns, o.last_lead_ns >= 0 ? 1 : 0};
+    }
     double eff = o.tokens_ns;
     if (lead >= 0) {
       // out of the mode with the mode's own slack (kFairLagNs), not empty:
@@ -3767,7 +3779,16 @@ MIVGPU_EXPORT int mivgpu_sampler_info(int dev, char* buf, int n) {
       o.state_ns[1] / 1e6, o.state_ns[2] / 1e6, o.state_ns[3] / 1e6, o.state_ns[4] / 1e6,
       (unsigned long long)o.fair_samples, (unsigned long long)o.fair_held_samples,
       o.last_lead_ns >= 0 ? o.last_lead_ns / 1e6 : -1.0, o.tokens_ns / 1e6);
-  put(",\"peers\":[");
+  put(",\"nonfair\":[");
+  {
+    const uint64_t k = o.nonfair_n < 16 ? o.nonfair_n : 16;
+    for (uint64_t i = 0; i < k; ++i) {
+      const OccDev::NonFair& nf = o.nonfair[(o.nonfair_n - k + i) % 16];
+      put("%s[%.3f,%.3f,%.3f,%.3f,%.3f,%d]", i ? "," : "", nf.t_ns / 1e6, nf.dt_ns / 1e6, nf.share, nf.run_ns / 1e6,
+          nf.tokens_ns / 1e6, nf.prev_fair);
+    }
+  }
+  put("],\"peers\":[");
   for (size_t i = 0; i < o.peers.size(); ++i) {
     const OccPeer& p = o.peers[i];
     put("%s{\"pid\":%d,\"v\":%d,\"avg\":%.2f,\"busy_age_ms\":%.1f}", i ? "," : "", p.pid, p.v, p.avg,

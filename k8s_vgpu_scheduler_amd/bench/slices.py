@@ -406,6 +406,7 @@ def _timed_counters() -> dict:
     for k in ("samples", "fair_samples", "fair_held_samples", "tokens_ms", "lead_ms"):
         if k in si:
             out[k] = si[k]
+
     for k in ("passes", "sub_passes", "fair_passes"):
         if k in bd:
             out["board_" + k] = bd[k]
@@ -433,6 +434,10 @@ def _governor_stats() -> dict:
         if k in g:
             out["gov_" + k] = g[k]
     si = g.get("sampler")
+    if si and os.environ.get("MIVGPU_GATE_TRACE") == "1":
+        # the samples outside the fair-share mode: [t ms, interval ms, share,
+        # run ms, bucket ms after, previous sample in the mode]
+        out["gov_nonfair"] = si.get("nonfair")
     if si:
         # how the share was charged: from the GPU's one sampler (board) or the
         # local estimate, and whose board it was
